@@ -1,0 +1,166 @@
+/*
+ * nxhip.h -- C ABI of the MI355X-native assemble + solve path for the hydraulic
+ * network saddle-point system of networks_fenicsx.
+ *
+ * The reference has no C/FFI boundary of its own: its hot path sits behind the
+ * Python classes HydraulicNetworkAssembler and Solver, which hand petsc4py
+ * Mat/Vec/KSP objects to DOLFINx C++ and PETSc/MUMPS. Each entry point below
+ * names the reference interface it replaces (file:line under
+ * /root/reference/src/networks_fenicsx/). The Python binding is
+ * networks_fenicsx_amd/_lib.py (ctypes); INTEGRATION.md shows the stub a
+ * maintainer would add on the reference side.
+ *
+ * Conventions
+ *   - every function returns NX_OK (0) or a negative NX_ERR_* code; the message
+ *     of the last failure on the calling thread is nx_last_error();
+ *   - host arrays are caller-owned and copied in/out; device buffers are owned by
+ *     the opaque handle and released by nx_destroy;
+ *   - calls on one handle must be serialised by the caller (the Python layer holds
+ *     the GIL); all work is issued on the handle's own HIP stream.
+ *
+ * Device layout (per rank): every local graph edge owns 2N+1 consecutive DoFs,
+ * interleaved [q_0, p_0, q_1, p_1, ..., p_{N-1}, q_N] (P1 flux vertices and DG0
+ * pressure cells, source -> target), then one multiplier per owned bifurcation.
+ * Columns >= n_own are ghosts (multipliers or flux end values owned by another
+ * rank). The pressure rows are negated so the assembled matrix is symmetric
+ * (the solution is unchanged); MINRES requires symmetry.
+ */
+#ifndef NXHIP_H
+#define NXHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NX_OK 0
+#define NX_ERR_ARG -1     /* invalid argument / shape */
+#define NX_ERR_HIP -2     /* HIP runtime failure */
+#define NX_ERR_RCCL -3    /* RCCL failure */
+#define NX_ERR_STATE -4   /* call out of order (e.g. solve before assemble) */
+#define NX_ERR_NOCONV -5  /* MINRES did not reach the tolerance in maxit */
+
+#define NX_UNIQUE_ID_BYTES 128
+
+typedef struct nx_network nx_network_t;
+
+/* Library/ABI version (major*10000 + minor*100 + patch). */
+int nx_version(void);
+
+/* Message of the last failure on this thread ("" if none). */
+const char* nx_last_error(void);
+
+/* Number of visible HIP devices. */
+int nx_device_count(int32_t* count);
+
+/*
+ * Create a network handle on `device` and build the CSR sparsity pattern on it.
+ * Replaces Solver.__init__'s fem.petsc.create_matrix / create_vector
+ * (solver.py:441-447) and the DoF layout of HydraulicNetworkAssembler.__init__
+ * (assembly.py:121-162).
+ *
+ *   N          cells per edge (>= 1)
+ *   n_edges    local edges E
+ *   edge_x     E*6 doubles: source xyz, target xyz (gdim < 3 padded with 0)
+ *   edge_lm    E*2 int32: column of the multiplier at the source / target end,
+ *              -1 when that end is not a bifurcation
+ *   n_lm       owned multiplier rows B
+ *   lm_rowptr  B+1 int32 CSR offsets of the multiplier rows
+ *   lm_col     int32 columns (sorted ascending per row): flux end DoFs
+ *   lm_val     double values (+1 at an in-edge end q_N, -1 at an out-edge start q_0;
+ *              assembly.py:271-277)
+ *   n_ghost    ghost columns appended after the n_own = E*(2N+1)+B owned ones
+ */
+int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
+              const int32_t* edge_lm, int64_t n_lm, const int32_t* lm_rowptr,
+              const int32_t* lm_col, const double* lm_val, int64_t n_ghost,
+              nx_network_t** out);
+
+/* Release every device buffer, graph and communicator of the handle. */
+int nx_destroy(nx_network_t* h);
+
+/* Local sizes: owned rows, columns (owned + ghosts), nonzeros. */
+int nx_dims(nx_network_t* h, int64_t* n_rows, int64_t* n_cols, int64_t* nnz);
+
+/*
+ * Coefficients of the forms (HydraulicNetworkAssembler.compute_forms,
+ * assembly.py:165-262), uploaded once and kept resident in HBM:
+ *   edge_R   E doubles (per-edge resistance) or NULL to use R_const everywhere
+ *   f        constant source term of the pressure equation
+ *   edge_bc  E*2 doubles: rhs contribution at q_0 and q_N of each edge
+ *            (-p_bc(source) at an inlet root, +p_bc(target) at an outlet leaf,
+ *            0 elsewhere; assembly.py:258-260)
+ */
+int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_const, double f,
+                        const double* edge_bc);
+
+/*
+ * Assemble matrix values and/or rhs on the device into the resident CSR.
+ * Replaces HydraulicNetworkAssembler.assemble (assembly.py:329-368) and
+ * Solver.assemble (solver.py:488-499). Asynchronous on the handle's stream.
+ */
+int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs);
+
+/*
+ * MINRES (Paige-Saunders) on the device; replaces the KSP solve of
+ * Solver.solve (solver.py:505-533; default there: LU/MUMPS).
+ *   rtol         stop when the MINRES residual estimate ||r_k|| / ||b|| <= rtol
+ *   maxit        iteration cap
+ *   check_every  iterations per host convergence check (graph chunk), >= 2, even
+ *   iters/relres/converged  outputs (host)
+ * Returns NX_OK also when not converged; `converged` tells. The solution stays on
+ * the device (nx_get_solution copies it out).
+ */
+int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
+             int32_t* iters, double* relres, int32_t* converged);
+
+/* Copy the owned part of the solution / rhs to the host (n_rows doubles). */
+int nx_get_solution(nx_network_t* h, double* x);
+int nx_get_rhs(nx_network_t* h, double* b);
+
+/* Copy the assembled CSR (n_rows+1, nnz, nnz) to the host -- parity tests. */
+int nx_get_csr(nx_network_t* h, int32_t* rowptr, int32_t* col, double* val);
+
+/* y = A x for host vectors (x has n_cols entries incl. ghosts) -- tests. */
+int nx_spmv_host(nx_network_t* h, const double* x, double* y);
+
+/* True residual ||b - A x|| / ||b|| of the current device solution. */
+int nx_true_residual(nx_network_t* h, double* relres);
+
+/* Wait for all work queued on the handle's stream. */
+int nx_sync(nx_network_t* h);
+
+/*
+ * Kernel timing with HIP events on the handle's stream.
+ *   nx_set_profiling(h, 1) brackets every SpMV launch inside nx_solve with an
+ *   event pair; nx_get_profile returns the summed SpMV time (ms), the number of
+ *   timed SpMV launches, and the summed assembly kernel time (ms).
+ *   nx_bench_spmv times `reps` back-to-back plain SpMV launches (ms per launch).
+ */
+int nx_set_profiling(nx_network_t* h, int32_t enable);
+int nx_get_profile(nx_network_t* h, double* spmv_ms, int64_t* spmv_count, double* asm_ms,
+                   int64_t* asm_count);
+int nx_reset_profile(nx_network_t* h);
+int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
+
+/*
+ * Multi-GPU (one process per GPU). Rank 0 creates the RCCL unique id, the
+ * host control plane (torch.distributed) broadcasts it, every rank calls
+ * nx_comm_init with its halo plan. Replaces the MPI ghost updates
+ * (assembly.py:363-367, solver.py:526-530) and MUMPS' internal communication.
+ *   n_peers                 neighbouring ranks
+ *   peer_rank[n_peers]
+ *   send_off[n_peers+1], send_idx[...]   owned local rows to send to each peer
+ *   recv_off[n_peers+1]     ghost slots [recv_off[p], recv_off[p+1]) filled by peer p
+ */
+int nx_comm_unique_id(unsigned char* id_out /* NX_UNIQUE_ID_BYTES */);
+int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned char* id,
+                 int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
+                 const int32_t* send_idx, const int32_t* recv_off);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NXHIP_H */

@@ -1,0 +1,240 @@
+"""ctypes binding of ``libnxhip.so`` (C ABI declared in ``include/nxhip.h``).
+
+There is no CPU fallback: if the library cannot be loaded, or no HIP device is
+visible, the device entry points raise. The library is loaded from the package
+directory (built in-tree by :mod:`networks_fenicsx_amd.build`).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from pathlib import Path
+
+import numpy as np
+
+__all__ = ["lib", "NxError", "NxNotConverged", "check", "Handle", "EXPORTED_SYMBOLS"]
+
+_LIB_PATH = Path(__file__).resolve().parent / "libnxhip.so"
+_lock = threading.Lock()
+_lib = None
+
+NX_OK, NX_ERR_ARG, NX_ERR_HIP, NX_ERR_RCCL, NX_ERR_STATE, NX_ERR_NOCONV = 0, -1, -2, -3, -4, -5
+UNIQUE_ID_BYTES = 128
+
+_i32, _i64, _f64 = C.c_int32, C.c_int64, C.c_double
+_pd = C.POINTER(C.c_double)
+_pi32 = C.POINTER(C.c_int32)
+_pi64 = C.POINTER(C.c_int64)
+_pu8 = C.POINTER(C.c_ubyte)
+_h = C.c_void_p
+
+# name -> (restype, argtypes); mirrors include/nxhip.h
+_SIGS = {
+    "nx_version": (C.c_int, []),
+    "nx_last_error": (C.c_char_p, []),
+    "nx_device_count": (C.c_int, [_pi32]),
+    "nx_create": (C.c_int, [_i32, _i32, _i64, _pd, _pi32, _i64, _pi32, _pi32, _pd, _i64,
+                            C.POINTER(_h)]),
+    "nx_destroy": (C.c_int, [_h]),
+    "nx_dims": (C.c_int, [_h, _pi64, _pi64, _pi64]),
+    "nx_set_coefficients": (C.c_int, [_h, _pd, _f64, _f64, _pd]),
+    "nx_assemble": (C.c_int, [_h, _i32, _i32]),
+    "nx_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
+    "nx_get_solution": (C.c_int, [_h, _pd]),
+    "nx_get_rhs": (C.c_int, [_h, _pd]),
+    "nx_get_csr": (C.c_int, [_h, _pi32, _pi32, _pd]),
+    "nx_spmv_host": (C.c_int, [_h, _pd, _pd]),
+    "nx_true_residual": (C.c_int, [_h, _pd]),
+    "nx_sync": (C.c_int, [_h]),
+    "nx_set_profiling": (C.c_int, [_h, _i32]),
+    "nx_get_profile": (C.c_int, [_h, _pd, _pi64, _pd, _pi64]),
+    "nx_reset_profile": (C.c_int, [_h]),
+    "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
+    "nx_comm_unique_id": (C.c_int, [_pu8]),
+    "nx_comm_init": (C.c_int, [_h, _i32, _i32, _pu8, _i32, _pi32, _pi32, _pi32, _pi32]),
+}
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+class NxError(RuntimeError):
+    """A failure reported by libnxhip (the message is ``nx_last_error()``)."""
+
+
+class NxNotConverged(NxError):
+    """MINRES did not reach the tolerance (mirrors ``ksp_error_if_not_converged``)."""
+
+
+def lib():
+    """Load ``libnxhip.so`` once; raise loudly if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not _LIB_PATH.exists():
+                raise NxError(
+                    f"{_LIB_PATH} is missing: build it with "
+                    "`python -m networks_fenicsx_amd.build` (there is no CPU fallback)"
+                )
+            handle = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != NX_OK:
+        msg = lib().nx_last_error().decode(errors="replace")
+        raise NxError(f"libnxhip error {rc}: {msg}")
+
+
+def _ptr(a: np.ndarray | None, ctype):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    check(lib().nx_device_count(C.byref(n)))
+    return int(n.value)
+
+
+class Handle:
+    """Owning wrapper of an ``nx_network_t*`` (one local problem on one device)."""
+
+    def __init__(self, device: int, N: int, edge_x: np.ndarray, edge_lm: np.ndarray,
+                 lm_rowptr: np.ndarray, lm_col: np.ndarray, lm_val: np.ndarray, n_ghost: int = 0):
+        L = lib()
+        self._keep = []
+        edge_x = np.ascontiguousarray(edge_x, dtype=np.float64).reshape(-1)
+        edge_lm = np.ascontiguousarray(edge_lm, dtype=np.int32).reshape(-1)
+        lm_rowptr = np.ascontiguousarray(lm_rowptr, dtype=np.int32)
+        lm_col = np.ascontiguousarray(lm_col, dtype=np.int32)
+        lm_val = np.ascontiguousarray(lm_val, dtype=np.float64)
+        n_edges = edge_x.size // 6
+        if edge_x.size != 6 * n_edges or edge_lm.size != 2 * n_edges:
+            raise ValueError("edge_x must be (E, 6) and edge_lm (E, 2)")
+        n_lm = lm_rowptr.size - 1
+        h = C.c_void_p()
+        check(L.nx_create(int(device), int(N), int(n_edges), _ptr(edge_x, C.c_double),
+                          _ptr(edge_lm, C.c_int32), int(n_lm), _ptr(lm_rowptr, C.c_int32),
+                          _ptr(lm_col, C.c_int32), _ptr(lm_val, C.c_double), int(n_ghost),
+                          C.byref(h)))
+        self._h = h
+        self.device = int(device)
+        self.N = int(N)
+        self.n_edges = int(n_edges)
+        self.n_lm = int(n_lm)
+        r, c, z = C.c_int64(), C.c_int64(), C.c_int64()
+        check(L.nx_dims(h, C.byref(r), C.byref(c), C.byref(z)))
+        self.n_rows, self.n_cols, self.nnz = int(r.value), int(c.value), int(z.value)
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().nx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ptr(self):
+        if not self._h:
+            raise NxError("handle is closed")
+        return self._h
+
+    # ------------------------------------------------------------------ calls
+    def set_coefficients(self, edge_R: np.ndarray | None, R_const: float, f: float,
+                         edge_bc: np.ndarray) -> None:
+        eR = None if edge_R is None else np.ascontiguousarray(edge_R, dtype=np.float64)
+        bc = np.ascontiguousarray(edge_bc, dtype=np.float64).reshape(-1)
+        if bc.size != 2 * self.n_edges or (eR is not None and eR.size != self.n_edges):
+            raise ValueError("edge_bc must be (E, 2) and edge_R (E,)")
+        check(lib().nx_set_coefficients(self.ptr, _ptr(eR, C.c_double), float(R_const), float(f),
+                                        _ptr(bc, C.c_double)))
+
+    def assemble(self, lhs: bool = True, rhs: bool = True) -> None:
+        check(lib().nx_assemble(self.ptr, int(bool(lhs)), int(bool(rhs))))
+
+    def solve(self, rtol: float, maxit: int, check_every: int = 32):
+        it, rr, conv = C.c_int32(), C.c_double(), C.c_int32()
+        check(lib().nx_solve(self.ptr, float(rtol), int(maxit), int(check_every), C.byref(it),
+                             C.byref(rr), C.byref(conv)))
+        return int(it.value), float(rr.value), bool(conv.value)
+
+    def solution(self) -> np.ndarray:
+        x = np.empty(self.n_rows, dtype=np.float64)
+        check(lib().nx_get_solution(self.ptr, _ptr(x, C.c_double)))
+        return x
+
+    def rhs(self) -> np.ndarray:
+        b = np.empty(self.n_rows, dtype=np.float64)
+        check(lib().nx_get_rhs(self.ptr, _ptr(b, C.c_double)))
+        return b
+
+    def csr(self):
+        rp = np.empty(self.n_rows + 1, dtype=np.int32)
+        col = np.empty(self.nnz, dtype=np.int32)
+        val = np.empty(self.nnz, dtype=np.float64)
+        check(lib().nx_get_csr(self.ptr, _ptr(rp, C.c_int32), _ptr(col, C.c_int32),
+                               _ptr(val, C.c_double)))
+        return rp, col, val
+
+    def spmv(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if x.size != self.n_cols:
+            raise ValueError(f"x must have {self.n_cols} entries")
+        y = np.empty(self.n_rows, dtype=np.float64)
+        check(lib().nx_spmv_host(self.ptr, _ptr(x, C.c_double), _ptr(y, C.c_double)))
+        return y
+
+    def true_residual(self) -> float:
+        r = C.c_double()
+        check(lib().nx_true_residual(self.ptr, C.byref(r)))
+        return float(r.value)
+
+    def sync(self) -> None:
+        check(lib().nx_sync(self.ptr))
+
+    def set_profiling(self, enable: bool) -> None:
+        check(lib().nx_set_profiling(self.ptr, int(bool(enable))))
+
+    def profile(self):
+        a, b, c, d = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
+        check(lib().nx_get_profile(self.ptr, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return {"spmv_ms": a.value, "spmv_count": b.value, "asm_ms": c.value, "asm_count": d.value}
+
+    def reset_profile(self) -> None:
+        check(lib().nx_reset_profile(self.ptr))
+
+    def bench_spmv(self, reps: int) -> float:
+        ms = C.c_double()
+        check(lib().nx_bench_spmv(self.ptr, int(reps), C.byref(ms)))
+        return float(ms.value)
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes, peers, send_off, send_idx, recv_off):
+        uid_arr = (C.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        peers = np.ascontiguousarray(peers, dtype=np.int32)
+        send_off = np.ascontiguousarray(send_off, dtype=np.int32)
+        send_idx = np.ascontiguousarray(send_idx, dtype=np.int32)
+        recv_off = np.ascontiguousarray(recv_off, dtype=np.int32)
+        check(lib().nx_comm_init(self.ptr, int(nranks), int(rank), uid_arr, int(peers.size),
+                                 _ptr(peers, C.c_int32), _ptr(send_off, C.c_int32),
+                                 _ptr(send_idx if send_idx.size else np.zeros(1, np.int32),
+                                      C.c_int32),
+                                 _ptr(recv_off, C.c_int32)))
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_ubyte * UNIQUE_ID_BYTES)()
+    check(lib().nx_comm_unique_id(buf))
+    return bytes(buf)

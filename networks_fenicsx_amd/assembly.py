@@ -1,0 +1,335 @@
+"""Device assembly of the hydraulic network system.
+
+Mirrors ``HydraulicNetworkAssembler`` of the reference
+(``src/networks_fenicsx/assembly.py:95-398``): same constructor, ``compute_forms``,
+``assemble`` and accessors. The forms are fixed by the model, so instead of
+generating code from UFL at run time (``assembly.py:288-299``) the closed-form P1/DG0
+element tensors are evaluated by the HIP kernel ``k_assemble`` (``csrc/nxhip.hip``),
+one wavefront per graph edge, straight into a CSR matrix resident in HBM:
+
+====================  =============================  ==========================
+reference form        element tensor (cell length h)  device rows
+====================  =============================  ==========================
+``R q v dx``          ``R h/3, R h/6``                flux rows (mass)
+``phi dq/ds dx``      ``[-1, +1]`` up/downstream      pressure rows (negated)
+``-p dv/ds dx``       ``[+1, -1]^T``                  flux rows
+``+-mu q ds``         ``+1`` in-edge end, ``-1`` out   multiplier rows
+``+-lmbda v ds``      same, transposed                flux end rows
+``p_bc v ds(in/out)`` ``+p_bc`` leaves, ``-p_bc`` roots rhs of flux end rows
+``f phi dx``          ``f h``                         rhs of pressure rows (negated)
+====================  =============================  ==========================
+
+The pressure rows (and their rhs) are negated so the matrix is symmetric; this does
+not change the solution and lets MINRES replace the direct solve.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import typing
+
+import numpy as np
+
+from . import _lib
+from .fem import Constant, FunctionSpace
+from .layout import LocalProblem, build_local_problem
+from .mesh import NetworkMesh
+from .timing import timed
+
+__all__ = ["HydraulicNetworkAssembler", "DeviceMatrix", "DeviceVector", "evaluate_nodal"]
+
+
+def _device_for_rank() -> int:
+    env = os.environ.get("NXHIP_DEVICE")
+    if env is not None:
+        return int(env)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = _lib.device_count()
+    if n < 1:
+        raise _lib.NxError("no HIP device visible: the network assembler runs on the GPU only")
+    return local % n
+
+
+def evaluate_nodal(p_bc_ex, pos: np.ndarray) -> np.ndarray:
+    """Nodal values of the pressure boundary data at the graph nodes.
+
+    The reference interpolates ``p_bc_ex`` into P1 on the network mesh
+    (``assembly.py:225-234``); only vertex values at boundary nodes reach the rhs, so
+    evaluating at the graph nodes is exact. Accepted forms: a callable ``x -> values``
+    with DOLFINx's ``x`` of shape ``(3, n)``; an object with ``eval(x)``
+    (``PressureFunction`` protocol, ``assembly.py:24-25``); an array of nodal values;
+    or a scalar.
+    """
+    n = pos.shape[0]
+    x = np.zeros((3, n), dtype=np.float64)
+    x[: pos.shape[1], :] = pos.T
+    if hasattr(p_bc_ex, "eval") and not callable(p_bc_ex):
+        vals = p_bc_ex.eval(x)
+    elif callable(p_bc_ex):
+        vals = p_bc_ex(x)
+    else:
+        vals = p_bc_ex
+    vals = np.asarray(vals, dtype=np.float64)
+    if vals.ndim == 0:
+        vals = np.full(n, float(vals))
+    vals = vals.reshape(-1)
+    if vals.size != n:
+        raise ValueError(f"p_bc gave {vals.size} values for {n} nodes")
+    return vals
+
+
+def _scalar(c, name: str, default: float) -> float:
+    if c is None:
+        return default
+    if isinstance(c, Constant):
+        return float(c.value)
+    if hasattr(c, "value"):
+        return float(np.asarray(c.value))
+    return float(c)
+
+
+class DeviceVector:
+    """The rhs ``b`` resident on the device (returned where PETSc returned a ``Vec``)."""
+
+    def __init__(self, handle: _lib.Handle):
+        self._handle = handle
+
+    def getArray(self) -> np.ndarray:  # noqa: N802 (petsc4py spelling)
+        return self._handle.rhs()
+
+    @property
+    def array(self) -> np.ndarray:
+        return self._handle.rhs()
+
+    def getSize(self) -> int:  # noqa: N802
+        return self._handle.n_rows
+
+
+class DeviceMatrix:
+    """The assembled CSR matrix resident on the device (stands in for a PETSc ``Mat``)."""
+
+    def __init__(self, handle: _lib.Handle, kind=None):
+        self._handle = handle
+        self.kind = kind
+
+    def getType(self) -> str:  # noqa: N802
+        return "nest" if self.kind == "nest" else "aij"
+
+    def getSize(self):  # noqa: N802
+        return (self._handle.n_rows, self._handle.n_cols)
+
+    def csr(self):
+        return self._handle.csr()
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+
+        rp, col, val = self._handle.csr()
+        return sp.csr_matrix((val, col, rp), shape=(self._handle.n_rows, self._handle.n_cols))
+
+    def mult(self, x: np.ndarray) -> np.ndarray:
+        return self._handle.spmv(x)
+
+
+class HydraulicNetworkAssembler:
+    """Assembler for the mixed hydraulic network problem
+
+    ``R q + dp/ds = 0``, ``dq/ds = f`` on every edge, with flux conservation at the
+    bifurcations enforced by Lagrange multipliers (reference ``assembly.py:95-118``).
+
+    Args:
+        mesh: the :class:`NetworkMesh`
+        flux_degree: polynomial degree of the flux (only 1 is implemented)
+        pressure_degree: polynomial degree of the pressure (only 0 is implemented)
+    """
+
+    @timed("nxfx:HydraulicNetworkAssembler:__init__")
+    def __init__(self, mesh: NetworkMesh, flux_degree: int = 1, pressure_degree: int = 0):
+        if flux_degree != 1 or pressure_degree != 0:
+            raise NotImplementedError(
+                "the device path implements the reference defaults flux_degree=1, "
+                "pressure_degree=0 (assembly.py:121); other degrees are a later extension"
+            )
+        self._network_mesh = mesh
+        comm = mesh.comm
+        self._rank, self._nranks = comm.rank, comm.size
+        src, dst = mesh.edges
+        self._local: LocalProblem = build_local_problem(
+            mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, self._rank, self._nranks
+        )
+        lp = self._local
+        self._handle = _lib.Handle(_device_for_rank(), mesh.N, lp.edge_x, lp.edge_lm,
+                                   lp.lm_rowptr, lp.lm_col, lp.lm_val, lp.n_ghost)
+        if self._nranks > 1:
+            self._init_comm()
+        self._a = None
+        self._L = None
+        self._make_spaces()
+
+    def _init_comm(self) -> None:
+        comm = self._network_mesh.comm
+        uid = _lib.comm_unique_id() if self._rank == 0 else None
+        uid = comm.bcast(uid, root=0)
+        lp = self._local
+        self._handle.comm_init(self._nranks, self._rank, uid, lp.peers, lp.send_off,
+                               lp.send_idx, lp.recv_off)
+
+    def _make_spaces(self) -> None:
+        mesh, lp, N = self._network_mesh, self._local, self._network_mesh.N
+        colors = mesh.edge_colors[lp.edges]
+        order = np.argsort(colors, kind="stable")  # graph.edges() order inside a colour
+        bounds = np.searchsorted(colors[order], np.arange(mesh.num_edge_colors + 1))
+        self._flux_spaces = []
+        for c in range(mesh.num_edge_colors):
+            edges = lp.edges[order[bounds[c]:bounds[c + 1]]]
+            self._flux_spaces.append(
+                FunctionSpace(mesh, "flux", "P", 1, False, edges.size * (N + 1), edges, c))
+        self._pressure_space = FunctionSpace(mesh, "pressure", "DG", 0, True,
+                                             lp.edges.size * N, lp.edges)
+        self._lm_space = FunctionSpace(mesh, "multiplier", "DG", 0, True, lp.lm_nodes.size)
+        # gather maps: device vector -> function arrays
+        per = 2 * N + 1
+        slot = np.full(mesh.num_edges, -1, dtype=np.int64)
+        slot[lp.edges] = np.arange(lp.edges.size)
+        all_q = (np.arange(lp.edges.size)[:, None] * per + 2 * np.arange(N + 1)[None, :])
+        q_sorted = all_q[slot[lp.edges[order]]].ravel()  # flux DoFs grouped by colour
+        cuts = bounds * (N + 1)
+        self._flux_idx = [q_sorted[cuts[c]:cuts[c + 1]] for c in range(mesh.num_edge_colors)]
+        self._p_idx = (np.arange(lp.edges.size)[:, None] * per
+                       + 2 * np.arange(N)[None, :] + 1).ravel()
+        self._lm_idx = lp.n_edge_dofs + np.arange(lp.lm_nodes.size)
+
+    # ------------------------------------------------------------------ forms
+    @timed("nxfx:HydraulicNetworkAssembler:compute_forms")
+    def compute_forms(
+        self,
+        p_bc_ex: typing.Any,
+        f: typing.Any = None,
+        R: typing.Any = None,
+        jit_options: dict | None = None,
+        form_compiler_options: dict | None = None,
+    ) -> None:
+        """Evaluate the coefficients of the forms and upload them to the device.
+
+        Args:
+            p_bc_ex: pressure boundary data (callable ``x -> values``, object with
+                ``eval``, nodal array or scalar), imposed weakly at inlet/outlet nodes.
+            f: constant source of the mass-conservation equation (default 0,
+                ``assembly.py:201-202``).
+            R: resistance -- a constant (default 1, ``assembly.py:204-205``) or one
+                value per graph edge (``graph.edges()`` order).
+            jit_options, form_compiler_options: accepted for API compatibility; the
+                element tensors are compiled into the HIP library ahead of time.
+        """
+        del jit_options, form_compiler_options
+        mesh, lp = self._network_mesh, self._local
+        f_val = _scalar(f, "f", 0.0)
+        R_const, R_edge = 1.0, None
+        if R is not None:
+            Rv = R.value if isinstance(R, Constant) else R
+            Rv = np.asarray(Rv, dtype=np.float64)
+            if Rv.ndim == 0:
+                R_const = float(Rv)
+            elif Rv.size == mesh.num_edges:
+                R_edge = np.ascontiguousarray(Rv[lp.edges])
+            else:
+                raise ValueError("R must be a constant or one value per graph edge")
+        pbc = evaluate_nodal(p_bc_ex, mesh.node_coordinates)
+        src, dst = mesh.edges
+        s, d = src[lp.edges], dst[lp.edges]
+        leaf = np.zeros(mesh.num_nodes, dtype=bool)
+        leaf[mesh.boundary_in_nodes] = True
+        root = np.zeros(mesh.num_nodes, dtype=bool)
+        root[mesh.boundary_out_nodes] = True
+        edge_bc = np.zeros((lp.edges.size, 2), dtype=np.float64)
+        edge_bc[:, 0] = np.where(root[s], -pbc[s], 0.0)  # - p_bc ds(out_marker)
+        edge_bc[:, 1] = np.where(leaf[d], pbc[d], 0.0)  # + p_bc ds(in_marker)
+        self._handle.set_coefficients(R_edge, R_const, f_val, edge_bc)
+        self._a = ("device-forms", R_const if R_edge is None else "per-edge", f_val)
+        self._L = ("device-rhs", pbc)
+
+    # ---------------------------------------------------------------- assemble
+    @timed("nxfx:HydraulicNetworkAssembler:assemble")
+    def assemble(self, A=None, b=None, assemble_lhs: bool = True, assemble_rhs: bool = True,
+                 kind=None):
+        """Assemble the system matrix and/or rhs on the device.
+
+        Returns ``(A, b)`` views of the device-resident CSR matrix and rhs (the
+        reference returns PETSc objects, ``assembly.py:329-368``). ``kind`` is
+        recorded; the device storage is always one CSR matrix.
+        """
+        if self._a is None:
+            raise RuntimeError("compute_forms() must be called before assemble()")
+        self._handle.assemble(assemble_lhs, assemble_rhs)
+        self._handle.sync()
+        if A is None and assemble_lhs:
+            A = DeviceMatrix(self._handle, kind)
+        if b is None and assemble_rhs:
+            b = DeviceVector(self._handle)
+        return (A, b)
+
+    # --------------------------------------------------------------- accessors
+    @property
+    def handle(self) -> _lib.Handle:
+        return self._handle
+
+    @property
+    def local_problem(self) -> LocalProblem:
+        return self._local
+
+    @property
+    def lm_space(self) -> FunctionSpace:
+        return self._lm_space
+
+    @property
+    def pressure_space(self) -> FunctionSpace:
+        return self._pressure_space
+
+    @property
+    def flux_spaces(self) -> list[FunctionSpace]:
+        return self._flux_spaces
+
+    @property
+    def function_spaces(self) -> list[FunctionSpace]:
+        return [*self._flux_spaces, self._pressure_space, self._lm_space]
+
+    @property
+    def network(self) -> NetworkMesh:
+        return self._network_mesh
+
+    @property
+    def bilinear_forms(self):
+        if self._a is None:
+            logging.error("Bilinear forms haven't been computed. Need to call compute_forms()")
+            return None
+        return self._a
+
+    def bilinear_form(self, i: int, j: int):
+        n = len(self.function_spaces)
+        if i >= n or j >= n:
+            logging.error("Bilinear form a[%d][%d] out of range", i, j)
+        return self.bilinear_forms
+
+    @property
+    def linear_forms(self):
+        if self._L is None:
+            logging.error("Linear forms haven't been computed. Need to call compute_forms()")
+            return None
+        return self._L
+
+    def linear_form(self, i: int):
+        if i >= len(self.function_spaces):
+            logging.error("Linear form L[%d] out of range", i)
+        return self.linear_forms
+
+    def scatter_solution(self, x: np.ndarray, functions: list) -> list:
+        """Split the device-layout vector into ``[flux..., pressure, multiplier]``."""
+        for fn, idx in zip(functions[:-2], self._flux_idx):
+            fn.x.array[:] = x[idx]
+        functions[-2].x.array[:] = x[self._p_idx]
+        functions[-1].x.array[:] = x[self._lm_idx]
+        return functions
+
+    def close(self) -> None:
+        self._handle.close()

@@ -1,0 +1,64 @@
+"""Build the in-tree HIP library ``libnxhip.so`` for gfx950.
+
+``hipcc`` cross-compiles for gfx950 without a GPU, so this runs in the CPU build
+container too. The ``.so`` is written next to this file (in-tree, git-ignored) so
+that it travels to the GPU box with the repository snapshot.
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+SRC = HERE / "csrc" / "nxhip.hip"
+HEADER = HERE.parent / "include" / "nxhip.h"
+LIB = HERE / "libnxhip.so"
+ARCH = os.environ.get("NXHIP_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the HIP toolchain is required to build libnxhip.so")
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in (SRC, HEADER))
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile ``csrc/nxhip.hip`` into ``libnxhip.so`` (skipped when up to date)."""
+    if not force and not needs_build():
+        return LIB
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [
+        _hipcc(),
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-shared",
+        "-Wall",
+        "-o",
+        str(tmp),
+        str(SRC),
+        "-lrccl",
+    ]
+    if verbose:
+        print(" ".join(cmd))
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

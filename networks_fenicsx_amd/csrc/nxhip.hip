@@ -1,0 +1,1175 @@
+// nxhip.hip -- MI355X (gfx950) assemble + MINRES path for the hydraulic network
+// saddle-point system of networks_fenicsx. C ABI in include/nxhip.h.
+//
+// Reference semantics (files under /root/reference/src/networks_fenicsx/):
+//   forms            assembly.py:243-277 (mass, divergence, gradient, junctions, rhs)
+//   assemble         assembly.py:328-368, solver.py:488-499
+//   solve            solver.py:505-533 (PETSc KSP; MUMPS LU by default) -> MINRES here
+//   mesh geometry    mesh.py:295-347 (interior points x_u (1-w) + x_v w, w = k/N)
+//
+// Layout per rank (see include/nxhip.h): edge e owns rows [e(2N+1), (e+1)(2N+1)),
+// interleaved q_0 p_0 q_1 ... p_{N-1} q_N, then the owned multipliers. With this
+// order an edge's CSR rows form ONE contiguous segment of 7N+1(+1 per junction end)
+// entries, so the assembly kernel writes every value with unit-stride stores and
+// the SpMV gathers x from a +-2 band (plus the far multiplier columns).
+//
+// Pressure rows are negated (and their rhs) so A is symmetric; MINRES needs that.
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nxhip.h"
+
+#define NX_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kVersion = 1 * 10000 + 0 * 100 + 0;
+constexpr int kBlock = 256;         // threads per block (4 wave64)
+constexpr int kRowsPerBlock = 256;  // SpMV: one row per thread
+constexpr int kLdsCap = 2048;       // SpMV: products staged per block (16 KiB)
+constexpr int kReduceThreads = 1024;
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCALL(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(NX_ERR_HIP, std::string(#expr) + " failed: " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCLCALL(expr)                                                                      \
+  do {                                                                                      \
+    ncclResult_t r_ = (expr);                                                               \
+    if (r_ != ncclSuccess)                                                                  \
+      return fail(NX_ERR_RCCL, std::string(#expr) + " failed: " + ncclGetErrorString(r_)); \
+  } while (0)
+
+#define CHECK(expr)      \
+  do {                   \
+    int rc_ = (expr);    \
+    if (rc_ != NX_OK) return rc_; \
+  } while (0)
+
+// ------------------------------------------------------------------------------------
+// MINRES state, resident in device memory. Scalar recurrences follow Paige & Saunders
+// (1975) in the form of scipy.sparse.linalg.minres (unpreconditioned, shift 0).
+struct MinresState {
+  double beta1, beta, oldb, alfa, dbar, epsln, phibar, cs, sn, tnorm2;
+  double p_oldeps, p_delta, p_denom, p_phi;  // pending w/x update of iteration `it`
+  double relres, rtol;
+  double red[4];  // cross-rank reduction slots
+  int it, maxit, done, converged;
+};
+
+// ------------------------------------------------------------------------------------
+// Entry decoding of one edge's CSR segment. With s = (source is a bifurcation), the
+// segment is   [q_0: 3+s][p_0: 2][q_1: 5][p_1: 2] ... [q_{N-1}: 5][p_{N-1}: 2][q_N: 3+t]
+// Columns are edge-local DoFs (2k = q_k, 2k+1 = p_k) or LM_SRC / LM_DST.
+enum : int { V_P1 = 0, V_M1 = 1, V_MD = 2, V_MO = 3, V_MD2 = 4 };
+constexpr int LM_SRC = -1, LM_DST = -2;
+
+struct Entry {
+  int row, col, vk, cell;
+};
+
+__device__ __forceinline__ Entry decode_entry(int i, int N, int s) {
+  Entry en;
+  const int q0len = 3 + s;
+  if (i < q0len) {  // row q_0: [q_0, p_0, q_1, (lambda_src)]
+    en.row = 0;
+    en.cell = 0;
+    en.col = (i < 3) ? i : LM_SRC;
+    en.vk = (i == 0) ? V_MD : (i == 1) ? V_P1 : (i == 2) ? V_MO : V_M1;
+    return en;
+  }
+  const int i1 = i - q0len;
+  const int g = i1 / 7;
+  const int r = i1 - 7 * g;
+  if (g < N - 1) {
+    if (r < 2) {  // row p_g (negated divergence): +1 at q_g, -1 at q_{g+1}
+      en.row = 2 * g + 1;
+      en.col = 2 * g + 2 * r;
+      en.vk = r ? V_M1 : V_P1;
+      en.cell = g;
+    } else {  // interior row q_{g+1}: [q_g, p_g, q_{g+1}, p_{g+1}, q_{g+2}]
+      const int j = r - 2;
+      en.row = 2 * g + 2;
+      en.col = 2 * g + j;
+      en.vk = (j == 0) ? V_MO : (j == 1) ? V_M1 : (j == 2) ? V_MD2 : (j == 3) ? V_P1 : V_MO;
+      en.cell = (j == 4) ? g + 1 : g;
+    }
+    return en;
+  }
+  const int i2 = i1 - 7 * (N - 1);
+  if (i2 < 2) {  // row p_{N-1}
+    en.row = 2 * N - 1;
+    en.col = 2 * (N - 1) + 2 * i2;
+    en.vk = i2 ? V_M1 : V_P1;
+    en.cell = N - 1;
+    return en;
+  }
+  const int j = i2 - 2;  // row q_N: [q_{N-1}, p_{N-1}, q_N, (lambda_dst)]
+  en.row = 2 * N;
+  en.cell = N - 1;
+  en.col = (j < 3) ? 2 * N - 2 + j : LM_DST;
+  en.vk = (j == 0) ? V_MO : (j == 1) ? V_M1 : (j == 2) ? V_MD : V_P1;
+  return en;
+}
+
+// Start of row q_k inside the segment (k = 0..N), and segment length.
+__device__ __forceinline__ int q_row_start(int k, int s) { return k == 0 ? 0 : s + 7 * k - 2; }
+
+struct EdgeArgs {
+  const double* edge_x;  // E*6
+  const int* edge_lm;    // E*2
+  const int* edge_seg;   // E+1 segment offsets into the CSR arrays
+  int64_t E;
+  int N;
+};
+
+// ------------------------------------------------------------------------------------
+// Pattern: one wave per edge writes the row pointers of its 2N+1 rows and the column
+// indices of its segment (unit stride across lanes).
+__global__ __launch_bounds__(kBlock) void k_pattern(EdgeArgs ea, int* __restrict__ rowptr,
+                                                      int* __restrict__ colidx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (e >= ea.E) return;
+  const int N = ea.N;
+  const int lm0 = ea.edge_lm[2 * e], lm1 = ea.edge_lm[2 * e + 1];
+  const int s = lm0 >= 0;
+  const int seg = ea.edge_seg[e];
+  const int len = ea.edge_seg[e + 1] - seg;
+  const int64_t base = e * (2 * N + 1);
+  for (int i = lane; i < len; i += 64) {
+    const Entry en = decode_entry(i, N, s);
+    const int gcol = en.col >= 0 ? (int)(base + en.col) : (en.col == LM_SRC ? lm0 : lm1);
+    colidx[seg + i] = gcol;
+    if (i == 0 || decode_entry(i - 1, N, s).row != en.row) rowptr[base + en.row] = seg + i;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Assembly: one wave per edge. Cells are processed in chunks of 64 (lane = cell):
+// each lane regenerates its cell's vertices exactly like the reference mesh
+// generator, computes the P1 mass element tensor (R h/3, R h/6) and stages it in
+// LDS; then the wave writes the chunk's CSR values (unit stride) reading the staged
+// tensors. Slot 0 of the staging row carries the previous chunk's last cell.
+struct AsmArgs {
+  EdgeArgs ea;
+  const double* edge_R;   // E (per-edge R)
+  const double* edge_bc;  // E*2 rhs at q_0 / q_N
+  double f;
+  double* val;
+  double* rhs;
+  int lhs, do_rhs;
+};
+
+__device__ __forceinline__ void vertex(const double* x0, const double* x1, int k, int N,
+                                       double invN, double* p) {
+#pragma clang fp contract(off)
+  if (k == 0) {
+    p[0] = x0[0]; p[1] = x0[1]; p[2] = x0[2];
+  } else if (k == N) {
+    p[0] = x1[0]; p[1] = x1[1]; p[2] = x1[2];
+  } else {
+    // numpy: w = k * (1/N); start * (1 - w) + end * w   (mesh.py:300, 315)
+    const double w = (double)k * invN;
+    const double om = 1.0 - w;
+    p[0] = x0[0] * om + x1[0] * w;
+    p[1] = x0[1] * om + x1[1] * w;
+    p[2] = x0[2] * om + x1[2] * w;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
+#pragma clang fp contract(off)
+  __shared__ double s_md[kBlock / 64][65];
+  __shared__ double s_mo[kBlock / 64][65];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * (kBlock / 64) + w;
+  const bool active = e < a.ea.E;  // all waves run the chunk loop (block barriers)
+  const int N = a.ea.N;
+  const double invN = 1.0 / (double)N;
+  double x0[3] = {0, 0, 0}, x1[3] = {0, 0, 0};
+  double R = 0.0, bc0 = 0.0, bc1 = 0.0;
+  int s = 0, seg = 0, seglen = 0, lm0 = -1, lm1 = -1;
+  int64_t base = 0;
+  if (active) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      x0[c] = a.ea.edge_x[6 * e + c];
+      x1[c] = a.ea.edge_x[6 * e + 3 + c];
+    }
+    R = a.edge_R[e];
+    lm0 = a.ea.edge_lm[2 * e];
+    lm1 = a.ea.edge_lm[2 * e + 1];
+    s = lm0 >= 0;
+    seg = a.ea.edge_seg[e];
+    seglen = a.ea.edge_seg[e + 1] - seg;
+    base = e * (2 * N + 1);
+    bc0 = a.edge_bc[2 * e];
+    bc1 = a.edge_bc[2 * e + 1];
+  }
+  (void)lm1;
+  for (int c0 = 0; c0 < N; c0 += 64) {
+    const int nc = min(64, N - c0);
+    if (active && lane < nc) {
+      const int k = c0 + lane;
+      double pa[3], pb[3];
+      vertex(x0, x1, k, N, invN, pa);
+      vertex(x0, x1, k + 1, N, invN, pb);
+      const double d0 = pb[0] - pa[0], d1 = pb[1] - pa[1], d2 = pb[2] - pa[2];
+      const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+      s_md[w][lane + 1] = R * h / 3.0;
+      s_mo[w][lane + 1] = R * h / 6.0;
+      if (a.do_rhs) {
+        a.rhs[base + 2 * k + 1] = -(a.f * h);  // negated pressure row: -(f h)
+        a.rhs[base + 2 * k] = (k == 0) ? bc0 : 0.0;
+      }
+    }
+    if (active && a.do_rhs && lane == 0 && c0 + nc == N) a.rhs[base + 2 * N] = bc1;
+    __syncthreads();
+    if (active && a.lhs) {
+      const int i0 = q_row_start(c0, s);
+      const int i1 = (c0 + nc == N) ? seglen : q_row_start(c0 + nc, s);
+      for (int i = i0 + lane; i < i1; i += 64) {
+        const Entry en = decode_entry(i, N, s);
+        const int slot = en.cell - c0 + 1;  // in [0, 64]
+        double v;
+        switch (en.vk) {
+          case V_P1: v = 1.0; break;
+          case V_M1: v = -1.0; break;
+          case V_MD: v = s_md[w][slot]; break;
+          case V_MO: v = s_mo[w][slot]; break;
+          default: v = s_md[w][slot] + s_md[w][slot + 1]; break;  // interior diagonal
+        }
+        a.val[seg + i] = v;
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+      s_md[w][0] = s_md[w][nc];
+      s_mo[w][0] = s_mo[w][nc];
+    }
+    __syncthreads();
+  }
+}
+
+// Multiplier rows: constant +-1 values and zero rhs (assembly.py:271-277; L[lm] = 0).
+__global__ void k_assemble_lm(int64_t nnz_lm, const double* __restrict__ lm_val,
+                              double* __restrict__ val_lm, int64_t B, double* __restrict__ rhs_lm,
+                              int lhs, int do_rhs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lhs && i < nnz_lm) val_lm[i] = lm_val[i];
+  if (do_rhs && i < B) rhs_lm[i] = 0.0;
+}
+
+// ------------------------------------------------------------------------------------
+// Reductions: deterministic (fixed grid, fixed order), no atomics.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block of kBlock threads -> one partial per block.
+__device__ __forceinline__ void block_sum_store(double v, double* out) {
+  __shared__ double s_w[kBlock / 64];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = s_w[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; ++i) t += s_w[i];
+    *out = t;
+  }
+}
+
+// Sum n partials with one kReduceThreads block; result valid in thread 0.
+__device__ __forceinline__ double reduce_partials(const double* __restrict__ p, int n) {
+  __shared__ double s_w[kReduceThreads / 64];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < n; i += kReduceThreads) v += p[i];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0) {
+    t = s_w[0];
+    for (int i = 1; i < kReduceThreads / 64; ++i) t += s_w[i];
+  }
+  return t;
+}
+
+__global__ __launch_bounds__(kReduceThreads) void k_reduce(const double* __restrict__ p, int n,
+                                                          double* __restrict__ out) {
+  const double t = reduce_partials(p, n);
+  if (threadIdx.x == 0) *out = t;
+}
+
+// ------------------------------------------------------------------------------------
+// CSR SpMV, "stream" form: the block's nonzeros (contiguous because its rows are)
+// are multiplied with the gathered x in one unit-stride sweep and staged in LDS;
+// then each thread sums its own row. Sum order is left-to-right per row in both
+// branches (no FMA), so results do not depend on the branch taken.
+struct Csr {
+  const int* rowptr;
+  const int* col;
+  const double* val;
+  int64_t n_rows;
+};
+
+__device__ __forceinline__ double spmv_row_sum(const Csr& A, const double* __restrict__ x,
+                                               int64_t r0, int nr) {
+#pragma clang fp contract(off)
+  __shared__ int s_rp[kRowsPerBlock + 1];
+  __shared__ double s_prod[kLdsCap];
+  const int tid = threadIdx.x;
+  for (int i = tid; i <= nr; i += kBlock) s_rp[i] = A.rowptr[r0 + i];
+  __syncthreads();
+  const int k0 = s_rp[0], k1 = s_rp[nr];
+  double sum = 0.0;
+  if (k1 - k0 <= kLdsCap) {
+    for (int k = k0 + tid; k < k1; k += kBlock) s_prod[k - k0] = A.val[k] * x[A.col[k]];
+    __syncthreads();
+    if (tid < nr) {
+      const int a = s_rp[tid] - k0, b = s_rp[tid + 1] - k0;
+      for (int k = a; k < b; ++k) sum += s_prod[k];
+    }
+  } else if (tid < nr) {
+    for (int k = s_rp[tid]; k < s_rp[tid + 1]; ++k) {
+      const double p = A.val[k] * x[A.col[k]];
+      sum += p;
+    }
+  }
+  return sum;
+}
+
+__global__ __launch_bounds__(kBlock) void k_spmv(Csr A, const double* __restrict__ x,
+                                                 double* __restrict__ y) {
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
+  const double s = spmv_row_sum(A, x, r0, nr);
+  if ((int)threadIdx.x < nr) y[r0 + threadIdx.x] = s;
+}
+
+// residual r = b - A x, partial ||r||^2 and ||b||^2
+__global__ __launch_bounds__(kBlock) void k_residual(Csr A, const double* __restrict__ x,
+                                                     const double* __restrict__ b,
+                                                     double* __restrict__ partials, int nblk) {
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
+  const double s = spmv_row_sum(A, x, r0, nr);
+  double rr = 0.0, bb = 0.0;
+  if ((int)threadIdx.x < nr) {
+    const double bv = b[r0 + threadIdx.x];
+    const double rv = bv - s;
+    rr = rv * rv;
+    bb = bv * bv;
+  }
+  block_sum_store(rr, partials + blockIdx.x);
+  __syncthreads();
+  block_sum_store(bb, partials + nblk + blockIdx.x);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dot_self(const double* __restrict__ a, int64_t n,
+                                                     double* __restrict__ partials) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const double v = i < n ? a[i] : 0.0;
+  block_sum_store(v * v, partials + blockIdx.x);
+}
+
+// ------------------------------------------------------------------------------------
+// MINRES kernels. One iteration k (1-based) = 4 launches:
+//   k_mr_spmv      y = A v_k - beta_k v_{k-1}  (v_k = r2/beta_k gathered), partial alpha;
+//                  plus the pending solution update of iteration k-1 (fused: it reads
+//                  r1 = beta_{k-1} v_{k-1} anyway)
+//   k_mr_alpha     alpha_k = sum of partials
+//   k_mr_lanczos   r2' = y - (alpha_k / beta_k) r2, partial ||r2'||^2
+//   k_mr_rotate    beta_{k+1}, Givens rotation, convergence test
+// r1/r2 swap roles every iteration and w1/w2 too; the host passes the pointers.
+struct MrVecs {
+  double* r1;        // in: beta_{k-1} v_{k-1} (b at k = 1); out: y
+  const double* r2;  // beta_k v_k, gathered (has ghost slots)
+  double* w1;        // w_{k-2} in, w_{k-1} out (in place)
+  const double* w2;  // w_{k-1}... see k_mr_spmv
+  double* x;
+};
+
+__global__ __launch_bounds__(kBlock) void k_mr_spmv(Csr A, MrVecs v, MinresState* __restrict__ st,
+                                                    double* __restrict__ partials) {
+  if (st->done) return;
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
+  const double Ay = spmv_row_sum(A, v.r2, r0, nr);
+  const int it = st->it;  // completed iterations = k - 1
+  const double beta = st->beta, oldb = st->oldb;
+  const double s = 1.0 / beta;
+  const double c1 = it > 0 ? beta / oldb : 0.0;
+  double part = 0.0;
+  if ((int)threadIdx.x < nr) {
+    const int64_t r = r0 + threadIdx.x;
+    const double r1v = v.r1[r];
+    const double y = s * Ay - c1 * r1v;
+    part = (s * v.r2[r]) * y;
+    v.r1[r] = y;
+    if (it > 0) {  // pending update of iteration k-1: w = (v - oldeps w1 - delta w2)/gamma
+      const double vk = r1v / oldb;
+      const double wn = (vk - st->p_oldeps * v.w1[r] - st->p_delta * v.w2[r]) * st->p_denom;
+      v.w1[r] = wn;
+      v.x[r] += st->p_phi * wn;
+    }
+  }
+  block_sum_store(part, partials + blockIdx.x);
+}
+
+// Solution update of the last iteration (after convergence / maxit).
+__global__ __launch_bounds__(kBlock) void k_mr_finalize(int64_t n, MrVecs v,
+                                                        const MinresState* __restrict__ st) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (st->it == 0 || r >= n) return;
+  const double vk = v.r1[r] / st->oldb;
+  const double wn = (vk - st->p_oldeps * v.w1[r] - st->p_delta * v.w2[r]) * st->p_denom;
+  v.w1[r] = wn;
+  v.x[r] += st->p_phi * wn;
+}
+
+__global__ __launch_bounds__(kBlock) void k_mr_lanczos(int64_t n, double* __restrict__ y,
+                                                       const double* __restrict__ r2,
+                                                       const MinresState* __restrict__ st,
+                                                       double* __restrict__ partials) {
+  if (st->done) return;
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const double c2 = st->alfa / st->beta;
+  double part = 0.0;
+  if (r < n) {
+    const double v = y[r] - c2 * r2[r];
+    y[r] = v;
+    part = v * v;
+  }
+  block_sum_store(part, partials + blockIdx.x);
+}
+
+__device__ void mr_rotate_scalar(MinresState* st, double b2) {
+  const double alfa = st->alfa;
+  const double oldb = st->beta;
+  const double beta = sqrt(b2);
+  st->oldb = oldb;
+  st->beta = beta;
+  st->tnorm2 += alfa * alfa + oldb * oldb + beta * beta;
+  const double oldeps = st->epsln;
+  const double delta = st->cs * st->dbar + st->sn * alfa;
+  const double gbar = st->sn * st->dbar - st->cs * alfa;
+  st->epsln = st->sn * beta;
+  st->dbar = -st->cs * beta;
+  double gamma = hypot(gbar, beta);
+  gamma = fmax(gamma, 2.220446049250313e-16);
+  st->cs = gbar / gamma;
+  st->sn = beta / gamma;
+  const double phi = st->cs * st->phibar;
+  st->phibar = st->sn * st->phibar;
+  st->p_oldeps = oldeps;
+  st->p_delta = delta;
+  st->p_denom = 1.0 / gamma;
+  st->p_phi = phi;
+  st->it += 1;
+  st->relres = st->phibar / st->beta1;
+  if (st->relres <= st->rtol || beta == 0.0) {
+    st->done = 1;
+    st->converged = 1;
+  } else if (st->it >= st->maxit || !(st->relres == st->relres)) {
+    st->done = 1;
+  }
+}
+
+// FROM_PARTIALS: single rank (sum partials here); else read the all-reduced slot.
+template <bool FROM_PARTIALS>
+__global__ __launch_bounds__(kReduceThreads) void k_mr_alpha(const double* __restrict__ partials,
+                                                             int n, MinresState* __restrict__ st) {
+  if (st->done) return;
+  double t = 0.0;
+  if (FROM_PARTIALS) t = reduce_partials(partials, n);
+  if (threadIdx.x == 0) st->alfa = FROM_PARTIALS ? t : st->red[0];
+}
+
+template <bool FROM_PARTIALS>
+__global__ __launch_bounds__(kReduceThreads) void k_mr_rotate(const double* __restrict__ partials,
+                                                              int n, MinresState* __restrict__ st) {
+  if (st->done) return;
+  double t = 0.0;
+  if (FROM_PARTIALS) t = reduce_partials(partials, n);
+  if (threadIdx.x == 0) mr_rotate_scalar(st, FROM_PARTIALS ? t : st->red[1]);
+}
+
+// Reduce partials into a state slot (multi-rank: the slot is then all-reduced).
+__global__ __launch_bounds__(kReduceThreads) void k_reduce_slot(const double* __restrict__ partials,
+                                                                int n, MinresState* __restrict__ st,
+                                                                int slot, int check_done) {
+  if (check_done && st->done) return;
+  const double t = reduce_partials(partials, n);
+  if (threadIdx.x == 0) st->red[slot] = t;
+}
+
+template <bool FROM_PARTIALS>
+__global__ __launch_bounds__(kReduceThreads) void k_mr_init(const double* __restrict__ partials,
+                                                            int n, MinresState* __restrict__ st,
+                                                            double rtol, int maxit) {
+  double t = 0.0;
+  if (FROM_PARTIALS) t = reduce_partials(partials, n);
+  if (threadIdx.x == 0) {
+    const double bb = FROM_PARTIALS ? t : st->red[2];
+    const double beta1 = sqrt(bb);
+    MinresState s{};
+    s.beta1 = beta1;
+    s.beta = beta1;
+    s.oldb = 0.0;
+    s.phibar = beta1;
+    s.cs = -1.0;
+    s.sn = 0.0;
+    s.rtol = rtol;
+    s.maxit = maxit;
+    s.relres = beta1 > 0.0 ? 1.0 : 0.0;
+    if (beta1 == 0.0) {
+      s.done = 1;
+      s.converged = 1;
+    }
+    *st = s;
+  }
+}
+
+__global__ void k_pack(const double* __restrict__ x, const int* __restrict__ idx, int n,
+                       double* __restrict__ buf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) buf[i] = x[idx[i]];
+}
+
+}  // namespace
+
+// ======================================================================================
+// Host side
+// ======================================================================================
+
+struct nx_network {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int N = 0;
+  int64_t E = 0, B = 0, n_edge_dofs = 0, n_own = 0, n_ghost = 0, n_col = 0;
+  int64_t nnz_edges = 0, nnz_lm = 0, nnz = 0;
+  int nblk = 0;  // blocks of kRowsPerBlock rows
+  // topology / coefficients
+  double* edge_x = nullptr;
+  int* edge_lm = nullptr;
+  int* edge_seg = nullptr;
+  double* edge_R = nullptr;
+  double* edge_bc = nullptr;
+  double* lm_val = nullptr;
+  double f = 0.0;
+  bool have_coeffs = false, have_lhs = false, have_rhs = false;
+  // CSR + rhs
+  int* rowptr = nullptr;
+  int* col = nullptr;
+  double* val = nullptr;
+  double* rhs = nullptr;
+  // Krylov vectors
+  double* vb[2] = {nullptr, nullptr};  // r1/r2, n_col each
+  double* wb[2] = {nullptr, nullptr};  // w1/w2, n_own each
+  double* x = nullptr;                 // n_col
+  double* tmp = nullptr;               // n_col (host SpMV / residual)
+  double* partials = nullptr;          // 2 * nblk
+  MinresState* st = nullptr;
+  MinresState* h_st = nullptr;  // pinned host mirror
+  // graph chunk
+  hipGraphExec_t chunk_exec = nullptr;
+  hipGraph_t chunk_graph = nullptr;
+  int chunk_len = 0;
+  // profiling
+  bool prof = false;
+  double spmv_ms = 0.0, asm_ms = 0.0;
+  int64_t spmv_cnt = 0, asm_cnt = 0;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  // multi-rank
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  std::vector<int> peers, send_off, recv_off;
+  int* send_idx = nullptr;
+  double* send_buf = nullptr;
+};
+
+namespace {
+
+int grid_of(int64_t n, int per) { return (int)((n + per - 1) / per); }
+
+template <class T>
+int dalloc(T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) return NX_OK;
+  HIPCALL(hipMalloc((void**)p, sizeof(T) * (size_t)count));
+  return NX_OK;
+}
+
+template <class T>
+int upload(T** p, const T* host, int64_t count, hipStream_t s) {
+  CHECK(dalloc(p, count));
+  if (count > 0) HIPCALL(hipMemcpyAsync(*p, host, sizeof(T) * count, hipMemcpyHostToDevice, s));
+  return NX_OK;
+}
+
+Csr csr_of(const nx_network* h) { return Csr{h->rowptr, h->col, h->val, h->n_own}; }
+
+// halo: fill the ghost slots of vector `v` (n_col) from the owning ranks
+int halo(nx_network* h, double* v) {
+  if (h->comm == nullptr || h->peers.empty()) return NX_OK;
+  const int nsend = h->send_off.back();
+  if (nsend > 0)
+    hipLaunchKernelGGL(k_pack, dim3(grid_of(nsend, 256)), dim3(256), 0, h->stream, v,
+                       h->send_idx, nsend, h->send_buf);
+  NCCLCALL(ncclGroupStart());
+  for (size_t p = 0; p < h->peers.size(); ++p) {
+    const int sc = h->send_off[p + 1] - h->send_off[p];
+    const int rc = h->recv_off[p + 1] - h->recv_off[p];
+    if (sc > 0)
+      NCCLCALL(ncclSend(h->send_buf + h->send_off[p], sc, ncclDouble, h->peers[p], h->comm,
+                        h->stream));
+    if (rc > 0)
+      NCCLCALL(ncclRecv(v + h->n_own + h->recv_off[p], rc, ncclDouble, h->peers[p], h->comm,
+                        h->stream));
+  }
+  NCCLCALL(ncclGroupEnd());
+  return NX_OK;
+}
+
+int allreduce_slot(nx_network* h, int slot) {
+  NCCLCALL(ncclAllReduce(&h->st->red[slot], &h->st->red[slot], 1, ncclDouble, ncclSum, h->comm,
+                         h->stream));
+  return NX_OK;
+}
+
+// One MINRES iteration on the stream; `k` = 1-based iteration index (parity only).
+int launch_iteration(nx_network* h, int64_t k) {
+  double* r1 = h->vb[(k - 1) & 1];
+  double* r2 = h->vb[k & 1];
+  // pending update belongs to iteration k-1: w1 = wb[(k-2)&1], w2 = wb[(k-1)&1]
+  double* w1 = h->wb[k & 1];
+  double* w2 = h->wb[(k - 1) & 1];
+  const bool multi = h->comm != nullptr;
+  if (multi) CHECK(halo(h, r2));
+  MrVecs mv{r1, r2, w1, w2, h->x};
+  if (h->nblk > 0) {
+    if (h->prof) HIPCALL(hipEventRecord(h->ev[0], h->stream));
+    hipLaunchKernelGGL(k_mr_spmv, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), mv, h->st,
+                       h->partials);
+    if (h->prof) {
+      HIPCALL(hipEventRecord(h->ev[1], h->stream));
+      HIPCALL(hipEventSynchronize(h->ev[1]));
+      float ms = 0.f;
+      HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+      h->spmv_ms += ms;
+      h->spmv_cnt += 1;
+    }
+  }
+  if (multi) {
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                       h->nblk, h->st, 0, 1);
+    CHECK(allreduce_slot(h, 0));
+    hipLaunchKernelGGL(k_mr_alpha<false>, dim3(1), dim3(kReduceThreads), 0, h->stream,
+                       h->partials, h->nblk, h->st);
+  } else {
+    hipLaunchKernelGGL(k_mr_alpha<true>, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                       h->nblk, h->st);
+  }
+  if (h->nblk > 0)
+    hipLaunchKernelGGL(k_mr_lanczos, dim3(h->nblk), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
+                       h->st, h->partials);
+  if (multi) {
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                       h->nblk, h->st, 1, 1);
+    CHECK(allreduce_slot(h, 1));
+    hipLaunchKernelGGL(k_mr_rotate<false>, dim3(1), dim3(kReduceThreads), 0, h->stream,
+                       h->partials, h->nblk, h->st);
+  } else {
+    hipLaunchKernelGGL(k_mr_rotate<true>, dim3(1), dim3(kReduceThreads), 0, h->stream,
+                       h->partials, h->nblk, h->st);
+  }
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+int build_chunk_graph(nx_network* h, int len) {
+  if (h->chunk_exec && h->chunk_len == len) return NX_OK;
+  if (h->chunk_exec) {
+    HIPCALL(hipGraphExecDestroy(h->chunk_exec));
+    h->chunk_exec = nullptr;
+  }
+  if (h->chunk_graph) {
+    HIPCALL(hipGraphDestroy(h->chunk_graph));
+    h->chunk_graph = nullptr;
+  }
+  HIPCALL(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  int rc = NX_OK;
+  for (int j = 0; j < len && rc == NX_OK; ++j) rc = launch_iteration(h, j + 1);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(h->stream, &g);
+  if (rc != NX_OK) return rc;
+  if (e != hipSuccess) return fail(NX_ERR_HIP, std::string("capture: ") + hipGetErrorString(e));
+  h->chunk_graph = g;
+  HIPCALL(hipGraphInstantiate(&h->chunk_exec, g, nullptr, nullptr, 0));
+  h->chunk_len = len;
+  return NX_OK;
+}
+
+int set_device(nx_network* h) {
+  HIPCALL(hipSetDevice(h->device));
+  return NX_OK;
+}
+
+}  // namespace
+
+// ======================================================================================
+// C ABI
+// ======================================================================================
+
+NX_API int nx_version(void) { return kVersion; }
+
+NX_API const char* nx_last_error(void) { return g_err.c_str(); }
+
+NX_API int nx_device_count(int32_t* count) {
+  int n = 0;
+  HIPCALL(hipGetDeviceCount(&n));
+  *count = n;
+  return NX_OK;
+}
+
+NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
+                     const int32_t* edge_lm, int64_t n_lm, const int32_t* lm_rowptr,
+                     const int32_t* lm_col, const double* lm_val, int64_t n_ghost,
+                     nx_network_t** out) {
+  if (out == nullptr) return fail(NX_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (N < 1) return fail(NX_ERR_ARG, "N must be >= 1");
+  if (n_edges < 0 || n_lm < 0 || n_ghost < 0) return fail(NX_ERR_ARG, "negative size");
+  if (n_edges > 0 && (edge_x == nullptr || edge_lm == nullptr))
+    return fail(NX_ERR_ARG, "edge arrays are NULL");
+  if (n_lm > 0 && (lm_rowptr == nullptr || lm_col == nullptr || lm_val == nullptr))
+    return fail(NX_ERR_ARG, "multiplier arrays are NULL");
+  const int64_t per = 2 * (int64_t)N + 1;
+  const int64_t n_edge_dofs = n_edges * per;
+  const int64_t n_own = n_edge_dofs + n_lm;
+  const int64_t n_col = n_own + n_ghost;
+  // segment offsets (host prefix sum), 32-bit CSR indices
+  std::vector<int> seg((size_t)n_edges + 1);
+  int64_t acc = 0;
+  for (int64_t e = 0; e < n_edges; ++e) {
+    seg[e] = (int)acc;
+    const int a = edge_lm[2 * e], b = edge_lm[2 * e + 1];
+    if (a >= n_col || b >= n_col || (a >= 0 && a < n_edge_dofs) || (b >= 0 && b < n_edge_dofs))
+      return fail(NX_ERR_ARG, "edge_lm column out of range (must be a multiplier or ghost column)");
+    acc += 7 * (int64_t)N + 1 + (a >= 0) + (b >= 0);
+  }
+  seg[n_edges] = (int)acc;
+  const int64_t nnz_lm = n_lm > 0 ? lm_rowptr[n_lm] : 0;
+  if (n_lm > 0 && lm_rowptr[0] != 0) return fail(NX_ERR_ARG, "lm_rowptr[0] must be 0");
+  for (int64_t i = 0; i < nnz_lm; ++i)
+    if (lm_col[i] < 0 || lm_col[i] >= n_col) return fail(NX_ERR_ARG, "lm_col out of range");
+  if (acc + nnz_lm >= (int64_t)INT32_MAX || n_col >= (int64_t)INT32_MAX)
+    return fail(NX_ERR_ARG, "problem too large for 32-bit CSR indices on one rank");
+
+  int ndev = 0;
+  HIPCALL(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return fail(NX_ERR_ARG, "device " + std::to_string(device) + " not visible (" +
+                                std::to_string(ndev) + " devices)");
+  HIPCALL(hipSetDevice(device));
+
+  auto* h = new nx_network();
+  h->device = device;
+  h->N = N;
+  h->E = n_edges;
+  h->B = n_lm;
+  h->n_edge_dofs = n_edge_dofs;
+  h->n_own = n_own;
+  h->n_ghost = n_ghost;
+  h->n_col = n_col;
+  h->nnz_edges = acc;
+  h->nnz_lm = nnz_lm;
+  h->nnz = acc + nnz_lm;
+  h->nblk = grid_of(n_own, kRowsPerBlock);
+  auto bail = [&](int rc) {
+    nx_destroy(h);
+    return rc;
+  };
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "hipStreamCreate failed"));
+  int rc = NX_OK;
+  if ((rc = upload(&h->edge_x, edge_x, 6 * n_edges, h->stream))) return bail(rc);
+  if ((rc = upload(&h->edge_lm, edge_lm, 2 * n_edges, h->stream))) return bail(rc);
+  if ((rc = upload(&h->edge_seg, seg.data(), n_edges + 1, h->stream))) return bail(rc);
+  if ((rc = upload(&h->lm_val, lm_val, nnz_lm, h->stream))) return bail(rc);
+  if ((rc = dalloc(&h->edge_R, n_edges))) return bail(rc);
+  if ((rc = dalloc(&h->edge_bc, 2 * n_edges))) return bail(rc);
+  if ((rc = dalloc(&h->rowptr, n_own + 1))) return bail(rc);
+  if ((rc = dalloc(&h->col, h->nnz))) return bail(rc);
+  if ((rc = dalloc(&h->val, h->nnz))) return bail(rc);
+  if ((rc = dalloc(&h->rhs, n_own))) return bail(rc);
+  for (int i = 0; i < 2; ++i) {
+    if ((rc = dalloc(&h->vb[i], n_col))) return bail(rc);
+    if ((rc = dalloc(&h->wb[i], n_own))) return bail(rc);
+  }
+  if ((rc = dalloc(&h->x, n_col))) return bail(rc);
+  if ((rc = dalloc(&h->tmp, n_col))) return bail(rc);
+  if ((rc = dalloc(&h->partials, 2 * (int64_t)std::max(h->nblk, 1)))) return bail(rc);
+  if (hipMalloc((void**)&h->st, sizeof(MinresState)) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "hipMalloc state failed"));
+  if (hipHostMalloc((void**)&h->h_st, sizeof(MinresState), hipHostMallocDefault) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "hipHostMalloc failed"));
+  for (auto& e : h->ev)
+    if (hipEventCreate(&e) != hipSuccess) return bail(fail(NX_ERR_HIP, "hipEventCreate failed"));
+  if (hipMemsetAsync(h->st, 0, sizeof(MinresState), h->stream) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "memset state failed"));
+
+  // pattern: edge segments on the device; multiplier rows from the host lists
+  if (n_edges > 0) {
+    EdgeArgs ea{h->edge_x, h->edge_lm, h->edge_seg, n_edges, N};
+    hipLaunchKernelGGL(k_pattern, dim3(grid_of(n_edges, kBlock / 64)), dim3(kBlock), 0, h->stream,
+                       ea, h->rowptr, h->col);
+  }
+  std::vector<int> rp_lm((size_t)n_lm + 1);
+  for (int64_t b = 0; b <= n_lm; ++b) rp_lm[b] = (int)(acc + (n_lm > 0 ? lm_rowptr[b] : 0));
+  if (hipMemcpyAsync(h->rowptr + n_edge_dofs, rp_lm.data(), sizeof(int) * (n_lm + 1),
+                     hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "rowptr upload failed"));
+  if (nnz_lm > 0 && hipMemcpyAsync(h->col + acc, lm_col, sizeof(int) * nnz_lm,
+                                   hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "lm col upload failed"));
+  if (hipGetLastError() != hipSuccess) return bail(fail(NX_ERR_HIP, "pattern kernel launch failed"));
+  if (hipStreamSynchronize(h->stream) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "pattern build failed"));
+  *out = h;
+  return NX_OK;
+}
+
+NX_API int nx_destroy(nx_network_t* h) {
+  if (h == nullptr) return NX_OK;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->chunk_exec) (void)hipGraphExecDestroy(h->chunk_exec);
+  if (h->chunk_graph) (void)hipGraphDestroy(h->chunk_graph);
+  if (h->comm) ncclCommDestroy(h->comm);
+  void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val,
+                  h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
+                  h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
+                  h->send_idx, h->send_buf};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (h->h_st) (void)hipHostFree(h->h_st);
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return NX_OK;
+}
+
+NX_API int nx_dims(nx_network_t* h, int64_t* n_rows, int64_t* n_cols, int64_t* nnz) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (n_rows) *n_rows = h->n_own;
+  if (n_cols) *n_cols = h->n_col;
+  if (nnz) *nnz = h->nnz;
+  return NX_OK;
+}
+
+NX_API int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_const, double f,
+                               const double* edge_bc) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (h->E > 0 && edge_bc == nullptr) return fail(NX_ERR_ARG, "edge_bc is NULL");
+  CHECK(set_device(h));
+  if (h->E > 0) {
+    if (edge_R) {
+      HIPCALL(hipMemcpyAsync(h->edge_R, edge_R, sizeof(double) * h->E, hipMemcpyHostToDevice,
+                             h->stream));
+    } else {
+      std::vector<double> Rc((size_t)h->E, R_const);
+      HIPCALL(hipMemcpyAsync(h->edge_R, Rc.data(), sizeof(double) * h->E, hipMemcpyHostToDevice,
+                             h->stream));
+      HIPCALL(hipStreamSynchronize(h->stream));
+    }
+    HIPCALL(hipMemcpyAsync(h->edge_bc, edge_bc, sizeof(double) * 2 * h->E, hipMemcpyHostToDevice,
+                           h->stream));
+  }
+  h->f = f;
+  h->have_coeffs = true;
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->have_coeffs) return fail(NX_ERR_STATE, "nx_set_coefficients must be called first");
+  CHECK(set_device(h));
+  if (!lhs && !rhs) return NX_OK;
+  if (h->prof) HIPCALL(hipEventRecord(h->ev[0], h->stream));
+  if (h->E > 0) {
+    AsmArgs a{EdgeArgs{h->edge_x, h->edge_lm, h->edge_seg, h->E, h->N},
+              h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs, rhs};
+    hipLaunchKernelGGL(k_assemble, dim3(grid_of(h->E, kBlock / 64)), dim3(kBlock), 0, h->stream, a);
+  }
+  const int64_t nlm = std::max(h->nnz_lm, h->B);
+  if (nlm > 0)
+    hipLaunchKernelGGL(k_assemble_lm, dim3(grid_of(nlm, 256)), dim3(256), 0, h->stream, h->nnz_lm,
+                       h->lm_val, h->val + h->nnz_edges, h->B, h->rhs + h->n_edge_dofs, lhs, rhs);
+  HIPCALL(hipGetLastError());
+  if (h->prof) {
+    HIPCALL(hipEventRecord(h->ev[1], h->stream));
+    HIPCALL(hipEventSynchronize(h->ev[1]));
+    float ms = 0.f;
+    HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    h->asm_ms += ms;
+    h->asm_cnt += 1;
+  }
+  if (lhs) h->have_lhs = true;
+  if (rhs) h->have_rhs = true;
+  return NX_OK;
+}
+
+NX_API int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
+                    int32_t* iters, double* relres, int32_t* converged) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->have_lhs || !h->have_rhs) return fail(NX_ERR_STATE, "assemble lhs and rhs before solve");
+  if (maxit < 1) return fail(NX_ERR_ARG, "maxit must be >= 1");
+  if (check_every < 2) check_every = 2;
+  if (check_every & 1) ++check_every;
+  CHECK(set_device(h));
+  hipStream_t s = h->stream;
+  const int64_t n = h->n_own;
+  // r1 = r2 = b, w1 = w2 = x = 0
+  for (int i = 0; i < 2; ++i) {
+    if (n > 0) HIPCALL(hipMemcpyAsync(h->vb[i], h->rhs, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    if (h->n_ghost > 0) HIPCALL(hipMemsetAsync(h->vb[i] + n, 0, sizeof(double) * h->n_ghost, s));
+    if (n > 0) HIPCALL(hipMemsetAsync(h->wb[i], 0, sizeof(double) * n, s));
+  }
+  HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, s));
+  const bool multi = h->comm != nullptr;
+  if (h->nblk > 0)
+    hipLaunchKernelGGL(k_dot_self, dim3(h->nblk), dim3(kBlock), 0, s, h->rhs, n, h->partials);
+  if (multi) {
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kReduceThreads), 0, s, h->partials, h->nblk,
+                       h->st, 2, 0);
+    CHECK(allreduce_slot(h, 2));
+    hipLaunchKernelGGL(k_mr_init<false>, dim3(1), dim3(kReduceThreads), 0, s, h->partials, h->nblk,
+                       h->st, rtol, maxit);
+  } else {
+    hipLaunchKernelGGL(k_mr_init<true>, dim3(1), dim3(kReduceThreads), 0, s, h->partials, h->nblk,
+                       h->st, rtol, maxit);
+  }
+  HIPCALL(hipGetLastError());
+
+  const bool use_graph = !multi && !h->prof;
+  if (use_graph) CHECK(build_chunk_graph(h, check_every));
+  // profiling: eager launches, one convergence check per iteration so that exactly
+  // the executed SpMVs are timed
+  const int chunk = h->prof ? 1 : check_every;
+  int64_t launched = 0;
+  for (;;) {
+    if (use_graph) {
+      HIPCALL(hipGraphLaunch(h->chunk_exec, s));
+    } else {
+      for (int j = 0; j < chunk; ++j) CHECK(launch_iteration(h, launched + j + 1));
+    }
+    launched += chunk;
+    HIPCALL(hipMemcpyAsync(h->h_st, h->st, sizeof(MinresState), hipMemcpyDeviceToHost, s));
+    HIPCALL(hipStreamSynchronize(s));
+    if (h->h_st->done) break;
+  }
+  // pending solution update of the last iteration k = it: r1 role at iteration k+1
+  const int64_t k = h->h_st->it;
+  if (k > 0 && n > 0) {
+    MrVecs mv{h->vb[k & 1], nullptr, h->wb[(k + 1) & 1], h->wb[k & 1], h->x};
+    hipLaunchKernelGGL(k_mr_finalize, dim3(grid_of(n, kBlock)), dim3(kBlock), 0, s, n, mv, h->st);
+    HIPCALL(hipGetLastError());
+  }
+  HIPCALL(hipStreamSynchronize(s));
+  if (iters) *iters = h->h_st->it;
+  if (relres) *relres = h->h_st->relres;
+  if (converged) *converged = h->h_st->converged;
+  return NX_OK;
+}
+
+NX_API int nx_get_solution(nx_network_t* h, double* xo) {
+  if (!h || !xo) return fail(NX_ERR_ARG, "null argument");
+  CHECK(set_device(h));
+  HIPCALL(hipMemcpyAsync(xo, h->x, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_get_rhs(nx_network_t* h, double* b) {
+  if (!h || !b) return fail(NX_ERR_ARG, "null argument");
+  CHECK(set_device(h));
+  HIPCALL(hipMemcpyAsync(b, h->rhs, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_get_csr(nx_network_t* h, int32_t* rowptr, int32_t* col, double* val) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  CHECK(set_device(h));
+  if (rowptr)
+    HIPCALL(hipMemcpyAsync(rowptr, h->rowptr, sizeof(int) * (h->n_own + 1), hipMemcpyDeviceToHost,
+                           h->stream));
+  if (col)
+    HIPCALL(hipMemcpyAsync(col, h->col, sizeof(int) * h->nnz, hipMemcpyDeviceToHost, h->stream));
+  if (val)
+    HIPCALL(hipMemcpyAsync(val, h->val, sizeof(double) * h->nnz, hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_spmv_host(nx_network_t* h, const double* xh, double* yh) {
+  if (!h || !xh || !yh) return fail(NX_ERR_ARG, "null argument");
+  if (!h->have_lhs) return fail(NX_ERR_STATE, "assemble the matrix first");
+  CHECK(set_device(h));
+  HIPCALL(hipMemcpyAsync(h->tmp, xh, sizeof(double) * h->n_col, hipMemcpyHostToDevice, h->stream));
+  // dedicated output buffer: the Krylov vectors keep their state
+  double* y = nullptr;
+  HIPCALL(hipMallocAsync((void**)&y, sizeof(double) * std::max<int64_t>(h->n_own, 1), h->stream));
+  if (h->nblk > 0)
+    hipLaunchKernelGGL(k_spmv, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->tmp, y);
+  HIPCALL(hipGetLastError());
+  HIPCALL(hipMemcpyAsync(yh, y, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipFreeAsync(y, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_true_residual(nx_network_t* h, double* relres) {
+  if (!h || !relres) return fail(NX_ERR_ARG, "null argument");
+  if (!h->have_lhs || !h->have_rhs) return fail(NX_ERR_STATE, "assemble first");
+  CHECK(set_device(h));
+  if (h->comm) CHECK(halo(h, h->x));
+  if (h->nblk > 0)
+    hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, h->nblk);
+  double* d = nullptr;
+  HIPCALL(hipMallocAsync((void**)&d, 2 * sizeof(double), h->stream));
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials, h->nblk, d);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials + h->nblk,
+                     h->nblk, d + 1);
+  HIPCALL(hipGetLastError());
+  if (h->comm) NCCLCALL(ncclAllReduce(d, d, 2, ncclDouble, ncclSum, h->comm, h->stream));
+  double hd[2];
+  HIPCALL(hipMemcpyAsync(hd, d, sizeof(hd), hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipFreeAsync(d, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  *relres = hd[1] > 0 ? std::sqrt(hd[0] / hd[1]) : std::sqrt(hd[0]);
+  return NX_OK;
+}
+
+NX_API int nx_sync(nx_network_t* h) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_set_profiling(nx_network_t* h, int32_t enable) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  h->prof = enable != 0;
+  return NX_OK;
+}
+
+NX_API int nx_get_profile(nx_network_t* h, double* spmv_ms, int64_t* spmv_count, double* asm_ms,
+                          int64_t* asm_count) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (spmv_ms) *spmv_ms = h->spmv_ms;
+  if (spmv_count) *spmv_count = h->spmv_cnt;
+  if (asm_ms) *asm_ms = h->asm_ms;
+  if (asm_count) *asm_count = h->asm_cnt;
+  return NX_OK;
+}
+
+NX_API int nx_reset_profile(nx_network_t* h) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  h->spmv_ms = h->asm_ms = 0.0;
+  h->spmv_cnt = h->asm_cnt = 0;
+  return NX_OK;
+}
+
+NX_API int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv) {
+  if (!h || !ms_per_spmv || reps < 1) return fail(NX_ERR_ARG, "bad argument");
+  if (!h->have_lhs) return fail(NX_ERR_STATE, "assemble the matrix first");
+  CHECK(set_device(h));
+  if (h->nblk == 0) {
+    *ms_per_spmv = 0.0;
+    return NX_OK;
+  }
+  // x = rhs-sized data already resident: use vb[0] as input, tmp as output
+  hipLaunchKernelGGL(k_spmv, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->vb[0], h->tmp);
+  HIPCALL(hipEventRecord(h->ev[0], h->stream));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL(k_spmv, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->vb[0],
+                       h->tmp);
+  HIPCALL(hipEventRecord(h->ev[1], h->stream));
+  HIPCALL(hipEventSynchronize(h->ev[1]));
+  HIPCALL(hipGetLastError());
+  float ms = 0.f;
+  HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+  *ms_per_spmv = ms / reps;
+  return NX_OK;
+}
+
+NX_API int nx_comm_unique_id(unsigned char* id_out) {
+  if (!id_out) return fail(NX_ERR_ARG, "null argument");
+  static_assert(sizeof(ncclUniqueId) == NX_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId id;
+  NCCLCALL(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  return NX_OK;
+}
+
+NX_API int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned char* id,
+                        int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
+                        const int32_t* send_idx, const int32_t* recv_off) {
+  if (!h || !id) return fail(NX_ERR_ARG, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(NX_ERR_ARG, "bad rank/nranks");
+  if (n_peers < 0 || (n_peers > 0 && (!peer_rank || !send_off || !recv_off)))
+    return fail(NX_ERR_ARG, "bad halo plan");
+  CHECK(set_device(h));
+  h->peers.assign(peer_rank, peer_rank + n_peers);
+  h->send_off.assign(send_off, send_off + n_peers + 1);
+  h->recv_off.assign(recv_off, recv_off + n_peers + 1);
+  if (n_peers == 0) {
+    h->send_off.assign(1, 0);
+    h->recv_off.assign(1, 0);
+  }
+  if (h->recv_off.back() != h->n_ghost)
+    return fail(NX_ERR_ARG, "halo plan receives " + std::to_string(h->recv_off.back()) +
+                                " values but the handle has " + std::to_string(h->n_ghost) +
+                                " ghost columns");
+  const int nsend = h->send_off.back();
+  for (int i = 0; i < nsend; ++i)
+    if (send_idx[i] < 0 || send_idx[i] >= h->n_own) return fail(NX_ERR_ARG, "send_idx out of range");
+  CHECK(upload(&h->send_idx, send_idx, nsend, h->stream));
+  CHECK(dalloc(&h->send_buf, nsend));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCLCALL(ncclCommInitRank(&h->comm, nranks, uid, rank));
+  h->nranks = nranks;
+  h->rank = rank;
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}

@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench. Each GPU step has its own time limit;
+# stop at the first crash/abort/timeout (exit codes other than 0/1).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name" ; date
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+step gpu_tests 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS}
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py ${BENCH_ARGS}

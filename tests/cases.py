@@ -1,0 +1,70 @@
+"""Shared test configurations (graphs + the oracle's view of them)."""
+
+from __future__ import annotations
+
+import networkx as nx
+import numpy as np
+
+from networks_fenicsx_amd import network_generation as ng
+
+
+def p_y(x):
+    return x[1]
+
+
+def p_x(x):
+    return x[0]
+
+
+def edge_info_graph() -> nx.DiGraph:
+    """The hand-built 8-node graph of the reference's tests/test_edge_info.py:8-35
+    (pass-through nodes, a 3-way split and a cycle)."""
+    G = nx.DiGraph()
+    G.add_node(0, pos=np.zeros(3))
+    G.add_node(1, pos=np.array([0.0, 0.0, 1.0]))
+    G.add_node(2, pos=np.array([0.2, 0.2, 2.0]))
+    G.add_node(3, pos=np.array([-0.2, 0.3, 2.0]))
+    G.add_node(4, pos=np.array([0.0, 0.1, 2.1]))
+    G.add_node(5, pos=np.array([0.1, -0.1, 3.0]))
+    G.add_node(6, pos=np.array([-0.3, 0.4, 4.0]))
+    G.add_node(7, pos=1.1 * G.nodes[1]["pos"])
+    for e in [(0, 1), (1, 7), (7, 2), (2, 5), (7, 3), (3, 4), (4, 5), (7, 4), (5, 6)]:
+        G.add_edge(*e)
+    return G
+
+
+def linear_graph(n: int, dim: int = 2, ordered=lambda _: True) -> nx.DiGraph:
+    """Reference tests/test_orientation.py:10-25."""
+    G = nx.DiGraph()
+    G.add_nodes_from(range(n))
+    for i in range(n - 1):
+        if ordered(i):
+            G.add_edge(i, i + 1)
+        else:
+            G.add_edge(i + 1, i)
+    for i in range(n):
+        pos = np.zeros(dim)
+        pos[0] = i / (n - 1)
+        G.nodes[i]["pos"] = pos
+    return G
+
+
+# name -> (graph factory, N, colour strategy, p_bc)
+CASES = {
+    "Y_N4": (lambda: ng.make_tree(2, 1, 3), 4, None, p_y),
+    "demo_tree_N2": (lambda: ng.make_tree(2, 1, 1), 2, None, p_y),
+    "demo_tree_N1": (lambda: ng.make_tree(2, 1, 1), 1, None, p_y),
+    "double_Y_N5": (lambda: ng.make_tree(2, 3.1, 7.3), 5, None, p_x),
+    "depth6_N40": (lambda: ng.make_tree(7, 7, 7), 40, "smallest_last", p_y),
+    "arterial5_N40": (lambda: ng.make_arterial_tree(5, direction=np.array([0.1, 1, 0])), 40,
+                      nx.coloring.strategy_largest_first, p_y),
+    "edge_info_N10": (edge_info_graph, 10, None, p_y),
+    "tree6_2d_N70": (lambda: ng.make_tree(6, 2, 1, dim=2), 70, "smallest_last", p_y),
+    "linear_alt_N3": (lambda: linear_graph(12, ordered=lambda k: k % 2), 3, None, p_x),
+}
+
+
+def graph_arrays(G):
+    pos = np.asarray([G.nodes[v]["pos"] for v in G.nodes()], dtype=np.float64)
+    edges = np.asarray(list(G.edges()), dtype=np.int64).reshape(-1, 2)
+    return pos, edges

@@ -1,0 +1,249 @@
+"""Host layout, partitioning and halo plans (CPU; the N>1 path over gloo)."""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import distributed_model as DM
+from cases import CASES
+from networks_fenicsx_amd import NetworkMesh
+from networks_fenicsx_amd import network_generation as ng
+from networks_fenicsx_amd.layout import build_local_problem, dfs_edge_order, partition_edges
+from oracle import nx_oracle as O
+
+
+def _setup(case):
+    make, N, strategy, pbc = CASES[case]
+    m = NetworkMesh(make(), N=N, color_strategy=strategy)
+    src, dst = m.edges
+    P = O.build_problem(m.node_coordinates, src, dst, N, m.edge_colors)
+    A, b = O.assemble_reference(P, pbc)
+    Ab, bb, perm, sign = O.to_build_layout(P, A, b)
+    return m, P, A, b, Ab, bb, perm
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_single_rank_layout_matches_oracle(case):
+    m, P, A, b, Ab, bb, perm = _setup(case)
+    src, dst = m.edges
+    lp = build_local_problem(m.node_coordinates, src, dst, m.degrees, m.N)
+    N, per = m.N, 2 * m.N + 1
+    ne = lp.n_edge_dofs
+    assert lp.n_own == Ab.shape[0] and lp.n_ghost == 0
+    sub = Ab[ne:]
+    np.testing.assert_array_equal(sub.indptr - sub.indptr[0], lp.lm_rowptr)
+    np.testing.assert_array_equal(sub.indices, lp.lm_col)
+    np.testing.assert_array_equal(sub.data, lp.lm_val)
+    for j in range(lp.edges.size):
+        r0, rN = Ab[j * per].indices, Ab[j * per + 2 * N].indices
+        has0, hasN = r0[-1] >= ne, rN[-1] >= ne
+        assert (lp.edge_lm[j, 0] >= 0) == has0 and (lp.edge_lm[j, 1] >= 0) == hasN
+        if has0:
+            assert r0[-1] == lp.edge_lm[j, 0]
+        if hasN:
+            assert rN[-1] == lp.edge_lm[j, 1]
+    np.testing.assert_array_equal(lp.edge_x[:, :3], np.pad(m.node_coordinates, ((0, 0), (0, 3 - m.geometric_dimension)))[src])
+
+
+def test_dfs_order_is_permutation_and_subtree_contiguous():
+    pos, src, dst = ng.tree_arrays(8, 1, 1)
+    order = dfs_edge_order(src, dst, pos.shape[0])
+    assert sorted(order.tolist()) == list(range(src.size))
+    # preorder: every edge appears after its parent edge
+    where = np.empty(src.size, dtype=np.int64)
+    where[order] = np.arange(src.size)
+    for e in range(1, src.size):
+        assert where[src[e] - 1] < where[e]
+
+
+@pytest.mark.parametrize("case,P", [("depth6_N40", 2), ("depth6_N40", 4), ("depth6_N40", 8),
+                                    ("arterial5_N40", 3), ("edge_info_N10", 2),
+                                    ("tree6_2d_N70", 4), ("linear_alt_N3", 3)])
+def test_partitioned_spmv_and_halo(case, P):
+    m, Pr, A, b, Ab, bb, perm = _setup(case)
+    src, dst = m.edges
+    bif_idx = m.bifurcation_index
+    lps = [build_local_problem(m.node_coordinates, src, dst, m.degrees, m.N, r, P)
+           for r in range(P)]
+    # every row owned exactly once
+    rows = np.concatenate([DM.global_rows(lp, m.num_edges, bif_idx) for lp in lps])
+    assert np.array_equal(np.sort(rows), np.arange(Ab.shape[0]))
+    rng = np.random.default_rng(1)
+    xg = rng.uniform(-1, 1, Ab.shape[0])
+    yg = Ab @ xg
+    xs = []
+    mats = []
+    for lp in lps:
+        Al, rws = DM.local_matrix(Ab, lp, m.num_edges, bif_idx)
+        mats.append((Al, rws))
+        v = np.zeros(lp.n_own + lp.n_ghost)
+        v[: lp.n_own] = xg[rws]
+        xs.append(v)
+    xs = DM.halo_exchange_local(lps, xs)
+    for lp, (Al, rws), v in zip(lps, mats, xs):
+        np.testing.assert_array_equal(v[lp.n_own:], xg[lp.ghost_global])
+        # the local rows see every nonzero of the global rows (no missing ghost)
+        assert Al.nnz == Ab[rws].nnz
+        np.testing.assert_allclose(Al @ v, yg[rws], rtol=1e-14, atol=1e-14)
+        # local column maps used by the device: edge_lm / lm_col point at the same
+        # global DoFs as the global matrix
+        cols_global = np.concatenate([rws, lp.ghost_global])
+        assert np.all(cols_global[lp.lm_col] >= 0)
+    if case.startswith("depth6"):
+        # subtree partition: a handful of cut bifurcations only
+        assert max(lp.n_ghost for lp in lps) <= 4 * P
+
+
+class _ThreadComm:
+    """P ranks as threads: barrier-synchronised all-reduce (fixed rank order) and halo."""
+
+    def __init__(self, lps):
+        import threading
+
+        self.lps = lps
+        self.P = len(lps)
+        self.bar = threading.Barrier(self.P)
+        self.buf = [0.0] * self.P
+        self.vecs = [None] * self.P
+
+    def allreduce(self, r, v):
+        self.buf[r] = v
+        self.bar.wait()
+        s = 0.0
+        for i in range(self.P):
+            s += self.buf[i]
+        self.bar.wait()
+        return s
+
+    def halo(self, r, v):
+        self.vecs[r] = v
+        self.bar.wait()
+        lp = self.lps[r]
+        for j, p in enumerate(lp.peers):
+            peer = self.lps[p]
+            k = list(peer.peers).index(r)
+            idx = peer.send_idx[peer.send_off[k]:peer.send_off[k + 1]]
+            v[lp.n_own + lp.recv_off[j]: lp.n_own + lp.recv_off[j + 1]] = self.vecs[p][idx]
+        self.bar.wait()
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_distributed_minres_model(P):
+    """The device MINRES schedule on P lock-stepped ranks equals the direct solve."""
+    import threading
+
+    m, Pr, A, b, Ab, bb, perm = _setup("depth6_N40")
+    src, dst = m.edges
+    bif_idx = m.bifurcation_index
+    lps = [build_local_problem(m.node_coordinates, src, dst, m.degrees, m.N, r, P)
+           for r in range(P)]
+    mats = [DM.local_matrix(Ab, lp, m.num_edges, bif_idx) for lp in lps]
+    xg_ref = O.solve_reference(A, b)[perm]
+    comm = _ThreadComm(lps)
+    results = [None] * P
+
+    def run(r):
+        Al, rows = mats[r]
+        results[r] = DM.minres(Al, bb[rows], lps[r].n_own,
+                               halo=lambda v: comm.halo(r, v),
+                               allreduce=lambda v: comm.allreduce(r, v), rtol=1e-12)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    its = {res[1] for res in results}
+    assert len(its) == 1
+    it = its.pop()
+    assert 400 < it < 800
+    x = np.zeros(Ab.shape[0])
+    for (Al, rows), res in zip(mats, results):
+        x[rows] = res[0]
+    assert np.linalg.norm(x - xg_ref) / np.linalg.norm(xg_ref) < 1e-10
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gloo_worker(rank: int, world: int, port: int, out_q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+
+        from networks_fenicsx_amd.comm import TorchComm
+
+        make, N, strategy, pbc = CASES["depth6_N40"]
+        comm = TorchComm()
+        G = make() if rank == 0 else None
+        m = NetworkMesh(G, N=N, color_strategy=strategy, comm=comm)  # graph bcast
+        src, dst = m.edges
+        lp = build_local_problem(m.node_coordinates, src, dst, m.degrees, N, rank, world)
+        Pr = O.build_problem(m.node_coordinates, src, dst, N, m.edge_colors)
+        A, b = O.assemble_reference(Pr, pbc)
+        Ab, bb, perm, _ = O.to_build_layout(Pr, A, b)
+        Al, rows = DM.local_matrix(Ab, lp, m.num_edges, m.bifurcation_index)
+
+        def halo(v):
+            reqs = []
+            bufs = []
+            for j, p in enumerate(lp.peers.tolist()):
+                snd = torch.from_numpy(
+                    v[lp.send_idx[lp.send_off[j]:lp.send_off[j + 1]]].copy())
+                rcv = torch.empty(int(lp.recv_off[j + 1] - lp.recv_off[j]), dtype=torch.float64)
+                if snd.numel():
+                    reqs.append(dist.isend(snd, p))
+                if rcv.numel():
+                    reqs.append(dist.irecv(rcv, p))
+                bufs.append((j, rcv))
+            for r in reqs:
+                r.wait()
+            for j, rcv in bufs:
+                v[lp.n_own + lp.recv_off[j]: lp.n_own + lp.recv_off[j + 1]] = rcv.numpy()
+
+        def allreduce(val):
+            t = torch.tensor([val], dtype=torch.float64)
+            dist.all_reduce(t)
+            return float(t.item())
+
+        x, it, rr = DM.minres(Al, bb[rows], lp.n_own, halo, allreduce, rtol=1e-12)
+        x_ref = O.solve_reference(A, b)[perm][rows]
+        err = float(np.linalg.norm(x - x_ref) / max(np.linalg.norm(x_ref), 1e-300))
+        out_q.put((rank, it, err, lp.n_ghost))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_minres():
+    """world_size-2 run of the multi-rank path over gloo: graph broadcast through
+    TorchComm, per-rank layout + halo plan, halo exchange with isend/irecv and dot
+    products with all_reduce, in the device's MINRES schedule."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    its = {r[1] for r in res}
+    assert len(its) == 1  # identical scalar recurrences on both ranks
+    for rank, it, err, ng_ in res:
+        assert err < 1e-10, (rank, err)
+        assert ng_ > 0

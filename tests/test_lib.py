@@ -1,0 +1,55 @@
+"""The C-ABI library: builds, loads, exports every symbol include/nxhip.h declares,
+and fails loudly (no CPU fallback) when no HIP device is visible."""
+
+import re
+from pathlib import Path
+
+import pytest
+
+from networks_fenicsx_amd import _lib
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "nxhip.h"
+
+
+def declared_symbols():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(?:int|const char\*)\s+(nx_\w+)\s*\(", text)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared_symbols():
+        assert hasattr(L, name), name
+    assert L.nx_version() >= 10000
+    assert isinstance(L.nx_last_error(), bytes)
+
+
+def test_no_silent_cpu_fallback():
+    """Without a GPU the device entry points raise; they never compute on the CPU."""
+    import numpy as np
+
+    try:
+        n = _lib.device_count()
+    except _lib.NxError:
+        n = 0
+    if n > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(_lib.NxError):
+        _lib.Handle(0, 2, np.zeros((1, 6)), -np.ones((1, 2), np.int32),
+                    np.zeros(1, np.int32), np.zeros(0, np.int32), np.zeros(0))
+
+
+def test_create_argument_errors():
+    """Argument validation happens before any device call."""
+    import numpy as np
+
+    with pytest.raises(_lib.NxError, match="N must be"):
+        _lib.Handle(0, 0, np.zeros((1, 6)), -np.ones((1, 2), np.int32),
+                    np.zeros(1, np.int32), np.zeros(0, np.int32), np.zeros(0))
+    with pytest.raises(_lib.NxError, match="edge_lm"):
+        _lib.Handle(0, 2, np.zeros((1, 6)), np.array([[0, -1]], np.int32),
+                    np.zeros(1, np.int32), np.zeros(0, np.int32), np.zeros(0))
