@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -63,17 +64,6 @@ int fail(int code, const std::string& msg) {
     int rc_ = (expr);    \
     if (rc_ != NX_OK) return rc_; \
   } while (0)
-
-// ------------------------------------------------------------------------------------
-// MINRES state, resident in device memory. Scalar recurrences follow Paige & Saunders
-// (1975) in the form of scipy.sparse.linalg.minres (unpreconditioned, shift 0).
-struct MinresState {
-  double beta1, beta, oldb, alfa, dbar, epsln, phibar, cs, sn, tnorm2;
-  double p_oldeps, p_delta, p_denom, p_phi;  // pending w/x update of iteration `it`
-  double relres, rtol;
-  double red[4];  // cross-rank reduction slots
-  int it, maxit, done, converged;
-};
 
 // ------------------------------------------------------------------------------------
 // Entry decoding of one edge's CSR segment. With s = (source is a bifurcation), the
@@ -389,160 +379,191 @@ __global__ __launch_bounds__(kBlock) void k_residual(Csr A, const double* __rest
   block_sum_store(bb, partials + nblk + blockIdx.x);
 }
 
-__global__ __launch_bounds__(kBlock) void k_dot_self(const double* __restrict__ a, int64_t n,
-                                                     double* __restrict__ partials) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const double v = i < n ? a[i] : 0.0;
-  block_sum_store(v * v, partials + blockIdx.x);
+// ------------------------------------------------------------------------------------
+// MINRES: Paige & Saunders (1975) recurrences in the form of scipy.sparse.linalg.minres
+// (unpreconditioned, shift 0). One iteration k (1-based) = 2 launches on one GPU:
+//   k_mr_a(k)  every block, redundantly: beta_k^2 = sum of k_mr_b(k-1)'s partials ->
+//              Givens rotation of iteration k-1 -> its pending solution update
+//              (w, x), fused with y = A v_k - beta_k v_{k-1} (v_k = r2/beta_k, gathered)
+//              and the block partial of alpha_k = v_k . y. Block 0 persists the state.
+//   k_mr_b(k)  every block, redundantly: alpha_k = sum of k_mr_a(k)'s partials;
+//              r2' = y - (alpha_k / beta_k) r2 and the block partial of ||r2'||^2.
+// No atomics and no reduction launches: each kernel re-reduces the previous launch's
+// few partials (nA ~ n/1024, nB = 512; L2-resident) in a fixed order, so every block
+// computes bit-identical scalars. The state is double-buffered -- k_mr_a(k) reads
+// S[(k+1)&1] and writes S[k&1] -- so block 0 can write while other blocks still read.
+// The kernel that detects convergence applies the last solution update and stops;
+// every later launch of the chunk returns at once.
+// Several ranks: partial sums go through k_reduce_slot + an RCCL all-reduce of one
+// double (red[0] = alpha, red[1] = beta^2, red[2] = ||b||^2) and the kernels read it.
+// r1/r2 swap roles every iteration and w1/w2 too; the host passes the pointers.
+constexpr int kChunksADefault = 2;   // k_mr_a: chunks of 256 rows per block (swept: 1,2,4)
+constexpr int kBlocksBDefault = 512;  // k_mr_b / start: grid-stride vector kernels
+constexpr int kMaxBlocksB = 4096;
+
+struct MrState {
+  double beta1, beta, oldb, alfa, dbar, epsln, phibar, cs, sn, tnorm2, relres, rtol;
+  int nb;  // completed Lanczos steps (k_mr_b launches that ran)
+  int it;  // completed MINRES iterations (rotations applied)
+  int maxit, done, converged, pad;
+};
+
+struct Rot {
+  double oldeps, delta, denom, phi;
+};
+
+// Rotation of iteration it+1 from b2 = beta_{it+2}^2 (scipy minres.py statement order).
+__device__ __forceinline__ Rot mr_rotate(MrState& s, double b2) {
+  const double alfa = s.alfa, oldb = s.beta, beta = sqrt(b2);
+  s.oldb = oldb;
+  s.beta = beta;
+  s.tnorm2 += alfa * alfa + oldb * oldb + beta * beta;
+  Rot r;
+  r.oldeps = s.epsln;
+  r.delta = s.cs * s.dbar + s.sn * alfa;
+  const double gbar = s.sn * s.dbar - s.cs * alfa;
+  s.epsln = s.sn * beta;
+  s.dbar = -s.cs * beta;
+  const double gamma = fmax(hypot(gbar, beta), 2.220446049250313e-16);
+  s.cs = gbar / gamma;
+  s.sn = beta / gamma;
+  r.phi = s.cs * s.phibar;
+  s.phibar = s.sn * s.phibar;
+  r.denom = 1.0 / gamma;
+  s.it += 1;
+  s.relres = s.phibar / s.beta1;
+  if (s.relres <= s.rtol || beta == 0.0) {
+    s.done = 1;
+    s.converged = 1;
+  } else if (s.it >= s.maxit || !(s.relres == s.relres)) {
+    s.done = 1;
+  }
+  return r;
 }
 
-// ------------------------------------------------------------------------------------
-// MINRES kernels. One iteration k (1-based) = 4 launches:
-//   k_mr_spmv      y = A v_k - beta_k v_{k-1}  (v_k = r2/beta_k gathered), partial alpha;
-//                  plus the pending solution update of iteration k-1 (fused: it reads
-//                  r1 = beta_{k-1} v_{k-1} anyway)
-//   k_mr_alpha     alpha_k = sum of partials
-//   k_mr_lanczos   r2' = y - (alpha_k / beta_k) r2, partial ||r2'||^2
-//   k_mr_rotate    beta_{k+1}, Givens rotation, convergence test
-// r1/r2 swap roles every iteration and w1/w2 too; the host passes the pointers.
+// Sum of n values in a fixed order, identical in every block; returned to all threads.
+__device__ __forceinline__ double block_allsum(const double* __restrict__ p, int n) {
+  __shared__ double s_w[kBlock / 64];
+  __shared__ double s_tot;
+  double v = 0.0;
+  for (int i = threadIdx.x; i < n; i += kBlock) v += p[i];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = s_w[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; ++i) t += s_w[i];
+    s_tot = t;
+  }
+  __syncthreads();
+  return s_tot;
+}
+
 struct MrVecs {
   double* r1;        // in: beta_{k-1} v_{k-1} (b at k = 1); out: y
   const double* r2;  // beta_k v_k, gathered (has ghost slots)
-  double* w1;        // w_{k-2} in, w_{k-1} out (in place)
-  const double* w2;  // w_{k-1}... see k_mr_spmv
+  double* w1;        // w_{k-3} in, w_{k-1} out (in place)
+  const double* w2;  // w_{k-2}
   double* x;
 };
 
-__global__ __launch_bounds__(kBlock) void k_mr_spmv(Csr A, MrVecs v, MinresState* __restrict__ st,
-                                                    double* __restrict__ partials) {
-  if (st->done) return;
-  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
-  const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
-  const double Ay = spmv_row_sum(A, v.r2, r0, nr);
-  const int it = st->it;  // completed iterations = k - 1
-  const double beta = st->beta, oldb = st->oldb;
-  const double s = 1.0 / beta;
-  const double c1 = it > 0 ? beta / oldb : 0.0;
+template <bool MULTI>
+__global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState* __restrict__ sin,
+                                                 MrState* __restrict__ sout,
+                                                 const double* __restrict__ partB, int nB,
+                                                 const double* __restrict__ red,
+                                                 double* __restrict__ partA, int chunksA) {
+  if (sin->done) return;
+  MrState s = *sin;
+  Rot rot{0.0, 0.0, 0.0, 0.0};
+  const bool upd = s.nb > 0;  // a Lanczos step is waiting for its rotation
+  if (upd) rot = mr_rotate(s, MULTI ? red[1] : block_allsum(partB, nB));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *sout = s;
+  const double beta = s.beta, oldb = s.oldb;  // beta_k, beta_{k-1}
+  const double sc = 1.0 / beta;
+  const double c1 = upd ? beta / oldb : 0.0;
+  const bool spmv = !s.done;
   double part = 0.0;
-  if ((int)threadIdx.x < nr) {
-    const int64_t r = r0 + threadIdx.x;
-    const double r1v = v.r1[r];
-    const double y = s * Ay - c1 * r1v;
-    part = (s * v.r2[r]) * y;
-    v.r1[r] = y;
-    if (it > 0) {  // pending update of iteration k-1: w = (v - oldeps w1 - delta w2)/gamma
-      const double vk = r1v / oldb;
-      const double wn = (vk - st->p_oldeps * v.w1[r] - st->p_delta * v.w2[r]) * st->p_denom;
-      v.w1[r] = wn;
-      v.x[r] += st->p_phi * wn;
+  for (int c = 0; c < chunksA; ++c) {
+    const int64_t r0 = ((int64_t)blockIdx.x * chunksA + c) * kRowsPerBlock;
+    if (r0 >= A.n_rows) break;
+    const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
+    const double Ay = spmv ? spmv_row_sum(A, v.r2, r0, nr) : 0.0;
+    if ((int)threadIdx.x < nr) {
+      const int64_t r = r0 + threadIdx.x;
+      const double r1v = v.r1[r];
+      if (upd) {  // w = (v - oldeps w1 - delta w2) / gamma ; x += phi w
+        const double vk = r1v / oldb;
+        const double wn = (vk - rot.oldeps * v.w1[r] - rot.delta * v.w2[r]) * rot.denom;
+        v.w1[r] = wn;
+        v.x[r] += rot.phi * wn;
+      }
+      if (spmv) {
+        const double y = sc * Ay - c1 * r1v;
+        part += (sc * v.r2[r]) * y;
+        v.r1[r] = y;
+      }
     }
+    __syncthreads();  // LDS of spmv_row_sum is reused by the next chunk
   }
-  block_sum_store(part, partials + blockIdx.x);
+  if (spmv) block_sum_store(part, partA + blockIdx.x);
 }
 
-// Solution update of the last iteration (after convergence / maxit).
-__global__ __launch_bounds__(kBlock) void k_mr_finalize(int64_t n, MrVecs v,
-                                                        const MinresState* __restrict__ st) {
-  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (st->it == 0 || r >= n) return;
-  const double vk = v.r1[r] / st->oldb;
-  const double wn = (vk - st->p_oldeps * v.w1[r] - st->p_delta * v.w2[r]) * st->p_denom;
-  v.w1[r] = wn;
-  v.x[r] += st->p_phi * wn;
-}
-
-__global__ __launch_bounds__(kBlock) void k_mr_lanczos(int64_t n, double* __restrict__ y,
-                                                       const double* __restrict__ r2,
-                                                       const MinresState* __restrict__ st,
-                                                       double* __restrict__ partials) {
-  if (st->done) return;
-  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const double c2 = st->alfa / st->beta;
+template <bool MULTI>
+__global__ __launch_bounds__(kBlock) void k_mr_b(int64_t n, double* __restrict__ y,
+                                                 const double* __restrict__ r2,
+                                                 MrState* __restrict__ st,
+                                                 MrState* __restrict__ other,
+                                                 const double* __restrict__ partA, int nA,
+                                                 const double* __restrict__ red,
+                                                 double* __restrict__ partB) {
+  if (st->done) {
+    // k_mr_a of this iteration stopped the solve: make the other buffer final too, or
+    // the k_mr_a two launches later would resume from its stale (not done) copy
+    if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;
+    return;
+  }
+  const double beta = st->beta;
+  const double alfa = MULTI ? red[0] : block_allsum(partA, nA);
+  const double c2 = alfa / beta;
   double part = 0.0;
-  if (r < n) {
-    const double v = y[r] - c2 * r2[r];
-    y[r] = v;
-    part = v * v;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const double v = y[i] - c2 * r2[i];
+    y[i] = v;
+    part += v * v;
   }
-  block_sum_store(part, partials + blockIdx.x);
-}
-
-__device__ void mr_rotate_scalar(MinresState* st, double b2) {
-  const double alfa = st->alfa;
-  const double oldb = st->beta;
-  const double beta = sqrt(b2);
-  st->oldb = oldb;
-  st->beta = beta;
-  st->tnorm2 += alfa * alfa + oldb * oldb + beta * beta;
-  const double oldeps = st->epsln;
-  const double delta = st->cs * st->dbar + st->sn * alfa;
-  const double gbar = st->sn * st->dbar - st->cs * alfa;
-  st->epsln = st->sn * beta;
-  st->dbar = -st->cs * beta;
-  double gamma = hypot(gbar, beta);
-  gamma = fmax(gamma, 2.220446049250313e-16);
-  st->cs = gbar / gamma;
-  st->sn = beta / gamma;
-  const double phi = st->cs * st->phibar;
-  st->phibar = st->sn * st->phibar;
-  st->p_oldeps = oldeps;
-  st->p_delta = delta;
-  st->p_denom = 1.0 / gamma;
-  st->p_phi = phi;
-  st->it += 1;
-  st->relres = st->phibar / st->beta1;
-  if (st->relres <= st->rtol || beta == 0.0) {
-    st->done = 1;
-    st->converged = 1;
-  } else if (st->it >= st->maxit || !(st->relres == st->relres)) {
-    st->done = 1;
+  block_sum_store(part, partB + blockIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // fields no other block reads here
+    st->alfa = alfa;
+    st->nb += 1;
   }
 }
 
-// FROM_PARTIALS: single rank (sum partials here); else read the all-reduced slot.
-template <bool FROM_PARTIALS>
-__global__ __launch_bounds__(kReduceThreads) void k_mr_alpha(const double* __restrict__ partials,
-                                                             int n, MinresState* __restrict__ st) {
-  if (st->done) return;
-  double t = 0.0;
-  if (FROM_PARTIALS) t = reduce_partials(partials, n);
-  if (threadIdx.x == 0) st->alfa = FROM_PARTIALS ? t : st->red[0];
+// ||b||^2 partials for the start
+__global__ __launch_bounds__(kBlock) void k_sumsq(const double* __restrict__ b, int64_t n,
+                                                  double* __restrict__ part) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    acc += b[i] * b[i];
+  block_sum_store(acc, part + blockIdx.x);
 }
 
-template <bool FROM_PARTIALS>
-__global__ __launch_bounds__(kReduceThreads) void k_mr_rotate(const double* __restrict__ partials,
-                                                              int n, MinresState* __restrict__ st) {
-  if (st->done) return;
-  double t = 0.0;
-  if (FROM_PARTIALS) t = reduce_partials(partials, n);
-  if (threadIdx.x == 0) mr_rotate_scalar(st, FROM_PARTIALS ? t : st->red[1]);
-}
-
-// Reduce partials into a state slot (multi-rank: the slot is then all-reduced).
-__global__ __launch_bounds__(kReduceThreads) void k_reduce_slot(const double* __restrict__ partials,
-                                                                int n, MinresState* __restrict__ st,
-                                                                int slot, int check_done) {
-  if (check_done && st->done) return;
-  const double t = reduce_partials(partials, n);
-  if (threadIdx.x == 0) st->red[slot] = t;
-}
-
-template <bool FROM_PARTIALS>
-__global__ __launch_bounds__(kReduceThreads) void k_mr_init(const double* __restrict__ partials,
-                                                            int n, MinresState* __restrict__ st,
-                                                            double rtol, int maxit) {
-  double t = 0.0;
-  if (FROM_PARTIALS) t = reduce_partials(partials, n);
+template <bool MULTI>
+__global__ __launch_bounds__(kBlock) void k_mr_init(const double* __restrict__ part, int np,
+                                                    const double* __restrict__ red,
+                                                    MrState* __restrict__ st, double rtol,
+                                                    int maxit) {
+  const double bb = MULTI ? red[2] : block_allsum(part, np);
   if (threadIdx.x == 0) {
-    const double bb = FROM_PARTIALS ? t : st->red[2];
     const double beta1 = sqrt(bb);
-    MinresState s{};
+    MrState s{};
     s.beta1 = beta1;
     s.beta = beta1;
-    s.oldb = 0.0;
     s.phibar = beta1;
     s.cs = -1.0;
-    s.sn = 0.0;
     s.rtol = rtol;
     s.maxit = maxit;
     s.relres = beta1 > 0.0 ? 1.0 : 0.0;
@@ -552,6 +573,13 @@ __global__ __launch_bounds__(kReduceThreads) void k_mr_init(const double* __rest
     }
     *st = s;
   }
+}
+
+// Reduce partials into red[slot] (multi-rank: then all-reduced).
+__global__ __launch_bounds__(kBlock) void k_reduce_slot(const double* __restrict__ part, int n,
+                                                        double* __restrict__ red, int slot) {
+  const double t = block_allsum(part, n);
+  if (threadIdx.x == 0) red[slot] = t;
 }
 
 __global__ void k_pack(const double* __restrict__ x, const int* __restrict__ idx, int n,
@@ -592,9 +620,15 @@ struct nx_network {
   double* wb[2] = {nullptr, nullptr};  // w1/w2, n_own each
   double* x = nullptr;                 // n_col
   double* tmp = nullptr;               // n_col (host SpMV / residual)
-  double* partials = nullptr;          // 2 * nblk
-  MinresState* st = nullptr;
-  MinresState* h_st = nullptr;  // pinned host mirror
+  double* partials = nullptr;          // nblk (residual) >= nA + nB
+  int nA = 1;                          // k_mr_a blocks (partials of alpha)
+  int chunksA = kChunksADefault;       // 256-row chunks per k_mr_a block
+  int nB = kBlocksBDefault;            // k_mr_b blocks (partials of beta^2)
+  double* partA = nullptr;             // nA
+  double* partB = nullptr;             // nB
+  double* red = nullptr;               // 4 cross-rank reduction slots
+  MrState* st = nullptr;               // 2 buffers (ping-pong)
+  MrState* h_st = nullptr;             // pinned host mirror of both
   // graph chunk
   hipGraphExec_t chunk_exec = nullptr;
   hipGraph_t chunk_graph = nullptr;
@@ -604,6 +638,8 @@ struct nx_network {
   double spmv_ms = 0.0, asm_ms = 0.0;
   int64_t spmv_cnt = 0, asm_cnt = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev_pool;  // SpMV timing pairs inside one convergence chunk
+  int prof_k = 0;
   // multi-rank
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -656,7 +692,7 @@ int halo(nx_network* h, double* v) {
 }
 
 int allreduce_slot(nx_network* h, int slot) {
-  NCCLCALL(ncclAllReduce(&h->st->red[slot], &h->st->red[slot], 1, ncclDouble, ncclSum, h->comm,
+  NCCLCALL(ncclAllReduce(h->red + slot, h->red + slot, 1, ncclDouble, ncclSum, h->comm,
                          h->stream));
   return NX_OK;
 }
@@ -665,47 +701,36 @@ int allreduce_slot(nx_network* h, int slot) {
 int launch_iteration(nx_network* h, int64_t k) {
   double* r1 = h->vb[(k - 1) & 1];
   double* r2 = h->vb[k & 1];
-  // pending update belongs to iteration k-1: w1 = wb[(k-2)&1], w2 = wb[(k-1)&1]
+  // pending update of iteration k-1: w1 = w_{k-3} (overwritten by w_{k-1}), w2 = w_{k-2}
   double* w1 = h->wb[k & 1];
   double* w2 = h->wb[(k - 1) & 1];
+  MrState* sin = h->st + ((k + 1) & 1);
+  MrState* sout = h->st + (k & 1);
   const bool multi = h->comm != nullptr;
   if (multi) CHECK(halo(h, r2));
   MrVecs mv{r1, r2, w1, w2, h->x};
-  if (h->nblk > 0) {
-    if (h->prof) HIPCALL(hipEventRecord(h->ev[0], h->stream));
-    hipLaunchKernelGGL(k_mr_spmv, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), mv, h->st,
-                       h->partials);
-    if (h->prof) {
-      HIPCALL(hipEventRecord(h->ev[1], h->stream));
-      HIPCALL(hipEventSynchronize(h->ev[1]));
-      float ms = 0.f;
-      HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-      h->spmv_ms += ms;
-      h->spmv_cnt += 1;
-    }
+  if (h->prof) HIPCALL(hipEventRecord(h->ev_pool[2 * h->prof_k], h->stream));
+  if (multi)
+    hipLaunchKernelGGL(k_mr_a<true>, dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv, sin,
+                       sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
+  else
+    hipLaunchKernelGGL(k_mr_a<false>, dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv, sin,
+                       sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
+  if (h->prof) {
+    HIPCALL(hipEventRecord(h->ev_pool[2 * h->prof_k + 1], h->stream));
+    h->prof_k += 1;
   }
   if (multi) {
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                       h->nblk, h->st, 0, 1);
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partA, h->nA, h->red, 0);
     CHECK(allreduce_slot(h, 0));
-    hipLaunchKernelGGL(k_mr_alpha<false>, dim3(1), dim3(kReduceThreads), 0, h->stream,
-                       h->partials, h->nblk, h->st);
-  } else {
-    hipLaunchKernelGGL(k_mr_alpha<true>, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                       h->nblk, h->st);
-  }
-  if (h->nblk > 0)
-    hipLaunchKernelGGL(k_mr_lanczos, dim3(h->nblk), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
-                       h->st, h->partials);
-  if (multi) {
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                       h->nblk, h->st, 1, 1);
+    hipLaunchKernelGGL(k_mr_b<true>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
+                       sout, sin, h->partA, h->nA, h->red, h->partB);
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partB, h->nB,
+                       h->red, 1);
     CHECK(allreduce_slot(h, 1));
-    hipLaunchKernelGGL(k_mr_rotate<false>, dim3(1), dim3(kReduceThreads), 0, h->stream,
-                       h->partials, h->nblk, h->st);
   } else {
-    hipLaunchKernelGGL(k_mr_rotate<true>, dim3(1), dim3(kReduceThreads), 0, h->stream,
-                       h->partials, h->nblk, h->st);
+    hipLaunchKernelGGL(k_mr_b<false>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
+                       sout, sin, h->partA, h->nA, h->red, h->partB);
   }
   HIPCALL(hipGetLastError());
   return NX_OK;
@@ -809,7 +834,7 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   h->nnz_edges = acc;
   h->nnz_lm = nnz_lm;
   h->nnz = acc + nnz_lm;
-  h->nblk = grid_of(n_own, kRowsPerBlock);
+  h->nblk = std::max(1, grid_of(n_own, kRowsPerBlock));  // >= 1: every rank joins the reductions
   auto bail = [&](int rc) {
     nx_destroy(h);
     return rc;
@@ -833,14 +858,21 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   }
   if ((rc = dalloc(&h->x, n_col))) return bail(rc);
   if ((rc = dalloc(&h->tmp, n_col))) return bail(rc);
-  if ((rc = dalloc(&h->partials, 2 * (int64_t)std::max(h->nblk, 1)))) return bail(rc);
-  if (hipMalloc((void**)&h->st, sizeof(MinresState)) != hipSuccess)
+  if (const char* e = std::getenv("NXHIP_A_CHUNKS")) h->chunksA = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("NXHIP_B_BLOCKS"))
+    h->nB = std::min(kMaxBlocksB, std::max(1, std::atoi(e)));
+  h->nA = std::max(1, grid_of(n_own, kRowsPerBlock * h->chunksA));
+  if ((rc = dalloc(&h->partials, 2 * (int64_t)h->nblk))) return bail(rc);
+  if ((rc = dalloc(&h->partA, h->nA))) return bail(rc);
+  if ((rc = dalloc(&h->partB, h->nB))) return bail(rc);
+  if ((rc = dalloc(&h->red, 4))) return bail(rc);
+  if (hipMalloc((void**)&h->st, 2 * sizeof(MrState)) != hipSuccess)
     return bail(fail(NX_ERR_HIP, "hipMalloc state failed"));
-  if (hipHostMalloc((void**)&h->h_st, sizeof(MinresState), hipHostMallocDefault) != hipSuccess)
+  if (hipHostMalloc((void**)&h->h_st, 2 * sizeof(MrState), hipHostMallocDefault) != hipSuccess)
     return bail(fail(NX_ERR_HIP, "hipHostMalloc failed"));
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return bail(fail(NX_ERR_HIP, "hipEventCreate failed"));
-  if (hipMemsetAsync(h->st, 0, sizeof(MinresState), h->stream) != hipSuccess)
+  if (hipMemsetAsync(h->st, 0, 2 * sizeof(MrState), h->stream) != hipSuccess)
     return bail(fail(NX_ERR_HIP, "memset state failed"));
 
   // pattern: edge segments on the device; multiplier rows from the host lists
@@ -874,11 +906,14 @@ NX_API int nx_destroy(nx_network_t* h) {
   void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val,
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
                   h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
+                  h->partA,  h->partB,   h->red,
                   h->send_idx, h->send_buf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (h->h_st) (void)hipHostFree(h->h_st);
   for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : h->ev_pool)
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -964,51 +999,63 @@ NX_API int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_e
   }
   HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, s));
   const bool multi = h->comm != nullptr;
-  if (h->nblk > 0)
-    hipLaunchKernelGGL(k_dot_self, dim3(h->nblk), dim3(kBlock), 0, s, h->rhs, n, h->partials);
+  hipLaunchKernelGGL(k_sumsq, dim3(h->nB), dim3(kBlock), 0, s, h->rhs, n, h->partB);
   if (multi) {
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kReduceThreads), 0, s, h->partials, h->nblk,
-                       h->st, 2, 0);
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, s, h->partB, h->nB, h->red, 2);
     CHECK(allreduce_slot(h, 2));
-    hipLaunchKernelGGL(k_mr_init<false>, dim3(1), dim3(kReduceThreads), 0, s, h->partials, h->nblk,
-                       h->st, rtol, maxit);
-  } else {
-    hipLaunchKernelGGL(k_mr_init<true>, dim3(1), dim3(kReduceThreads), 0, s, h->partials, h->nblk,
-                       h->st, rtol, maxit);
+  }
+  for (int b = 0; b < 2; ++b) {  // both state buffers start identical
+    if (multi)
+      hipLaunchKernelGGL(k_mr_init<true>, dim3(1), dim3(kBlock), 0, s, h->partB, h->nB, h->red,
+                         h->st + b, rtol, maxit);
+    else
+      hipLaunchKernelGGL(k_mr_init<false>, dim3(1), dim3(kBlock), 0, s, h->partB, h->nB, h->red,
+                         h->st + b, rtol, maxit);
   }
   HIPCALL(hipGetLastError());
 
+  // Profiling: eager launches with an event pair around every k_mr_a of a chunk; after
+  // the chunk's convergence check only the launches that ran a Lanczos step are added.
   const bool use_graph = !multi && !h->prof;
   if (use_graph) CHECK(build_chunk_graph(h, check_every));
-  // profiling: eager launches, one convergence check per iteration so that exactly
-  // the executed SpMVs are timed
-  const int chunk = h->prof ? 1 : check_every;
+  if (h->prof && (int)h->ev_pool.size() < 2 * check_every) {
+    for (auto& e : h->ev_pool) (void)hipEventDestroy(e);
+    h->ev_pool.assign(2 * check_every, nullptr);
+    for (auto& e : h->ev_pool) HIPCALL(hipEventCreate(&e));
+  }
   int64_t launched = 0;
+  int nb_before = 0;
+  const MrState* last = nullptr;
   for (;;) {
     if (use_graph) {
       HIPCALL(hipGraphLaunch(h->chunk_exec, s));
     } else {
-      for (int j = 0; j < chunk; ++j) CHECK(launch_iteration(h, launched + j + 1));
+      h->prof_k = 0;
+      for (int j = 0; j < check_every; ++j) CHECK(launch_iteration(h, launched + j + 1));
     }
-    launched += chunk;
-    HIPCALL(hipMemcpyAsync(h->h_st, h->st, sizeof(MinresState), hipMemcpyDeviceToHost, s));
+    launched += check_every;
+    HIPCALL(hipMemcpyAsync(h->h_st, h->st, 2 * sizeof(MrState), hipMemcpyDeviceToHost, s));
     HIPCALL(hipStreamSynchronize(s));
-    if (h->h_st->done) break;
+    // the chunk ends with k even -> S[0] is the latest; once the solve stopped, k_mr_b
+    // has made both buffers identical
+    last = &h->h_st[0];
+    if (h->prof) {
+      const int ran = last->nb - nb_before;
+      for (int j = 0; j < ran && j < h->prof_k; ++j) {
+        float ms = 0.f;
+        HIPCALL(hipEventElapsedTime(&ms, h->ev_pool[2 * j], h->ev_pool[2 * j + 1]));
+        h->spmv_ms += ms;
+        h->spmv_cnt += 1;
+      }
+      nb_before = last->nb;
+    }
+    if (last->done) break;
   }
-  // pending solution update of the last iteration k = it: r1 role at iteration k+1
-  const int64_t k = h->h_st->it;
-  if (k > 0 && n > 0) {
-    MrVecs mv{h->vb[k & 1], nullptr, h->wb[(k + 1) & 1], h->wb[k & 1], h->x};
-    hipLaunchKernelGGL(k_mr_finalize, dim3(grid_of(n, kBlock)), dim3(kBlock), 0, s, n, mv, h->st);
-    HIPCALL(hipGetLastError());
-  }
-  HIPCALL(hipStreamSynchronize(s));
-  if (iters) *iters = h->h_st->it;
-  if (relres) *relres = h->h_st->relres;
-  if (converged) *converged = h->h_st->converged;
+  if (iters) *iters = last->it;
+  if (relres) *relres = last->relres;
+  if (converged) *converged = last->converged;
   return NX_OK;
 }
-
 NX_API int nx_get_solution(nx_network_t* h, double* xo) {
   if (!h || !xo) return fail(NX_ERR_ARG, "null argument");
   CHECK(set_device(h));

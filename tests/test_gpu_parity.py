@@ -217,3 +217,23 @@ def test_profiling_counters():
     assert conv and prof["spmv_count"] == it
     assert prof["spmv_ms"] > 0 and prof["asm_count"] == 1
     assert h.bench_spmv(5) > 0
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "depth6_N40"])
+def test_convergence_chunk_invariance(case):
+    """Iterations run in graph chunks; after convergence every later launch of a chunk
+    must be a no-op. Results must not depend on the chunk length or on graph vs eager
+    launches (regression: a stale double-buffered state used to resume iterating)."""
+    mesh, asm, P, A, b, _ = _build(case)
+    asm.assemble()
+    h = asm.handle
+    ref = None
+    for eager, chunk in ((False, 2), (False, 8), (False, 32), (False, 1000), (True, 32)):
+        h.set_profiling(eager)
+        it, rr, conv = h.solve(1e-12, 5000, chunk)
+        x = h.solution()
+        if ref is None:
+            ref = (it, x)
+        assert conv and it == ref[0]
+        np.testing.assert_array_equal(x, ref[1])
+    h.set_profiling(False)
