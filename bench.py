@@ -55,6 +55,19 @@ def mr_spmv_bytes(n_rows: int, nnz: int) -> int:
     return 12 * nnz + 4 * (n_rows + 1) + 8 * n_rows + 56 * n_rows
 
 
+def pmc_traffic(kernel_prefix: str):
+    """Per-launch HBM bytes of a kernel from the newest committed PMC summary
+    (profiles/<tag>_summary.json, written by scripts/summarize_profile.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same workload)."""
+    cands = sorted((REPO / "profiles").glob("*_summary.json"), key=lambda p: p.stat().st_mtime)
+    for path in reversed(cands):
+        doc = json.loads(path.read_text())
+        for name, d in doc.get("kernels", {}).items():
+            if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in d:
+                return d["hbm_bytes_per_launch"], f"profiles/{path.name}", d.get("avg_ns")
+    return None, None, None
+
+
 def cpu_baseline(mesh, budget_s: float):
     """CPU restatement of the reference path on the host: oracle assembly + SuperLU
     direct solve (the MUMPS stand-in), repeated up to ``budget_s`` seconds."""
@@ -157,6 +170,7 @@ def main() -> int:
     nbytes = mr_spmv_bytes(h.n_rows, h.nnz)
     achieved = nbytes / (spmv_ms * 1e-3) / 1e9
     sbytes = spmv_bytes(h.n_rows, h.nnz)
+    traffic, traffic_src, rocprof_ns = pmc_traffic("k_mr_a<false>") if world == 1 else (None, None, None)
 
     # --- parity outside the timed region
     true_rr = h.true_residual()
@@ -201,12 +215,15 @@ def main() -> int:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_mr_spmv (fused CSR SpMV + Lanczos/solution update)",
+                "kernel": "k_mr_a (CSR SpMV fused with the Lanczos step, Givens rotation and solution update)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+                "traffic_source": traffic_src,
+                "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
                 "algorithmic_bytes_per_launch": nbytes,
                 "avg_launch_ms": spmv_ms,
                 "spmv_algorithmic_bytes": sbytes,

@@ -15,6 +15,7 @@
 //
 // Pressure rows are negated (and their rhs) so A is symmetric; MINRES needs that.
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -709,17 +710,17 @@ int launch_iteration(nx_network* h, int64_t k) {
   const bool multi = h->comm != nullptr;
   if (multi) CHECK(halo(h, r2));
   MrVecs mv{r1, r2, w1, w2, h->x};
-  if (h->prof) HIPCALL(hipEventRecord(h->ev_pool[2 * h->prof_k], h->stream));
+  // profiling: events bound to the kernel's own dispatch packet (hipExtLaunchKernel), so
+  // the measured interval is the kernel's execution like rocprofv3's, not marker latency
+  hipEvent_t e0 = h->prof ? h->ev_pool[2 * h->prof_k] : nullptr;
+  hipEvent_t e1 = h->prof ? h->ev_pool[2 * h->prof_k + 1] : nullptr;
   if (multi)
-    hipLaunchKernelGGL(k_mr_a<true>, dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv, sin,
-                       sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
+    hipExtLaunchKernelGGL(k_mr_a<true>, dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,
+                          csr_of(h), mv, sin, sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
   else
-    hipLaunchKernelGGL(k_mr_a<false>, dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv, sin,
-                       sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
-  if (h->prof) {
-    HIPCALL(hipEventRecord(h->ev_pool[2 * h->prof_k + 1], h->stream));
-    h->prof_k += 1;
-  }
+    hipExtLaunchKernelGGL(k_mr_a<false>, dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,
+                          csr_of(h), mv, sin, sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
+  if (h->prof) h->prof_k += 1;
   if (multi) {
     hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partA, h->nA, h->red, 0);
     CHECK(allreduce_slot(h, 0));
@@ -957,19 +958,18 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   if (!h->have_coeffs) return fail(NX_ERR_STATE, "nx_set_coefficients must be called first");
   CHECK(set_device(h));
   if (!lhs && !rhs) return NX_OK;
-  if (h->prof) HIPCALL(hipEventRecord(h->ev[0], h->stream));
   if (h->E > 0) {
     AsmArgs a{EdgeArgs{h->edge_x, h->edge_lm, h->edge_seg, h->E, h->N},
               h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs, rhs};
-    hipLaunchKernelGGL(k_assemble, dim3(grid_of(h->E, kBlock / 64)), dim3(kBlock), 0, h->stream, a);
+    hipExtLaunchKernelGGL(k_assemble, dim3(grid_of(h->E, kBlock / 64)), dim3(kBlock), 0, h->stream,
+                          h->prof ? h->ev[0] : nullptr, h->prof ? h->ev[1] : nullptr, 0, a);
   }
   const int64_t nlm = std::max(h->nnz_lm, h->B);
   if (nlm > 0)
     hipLaunchKernelGGL(k_assemble_lm, dim3(grid_of(nlm, 256)), dim3(256), 0, h->stream, h->nnz_lm,
                        h->lm_val, h->val + h->nnz_edges, h->B, h->rhs + h->n_edge_dofs, lhs, rhs);
   HIPCALL(hipGetLastError());
-  if (h->prof) {
-    HIPCALL(hipEventRecord(h->ev[1], h->stream));
+  if (h->prof && h->E > 0) {
     HIPCALL(hipEventSynchronize(h->ev[1]));
     float ms = 0.f;
     HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
