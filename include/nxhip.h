@@ -115,6 +115,27 @@ int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs);
 int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
              int32_t* iters, double* relres, int32_t* converged);
 
+/*
+ * Tree Schur-complement preconditioner for MINRES, P = blockdiag(D, G^T D^{-1} G) with D the
+ * lumped flux mass (networks_fenicsx_amd/precond.py derives it and builds these arrays).
+ * There is no reference counterpart: the reference factorises with MUMPS
+ * (solver.py:456-463); this makes the iterative replacement converge in O(10) iterations.
+ * enable = 0 switches back to unpreconditioned MINRES. Chains (one per local edge, in job
+ * order): edge slot, flip (chain runs target -> source), top / bottom junction slot (-1 =
+ * ground). Junction slots (one per owned multiplier, level order per job): multiplier row,
+ * chain to the parent, parent slot, CSR of chains hanging below. Jobs (one workgroup each):
+ * chain ranges and level ranges; lvl_slot_off / top_lvl_off: slot offsets per level (root
+ * level first) of the lower jobs / of the single top workgroup. Requires N <= 256.
+ */
+int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
+                          const int32_t* chain_edge, const int32_t* chain_flip,
+                          const int32_t* chain_up, const int32_t* chain_lo, int64_t n_slots,
+                          const int32_t* slot_lam, const int32_t* slot_pchain,
+                          const int32_t* slot_parent, const int32_t* slot_dc_off,
+                          const int32_t* slot_dc, int32_t n_jobs, const int32_t* job_chain_off,
+                          const int32_t* job_lvl_off, int32_t n_lvl, const int32_t* lvl_slot_off,
+                          int32_t n_top_lvl, const int32_t* top_lvl_off);
+
 /* Copy the owned part of the solution / rhs to the host (n_rows doubles). */
 int nx_get_solution(nx_network_t* h, double* x);
 int nx_get_rhs(nx_network_t* h, double* b);

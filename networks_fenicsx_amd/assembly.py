@@ -35,6 +35,7 @@ from . import _lib
 from .fem import Constant, FunctionSpace
 from .layout import LocalProblem, build_local_problem
 from .mesh import NetworkMesh
+from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
 
 __all__ = ["HydraulicNetworkAssembler", "DeviceMatrix", "DeviceVector", "evaluate_nodal"]
@@ -163,6 +164,11 @@ class HydraulicNetworkAssembler:
                                    lp.lm_rowptr, lp.lm_col, lp.lm_val, lp.n_ghost)
         if self._nranks > 1:
             self._init_comm()
+        # MINRES preconditioner (tree Schur complement); topology-only, built once
+        self._pc: TreePreconditioner | None = None
+        if mesh.N <= 256:
+            self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees)
+        self.set_preconditioner(True)
         self._a = None
         self._L = None
         self._make_spaces()
@@ -199,6 +205,17 @@ class HydraulicNetworkAssembler:
         self._p_idx = (np.arange(lp.edges.size)[:, None] * per
                        + 2 * np.arange(N)[None, :] + 1).ravel()
         self._lm_idx = lp.n_edge_dofs + np.arange(lp.lm_nodes.size)
+
+    def set_preconditioner(self, enable: bool) -> bool:
+        """Switch the device MINRES between preconditioned and plain; returns the state."""
+        on = bool(enable) and self._pc is not None
+        self._handle.set_preconditioner(self._pc if on else None)
+        self._pc_on = on
+        return on
+
+    @property
+    def preconditioned(self) -> bool:
+        return self._pc_on
 
     # ------------------------------------------------------------------ forms
     @timed("nxfx:HydraulicNetworkAssembler:compute_forms")

@@ -167,6 +167,7 @@ struct AsmArgs {
   double f;
   double* val;
   double* rhs;
+  double* dq;  // E*(N+1) lumped flux mass (preconditioner), or nullptr
   int lhs, do_rhs;
 };
 
@@ -251,6 +252,19 @@ __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
           default: v = s_md[w][slot] + s_md[w][slot + 1]; break;  // interior diagonal
         }
         a.val[seg + i] = v;
+      }
+      // lumped (row-sum) flux mass of q_k, k in the chunk (and q_N in the last chunk):
+      // the preconditioner's D block
+      if (a.dq != nullptr) {
+        const int64_t qb = e * (int64_t)(N + 1);
+        if (lane < nc) {
+          const int k = c0 + lane;
+          const int sl = lane + 1;  // cell k; cell k-1 is sl-1
+          double d = s_md[w][sl] + s_mo[w][sl];
+          if (k > 0) d = (s_mo[w][sl - 1] + s_md[w][sl - 1]) + d;
+          a.dq[qb + k] = d;
+        }
+        if (lane == 0 && c0 + nc == N) a.dq[qb + N] = s_mo[w][nc] + s_md[w][nc];
       }
     }
     __syncthreads();
@@ -443,33 +457,51 @@ __device__ __forceinline__ Rot mr_rotate(MrState& s, double b2) {
 }
 
 // Sum of n values in a fixed order, identical in every block; returned to all threads.
+template <int BS = kBlock>
 __device__ __forceinline__ double block_allsum(const double* __restrict__ p, int n) {
-  __shared__ double s_w[kBlock / 64];
+  __shared__ double s_w[BS / 64];
   __shared__ double s_tot;
   double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += kBlock) v += p[i];
+  for (int i = threadIdx.x; i < n; i += BS) v += p[i];
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = s_w[0];
 #pragma unroll
-    for (int i = 1; i < kBlock / 64; ++i) t += s_w[i];
+    for (int i = 1; i < BS / 64; ++i) t += s_w[i];
     s_tot = t;
   }
   __syncthreads();
   return s_tot;
 }
 
+// Block sum of one value per thread -> *out (thread 0). Block size BS.
+template <int BS>
+__device__ __forceinline__ void block_sum_store_n(double v, double* out) {
+  __shared__ double s_w[BS / 64];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = s_w[0];
+#pragma unroll
+    for (int i = 1; i < BS / 64; ++i) t += s_w[i];
+    *out = t;
+  }
+}
+
 struct MrVecs {
-  double* r1;        // in: beta_{k-1} v_{k-1} (b at k = 1); out: y
-  const double* r2;  // beta_k v_k, gathered (has ghost slots)
+  double* r1;        // in: r_{k-1} (b at k = 1); out: y
+  const double* r2;  // r_k; without preconditioner r_k = beta_k v_k and it is gathered
   double* w1;        // w_{k-3} in, w_{k-1} out (in place)
   const double* w2;  // w_{k-2}
   double* x;
+  const double* z;   // preconditioned: z_k = P^{-1} r_k, gathered (has ghost slots)
+  double* v;         // preconditioned: v_{k-1} in, v_k = z_k / beta_k out (in place)
 };
 
-template <bool MULTI>
+template <bool MULTI, bool PC>
 __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState* __restrict__ sin,
                                                  MrState* __restrict__ sout,
                                                  const double* __restrict__ partB, int nB,
@@ -485,25 +517,28 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
   const double sc = 1.0 / beta;
   const double c1 = upd ? beta / oldb : 0.0;
   const bool spmv = !s.done;
+  const double* g = PC ? v.z : v.r2;  // v_k = g / beta_k
   double part = 0.0;
   for (int c = 0; c < chunksA; ++c) {
     const int64_t r0 = ((int64_t)blockIdx.x * chunksA + c) * kRowsPerBlock;
     if (r0 >= A.n_rows) break;
     const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
-    const double Ay = spmv ? spmv_row_sum(A, v.r2, r0, nr) : 0.0;
+    const double Ay = spmv ? spmv_row_sum(A, g, r0, nr) : 0.0;
     if ((int)threadIdx.x < nr) {
       const int64_t r = r0 + threadIdx.x;
       const double r1v = v.r1[r];
       if (upd) {  // w = (v - oldeps w1 - delta w2) / gamma ; x += phi w
-        const double vk = r1v / oldb;
+        const double vk = PC ? v.v[r] : r1v / oldb;
         const double wn = (vk - rot.oldeps * v.w1[r] - rot.delta * v.w2[r]) * rot.denom;
         v.w1[r] = wn;
         v.x[r] += rot.phi * wn;
       }
       if (spmv) {
+        const double vn = sc * g[r];
         const double y = sc * Ay - c1 * r1v;
-        part += (sc * v.r2[r]) * y;
+        part += vn * y;
         v.r1[r] = y;
+        if (PC) v.v[r] = vn;
       }
     }
     __syncthreads();  // LDS of spmv_row_sum is reused by the next chunk
@@ -583,6 +618,308 @@ __global__ __launch_bounds__(kBlock) void k_reduce_slot(const double* __restrict
   if (threadIdx.x == 0) red[slot] = t;
 }
 
+// ------------------------------------------------------------------------------------
+// Tree Schur-complement preconditioner z = P^{-1} r, P = blockdiag(D, G^T D^{-1} G)
+// (networks_fenicsx_amd/precond.py has the derivation and the host decomposition).
+// Per iteration: k_pc_up (lower subtrees + chain-only jobs: Lanczos update of r, chain
+// condensation, junction elimination inside each subtree) -> k_pc_top (one workgroup:
+// junctions above the cut, solve, back-substitution) -> k_pc_down (subtree back-
+// substitution, chain cells by the 1-D Green's function, z and partial r.z).
+// A chain is processed by a W-lane segment, CPL cells per lane (N <= W*CPL).
+struct PcArgs {
+  int N;
+  const int* chain_edge;
+  const int* chain_flip;
+  const int* chain_up;
+  const int* chain_lo;
+  const int* slot_lam;
+  const int* slot_pchain;
+  const int* slot_parent;
+  const int* slot_dc_off;
+  const int* slot_dc;
+  const int* job_chain_off;
+  const int* job_lvl_off;
+  const int* lvl_slot_off;
+  const int* top_lvl_off;
+  int n_top_lvl;
+  int n_jobs;
+  const double* dq;  // E*(N+1) lumped flux mass
+  double* chain_T;
+  double* chain_It;
+  double* chain_Ib;
+  double* slot_D;
+  double* slot_J;
+};
+
+template <int W>
+__device__ __forceinline__ double seg_incl_scan(double v) {
+  const int l = threadIdx.x & (W - 1);
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) {
+    const double t = __shfl_up(v, o, W);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+
+template <int W>
+__device__ __forceinline__ double seg_sum(double v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+  return v;
+}
+
+// Cells / fluxes of one chain seen by one lane: chain order runs top -> bottom.
+template <int W, int CPL>
+struct ChainLane {
+  int valid[CPL];
+  int64_t dof_c[CPL];  // pressure DoF of chain cell k = l*CPL + t
+  int64_t dof_q[CPL];  // flux DoF of chain q_k (between cell k-1 and k)
+  double rho[CPL];
+  double D[CPL];       // resistance distance top -> cell k
+  int has_last;        // this lane also owns q_N
+  int64_t dof_qN;
+  double rhoN;
+  double T;
+
+  __device__ __forceinline__ void setup(const PcArgs& pa, int c, bool active) {
+    const int N = pa.N;
+    const int l = threadIdx.x & (W - 1);
+    const int e = active ? pa.chain_edge[c] : 0;
+    const int flip = active ? pa.chain_flip[c] : 0;
+    const int64_t base = (int64_t)e * (2 * N + 1);
+    const double* dqe = pa.dq + (int64_t)e * (N + 1);
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      const int k = l * CPL + t;
+      valid[t] = active && k < N;
+      const int kp = flip ? N - 1 - k : k;
+      const int qp = flip ? N - k : k;
+      dof_c[t] = base + 2 * kp + 1;
+      dof_q[t] = base + 2 * qp;
+      rho[t] = valid[t] ? dqe[qp] : 0.0;
+      acc += rho[t];
+      D[t] = acc;
+    }
+    has_last = active && (l == (N - 1) / CPL);
+    dof_qN = base + 2 * (flip ? 0 : N);
+    rhoN = has_last ? dqe[flip ? 0 : N] : 0.0;
+    const double excl = seg_incl_scan<W>(acc) - acc;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) D[t] += excl;
+    T = seg_sum<W>(acc + rhoN);
+  }
+};
+
+template <int BS>
+__device__ __forceinline__ void pc_eliminate(const PcArgs& pa, const double* __restrict__ y,
+                                             int j) {
+  const int pcn = pa.slot_pchain[j];
+  double D = pcn >= 0 ? 1.0 / pa.chain_T[pcn] : 0.0;
+  double J = y[pa.slot_lam[j]] + (pcn >= 0 ? pa.chain_Ib[pcn] : 0.0);
+  for (int i = pa.slot_dc_off[j]; i < pa.slot_dc_off[j + 1]; ++i) {
+    const int c = pa.slot_dc[i];
+    const double g = 1.0 / pa.chain_T[c];
+    J += pa.chain_It[c];
+    const int lo = pa.chain_lo[c];
+    if (lo >= 0) {
+      const double Dl = pa.slot_D[lo];
+      D += g * (1.0 - g / Dl);
+      J += g * pa.slot_J[lo] / Dl;
+    } else {
+      D += g;
+    }
+  }
+  pa.slot_D[j] = D;
+  pa.slot_J[j] = J;
+}
+
+__device__ __forceinline__ double pc_backsub(const PcArgs& pa, double* __restrict__ z, int j) {
+  const int p = pa.slot_parent[j];
+  double num = pa.slot_J[j];
+  if (p >= 0) num += z[pa.slot_lam[p]] / pa.chain_T[pa.slot_pchain[j]];
+  const double zj = num / pa.slot_D[j];
+  z[pa.slot_lam[j]] = zj;
+  return zj;
+}
+
+// mode 0: Lanczos step (r' = y - (alpha/beta) r2 in place of y, then condense r');
+// mode 1: start (condense y = b as is).
+template <bool MULTI, int W, int CPL>
+__global__ __launch_bounds__(kBlock) void k_pc_up(PcArgs pa, double* __restrict__ y,
+                                                  const double* __restrict__ r2,
+                                                  MrState* __restrict__ st,
+                                                  MrState* __restrict__ other,
+                                                  const double* __restrict__ partA, int nA,
+                                                  const double* __restrict__ red, int mode) {
+  double c2 = 0.0;
+  if (mode == 0) {
+    if (st->done) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
+      return;
+    }
+    const double alfa = MULTI ? red[0] : block_allsum(partA, nA);
+    c2 = alfa / st->beta;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->alfa = alfa;
+      st->nb += 1;
+    }
+  }
+  const int job = blockIdx.x;
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kBlock / W;  // chains per pass
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    ChainLane<W, CPL> ch;
+    ch.setup(pa, c, active);
+    double sr = 0.0, srd = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      if (!ch.valid[t]) continue;
+      double rc = y[ch.dof_c[t]];
+      if (mode == 0) {
+        rc -= c2 * r2[ch.dof_c[t]];
+        y[ch.dof_c[t]] = rc;
+        y[ch.dof_q[t]] -= c2 * r2[ch.dof_q[t]];
+      }
+      sr += rc;
+      srd += rc * ch.D[t];
+    }
+    if (mode == 0 && ch.has_last) y[ch.dof_qN] -= c2 * r2[ch.dof_qN];
+    sr = seg_sum<W>(sr);
+    srd = seg_sum<W>(srd);
+    if (active && l == 0) {
+      const double ib = srd / ch.T;
+      pa.chain_T[c] = ch.T;
+      pa.chain_Ib[c] = ib;
+      pa.chain_It[c] = sr - ib;
+    }
+  }
+  // junction levels of this job, deepest first
+  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
+  if (lv1 > lv0) {
+    if (mode == 0) {
+      for (int j = pa.lvl_slot_off[lv0] + threadIdx.x; j < pa.lvl_slot_off[lv1]; j += kBlock) {
+        const int lam = pa.slot_lam[j];
+        y[lam] -= c2 * r2[lam];
+      }
+    }
+    __syncthreads();
+    for (int lv = lv1 - 1; lv >= lv0; --lv) {
+      for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kBlock)
+        pc_eliminate<kBlock>(pa, y, j);
+      __syncthreads();
+    }
+  }
+}
+
+constexpr int kTopThreads = 1024;
+
+template <bool MULTI>
+__global__ __launch_bounds__(kTopThreads) void k_pc_top(PcArgs pa, double* __restrict__ y,
+                                                        const double* __restrict__ r2,
+                                                        double* __restrict__ z,
+                                                        const MrState* __restrict__ st,
+                                                        const double* __restrict__ partA, int nA,
+                                                        const double* __restrict__ red,
+                                                        double* __restrict__ partB, int mode) {
+  double c2 = 0.0;
+  if (mode == 0) {
+    if (st->done) return;
+    const double alfa = MULTI ? red[0] : block_allsum<kTopThreads>(partA, nA);
+    c2 = alfa / st->beta;
+  }
+  const int nl = pa.n_top_lvl;
+  const int s0 = pa.top_lvl_off[0], s1 = pa.top_lvl_off[nl];
+  if (mode == 0) {
+    for (int j = s0 + threadIdx.x; j < s1; j += kTopThreads) {
+      const int lam = pa.slot_lam[j];
+      y[lam] -= c2 * r2[lam];
+    }
+  }
+  __syncthreads();
+  for (int lv = nl - 1; lv >= 0; --lv) {
+    for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads)
+      pc_eliminate<kTopThreads>(pa, y, j);
+    __syncthreads();
+  }
+  double part = 0.0;
+  for (int lv = 0; lv < nl; ++lv) {
+    for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads)
+      part += y[pa.slot_lam[j]] * pc_backsub(pa, z, j);
+    __syncthreads();
+  }
+  block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
+}
+
+template <bool MULTI, int W, int CPL>
+__global__ __launch_bounds__(kBlock) void k_pc_down(PcArgs pa, const double* __restrict__ y,
+                                                    double* __restrict__ z,
+                                                    const MrState* __restrict__ st,
+                                                    double* __restrict__ partB, int mode) {
+  if (mode == 0 && st->done) return;
+  const int job = blockIdx.x;
+  double part = 0.0;
+  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
+  for (int lv = lv0; lv < lv1; ++lv) {
+    for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kBlock)
+      part += y[pa.slot_lam[j]] * pc_backsub(pa, z, j);
+    __syncthreads();
+  }
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kBlock / W;
+  const int seg = threadIdx.x / W;
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    ChainLane<W, CPL> ch;
+    ch.setup(pa, c, active);
+    const int up = active ? pa.chain_up[c] : -1, lo = active ? pa.chain_lo[c] : -1;
+    const double zt = up >= 0 ? z[pa.slot_lam[up]] : 0.0;
+    const double zb = lo >= 0 ? z[pa.slot_lam[lo]] : 0.0;
+    const double T = ch.T, iT = 1.0 / T;
+    double rc[CPL], a[CPL], b[CPL];
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      rc[t] = ch.valid[t] ? y[ch.dof_c[t]] : 0.0;
+      a[t] = (T - ch.D[t]) * rc[t];  // suffix sums over j >= k
+      b[t] = ch.D[t] * rc[t];        // prefix sums over j < k
+      sa += a[t];
+      sb += b[t];
+    }
+    const double ia = seg_incl_scan<W>(sa), ib = seg_incl_scan<W>(sb);
+    const double Atot = seg_sum<W>(sa);
+    double pa_ = ia - sa, pb_ = ib - sb;  // exclusive lane carries
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      pa_ += a[t];  // inclusive prefix of a up to k
+      const double suffix = Atot - pa_ + a[t];
+      const double prefix = pb_;  // sum_{j<k} b_j
+      pb_ += b[t];
+      if (!ch.valid[t]) continue;
+      const double Dk = ch.D[t];
+      const double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      z[ch.dof_c[t]] = zk;
+      part += rc[t] * zk;
+      const double rq = y[ch.dof_q[t]];
+      const double zq = rq / ch.rho[t];
+      z[ch.dof_q[t]] = zq;
+      part += rq * zq;
+    }
+    if (ch.has_last) {
+      const double rq = y[ch.dof_qN];
+      const double zq = rq / ch.rhoN;
+      z[ch.dof_qN] = zq;
+      part += rq * zq;
+    }
+  }
+  block_sum_store(part, partB + blockIdx.x);
+}
+
 __global__ void k_pack(const double* __restrict__ x, const int* __restrict__ idx, int n,
                        double* __restrict__ buf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -609,6 +946,7 @@ struct nx_network {
   double* edge_R = nullptr;
   double* edge_bc = nullptr;
   double* lm_val = nullptr;
+  double* dq = nullptr;  // E*(N+1) lumped flux mass (preconditioner D block)
   double f = 0.0;
   bool have_coeffs = false, have_lhs = false, have_rhs = false;
   // CSR + rhs
@@ -629,6 +967,14 @@ struct nx_network {
   double* partB = nullptr;             // nB
   double* red = nullptr;               // 4 cross-rank reduction slots
   MrState* st = nullptr;               // 2 buffers (ping-pong)
+  // tree Schur preconditioner (nx_set_preconditioner)
+  bool pc = false;
+  int pc_variant = 0;   // (W, CPL) instantiation
+  int pc_jobs = 0;
+  PcArgs pa{};
+  std::vector<void*> pc_bufs;
+  double* z = nullptr;  // P^{-1} r, n_col
+  double* vv = nullptr; // Lanczos vector v, n_own
   MrState* h_st = nullptr;             // pinned host mirror of both
   // graph chunk
   hipGraphExec_t chunk_exec = nullptr;
@@ -698,6 +1044,34 @@ int allreduce_slot(nx_network* h, int slot) {
   return NX_OK;
 }
 
+// Preconditioner application on the stream: z = P^{-1} r' where r' = y - (alpha/beta) r2
+// (mode 0, written back into y) or r' = y (mode 1, start). Partials of r'.z -> partB.
+template <bool MULTI, int W, int CPL>
+void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other,
+                  int mode) {
+  if (h->pc_jobs > 0)
+    hipLaunchKernelGGL((k_pc_up<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
+                       h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
+  hipLaunchKernelGGL((k_pc_top<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2,
+                     h->z, st, h->partA, h->nA, h->red, h->partB, mode);
+  if (h->pc_jobs > 0)
+    hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
+                       h->pa, y, h->z, st, h->partB, mode);
+}
+
+template <bool MULTI>
+void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other, int mode) {
+  switch (h->pc_variant) {
+    case 0: launch_pc_wc<MULTI, 16, 1>(h, y, r2, st, other, mode); break;
+    case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode); break;
+    case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode); break;
+    case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode); break;
+    default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode); break;
+  }
+}
+
+int nB_of(const nx_network* h) { return h->pc ? h->pc_jobs + 1 : h->nB; }
+
 // One MINRES iteration on the stream; `k` = 1-based iteration index (parity only).
 int launch_iteration(nx_network* h, int64_t k) {
   double* r1 = h->vb[(k - 1) & 1];
@@ -708,30 +1082,40 @@ int launch_iteration(nx_network* h, int64_t k) {
   MrState* sin = h->st + ((k + 1) & 1);
   MrState* sout = h->st + (k & 1);
   const bool multi = h->comm != nullptr;
-  if (multi) CHECK(halo(h, r2));
-  MrVecs mv{r1, r2, w1, w2, h->x};
+  const bool pc = h->pc;
+  if (multi) CHECK(halo(h, pc ? h->z : r2));
+  MrVecs mv{r1, r2, w1, w2, h->x, h->z, h->vv};
+  const int nB = nB_of(h);
   // profiling: events bound to the kernel's own dispatch packet (hipExtLaunchKernel), so
   // the measured interval is the kernel's execution like rocprofv3's, not marker latency
   hipEvent_t e0 = h->prof ? h->ev_pool[2 * h->prof_k] : nullptr;
   hipEvent_t e1 = h->prof ? h->ev_pool[2 * h->prof_k + 1] : nullptr;
-  if (multi)
-    hipExtLaunchKernelGGL(k_mr_a<true>, dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,
-                          csr_of(h), mv, sin, sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
-  else
-    hipExtLaunchKernelGGL(k_mr_a<false>, dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,
-                          csr_of(h), mv, sin, sout, h->partB, h->nB, h->red, h->partA, h->chunksA);
+#define NX_LAUNCH_A(M, P)                                                                        \
+  hipExtLaunchKernelGGL((k_mr_a<M, P>), dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,     \
+                        csr_of(h), mv, sin, sout, h->partB, nB, h->red, h->partA, h->chunksA)
+  if (multi) {
+    if (pc) NX_LAUNCH_A(true, true); else NX_LAUNCH_A(true, false);
+  } else {
+    if (pc) NX_LAUNCH_A(false, true); else NX_LAUNCH_A(false, false);
+  }
+#undef NX_LAUNCH_A
   if (h->prof) h->prof_k += 1;
   if (multi) {
     hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partA, h->nA, h->red, 0);
     CHECK(allreduce_slot(h, 0));
-    hipLaunchKernelGGL(k_mr_b<true>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
-                       sout, sin, h->partA, h->nA, h->red, h->partB);
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partB, h->nB,
-                       h->red, 1);
+    if (pc)
+      launch_pc<true>(h, r1, r2, sout, sin, 0);
+    else
+      hipLaunchKernelGGL(k_mr_b<true>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
+                         sout, sin, h->partA, h->nA, h->red, h->partB);
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partB, nB, h->red, 1);
     CHECK(allreduce_slot(h, 1));
   } else {
-    hipLaunchKernelGGL(k_mr_b<false>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
-                       sout, sin, h->partA, h->nA, h->red, h->partB);
+    if (pc)
+      launch_pc<false>(h, r1, r2, sout, sin, 0);
+    else
+      hipLaunchKernelGGL(k_mr_b<false>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
+                         sout, sin, h->partA, h->nA, h->red, h->partB);
   }
   HIPCALL(hipGetLastError());
   return NX_OK;
@@ -849,6 +1233,7 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   if ((rc = upload(&h->lm_val, lm_val, nnz_lm, h->stream))) return bail(rc);
   if ((rc = dalloc(&h->edge_R, n_edges))) return bail(rc);
   if ((rc = dalloc(&h->edge_bc, 2 * n_edges))) return bail(rc);
+  if ((rc = dalloc(&h->dq, n_edges * (int64_t)(N + 1)))) return bail(rc);
   if ((rc = dalloc(&h->rowptr, n_own + 1))) return bail(rc);
   if ((rc = dalloc(&h->col, h->nnz))) return bail(rc);
   if ((rc = dalloc(&h->val, h->nnz))) return bail(rc);
@@ -904,12 +1289,15 @@ NX_API int nx_destroy(nx_network_t* h) {
   if (h->chunk_exec) (void)hipGraphExecDestroy(h->chunk_exec);
   if (h->chunk_graph) (void)hipGraphDestroy(h->chunk_graph);
   if (h->comm) ncclCommDestroy(h->comm);
-  void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val,
+  void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val, h->dq,
+                  h->z, h->vv,
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
                   h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
                   h->partA,  h->partB,   h->red,
                   h->send_idx, h->send_buf};
   for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  for (void* p : h->pc_bufs)
     if (p) (void)hipFree(p);
   if (h->h_st) (void)hipHostFree(h->h_st);
   for (auto& e : h->ev)
@@ -960,7 +1348,7 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   if (!lhs && !rhs) return NX_OK;
   if (h->E > 0) {
     AsmArgs a{EdgeArgs{h->edge_x, h->edge_lm, h->edge_seg, h->E, h->N},
-              h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs, rhs};
+              h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs ? h->dq : nullptr, lhs, rhs};
     hipExtLaunchKernelGGL(k_assemble, dim3(grid_of(h->E, kBlock / 64)), dim3(kBlock), 0, h->stream,
                           h->prof ? h->ev[0] : nullptr, h->prof ? h->ev[1] : nullptr, 0, a);
   }
@@ -999,17 +1387,25 @@ NX_API int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_e
   }
   HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, s));
   const bool multi = h->comm != nullptr;
-  hipLaunchKernelGGL(k_sumsq, dim3(h->nB), dim3(kBlock), 0, s, h->rhs, n, h->partB);
+  const int nB = nB_of(h);
+  if (h->pc) {  // beta_1^2 = b . P^{-1} b
+    if (multi)
+      launch_pc<true>(h, h->vb[0], h->vb[1], h->st, h->st + 1, 1);
+    else
+      launch_pc<false>(h, h->vb[0], h->vb[1], h->st, h->st + 1, 1);
+  } else {
+    hipLaunchKernelGGL(k_sumsq, dim3(h->nB), dim3(kBlock), 0, s, h->rhs, n, h->partB);
+  }
   if (multi) {
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, s, h->partB, h->nB, h->red, 2);
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, s, h->partB, nB, h->red, 2);
     CHECK(allreduce_slot(h, 2));
   }
   for (int b = 0; b < 2; ++b) {  // both state buffers start identical
     if (multi)
-      hipLaunchKernelGGL(k_mr_init<true>, dim3(1), dim3(kBlock), 0, s, h->partB, h->nB, h->red,
+      hipLaunchKernelGGL(k_mr_init<true>, dim3(1), dim3(kBlock), 0, s, h->partB, nB, h->red,
                          h->st + b, rtol, maxit);
     else
-      hipLaunchKernelGGL(k_mr_init<false>, dim3(1), dim3(kBlock), 0, s, h->partB, h->nB, h->red,
+      hipLaunchKernelGGL(k_mr_init<false>, dim3(1), dim3(kBlock), 0, s, h->partB, nB, h->red,
                          h->st + b, rtol, maxit);
   }
   HIPCALL(hipGetLastError());
@@ -1108,20 +1504,17 @@ NX_API int nx_true_residual(nx_network_t* h, double* relres) {
   if (!h->have_lhs || !h->have_rhs) return fail(NX_ERR_STATE, "assemble first");
   CHECK(set_device(h));
   if (h->comm) CHECK(halo(h, h->x));
-  if (h->nblk > 0)
-    hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                       h->rhs, h->partials, h->nblk);
-  double* d = nullptr;
-  HIPCALL(hipMallocAsync((void**)&d, 2 * sizeof(double), h->stream));
+  hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                     h->rhs, h->partials, h->nblk);
+  double* d = h->red + 2;  // slots 2, 3 are free outside nx_solve
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials, h->nblk, d);
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials + h->nblk,
                      h->nblk, d + 1);
   HIPCALL(hipGetLastError());
   if (h->comm) NCCLCALL(ncclAllReduce(d, d, 2, ncclDouble, ncclSum, h->comm, h->stream));
-  double hd[2];
-  HIPCALL(hipMemcpyAsync(hd, d, sizeof(hd), hipMemcpyDeviceToHost, h->stream));
-  HIPCALL(hipFreeAsync(d, h->stream));
   HIPCALL(hipStreamSynchronize(h->stream));
+  double hd[2] = {0.0, 0.0};
+  HIPCALL(hipMemcpy(hd, d, sizeof(hd), hipMemcpyDeviceToHost));
   *relres = hd[1] > 0 ? std::sqrt(hd[0] / hd[1]) : std::sqrt(hd[0]);
   return NX_OK;
 }
@@ -1176,6 +1569,122 @@ NX_API int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv) {
   float ms = 0.f;
   HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
   *ms_per_spmv = ms / reps;
+  return NX_OK;
+}
+
+
+NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
+                                 const int32_t* chain_edge, const int32_t* chain_flip,
+                                 const int32_t* chain_up, const int32_t* chain_lo, int64_t n_slots,
+                                 const int32_t* slot_lam, const int32_t* slot_pchain,
+                                 const int32_t* slot_parent, const int32_t* slot_dc_off,
+                                 const int32_t* slot_dc, int32_t n_jobs,
+                                 const int32_t* job_chain_off, const int32_t* job_lvl_off,
+                                 int32_t n_lvl, const int32_t* lvl_slot_off, int32_t n_top_lvl,
+                                 const int32_t* top_lvl_off) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  if (h->chunk_exec) {  // captured launches depend on the preconditioner: recapture
+    HIPCALL(hipGraphExecDestroy(h->chunk_exec));
+    h->chunk_exec = nullptr;
+    h->chunk_len = 0;
+  }
+  if (!enable) {
+    h->pc = false;
+    return NX_OK;
+  }
+  const int N = h->N;
+  int variant;
+  if (N <= 16) variant = 0;
+  else if (N <= 32) variant = 1;
+  else if (N <= 64) variant = 2;
+  else if (N <= 128) variant = 3;
+  else if (N <= 256) variant = 4;
+  else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 256 cells per edge");
+  if (n_chains != h->E) return fail(NX_ERR_ARG, "one chain per local edge expected");
+  if (n_slots != h->B) return fail(NX_ERR_ARG, "one junction slot per owned multiplier expected");
+  if (n_jobs < 0 || n_lvl < 0 || n_top_lvl < 0) return fail(NX_ERR_ARG, "negative sizes");
+  if (h->E > 0 && n_jobs < 1) return fail(NX_ERR_ARG, "chains need at least one job");
+  for (int64_t c = 0; c < n_chains; ++c) {
+    if (chain_edge[c] < 0 || chain_edge[c] >= h->E) return fail(NX_ERR_ARG, "chain_edge out of range");
+    if (chain_up[c] < -1 || chain_up[c] >= n_slots || chain_lo[c] < -1 || chain_lo[c] >= n_slots)
+      return fail(NX_ERR_ARG, "chain end slot out of range");
+  }
+  for (int64_t j = 0; j < n_slots; ++j) {
+    if (slot_lam[j] < h->n_edge_dofs || slot_lam[j] >= h->n_own)
+      return fail(NX_ERR_ARG, "slot_lam must be an owned multiplier row");
+    if (slot_pchain[j] < -1 || slot_pchain[j] >= n_chains || slot_parent[j] < -1 ||
+        slot_parent[j] >= n_slots)
+      return fail(NX_ERR_ARG, "slot parent out of range");
+  }
+  if (job_chain_off[0] != 0 || job_chain_off[n_jobs] != n_chains)
+    return fail(NX_ERR_ARG, "job_chain_off must cover all chains");
+  if (job_lvl_off[n_jobs] != n_lvl) return fail(NX_ERR_ARG, "job_lvl_off must end at n_lvl");
+  if (n_slots > 0 && (int64_t)(n_lvl > 0 ? lvl_slot_off[n_lvl] : 0) +
+                             (top_lvl_off[n_top_lvl] - top_lvl_off[0]) != n_slots)
+    return fail(NX_ERR_ARG, "levels must cover all slots");
+  for (void* p : h->pc_bufs) (void)hipFree(p);
+  h->pc_bufs.clear();
+  auto up = [&](const int32_t* src, int64_t n) -> const int* {
+    int* d = nullptr;
+    if (n <= 0) n = 1;
+    if (hipMalloc((void**)&d, sizeof(int) * n) != hipSuccess) return nullptr;
+    h->pc_bufs.push_back(d);
+    if (src && hipMemcpy(d, src, sizeof(int) * n, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return d;
+  };
+  auto scratch = [&](int64_t n) -> double* {
+    double* d = nullptr;
+    if (n <= 0) n = 1;
+    if (hipMalloc((void**)&d, sizeof(double) * n) != hipSuccess) return nullptr;
+    h->pc_bufs.push_back(d);
+    return d;
+  };
+  PcArgs pa{};
+  pa.N = N;
+  pa.chain_edge = up(chain_edge, n_chains);
+  pa.chain_flip = up(chain_flip, n_chains);
+  pa.chain_up = up(chain_up, n_chains);
+  pa.chain_lo = up(chain_lo, n_chains);
+  pa.slot_lam = up(slot_lam, n_slots);
+  pa.slot_pchain = up(slot_pchain, n_slots);
+  pa.slot_parent = up(slot_parent, n_slots);
+  pa.slot_dc_off = up(slot_dc_off, n_slots + 1);
+  pa.slot_dc = up(slot_dc, slot_dc_off[n_slots]);
+  pa.job_chain_off = up(job_chain_off, n_jobs + 1);
+  pa.job_lvl_off = up(job_lvl_off, n_jobs + 1);
+  pa.lvl_slot_off = up(lvl_slot_off, n_lvl + 1);
+  pa.top_lvl_off = up(top_lvl_off, n_top_lvl + 1);
+  pa.n_top_lvl = n_top_lvl;
+  pa.n_jobs = n_jobs;
+  pa.dq = h->dq;
+  pa.chain_T = scratch(n_chains);
+  pa.chain_It = scratch(n_chains);
+  pa.chain_Ib = scratch(n_chains);
+  pa.slot_D = scratch(n_slots);
+  pa.slot_J = scratch(n_slots);
+  for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
+                        (const void*)pa.chain_lo, (const void*)pa.slot_lam, (const void*)pa.slot_pchain,
+                        (const void*)pa.slot_parent, (const void*)pa.slot_dc_off, (const void*)pa.slot_dc,
+                        (const void*)pa.job_chain_off, (const void*)pa.job_lvl_off,
+                        (const void*)pa.lvl_slot_off, (const void*)pa.top_lvl_off,
+                        (const void*)pa.chain_T, (const void*)pa.chain_It, (const void*)pa.chain_Ib,
+                        (const void*)pa.slot_D, (const void*)pa.slot_J})
+    if (p == nullptr) return fail(NX_ERR_HIP, "preconditioner upload failed");
+  if (!h->z) CHECK(dalloc(&h->z, std::max<int64_t>(h->n_col, 1)));
+  if (!h->vv) CHECK(dalloc(&h->vv, std::max<int64_t>(h->n_own, 1)));
+  HIPCALL(hipMemset(h->z, 0, sizeof(double) * std::max<int64_t>(h->n_col, 1)));
+  if (n_jobs + 1 > h->nB) {  // partB holds one partial per job + the top block
+    HIPCALL(hipFree(h->partB));
+    h->partB = nullptr;
+    h->nB = n_jobs + 1;
+    CHECK(dalloc(&h->partB, h->nB));
+  }
+  h->pa = pa;
+  h->pc_jobs = n_jobs;
+  h->pc_variant = variant;
+  h->pc = true;
   return NX_OK;
 }
 

@@ -17,9 +17,13 @@ PETSc options understood (with or without the options prefix):
 ``ksp_monitor``                   print iterations / residual after each solve
 ``ksp_check_every``               iterations per host convergence check (default 32)
 
-``ksp_type``, ``pc_type`` and ``pc_factor_mat_solver_type`` are accepted and recorded:
-whatever they say, the device solve is MINRES (a direct LU has no place on this
-path); the tolerance above makes the result agree with the direct solve.
+``pc_type``                       ``"none"`` runs plain MINRES; anything else (the reference's
+                                  default ``"lu"`` included) uses the tree Schur-complement
+                                  preconditioner (``precond.py``)
+
+``ksp_type`` and ``pc_factor_mat_solver_type`` are accepted and recorded: whatever they
+say, the device solve is MINRES (a direct LU has no place on this path); the tolerance
+above makes the result agree with the direct solve.
 """
 
 from __future__ import annotations
@@ -108,6 +112,7 @@ class Solver:
         self._raise = _truthy(clean.get("ksp_error_if_not_converged", True))
         self._monitor = "ksp_monitor" in clean and _truthy(clean["ksp_monitor"])
         self._ksp = KSPInfo(petsc_options_prefix, clean)
+        self._pc = str(clean.get("pc_type", "lu")).lower() != "none"
         self._kind = kind
         self._A = DeviceMatrix(assembler.handle, kind)
         self._b = DeviceVector(assembler.handle)
@@ -145,6 +150,8 @@ class Solver:
             functions.append(Function(self.assembler.pressure_space, name="pressure"))
             functions.append(Function(self.assembler.lm_space, name="global_flux"))
         h = self.assembler.handle
+        if self.assembler.preconditioned != self._pc:
+            self.assembler.set_preconditioner(self._pc)
         it, relres, conv = h.solve(self._rtol, self._maxit, self._check_every)
         self._ksp.iterations, self._ksp.residual_estimate, self._ksp.converged = it, relres, conv
         if self._monitor:
