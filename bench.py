@@ -48,11 +48,13 @@ def spmv_bytes(n_rows: int, nnz: int) -> int:
     return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
-def mr_spmv_bytes(n_rows: int, nnz: int) -> int:
-    """Algorithmic bytes of one fused ``k_mr_spmv`` launch: the CSR SpMV on r2 (matrix,
-    row pointers, r2 gathered once) plus the fused vector traffic -- r1 read+write,
-    w1 read+write, w2 read, x read+write (7 passes of 8 B per row)."""
-    return 12 * nnz + 4 * (n_rows + 1) + 8 * n_rows + 56 * n_rows
+def mr_spmv_bytes(n_rows: int, nnz: int, preconditioned: bool) -> int:
+    """Algorithmic bytes of one fused ``k_mr_a`` launch: the CSR SpMV (matrix, row
+    pointers, the gathered vector read once) plus the fused vector traffic -- r1
+    read+write, w1 read+write, w2 read, x read+write (7 passes of 8 B per row), and with
+    the preconditioner the Lanczos vector v read+write (2 more passes)."""
+    passes = 9 if preconditioned else 7
+    return 12 * nnz + 4 * (n_rows + 1) + 8 * n_rows + 8 * passes * n_rows
 
 
 def pmc_traffic(kernel_prefix: str):
@@ -100,6 +102,7 @@ def main() -> int:
     ap.add_argument("--check-every", type=int, default=32)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,6 +129,8 @@ def main() -> int:
     del G
     asm = HydraulicNetworkAssembler(mesh)
     asm.compute_forms(p_bc_ex=lambda x: x[1])
+    if args.no_pc:
+        asm.set_preconditioner(False)
     h = asm.handle
     E, B = mesh.num_edges, len(mesh.bifurcation_values)
     dof_total = E * (2 * args.N + 1) + B
@@ -167,10 +172,12 @@ def main() -> int:
     spmv_ms = prof["spmv_ms"] / max(prof["spmv_count"], 1)
     asm_ms = prof["asm_ms"] / max(prof["asm_count"], 1)
     warm_spmv_ms = h.bench_spmv(200)
-    nbytes = mr_spmv_bytes(h.n_rows, h.nnz)
+    pc_on = asm.preconditioned
+    nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on)
     achieved = nbytes / (spmv_ms * 1e-3) / 1e9
     sbytes = spmv_bytes(h.n_rows, h.nnz)
-    traffic, traffic_src, rocprof_ns = pmc_traffic("k_mr_a<false>") if world == 1 else (None, None, None)
+    kname = "k_mr_a<false, true>" if pc_on else "k_mr_a<false, false>"
+    traffic, traffic_src, rocprof_ns = pmc_traffic(kname) if world == 1 else (None, None, None)
 
     # --- parity outside the timed region
     true_rr = h.true_residual()
@@ -212,10 +219,12 @@ def main() -> int:
                 "edges": E,
                 "minres_iterations": state["it"],
                 "parallelism": f"edge-partition x{world}" if world > 1 else "single GPU",
+                "preconditioner": "tree Schur complement" if pc_on else "none",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_mr_a (CSR SpMV fused with the Lanczos step, Givens rotation and solution update)",
+                "kernel": f"{kname} (CSR SpMV fused with the Lanczos step, Givens rotation and "
+                          "solution update)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

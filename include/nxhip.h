@@ -123,7 +123,9 @@ int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
  * enable = 0 switches back to unpreconditioned MINRES. Chains (one per local edge, in job
  * order): edge slot, flip (chain runs target -> source), top / bottom junction slot (-1 =
  * ground). Junction slots (one per owned multiplier, level order per job): multiplier row,
- * chain to the parent, parent slot, CSR of chains hanging below. Jobs (one workgroup each):
+ * chain to the parent, parent slot, CSR of chains hanging below (dc_lo: bottom slot of each
+ * entry, slot_plam: the parent's multiplier row -- both derivable, passed to save the
+ * kernels a dependent load). Jobs (one workgroup each):
  * chain ranges and level ranges; lvl_slot_off / top_lvl_off: slot offsets per level (root
  * level first) of the lower jobs / of the single top workgroup. Requires N <= 256.
  */
@@ -132,7 +134,8 @@ int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
                           const int32_t* chain_up, const int32_t* chain_lo, int64_t n_slots,
                           const int32_t* slot_lam, const int32_t* slot_pchain,
                           const int32_t* slot_parent, const int32_t* slot_dc_off,
-                          const int32_t* slot_dc, int32_t n_jobs, const int32_t* job_chain_off,
+                          const int32_t* slot_dc, const int32_t* dc_lo, const int32_t* slot_plam,
+                          int32_t n_jobs, const int32_t* job_chain_off,
                           const int32_t* job_lvl_off, int32_t n_lvl, const int32_t* lvl_slot_off,
                           int32_t n_top_lvl, const int32_t* top_lvl_off);
 

@@ -52,8 +52,8 @@ _SIGS = {
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
     "nx_set_preconditioner": (C.c_int, [_h, _i32, _i64, _pi32, _pi32, _pi32, _pi32, _i64, _pi32,
-                                        _pi32, _pi32, _pi32, _pi32, _i32, _pi32, _pi32, _i32,
-                                        _pi32, _i32, _pi32]),
+                                        _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, _i32, _pi32,
+                                        _pi32, _i32, _pi32, _i32, _pi32]),
     "nx_comm_unique_id": (C.c_int, [_pu8]),
     "nx_comm_init": (C.c_int, [_h, _i32, _i32, _pu8, _i32, _pi32, _pi32, _pi32, _pi32]),
 }
@@ -229,21 +229,22 @@ class Handle:
         if pc is None:
             z = np.zeros(1, np.int32)
             check(lib().nx_set_preconditioner(self.ptr, 0, 0, *([_ptr(z, C.c_int32)] * 4), 0,
-                                              *([_ptr(z, C.c_int32)] * 5), 0, _ptr(z, C.c_int32),
+                                              *([_ptr(z, C.c_int32)] * 7), 0, _ptr(z, C.c_int32),
                                               _ptr(z, C.c_int32), 0, _ptr(z, C.c_int32), 0,
                                               _ptr(z, C.c_int32)))
             return
         arr = {k: np.ascontiguousarray(getattr(pc, k), dtype=np.int32) for k in (
             "chain_edge", "chain_flip", "chain_up", "chain_lo", "slot_lam", "slot_pchain",
-            "slot_parent", "slot_dc_off", "slot_dc", "job_chain_off", "job_lvl_off",
-            "lvl_slot_off", "top_lvl_off")}
+            "slot_parent", "slot_dc_off", "slot_dc", "dc_lo", "slot_plam", "job_chain_off",
+            "job_lvl_off", "lvl_slot_off", "top_lvl_off")}
         arr = {k: (v if v.size else np.zeros(1, np.int32)) for k, v in arr.items()}
         self._pc_keep = arr
         p = {k: _ptr(v, C.c_int32) for k, v in arr.items()}
         check(lib().nx_set_preconditioner(
             self.ptr, 1, int(pc.n_chains), p["chain_edge"], p["chain_flip"], p["chain_up"],
             p["chain_lo"], int(pc.n_slots), p["slot_lam"], p["slot_pchain"], p["slot_parent"],
-            p["slot_dc_off"], p["slot_dc"], int(pc.n_jobs), p["job_chain_off"], p["job_lvl_off"],
+            p["slot_dc_off"], p["slot_dc"], p["dc_lo"], p["slot_plam"], int(pc.n_jobs),
+            p["job_chain_off"], p["job_lvl_off"],
             int(pc.lvl_slot_off.size - 1), p["lvl_slot_off"], int(pc.top_lvl_off.size - 1),
             p["top_lvl_off"]))
 

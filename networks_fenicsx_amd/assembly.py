@@ -167,7 +167,8 @@ class HydraulicNetworkAssembler:
         # MINRES preconditioner (tree Schur complement); topology-only, built once
         self._pc: TreePreconditioner | None = None
         if mesh.N <= 256:
-            self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees)
+            jobs = int(os.environ.get("NXHIP_PC_JOBS", "256"))  # swept: 64..1024
+            self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=jobs)
         self.set_preconditioner(True)
         self._a = None
         self._L = None

@@ -637,6 +637,8 @@ struct PcArgs {
   const int* slot_parent;
   const int* slot_dc_off;
   const int* slot_dc;
+  const int* dc_lo;      // bottom slot of every slot_dc entry (host-precomputed)
+  const int* slot_plam;  // multiplier row of the parent slot, -1
   const int* job_chain_off;
   const int* job_lvl_off;
   const int* lvl_slot_off;
@@ -649,6 +651,8 @@ struct PcArgs {
   double* chain_Ib;
   double* slot_D;
   double* slot_J;
+  double* slot_A;  // back-substitution z_j = A_j + B_j z_parent (LDS kernels)
+  double* slot_B;
 };
 
 template <int W>
@@ -920,6 +924,351 @@ __global__ __launch_bounds__(kBlock) void k_pc_down(PcArgs pa, const double* __r
   block_sum_store(part, partB + blockIdx.x);
 }
 
+// ---- LDS variants: one 1024-thread workgroup per job, the junction levels run in LDS.
+// Phase A gathers, in one parallel pass, every static index and every chain result a
+// junction needs (own parent chain, chains hanging below, children as local LDS indices);
+// phase B sweeps the levels touching LDS only. The host picks these kernels when every
+// job fits the caps below (always for the binary / arterial trees), else the global ones.
+constexpr int kPcThreads = 1024;
+constexpr int kCapC = 512;    // chains per job
+constexpr int kCapS = 256;    // junction slots per job
+constexpr int kCapDC = 768;   // down-chain entries per job
+constexpr int kCapT = 1152;   // top junction slots (host caps the top part at 1024)
+constexpr int kCapTDC = 2304; // top down-chain entries
+constexpr int kMaxTopLvl = 255;
+
+template <bool MULTI, int W, int CPL>
+__global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __restrict__ y,
+                                                          const double* __restrict__ r2,
+                                                          MrState* __restrict__ st,
+                                                          MrState* __restrict__ other,
+                                                          const double* __restrict__ partA,
+                                                          int nA, const double* __restrict__ red,
+                                                          int mode) {
+  __shared__ double sT[kCapC], sIt[kCapC], sIb[kCapC];
+  __shared__ double sD0[kCapS], sJ0[kCapS], sD[kCapS], sJ[kCapS];
+  __shared__ int sChild[kCapDC];
+  __shared__ double sG[kCapDC];
+  __shared__ int sOff[kCapS + 1];
+  double c2 = 0.0;
+  if (mode == 0) {
+    if (st->done) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
+      return;
+    }
+    const double alfa = MULTI ? red[0] : block_allsum<kPcThreads>(partA, nA);
+    c2 = alfa / st->beta;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->alfa = alfa;
+      st->nb += 1;
+    }
+  }
+  const int job = blockIdx.x;
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    ChainLane<W, CPL> ch;
+    ch.setup(pa, c, active);
+    double sr = 0.0, srd = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      if (!ch.valid[t]) continue;
+      double rc = y[ch.dof_c[t]];
+      if (mode == 0) {
+        rc -= c2 * r2[ch.dof_c[t]];
+        y[ch.dof_c[t]] = rc;
+        y[ch.dof_q[t]] -= c2 * r2[ch.dof_q[t]];
+      }
+      sr += rc;
+      srd += rc * ch.D[t];
+    }
+    if (mode == 0 && ch.has_last) y[ch.dof_qN] -= c2 * r2[ch.dof_qN];
+    sr = seg_sum<W>(sr);
+    srd = seg_sum<W>(srd);
+    if (active && l == 0) {
+      const double ib = srd / ch.T;
+      sT[c - c0] = ch.T;
+      sIb[c - c0] = ib;
+      sIt[c - c0] = sr - ib;
+      pa.chain_T[c] = ch.T;
+      pa.chain_Ib[c] = ib;
+      pa.chain_It[c] = sr - ib;
+    }
+  }
+  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
+  if (lv1 == lv0) return;
+  const int js0 = pa.lvl_slot_off[lv0], js1 = pa.lvl_slot_off[lv1];
+  const int ns = js1 - js0;
+  const int dc0 = pa.slot_dc_off[js0];
+  __syncthreads();
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {  // phase A
+    const int j = js0 + sl;
+    const int lam = pa.slot_lam[j];
+    double yl = y[lam];
+    if (mode == 0) {
+      yl -= c2 * r2[lam];
+      y[lam] = yl;
+    }
+    const int pcn = pa.slot_pchain[j];
+    double D0 = pcn >= 0 ? 1.0 / sT[pcn - c0] : 0.0;
+    double J0 = yl + (pcn >= 0 ? sIb[pcn - c0] : 0.0);
+    const int o0 = pa.slot_dc_off[j], o1 = pa.slot_dc_off[j + 1];
+    sOff[sl] = o0 - dc0;
+    for (int i = o0; i < o1; ++i) {
+      const int cl = pa.slot_dc[i] - c0;
+      const int lo = pa.dc_lo[i];
+      const double g = 1.0 / sT[cl];
+      J0 += sIt[cl];
+      if (lo >= 0) {
+        sChild[i - dc0] = lo - js0;
+        sG[i - dc0] = g;
+      } else {
+        sChild[i - dc0] = -1;
+        D0 += g;
+      }
+    }
+    sD0[sl] = D0;
+    sJ0[sl] = J0;
+  }
+  if (threadIdx.x == 0) sOff[ns] = pa.slot_dc_off[js1] - dc0;
+  __syncthreads();
+  for (int lv = lv1 - 1; lv >= lv0; --lv) {  // phase B, deepest level first
+    for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kPcThreads) {
+      const int sl = j - js0;
+      double D = sD0[sl], J = sJ0[sl];
+      for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+        const int ch = sChild[i];
+        if (ch < 0) continue;
+        const double g = sG[i], Dc = sD[ch];
+        D += g * (1.0 - g / Dc);
+        J += g * sJ[ch] / Dc;
+      }
+      sD[sl] = D;
+      sJ[sl] = J;
+    }
+    __syncthreads();
+  }
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
+    const int j = js0 + sl;
+    const int pcn = pa.slot_pchain[j];
+    const double D = sD[sl], J = sJ[sl];
+    pa.slot_D[j] = D;
+    pa.slot_J[j] = J;
+    pa.slot_A[j] = J / D;
+    pa.slot_B[j] = pcn >= 0 ? 1.0 / (sT[pcn - c0] * D) : 0.0;
+  }
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* __restrict__ y,
+                                                            const double* __restrict__ r2,
+                                                            double* __restrict__ z,
+                                                            const MrState* __restrict__ st,
+                                                            const double* __restrict__ partA,
+                                                            int nA, const double* __restrict__ red,
+                                                            double* __restrict__ partB, int mode) {
+  __shared__ double sD0[kCapT], sJ0[kCapT], sD[kCapT], sJ[kCapT], sGp[kCapT], sY[kCapT];
+  __shared__ int sPar[kCapT], sLam[kCapT];
+  __shared__ int sOff[kCapT + 1];
+  __shared__ int sChild[kCapTDC];
+  __shared__ double sG[kCapTDC], sDD[kCapTDC], sDJ[kCapTDC];
+  __shared__ int sLv[kMaxTopLvl + 1];
+  double c2 = 0.0;
+  if (mode == 0) {
+    if (st->done) return;
+    const double alfa = MULTI ? red[0] : block_allsum<kTopThreads>(partA, nA);
+    c2 = alfa / st->beta;
+  }
+  const int nl = pa.n_top_lvl;
+  const int ts0 = pa.top_lvl_off[0], ts1 = pa.top_lvl_off[nl];
+  const int nt = ts1 - ts0;
+  const int dc0 = nt > 0 ? pa.slot_dc_off[ts0] : 0;
+  const int ndc = nt > 0 ? pa.slot_dc_off[ts1] - dc0 : 0;
+  for (int i = threadIdx.x; i <= nl; i += kTopThreads) sLv[i] = pa.top_lvl_off[i];
+  // phase A1, one thread per hanging chain: its conductance, its top current and, for a
+  // lower-job root below it (final Norton pair) or ground, its whole contribution
+  for (int i = threadIdx.x; i < ndc; i += kTopThreads) {
+    const int c = pa.slot_dc[dc0 + i];
+    const int lo = pa.dc_lo[dc0 + i];
+    const double g = 1.0 / pa.chain_T[c];
+    const double it = pa.chain_It[c];
+    int child = -1;
+    double dD = 0.0, dJ = it;
+    if (lo >= ts0 && lo < ts1) {  // child above the cut: solved in the level sweep
+      child = lo - ts0;
+    } else if (lo >= 0) {
+      const double Dl = pa.slot_D[lo];
+      dD = g * (1.0 - g / Dl);
+      dJ += g * pa.slot_J[lo] / Dl;
+    } else {
+      dD = g;
+    }
+    sChild[i] = child;
+    sG[i] = g;
+    sDD[i] = dD;
+    sDJ[i] = dJ;
+  }
+  // phase A2, one thread per junction: own data + parent chain
+  for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
+    const int j = ts0 + sl;
+    const int lam = pa.slot_lam[j];
+    double yl = y[lam];
+    if (mode == 0) {
+      yl -= c2 * r2[lam];
+      y[lam] = yl;
+    }
+    sLam[sl] = lam;
+    sY[sl] = yl;
+    const int pcn = pa.slot_pchain[j];
+    const double gp = pcn >= 0 ? 1.0 / pa.chain_T[pcn] : 0.0;
+    sD0[sl] = gp;
+    sJ0[sl] = yl + (pcn >= 0 ? pa.chain_Ib[pcn] : 0.0);
+    const int par = pa.slot_parent[j];
+    sPar[sl] = par >= 0 ? par - ts0 : -1;
+    sGp[sl] = gp;
+    sOff[sl] = pa.slot_dc_off[j] - dc0;
+  }
+  if (threadIdx.x == 0) sOff[nt] = ndc;
+  __syncthreads();
+  for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {  // phase A3: fold the fixed parts
+    double D0 = sD0[sl], J0 = sJ0[sl];
+    for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+      D0 += sDD[i];
+      J0 += sDJ[i];
+    }
+    sD0[sl] = D0;
+    sJ0[sl] = J0;
+  }
+  __syncthreads();
+  for (int lv = nl - 1; lv >= 0; --lv) {
+    for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
+      const int sl = j - ts0;
+      double D = sD0[sl], J = sJ0[sl];
+      for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+        const int ch = sChild[i];
+        if (ch < 0) continue;
+        const double g = sG[i], Dc = sD[ch];
+        D += g * (1.0 - g / Dc);
+        J += g * sJ[ch] / Dc;
+      }
+      sD[sl] = D;
+      sJ[sl] = J;
+    }
+    __syncthreads();
+  }
+  double part = 0.0;
+  for (int lv = 0; lv < nl; ++lv) {  // root level first: z_j = (J_j + g_par z_par) / D_j
+    for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
+      const int sl = j - ts0;
+      const int p = sPar[sl];
+      const double zj = (sJ[sl] + (p >= 0 ? sGp[sl] * sJ0[p] : 0.0)) / sD[sl];
+      sJ0[sl] = zj;  // reuse: z of top slots
+      z[sLam[sl]] = zj;
+      part += sY[sl] * zj;
+    }
+    __syncthreads();
+  }
+  for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {  // lower-job roots read these
+    pa.slot_D[ts0 + sl] = sD[sl];
+    pa.slot_J[ts0 + sl] = sJ[sl];
+  }
+  block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
+}
+
+template <bool MULTI, int W, int CPL>
+__global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
+                                                            const double* __restrict__ y,
+                                                            double* __restrict__ z,
+                                                            const MrState* __restrict__ st,
+                                                            double* __restrict__ partB, int mode) {
+  __shared__ double sZ[kCapS], sA[kCapS], sB[kCapS];
+  __shared__ int sP[kCapS];
+  if (mode == 0 && st->done) return;
+  const int job = blockIdx.x;
+  double part = 0.0;
+  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
+  const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
+  const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
+  const int ns = js1 - js0;
+  // phase A: every slot's A, B, parent (local index, or the parent's z for the root)
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
+    const int j = js0 + sl;
+    const int p = pa.slot_parent[j];
+    const bool local = p >= js0 && p < js1;
+    sA[sl] = pa.slot_A[j];
+    sB[sl] = pa.slot_B[j];
+    sP[sl] = local ? p - js0 : -1;
+    const int plam = pa.slot_plam[j];
+    sZ[sl] = (!local && plam >= 0) ? z[plam] : 0.0;  // z of an outside parent (top part)
+  }
+  __syncthreads();
+  for (int lv = lv0; lv < lv1; ++lv) {  // phase B, root level first, LDS only
+    for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kPcThreads) {
+      const int sl = j - js0;
+      const int p = sP[sl];
+      sZ[sl] = sA[sl] + sB[sl] * (p >= 0 ? sZ[p] : sZ[sl]);
+    }
+    __syncthreads();
+  }
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
+    const int lam = pa.slot_lam[js0 + sl];
+    z[lam] = sZ[sl];
+    part += y[lam] * sZ[sl];
+  }
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W;
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    ChainLane<W, CPL> ch;
+    ch.setup(pa, c, active);
+    const int up = active ? pa.chain_up[c] : -1, lo = active ? pa.chain_lo[c] : -1;
+    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : z[pa.slot_lam[up]];
+    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : z[pa.slot_lam[lo]];
+    const double T = ch.T, iT = 1.0 / T;
+    double rc[CPL], a[CPL], b[CPL];
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      rc[t] = ch.valid[t] ? y[ch.dof_c[t]] : 0.0;
+      a[t] = (T - ch.D[t]) * rc[t];
+      b[t] = ch.D[t] * rc[t];
+      sa += a[t];
+      sb += b[t];
+    }
+    const double ia = seg_incl_scan<W>(sa), ib = seg_incl_scan<W>(sb);
+    const double Atot = seg_sum<W>(sa);
+    double pa_ = ia - sa, pb_ = ib - sb;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      pa_ += a[t];
+      const double suffix = Atot - pa_ + a[t];
+      const double prefix = pb_;
+      pb_ += b[t];
+      if (!ch.valid[t]) continue;
+      const double Dk = ch.D[t];
+      const double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      z[ch.dof_c[t]] = zk;
+      part += rc[t] * zk;
+      const double rq = y[ch.dof_q[t]];
+      const double zq = rq / ch.rho[t];
+      z[ch.dof_q[t]] = zq;
+      part += rq * zq;
+    }
+    if (ch.has_last) {
+      const double rq = y[ch.dof_qN];
+      const double zq = rq / ch.rhoN;
+      z[ch.dof_qN] = zq;
+      part += rq * zq;
+    }
+  }
+  block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
+}
+
 __global__ void k_pack(const double* __restrict__ x, const int* __restrict__ idx, int n,
                        double* __restrict__ buf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -969,6 +1318,7 @@ struct nx_network {
   MrState* st = nullptr;               // 2 buffers (ping-pong)
   // tree Schur preconditioner (nx_set_preconditioner)
   bool pc = false;
+  bool pc_lds = false;  // every job fits the LDS kernels' caps
   int pc_variant = 0;   // (W, CPL) instantiation
   int pc_jobs = 0;
   PcArgs pa{};
@@ -1049,6 +1399,17 @@ int allreduce_slot(nx_network* h, int slot) {
 template <bool MULTI, int W, int CPL>
 void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other,
                   int mode) {
+  if (h->pc_lds) {
+    if (h->pc_jobs > 0)
+      hipLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
+                         h->stream, h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
+    hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y,
+                       r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
+    if (h->pc_jobs > 0)
+      hipLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
+                         h->stream, h->pa, y, h->z, st, h->partB, mode);
+    return;
+  }
   if (h->pc_jobs > 0)
     hipLaunchKernelGGL((k_pc_up<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
                        h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
@@ -1578,7 +1939,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
                                  const int32_t* chain_up, const int32_t* chain_lo, int64_t n_slots,
                                  const int32_t* slot_lam, const int32_t* slot_pchain,
                                  const int32_t* slot_parent, const int32_t* slot_dc_off,
-                                 const int32_t* slot_dc, int32_t n_jobs,
+                                 const int32_t* slot_dc, const int32_t* dc_lo,
+                                 const int32_t* slot_plam, int32_t n_jobs,
                                  const int32_t* job_chain_off, const int32_t* job_lvl_off,
                                  int32_t n_lvl, const int32_t* lvl_slot_off, int32_t n_top_lvl,
                                  const int32_t* top_lvl_off) {
@@ -1618,6 +1980,9 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
         slot_parent[j] >= n_slots)
       return fail(NX_ERR_ARG, "slot parent out of range");
   }
+  for (int64_t i = 0; i < (n_slots > 0 ? slot_dc_off[n_slots] : 0); ++i)
+    if (slot_dc[i] < 0 || slot_dc[i] >= n_chains || dc_lo[i] != chain_lo[slot_dc[i]])
+      return fail(NX_ERR_ARG, "slot_dc / dc_lo inconsistent");
   if (job_chain_off[0] != 0 || job_chain_off[n_jobs] != n_chains)
     return fail(NX_ERR_ARG, "job_chain_off must cover all chains");
   if (job_lvl_off[n_jobs] != n_lvl) return fail(NX_ERR_ARG, "job_lvl_off must end at n_lvl");
@@ -1652,6 +2017,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.slot_parent = up(slot_parent, n_slots);
   pa.slot_dc_off = up(slot_dc_off, n_slots + 1);
   pa.slot_dc = up(slot_dc, slot_dc_off[n_slots]);
+  pa.dc_lo = up(dc_lo, slot_dc_off[n_slots]);
+  pa.slot_plam = up(slot_plam, n_slots);
   pa.job_chain_off = up(job_chain_off, n_jobs + 1);
   pa.job_lvl_off = up(job_lvl_off, n_jobs + 1);
   pa.lvl_slot_off = up(lvl_slot_off, n_lvl + 1);
@@ -1664,13 +2031,16 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.chain_Ib = scratch(n_chains);
   pa.slot_D = scratch(n_slots);
   pa.slot_J = scratch(n_slots);
+  pa.slot_A = scratch(n_slots);
+  pa.slot_B = scratch(n_slots);
   for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
                         (const void*)pa.chain_lo, (const void*)pa.slot_lam, (const void*)pa.slot_pchain,
                         (const void*)pa.slot_parent, (const void*)pa.slot_dc_off, (const void*)pa.slot_dc,
                         (const void*)pa.job_chain_off, (const void*)pa.job_lvl_off,
                         (const void*)pa.lvl_slot_off, (const void*)pa.top_lvl_off,
                         (const void*)pa.chain_T, (const void*)pa.chain_It, (const void*)pa.chain_Ib,
-                        (const void*)pa.slot_D, (const void*)pa.slot_J})
+                        (const void*)pa.slot_D, (const void*)pa.slot_J, (const void*)pa.dc_lo,
+                        (const void*)pa.slot_plam, (const void*)pa.slot_A, (const void*)pa.slot_B})
     if (p == nullptr) return fail(NX_ERR_HIP, "preconditioner upload failed");
   if (!h->z) CHECK(dalloc(&h->z, std::max<int64_t>(h->n_col, 1)));
   if (!h->vv) CHECK(dalloc(&h->vv, std::max<int64_t>(h->n_own, 1)));
@@ -1681,6 +2051,19 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     h->nB = n_jobs + 1;
     CHECK(dalloc(&h->partB, h->nB));
   }
+  // LDS kernels when every job (and the top part) fits their caps
+  bool lds = (top_lvl_off[n_top_lvl] - top_lvl_off[0]) <= kCapT && n_top_lvl <= kMaxTopLvl;
+  if (lds && n_top_lvl > 0 && top_lvl_off[n_top_lvl] > top_lvl_off[0])
+    lds = slot_dc_off[top_lvl_off[n_top_lvl]] - slot_dc_off[top_lvl_off[0]] <= kCapTDC;
+  for (int j = 0; lds && j < n_jobs; ++j) {
+    if (job_chain_off[j + 1] - job_chain_off[j] > kCapC) lds = false;
+    if (job_lvl_off[j + 1] > job_lvl_off[j]) {
+      const int a = lvl_slot_off[job_lvl_off[j]], b = lvl_slot_off[job_lvl_off[j + 1]];
+      if (b - a > kCapS || slot_dc_off[b] - slot_dc_off[a] > kCapDC) lds = false;
+    }
+  }
+  if (const char* e = std::getenv("NXHIP_PC_GLOBAL")) lds = lds && std::atoi(e) == 0;
+  h->pc_lds = lds;
   h->pa = pa;
   h->pc_jobs = n_jobs;
   h->pc_variant = variant;

@@ -60,6 +60,8 @@ class TreePreconditioner:
     slot_parent: np.ndarray  # parent slot, -1
     slot_dc_off: np.ndarray  # CSR over chains whose top end is the slot
     slot_dc: np.ndarray
+    dc_lo: np.ndarray  # bottom slot of every slot_dc entry (-1 = ground), precomputed
+    slot_plam: np.ndarray  # multiplier row of the parent slot, -1
     # jobs: lower subtrees first (chains + junction levels), then chain-only jobs
     job_chain_off: np.ndarray  # n_jobs + 1
     job_lvl_off: np.ndarray  # n_jobs + 1, offsets into lvl_slot_off
@@ -75,7 +77,7 @@ class TreePreconditioner:
 
 
 def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
-                              target_jobs: int = 512, max_top: int = 1024) -> TreePreconditioner:
+                              target_jobs: int = 256, max_top: int = 1024) -> TreePreconditioner:
     """Decompose the rank-local problem ``lp`` (:class:`layout.LocalProblem`).
 
     ``src``/``dst`` are the global node ids of all edges, ``degree`` the global degrees.
@@ -232,10 +234,13 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     slot_dc_off = np.zeros(n_slots + 1, dtype=np.int32)
     np.cumsum([len(d) for d in down], out=slot_dc_off[1:])
     slot_dc = np.array([c for d in down for c in d], dtype=np.int32)
+    dc_lo = c_lo[slot_dc] if slot_dc.size else np.zeros(0, np.int32)
+    slot_plam = np.where(slot_parent >= 0, slot_lam[np.maximum(slot_parent, 0)], -1).astype(np.int32)
     return TreePreconditioner(
         N=N, chain_edge=order.astype(np.int32), chain_flip=flip[order].astype(np.int32),
         chain_up=c_up, chain_lo=c_lo, slot_lam=slot_lam, slot_pchain=slot_pchain,
         slot_parent=slot_parent, slot_dc_off=slot_dc_off, slot_dc=slot_dc,
+        dc_lo=dc_lo.astype(np.int32), slot_plam=slot_plam,
         job_chain_off=job_chain_off, job_lvl_off=np.asarray(job_lvl_off, dtype=np.int32),
         lvl_slot_off=np.asarray(lvl_slot_off, dtype=np.int32),
         top_lvl_off=np.asarray(top_lvl_off, dtype=np.int32), n_jobs=int(n_jobs),

@@ -272,3 +272,20 @@ def test_solver_pc_option():
     pre = Solver(asm)  # reference default options (pc_type lu) -> tree preconditioner
     pre.solve()
     assert pre.ksp.getIterationNumber() < it_plain / 5
+
+
+@pytest.mark.parametrize("path", ["lds", "global"])
+@pytest.mark.parametrize("case", ["depth6_N40", "edge_info_N10", "demo_tree_N1"])
+def test_preconditioner_kernel_paths(case, path, monkeypatch):
+    """The LDS preconditioner kernels and the global-memory fallback give the same
+    iterates (up to rounding) and both reach the direct solution."""
+    if path == "global":
+        monkeypatch.setenv("NXHIP_PC_GLOBAL", "1")
+    mesh, asm, P, A, b, pbc = _build(case)
+    asm.assemble()
+    it, rr, conv = asm.handle.solve(1e-12, 20000, 32)
+    assert conv
+    x_ref = O.solve_reference(A, b)
+    _, _, perm, _ = O.to_build_layout(P, A, b)
+    x = asm.handle.solution()
+    assert np.linalg.norm(x - x_ref[perm]) / np.linalg.norm(x_ref) <= SOL_TOL
