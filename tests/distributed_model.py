@@ -107,3 +107,49 @@ def minres(A_local, b_local, n_own: int, halo, allreduce, rtol=1e-12, maxit=5000
     wn = (vk - pend[0] * w1 - pend[1] * w2) * pend[2]
     x += pend[3] * wn
     return x, it, relres
+
+
+def minres_pc(A_local, b_local, n_own: int, halo, allreduce, apply_pc, rtol=1e-12, maxit=5000):
+    """Preconditioned MINRES (scipy's statement order) with a rank-local SPD
+    preconditioner ``apply_pc(r_owned) -> z_owned``; ``halo`` fills ghost slots of the
+    gathered vector (z), as the device does before each SpMV."""
+    n_col = A_local.shape[1]
+    r1 = b_local.copy()
+    r2 = b_local.copy()
+    z = np.zeros(n_col)
+    z[:n_own] = apply_pc(r1)
+    beta1 = np.sqrt(allreduce(float(r1 @ z[:n_own])))
+    x = np.zeros(n_own)
+    w = np.zeros(n_own)
+    w2 = np.zeros(n_own)
+    oldb, beta, dbar, epsln, phibar, cs, sn = 0.0, beta1, 0.0, 0.0, beta1, -1.0, 0.0
+    it = 0
+    while it < maxit:
+        it += 1
+        s = 1.0 / beta
+        halo(z)
+        v = s * z[:n_own]
+        y = s * (A_local @ z)
+        if it >= 2:
+            y = y - (beta / oldb) * r1
+        alfa = allreduce(float(v @ y))
+        y = y - (alfa / beta) * r2
+        r1, r2 = r2, y
+        z = np.zeros(n_col)
+        z[:n_own] = apply_pc(r2)
+        oldb, beta = beta, np.sqrt(allreduce(float(r2 @ z[:n_own])))
+        oldeps = epsln
+        delta = cs * dbar + sn * alfa
+        gbar = sn * dbar - cs * alfa
+        epsln = sn * beta
+        dbar = -cs * beta
+        gamma = max(np.hypot(gbar, beta), 2.220446049250313e-16)
+        cs, sn = gbar / gamma, beta / gamma
+        phi = cs * phibar
+        phibar = sn * phibar
+        w1, w2 = w2, w
+        w = (v - oldeps * w1 - delta * w2) / gamma
+        x = x + phi * w
+        if phibar / beta1 <= rtol:
+            break
+    return x, it, phibar / beta1
