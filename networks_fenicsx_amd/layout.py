@@ -100,6 +100,9 @@ class LocalProblem:
     recv_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
     # global single-rank layout index of every ghost column (diagnostics / tests)
     ghost_global: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    # owning rank of every global edge (the partition; the preconditioner's coarse step
+    # needs the whole map)
+    edge_owner: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
 
     @property
     def n_edge_dofs(self) -> int:
@@ -239,6 +242,7 @@ def build_local_problem(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degre
     lp.ghost_global = np.asarray(
         [E * per + bif_idx[k[1]] if k[0] == "lm" else k[1] * per + (2 * N if k[2] else 0)
          for k in gkeys], dtype=np.int64)
+    lp.edge_owner = owner
     if nranks > 1:
         # receive plan: my ghosts grouped by owner
         peers_recv = sorted(set(gowner))

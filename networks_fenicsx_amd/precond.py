@@ -30,20 +30,157 @@ junction levels) number a few hundred and the *top* part (all junctions above th
 one workgroup, junction math only) stays small; chains whose lower end is in the top part
 are processed by extra chain-only jobs in the same kernels.
 
-Graphs that are not trees, and ranks of a partitioned problem, use the same machinery on
-a spanning forest: a chain that would close a cycle, or whose far end is a junction owned
-by another rank, is grounded at that end. ``P`` stays SPD (a grounded Laplacian block);
+Graphs that are not trees use the same machinery on a spanning forest: a chain that
+would close a cycle is grounded at one end. ``P`` stays SPD (a grounded Laplacian block);
 only its quality drops.
+
+Partitioned problems keep ``P^{-1}`` exact through a *coarse step*. The coarse set ``C``
+holds every interface junction (edges of two or more ranks meet there) and, per rank,
+the junctions on paths between its interface junctions (Steiner closure). Each rank roots
+its local forest at its coarse junctions -- owned or ghost -- so every non-coarse piece
+hangs from exactly one coarse junction and eliminates into it independently. The ranks'
+partial ``(D, J)`` of the coarse junctions and the conductances of the chains joining two
+coarse junctions are summed in one all-reduce; the result is the Schur complement of ``S``
+on ``C``, again a tree Laplacian, which every rank solves redundantly (same order, same
+bits). The back-substitution then starts from exact coarse values. Without the coarse
+step (cut junctions grounded per rank) MINRES needs 5x the iterations at 8 ranks.
 """
 
 from __future__ import annotations
 
 from collections import deque
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
-__all__ = ["TreePreconditioner", "build_tree_preconditioner", "apply_model"]
+__all__ = ["CoarseStructure", "TreePreconditioner", "build_tree_preconditioner",
+           "coarse_structure", "apply_model", "pc_up_model", "pc_finish_model"]
+
+_EMPTY_I = np.zeros(0, dtype=np.int32)
+
+
+@dataclass
+class CoarseStructure:
+    """Global coarse forest of a partitioned problem (identical on every rank)."""
+
+    node: np.ndarray  # (nC,) global node id of every coarse junction, level order
+    cidx: np.ndarray  # (n_nodes,) coarse index of a node, -1
+    parent: np.ndarray  # (nC,) parent coarse index, -1 at a root
+    pedge: np.ndarray  # (nC,) global edge joining the junction to its parent, -1
+    child_off: np.ndarray  # (nC + 1,) CSR of children
+    child: np.ndarray
+    lvl_off: np.ndarray  # level offsets, root level first
+    demoted: np.ndarray  # (E,) bool: coarse-coarse edge closing a cycle (grounded at one end)
+
+    @property
+    def n(self) -> int:
+        return int(self.node.size)
+
+
+def coarse_structure(src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
+                     owner: np.ndarray, nranks: int) -> CoarseStructure:
+    """Interface junctions + per-rank Steiner closure, as a level-ordered forest."""
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    n_nodes, E = int(np.asarray(degree).size), int(src.size)
+    is_bif = np.asarray(degree) > 1
+    coarse = np.zeros(n_nodes, dtype=bool)
+    if nranks > 1 and E > 0:
+        owner = np.asarray(owner, dtype=np.int64)
+        ends = np.concatenate([src, dst])
+        eo = np.concatenate([owner, owner])
+        m = is_bif[ends]
+        mn = np.full(n_nodes, nranks, dtype=np.int64)
+        mx = np.full(n_nodes, -1, dtype=np.int64)
+        np.minimum.at(mn, ends[m], eo[m])
+        np.maximum.at(mx, ends[m], eo[m])
+        terminal = is_bif & (mx > mn)
+        coarse |= terminal
+        order = np.argsort(owner, kind="stable")
+        bounds = np.searchsorted(owner[order], np.arange(nranks + 1))
+        for r in range(nranks):
+            er = order[bounds[r]:bounds[r + 1]]
+            if er.size == 0:
+                continue
+            nodes, inv = np.unique(np.concatenate([src[er], dst[er]]), return_inverse=True)
+            a, b = inv[:er.size], inv[er.size:]
+            k = nodes.size
+            deg = np.bincount(a, minlength=k) + np.bincount(b, minlength=k)
+            inc_v = np.concatenate([a, b])
+            inc_e = np.concatenate([np.arange(er.size), np.arange(er.size)])
+            o = np.argsort(inc_v, kind="stable")
+            inc_e = inc_e[o]
+            off = np.searchsorted(inc_v[o], np.arange(k + 1))
+            alive = np.ones(er.size, dtype=bool)
+            term = terminal[nodes]
+            # prune non-terminal leaves: what stays is the Steiner forest of the terminals
+            stack = np.flatnonzero((deg == 1) & ~term).tolist()
+            while stack:
+                v = stack.pop()
+                if deg[v] != 1:
+                    continue
+                for i in range(off[v], off[v + 1]):
+                    e = inc_e[i]
+                    if alive[e]:
+                        break
+                alive[e] = False
+                deg[v] = 0
+                w = a[e] if b[e] == v else b[e]
+                deg[w] -= 1
+                if deg[w] == 1 and not term[w]:
+                    stack.append(w)
+            keep = (deg > 0) & is_bif[nodes]
+            coarse[nodes[keep]] = True
+    cn = np.flatnonzero(coarse)
+    demoted = np.zeros(E, dtype=bool)
+    adj: dict[int, list[tuple[int, int]]] = {int(v): [] for v in cn}
+    for e in np.flatnonzero(coarse[src] & coarse[dst]).tolist():
+        a, b = int(src[e]), int(dst[e])
+        adj[a].append((e, b))
+        adj[b].append((e, a))
+    depth: dict[int, int] = {}
+    par: dict[int, int] = {}
+    pe: dict[int, int] = {}
+    disc: list[int] = []
+    tree = set()
+    for r in cn.tolist():
+        if r in depth:
+            continue
+        depth[r], par[r], pe[r] = 0, -1, -1
+        disc.append(r)
+        q = deque([r])
+        while q:
+            u = q.popleft()
+            for e, w in adj[u]:
+                if w not in depth:
+                    depth[w], par[w], pe[w] = depth[u] + 1, u, e
+                    tree.add(e)
+                    disc.append(w)
+                    q.append(w)
+    for v in cn.tolist():
+        for e, _ in adj[v]:
+            if e not in tree:
+                demoted[e] = True
+    pos = {v: i for i, v in enumerate(disc)}
+    lvl = sorted(disc, key=lambda v: (depth[v], pos[v]))
+    cidx = np.full(n_nodes, -1, dtype=np.int32)
+    cidx[np.asarray(lvl, dtype=np.int64)] = np.arange(len(lvl), dtype=np.int32)
+    nC = len(lvl)
+    parent = np.array([cidx[par[v]] if par[v] != -1 else -1 for v in lvl], dtype=np.int32)
+    pedge = np.array([pe[v] for v in lvl], dtype=np.int64)
+    kids: list[list[int]] = [[] for _ in range(nC)]
+    for i in range(nC):
+        if parent[i] >= 0:
+            kids[parent[i]].append(i)
+    child_off = np.zeros(nC + 1, dtype=np.int32)
+    np.cumsum([len(k) for k in kids], out=child_off[1:])
+    child = np.array([c for k in kids for c in k], dtype=np.int32)
+    dl = np.array([depth[v] for v in lvl], dtype=np.int64)
+    nlv = int(dl.max()) + 1 if nC else 0
+    lvl_off = np.searchsorted(dl, np.arange(nlv + 1)).astype(np.int32)
+    return CoarseStructure(node=np.asarray(lvl, dtype=np.int64), cidx=cidx, parent=parent,
+                           pedge=pedge, child_off=child_off, child=child, lvl_off=lvl_off,
+                           demoted=demoted)
 
 
 @dataclass
@@ -70,6 +207,18 @@ class TreePreconditioner:
     top_lvl_off: np.ndarray  # slot offsets of the top levels (root level first)
     n_jobs: int
     n_slots: int
+    # coarse step (several ranks): coarse index of every slot (-1 = not coarse), the local
+    # chains joining two coarse junctions (their top / bottom coarse index; the bottom one
+    # is the child in the coarse forest and indexes its conductance), the global forest
+    n_coarse: int = 0
+    slot_cidx: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    cc_chain: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    cc_top: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    cc_bot: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    c_parent: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    c_child_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
+    c_child: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    c_lvl_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
 
     @property
     def n_chains(self) -> int:
@@ -77,17 +226,29 @@ class TreePreconditioner:
 
 
 def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
-                              target_jobs: int = 256, max_top: int = 1024) -> TreePreconditioner:
+                              target_jobs: int = 256, max_top: int = 1024,
+                              coarse: CoarseStructure | None = None) -> TreePreconditioner:
     """Decompose the rank-local problem ``lp`` (:class:`layout.LocalProblem`).
 
     ``src``/``dst`` are the global node ids of all edges, ``degree`` the global degrees.
+    With several ranks the coarse forest is derived from ``lp.edge_owner`` unless given.
     """
     N = lp.N
     E = lp.edges.size
     es, ed = src[lp.edges], dst[lp.edges]
-    # owned junctions: node -> slot candidate
-    owned = {int(v): i for i, v in enumerate(lp.lm_nodes)}
+    if coarse is None and lp.nranks > 1:
+        coarse = coarse_structure(src, dst, degree, lp.edge_owner, lp.nranks)
+    is_c = (lambda v: coarse.cidx[v] >= 0) if coarse is not None else (lambda v: False)  # noqa: E731
+    # junction slots: owned multipliers + ghost junctions at the ends of local edges (the
+    # latter are interface junctions, hence coarse)
     lam_of = {int(v): lp.n_edge_dofs + i for i, v in enumerate(lp.lm_nodes)}
+    if lp.nranks > 1:
+        for j in range(E):
+            for end, v in ((0, int(es[j])), (1, int(ed[j]))):
+                col = int(lp.edge_lm[j, end])
+                if col >= lp.n_own and v not in lam_of:
+                    lam_of[v] = col
+    owned = lam_of
     is_j = lambda v: v in owned  # noqa: E731
     # junction adjacency through local edges
     adj: dict[int, list[tuple[int, int]]] = {v: [] for v in owned}
@@ -98,20 +259,26 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         if is_j(b):
             adj[b].append((e, a))
 
-    # spanning forest: BFS from junctions touching ground first (they become roots)
+    # spanning forest: coarse junctions are the roots (BFS never enters another coarse
+    # junction: a path between two would make its junctions coarse too); the rest from
+    # junctions touching ground first
     depth = {}
     parent_j = {}
     pchain = {}
     tree_edge = np.zeros(E, dtype=bool)
-    ground_touch = [v for v in lp.lm_nodes.tolist() if any(not is_j(w) for _, w in adj[v])]
-    order_roots = ground_touch + lp.lm_nodes.tolist()
-    for r in order_roots:
+    slot_nodes = sorted(owned)
+    croots = [v for v in slot_nodes if is_c(v)]
+    for r in croots:
+        depth[r], parent_j[r], pchain[r] = 0, -1, -1
+    ground_touch = [v for v in slot_nodes if any(not is_j(w) for _, w in adj[v])]
+    grown = set()
+    for r in croots + ground_touch + slot_nodes:
         r = int(r)
-        if r in depth:
+        if r in grown or (r in depth and not is_c(r)):
             continue
-        depth[r] = 0
-        parent_j[r] = -1
-        pchain[r] = -1
+        grown.add(r)
+        if r not in depth:
+            depth[r], parent_j[r], pchain[r] = 0, -1, -1
         q = deque([r])
         while q:
             u = q.popleft()
@@ -126,11 +293,20 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     # chain ends: top = parent side (junction or ground), bottom = other
     chain_up_node = np.full(E, -1, dtype=np.int64)
     chain_lo_node = np.full(E, -1, dtype=np.int64)
+    is_cc = np.zeros(E, dtype=bool)  # joins two coarse junctions (coarse step)
     flip = np.zeros(E, dtype=np.int8)
     for e in range(E):
         a, b = int(es[e]), int(ed[e])
         ja, jb = is_j(a), is_j(b)
-        if tree_edge[e]:
+        ge = int(lp.edges[e])
+        if is_c(a) and is_c(b):
+            if coarse.demoted[ge]:  # closes a cycle of the coarse graph: ground one end
+                up, lo = a, -1
+            else:  # coarse forest edge: top = parent end, bottom = child end
+                child = b if coarse.pedge[coarse.cidx[b]] == ge else a
+                up, lo = (a if child == b else b), child
+                is_cc[e] = True
+        elif tree_edge[e]:
             # the child is the endpoint whose parent chain is e
             if jb and pchain.get(b) == e:
                 up, lo = a, b
@@ -148,8 +324,8 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         chain_lo_node[e] = lo
         flip[e] = 1 if (up == b and up != -1) or (up == -1 and lo == a and lo != -1) else 0
 
-    # cut depth: lower subtrees rooted at depth L
-    dvals = np.array([depth[int(v)] for v in lp.lm_nodes], dtype=np.int64)
+    # cut depth: lower subtrees rooted at depth L (coarse junctions, depth 0, stay on top)
+    dvals = np.array([depth[int(v)] for v in slot_nodes], dtype=np.int64)
     maxd = int(dvals.max()) if dvals.size else -1
     counts = np.bincount(dvals, minlength=maxd + 1) if dvals.size else np.zeros(0, np.int64)
     L = maxd + 1  # default: everything in the top part
@@ -157,11 +333,11 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         if counts[cand] >= target_jobs or counts[:cand].sum() + counts[cand] > max_top:
             L = cand
             break
-    if dvals.size and counts[:L].sum() > max_top:
-        L = max(0, L)
+    if croots:
+        L = max(L, 1)
 
-    children: dict[int, list[int]] = {v: [] for v in owned}
-    for v in lp.lm_nodes.tolist():
+    children: dict[int, list[int]] = {v: [] for v in slot_nodes}
+    for v in slot_nodes:
         p = parent_j[v]
         if p != -1:
             children[p].append(v)
@@ -170,7 +346,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     slots: list[int] = []
     job_lvl_off = [0]
     lvl_slot_off = [0]
-    job_roots = [v for v in lp.lm_nodes.tolist() if depth[v] == L]
+    job_roots = [v for v in slot_nodes if depth[v] == L]
     for r in job_roots:
         level = [r]
         while level:
@@ -180,12 +356,10 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         job_lvl_off.append(len(lvl_slot_off) - 1)
     n_lower_slots = len(slots)
     top_lvl_off = [n_lower_slots]
-    for dlev in range(L):
-        level = [v for v in lp.lm_nodes.tolist() if depth[v] == dlev]
-        # keep siblings together (parents' order) for locality
-        slots.extend(level)
+    for dlev in range(min(L, maxd + 1)):
+        slots.extend(v for v in slot_nodes if depth[v] == dlev)
         top_lvl_off.append(len(slots))
-    assert len(slots) == len(lp.lm_nodes)
+    assert len(slots) == len(slot_nodes)
     slot_of = {v: i for i, v in enumerate(slots)}
 
     # chains: per lower job, the parent chains of its junctions + chains hanging from them
@@ -220,6 +394,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     to_slot = lambda v: slot_of[int(v)] if v != -1 else -1  # noqa: E731
     c_up = np.array([to_slot(chain_up_node[e]) for e in order], dtype=np.int32)
     c_lo = np.array([to_slot(chain_lo_node[e]) for e in order], dtype=np.int32)
+    cc = is_cc[order]
 
     n_slots = len(slots)
     slot_lam = np.array([lam_of[v] for v in slots], dtype=np.int32)
@@ -229,14 +404,14 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
                            dtype=np.int32)
     down = [[] for _ in range(n_slots)]
     for c in range(E):
-        if c_up[c] != -1:
+        if c_up[c] != -1 and not cc[c]:
             down[c_up[c]].append(c)
     slot_dc_off = np.zeros(n_slots + 1, dtype=np.int32)
     np.cumsum([len(d) for d in down], out=slot_dc_off[1:])
     slot_dc = np.array([c for d in down for c in d], dtype=np.int32)
     dc_lo = c_lo[slot_dc] if slot_dc.size else np.zeros(0, np.int32)
     slot_plam = np.where(slot_parent >= 0, slot_lam[np.maximum(slot_parent, 0)], -1).astype(np.int32)
-    return TreePreconditioner(
+    pc = TreePreconditioner(
         N=N, chain_edge=order.astype(np.int32), chain_flip=flip[order].astype(np.int32),
         chain_up=c_up, chain_lo=c_lo, slot_lam=slot_lam, slot_pchain=slot_pchain,
         slot_parent=slot_parent, slot_dc_off=slot_dc_off, slot_dc=slot_dc,
@@ -245,6 +420,19 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         lvl_slot_off=np.asarray(lvl_slot_off, dtype=np.int32),
         top_lvl_off=np.asarray(top_lvl_off, dtype=np.int32), n_jobs=int(n_jobs),
         n_slots=n_slots)
+    if coarse is not None and coarse.n > 0:
+        cid = coarse.cidx
+        pc.n_coarse = coarse.n
+        pc.slot_cidx = np.array([cid[v] for v in slots], dtype=np.int32)
+        ccs = np.flatnonzero(cc).astype(np.int32)
+        pc.cc_chain = ccs
+        pc.cc_top = pc.slot_cidx[c_up[ccs]] if ccs.size else _EMPTY_I
+        pc.cc_bot = pc.slot_cidx[c_lo[ccs]] if ccs.size else _EMPTY_I
+        pc.c_parent = coarse.parent
+        pc.c_child_off = coarse.child_off
+        pc.c_child = coarse.child
+        pc.c_lvl_off = coarse.lvl_off
+    return pc
 
 
 # ----------------------------------------------------------------------------- model
@@ -265,29 +453,40 @@ def lumped_mass(Ab, lp) -> np.ndarray:
 
 
 def apply_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray) -> np.ndarray:
-    """numpy model of the device application ``z = P^{-1} r`` (same decomposition)."""
+    """numpy model of the device application ``z = P^{-1} r`` on one rank (no coarse
+    exchange: with several ranks use :func:`pc_up_model` / :func:`pc_finish_model` around
+    a sum of the partials over ranks)."""
+    st = pc_up_model(pc, lp, dq, r)
+    return pc_finish_model(pc, lp, dq, st, st["partial"])
+
+
+def _chain_dofs(pc, dq, c):
     N, per = pc.N, 2 * pc.N + 1
-    z = np.zeros_like(r)
+    e = pc.chain_edge[c]
+    base = e * per
+    cells = base + 2 * np.arange(N) + 1
+    qs = base + 2 * np.arange(N + 1)
+    rho = dq[e].copy()
+    if pc.chain_flip[c]:
+        cells, qs, rho = cells[::-1], qs[::-1], rho[::-1]
+    return cells, qs, rho
+
+
+def pc_up_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray) -> dict:
+    """Chain condensation and junction elimination (k_pc_up + the top elimination);
+    returns the state and this rank's coarse partial ``[D | J | G]`` (length 3 nC)."""
+    N = pc.N
+    n_col = lp.n_own + lp.n_ghost
+    rr = np.zeros(n_col)
+    rr[:r.size] = r
     T = np.zeros(pc.n_chains)
     It = np.zeros(pc.n_chains)
     Ib = np.zeros(pc.n_chains)
-    Dc = np.zeros(pc.n_chains * N)
-
-    def chain_dofs(c):
-        e = pc.chain_edge[c]
-        base = e * per
-        cells = base + 2 * np.arange(N) + 1
-        qs = base + 2 * np.arange(N + 1)
-        rho = dq[e].copy()
-        if pc.chain_flip[c]:
-            cells, qs, rho = cells[::-1], qs[::-1], rho[::-1]
-        return cells, qs, rho
-
     for c in range(pc.n_chains):
-        cells, qs, rho = chain_dofs(c)
+        cells, qs, rho = _chain_dofs(pc, dq, c)
         Dk = np.cumsum(rho)[:N]
         T[c] = rho.sum()
-        rp = r[cells]
+        rp = rr[cells]
         It[c] = np.sum(rp * (T[c] - Dk)) / T[c]
         Ib[c] = np.sum(rp * Dk) / T[c]
     Dj = np.zeros(pc.n_slots)
@@ -296,7 +495,7 @@ def apply_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray) -> np
     def eliminate(j):
         pcn = pc.slot_pchain[j]
         D = 1.0 / T[pcn] if pcn >= 0 else 0.0
-        J = r[pc.slot_lam[j]] + (Ib[pcn] if pcn >= 0 else 0.0)
+        J = rr[pc.slot_lam[j]] + (Ib[pcn] if pcn >= 0 else 0.0)
         for c in pc.slot_dc[pc.slot_dc_off[j]:pc.slot_dc_off[j + 1]]:
             g = 1.0 / T[c]
             J += It[c]
@@ -318,16 +517,63 @@ def apply_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray) -> np
     for lv in range(tl.size - 2, -1, -1):
         for j in range(tl[lv], tl[lv + 1]):
             eliminate(j)
+    nC = pc.n_coarse
+    partial = np.zeros(3 * nC)
+    for j in np.flatnonzero(pc.slot_cidx >= 0) if nC else []:
+        k = pc.slot_cidx[j]
+        partial[k] += Dj[j]
+        partial[nC + k] += Jj[j]
+    for c, t, b in zip(pc.cc_chain, pc.cc_top, pc.cc_bot):
+        g = 1.0 / T[c]
+        partial[t] += g
+        partial[b] += g
+        partial[nC + t] += It[c]
+        partial[nC + b] += Ib[c]
+        partial[2 * nC + b] = g
+    return dict(r=rr, T=T, Dj=Dj, Jj=Jj, partial=partial)
+
+
+def coarse_solve_model(pc: TreePreconditioner, total: np.ndarray) -> np.ndarray:
+    """Tree elimination on the coarse forest from the summed partials (k_pc_coarse)."""
+    nC = pc.n_coarse
+    D = total[:nC].copy()
+    J = total[nC:2 * nC].copy()
+    G = total[2 * nC:3 * nC]
+    lo = pc.c_lvl_off
+    for lv in range(lo.size - 2, -1, -1):
+        for j in range(lo[lv], lo[lv + 1]):
+            for k in pc.c_child[pc.c_child_off[j]:pc.c_child_off[j + 1]]:
+                D[j] -= G[k] * G[k] / D[k]
+                J[j] += G[k] * J[k] / D[k]
+    zc = np.zeros(nC)
+    for lv in range(lo.size - 1):
+        for j in range(lo[lv], lo[lv + 1]):
+            p = pc.c_parent[j]
+            zc[j] = (J[j] + (G[j] * zc[p] if p >= 0 else 0.0)) / D[j]
+    return zc
+
+
+def pc_finish_model(pc: TreePreconditioner, lp, dq: np.ndarray, st: dict,
+                    total: np.ndarray) -> np.ndarray:
+    """Coarse solve, back-substitution and chain cells (k_pc_coarse / top + k_pc_down).
+    Returns z on the owned DoFs."""
+    N = pc.N
+    rr, T, Dj, Jj = st["r"], st["T"], st["Dj"], st["Jj"]
+    z = np.zeros_like(rr)
+    zc = coarse_solve_model(pc, total) if pc.n_coarse else np.zeros(0)
     zj = np.zeros(pc.n_slots)
 
     def back(j):
         p = pc.slot_parent[j]
-        if p < 0:
+        if pc.n_coarse and pc.slot_cidx[j] >= 0:
+            zj[j] = zc[pc.slot_cidx[j]]
+        elif p < 0:
             zj[j] = Jj[j] / Dj[j]
         else:
             zj[j] = (Jj[j] + zj[p] / T[pc.slot_pchain[j]]) / Dj[j]
         z[pc.slot_lam[j]] = zj[j]
 
+    tl = pc.top_lvl_off
     for lv in range(tl.size - 1):
         for j in range(tl[lv], tl[lv + 1]):
             back(j)
@@ -337,10 +583,10 @@ def apply_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray) -> np
             for j in range(pc.lvl_slot_off[lv], pc.lvl_slot_off[lv + 1]):
                 back(j)
     for c in range(pc.n_chains):
-        cells, qs, rho = chain_dofs(c)
+        cells, qs, rho = _chain_dofs(pc, dq, c)
         Dk = np.cumsum(rho)[:N]
         Tc = T[c]
-        rp = r[cells]
+        rp = rr[cells]
         zt = zj[pc.chain_up[c]] if pc.chain_up[c] >= 0 else 0.0
         zb = zj[pc.chain_lo[c]] if pc.chain_lo[c] >= 0 else 0.0
         a = (Tc - Dk) * rp  # suffix sums j >= k
@@ -348,5 +594,5 @@ def apply_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray) -> np
         b = Dk * rp  # prefix sums j < k
         pre = np.concatenate([[0.0], np.cumsum(b)[:-1]])
         z[cells] = zt * (Tc - Dk) / Tc + zb * Dk / Tc + (Dk / Tc) * suf + ((Tc - Dk) / Tc) * pre
-        z[qs] = r[qs] / rho
-    return z
+        z[qs] = rr[qs] / rho
+    return z[:lp.n_own]
