@@ -44,6 +44,7 @@ extern "C" {
 #define NX_UNIQUE_ID_BYTES 128
 
 typedef struct nx_network nx_network_t;
+typedef struct nx_group nx_group_t;
 
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int nx_version(void);
@@ -128,6 +129,8 @@ int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
  * kernels a dependent load). Jobs (one workgroup each):
  * chain ranges and level ranges; lvl_slot_off / top_lvl_off: slot offsets per level (root
  * level first) of the lower jobs / of the single top workgroup. Requires N <= 256.
+ * With several ranks the slots also cover the ghost junctions at the ends of local edges
+ * (slot_lam = their ghost column) and nx_set_coarse must follow.
  */
 int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
                           const int32_t* chain_edge, const int32_t* chain_flip,
@@ -138,6 +141,24 @@ int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
                           int32_t n_jobs, const int32_t* job_chain_off,
                           const int32_t* job_lvl_off, int32_t n_lvl, const int32_t* lvl_slot_off,
                           int32_t n_top_lvl, const int32_t* top_lvl_off);
+
+/*
+ * Coarse step of the preconditioner on a partitioned problem (precond.py derives it): the
+ * coarse junctions (interface junctions + the junctions on paths between them inside a
+ * rank) form a forest that every rank solves redundantly from one all-reduce of
+ * [D | J | G] (3 n_coarse doubles) per application, which keeps P^{-1} exact, i.e. the
+ * iteration count independent of the number of ranks.
+ *   slot_cidx[n_slots]        coarse index of every slot, -1 (coarse slots: top part)
+ *   cc_chain/cc_top/cc_bot    local chains joining two coarse junctions: chain, coarse
+ *                             index of its top / bottom end (the bottom is the child)
+ *   c_parent[n_coarse], c_child_off/c_child (CSR), c_lvl_off[n_clvl+1]: the global
+ *                             forest in level order (root level first)
+ * n_coarse = 0 disables the step. Call after nx_set_preconditioner.
+ */
+int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_cidx, int32_t n_cc,
+                  const int32_t* cc_chain, const int32_t* cc_top, const int32_t* cc_bot,
+                  const int32_t* c_parent, const int32_t* c_child_off, const int32_t* c_child,
+                  int32_t n_clvl, const int32_t* c_lvl_off);
 
 /* Copy the owned part of the solution / rhs to the host (n_rows doubles). */
 int nx_get_solution(nx_network_t* h, double* x);
@@ -177,11 +198,31 @@ int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
  *   peer_rank[n_peers]
  *   send_off[n_peers+1], send_idx[...]   owned local rows to send to each peer
  *   recv_off[n_peers+1]     ghost slots [recv_off[p], recv_off[p+1]) filled by peer p
+ * nx_set_halo records the plan only; nx_comm_init = nx_set_halo + the RCCL communicator.
+ * Both must precede nx_set_preconditioner.
  */
 int nx_comm_unique_id(unsigned char* id_out /* NX_UNIQUE_ID_BYTES */);
+int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_peers,
+                const int32_t* peer_rank, const int32_t* send_off, const int32_t* send_idx,
+                const int32_t* recv_off);
 int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned char* id,
                  int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
                  const int32_t* send_idx, const int32_t* recv_off);
+
+/*
+ * In-process rank group: the ranks of a partitioned problem as handles on ONE device,
+ * driven in lock-step from one host thread, with the halo exchange as device copies and
+ * the all-reduces as a fixed-order device sum. Same kernels and schedule as the RCCL path,
+ * so a multi-rank solve can be checked on a single GPU (RCCL rejects two ranks on one
+ * device). Each handle h_r needs nx_set_halo(h_r, nranks, r, ...) first; the group lends
+ * the handles one shared stream until nx_group_destroy (which must precede nx_destroy).
+ * nx_group_solve = nx_solve over all ranks; fails with NX_ERR_STATE if the ranks' MINRES
+ * recurrences ever differ.
+ */
+int nx_group_create(int32_t nranks, nx_network_t* const* handles, nx_group_t** out);
+int nx_group_solve(nx_group_t* g, double rtol, int32_t maxit, int32_t check_every,
+                   int32_t* iters, double* relres, int32_t* converged);
+int nx_group_destroy(nx_group_t* g);
 
 #ifdef __cplusplus
 }

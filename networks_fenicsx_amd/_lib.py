@@ -13,7 +13,7 @@ from pathlib import Path
 
 import numpy as np
 
-__all__ = ["lib", "NxError", "NxNotConverged", "check", "Handle", "EXPORTED_SYMBOLS"]
+__all__ = ["lib", "NxError", "NxNotConverged", "check", "Handle", "Group", "EXPORTED_SYMBOLS"]
 
 _LIB_PATH = Path(__file__).resolve().parent / "libnxhip.so"
 _lock = threading.Lock()
@@ -56,6 +56,12 @@ _SIGS = {
                                         _pi32, _i32, _pi32, _i32, _pi32]),
     "nx_comm_unique_id": (C.c_int, [_pu8]),
     "nx_comm_init": (C.c_int, [_h, _i32, _i32, _pu8, _i32, _pi32, _pi32, _pi32, _pi32]),
+    "nx_set_coarse": (C.c_int, [_h, _i32, _pi32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
+                                _i32, _pi32]),
+    "nx_set_halo": (C.c_int, [_h, _i32, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
+    "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
+    "nx_group_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
+    "nx_group_destroy": (C.c_int, [_h]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
@@ -247,6 +253,31 @@ class Handle:
             p["job_chain_off"], p["job_lvl_off"],
             int(pc.lvl_slot_off.size - 1), p["lvl_slot_off"], int(pc.top_lvl_off.size - 1),
             p["top_lvl_off"]))
+        nC = int(getattr(pc, "n_coarse", 0))
+        if nC:
+            ca = {k: np.ascontiguousarray(getattr(pc, k), dtype=np.int32) for k in (
+                "slot_cidx", "cc_chain", "cc_top", "cc_bot", "c_parent", "c_child_off",
+                "c_child", "c_lvl_off")}
+            ca = {k: (v if v.size else np.zeros(1, np.int32)) for k, v in ca.items()}
+            self._pc_keep_c = ca
+            q = {k: _ptr(v, C.c_int32) for k, v in ca.items()}
+            check(lib().nx_set_coarse(
+                self.ptr, nC, q["slot_cidx"], int(pc.cc_chain.size), q["cc_chain"], q["cc_top"],
+                q["cc_bot"], q["c_parent"], q["c_child_off"], q["c_child"],
+                int(pc.c_lvl_off.size - 1), q["c_lvl_off"]))
+
+    def set_halo(self, nranks: int, rank: int, peers, send_off, send_idx, recv_off):
+        """Halo plan without a transport (in-process group members)."""
+        peers = np.ascontiguousarray(peers, dtype=np.int32)
+        send_off = np.ascontiguousarray(send_off, dtype=np.int32)
+        send_idx = np.ascontiguousarray(send_idx, dtype=np.int32)
+        recv_off = np.ascontiguousarray(recv_off, dtype=np.int32)
+        check(lib().nx_set_halo(self.ptr, int(nranks), int(rank), int(peers.size),
+                                _ptr(peers if peers.size else np.zeros(1, np.int32), C.c_int32),
+                                _ptr(send_off, C.c_int32),
+                                _ptr(send_idx if send_idx.size else np.zeros(1, np.int32),
+                                     C.c_int32),
+                                _ptr(recv_off, C.c_int32)))
 
     def comm_init(self, nranks: int, rank: int, uid: bytes, peers, send_off, send_idx, recv_off):
         uid_arr = (C.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid)
@@ -259,6 +290,36 @@ class Handle:
                                  _ptr(send_idx if send_idx.size else np.zeros(1, np.int32),
                                       C.c_int32),
                                  _ptr(recv_off, C.c_int32)))
+
+
+class Group:
+    """In-process rank group (``nx_group_*``): handles of all ranks on one device."""
+
+    def __init__(self, handles):
+        self._handles = list(handles)  # keeps the handles alive while the group exists
+        arr = (_h * len(self._handles))(*[h.ptr for h in self._handles])
+        out = _h()
+        check(lib().nx_group_create(len(self._handles), arr, C.byref(out)))
+        self._g = out
+
+    def solve(self, rtol: float = 1e-12, maxit: int = 50000, check_every: int = 32):
+        it = C.c_int32(0)
+        rr = C.c_double(0.0)
+        conv = C.c_int32(0)
+        check(lib().nx_group_solve(self._g, float(rtol), int(maxit), int(check_every),
+                                   C.byref(it), C.byref(rr), C.byref(conv)))
+        return int(it.value), float(rr.value), bool(conv.value)
+
+    def close(self) -> None:
+        if getattr(self, "_g", None):
+            lib().nx_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
 
 def comm_unique_id() -> bytes:

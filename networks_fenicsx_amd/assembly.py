@@ -32,6 +32,7 @@ import typing
 import numpy as np
 
 from . import _lib
+from .comm import GroupRankComm
 from .fem import Constant, FunctionSpace
 from .layout import LocalProblem, build_local_problem
 from .mesh import NetworkMesh
@@ -176,9 +177,13 @@ class HydraulicNetworkAssembler:
 
     def _init_comm(self) -> None:
         comm = self._network_mesh.comm
+        lp = self._local
+        if isinstance(comm, GroupRankComm):  # in-process group: plan only (RankGroup)
+            self._handle.set_halo(self._nranks, self._rank, lp.peers, lp.send_off, lp.send_idx,
+                                  lp.recv_off)
+            return
         uid = _lib.comm_unique_id() if self._rank == 0 else None
         uid = comm.bcast(uid, root=0)
-        lp = self._local
         self._handle.comm_init(self._nranks, self._rank, uid, lp.peers, lp.send_off,
                                lp.send_idx, lp.recv_off)
 

@@ -14,7 +14,8 @@ from __future__ import annotations
 import operator
 from typing import Any
 
-__all__ = ["Comm", "SerialComm", "TorchComm", "COMM_WORLD", "SUM", "MAX", "MIN"]
+__all__ = ["Comm", "SerialComm", "TorchComm", "LocalGroup", "GroupRankComm", "COMM_WORLD",
+           "SUM", "MAX", "MIN"]
 
 SUM = "sum"
 MAX = "max"
@@ -111,6 +112,58 @@ class TorchComm(Comm):
 
     def barrier(self) -> None:
         self._dist.barrier(group=self._group)
+
+    Get_rank = lambda self: self.rank  # noqa: E731
+    Get_size = lambda self: self.size  # noqa: E731
+
+
+class LocalGroup:
+    """Ranks of a partitioned problem simulated inside ONE process on one device (the
+    in-process group transport of the HIP library, ``nx_group_create``). The host objects
+    of every rank are built one after the other, rank 0 first, from one thread."""
+
+    def __init__(self, size: int):
+        if size < 1:
+            raise ValueError("group size must be >= 1")
+        self.size = int(size)
+        self._store: dict[int, Any] = {}
+
+    def comm(self, rank: int) -> "GroupRankComm":
+        return GroupRankComm(self, rank)
+
+
+class GroupRankComm(Comm):
+    """Communicator of one rank of a :class:`LocalGroup`. ``bcast`` works when the root
+    rank's call comes first (rank-order construction); collectives that need every rank's
+    value at once cannot run from one thread and raise."""
+
+    def __init__(self, group: LocalGroup, rank: int):
+        if not 0 <= rank < group.size:
+            raise ValueError(f"rank {rank} outside group of {group.size}")
+        self.group = group
+        self.rank = int(rank)
+        self.size = group.size
+        self._calls = 0
+
+    def bcast(self, obj: Any, root: int = 0) -> Any:
+        k = self._calls
+        self._calls += 1
+        if self.rank == root:
+            self.group._store[k] = obj
+            return obj
+        if k not in self.group._store:
+            raise RuntimeError("in-process group: build the root rank's objects first")
+        return self.group._store[k]
+
+    def allreduce(self, value: Any, op: Any = None) -> Any:
+        raise NotImplementedError("in-process group ranks run one after the other; "
+                                  "reduce over the ranks' results on the host instead")
+
+    def allgather(self, obj: Any) -> list:
+        raise NotImplementedError("in-process group: gather the ranks' results on the host")
+
+    def barrier(self) -> None:
+        return None
 
     Get_rank = lambda self: self.rank  # noqa: E731
     Get_size = lambda self: self.size  # noqa: E731

@@ -653,7 +653,53 @@ struct PcArgs {
   double* slot_J;
   double* slot_A;  // back-substitution z_j = A_j + B_j z_parent (LDS kernels)
   double* slot_B;
+  // coarse step (several ranks, precond.py): coarse index of every slot, local chains
+  // joining two coarse junctions (top / bottom coarse index; the bottom one is the child
+  // and indexes the conductance), the global coarse forest, and the exchange buffer
+  // [D | J | G] (3 n_coarse doubles) that is all-reduced between the two halves
+  int n_coarse;
+  int n_cc;
+  int n_clvl;
+  const int* slot_cidx;
+  const int* cc_chain;
+  const int* cc_top;
+  const int* cc_bot;
+  const int* c_parent;
+  const int* c_child_off;
+  const int* c_child;
+  const int* c_lvl_off;
+  double* cbuf;
 };
+
+// This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
+// in the top part, level 0) and the chains joining two coarse junctions. sD/sJ are indexed
+// by top-part position. Ends with the buffer complete (one workgroup).
+template <int BS>
+__device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const double* sD,
+                                   const double* sJ) {
+  const int nC = pa.n_coarse;
+  for (int i = threadIdx.x; i < 3 * nC; i += BS) pa.cbuf[i] = 0.0;
+  __syncthreads();
+  for (int sl = threadIdx.x; sl < nt; sl += BS) {
+    const int k = pa.slot_cidx[ts0 + sl];
+    if (k >= 0) {
+      pa.cbuf[k] = sD[sl];
+      pa.cbuf[nC + k] = sJ[sl];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // few chains; serial keeps the sums in a fixed order
+    for (int i = 0; i < pa.n_cc; ++i) {
+      const int c = pa.cc_chain[i], t = pa.cc_top[i], b = pa.cc_bot[i];
+      const double g = 1.0 / pa.chain_T[c];
+      pa.cbuf[t] += g;
+      pa.cbuf[b] += g;
+      pa.cbuf[nC + t] += pa.chain_It[c];
+      pa.cbuf[nC + b] += pa.chain_Ib[c];
+      pa.cbuf[2 * nC + b] = g;
+    }
+  }
+}
 
 template <int W>
 __device__ __forceinline__ double seg_incl_scan(double v) {
@@ -849,6 +895,10 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top(PcArgs pa, double* __res
     for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads)
       pc_eliminate<kTopThreads>(pa, y, j);
     __syncthreads();
+  }
+  if (MULTI && pa.n_coarse > 0) {  // back-substitution after the exchange (k_pc_coarse)
+    pc_coarse_partials<kTopThreads>(pa, s0, s1 - s0, pa.slot_D + s0, pa.slot_J + s0);
+    return;
   }
   double part = 0.0;
   for (int lv = 0; lv < nl; ++lv) {
@@ -1159,6 +1209,14 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     }
     __syncthreads();
   }
+  if (MULTI && pa.n_coarse > 0) {  // back-substitution after the exchange (k_pc_coarse)
+    for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
+      pa.slot_D[ts0 + sl] = sD[sl];
+      pa.slot_J[ts0 + sl] = sJ[sl];
+    }
+    pc_coarse_partials<kTopThreads>(pa, ts0, nt, sD, sJ);
+    return;
+  }
   double part = 0.0;
   for (int lv = 0; lv < nl; ++lv) {  // root level first: z_j = (J_j + g_par z_par) / D_j
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
@@ -1269,10 +1327,86 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
 }
 
+// Second half of the top part with several ranks: solve the coarse forest from the
+// all-reduced [D | J | G] (every rank identically), then back-substitute the top part --
+// coarse slots take their coarse value -- and the partial r.z of the top slots.
+constexpr int kCapCoarse = 2048;
+
+__global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, const double* __restrict__ y,
+                                                           double* __restrict__ z,
+                                                           const MrState* __restrict__ st,
+                                                           double* __restrict__ partB, int mode) {
+  __shared__ double sD[kCapCoarse], sJ[kCapCoarse], sZ[kCapCoarse];
+  if (mode == 0 && st->done) return;
+  const int nC = pa.n_coarse;
+  const double* __restrict__ G = pa.cbuf + 2 * nC;
+  for (int i = threadIdx.x; i < nC; i += kTopThreads) {
+    sD[i] = pa.cbuf[i];
+    sJ[i] = pa.cbuf[nC + i];
+  }
+  __syncthreads();
+  for (int lv = pa.n_clvl - 1; lv >= 0; --lv) {  // deepest level first
+    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kTopThreads) {
+      double D = sD[j], J = sJ[j];
+      for (int i = pa.c_child_off[j]; i < pa.c_child_off[j + 1]; ++i) {
+        const int k = pa.c_child[i];
+        const double g = G[k], Dk = sD[k];
+        D -= g * g / Dk;
+        J += g * sJ[k] / Dk;
+      }
+      sD[j] = D;
+      sJ[j] = J;
+    }
+    __syncthreads();
+  }
+  for (int lv = 0; lv < pa.n_clvl; ++lv) {  // root level first
+    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kTopThreads) {
+      const int p = pa.c_parent[j];
+      sZ[j] = (sJ[j] + (p >= 0 ? G[j] * sZ[p] : 0.0)) / sD[j];
+    }
+    __syncthreads();
+  }
+  double part = 0.0;
+  for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
+    for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads) {
+      const int k = pa.slot_cidx[j];
+      const int lam = pa.slot_lam[j];
+      double zj;
+      if (k >= 0) {
+        zj = sZ[k];
+      } else {
+        const int p = pa.slot_parent[j];
+        double num = pa.slot_J[j];
+        if (p >= 0) num += z[pa.slot_lam[p]] / pa.chain_T[pa.slot_pchain[j]];
+        zj = num / pa.slot_D[j];
+      }
+      z[lam] = zj;
+      part += y[lam] * zj;  // ghost slots: y = 0
+    }
+    __syncthreads();
+  }
+  block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
+}
+
 __global__ void k_pack(const double* __restrict__ x, const int* __restrict__ idx, int n,
                        double* __restrict__ buf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) buf[i] = x[idx[i]];
+}
+
+// In-process group transport: sum n values over the ranks' buffers in rank order and
+// store the total in every buffer (the RCCL all-reduce of a group on one device).
+constexpr int kMaxGroup = 16;
+struct GroupPtrs {
+  double* p[kMaxGroup];
+};
+
+__global__ void k_group_sum(GroupPtrs g, int P, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int r = 0; r < P; ++r) s += g.p[r][i];
+    for (int r = 0; r < P; ++r) g.p[r][i] = s;
+  }
 }
 
 }  // namespace
@@ -1321,6 +1455,7 @@ struct nx_network {
   bool pc_lds = false;  // every job fits the LDS kernels' caps
   int pc_variant = 0;   // (W, CPL) instantiation
   int pc_jobs = 0;
+  int64_t pc_slots = 0;
   PcArgs pa{};
   std::vector<void*> pc_bufs;
   double* z = nullptr;  // P^{-1} r, n_col
@@ -1337,12 +1472,26 @@ struct nx_network {
   hipEvent_t ev[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> ev_pool;  // SpMV timing pairs inside one convergence chunk
   int prof_k = 0;
-  // multi-rank
+  // multi-rank: halo plan (nx_set_halo) and transport -- an RCCL communicator (one
+  // process per GPU) or membership of an in-process group (nx_group_create)
   ncclComm_t comm = nullptr;
+  nx_group* group = nullptr;
+  hipStream_t own_stream = nullptr;  // the handle's stream while it is lent to a group
   int nranks = 1, rank = 0;
+  bool have_plan = false;
   std::vector<int> peers, send_off, recv_off;
+  std::vector<int> peer_src_off;  // group: offset of my segment in each peer's send_buf
   int* send_idx = nullptr;
   double* send_buf = nullptr;
+};
+
+struct nx_group {
+  int P = 0;
+  std::vector<nx_network*> hs;
+  hipStream_t stream = nullptr;
+  hipGraphExec_t chunk_exec = nullptr;
+  hipGraph_t chunk_graph = nullptr;
+  int chunk_len = 0;
 };
 
 namespace {
@@ -1366,13 +1515,49 @@ int upload(T** p, const T* host, int64_t count, hipStream_t s) {
 
 Csr csr_of(const nx_network* h) { return Csr{h->rowptr, h->col, h->val, h->n_own}; }
 
-// halo: fill the ghost slots of vector `v` (n_col) from the owning ranks
-int halo(nx_network* h, double* v) {
-  if (h->comm == nullptr || h->peers.empty()) return NX_OK;
-  const int nsend = h->send_off.back();
-  if (nsend > 0)
-    hipLaunchKernelGGL(k_pack, dim3(grid_of(nsend, 256)), dim3(256), 0, h->stream, v,
-                       h->send_idx, nsend, h->send_buf);
+// ---- transport. A Team is the set of handles one host thread drives in lock-step: one
+// handle (single GPU, or one rank of an RCCL job) or all members of an in-process group
+// (several ranks on one device, sharing one stream; exchanges are device copies).
+struct Team {
+  nx_network* const* hs;
+  int P;
+  nx_group* g;
+};
+
+bool team_multi(const Team& t) { return t.g != nullptr || t.hs[0]->comm != nullptr; }
+
+enum VecSel { VS_Z, VS_R2, VS_X };
+double* vec_of(nx_network* h, VecSel s, int64_t k) {
+  return s == VS_Z ? h->z : s == VS_X ? h->x : h->vb[k & 1];
+}
+
+// fill the ghost slots of the selected vector (n_col) from the owning ranks
+int team_halo(const Team& t, VecSel sel, int64_t k) {
+  if (!team_multi(t)) return NX_OK;
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    const int nsend = h->send_off.back();
+    if (nsend > 0)
+      hipLaunchKernelGGL(k_pack, dim3(grid_of(nsend, 256)), dim3(256), 0, h->stream,
+                         vec_of(h, sel, k), h->send_idx, nsend, h->send_buf);
+  }
+  if (t.g) {
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      double* v = vec_of(h, sel, k);
+      for (size_t j = 0; j < h->peers.size(); ++j) {
+        const int cnt = h->recv_off[j + 1] - h->recv_off[j];
+        if (cnt > 0)
+          HIPCALL(hipMemcpyAsync(v + h->n_own + h->recv_off[j],
+                                 t.hs[h->peers[j]]->send_buf + h->peer_src_off[j],
+                                 sizeof(double) * cnt, hipMemcpyDeviceToDevice, h->stream));
+      }
+    }
+    return NX_OK;
+  }
+  nx_network* h = t.hs[0];
+  if (h->peers.empty()) return NX_OK;
+  double* v = vec_of(h, sel, k);
   NCCLCALL(ncclGroupStart());
   for (size_t p = 0; p < h->peers.size(); ++p) {
     const int sc = h->send_off[p + 1] - h->send_off[p];
@@ -1388,120 +1573,195 @@ int halo(nx_network* h, double* v) {
   return NX_OK;
 }
 
-int allreduce_slot(nx_network* h, int slot) {
-  NCCLCALL(ncclAllReduce(h->red + slot, h->red + slot, 1, ncclDouble, ncclSum, h->comm,
+// sum-all-reduce of n doubles: red + slot (slot 0..3) or the coarse buffer (slot -1)
+double* xbuf_of(nx_network* h, int slot) { return slot < 0 ? h->pa.cbuf : h->red + slot; }
+
+int team_allreduce(const Team& t, int slot, int n) {
+  if (!team_multi(t) || n <= 0) return NX_OK;
+  if (t.g) {
+    GroupPtrs gp{};
+    for (int r = 0; r < t.P; ++r) gp.p[r] = xbuf_of(t.hs[r], slot);
+    hipLaunchKernelGGL(k_group_sum, dim3(std::min(grid_of(n, 256), 64)), dim3(256), 0,
+                       t.hs[0]->stream, gp, t.P, n);
+    return NX_OK;
+  }
+  nx_network* h = t.hs[0];
+  NCCLCALL(ncclAllReduce(xbuf_of(h, slot), xbuf_of(h, slot), n, ncclDouble, ncclSum, h->comm,
                          h->stream));
   return NX_OK;
 }
 
 // Preconditioner application on the stream: z = P^{-1} r' where r' = y - (alpha/beta) r2
 // (mode 0, written back into y) or r' = y (mode 1, start). Partials of r'.z -> partB.
+// half 0: chain condensation + junction elimination (up, top); half 1: back-substitution
+// (top, down). With a coarse step the top kernel stops after the elimination, the coarse
+// buffer is all-reduced between the halves and k_pc_coarse finishes the top part.
 template <bool MULTI, int W, int CPL>
 void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other,
-                  int mode) {
-  if (h->pc_lds) {
-    if (h->pc_jobs > 0)
-      hipLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
-                         h->stream, h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
-    hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y,
-                       r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
-    if (h->pc_jobs > 0)
-      hipLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
-                         h->stream, h->pa, y, h->z, st, h->partB, mode);
+                  int mode, int half) {
+  const bool coarse = MULTI && h->pa.n_coarse > 0;
+  if (half == 0) {
+    if (h->pc_lds) {
+      if (h->pc_jobs > 0)
+        hipLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
+                           h->stream, h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
+      hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa,
+                         y, r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
+    } else {
+      if (h->pc_jobs > 0)
+        hipLaunchKernelGGL((k_pc_up<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
+                           h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
+      hipLaunchKernelGGL((k_pc_top<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y,
+                         r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
+    }
     return;
   }
-  if (h->pc_jobs > 0)
-    hipLaunchKernelGGL((k_pc_up<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
-                       h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
-  hipLaunchKernelGGL((k_pc_top<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2,
-                     h->z, st, h->partA, h->nA, h->red, h->partB, mode);
-  if (h->pc_jobs > 0)
-    hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
-                       h->pa, y, h->z, st, h->partB, mode);
+  if (coarse)
+    hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, h->z, st,
+                       h->partB, mode);
+  if (h->pc_jobs > 0) {
+    if (h->pc_lds)
+      hipLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
+                         h->stream, h->pa, y, h->z, st, h->partB, mode);
+    else
+      hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
+                         h->pa, y, h->z, st, h->partB, mode);
+  }
 }
 
 template <bool MULTI>
-void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other, int mode) {
+void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other, int mode,
+               int half) {
   switch (h->pc_variant) {
-    case 0: launch_pc_wc<MULTI, 16, 1>(h, y, r2, st, other, mode); break;
-    case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode); break;
-    case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode); break;
-    case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode); break;
-    default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode); break;
+    case 0: launch_pc_wc<MULTI, 16, 1>(h, y, r2, st, other, mode, half); break;
+    case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode, half); break;
+    case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode, half); break;
+    case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode, half); break;
+    default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half); break;
   }
 }
 
 int nB_of(const nx_network* h) { return h->pc ? h->pc_jobs + 1 : h->nB; }
 
-// One MINRES iteration on the stream; `k` = 1-based iteration index (parity only).
-int launch_iteration(nx_network* h, int64_t k) {
-  double* r1 = h->vb[(k - 1) & 1];
-  double* r2 = h->vb[k & 1];
-  // pending update of iteration k-1: w1 = w_{k-3} (overwritten by w_{k-1}), w2 = w_{k-2}
-  double* w1 = h->wb[k & 1];
-  double* w2 = h->wb[(k - 1) & 1];
-  MrState* sin = h->st + ((k + 1) & 1);
-  MrState* sout = h->st + (k & 1);
-  const bool multi = h->comm != nullptr;
-  const bool pc = h->pc;
-  if (multi) CHECK(halo(h, pc ? h->z : r2));
-  MrVecs mv{r1, r2, w1, w2, h->x, h->z, h->vv};
-  const int nB = nB_of(h);
-  // profiling: events bound to the kernel's own dispatch packet (hipExtLaunchKernel), so
-  // the measured interval is the kernel's execution like rocprofv3's, not marker latency
-  hipEvent_t e0 = h->prof ? h->ev_pool[2 * h->prof_k] : nullptr;
-  hipEvent_t e1 = h->prof ? h->ev_pool[2 * h->prof_k + 1] : nullptr;
+// Whole preconditioner application for every rank of the team, with the coarse exchange.
+int team_pc(const Team& t, int64_t k, int mode) {
+  const bool multi = team_multi(t);
+  for (int half = 0; half < 2; ++half) {
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      double* y = mode ? h->vb[0] : h->vb[(k - 1) & 1];
+      const double* r2 = mode ? h->vb[1] : h->vb[k & 1];
+      MrState* st = mode ? h->st : h->st + (k & 1);
+      MrState* other = mode ? h->st + 1 : h->st + ((k + 1) & 1);
+      if (multi) launch_pc<true>(h, y, r2, st, other, mode, half);
+      else launch_pc<false>(h, y, r2, st, other, mode, half);
+    }
+    if (half == 0 && multi && t.hs[0]->pa.n_coarse > 0)
+      CHECK(team_allreduce(t, -1, 3 * t.hs[0]->pa.n_coarse));
+  }
+  return NX_OK;
+}
+
+int team_reduce_slot(const Team& t, bool from_a, int slot) {
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream,
+                       from_a ? h->partA : h->partB, from_a ? h->nA : nB_of(h), h->red, slot);
+  }
+  return team_allreduce(t, slot, 1);
+}
+
+// One MINRES iteration of every rank on the stream; `k` = 1-based iteration index.
+int launch_iteration(const Team& t, int64_t k) {
+  const bool multi = team_multi(t);
+  const bool pc = t.hs[0]->pc;
+  if (multi) CHECK(team_halo(t, pc ? VS_Z : VS_R2, k));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    double* r1 = h->vb[(k - 1) & 1];
+    double* r2 = h->vb[k & 1];
+    // pending update of iteration k-1: w1 = w_{k-3} (overwritten by w_{k-1}), w2 = w_{k-2}
+    double* w1 = h->wb[k & 1];
+    double* w2 = h->wb[(k - 1) & 1];
+    MrState* sin = h->st + ((k + 1) & 1);
+    MrState* sout = h->st + (k & 1);
+    MrVecs mv{r1, r2, w1, w2, h->x, h->z, h->vv};
+    const int nB = nB_of(h);
+    // profiling (single handle): events bound to the kernel's own dispatch packet
+    // (hipExtLaunchKernel), so the interval is the kernel's execution like rocprofv3's
+    const bool prof = h->prof && t.g == nullptr;
+    hipEvent_t e0 = prof ? h->ev_pool[2 * h->prof_k] : nullptr;
+    hipEvent_t e1 = prof ? h->ev_pool[2 * h->prof_k + 1] : nullptr;
 #define NX_LAUNCH_A(M, P)                                                                        \
   hipExtLaunchKernelGGL((k_mr_a<M, P>), dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,     \
                         csr_of(h), mv, sin, sout, h->partB, nB, h->red, h->partA, h->chunksA)
-  if (multi) {
-    if (pc) NX_LAUNCH_A(true, true); else NX_LAUNCH_A(true, false);
-  } else {
-    if (pc) NX_LAUNCH_A(false, true); else NX_LAUNCH_A(false, false);
-  }
+    if (multi) {
+      if (pc) NX_LAUNCH_A(true, true); else NX_LAUNCH_A(true, false);
+    } else {
+      if (pc) NX_LAUNCH_A(false, true); else NX_LAUNCH_A(false, false);
+    }
 #undef NX_LAUNCH_A
-  if (h->prof) h->prof_k += 1;
-  if (multi) {
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partA, h->nA, h->red, 0);
-    CHECK(allreduce_slot(h, 0));
-    if (pc)
-      launch_pc<true>(h, r1, r2, sout, sin, 0);
-    else
-      hipLaunchKernelGGL(k_mr_b<true>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
-                         sout, sin, h->partA, h->nA, h->red, h->partB);
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream, h->partB, nB, h->red, 1);
-    CHECK(allreduce_slot(h, 1));
-  } else {
-    if (pc)
-      launch_pc<false>(h, r1, r2, sout, sin, 0);
-    else
-      hipLaunchKernelGGL(k_mr_b<false>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
-                         sout, sin, h->partA, h->nA, h->red, h->partB);
+    if (prof) h->prof_k += 1;
   }
+  if (multi) CHECK(team_reduce_slot(t, true, 0));
+  if (pc) {
+    CHECK(team_pc(t, k, 0));
+  } else {
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      double* r1 = h->vb[(k - 1) & 1];
+      double* r2 = h->vb[k & 1];
+      MrState* sin = h->st + ((k + 1) & 1);
+      MrState* sout = h->st + (k & 1);
+      if (multi)
+        hipLaunchKernelGGL(k_mr_b<true>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1, r2,
+                           sout, sin, h->partA, h->nA, h->red, h->partB);
+      else
+        hipLaunchKernelGGL(k_mr_b<false>, dim3(h->nB), dim3(kBlock), 0, h->stream, h->n_own, r1,
+                           r2, sout, sin, h->partA, h->nA, h->red, h->partB);
+    }
+  }
+  if (multi) CHECK(team_reduce_slot(t, false, 1));
   HIPCALL(hipGetLastError());
   return NX_OK;
 }
 
-int build_chunk_graph(nx_network* h, int len) {
-  if (h->chunk_exec && h->chunk_len == len) return NX_OK;
-  if (h->chunk_exec) {
-    HIPCALL(hipGraphExecDestroy(h->chunk_exec));
-    h->chunk_exec = nullptr;
-  }
-  if (h->chunk_graph) {
-    HIPCALL(hipGraphDestroy(h->chunk_graph));
-    h->chunk_graph = nullptr;
-  }
-  HIPCALL(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+struct GraphSlot {
+  hipGraphExec_t* exec;
+  hipGraph_t* graph;
+  int* len;
+};
+
+GraphSlot graph_slot(const Team& t) {
+  if (t.g) return GraphSlot{&t.g->chunk_exec, &t.g->chunk_graph, &t.g->chunk_len};
+  nx_network* h = t.hs[0];
+  return GraphSlot{&h->chunk_exec, &h->chunk_graph, &h->chunk_len};
+}
+
+int drop_graph(GraphSlot gs) {
+  if (*gs.exec) HIPCALL(hipGraphExecDestroy(*gs.exec));
+  if (*gs.graph) HIPCALL(hipGraphDestroy(*gs.graph));
+  *gs.exec = nullptr;
+  *gs.graph = nullptr;
+  *gs.len = 0;
+  return NX_OK;
+}
+
+int build_chunk_graph(const Team& t, int len) {
+  GraphSlot gs = graph_slot(t);
+  if (*gs.exec && *gs.len == len) return NX_OK;
+  CHECK(drop_graph(gs));
+  hipStream_t s = t.hs[0]->stream;
+  HIPCALL(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
   int rc = NX_OK;
-  for (int j = 0; j < len && rc == NX_OK; ++j) rc = launch_iteration(h, j + 1);
+  for (int j = 0; j < len && rc == NX_OK; ++j) rc = launch_iteration(t, j + 1);
   hipGraph_t g = nullptr;
-  const hipError_t e = hipStreamEndCapture(h->stream, &g);
+  const hipError_t e = hipStreamEndCapture(s, &g);
   if (rc != NX_OK) return rc;
   if (e != hipSuccess) return fail(NX_ERR_HIP, std::string("capture: ") + hipGetErrorString(e));
-  h->chunk_graph = g;
-  HIPCALL(hipGraphInstantiate(&h->chunk_exec, g, nullptr, nullptr, 0));
-  h->chunk_len = len;
+  *gs.graph = g;
+  HIPCALL(hipGraphInstantiate(gs.exec, g, nullptr, nullptr, 0));
+  *gs.len = len;
   return NX_OK;
 }
 
@@ -1645,6 +1905,7 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
 
 NX_API int nx_destroy(nx_network_t* h) {
   if (h == nullptr) return NX_OK;
+  if (h->group) return fail(NX_ERR_STATE, "destroy the group (nx_group_destroy) first");
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->chunk_exec) (void)hipGraphExecDestroy(h->chunk_exec);
@@ -1730,79 +1991,99 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   return NX_OK;
 }
 
-NX_API int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
-                    int32_t* iters, double* relres, int32_t* converged) {
-  if (!h) return fail(NX_ERR_ARG, "null handle");
-  if (!h->have_lhs || !h->have_rhs) return fail(NX_ERR_STATE, "assemble lhs and rhs before solve");
+namespace {
+
+// MINRES of every rank of the team (nx_solve / nx_group_solve).
+int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, int32_t* iters,
+               double* relres, int32_t* converged) {
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    if (!h->have_lhs || !h->have_rhs) return fail(NX_ERR_STATE, "assemble lhs and rhs before solve");
+    if (h->pc != t.hs[0]->pc) return fail(NX_ERR_STATE, "ranks disagree on the preconditioner");
+  }
   if (maxit < 1) return fail(NX_ERR_ARG, "maxit must be >= 1");
   if (check_every < 2) check_every = 2;
   if (check_every & 1) ++check_every;
-  CHECK(set_device(h));
-  hipStream_t s = h->stream;
-  const int64_t n = h->n_own;
+  CHECK(set_device(t.hs[0]));
+  const bool multi = team_multi(t);
+  hipStream_t s = t.hs[0]->stream;
   // r1 = r2 = b, w1 = w2 = x = 0
-  for (int i = 0; i < 2; ++i) {
-    if (n > 0) HIPCALL(hipMemcpyAsync(h->vb[i], h->rhs, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-    if (h->n_ghost > 0) HIPCALL(hipMemsetAsync(h->vb[i] + n, 0, sizeof(double) * h->n_ghost, s));
-    if (n > 0) HIPCALL(hipMemsetAsync(h->wb[i], 0, sizeof(double) * n, s));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    const int64_t n = h->n_own;
+    for (int i = 0; i < 2; ++i) {
+      if (n > 0)
+        HIPCALL(hipMemcpyAsync(h->vb[i], h->rhs, sizeof(double) * n, hipMemcpyDeviceToDevice, h->stream));
+      if (h->n_ghost > 0) HIPCALL(hipMemsetAsync(h->vb[i] + n, 0, sizeof(double) * h->n_ghost, h->stream));
+      if (n > 0) HIPCALL(hipMemsetAsync(h->wb[i], 0, sizeof(double) * n, h->stream));
+    }
+    HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, h->stream));
   }
-  HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, s));
-  const bool multi = h->comm != nullptr;
-  const int nB = nB_of(h);
-  if (h->pc) {  // beta_1^2 = b . P^{-1} b
-    if (multi)
-      launch_pc<true>(h, h->vb[0], h->vb[1], h->st, h->st + 1, 1);
-    else
-      launch_pc<false>(h, h->vb[0], h->vb[1], h->st, h->st + 1, 1);
+  if (t.hs[0]->pc) {  // beta_1^2 = b . P^{-1} b
+    CHECK(team_pc(t, 0, 1));
   } else {
-    hipLaunchKernelGGL(k_sumsq, dim3(h->nB), dim3(kBlock), 0, s, h->rhs, n, h->partB);
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      hipLaunchKernelGGL(k_sumsq, dim3(h->nB), dim3(kBlock), 0, h->stream, h->rhs, h->n_own, h->partB);
+    }
   }
-  if (multi) {
-    hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, s, h->partB, nB, h->red, 2);
-    CHECK(allreduce_slot(h, 2));
-  }
-  for (int b = 0; b < 2; ++b) {  // both state buffers start identical
-    if (multi)
-      hipLaunchKernelGGL(k_mr_init<true>, dim3(1), dim3(kBlock), 0, s, h->partB, nB, h->red,
-                         h->st + b, rtol, maxit);
-    else
-      hipLaunchKernelGGL(k_mr_init<false>, dim3(1), dim3(kBlock), 0, s, h->partB, nB, h->red,
-                         h->st + b, rtol, maxit);
+  if (multi) CHECK(team_reduce_slot(t, false, 2));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    for (int b = 0; b < 2; ++b) {  // both state buffers start identical
+      if (multi)
+        hipLaunchKernelGGL(k_mr_init<true>, dim3(1), dim3(kBlock), 0, h->stream, h->partB, nB_of(h),
+                           h->red, h->st + b, rtol, maxit);
+      else
+        hipLaunchKernelGGL(k_mr_init<false>, dim3(1), dim3(kBlock), 0, h->stream, h->partB,
+                           nB_of(h), h->red, h->st + b, rtol, maxit);
+    }
   }
   HIPCALL(hipGetLastError());
 
-  // Profiling: eager launches with an event pair around every k_mr_a of a chunk; after
-  // the chunk's convergence check only the launches that ran a Lanczos step are added.
-  const bool use_graph = !multi && !h->prof;
-  if (use_graph) CHECK(build_chunk_graph(h, check_every));
-  if (h->prof && (int)h->ev_pool.size() < 2 * check_every) {
-    for (auto& e : h->ev_pool) (void)hipEventDestroy(e);
-    h->ev_pool.assign(2 * check_every, nullptr);
-    for (auto& e : h->ev_pool) HIPCALL(hipEventCreate(&e));
+  // Chunks of check_every iterations, one host check each: a HIP graph, except with RCCL
+  // (eager launches) and when profiling (an event pair around every k_mr_a of a chunk;
+  // after the check only the launches that ran a Lanczos step are added).
+  nx_network* h0 = t.hs[0];
+  const bool prof = h0->prof && t.g == nullptr;
+  const bool use_graph = t.hs[0]->comm == nullptr && !prof;
+  if (use_graph) CHECK(build_chunk_graph(t, check_every));
+  if (prof && (int)h0->ev_pool.size() < 2 * check_every) {
+    for (auto& e : h0->ev_pool) (void)hipEventDestroy(e);
+    h0->ev_pool.assign(2 * check_every, nullptr);
+    for (auto& e : h0->ev_pool) HIPCALL(hipEventCreate(&e));
   }
   int64_t launched = 0;
   int nb_before = 0;
   const MrState* last = nullptr;
   for (;;) {
     if (use_graph) {
-      HIPCALL(hipGraphLaunch(h->chunk_exec, s));
+      HIPCALL(hipGraphLaunch(*graph_slot(t).exec, s));
     } else {
-      h->prof_k = 0;
-      for (int j = 0; j < check_every; ++j) CHECK(launch_iteration(h, launched + j + 1));
+      h0->prof_k = 0;
+      for (int j = 0; j < check_every; ++j) CHECK(launch_iteration(t, launched + j + 1));
     }
     launched += check_every;
-    HIPCALL(hipMemcpyAsync(h->h_st, h->st, 2 * sizeof(MrState), hipMemcpyDeviceToHost, s));
+    for (int r = 0; r < t.P; ++r)
+      HIPCALL(hipMemcpyAsync(t.hs[r]->h_st, t.hs[r]->st, 2 * sizeof(MrState), hipMemcpyDeviceToHost,
+                             t.hs[r]->stream));
     HIPCALL(hipStreamSynchronize(s));
     // the chunk ends with k even -> S[0] is the latest; once the solve stopped, k_mr_b
     // has made both buffers identical
-    last = &h->h_st[0];
-    if (h->prof) {
+    last = &h0->h_st[0];
+    for (int r = 1; r < t.P; ++r) {  // the ranks run the same recurrence on the same scalars
+      const MrState& o = t.hs[r]->h_st[0];
+      if (o.it != last->it || o.done != last->done || o.relres != last->relres)
+        return fail(NX_ERR_STATE, "ranks diverged: rank " + std::to_string(r) + " at iteration " +
+                                      std::to_string(o.it) + " vs " + std::to_string(last->it));
+    }
+    if (prof) {
       const int ran = last->nb - nb_before;
-      for (int j = 0; j < ran && j < h->prof_k; ++j) {
+      for (int j = 0; j < ran && j < h0->prof_k; ++j) {
         float ms = 0.f;
-        HIPCALL(hipEventElapsedTime(&ms, h->ev_pool[2 * j], h->ev_pool[2 * j + 1]));
-        h->spmv_ms += ms;
-        h->spmv_cnt += 1;
+        HIPCALL(hipEventElapsedTime(&ms, h0->ev_pool[2 * j], h0->ev_pool[2 * j + 1]));
+        h0->spmv_ms += ms;
+        h0->spmv_cnt += 1;
       }
       nb_before = last->nb;
     }
@@ -1813,6 +2094,17 @@ NX_API int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_e
   if (converged) *converged = last->converged;
   return NX_OK;
 }
+
+}  // namespace
+
+NX_API int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
+                    int32_t* iters, double* relres, int32_t* converged) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (h->group) return fail(NX_ERR_STATE, "the handle belongs to a group: use nx_group_solve");
+  nx_network* hs[1] = {h};
+  return solve_team(Team{hs, 1, nullptr}, rtol, maxit, check_every, iters, relres, converged);
+}
+
 NX_API int nx_get_solution(nx_network_t* h, double* xo) {
   if (!h || !xo) return fail(NX_ERR_ARG, "null argument");
   CHECK(set_device(h));
@@ -1863,8 +2155,12 @@ NX_API int nx_spmv_host(nx_network_t* h, const double* xh, double* yh) {
 NX_API int nx_true_residual(nx_network_t* h, double* relres) {
   if (!h || !relres) return fail(NX_ERR_ARG, "null argument");
   if (!h->have_lhs || !h->have_rhs) return fail(NX_ERR_STATE, "assemble first");
+  if (h->group) return fail(NX_ERR_STATE, "group member: compute the residual from the solutions");
   CHECK(set_device(h));
-  if (h->comm) CHECK(halo(h, h->x));
+  {
+    nx_network* hs[1] = {h};
+    CHECK(team_halo(Team{hs, 1, nullptr}, VS_X, 0));
+  }
   hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
                      h->rhs, h->partials, h->nblk);
   double* d = h->red + 2;  // slots 2, 3 are free outside nx_solve
@@ -1947,10 +2243,11 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   if (!h) return fail(NX_ERR_ARG, "null handle");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
-  if (h->chunk_exec) {  // captured launches depend on the preconditioner: recapture
-    HIPCALL(hipGraphExecDestroy(h->chunk_exec));
-    h->chunk_exec = nullptr;
-    h->chunk_len = 0;
+  {  // captured launches depend on the preconditioner: recapture
+    nx_network* hs[1] = {h};
+    CHECK(drop_graph(graph_slot(Team{hs, 1, nullptr})));
+    if (h->group) CHECK(drop_graph(GraphSlot{&h->group->chunk_exec, &h->group->chunk_graph,
+                                             &h->group->chunk_len}));
   }
   if (!enable) {
     h->pc = false;
@@ -1965,7 +2262,10 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   else if (N <= 256) variant = 4;
   else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 256 cells per edge");
   if (n_chains != h->E) return fail(NX_ERR_ARG, "one chain per local edge expected");
-  if (n_slots != h->B) return fail(NX_ERR_ARG, "one junction slot per owned multiplier expected");
+  // one slot per owned multiplier, plus (several ranks) the ghost junctions at the ends of
+  // local edges, which are coarse (nx_set_coarse)
+  if (n_slots < h->B || n_slots > h->B + h->n_ghost)
+    return fail(NX_ERR_ARG, "one junction slot per owned multiplier (+ ghost junctions) expected");
   if (n_jobs < 0 || n_lvl < 0 || n_top_lvl < 0) return fail(NX_ERR_ARG, "negative sizes");
   if (h->E > 0 && n_jobs < 1) return fail(NX_ERR_ARG, "chains need at least one job");
   for (int64_t c = 0; c < n_chains; ++c) {
@@ -1974,8 +2274,9 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
       return fail(NX_ERR_ARG, "chain end slot out of range");
   }
   for (int64_t j = 0; j < n_slots; ++j) {
-    if (slot_lam[j] < h->n_edge_dofs || slot_lam[j] >= h->n_own)
-      return fail(NX_ERR_ARG, "slot_lam must be an owned multiplier row");
+    if (slot_lam[j] < h->n_edge_dofs || slot_lam[j] >= h->n_col ||
+        (slot_lam[j] >= h->n_own && h->nranks == 1))
+      return fail(NX_ERR_ARG, "slot_lam must be a multiplier row or ghost column");
     if (slot_pchain[j] < -1 || slot_pchain[j] >= n_chains || slot_parent[j] < -1 ||
         slot_parent[j] >= n_slots)
       return fail(NX_ERR_ARG, "slot parent out of range");
@@ -2067,7 +2368,83 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->pa = pa;
   h->pc_jobs = n_jobs;
   h->pc_variant = variant;
+  h->pc_slots = n_slots;
   h->pc = true;
+  return NX_OK;
+}
+
+NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_cidx,
+                         int32_t n_cc, const int32_t* cc_chain, const int32_t* cc_top,
+                         const int32_t* cc_bot, const int32_t* c_parent,
+                         const int32_t* c_child_off, const int32_t* c_child, int32_t n_clvl,
+                         const int32_t* c_lvl_off) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
+  if (n_coarse < 0 || n_cc < 0 || n_clvl < 0) return fail(NX_ERR_ARG, "negative sizes");
+  if (n_coarse > kCapCoarse)
+    return fail(NX_ERR_ARG, "coarse forest has " + std::to_string(n_coarse) + " junctions (cap " +
+                                std::to_string(kCapCoarse) + ")");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  const int64_t ns = h->pc_slots;
+  if (n_coarse == 0) {
+    h->pa.n_coarse = 0;
+    return NX_OK;
+  }
+  if (!slot_cidx || !c_parent || !c_child_off || !c_lvl_off || (n_cc > 0 && (!cc_chain || !cc_top || !cc_bot)))
+    return fail(NX_ERR_ARG, "null coarse array");
+  // host copies of the top-level offsets to check that coarse slots sit in the top part
+  std::vector<int> top_off(h->pa.n_top_lvl + 1);
+  HIPCALL(hipMemcpy(top_off.data(), h->pa.top_lvl_off, sizeof(int) * top_off.size(),
+                    hipMemcpyDeviceToHost));
+  std::vector<int> lam(ns > 0 ? ns : 1);
+  if (ns > 0) HIPCALL(hipMemcpy(lam.data(), h->pa.slot_lam, sizeof(int) * ns, hipMemcpyDeviceToHost));
+  const int top0 = top_off[0], top1 = top_off.back();
+  for (int64_t j = 0; j < ns; ++j) {
+    if (slot_cidx[j] < -1 || slot_cidx[j] >= n_coarse) return fail(NX_ERR_ARG, "slot_cidx out of range");
+    if (slot_cidx[j] >= 0 && (j < top0 || j >= top1))
+      return fail(NX_ERR_ARG, "coarse slots must lie in the top part");
+    if (lam[j] >= h->n_own && slot_cidx[j] < 0) return fail(NX_ERR_ARG, "ghost slot must be coarse");
+  }
+  for (int i = 0; i < n_cc; ++i)
+    if (cc_chain[i] < 0 || cc_chain[i] >= h->E || cc_top[i] < 0 || cc_top[i] >= n_coarse ||
+        cc_bot[i] < 0 || cc_bot[i] >= n_coarse)
+      return fail(NX_ERR_ARG, "coarse chain out of range");
+  if (c_child_off[0] != 0 || c_lvl_off[0] != 0 || c_lvl_off[n_clvl] != n_coarse)
+    return fail(NX_ERR_ARG, "bad coarse offsets");
+  for (int j = 0; j < n_coarse; ++j)
+    if (c_parent[j] < -1 || c_parent[j] >= n_coarse) return fail(NX_ERR_ARG, "c_parent out of range");
+  const int ncl = c_child_off[n_coarse];
+  for (int i = 0; i < ncl; ++i)
+    if (c_child[i] < 0 || c_child[i] >= n_coarse) return fail(NX_ERR_ARG, "c_child out of range");
+  auto up = [&](const int32_t* src, int64_t n) -> const int* {
+    int* d = nullptr;
+    if (n <= 0) n = 1;
+    if (hipMalloc((void**)&d, sizeof(int) * n) != hipSuccess) return nullptr;
+    h->pc_bufs.push_back(d);
+    if (src && hipMemcpy(d, src, sizeof(int) * n, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return d;
+  };
+  PcArgs& pa = h->pa;
+  pa.slot_cidx = up(slot_cidx, ns);
+  pa.cc_chain = up(n_cc ? cc_chain : nullptr, n_cc);
+  pa.cc_top = up(n_cc ? cc_top : nullptr, n_cc);
+  pa.cc_bot = up(n_cc ? cc_bot : nullptr, n_cc);
+  pa.c_parent = up(c_parent, n_coarse);
+  pa.c_child_off = up(c_child_off, n_coarse + 1);
+  pa.c_child = up(ncl ? c_child : nullptr, ncl);
+  pa.c_lvl_off = up(c_lvl_off, n_clvl + 1);
+  double* cb = nullptr;
+  HIPCALL(hipMalloc((void**)&cb, sizeof(double) * 3 * n_coarse));
+  h->pc_bufs.push_back(cb);
+  pa.cbuf = cb;
+  for (const void* q : {(const void*)pa.slot_cidx, (const void*)pa.cc_chain, (const void*)pa.cc_top,
+                        (const void*)pa.cc_bot, (const void*)pa.c_parent, (const void*)pa.c_child_off,
+                        (const void*)pa.c_child, (const void*)pa.c_lvl_off})
+    if (q == nullptr) return fail(NX_ERR_HIP, "coarse upload failed");
+  pa.n_cc = n_cc;
+  pa.n_clvl = n_clvl;
+  pa.n_coarse = n_coarse;
   return NX_OK;
 }
 
@@ -2080,14 +2457,18 @@ NX_API int nx_comm_unique_id(unsigned char* id_out) {
   return NX_OK;
 }
 
-NX_API int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned char* id,
-                        int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
-                        const int32_t* send_idx, const int32_t* recv_off) {
-  if (!h || !id) return fail(NX_ERR_ARG, "null argument");
+NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_peers,
+                       const int32_t* peer_rank, const int32_t* send_off,
+                       const int32_t* send_idx, const int32_t* recv_off) {
+  if (!h) return fail(NX_ERR_ARG, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(NX_ERR_ARG, "bad rank/nranks");
+  if (nranks > 1 && h->pc) return fail(NX_ERR_STATE, "set the halo plan before the preconditioner");
   if (n_peers < 0 || (n_peers > 0 && (!peer_rank || !send_off || !recv_off)))
     return fail(NX_ERR_ARG, "bad halo plan");
   CHECK(set_device(h));
+  for (int i = 0; i < n_peers; ++i)
+    if (peer_rank[i] < 0 || peer_rank[i] >= nranks || peer_rank[i] == rank)
+      return fail(NX_ERR_ARG, "bad peer rank");
   h->peers.assign(peer_rank, peer_rank + n_peers);
   h->send_off.assign(send_off, send_off + n_peers + 1);
   h->recv_off.assign(recv_off, recv_off + n_peers + 1);
@@ -2102,13 +2483,101 @@ NX_API int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const uns
   const int nsend = h->send_off.back();
   for (int i = 0; i < nsend; ++i)
     if (send_idx[i] < 0 || send_idx[i] >= h->n_own) return fail(NX_ERR_ARG, "send_idx out of range");
+  if (h->send_idx) HIPCALL(hipFree(h->send_idx));
+  if (h->send_buf) HIPCALL(hipFree(h->send_buf));
+  h->send_idx = nullptr;
+  h->send_buf = nullptr;
   CHECK(upload(&h->send_idx, send_idx, nsend, h->stream));
   CHECK(dalloc(&h->send_buf, nsend));
+  h->nranks = nranks;
+  h->rank = rank;
+  h->have_plan = true;
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned char* id,
+                        int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
+                        const int32_t* send_idx, const int32_t* recv_off) {
+  if (!h || !id) return fail(NX_ERR_ARG, "null argument");
+  if (h->group) return fail(NX_ERR_STATE, "the handle belongs to a group");
+  CHECK(nx_set_halo(h, nranks, rank, n_peers, peer_rank, send_off, send_idx, recv_off));
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   NCCLCALL(ncclCommInitRank(&h->comm, nranks, uid, rank));
-  h->nranks = nranks;
-  h->rank = rank;
-  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_group_create(int32_t nranks, nx_network_t* const* handles, nx_group_t** out) {
+  if (!out || !handles) return fail(NX_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (nranks < 1 || nranks > kMaxGroup)
+    return fail(NX_ERR_ARG, "group size must be 1.." + std::to_string(kMaxGroup));
+  for (int r = 0; r < nranks; ++r) {
+    nx_network* h = handles[r];
+    if (!h) return fail(NX_ERR_ARG, "null handle in group");
+    if (h->group || h->comm) return fail(NX_ERR_STATE, "handle already has a transport");
+    if (h->device != handles[0]->device) return fail(NX_ERR_ARG, "group members share one device");
+    if (nranks > 1 && (!h->have_plan || h->rank != r || h->nranks != nranks))
+      return fail(NX_ERR_STATE, "handle " + std::to_string(r) + " needs nx_set_halo(rank " +
+                                    std::to_string(r) + " of " + std::to_string(nranks) + ")");
+  }
+  // where each ghost segment comes from: my segment in the peer's send buffer
+  for (int r = 0; r < nranks; ++r) {
+    nx_network* h = handles[r];
+    h->peer_src_off.assign(h->peers.size(), 0);
+    for (size_t j = 0; j < h->peers.size(); ++j) {
+      nx_network* p = handles[h->peers[j]];
+      const auto it = std::find(p->peers.begin(), p->peers.end(), r);
+      const int cnt = h->recv_off[j + 1] - h->recv_off[j];
+      if (it == p->peers.end()) {
+        if (cnt > 0) return fail(NX_ERR_ARG, "halo plans disagree (missing peer)");
+        continue;
+      }
+      const size_t i = (size_t)(it - p->peers.begin());
+      if (p->send_off[i + 1] - p->send_off[i] != cnt)
+        return fail(NX_ERR_ARG, "halo plans disagree: rank " + std::to_string(h->peers[j]) +
+                                    " sends " + std::to_string(p->send_off[i + 1] - p->send_off[i]) +
+                                    " values, rank " + std::to_string(r) + " expects " +
+                                    std::to_string(cnt));
+      h->peer_src_off[j] = p->send_off[i];
+    }
+  }
+  HIPCALL(hipSetDevice(handles[0]->device));
+  auto* g = new nx_group();
+  g->P = nranks;
+  g->hs.assign(handles, handles + nranks);
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete g;
+    return fail(NX_ERR_HIP, "hipStreamCreate failed");
+  }
+  for (nx_network* h : g->hs) {
+    (void)hipStreamSynchronize(h->stream);
+    h->own_stream = h->stream;
+    h->stream = g->stream;
+    h->group = g;
+  }
+  *out = g;
+  return NX_OK;
+}
+
+NX_API int nx_group_solve(nx_group_t* g, double rtol, int32_t maxit, int32_t check_every,
+                          int32_t* iters, double* relres, int32_t* converged) {
+  if (!g) return fail(NX_ERR_ARG, "null group");
+  return solve_team(Team{g->hs.data(), g->P, g}, rtol, maxit, check_every, iters, relres, converged);
+}
+
+NX_API int nx_group_destroy(nx_group_t* g) {
+  if (!g) return NX_OK;
+  (void)hipSetDevice(g->hs[0]->device);
+  (void)hipStreamSynchronize(g->stream);
+  (void)drop_graph(GraphSlot{&g->chunk_exec, &g->chunk_graph, &g->chunk_len});
+  for (nx_network* h : g->hs) {
+    h->stream = h->own_stream;
+    h->own_stream = nullptr;
+    h->group = nullptr;
+  }
+  (void)hipStreamDestroy(g->stream);
+  delete g;
   return NX_OK;
 }

@@ -1,0 +1,88 @@
+"""All ranks of a partitioned network problem in ONE process, on one GPU.
+
+The multi-GPU path runs one process per GPU over RCCL (``assembly.py`` +
+``nx_comm_init``). RCCL refuses two ranks on one device, so this module drives the same
+per-rank handles -- same partition, halo plans, preconditioner decomposition with the
+coarse step, kernels and MINRES schedule -- through the library's in-process group
+transport (``nx_group_*`` in ``include/nxhip.h``), where the halo exchange is a device
+copy and every all-reduce a fixed-order device sum. It exists to check the multi-rank
+algorithm on a single GPU against the single-rank solve; it is not a performance path.
+"""
+
+from __future__ import annotations
+
+import networkx as nx
+import numpy as np
+
+from . import _lib
+from .assembly import HydraulicNetworkAssembler
+from .comm import LocalGroup
+from .mesh import NetworkMesh
+
+__all__ = ["RankGroup"]
+
+
+class RankGroup:
+    """``nranks`` ranks of the network problem on graph ``graph``.
+
+    Args:
+        graph: the network (built once; the other ranks receive it by the group's bcast)
+        N: cells per edge
+        nranks: number of simulated ranks (<= 16)
+        color_strategy: edge colouring strategy, as for :class:`NetworkMesh`
+    """
+
+    def __init__(self, graph: nx.DiGraph, N: int, nranks: int, color_strategy=None):
+        group = LocalGroup(nranks)
+        self.meshes = [NetworkMesh(graph if r == 0 else None, N=N, color_strategy=color_strategy,
+                                   comm=group.comm(r)) for r in range(nranks)]
+        self.assemblers = [HydraulicNetworkAssembler(m) for m in self.meshes]
+        self._group: _lib.Group | None = None
+        self.iterations = 0
+        self.relres = float("nan")
+        self.converged = False
+
+    @property
+    def nranks(self) -> int:
+        return len(self.assemblers)
+
+    def compute_forms(self, **kwargs) -> None:
+        for a in self.assemblers:
+            a.compute_forms(**kwargs)
+
+    def assemble(self) -> None:
+        for a in self.assemblers:
+            a.assemble()
+
+    def set_preconditioner(self, enable: bool) -> None:
+        self._close_group()
+        for a in self.assemblers:
+            a.set_preconditioner(enable)
+
+    def solve(self, rtol: float = 1e-12, maxit: int = 50000, check_every: int = 32):
+        """MINRES over all ranks; returns ``(iterations, relres, converged)``."""
+        if self._group is None:
+            self._group = _lib.Group([a.handle for a in self.assemblers])
+        it, rr, conv = self._group.solve(rtol, maxit, check_every)
+        self.iterations, self.relres, self.converged = it, rr, conv
+        return it, rr, conv
+
+    def solutions(self) -> list[np.ndarray]:
+        """Device-layout solution of every rank (owned DoFs)."""
+        return [a.handle.solution() for a in self.assemblers]
+
+    def _close_group(self) -> None:
+        if self._group is not None:
+            self._group.close()
+            self._group = None
+
+    def close(self) -> None:
+        self._close_group()
+        for a in self.assemblers:
+            a.close()
+
+    def __del__(self):
+        try:
+            self._close_group()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass

@@ -267,6 +267,26 @@ def test_coarse_structure_steiner_closure():
     assert cs.parent.tolist() == [-1, 0, 1]
 
 
+def test_local_group_meshes_match_serial():
+    """Ranks of an in-process group build their meshes from rank 0's broadcast."""
+    from networks_fenicsx_amd.comm import LocalGroup
+
+    make, N, strategy, _ = CASES["arterial5_N40"]
+    G = make()
+    ref = NetworkMesh(G, N=N, color_strategy=strategy)
+    grp = LocalGroup(3)
+    meshes = [NetworkMesh(G if r == 0 else None, N=N, color_strategy=strategy, comm=grp.comm(r))
+              for r in range(3)]
+    for m in meshes:
+        np.testing.assert_array_equal(m.node_coordinates, ref.node_coordinates)
+        np.testing.assert_array_equal(m.edges[0], ref.edges[0])
+        np.testing.assert_array_equal(m.edge_colors, ref.edge_colors)
+    with pytest.raises(RuntimeError):
+        NetworkMesh(None, N=N, comm=LocalGroup(2).comm(1))
+    with pytest.raises(NotImplementedError):
+        grp.comm(0).allreduce(1.0)
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
