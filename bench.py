@@ -176,7 +176,7 @@ def main() -> int:
     nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on)
     achieved = nbytes / (spmv_ms * 1e-3) / 1e9
     sbytes = spmv_bytes(h.n_rows, h.nnz)
-    kname = "k_mr_a<false, true>" if pc_on else "k_mr_a<false, false>"
+    kname = f"k_mr_a<{str(world > 1).lower()}, {str(pc_on).lower()}>"
     traffic, traffic_src, rocprof_ns = pmc_traffic(kname) if world == 1 else (None, None, None)
 
     # --- parity outside the timed region
