@@ -669,6 +669,12 @@ struct PcArgs {
   const int* c_child;
   const int* c_lvl_off;
   double* cbuf;
+  // linear form (several ranks, LDS kernels): the sweeps condense y instead of
+  // r' = y - (alpha/beta) r2 and the down sweep forms z = P^{-1}y - (alpha/beta) z_old,
+  // so alpha's partial rides in the coarse all-reduce (xalpha = cbuf + 3 n_coarse)
+  int lin;
+  const double* xalpha;
+  double* slot_z;  // P^{-1}y at every junction slot (written by the top part, read across jobs)
 };
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
@@ -1006,13 +1012,16 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
       return;
     }
-    const double alfa = MULTI ? red[0] : block_allsum<kPcThreads>(partA, nA);
-    c2 = alfa / st->beta;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      st->alfa = alfa;
-      st->nb += 1;
+    if (!(MULTI && pa.lin)) {  // linear form: alpha is not known yet (k_pc_coarse)
+      const double alfa = MULTI ? red[0] : block_allsum<kPcThreads>(partA, nA);
+      c2 = alfa / st->beta;
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->alfa = alfa;
+        st->nb += 1;
+      }
     }
   }
+  const bool upd = mode == 0 && !(MULTI && pa.lin);
   const int job = blockIdx.x;
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
@@ -1027,7 +1036,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     for (int t = 0; t < CPL; ++t) {
       if (!ch.valid[t]) continue;
       double rc = y[ch.dof_c[t]];
-      if (mode == 0) {
+      if (upd) {
         rc -= c2 * r2[ch.dof_c[t]];
         y[ch.dof_c[t]] = rc;
         y[ch.dof_q[t]] -= c2 * r2[ch.dof_q[t]];
@@ -1035,7 +1044,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       sr += rc;
       srd += rc * ch.D[t];
     }
-    if (mode == 0 && ch.has_last) y[ch.dof_qN] -= c2 * r2[ch.dof_qN];
+    if (upd && ch.has_last) y[ch.dof_qN] -= c2 * r2[ch.dof_qN];
     sr = seg_sum<W>(sr);
     srd = seg_sum<W>(srd);
     if (active && l == 0) {
@@ -1058,7 +1067,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     const int j = js0 + sl;
     const int lam = pa.slot_lam[j];
     double yl = y[lam];
-    if (mode == 0) {
+    if (upd) {
       yl -= c2 * r2[lam];
       y[lam] = yl;
     }
@@ -1127,10 +1136,13 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   __shared__ double sG[kCapTDC], sDD[kCapTDC], sDJ[kCapTDC];
   __shared__ int sLv[kMaxTopLvl + 1];
   double c2 = 0.0;
+  const bool upd = mode == 0 && !(MULTI && pa.lin);
   if (mode == 0) {
     if (st->done) return;
-    const double alfa = MULTI ? red[0] : block_allsum<kTopThreads>(partA, nA);
-    c2 = alfa / st->beta;
+    if (upd) {
+      const double alfa = MULTI ? red[0] : block_allsum<kTopThreads>(partA, nA);
+      c2 = alfa / st->beta;
+    }
   }
   const int nl = pa.n_top_lvl;
   const int ts0 = pa.top_lvl_off[0], ts1 = pa.top_lvl_off[nl];
@@ -1166,7 +1178,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     const int j = ts0 + sl;
     const int lam = pa.slot_lam[j];
     double yl = y[lam];
-    if (mode == 0) {
+    if (upd) {
       yl -= c2 * r2[lam];
       y[lam] = yl;
     }
@@ -1225,6 +1237,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
       const double zj = (sJ[sl] + (p >= 0 ? sGp[sl] * sJ0[p] : 0.0)) / sD[sl];
       sJ0[sl] = zj;  // reuse: z of top slots
       z[sLam[sl]] = zj;
+      pa.slot_z[ts0 + sl] = zj;
       part += sY[sl] * zj;
     }
     __syncthreads();
@@ -1237,21 +1250,24 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
 }
 
 template <bool MULTI, int W, int CPL>
-__global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
-                                                            const double* __restrict__ y,
+__global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* __restrict__ y,
+                                                            const double* __restrict__ r2,
                                                             double* __restrict__ z,
                                                             const MrState* __restrict__ st,
                                                             double* __restrict__ partB, int mode) {
   __shared__ double sZ[kCapS], sA[kCapS], sB[kCapS];
   __shared__ int sP[kCapS];
   if (mode == 0 && st->done) return;
+  // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
+  const bool lin = MULTI && pa.lin && mode == 0;
+  const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
   const int job = blockIdx.x;
   double part = 0.0;
   const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
   const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
   const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
   const int ns = js1 - js0;
-  // phase A: every slot's A, B, parent (local index, or the parent's z for the root)
+  // phase A: every slot's A, B, parent (local index, or the parent's value for the root)
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
     const int j = js0 + sl;
     const int p = pa.slot_parent[j];
@@ -1259,8 +1275,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
     sA[sl] = pa.slot_A[j];
     sB[sl] = pa.slot_B[j];
     sP[sl] = local ? p - js0 : -1;
-    const int plam = pa.slot_plam[j];
-    sZ[sl] = (!local && plam >= 0) ? z[plam] : 0.0;  // z of an outside parent (top part)
+    sZ[sl] = (!local && p >= 0) ? pa.slot_z[p] : 0.0;  // an outside parent is a top slot
   }
   __syncthreads();
   for (int lv = lv0; lv < lv1; ++lv) {  // phase B, root level first, LDS only
@@ -1273,8 +1288,14 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
   }
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
     const int lam = pa.slot_lam[js0 + sl];
-    z[lam] = sZ[sl];
-    part += y[lam] * sZ[sl];
+    double zl = sZ[sl], yl = y[lam];
+    if (lin) {
+      zl -= c2 * z[lam];
+      yl -= c2 * r2[lam];
+      y[lam] = yl;
+    }
+    z[lam] = zl;
+    part += yl * zl;
   }
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
@@ -1285,8 +1306,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
     ChainLane<W, CPL> ch;
     ch.setup(pa, c, active);
     const int up = active ? pa.chain_up[c] : -1, lo = active ? pa.chain_lo[c] : -1;
-    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : z[pa.slot_lam[up]];
-    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : z[pa.slot_lam[lo]];
+    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : pa.slot_z[up];
+    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : pa.slot_z[lo];
     const double T = ch.T, iT = 1.0 / T;
     double rc[CPL], a[CPL], b[CPL];
     double sa = 0.0, sb = 0.0;
@@ -1309,16 +1330,30 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
       pb_ += b[t];
       if (!ch.valid[t]) continue;
       const double Dk = ch.D[t];
-      const double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      double rk = rc[t];
+      if (lin) {
+        zk -= c2 * z[ch.dof_c[t]];
+        rk -= c2 * r2[ch.dof_c[t]];
+        y[ch.dof_c[t]] = rk;
+      }
       z[ch.dof_c[t]] = zk;
-      part += rc[t] * zk;
-      const double rq = y[ch.dof_q[t]];
+      part += rk * zk;
+      double rq = y[ch.dof_q[t]];
+      if (lin) {
+        rq -= c2 * r2[ch.dof_q[t]];
+        y[ch.dof_q[t]] = rq;
+      }
       const double zq = rq / ch.rho[t];
       z[ch.dof_q[t]] = zq;
       part += rq * zq;
     }
     if (ch.has_last) {
-      const double rq = y[ch.dof_qN];
+      double rq = y[ch.dof_qN];
+      if (lin) {
+        rq -= c2 * r2[ch.dof_qN];
+        y[ch.dof_qN] = rq;
+      }
       const double zq = rq / ch.rhoN;
       z[ch.dof_qN] = zq;
       part += rq * zq;
@@ -1332,12 +1367,25 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa,
 // coarse slots take their coarse value -- and the partial r.z of the top slots.
 constexpr int kCapCoarse = 2048;
 
-__global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, const double* __restrict__ y,
+__global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __restrict__ y,
+                                                           const double* __restrict__ r2,
                                                            double* __restrict__ z,
-                                                           const MrState* __restrict__ st,
+                                                           MrState* __restrict__ st,
                                                            double* __restrict__ partB, int mode) {
   __shared__ double sD[kCapCoarse], sJ[kCapCoarse], sZ[kCapCoarse];
   if (mode == 0 && st->done) return;
+  // linear form: alpha arrived with the coarse partials; the Lanczos step is completed here
+  double c2 = 0.0;
+  const bool lin = pa.lin && mode == 0;
+  if (lin) {
+    const double alfa = pa.xalpha[0];
+    c2 = alfa / st->beta;
+    __syncthreads();  // every thread has read st->beta before thread 0 updates st
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->alfa = alfa;
+      st->nb += 1;
+    }
+  }
   const int nC = pa.n_coarse;
   const double* __restrict__ G = pa.cbuf + 2 * nC;
   for (int i = threadIdx.x; i < nC; i += kTopThreads) {
@@ -1377,11 +1425,18 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, const doub
       } else {
         const int p = pa.slot_parent[j];
         double num = pa.slot_J[j];
-        if (p >= 0) num += z[pa.slot_lam[p]] / pa.chain_T[pa.slot_pchain[j]];
+        if (p >= 0) num += pa.slot_z[p] / pa.chain_T[pa.slot_pchain[j]];
         zj = num / pa.slot_D[j];
       }
+      pa.slot_z[j] = zj;
+      double yl = y[lam];
+      if (lin) {  // ghost slots: y = r2 = 0 and the halo overwrites z
+        zj -= c2 * z[lam];
+        yl -= c2 * r2[lam];
+        y[lam] = yl;
+      }
       z[lam] = zj;
-      part += y[lam] * zj;  // ghost slots: y = 0
+      part += yl * zj;
     }
     __syncthreads();
   }
@@ -1617,12 +1672,12 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
     return;
   }
   if (coarse)
-    hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, h->z, st,
-                       h->partB, mode);
+    hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2, h->z,
+                       st, h->partB, mode);
   if (h->pc_jobs > 0) {
     if (h->pc_lds)
       hipLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
-                         h->stream, h->pa, y, h->z, st, h->partB, mode);
+                         h->stream, h->pa, y, r2, h->z, st, h->partB, mode);
     else
       hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
                          h->pa, y, h->z, st, h->partB, mode);
@@ -1643,6 +1698,12 @@ void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState*
 
 int nB_of(const nx_network* h) { return h->pc ? h->pc_jobs + 1 : h->nB; }
 
+bool team_lin(const Team& t) {
+  const nx_network* h = t.hs[0];
+  return team_multi(t) && h->pc && h->pa.n_coarse > 0 && h->pa.lin;
+}
+
+
 // Whole preconditioner application for every rank of the team, with the coarse exchange.
 int team_pc(const Team& t, int64_t k, int mode) {
   const bool multi = team_multi(t);
@@ -1657,18 +1718,21 @@ int team_pc(const Team& t, int64_t k, int mode) {
       else launch_pc<false>(h, y, r2, st, other, mode, half);
     }
     if (half == 0 && multi && t.hs[0]->pa.n_coarse > 0)
-      CHECK(team_allreduce(t, -1, 3 * t.hs[0]->pa.n_coarse));
+      CHECK(team_allreduce(t, -1, 3 * t.hs[0]->pa.n_coarse + (team_lin(t) ? 1 : 0)));
   }
   return NX_OK;
 }
 
 int team_reduce_slot(const Team& t, bool from_a, int slot) {
+  // linear form: alpha's partial goes into the coarse buffer and is reduced with it
+  const bool to_coarse = from_a && slot == 0 && team_lin(t);
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
     hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream,
-                       from_a ? h->partA : h->partB, from_a ? h->nA : nB_of(h), h->red, slot);
+                       from_a ? h->partA : h->partB, from_a ? h->nA : nB_of(h),
+                       to_coarse ? h->pa.cbuf + 3 * h->pa.n_coarse : h->red, to_coarse ? 0 : slot);
   }
-  return team_allreduce(t, slot, 1);
+  return to_coarse ? NX_OK : team_allreduce(t, slot, 1);
 }
 
 // One MINRES iteration of every rank on the stream; `k` = 1-based iteration index.
@@ -2334,6 +2398,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.slot_J = scratch(n_slots);
   pa.slot_A = scratch(n_slots);
   pa.slot_B = scratch(n_slots);
+  pa.slot_z = scratch(n_slots);
+  pa.lin = 0;
   for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
                         (const void*)pa.chain_lo, (const void*)pa.slot_lam, (const void*)pa.slot_pchain,
                         (const void*)pa.slot_parent, (const void*)pa.slot_dc_off, (const void*)pa.slot_dc,
@@ -2341,7 +2407,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
                         (const void*)pa.lvl_slot_off, (const void*)pa.top_lvl_off,
                         (const void*)pa.chain_T, (const void*)pa.chain_It, (const void*)pa.chain_Ib,
                         (const void*)pa.slot_D, (const void*)pa.slot_J, (const void*)pa.dc_lo,
-                        (const void*)pa.slot_plam, (const void*)pa.slot_A, (const void*)pa.slot_B})
+                        (const void*)pa.slot_plam, (const void*)pa.slot_A, (const void*)pa.slot_B,
+                        (const void*)pa.slot_z})
     if (p == nullptr) return fail(NX_ERR_HIP, "preconditioner upload failed");
   if (!h->z) CHECK(dalloc(&h->z, std::max<int64_t>(h->n_col, 1)));
   if (!h->vv) CHECK(dalloc(&h->vv, std::max<int64_t>(h->n_own, 1)));
@@ -2434,10 +2501,15 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   pa.c_child_off = up(c_child_off, n_coarse + 1);
   pa.c_child = up(ncl ? c_child : nullptr, ncl);
   pa.c_lvl_off = up(c_lvl_off, n_clvl + 1);
-  double* cb = nullptr;
-  HIPCALL(hipMalloc((void**)&cb, sizeof(double) * 3 * n_coarse));
+  double* cb = nullptr;  // [D | J | G | alpha]
+  HIPCALL(hipMalloc((void**)&cb, sizeof(double) * (3 * n_coarse + 1)));
+  HIPCALL(hipMemset(cb, 0, sizeof(double) * (3 * n_coarse + 1)));
   h->pc_bufs.push_back(cb);
   pa.cbuf = cb;
+  pa.xalpha = cb + 3 * n_coarse;
+  // linear form needs the LDS kernels; NXHIP_PC_LIN=0 keeps alpha's own all-reduce
+  pa.lin = h->pc_lds ? 1 : 0;
+  if (const char* e = std::getenv("NXHIP_PC_LIN")) pa.lin = pa.lin && std::atoi(e) != 0;
   for (const void* q : {(const void*)pa.slot_cidx, (const void*)pa.cc_chain, (const void*)pa.cc_top,
                         (const void*)pa.cc_bot, (const void*)pa.c_parent, (const void*)pa.c_child_off,
                         (const void*)pa.c_child, (const void*)pa.c_lvl_off})

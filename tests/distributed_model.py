@@ -109,10 +109,13 @@ def minres(A_local, b_local, n_own: int, halo, allreduce, rtol=1e-12, maxit=5000
     return x, it, relres
 
 
-def minres_pc(A_local, b_local, n_own: int, halo, allreduce, apply_pc, rtol=1e-12, maxit=5000):
+def minres_pc(A_local, b_local, n_own: int, halo, allreduce, apply_pc, rtol=1e-12, maxit=5000,
+              linear: bool = False):
     """Preconditioned MINRES (scipy's statement order) with a rank-local SPD
     preconditioner ``apply_pc(r_owned) -> z_owned``; ``halo`` fills ghost slots of the
-    gathered vector (z), as the device does before each SpMV."""
+    gathered vector (z), as the device does before each SpMV. ``linear`` models the
+    device's multi-rank form: the preconditioner is applied to y before alpha is known
+    and z' = P^{-1}y - (alpha/beta) z (csrc/nxhip.hip, PcArgs::lin)."""
     n_col = A_local.shape[1]
     r1 = b_local.copy()
     r2 = b_local.copy()
@@ -132,11 +135,14 @@ def minres_pc(A_local, b_local, n_own: int, halo, allreduce, apply_pc, rtol=1e-1
         y = s * (A_local @ z)
         if it >= 2:
             y = y - (beta / oldb) * r1
+        if linear:
+            py = apply_pc(y)  # before alpha (its partial travels with the coarse exchange)
         alfa = allreduce(float(v @ y))
         y = y - (alfa / beta) * r2
         r1, r2 = r2, y
+        z_old = z[:n_own].copy()
         z = np.zeros(n_col)
-        z[:n_own] = apply_pc(r2)
+        z[:n_own] = py - (alfa / beta) * z_old if linear else apply_pc(r2)
         oldb, beta = beta, np.sqrt(allreduce(float(r2 @ z[:n_own])))
         oldeps = epsln
         delta = cs * dbar + sn * alfa

@@ -91,6 +91,30 @@ def test_group_solve_matches_direct(case, P, pc):
         grp.close()
 
 
+@pytest.mark.parametrize("env", [{"NXHIP_PC_LIN": "0"}, {"NXHIP_PC_GLOBAL": "1"}])
+def test_group_alternative_kernel_paths(env, monkeypatch):
+    """alpha with its own all-reduce (NXHIP_PC_LIN=0) and the global-memory preconditioner
+    kernels (NXHIP_PC_GLOBAL=1) on several ranks."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    case, P = "depth6_N40", 4
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.assemble()
+        it, relres, conv = grp.solve(1e-12, 50000, 32)
+        assert conv
+        x = np.zeros(Ab.shape[0])
+        for a, xl in zip(grp.assemblers, grp.solutions()):
+            x[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
+        assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+        assert it <= _single_iterations(mesh, pbc, True) + 2
+    finally:
+        grp.close()
+
+
 def test_group_large_tree_iterations_flat():
     """Depth-10 binary tree (N=15, ~61k DoF) on 8 ranks: same iteration count as 1 rank
     (block-Jacobi grounding of the cuts would need ~5x more)."""

@@ -176,11 +176,12 @@ def test_distributed_minres_model(P):
     assert np.linalg.norm(x - xg_ref) / np.linalg.norm(xg_ref) < 1e-10
 
 
+@pytest.mark.parametrize("linear", [False, True])
 @pytest.mark.parametrize("case,P", [("depth6_N40", 1), ("depth6_N40", 2), ("depth6_N40", 4),
                                     ("depth6_N40", 8), ("arterial5_N40", 3),
                                     ("edge_info_N10", 2), ("tree6_2d_N70", 5),
                                     ("linear_alt_N3", 3), ("double_Y_N5", 2)])
-def test_distributed_preconditioned_minres_model(case, P):
+def test_distributed_preconditioned_minres_model(case, P, linear):
     """Multi-rank preconditioned MINRES with the coarse step: each rank condenses its
     pieces into the coarse junctions, the partials are summed (one vector all-reduce),
     every rank solves the coarse forest. The preconditioner is the exact single-rank one,
@@ -215,7 +216,7 @@ def test_distributed_preconditioned_minres_model(case, P):
 
         results[r] = DM.minres_pc(Al, bb[rows], lp.n_own, halo=lambda v: comm.halo(r, v),
                                   allreduce=lambda v: comm.allreduce(r, v),
-                                  apply_pc=apply_pc, rtol=1e-13)
+                                  apply_pc=apply_pc, rtol=1e-13, linear=linear)
 
     threads = [threading.Thread(target=run, args=(r,)) for r in range(P)]
     for t in threads:
