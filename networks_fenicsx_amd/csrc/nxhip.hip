@@ -1456,6 +1456,13 @@ struct GroupPtrs {
   double* p[kMaxGroup];
 };
 
+// dst[r][q] = src[q][0] for all ranks r, q (the group's point-to-point all-gather of one
+// double per rank)
+__global__ void k_group_gather(GroupPtrs src, GroupPtrs dst, int P) {
+  const int i = threadIdx.x;
+  if (i < P * P) dst.p[i / P][i % P] = src.p[i % P][0];
+}
+
 __global__ void k_group_sum(GroupPtrs g, int P, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     double s = 0.0;
@@ -1538,6 +1545,10 @@ struct nx_network {
   std::vector<int> peer_src_off;  // group: offset of my segment in each peer's send_buf
   int* send_idx = nullptr;
   double* send_buf = nullptr;
+  // beta^2 partials of all ranks (nranks), gathered point-to-point with the halo so the
+  // iteration needs no separate all-reduce for it (NXHIP_BETA_P2P=0: all-reduce instead)
+  double* gath = nullptr;
+  bool beta_p2p = true;
 };
 
 struct nx_group {
@@ -1587,7 +1598,7 @@ double* vec_of(nx_network* h, VecSel s, int64_t k) {
 }
 
 // fill the ghost slots of the selected vector (n_col) from the owning ranks
-int team_halo(const Team& t, VecSel sel, int64_t k) {
+int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false) {
   if (!team_multi(t)) return NX_OK;
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
@@ -1608,12 +1619,30 @@ int team_halo(const Team& t, VecSel sel, int64_t k) {
                                  sizeof(double) * cnt, hipMemcpyDeviceToDevice, h->stream));
       }
     }
+    if (beta) {
+      GroupPtrs src{}, dst{};
+      for (int r = 0; r < t.P; ++r) {
+        src.p[r] = t.hs[r]->red + 1;
+        dst.p[r] = t.hs[r]->gath;
+      }
+      hipLaunchKernelGGL(k_group_gather, dim3(1), dim3(256), 0, t.hs[0]->stream, src, dst, t.P);
+    }
     return NX_OK;
   }
   nx_network* h = t.hs[0];
-  if (h->peers.empty()) return NX_OK;
+  if (h->peers.empty() && !beta) return NX_OK;
   double* v = vec_of(h, sel, k);
+  if (beta)
+    HIPCALL(hipMemcpyAsync(h->gath + h->rank, h->red + 1, sizeof(double), hipMemcpyDeviceToDevice,
+                           h->stream));
   NCCLCALL(ncclGroupStart());
+  if (beta) {  // beta^2 partial to / from every other rank
+    for (int q = 0; q < h->nranks; ++q) {
+      if (q == h->rank) continue;
+      NCCLCALL(ncclSend(h->red + 1, 1, ncclDouble, q, h->comm, h->stream));
+      NCCLCALL(ncclRecv(h->gath + q, 1, ncclDouble, q, h->comm, h->stream));
+    }
+  }
   for (size_t p = 0; p < h->peers.size(); ++p) {
     const int sc = h->send_off[p + 1] - h->send_off[p];
     const int rc = h->recv_off[p + 1] - h->recv_off[p];
@@ -1723,7 +1752,7 @@ int team_pc(const Team& t, int64_t k, int mode) {
   return NX_OK;
 }
 
-int team_reduce_slot(const Team& t, bool from_a, int slot) {
+int team_reduce_slot(const Team& t, bool from_a, int slot, bool allreduce = true) {
   // linear form: alpha's partial goes into the coarse buffer and is reduced with it
   const bool to_coarse = from_a && slot == 0 && team_lin(t);
   for (int r = 0; r < t.P; ++r) {
@@ -1732,14 +1761,16 @@ int team_reduce_slot(const Team& t, bool from_a, int slot) {
                        from_a ? h->partA : h->partB, from_a ? h->nA : nB_of(h),
                        to_coarse ? h->pa.cbuf + 3 * h->pa.n_coarse : h->red, to_coarse ? 0 : slot);
   }
-  return to_coarse ? NX_OK : team_allreduce(t, slot, 1);
+  return (to_coarse || !allreduce) ? NX_OK : team_allreduce(t, slot, 1);
 }
 
 // One MINRES iteration of every rank on the stream; `k` = 1-based iteration index.
 int launch_iteration(const Team& t, int64_t k) {
   const bool multi = team_multi(t);
   const bool pc = t.hs[0]->pc;
-  if (multi) CHECK(team_halo(t, pc ? VS_Z : VS_R2, k));
+  // beta^2 of the previous iteration travels with the halo (point-to-point gather)
+  const bool p2p_beta = multi && t.hs[0]->beta_p2p;
+  if (multi) CHECK(team_halo(t, pc ? VS_Z : VS_R2, k, p2p_beta));
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
     double* r1 = h->vb[(k - 1) & 1];
@@ -1758,8 +1789,9 @@ int launch_iteration(const Team& t, int64_t k) {
     hipEvent_t e1 = prof ? h->ev_pool[2 * h->prof_k + 1] : nullptr;
 #define NX_LAUNCH_A(M, P)                                                                        \
   hipExtLaunchKernelGGL((k_mr_a<M, P>), dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,     \
-                        csr_of(h), mv, sin, sout, h->partB, nB, h->red, h->partA, h->chunksA)
-    if (multi) {
+                        csr_of(h), mv, sin, sout, p2p_beta ? h->gath : h->partB,              \
+                        p2p_beta ? h->nranks : nB, h->red, h->partA, h->chunksA)
+    if (multi && !p2p_beta) {
       if (pc) NX_LAUNCH_A(true, true); else NX_LAUNCH_A(true, false);
     } else {
       if (pc) NX_LAUNCH_A(false, true); else NX_LAUNCH_A(false, false);
@@ -1785,7 +1817,7 @@ int launch_iteration(const Team& t, int64_t k) {
                            r2, sout, sin, h->partA, h->nA, h->red, h->partB);
     }
   }
-  if (multi) CHECK(team_reduce_slot(t, false, 1));
+  if (multi) CHECK(team_reduce_slot(t, false, 1, !p2p_beta));
   HIPCALL(hipGetLastError());
   return NX_OK;
 }
@@ -1980,7 +2012,7 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
                   h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
                   h->partA,  h->partB,   h->red,
-                  h->send_idx, h->send_buf};
+                  h->send_idx, h->send_buf, h->gath};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -2561,6 +2593,12 @@ NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_
   h->send_buf = nullptr;
   CHECK(upload(&h->send_idx, send_idx, nsend, h->stream));
   CHECK(dalloc(&h->send_buf, nsend));
+  if (h->gath) HIPCALL(hipFree(h->gath));
+  h->gath = nullptr;
+  CHECK(dalloc(&h->gath, nranks));
+  HIPCALL(hipMemsetAsync(h->gath, 0, sizeof(double) * nranks, h->stream));
+  h->beta_p2p = true;
+  if (const char* e = std::getenv("NXHIP_BETA_P2P")) h->beta_p2p = std::atoi(e) != 0;
   h->nranks = nranks;
   h->rank = rank;
   h->have_plan = true;

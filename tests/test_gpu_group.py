@@ -91,7 +91,8 @@ def test_group_solve_matches_direct(case, P, pc):
         grp.close()
 
 
-@pytest.mark.parametrize("env", [{"NXHIP_PC_LIN": "0"}, {"NXHIP_PC_GLOBAL": "1"}])
+@pytest.mark.parametrize("env", [{"NXHIP_PC_LIN": "0"}, {"NXHIP_PC_GLOBAL": "1"},
+                                 {"NXHIP_BETA_P2P": "0"}])
 def test_group_alternative_kernel_paths(env, monkeypatch):
     """alpha with its own all-reduce (NXHIP_PC_LIN=0) and the global-memory preconditioner
     kernels (NXHIP_PC_GLOBAL=1) on several ranks."""
