@@ -132,3 +132,30 @@ def test_group_large_tree_iterations_flat():
         assert it <= it1 + 2, (it, it1)
     finally:
         grp.close()
+
+
+@pytest.mark.parametrize("pc", [True, False])
+def test_rccl_single_rank_communicator(pc):
+    """A one-rank RCCL communicator drives the RCCL transport code (unique id, comm init,
+    ncclAllReduce, grouped send/recv, eager launches, the multi-rank kernel variants) on
+    one GPU; results must equal the single-handle solve."""
+    from networks_fenicsx_amd import _lib
+
+    make, N, strategy, pbc = CASES["depth6_N40"]
+    G, mesh, Ab, bb, x_ref = _reference("depth6_N40")
+    asm = HydraulicNetworkAssembler(mesh)
+    try:
+        lp = asm.local_problem
+        asm.handle.comm_init(1, 0, _lib.comm_unique_id(), lp.peers, lp.send_off, lp.send_idx,
+                             lp.recv_off)
+        asm.set_preconditioner(pc)
+        asm.compute_forms(p_bc_ex=pbc)
+        asm.assemble()
+        it, relres, conv = asm.handle.solve(1e-12, 50000, 32)
+        assert conv
+        x = asm.handle.solution()
+        assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+        assert it <= _single_iterations(mesh, pbc, pc) + 2
+        assert asm.handle.true_residual() < 1e-9
+    finally:
+        asm.close()
