@@ -8,6 +8,7 @@ directory (built in-tree by :mod:`networks_fenicsx_amd.build`).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 from pathlib import Path
 
@@ -15,7 +16,7 @@ import numpy as np
 
 __all__ = ["lib", "NxError", "NxNotConverged", "check", "Handle", "Group", "EXPORTED_SYMBOLS"]
 
-_LIB_PATH = Path(__file__).resolve().parent / "libnxhip.so"
+_LIB_PATH = Path(os.environ.get("NXHIP_LIB") or Path(__file__).resolve().parent / "libnxhip.so")
 _lock = threading.Lock()
 _lib = None
 

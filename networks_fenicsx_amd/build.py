@@ -33,11 +33,14 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in (SRC, HEADER))
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile ``csrc/nxhip.hip`` into ``libnxhip.so`` (skipped when up to date)."""
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, phase_timing: bool = False) -> Path:
+    """Compile ``csrc/nxhip.hip`` into ``libnxhip.so`` (skipped when up to date).
+    ``phase_timing`` builds the instrumented debug variant ``libnxhip_phase.so`` instead
+    (``-DNX_PHASE_TIMING``; scripts/phase_timing.py loads it via ``NXHIP_LIB``)."""
+    out = HERE / "libnxhip_phase.so" if phase_timing else LIB
+    if not phase_timing and not force and not needs_build():
         return LIB
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = out.with_suffix(".so.tmp")
     cmd = [
         _hipcc(),
         f"--offload-arch={ARCH}",
@@ -50,14 +53,14 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         str(tmp),
         str(SRC),
         "-lrccl",
-    ]
+    ] + (["-DNX_PHASE_TIMING"] if phase_timing else [])
     if verbose:
         print(" ".join(cmd))
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

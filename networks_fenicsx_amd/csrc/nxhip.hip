@@ -41,6 +41,50 @@ constexpr int kReduceThreads = 1024;
 
 thread_local std::string g_err;
 
+// Phase timing (debug builds only, -DNX_PHASE_TIMING: scripts/phase_timing.py). Workgroup 0
+// stamps wall_clock64() (100 MHz) at phase boundaries; every workgroup raises the latest
+// start / end of its kernel. Slot bases: k_mr_a 0, up 16, top 32, down 48, coarse 64.
+#ifdef NX_PHASE_TIMING
+__device__ unsigned long long g_phase[128];
+__device__ unsigned long long g_wgs[8][512];  // per-workgroup start / end, last launch wins
+__device__ unsigned long long g_wge[8][512];
+#define NX_PHASE(slot)                                           \
+  do {                                                           \
+    if (blockIdx.x == 0) {                                       \
+      __syncthreads();                                           \
+      if (threadIdx.x == 0) g_phase[(slot)] = wall_clock64();    \
+    }                                                            \
+  } while (0)
+#define NX_PHASE_START(base)                                                        \
+  do {                                                                              \
+    if (threadIdx.x == 0) {                                                         \
+      const unsigned long long t_ = wall_clock64();                                 \
+      if (blockIdx.x == 0) g_phase[(base)] = t_;                                    \
+      atomicMax(&g_phase[(base) + 14], t_);                                         \
+      if (blockIdx.x < 512) g_wgs[(base) / 16][blockIdx.x] = t_;                    \
+    }                                                                               \
+  } while (0)
+#define NX_PHASE_END(base)                                                          \
+  do {                                                                              \
+    __syncthreads();                                                                \
+    if (threadIdx.x == 0) {                                                         \
+      const unsigned long long t_ = wall_clock64();                                 \
+      atomicMax(&g_phase[(base) + 15], t_);                                         \
+      if (blockIdx.x < 512) g_wge[(base) / 16][blockIdx.x] = t_;                    \
+    }                                                                               \
+  } while (0)
+#else
+#define NX_PHASE(slot) \
+  do {                 \
+  } while (0)
+#define NX_PHASE_START(base) \
+  do {                       \
+  } while (0)
+#define NX_PHASE_END(base) \
+  do {                     \
+  } while (0)
+#endif
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -508,10 +552,12 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
                                                  const double* __restrict__ red,
                                                  double* __restrict__ partA, int chunksA) {
   if (sin->done) return;
+  NX_PHASE_START(0);
   MrState s = *sin;
   Rot rot{0.0, 0.0, 0.0, 0.0};
   const bool upd = s.nb > 0;  // a Lanczos step is waiting for its rotation
   if (upd) rot = mr_rotate(s, MULTI ? red[1] : block_allsum(partB, nB));
+  NX_PHASE(1);
   if (blockIdx.x == 0 && threadIdx.x == 0) *sout = s;
   const double beta = s.beta, oldb = s.oldb;  // beta_k, beta_{k-1}
   const double sc = 1.0 / beta;
@@ -543,7 +589,9 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
     }
     __syncthreads();  // LDS of spmv_row_sum is reused by the next chunk
   }
+  NX_PHASE(2);
   if (spmv) block_sum_store(part, partA + blockIdx.x);
+  NX_PHASE_END(0);
 }
 
 template <bool MULTI>
@@ -1022,6 +1070,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     }
   }
   const bool upd = mode == 0 && !(MULTI && pa.lin);
+  NX_PHASE_START(16);
   const int job = blockIdx.x;
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
@@ -1057,8 +1106,12 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       pa.chain_It[c] = sr - ib;
     }
   }
+  NX_PHASE(17);
   const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
-  if (lv1 == lv0) return;
+  if (lv1 == lv0) {
+    NX_PHASE_END(16);
+    return;
+  }
   const int js0 = pa.lvl_slot_off[lv0], js1 = pa.lvl_slot_off[lv1];
   const int ns = js1 - js0;
   const int dc0 = pa.slot_dc_off[js0];
@@ -1094,6 +1147,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   }
   if (threadIdx.x == 0) sOff[ns] = pa.slot_dc_off[js1] - dc0;
   __syncthreads();
+  NX_PHASE(18);
   for (int lv = lv1 - 1; lv >= lv0; --lv) {  // phase B, deepest level first
     for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kPcThreads) {
       const int sl = j - js0;
@@ -1119,6 +1173,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     pa.slot_A[j] = J / D;
     pa.slot_B[j] = pcn >= 0 ? 1.0 / (sT[pcn - c0] * D) : 0.0;
   }
+  NX_PHASE(19);
+  NX_PHASE_END(16);
 }
 
 template <bool MULTI>
@@ -1144,6 +1200,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
       c2 = alfa / st->beta;
     }
   }
+  NX_PHASE_START(32);
   const int nl = pa.n_top_lvl;
   const int ts0 = pa.top_lvl_off[0], ts1 = pa.top_lvl_off[nl];
   const int nt = ts1 - ts0;
@@ -1195,6 +1252,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   }
   if (threadIdx.x == 0) sOff[nt] = ndc;
   __syncthreads();
+  NX_PHASE(33);
   for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {  // phase A3: fold the fixed parts
     double D0 = sD0[sl], J0 = sJ0[sl];
     for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
@@ -1205,6 +1263,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     sJ0[sl] = J0;
   }
   __syncthreads();
+  NX_PHASE(34);
   for (int lv = nl - 1; lv >= 0; --lv) {
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
       const int sl = j - ts0;
@@ -1221,6 +1280,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     }
     __syncthreads();
   }
+  NX_PHASE(35);
   if (MULTI && pa.n_coarse > 0) {  // back-substitution after the exchange (k_pc_coarse)
     for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
       pa.slot_D[ts0 + sl] = sD[sl];
@@ -1242,11 +1302,13 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     }
     __syncthreads();
   }
+  NX_PHASE(36);
   for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {  // lower-job roots read these
     pa.slot_D[ts0 + sl] = sD[sl];
     pa.slot_J[ts0 + sl] = sJ[sl];
   }
   block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
+  NX_PHASE_END(32);
 }
 
 template <bool MULTI, int W, int CPL>
@@ -1261,6 +1323,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
   const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
+  NX_PHASE_START(48);
   const int job = blockIdx.x;
   double part = 0.0;
   const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
@@ -1278,6 +1341,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     sZ[sl] = (!local && p >= 0) ? pa.slot_z[p] : 0.0;  // an outside parent is a top slot
   }
   __syncthreads();
+  NX_PHASE(49);
   for (int lv = lv0; lv < lv1; ++lv) {  // phase B, root level first, LDS only
     for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kPcThreads) {
       const int sl = j - js0;
@@ -1297,6 +1361,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     z[lam] = zl;
     part += yl * zl;
   }
+  NX_PHASE(50);
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
   const int seg = threadIdx.x / W;
@@ -1359,7 +1424,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       part += rq * zq;
     }
   }
+  NX_PHASE(51);
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
+  NX_PHASE_END(48);
 }
 
 // Second half of the top part with several ranks: solve the coarse forest from the
@@ -2691,3 +2758,19 @@ NX_API int nx_group_destroy(nx_group_t* g) {
   delete g;
   return NX_OK;
 }
+
+#ifdef NX_PHASE_TIMING
+NX_API int nx_debug_phases(unsigned long long* out, int32_t n) {
+  if (!out || n < 1 || n > 128) return fail(NX_ERR_ARG, "bad argument");
+  HIPCALL(hipDeviceSynchronize());
+  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n));
+  return NX_OK;
+}
+
+NX_API int nx_debug_wg(unsigned long long* starts, unsigned long long* ends) {
+  HIPCALL(hipDeviceSynchronize());
+  HIPCALL(hipMemcpyFromSymbol(starts, HIP_SYMBOL(g_wgs), sizeof(unsigned long long) * 8 * 512));
+  HIPCALL(hipMemcpyFromSymbol(ends, HIP_SYMBOL(g_wge), sizeof(unsigned long long) * 8 * 512));
+  return NX_OK;
+}
+#endif

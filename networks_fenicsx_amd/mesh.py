@@ -114,8 +114,10 @@ class _Geometry:
 class IntervalMesh:
     """Interval mesh of the network: ``N`` cells per graph edge, source -> target."""
 
-    def __init__(self, comm: Comm, x: np.ndarray, cells: np.ndarray, gdim: int, tdim: int = 1):
+    def __init__(self, comm: Comm, x: np.ndarray, cells: np.ndarray, gdim: int, tdim: int = 1,
+                 network=None):
         self.comm = comm
+        self.network = network  # the NetworkMesh this mesh discretises
         self.geometry = _Geometry(x, gdim)
         n_vertices = int(np.unique(cells).size) if cells.size else 0
         self.topology = _Topology(tdim, {0: n_vertices, tdim: cells.shape[0]}, cells)
@@ -313,11 +315,20 @@ class NetworkMesh:
             idx[:, 1:N] = first[:, None] + np.arange(N - 1, dtype=np.int64)[None, :]
             idx[:, N] = self._dst
             cells = np.stack([idx[:, :-1], idx[:, 1:]], axis=2).reshape(-1, 2)
-        return IntervalMesh(self._comm, x, cells, self._geom_dim)
+        return IntervalMesh(self._comm, x, cells, self._geom_dim, network=self)
 
     def cell_lengths(self) -> np.ndarray:
         """Length of every cell, edge-major (``E * N``)."""
         return self.mesh.cell_lengths()
+
+    def local_edges(self) -> np.ndarray:
+        """Graph edges owned by this rank (the assembler's partition, ``layout.py``)."""
+        from .layout import partition_edges
+
+        if self._comm.size == 1:
+            return np.arange(self._src.size, dtype=np.int64)
+        owner = partition_edges(self._src, self._dst, self._pos.shape[0], self._comm.size)
+        return np.flatnonzero(owner == self._comm.rank)
 
     def tangents(self) -> np.ndarray:
         """Unit tangent of every cell (``E * N x 3``), source -> target of its edge."""

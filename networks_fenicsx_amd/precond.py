@@ -28,7 +28,7 @@ Device decomposition (csrc/nxhip.hip k_pc_up / k_pc_top / k_pc_down): the juncti
 is cut at a depth so that the *lower subtrees* (each processed by one workgroup, chains +
 junction levels) number a few hundred and the *top* part (all junctions above the cut,
 one workgroup, junction math only) stays small; chains whose lower end is in the top part
-are processed by extra chain-only jobs in the same kernels.
+are handed round-robin to the lower jobs (one workgroup per job, no extra launches).
 
 Graphs that are not trees use the same machinery on a spanning forest: a chain that
 would close a cycle is grounded at one end. ``P`` stays SPD (a grounded Laplacian block);
@@ -199,7 +199,8 @@ class TreePreconditioner:
     slot_dc: np.ndarray
     dc_lo: np.ndarray  # bottom slot of every slot_dc entry (-1 = ground), precomputed
     slot_plam: np.ndarray  # multiplier row of the parent slot, -1
-    # jobs: lower subtrees first (chains + junction levels), then chain-only jobs
+    # jobs: lower subtrees (chains + junction levels); chain-only jobs only when there is
+    # no lower subtree
     job_chain_off: np.ndarray  # n_jobs + 1
     job_lvl_off: np.ndarray  # n_jobs + 1, offsets into lvl_slot_off
     lvl_slot_off: np.ndarray  # slot offsets of every level (per job, root level first)
@@ -363,7 +364,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     slot_of = {v: i for i, v in enumerate(slots)}
 
     # chains: per lower job, the parent chains of its junctions + chains hanging from them
-    # (grounded / cycle-closing); then chain-only jobs for the rest (top part chains)
+    # (grounded / cycle-closing); the rest (top part chains) go round-robin to the jobs
     job_of_slot = np.full(len(slots), -1, dtype=np.int64)
     for j in range(len(job_roots)):
         a = lvl_slot_off[job_lvl_off[j]]
@@ -378,11 +379,17 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
             chain_job[e] = job_of_slot[slot_of[up]]
     n_lower = len(job_roots)
     rest = np.flatnonzero(chain_job < 0)
-    per_job = max(1, int(np.ceil(E / max(1, target_jobs)))) if E else 1
-    per_job = max(per_job, 16)
-    for i, e in enumerate(rest):
-        chain_job[e] = n_lower + i // per_job
-    n_jobs = n_lower + (int(np.ceil(rest.size / per_job)) if rest.size else 0)
+    if n_lower > 0:
+        # chains of the top part ride along with the lower jobs (round-robin): one
+        # workgroup per job and no extra jobs, so a launch has exactly n_lower
+        # workgroups (<= #CUs); two extra chain-only workgroups started ~10 us late on
+        # the GPU (scripts/phase_timing.py)
+        chain_job[rest] = np.arange(rest.size) % n_lower
+        n_jobs = n_lower
+    else:
+        per_job = max(16, int(np.ceil(E / max(1, target_jobs)))) if E else 1
+        chain_job[rest] = np.arange(rest.size) // per_job
+        n_jobs = int(np.ceil(rest.size / per_job)) if rest.size else 0
     order = np.lexsort((np.arange(E), chain_job))
     job_chain_off = np.searchsorted(chain_job[order], np.arange(n_jobs + 1)).astype(np.int32)
     # chain-only jobs have no levels
