@@ -143,6 +143,19 @@ int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
                           int32_t n_top_lvl, const int32_t* top_lvl_off);
 
 /*
+ * Dense top part (single rank): the down kernel computes the top junction values it
+ * needs as rows of G (inverse of the top tree Schur matrix, built once per solve) times
+ * the top inputs, which removes the one-workgroup top kernel from every iteration.
+ *   job_tslot_off/job_tslot  top slots each job updates and writes (round-robin)
+ *   job_need_off/job_need    top slots whose values each job reads (<= 64 per job)
+ * Ignored (kept off) with several ranks or when the LDS kernels are not in use;
+ * NXHIP_PC_DENSE=0 disables it. Call after nx_set_preconditioner.
+ */
+int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs, const int32_t* job_tslot_off,
+                    const int32_t* job_tslot, const int32_t* job_need_off,
+                    const int32_t* job_need);
+
+/*
  * Coarse step of the preconditioner on a partitioned problem (precond.py derives it): the
  * coarse junctions (interface junctions + the junctions on paths between them inside a
  * rank) form a forest that every rank solves redundantly from one all-reduce of

@@ -723,6 +723,16 @@ struct PcArgs {
   int lin;
   const double* xalpha;
   double* slot_z;  // P^{-1}y at every junction slot (written by the top part, read across jobs)
+  // dense top part (single rank, LDS kernels; precond.py: _dense_top_lists): G = inverse
+  // of the top tree Schur matrix (n_top^2, built once per solve by k_pc_gbuild); per job
+  // the top slots it updates / writes and the top slots whose values it needs
+  int dense;
+  int n_top;
+  const int* job_tslot_off;
+  const int* job_tslot;
+  const int* job_need_off;
+  const int* job_need;
+  double* G;
 };
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
@@ -1040,6 +1050,7 @@ constexpr int kCapDC = 768;   // down-chain entries per job
 constexpr int kCapT = 1152;   // top junction slots (host caps the top part at 1024)
 constexpr int kCapTDC = 2304; // top down-chain entries
 constexpr int kMaxTopLvl = 255;
+constexpr int kMaxNeed = 64;   // dense top: top values one job reads
 
 template <bool MULTI, int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __restrict__ y,
@@ -1107,6 +1118,12 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     }
   }
   NX_PHASE(17);
+  if (!MULTI && pa.dense && upd) {  // the top kernel does not run: update the job's top rows
+    for (int i = pa.job_tslot_off[job] + threadIdx.x; i < pa.job_tslot_off[job + 1]; i += kPcThreads) {
+      const int lam = pa.slot_lam[pa.job_tslot[i]];
+      y[lam] -= c2 * r2[lam];
+    }
+  }
   const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
   if (lv1 == lv0) {
     NX_PHASE_END(16);
@@ -1319,6 +1336,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
                                                             double* __restrict__ partB, int mode) {
   __shared__ double sZ[kCapS], sA[kCapS], sB[kCapS];
   __shared__ int sP[kCapS];
+  __shared__ double sTa[kCapT];  // dense top: a_s of every top slot
+  __shared__ int sNs[kMaxNeed];
+  __shared__ double sNz[kMaxNeed];
   if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
@@ -1330,6 +1350,58 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
   const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
   const int ns = js1 - js0;
+  // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
+  const bool dense = !MULTI && pa.dense && mode == 0;
+  int nneed = 0;
+  if (dense) {
+    const int ts0 = pa.top_lvl_off[0], nt = pa.n_top;
+    for (int sl = threadIdx.x; sl < nt; sl += kPcThreads) {  // a_s (y holds r' already)
+      const int j = ts0 + sl;
+      const int pcn = pa.slot_pchain[j];
+      double a = y[pa.slot_lam[j]] + (pcn >= 0 ? pa.chain_Ib[pcn] : 0.0);
+      for (int i = pa.slot_dc_off[j]; i < pa.slot_dc_off[j + 1]; ++i) {
+        const int c = pa.slot_dc[i];
+        const int lo = pa.dc_lo[i];
+        a += pa.chain_It[c];
+        if (lo >= 0 && lo < ts0) a += pa.slot_J[lo] / pa.chain_T[c] / pa.slot_D[lo];
+      }
+      sTa[sl] = a;
+    }
+    const int n0 = pa.job_need_off[job];
+    nneed = pa.job_need_off[job + 1] - n0;
+    __syncthreads();
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    for (int k = wv; k < nneed; k += kPcThreads / 64) {  // one wave per needed row
+      const int t = pa.job_need[n0 + k];
+      const double* __restrict__ g = pa.G + (int64_t)(t - ts0) * nt;
+      double acc = 0.0;
+      for (int sl = ln; sl < nt; sl += 64) acc += g[sl] * sTa[sl];
+      acc = wave_sum(acc);
+      if (ln == 0) {
+        sNs[k] = t;
+        sNz[k] = acc;
+      }
+    }
+    __syncthreads();
+    // the job's own top rows: z and their share of r'.z
+    for (int i = pa.job_tslot_off[job] + threadIdx.x; i < pa.job_tslot_off[job + 1]; i += kPcThreads) {
+      const int t = pa.job_tslot[i];
+      double zt = 0.0;
+      for (int k = 0; k < nneed; ++k)
+        if (sNs[k] == t) zt = sNz[k];
+      const int lam = pa.slot_lam[t];
+      z[lam] = zt;
+      part += y[lam] * zt;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) partB[pa.n_jobs] = 0.0;  // no top kernel
+  }
+  auto outside = [&](int t) -> double {  // value of a top slot (outside this job)
+    if (!dense) return pa.slot_z[t];
+    double v = 0.0;
+    for (int k = 0; k < nneed; ++k)
+      if (sNs[k] == t) v = sNz[k];
+    return v;
+  };
   // phase A: every slot's A, B, parent (local index, or the parent's value for the root)
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
     const int j = js0 + sl;
@@ -1338,7 +1410,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     sA[sl] = pa.slot_A[j];
     sB[sl] = pa.slot_B[j];
     sP[sl] = local ? p - js0 : -1;
-    sZ[sl] = (!local && p >= 0) ? pa.slot_z[p] : 0.0;  // an outside parent is a top slot
+    sZ[sl] = (!local && p >= 0) ? outside(p) : 0.0;  // an outside parent is a top slot
   }
   __syncthreads();
   NX_PHASE(49);
@@ -1371,8 +1443,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     ChainLane<W, CPL> ch;
     ch.setup(pa, c, active);
     const int up = active ? pa.chain_up[c] : -1, lo = active ? pa.chain_lo[c] : -1;
-    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : pa.slot_z[up];
-    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : pa.slot_z[lo];
+    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : outside(up);
+    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : outside(lo);
     const double T = ch.T, iT = 1.0 / T;
     double rc[CPL], a[CPL], b[CPL];
     double sa = 0.0, sb = 0.0;
@@ -1427,6 +1499,37 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   NX_PHASE(51);
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
   NX_PHASE_END(48);
+}
+
+// Dense top: column s of G = response of the top part to a unit J at top slot s (J up the
+// ancestors with kappa = g_up / D, then the root-to-leaf back-substitution). One wave per
+// column; once per solve (D is fixed by the assembly).
+__global__ __launch_bounds__(64) void k_pc_gbuild(PcArgs pa) {
+  __shared__ double sJ[kCapT], sZ[kCapT];
+  const int nt = pa.n_top, ts0 = pa.top_lvl_off[0];
+  const int s = blockIdx.x;
+  for (int i = threadIdx.x; i < nt; i += 64) sJ[i] = 0.0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double J = 1.0;
+    int t = ts0 + s;
+    sJ[s] = 1.0;
+    for (int p = pa.slot_parent[t]; p >= ts0; t = p, p = pa.slot_parent[t]) {
+      J = J / pa.chain_T[pa.slot_pchain[t]] / pa.slot_D[t];
+      sJ[p - ts0] = J;
+    }
+  }
+  __syncthreads();
+  for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
+    for (int u = pa.top_lvl_off[lv] + threadIdx.x; u < pa.top_lvl_off[lv + 1]; u += 64) {
+      const int p = pa.slot_parent[u];
+      double num = sJ[u - ts0];
+      if (p >= ts0) num += sZ[p - ts0] / pa.chain_T[pa.slot_pchain[u]];
+      sZ[u - ts0] = num / pa.slot_D[u];
+    }
+    __syncthreads();
+  }
+  for (int t = threadIdx.x; t < nt; t += 64) pa.G[(int64_t)t * nt + s] = sZ[t];
 }
 
 // Second half of the top part with several ranks: solve the coarse forest from the
@@ -1756,8 +1859,9 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
       if (h->pc_jobs > 0)
         hipLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
                            h->stream, h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
-      hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa,
-                         y, r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
+      if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
+        hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream,
+                           h->pa, y, r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
     } else {
       if (h->pc_jobs > 0)
         hipLaunchKernelGGL((k_pc_up<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
@@ -1788,6 +1892,9 @@ void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState*
     case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode, half); break;
     case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode, half); break;
     case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode, half); break;
+    case 5: launch_pc_wc<MULTI, 8, 2>(h, y, r2, st, other, mode, half); break;
+    case 6: launch_pc_wc<MULTI, 4, 4>(h, y, r2, st, other, mode, half); break;
+    case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half); break;
     default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half); break;
   }
 }
@@ -2184,6 +2291,11 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   }
   if (t.hs[0]->pc) {  // beta_1^2 = b . P^{-1} b
     CHECK(team_pc(t, 0, 1));
+    for (int r = 0; r < t.P; ++r) {  // dense top: G from this assembly's D (fixed per solve)
+      nx_network* h = t.hs[r];
+      if (h->pa.dense && !multi)
+        hipLaunchKernelGGL(k_pc_gbuild, dim3(h->pa.n_top), dim3(64), 0, h->stream, h->pa);
+    }
   } else {
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
@@ -2424,6 +2536,11 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   else if (N <= 128) variant = 3;
   else if (N <= 256) variant = 4;
   else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 256 cells per edge");
+  if (const char* e = std::getenv("NXHIP_PC_VARIANT")) {  // tuning: (W, CPL) override
+    const int v = std::atoi(e);
+    const int cap[8] = {16, 32, 64, 128, 256, 16, 16, 32};
+    if (v >= 0 && v < 8 && N <= cap[v]) variant = v;
+  }
   if (n_chains != h->E) return fail(NX_ERR_ARG, "one chain per local edge expected");
   // one slot per owned multiplier, plus (several ranks) the ghost junctions at the ends of
   // local edges, which are coarse (nx_set_coarse)
@@ -2499,6 +2616,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.slot_B = scratch(n_slots);
   pa.slot_z = scratch(n_slots);
   pa.lin = 0;
+  pa.dense = 0;
   for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
                         (const void*)pa.chain_lo, (const void*)pa.slot_lam, (const void*)pa.slot_pchain,
                         (const void*)pa.slot_parent, (const void*)pa.slot_dc_off, (const void*)pa.slot_dc,
@@ -2536,6 +2654,61 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->pc_variant = variant;
   h->pc_slots = n_slots;
   h->pc = true;
+  return NX_OK;
+}
+
+NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
+                           const int32_t* job_tslot_off, const int32_t* job_tslot,
+                           const int32_t* job_need_off, const int32_t* job_need) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  {
+    nx_network* hs[1] = {h};
+    CHECK(drop_graph(graph_slot(Team{hs, 1, nullptr})));
+  }
+  h->pa.dense = 0;
+  if (!enable) return NX_OK;
+  if (n_jobs != h->pc_jobs) return fail(NX_ERR_ARG, "n_jobs differs from the preconditioner's");
+  std::vector<int> top_off(h->pa.n_top_lvl + 1);
+  HIPCALL(hipMemcpy(top_off.data(), h->pa.top_lvl_off, sizeof(int) * top_off.size(),
+                    hipMemcpyDeviceToHost));
+  const int ts0 = top_off[0], nt = top_off.back() - top_off[0];
+  if (job_tslot_off[0] != 0 || job_need_off[0] != 0 || job_tslot_off[n_jobs] != nt)
+    return fail(NX_ERR_ARG, "job_tslot must cover the top slots once");
+  bool fits = true;  // a job reading more than kMaxNeed top values keeps the top kernel
+  for (int j = 0; j < n_jobs; ++j)
+    if (job_need_off[j + 1] - job_need_off[j] > kMaxNeed) fits = false;
+  for (int i = 0; i < nt; ++i)
+    if (job_tslot[i] < ts0 || job_tslot[i] >= ts0 + nt) return fail(NX_ERR_ARG, "job_tslot out of range");
+  for (int i = 0; i < job_need_off[n_jobs]; ++i)
+    if (job_need[i] < ts0 || job_need[i] >= ts0 + nt) return fail(NX_ERR_ARG, "job_need out of range");
+  // dense mode: single rank, LDS kernels, a top part that fits
+  if (!fits || h->nranks > 1 || !h->pc_lds || nt < 1 || nt > kCapT || n_jobs < 1) return NX_OK;
+  if (const char* e = std::getenv("NXHIP_PC_DENSE"))
+    if (std::atoi(e) == 0) return NX_OK;
+  auto up = [&](const int32_t* src, int64_t n) -> const int* {
+    int* d = nullptr;
+    if (n <= 0) n = 1;
+    if (hipMalloc((void**)&d, sizeof(int) * n) != hipSuccess) return nullptr;
+    h->pc_bufs.push_back(d);
+    if (hipMemcpy(d, src, sizeof(int) * n, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return d;
+  };
+  PcArgs& pa = h->pa;
+  pa.job_tslot_off = up(job_tslot_off, n_jobs + 1);
+  pa.job_tslot = up(job_tslot, nt);
+  pa.job_need_off = up(job_need_off, n_jobs + 1);
+  pa.job_need = up(job_need, std::max(1, job_need_off[n_jobs]));
+  double* G = nullptr;
+  HIPCALL(hipMalloc((void**)&G, sizeof(double) * (size_t)nt * nt));
+  h->pc_bufs.push_back(G);
+  pa.G = G;
+  if (!pa.job_tslot_off || !pa.job_tslot || !pa.job_need_off || !pa.job_need)
+    return fail(NX_ERR_HIP, "dense top upload failed");
+  pa.n_top = nt;
+  pa.dense = 1;
   return NX_OK;
 }
 

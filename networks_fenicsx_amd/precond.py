@@ -211,6 +211,14 @@ class TreePreconditioner:
     # coarse step (several ranks): coarse index of every slot (-1 = not coarse), the local
     # chains joining two coarse junctions (their top / bottom coarse index; the bottom one
     # is the child in the coarse forest and indexes its conductance), the global forest
+    # dense top part (single rank): the down workgroups compute the top junction values
+    # they need as z_t = sum_s G[t, s] a_s (G = inverse of the top part's tree Schur
+    # matrix, built once per solve). job_tslot: top slots whose multiplier row a job
+    # updates / writes (round-robin); job_need: top slots whose value a job reads
+    job_tslot_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
+    job_tslot: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    job_need_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
+    job_need: np.ndarray = field(default_factory=lambda: _EMPTY_I)
     n_coarse: int = 0
     slot_cidx: np.ndarray = field(default_factory=lambda: _EMPTY_I)
     cc_chain: np.ndarray = field(default_factory=lambda: _EMPTY_I)
@@ -427,6 +435,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         lvl_slot_off=np.asarray(lvl_slot_off, dtype=np.int32),
         top_lvl_off=np.asarray(top_lvl_off, dtype=np.int32), n_jobs=int(n_jobs),
         n_slots=n_slots)
+    _dense_top_lists(pc)
     if coarse is not None and coarse.n > 0:
         cid = coarse.cidx
         pc.n_coarse = coarse.n
@@ -440,6 +449,63 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         pc.c_child = coarse.child
         pc.c_lvl_off = coarse.lvl_off
     return pc
+
+
+def _dense_top_lists(pc: TreePreconditioner) -> None:
+    """Per job: the top slots it owns for updates (round-robin) and the top slots whose
+    values it reads (its root's parent, the top ends of its chains, its own top slots)."""
+    ts0, ts1 = int(pc.top_lvl_off[0]), int(pc.top_lvl_off[-1])
+    nj = pc.n_jobs
+    if nj == 0 or ts1 == ts0:
+        return
+    own: list[list[int]] = [[] for _ in range(nj)]
+    for i, t in enumerate(range(ts0, ts1)):
+        own[i % nj].append(t)
+    need: list[list[int]] = []
+    for j in range(nj):
+        ns = set(own[j])
+        for c in range(pc.job_chain_off[j], pc.job_chain_off[j + 1]):
+            for e in (pc.chain_up[c], pc.chain_lo[c]):
+                if e >= ts0:
+                    ns.add(int(e))
+        lv0, lv1 = pc.job_lvl_off[j], pc.job_lvl_off[j + 1]
+        for sl in range(pc.lvl_slot_off[lv0], pc.lvl_slot_off[lv1]) if lv1 > lv0 else []:
+            p = pc.slot_parent[sl]
+            if p >= ts0:
+                ns.add(int(p))
+        need.append(sorted(ns))
+    pc.job_tslot_off = np.zeros(nj + 1, dtype=np.int32)
+    np.cumsum([len(o) for o in own], out=pc.job_tslot_off[1:])
+    pc.job_tslot = np.array([t for o in own for t in o], dtype=np.int32)
+    pc.job_need_off = np.zeros(nj + 1, dtype=np.int32)
+    np.cumsum([len(n) for n in need], out=pc.job_need_off[1:])
+    pc.job_need = np.array([t for n in need for t in n], dtype=np.int32)
+
+
+def top_inverse_model(pc: TreePreconditioner, T: np.ndarray, Dj: np.ndarray) -> np.ndarray:
+    """G (n_top x n_top): column s = the top part's response to a unit J at top slot s
+    (J up the ancestors with kappa = g_up / D, then the root-to-leaf back-substitution),
+    i.e. the inverse of the top tree Schur matrix (k_pc_gbuild)."""
+    ts0, ts1 = int(pc.top_lvl_off[0]), int(pc.top_lvl_off[-1])
+    nt = ts1 - ts0
+    G = np.zeros((nt, nt))
+    lv = pc.top_lvl_off
+    for s in range(nt):
+        J = np.zeros(nt)
+        J[s] = 1.0
+        t = ts0 + s
+        while pc.slot_parent[t] >= ts0:  # ancestors inside the top part
+            p = pc.slot_parent[t]
+            J[p - ts0] += J[t - ts0] / T[pc.slot_pchain[t]] / Dj[t]
+            t = p
+        z = np.zeros(nt)
+        for li in range(lv.size - 1):
+            for u in range(lv[li], lv[li + 1]):
+                p = pc.slot_parent[u]
+                num = J[u - ts0] + (z[p - ts0] / T[pc.slot_pchain[u]] if p >= ts0 else 0.0)
+                z[u - ts0] = num / Dj[u]
+        G[:, s] = z
+    return G
 
 
 # ----------------------------------------------------------------------------- model

@@ -1,0 +1,81 @@
+"""Preconditioner host decomposition and its numpy model (CPU)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from cases import CASES
+from networks_fenicsx_amd import NetworkMesh
+from networks_fenicsx_amd import network_generation as ng
+from networks_fenicsx_amd.layout import build_local_problem
+from networks_fenicsx_amd.precond import (apply_model, build_tree_preconditioner, lumped_mass,
+                                          pc_finish_model, pc_up_model, top_inverse_model)
+from oracle import nx_oracle as O
+
+
+def _problem(G, N, strategy=None):
+    m = NetworkMesh(G, N=N, color_strategy=strategy)
+    src, dst = m.edges
+    P = O.build_problem(m.node_coordinates, src, dst, N, m.edge_colors)
+    A, b = O.assemble_reference(P, lambda x: x[1])
+    Ab, bb, perm, sign = O.to_build_layout(P, A, b)
+    lp = build_local_problem(m.node_coordinates, src, dst, m.degrees, N)
+    return m, Ab, lp
+
+
+@pytest.mark.parametrize("case", ["depth6_N40", "arterial5_N40", "tree6_2d_N70", "Y_N4"])
+@pytest.mark.parametrize("jobs", [4, 16, 256])
+def test_exact_schur_solve_on_trees(case, jobs):
+    """P^{-1} from the decomposition equals a direct solve of blockdiag(D, G^T D^-1 G)."""
+    make, N, strategy, _ = CASES[case]
+    m, Ab, lp = _problem(make(), N, strategy)
+    src, dst = m.edges
+    pc = build_tree_preconditioner(lp, src, dst, m.degrees, target_jobs=jobs)
+    dq = lumped_mass(Ab, lp)
+    n = Ab.shape[0]
+    per = 2 * N + 1
+    E = lp.edges.size
+    qrows = (np.arange(E)[:, None] * per + 2 * np.arange(N + 1)[None, :]).ravel()
+    other = np.setdiff1d(np.arange(n), qrows)
+    Dq = dq.ravel()
+    Gm = Ab[qrows][:, other].toarray()
+    S = Gm.T @ (Gm / Dq[:, None])
+    r = np.random.default_rng(3).standard_normal(n)
+    z = apply_model(pc, lp, dq, r)
+    np.testing.assert_allclose(z[qrows], r[qrows] / Dq, rtol=1e-13)
+    zs = np.linalg.solve(S, r[other])
+    assert np.linalg.norm(z[other] - zs) <= 1e-11 * np.linalg.norm(zs)
+
+
+@pytest.mark.parametrize("depth,jobs", [(6, 8), (8, 16), (9, 64)])
+def test_dense_top_inverse_matches_back_substitution(depth, jobs):
+    """z of the top slots = G a (k_pc_down's dense top) with a_s = J_s minus the top
+    children's eliminated contributions."""
+    m, Ab, lp = _problem(ng.make_tree(depth, depth, depth), 7)
+    src, dst = m.edges
+    pc = build_tree_preconditioner(lp, src, dst, m.degrees, target_jobs=jobs)
+    dq = lumped_mass(Ab, lp)
+    ts0, ts1 = int(pc.top_lvl_off[0]), int(pc.top_lvl_off[-1])
+    assert ts1 > ts0 and pc.n_jobs > 0
+    r = np.random.default_rng(1).standard_normal(lp.n_own)
+    st = pc_up_model(pc, lp, dq, r)
+    z = pc_finish_model(pc, lp, dq, st, st["partial"])
+    T, Dj, Jj = st["T"], st["Dj"], st["Jj"]
+    a = Jj[ts0:ts1].copy()
+    for t in range(ts0, ts1):
+        p = pc.slot_parent[t]
+        if p >= ts0:
+            a[p - ts0] -= Jj[t] / T[pc.slot_pchain[t]] / Dj[t]
+    G = top_inverse_model(pc, T, Dj)
+    zt = G @ a
+    np.testing.assert_allclose(zt, z[pc.slot_lam[ts0:ts1]], rtol=1e-12, atol=1e-14)
+    # every job's needed list covers its root's parent, its chain ends and its own slots
+    for j in range(pc.n_jobs):
+        need = set(pc.job_need[pc.job_need_off[j]:pc.job_need_off[j + 1]].tolist())
+        own = pc.job_tslot[pc.job_tslot_off[j]:pc.job_tslot_off[j + 1]].tolist()
+        assert set(own) <= need
+        for c in range(pc.job_chain_off[j], pc.job_chain_off[j + 1]):
+            for e in (pc.chain_up[c], pc.chain_lo[c]):
+                assert e < ts0 or e in need
+    assert sorted(pc.job_tslot.tolist()) == list(range(ts0, ts1))
