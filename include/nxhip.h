@@ -148,12 +148,19 @@ int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
  * the top inputs, which removes the one-workgroup top kernel from every iteration.
  *   job_tslot_off/job_tslot  top slots each job updates and writes (round-robin)
  *   job_need_off/job_need    top slots whose values each job reads (<= 64 per job)
+ *   top_uoff[n_top+1]        the top inputs a_s = sum of u[top_uoff[s] .. top_uoff[s+1]),
+ *                            posted by the up kernel at fixed places: slot_uy (y' of a top
+ *                            slot), chain_uit / chain_uib (I_top / I_bot of a chain, -1 =
+ *                            none), job_root_u (kappa J_root + I_top of the root's parent
+ *                            chain, kappa = dc entry job_root_dc) -- precond.py
  * Ignored (kept off) with several ranks or when the LDS kernels are not in use;
  * NXHIP_PC_DENSE=0 disables it. Call after nx_set_preconditioner.
  */
 int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs, const int32_t* job_tslot_off,
                     const int32_t* job_tslot, const int32_t* job_need_off,
-                    const int32_t* job_need);
+                    const int32_t* job_need, const int32_t* top_uoff, const int32_t* slot_uy,
+                    const int32_t* chain_uit, const int32_t* chain_uib,
+                    const int32_t* job_root_u, const int32_t* job_root_dc);
 
 /*
  * Coarse step of the preconditioner on a partitioned problem (precond.py derives it): the

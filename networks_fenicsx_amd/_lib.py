@@ -60,7 +60,8 @@ _SIGS = {
     "nx_set_coarse": (C.c_int, [_h, _i32, _pi32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                 _i32, _pi32]),
     "nx_set_halo": (C.c_int, [_h, _i32, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
-    "nx_set_pc_dense": (C.c_int, [_h, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
+    "nx_set_pc_dense": (C.c_int, [_h, _i32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
+                                  _pi32, _pi32, _pi32, _pi32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
     "nx_group_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
     "nx_group_destroy": (C.c_int, [_h]),
@@ -256,14 +257,13 @@ class Handle:
             int(pc.lvl_slot_off.size - 1), p["lvl_slot_off"], int(pc.top_lvl_off.size - 1),
             p["top_lvl_off"]))
         if getattr(pc, "job_tslot", None) is not None and pc.job_tslot.size:
-            da = {k: np.ascontiguousarray(getattr(pc, k), dtype=np.int32) for k in (
-                "job_tslot_off", "job_tslot", "job_need_off", "job_need")}
+            keys = ("job_tslot_off", "job_tslot", "job_need_off", "job_need", "top_uoff",
+                    "slot_uy", "chain_uit", "chain_uib", "job_root_u", "job_root_dc")
+            da = {k: np.ascontiguousarray(getattr(pc, k), dtype=np.int32) for k in keys}
             da = {k: (v if v.size else np.zeros(1, np.int32)) for k, v in da.items()}
             self._pc_keep_d = da
             check(lib().nx_set_pc_dense(self.ptr, 1, int(pc.n_jobs),
-                                        *[_ptr(da[k], C.c_int32) for k in (
-                                            "job_tslot_off", "job_tslot", "job_need_off",
-                                            "job_need")]))
+                                        *[_ptr(da[k], C.c_int32) for k in keys]))
         nC = int(getattr(pc, "n_coarse", 0))
         if nC:
             ca = {k: np.ascontiguousarray(getattr(pc, k), dtype=np.int32) for k in (

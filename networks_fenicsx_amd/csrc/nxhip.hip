@@ -733,6 +733,19 @@ struct PcArgs {
   const int* job_need_off;
   const int* job_need;
   double* G;
+  // producer-side top inputs: a_s = sum u[top_uoff[s] .. top_uoff[s+1])
+  const int* top_uoff;
+  const int* slot_uy;
+  const int* chain_uit;
+  const int* chain_uib;
+  const int* job_root_u;
+  const int* job_root_dc;
+  double* u;
+  // factored coefficients (single rank, once per solve by k_pc_factor; D is fixed by the
+  // assembly): kappa = g / D_child per hanging-chain entry (0 when grounded), 1 / D
+  int factored;
+  double* dc_kappa;
+  double* slot_invD;
 };
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
@@ -1081,6 +1094,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     }
   }
   const bool upd = mode == 0 && !(MULTI && pa.lin);
+  const bool dense = !MULTI && pa.dense && mode == 0;  // write the top inputs u
   NX_PHASE_START(16);
   const int job = blockIdx.x;
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
@@ -1115,13 +1129,22 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       pa.chain_T[c] = ch.T;
       pa.chain_Ib[c] = ib;
       pa.chain_It[c] = sr - ib;
+      if (dense) {
+        const int ui = pa.chain_uit[c], ub = pa.chain_uib[c];
+        if (ui >= 0) pa.u[ui] = sr - ib;
+        if (ub >= 0) pa.u[ub] = ib;
+      }
     }
   }
   NX_PHASE(17);
-  if (!MULTI && pa.dense && upd) {  // the top kernel does not run: update the job's top rows
+  if (dense) {  // the top kernel does not run: update the job's top rows, post their y'
+    const int ts0 = pa.top_lvl_off[0];
     for (int i = pa.job_tslot_off[job] + threadIdx.x; i < pa.job_tslot_off[job + 1]; i += kPcThreads) {
-      const int lam = pa.slot_lam[pa.job_tslot[i]];
-      y[lam] -= c2 * r2[lam];
+      const int t = pa.job_tslot[i];
+      const int lam = pa.slot_lam[t];
+      const double yl = y[lam] - c2 * r2[lam];
+      y[lam] = yl;
+      pa.u[pa.slot_uy[t - ts0]] = yl;
     }
   }
   const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
@@ -1132,6 +1155,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   const int js0 = pa.lvl_slot_off[lv0], js1 = pa.lvl_slot_off[lv1];
   const int ns = js1 - js0;
   const int dc0 = pa.slot_dc_off[js0];
+  // factored: D is fixed by the assembly -> J += kappa J_child, no divisions, no D stores
+  const bool fac = !MULTI && pa.factored && mode == 0;
   __syncthreads();
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {  // phase A
     const int j = js0 + sl;
@@ -1153,7 +1178,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       J0 += sIt[cl];
       if (lo >= 0) {
         sChild[i - dc0] = lo - js0;
-        sG[i - dc0] = g;
+        sG[i - dc0] = fac ? pa.dc_kappa[i] : g;
       } else {
         sChild[i - dc0] = -1;
         D0 += g;
@@ -1169,12 +1194,19 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kPcThreads) {
       const int sl = j - js0;
       double D = sD0[sl], J = sJ0[sl];
-      for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
-        const int ch = sChild[i];
-        if (ch < 0) continue;
-        const double g = sG[i], Dc = sD[ch];
-        D += g * (1.0 - g / Dc);
-        J += g * sJ[ch] / Dc;
+      if (fac) {
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int ch = sChild[i];
+          if (ch >= 0) J += sG[i] * sJ[ch];
+        }
+      } else {
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int ch = sChild[i];
+          if (ch < 0) continue;
+          const double g = sG[i], Dc = sD[ch];
+          D += g * (1.0 - g / Dc);
+          J += g * sJ[ch] / Dc;
+        }
       }
       sD[sl] = D;
       sJ[sl] = J;
@@ -1183,12 +1215,23 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   }
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
     const int j = js0 + sl;
-    const int pcn = pa.slot_pchain[j];
-    const double D = sD[sl], J = sJ[sl];
-    pa.slot_D[j] = D;
+    const double J = sJ[sl];
     pa.slot_J[j] = J;
-    pa.slot_A[j] = J / D;
-    pa.slot_B[j] = pcn >= 0 ? 1.0 / (sT[pcn - c0] * D) : 0.0;
+    if (fac) {
+      pa.slot_A[j] = J * pa.slot_invD[j];
+    } else {
+      const int pcn = pa.slot_pchain[j];
+      const double D = sD[sl];
+      pa.slot_D[j] = D;
+      pa.slot_A[j] = J / D;
+      pa.slot_B[j] = pcn >= 0 ? 1.0 / (sT[pcn - c0] * D) : 0.0;
+    }
+  }
+  if (dense && threadIdx.x == 0 && pa.job_root_u[job] >= 0) {  // root -> its top parent
+    const int k = pa.job_root_dc[job];
+    const int pcn = pa.slot_pchain[js0];
+    const double kap = fac ? pa.dc_kappa[k] : 1.0 / sT[pcn - c0] / sD[0];
+    pa.u[pa.job_root_u[job]] = sIt[pcn - c0] + kap * sJ[0];
   }
   NX_PHASE(19);
   NX_PHASE_END(16);
@@ -1355,16 +1398,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   int nneed = 0;
   if (dense) {
     const int ts0 = pa.top_lvl_off[0], nt = pa.n_top;
-    for (int sl = threadIdx.x; sl < nt; sl += kPcThreads) {  // a_s (y holds r' already)
-      const int j = ts0 + sl;
-      const int pcn = pa.slot_pchain[j];
-      double a = y[pa.slot_lam[j]] + (pcn >= 0 ? pa.chain_Ib[pcn] : 0.0);
-      for (int i = pa.slot_dc_off[j]; i < pa.slot_dc_off[j + 1]; ++i) {
-        const int c = pa.slot_dc[i];
-        const int lo = pa.dc_lo[i];
-        a += pa.chain_It[c];
-        if (lo >= 0 && lo < ts0) a += pa.slot_J[lo] / pa.chain_T[c] / pa.slot_D[lo];
-      }
+    for (int sl = threadIdx.x; sl < nt; sl += kPcThreads) {  // a_s from the posted inputs
+      double a = 0.0;
+      for (int i = pa.top_uoff[sl]; i < pa.top_uoff[sl + 1]; ++i) a += pa.u[i];
       sTa[sl] = a;
     }
     const int n0 = pa.job_need_off[job];
@@ -1499,6 +1535,16 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   NX_PHASE(51);
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
   NX_PHASE_END(48);
+}
+
+// Factored coefficients from this solve's D (after the start application).
+__global__ void k_pc_factor(PcArgs pa, int n_dc, int n_slots) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_dc) {
+    const int lo = pa.dc_lo[i];
+    pa.dc_kappa[i] = lo >= 0 ? 1.0 / pa.chain_T[pa.slot_dc[i]] / pa.slot_D[lo] : 0.0;
+  }
+  if (i < n_slots) pa.slot_invD[i] = 1.0 / pa.slot_D[i];
 }
 
 // Dense top: column s of G = response of the top part to a unit J at top slot s (J up the
@@ -1688,6 +1734,7 @@ struct nx_network {
   int pc_variant = 0;   // (W, CPL) instantiation
   int pc_jobs = 0;
   int64_t pc_slots = 0;
+  int64_t pc_ndc = 0;
   PcArgs pa{};
   std::vector<void*> pc_bufs;
   double* z = nullptr;  // P^{-1} r, n_col
@@ -2291,11 +2338,19 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   }
   if (t.hs[0]->pc) {  // beta_1^2 = b . P^{-1} b
     CHECK(team_pc(t, 0, 1));
-    for (int r = 0; r < t.P; ++r) {  // dense top: G from this assembly's D (fixed per solve)
+    for (int r = 0; r < t.P; ++r) {  // coefficients of this assembly's D (fixed per solve)
       nx_network* h = t.hs[r];
+      if (!multi && h->pa.dc_kappa) {
+        const int nmax = (int)std::max<int64_t>(h->pc_ndc, h->pc_slots);
+        if (nmax > 0)
+          hipLaunchKernelGGL(k_pc_factor, dim3(grid_of(nmax, 256)), dim3(256), 0, h->stream,
+                             h->pa, (int)h->pc_ndc, (int)h->pc_slots);
+      }
       if (h->pa.dense && !multi)
         hipLaunchKernelGGL(k_pc_gbuild, dim3(h->pa.n_top), dim3(64), 0, h->stream, h->pa);
     }
+    // the iterations use them (the start above computed D)
+    for (int r = 0; r < t.P; ++r) t.hs[r]->pa.factored = (!multi && t.hs[r]->pa.dc_kappa) ? 1 : 0;
   } else {
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
@@ -2617,6 +2672,11 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.slot_z = scratch(n_slots);
   pa.lin = 0;
   pa.dense = 0;
+  pa.factored = 0;  // set by solve after k_pc_factor
+  pa.dc_kappa = scratch(slot_dc_off[n_slots]);
+  pa.slot_invD = scratch(n_slots);
+  if (const char* e = std::getenv("NXHIP_PC_FACTOR"))
+    if (std::atoi(e) == 0) pa.dc_kappa = nullptr;  // keep the per-iteration eliminations
   for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
                         (const void*)pa.chain_lo, (const void*)pa.slot_lam, (const void*)pa.slot_pchain,
                         (const void*)pa.slot_parent, (const void*)pa.slot_dc_off, (const void*)pa.slot_dc,
@@ -2653,13 +2713,17 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->pc_jobs = n_jobs;
   h->pc_variant = variant;
   h->pc_slots = n_slots;
+  h->pc_ndc = n_slots > 0 ? slot_dc_off[n_slots] : 0;
   h->pc = true;
   return NX_OK;
 }
 
 NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
                            const int32_t* job_tslot_off, const int32_t* job_tslot,
-                           const int32_t* job_need_off, const int32_t* job_need) {
+                           const int32_t* job_need_off, const int32_t* job_need,
+                           const int32_t* top_uoff, const int32_t* slot_uy,
+                           const int32_t* chain_uit, const int32_t* chain_uib,
+                           const int32_t* job_root_u, const int32_t* job_root_dc) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
   CHECK(set_device(h));
@@ -2684,6 +2748,16 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
     if (job_tslot[i] < ts0 || job_tslot[i] >= ts0 + nt) return fail(NX_ERR_ARG, "job_tslot out of range");
   for (int i = 0; i < job_need_off[n_jobs]; ++i)
     if (job_need[i] < ts0 || job_need[i] >= ts0 + nt) return fail(NX_ERR_ARG, "job_need out of range");
+  const int n_u = top_uoff[nt];
+  if (top_uoff[0] != 0 || n_u < nt) return fail(NX_ERR_ARG, "bad top_uoff");
+  for (int i = 0; i < nt; ++i)
+    if (slot_uy[i] < 0 || slot_uy[i] >= n_u) return fail(NX_ERR_ARG, "slot_uy out of range");
+  for (int64_t c = 0; c < h->E; ++c)
+    if (chain_uit[c] >= n_u || chain_uib[c] >= n_u) return fail(NX_ERR_ARG, "chain_u* out of range");
+  for (int j = 0; j < n_jobs; ++j)
+    if (job_root_u[j] >= n_u || job_root_dc[j] >= h->pc_ndc ||
+        (job_root_u[j] >= 0 && job_root_dc[j] < 0))
+      return fail(NX_ERR_ARG, "job_root_u / job_root_dc out of range");
   // dense mode: single rank, LDS kernels, a top part that fits
   if (!fits || h->nranks > 1 || !h->pc_lds || nt < 1 || nt > kCapT || n_jobs < 1) return NX_OK;
   if (const char* e = std::getenv("NXHIP_PC_DENSE"))
@@ -2701,11 +2775,23 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
   pa.job_tslot = up(job_tslot, nt);
   pa.job_need_off = up(job_need_off, n_jobs + 1);
   pa.job_need = up(job_need, std::max(1, job_need_off[n_jobs]));
+  pa.top_uoff = up(top_uoff, nt + 1);
+  pa.slot_uy = up(slot_uy, nt);
+  pa.chain_uit = up(chain_uit, h->E);
+  pa.chain_uib = up(chain_uib, h->E);
+  pa.job_root_u = up(job_root_u, n_jobs);
+  pa.job_root_dc = up(job_root_dc, n_jobs);
+  double* ub = nullptr;
+  HIPCALL(hipMalloc((void**)&ub, sizeof(double) * n_u));
+  HIPCALL(hipMemset(ub, 0, sizeof(double) * n_u));
+  h->pc_bufs.push_back(ub);
+  pa.u = ub;
   double* G = nullptr;
   HIPCALL(hipMalloc((void**)&G, sizeof(double) * (size_t)nt * nt));
   h->pc_bufs.push_back(G);
   pa.G = G;
-  if (!pa.job_tslot_off || !pa.job_tslot || !pa.job_need_off || !pa.job_need)
+  if (!pa.job_tslot_off || !pa.job_tslot || !pa.job_need_off || !pa.job_need || !pa.top_uoff ||
+      !pa.slot_uy || !pa.chain_uit || !pa.chain_uib || !pa.job_root_u || !pa.job_root_dc)
     return fail(NX_ERR_HIP, "dense top upload failed");
   pa.n_top = nt;
   pa.dense = 1;

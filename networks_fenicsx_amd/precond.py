@@ -219,6 +219,17 @@ class TreePreconditioner:
     job_tslot: np.ndarray = field(default_factory=lambda: _EMPTY_I)
     job_need_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
     job_need: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    # producer-side inputs of the dense top: a_s = sum of u[top_uoff[s]:top_uoff[s+1]];
+    # the up kernel writes every contribution to its fixed place: y' of top slot s at
+    # slot_uy[s - ts0], I_top / I_bot of chain c at chain_uit[c] / chain_uib[c] (-1: not
+    # a top input), and for a job root kappa J_root + I_top(root's parent chain) at
+    # job_root_u[j] with kappa = dc entry job_root_dc[j]
+    top_uoff: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
+    slot_uy: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    chain_uit: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    chain_uib: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    job_root_u: np.ndarray = field(default_factory=lambda: _EMPTY_I)
+    job_root_dc: np.ndarray = field(default_factory=lambda: _EMPTY_I)
     n_coarse: int = 0
     slot_cidx: np.ndarray = field(default_factory=lambda: _EMPTY_I)
     cc_chain: np.ndarray = field(default_factory=lambda: _EMPTY_I)
@@ -480,6 +491,42 @@ def _dense_top_lists(pc: TreePreconditioner) -> None:
     pc.job_need_off = np.zeros(nj + 1, dtype=np.int32)
     np.cumsum([len(n) for n in need], out=pc.job_need_off[1:])
     pc.job_need = np.array([t for n in need for t in n], dtype=np.int32)
+    # producer-side input layout: per top slot [y', I_bot(parent chain), one per dc entry]
+    nt = ts1 - ts0
+    cnt = np.zeros(nt, dtype=np.int64)
+    for t in range(ts0, ts1):
+        cnt[t - ts0] = 1 + (pc.slot_pchain[t] >= 0) + (pc.slot_dc_off[t + 1] - pc.slot_dc_off[t])
+    uoff = np.zeros(nt + 1, dtype=np.int32)
+    np.cumsum(cnt, out=uoff[1:])
+    slot_uy = uoff[:-1].copy()
+    chain_uit = np.full(pc.n_chains, -1, dtype=np.int32)
+    chain_uib = np.full(pc.n_chains, -1, dtype=np.int32)
+    job_root_u = np.full(nj, -1, dtype=np.int32)
+    job_root_dc = np.full(nj, -1, dtype=np.int32)
+    root_job = {}
+    for j in range(nj):
+        lv0, lv1 = pc.job_lvl_off[j], pc.job_lvl_off[j + 1]
+        if lv1 > lv0:
+            for sl in range(pc.lvl_slot_off[lv0], pc.lvl_slot_off[lv0 + 1]):
+                root_job[sl] = j
+    for t in range(ts0, ts1):
+        k = uoff[t - ts0] + 1
+        if pc.slot_pchain[t] >= 0:
+            chain_uib[pc.slot_pchain[t]] = k
+            k += 1
+        for i in range(pc.slot_dc_off[t], pc.slot_dc_off[t + 1]):
+            c, lo = pc.slot_dc[i], pc.dc_lo[i]
+            if 0 <= lo < ts0:  # a lower job's root: kappa J_root + I_top, after its levels
+                j = root_job[int(lo)]
+                assert job_root_u[j] < 0, "one root per job"
+                job_root_u[j] = k
+                job_root_dc[j] = i
+            else:
+                chain_uit[c] = k
+            k += 1
+    pc.top_uoff, pc.slot_uy = uoff, slot_uy.astype(np.int32)
+    pc.chain_uit, pc.chain_uib = chain_uit, chain_uib
+    pc.job_root_u, pc.job_root_dc = job_root_u, job_root_dc
 
 
 def top_inverse_model(pc: TreePreconditioner, T: np.ndarray, Dj: np.ndarray) -> np.ndarray:

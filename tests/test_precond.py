@@ -79,3 +79,31 @@ def test_dense_top_inverse_matches_back_substitution(depth, jobs):
             for e in (pc.chain_up[c], pc.chain_lo[c]):
                 assert e < ts0 or e in need
     assert sorted(pc.job_tslot.tolist()) == list(range(ts0, ts1))
+    # producer-side input layout reproduces a_s
+    u = np.zeros(int(pc.top_uoff[-1]))
+    rr = st["r"]
+    for t in range(ts0, ts1):
+        u[pc.slot_uy[t - ts0]] = rr[pc.slot_lam[t]]
+    It = np.zeros(pc.n_chains)
+    Ib = np.zeros(pc.n_chains)
+    N = pc.N
+    for c in range(pc.n_chains):  # recompute the chain currents of the model
+        e = pc.chain_edge[c]
+        cells = e * (2 * N + 1) + 2 * np.arange(N) + 1
+        rho = dq[e][::-1] if pc.chain_flip[c] else dq[e]
+        cells = cells[::-1] if pc.chain_flip[c] else cells
+        Dk = np.cumsum(rho)[:N]
+        Ib[c] = np.sum(rr[cells] * Dk) / T[c]
+        It[c] = np.sum(rr[cells] * (T[c] - Dk)) / T[c]
+        if pc.chain_uit[c] >= 0:
+            u[pc.chain_uit[c]] = It[c]
+        if pc.chain_uib[c] >= 0:
+            u[pc.chain_uib[c]] = Ib[c]
+    for j in range(pc.n_jobs):
+        if pc.job_root_u[j] >= 0:
+            i = pc.job_root_dc[j]
+            root = pc.dc_lo[i]
+            c = pc.slot_dc[i]
+            u[pc.job_root_u[j]] = It[c] + Jj[root] / T[c] / Dj[root]
+    a_u = np.add.reduceat(u, pc.top_uoff[:-1]) if u.size else u
+    np.testing.assert_allclose(a_u, a, rtol=1e-12, atol=1e-14)
