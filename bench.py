@@ -172,6 +172,7 @@ def main() -> int:
     spmv_ms = prof["spmv_ms"] / max(prof["spmv_count"], 1)
     asm_ms = prof["asm_ms"] / max(prof["asm_count"], 1)
     warm_spmv_ms = h.bench_spmv(200)
+    cold_spmv_ms, cold_copies = h.bench_spmv_cold(120)
     pc_on = asm.preconditioned
     nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on)
     achieved = nbytes / (spmv_ms * 1e-3) / 1e9
@@ -238,6 +239,9 @@ def main() -> int:
                 "spmv_algorithmic_bytes": sbytes,
                 "isolated_warm_spmv_ms": warm_spmv_ms,
                 "isolated_warm_spmv_GBs": sbytes / (warm_spmv_ms * 1e-3) / 1e9,
+                "isolated_cold_spmv_ms": cold_spmv_ms,
+                "isolated_cold_spmv_GBs": sbytes / (cold_spmv_ms * 1e-3) / 1e9,
+                "cold_rotation_copies": cold_copies,
                 "assembly_kernel_ms": asm_ms,
             },
             "cpu_baseline": cpu,

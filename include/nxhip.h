@@ -208,6 +208,9 @@ int nx_get_profile(nx_network_t* h, double* spmv_ms, int64_t* spmv_count, double
                    int64_t* asm_count);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
+/* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,
+ * twice the Infinity Cache) so every launch streams from HBM ("cold"). */
+int nx_bench_spmv_cold(nx_network_t* h, int32_t reps, int32_t* copies, double* ms_per_spmv);
 
 /*
  * Multi-GPU (one process per GPU). Rank 0 creates the RCCL unique id, the

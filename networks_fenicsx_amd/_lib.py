@@ -52,6 +52,7 @@ _SIGS = {
     "nx_get_profile": (C.c_int, [_h, _pd, _pi64, _pd, _pi64]),
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
+    "nx_bench_spmv_cold": (C.c_int, [_h, _i32, _pi32, _pd]),
     "nx_set_preconditioner": (C.c_int, [_h, _i32, _i64, _pi32, _pi32, _pi32, _pi32, _i64, _pi32,
                                         _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, _i32, _pi32,
                                         _pi32, _i32, _pi32, _i32, _pi32]),
@@ -232,6 +233,13 @@ class Handle:
         ms = C.c_double()
         check(lib().nx_bench_spmv(self.ptr, int(reps), C.byref(ms)))
         return float(ms.value)
+
+    def bench_spmv_cold(self, reps: int = 200):
+        """(ms per SpMV, number of rotated copies) with operands streamed from HBM."""
+        ms = C.c_double(0.0)
+        k = C.c_int32(0)
+        check(lib().nx_bench_spmv_cold(self.ptr, int(reps), C.byref(k), C.byref(ms)))
+        return float(ms.value), int(k.value)
 
     def set_preconditioner(self, pc) -> None:
         """Upload a :class:`precond.TreePreconditioner` (``None`` disables it)."""

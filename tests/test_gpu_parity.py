@@ -289,3 +289,13 @@ def test_preconditioner_kernel_paths(case, path, monkeypatch):
     _, _, perm, _ = O.to_build_layout(P, A, b)
     x = asm.handle.solution()
     assert np.linalg.norm(x - x_ref[perm]) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
+def test_cold_spmv_benchmark_runs():
+    """The cold (cache-defeating) SpMV timing rotates over >= 2 copies and is no faster
+    than a tiny fraction of the warm one (sanity, not a performance gate)."""
+    mesh, asm, P, A, b, _ = _build("depth6_N40")
+    asm.assemble()
+    warm = asm.handle.bench_spmv(20)
+    cold, k = asm.handle.bench_spmv_cold(20)
+    assert k >= 2 and cold > 0 and warm > 0
