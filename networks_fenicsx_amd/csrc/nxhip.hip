@@ -1094,6 +1094,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     }
   }
   const bool upd = mode == 0 && !(MULTI && pa.lin);
+  if (MULTI && pa.lin && mode == 0 && blockIdx.x == 0) {  // this rank's alpha partial sum
+    const double a = block_allsum<kPcThreads>(partA, nA);
+    if (threadIdx.x == 0) const_cast<double*>(pa.xalpha)[0] = a;
+  }
   const bool dense = !MULTI && pa.dense && mode == 0;  // write the top inputs u
   NX_PHASE_START(16);
   const int job = blockIdx.x;
@@ -1665,6 +1669,25 @@ __global__ void k_pack(const double* __restrict__ x, const int* __restrict__ idx
   if (i < n) buf[i] = x[idx[i]];
 }
 
+// Halo pack + this rank's beta^2 (sum of the previous iteration's partials, block 0) into
+// red[1] and its own slot of the gathered array: saves a reduction launch per iteration.
+__global__ __launch_bounds__(kBlock) void k_pack_beta(const double* __restrict__ x,
+                                                      const int* __restrict__ idx, int n,
+                                                      double* __restrict__ buf,
+                                                      const double* __restrict__ partB, int nB,
+                                                      double* __restrict__ red1,
+                                                      double* __restrict__ gath_self) {
+  if (blockIdx.x == 0) {
+    const double t = block_allsum(partB, nB);
+    if (threadIdx.x == 0) {
+      *red1 = t;
+      *gath_self = t;
+    }
+  }
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) buf[i] = x[idx[i]];
+}
+
 // In-process group transport: sum n values over the ranks' buffers in rank order and
 // store the total in every buffer (the RCCL all-reduce of a group on one device).
 constexpr int kMaxGroup = 16;
@@ -1815,12 +1838,18 @@ double* vec_of(nx_network* h, VecSel s, int64_t k) {
 }
 
 // fill the ghost slots of the selected vector (n_col) from the owning ranks
+int nB_of(const nx_network* h);
+
 int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false) {
   if (!team_multi(t)) return NX_OK;
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
     const int nsend = h->send_off.back();
-    if (nsend > 0)
+    if (beta)  // with the previous iteration's beta^2 partial sum
+      hipLaunchKernelGGL(k_pack_beta, dim3(std::max(1, grid_of(nsend, kBlock))), dim3(kBlock), 0,
+                         h->stream, vec_of(h, sel, k), h->send_idx, nsend, h->send_buf,
+                         h->partB, nB_of(h), h->red + 1, h->gath + h->rank);
+    else if (nsend > 0)
       hipLaunchKernelGGL(k_pack, dim3(grid_of(nsend, 256)), dim3(256), 0, h->stream,
                          vec_of(h, sel, k), h->send_idx, nsend, h->send_buf);
   }
@@ -1849,9 +1878,6 @@ int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false) {
   nx_network* h = t.hs[0];
   if (h->peers.empty() && !beta) return NX_OK;
   double* v = vec_of(h, sel, k);
-  if (beta)
-    HIPCALL(hipMemcpyAsync(h->gath + h->rank, h->red + 1, sizeof(double), hipMemcpyDeviceToDevice,
-                           h->stream));
   NCCLCALL(ncclGroupStart());
   if (beta) {  // beta^2 partial to / from every other rank
     for (int q = 0; q < h->nranks; ++q) {
@@ -1974,10 +2000,12 @@ int team_pc(const Team& t, int64_t k, int mode) {
 }
 
 int team_reduce_slot(const Team& t, bool from_a, int slot, bool allreduce = true) {
-  // linear form: alpha's partial goes into the coarse buffer and is reduced with it
+  // linear form: alpha's partial goes into the coarse buffer and is reduced with it; the
+  // up kernel's workgroup 0 sums it (no launch here) when the rank has LDS jobs
   const bool to_coarse = from_a && slot == 0 && team_lin(t);
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
+    if (to_coarse && h->pc_lds && h->pc_jobs > 0) continue;
     hipLaunchKernelGGL(k_reduce_slot, dim3(1), dim3(kBlock), 0, h->stream,
                        from_a ? h->partA : h->partB, from_a ? h->nA : nB_of(h),
                        to_coarse ? h->pa.cbuf + 3 * h->pa.n_coarse : h->red, to_coarse ? 0 : slot);
@@ -2038,7 +2066,7 @@ int launch_iteration(const Team& t, int64_t k) {
                            r2, sout, sin, h->partA, h->nA, h->red, h->partB);
     }
   }
-  if (multi) CHECK(team_reduce_slot(t, false, 1, !p2p_beta));
+  if (multi && !p2p_beta) CHECK(team_reduce_slot(t, false, 1));  // p2p: k_pack_beta sums
   HIPCALL(hipGetLastError());
   return NX_OK;
 }
