@@ -180,6 +180,10 @@ int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_cidx, i
                   const int32_t* c_parent, const int32_t* c_child_off, const int32_t* c_child,
                   int32_t n_clvl, const int32_t* c_lvl_off);
 
+/* 1 if the last nx_solve replayed its iterations as HIP graphs (also with RCCL, unless
+ * the capture failed or NXHIP_RCCL_GRAPH=0), 0 if it launched them one by one. */
+int nx_get_graph_mode(nx_network_t* h, int32_t* graph);
+
 /* Copy the owned part of the solution / rhs to the host (n_rows doubles). */
 int nx_get_solution(nx_network_t* h, double* x);
 int nx_get_rhs(nx_network_t* h, double* b);

@@ -53,6 +53,7 @@ _SIGS = {
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
     "nx_bench_spmv_cold": (C.c_int, [_h, _i32, _pi32, _pd]),
+    "nx_get_graph_mode": (C.c_int, [_h, _pi32]),
     "nx_set_preconditioner": (C.c_int, [_h, _i32, _i64, _pi32, _pi32, _pi32, _pi32, _i64, _pi32,
                                         _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, _i32, _pi32,
                                         _pi32, _i32, _pi32, _i32, _pi32]),
@@ -233,6 +234,12 @@ class Handle:
         ms = C.c_double()
         check(lib().nx_bench_spmv(self.ptr, int(reps), C.byref(ms)))
         return float(ms.value)
+
+    def graph_mode(self) -> bool:
+        """True if the last solve replayed HIP graphs."""
+        g = C.c_int32(0)
+        check(lib().nx_get_graph_mode(self.ptr, C.byref(g)))
+        return bool(g.value)
 
     def bench_spmv_cold(self, reps: int = 200):
         """(ms per SpMV, number of rotated copies) with operands streamed from HBM."""

@@ -1789,6 +1789,8 @@ struct nx_network {
   // iteration needs no separate all-reduce for it (NXHIP_BETA_P2P=0: all-reduce instead)
   double* gath = nullptr;
   bool beta_p2p = true;
+  bool rccl_graph_ok = true;  // capture of the RCCL iteration worked (or was not tried)
+  bool last_graph = false;    // the last nx_solve replayed HIP graphs
 };
 
 struct nx_group {
@@ -2404,8 +2406,25 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   // after the check only the launches that ran a Lanczos step are added).
   nx_network* h0 = t.hs[0];
   const bool prof = h0->prof && t.g == nullptr;
-  const bool use_graph = t.hs[0]->comm == nullptr && !prof;
-  if (use_graph) CHECK(build_chunk_graph(t, check_every));
+  // RCCL iterations are captured too (host-side enqueue of ~8 operations per iteration
+  // would otherwise pace the loop); if the capture fails, that handle stays eager
+  static const bool rccl_graph_env = [] {
+    const char* e = std::getenv("NXHIP_RCCL_GRAPH");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  const bool rccl = t.hs[0]->comm != nullptr;
+  bool use_graph = !prof && (!rccl || (rccl_graph_env && h0->rccl_graph_ok));
+  if (use_graph) {
+    const int rc = build_chunk_graph(t, check_every);
+    if (rc != NX_OK) {
+      if (!rccl) return rc;
+      (void)hipGetLastError();
+      (void)drop_graph(graph_slot(t));
+      h0->rccl_graph_ok = false;
+      use_graph = false;
+    }
+  }
+  h0->last_graph = use_graph;
   if (prof && (int)h0->ev_pool.size() < 2 * check_every) {
     for (auto& e : h0->ev_pool) (void)hipEventDestroy(e);
     h0->ev_pool.assign(2 * check_every, nullptr);
@@ -2587,6 +2606,12 @@ NX_API int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv) {
   return NX_OK;
 }
 
+
+NX_API int nx_get_graph_mode(nx_network_t* h, int32_t* graph) {
+  if (!h || !graph) return fail(NX_ERR_ARG, "null argument");
+  *graph = h->last_graph ? 1 : 0;
+  return NX_OK;
+}
 
 NX_API int nx_bench_spmv_cold(nx_network_t* h, int32_t reps, int32_t* copies_out,
                               double* ms_per_spmv) {

@@ -156,6 +156,7 @@ def test_rccl_single_rank_communicator(pc):
         x = asm.handle.solution()
         assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
         assert it <= _single_iterations(mesh, pbc, pc) + 2
+        assert asm.handle.graph_mode()  # the RCCL iterations were captured as HIP graphs
         assert asm.handle.true_residual() < 1e-9
     finally:
         asm.close()
