@@ -188,6 +188,10 @@ int nx_get_graph_mode(nx_network_t* h, int32_t* graph);
 int nx_get_solution(nx_network_t* h, double* x);
 int nx_get_rhs(nx_network_t* h, double* b);
 
+/* Owned part of an internal vector (n_rows doubles): 0 = solution, 1 = rhs,
+ * 2 = the latest preconditioned residual z = P^{-1} r (with the preconditioner). */
+int nx_get_vector(nx_network_t* h, int32_t which, double* out);
+
 /* Copy the assembled CSR (n_rows+1, nnz, nnz) to the host -- parity tests. */
 int nx_get_csr(nx_network_t* h, int32_t* rowptr, int32_t* col, double* val);
 

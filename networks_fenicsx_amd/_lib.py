@@ -44,6 +44,7 @@ _SIGS = {
     "nx_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
     "nx_get_solution": (C.c_int, [_h, _pd]),
     "nx_get_rhs": (C.c_int, [_h, _pd]),
+    "nx_get_vector": (C.c_int, [_h, _i32, _pd]),
     "nx_get_csr": (C.c_int, [_h, _pi32, _pi32, _pd]),
     "nx_spmv_host": (C.c_int, [_h, _pd, _pd]),
     "nx_true_residual": (C.c_int, [_h, _pd]),
@@ -234,6 +235,12 @@ class Handle:
         ms = C.c_double()
         check(lib().nx_bench_spmv(self.ptr, int(reps), C.byref(ms)))
         return float(ms.value)
+
+    def vector(self, which: int) -> np.ndarray:
+        """0 = solution, 1 = rhs, 2 = latest preconditioned residual (owned rows)."""
+        out = np.empty(self.n_rows, dtype=np.float64)
+        check(lib().nx_get_vector(self.ptr, int(which), _ptr(out, C.c_double)))
+        return out
 
     def graph_mode(self) -> bool:
         """True if the last solve replayed HIP graphs."""

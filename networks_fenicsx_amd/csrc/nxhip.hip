@@ -20,6 +20,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -746,6 +747,15 @@ struct PcArgs {
   int factored;
   double* dc_kappa;
   double* slot_invD;
+  // dense top with several ranks (mdense): the top trees are rooted at coarse junctions
+  // (Dirichlet): z_t = G[t,:] a + w_t zc[root(t)], and the coarse partial J of a root r is
+  // KJ[r,:] a; atop = a (k_pc_cpart), zc = the coarse solution (k_pc_coarse)
+  int mdense;
+  double* KJ;
+  double* top_w;
+  int* top_rootc;
+  double* atop;
+  double* zc;
 };
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
@@ -1098,7 +1108,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     const double a = block_allsum<kPcThreads>(partA, nA);
     if (threadIdx.x == 0) const_cast<double*>(pa.xalpha)[0] = a;
   }
-  const bool dense = !MULTI && pa.dense && mode == 0;  // write the top inputs u
+  const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;  // write the top inputs u
   NX_PHASE_START(16);
   const int job = blockIdx.x;
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
@@ -1160,7 +1170,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   const int ns = js1 - js0;
   const int dc0 = pa.slot_dc_off[js0];
   // factored: D is fixed by the assembly -> J += kappa J_child, no divisions, no D stores
-  const bool fac = !MULTI && pa.factored && mode == 0;
+  const bool fac = pa.factored && mode == 0;
   __syncthreads();
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {  // phase A
     const int j = js0 + sl;
@@ -1398,13 +1408,17 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
   const int ns = js1 - js0;
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
-  const bool dense = !MULTI && pa.dense && mode == 0;
+  const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
   int nneed = 0;
   if (dense) {
     const int ts0 = pa.top_lvl_off[0], nt = pa.n_top;
     for (int sl = threadIdx.x; sl < nt; sl += kPcThreads) {  // a_s from the posted inputs
       double a = 0.0;
-      for (int i = pa.top_uoff[sl]; i < pa.top_uoff[sl + 1]; ++i) a += pa.u[i];
+      if (MULTI) {
+        a = pa.atop[sl];  // summed once by k_pc_cpart
+      } else {
+        for (int i = pa.top_uoff[sl]; i < pa.top_uoff[sl + 1]; ++i) a += pa.u[i];
+      }
       sTa[sl] = a;
     }
     const int n0 = pa.job_need_off[job];
@@ -1418,6 +1432,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       for (int sl = ln; sl < nt; sl += 64) acc += g[sl] * sTa[sl];
       acc = wave_sum(acc);
       if (ln == 0) {
+        if (MULTI) {  // + the coarse root's value through the tree
+          const int rc = pa.top_rootc[t - ts0];
+          if (rc >= 0) acc += pa.top_w[t - ts0] * pa.zc[rc];
+        }
         sNs[k] = t;
         sNz[k] = acc;
       }
@@ -1430,8 +1448,14 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       for (int k = 0; k < nneed; ++k)
         if (sNs[k] == t) zt = sNz[k];
       const int lam = pa.slot_lam[t];
+      double yl = y[lam];
+      if (lin) {  // several ranks: linear form, as for every other row of this kernel
+        zt -= c2 * z[lam];
+        yl -= c2 * r2[lam];
+        y[lam] = yl;
+      }
       z[lam] = zt;
-      part += y[lam] * zt;
+      part += yl * zt;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) partB[pa.n_jobs] = 0.0;  // no top kernel
   }
@@ -1551,6 +1575,69 @@ __global__ void k_pc_factor(PcArgs pa, int n_dc, int n_slots) {
   if (i < n_slots) pa.slot_invD[i] = 1.0 / pa.slot_D[i];
 }
 
+// Several ranks, dense top: root (coarse index) of every top slot and the response w_t of
+// t to a unit value at its coarse root (w = prod of g_up / D along the path). Once per solve.
+__global__ __launch_bounds__(kTopThreads) void k_pc_wroot(PcArgs pa) {
+  const int ts0 = pa.top_lvl_off[0];
+  for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
+    for (int t = pa.top_lvl_off[lv] + threadIdx.x; t < pa.top_lvl_off[lv + 1]; t += kTopThreads) {
+      const int p = pa.slot_parent[t];
+      if (p < ts0) {
+        const int c = pa.slot_cidx[t];
+        pa.top_rootc[t - ts0] = c;
+        pa.top_w[t - ts0] = c >= 0 ? 1.0 : 0.0;
+      } else {
+        pa.top_rootc[t - ts0] = pa.top_rootc[p - ts0];
+        pa.top_w[t - ts0] =
+            pa.top_w[p - ts0] / pa.chain_T[pa.slot_pchain[t]] / pa.slot_D[t];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Several ranks, dense top, every iteration: a = the summed top inputs, then this rank's
+// coarse partials [D | J | G] (D fixed by the assembly, J = KJ[root,:] a, coarse chains).
+__global__ __launch_bounds__(kTopThreads) void k_pc_cpart(PcArgs pa, const MrState* __restrict__ st,
+                                                          int mode) {
+  __shared__ double sA[kCapT];
+  if (mode == 0 && st->done) return;
+  const int ts0 = pa.top_lvl_off[0], nt = pa.n_top, nC = pa.n_coarse;
+  for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
+    double a = 0.0;
+    for (int i = pa.top_uoff[sl]; i < pa.top_uoff[sl + 1]; ++i) a += pa.u[i];
+    sA[sl] = a;
+    pa.atop[sl] = a;
+  }
+  for (int i = threadIdx.x; i < 3 * nC; i += kTopThreads) pa.cbuf[i] = 0.0;
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  for (int r = wv; r < nt; r += kTopThreads / 64) {  // one wave per coarse root
+    const int c = pa.slot_cidx[ts0 + r];
+    if (c < 0 || pa.slot_parent[ts0 + r] >= ts0) continue;
+    const double* __restrict__ k = pa.KJ + (int64_t)r * nt;
+    double acc = 0.0;
+    for (int sl = ln; sl < nt; sl += 64) acc += k[sl] * sA[sl];
+    acc = wave_sum(acc);
+    if (ln == 0) {
+      pa.cbuf[c] = pa.slot_D[ts0 + r];
+      pa.cbuf[nC + c] = acc;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // chains joining two coarse junctions (serial: fixed order)
+    for (int i = 0; i < pa.n_cc; ++i) {
+      const int c = pa.cc_chain[i], t = pa.cc_top[i], b = pa.cc_bot[i];
+      const double g = 1.0 / pa.chain_T[c];
+      pa.cbuf[t] += g;
+      pa.cbuf[b] += g;
+      pa.cbuf[nC + t] += pa.chain_It[c];
+      pa.cbuf[nC + b] += pa.chain_Ib[c];
+      pa.cbuf[2 * nC + b] = g;
+    }
+  }
+}
+
 // Dense top: column s of G = response of the top part to a unit J at top slot s (J up the
 // ancestors with kappa = g_up / D, then the root-to-leaf back-substitution). One wave per
 // column; once per solve (D is fixed by the assembly).
@@ -1560,6 +1647,7 @@ __global__ __launch_bounds__(64) void k_pc_gbuild(PcArgs pa) {
   const int s = blockIdx.x;
   for (int i = threadIdx.x; i < nt; i += 64) sJ[i] = 0.0;
   __syncthreads();
+  const bool cd = pa.KJ != nullptr;  // several ranks: coarse roots are Dirichlet nodes
   if (threadIdx.x == 0) {
     double J = 1.0;
     int t = ts0 + s;
@@ -1568,6 +1656,10 @@ __global__ __launch_bounds__(64) void k_pc_gbuild(PcArgs pa) {
       J = J / pa.chain_T[pa.slot_pchain[t]] / pa.slot_D[t];
       sJ[p - ts0] = J;
     }
+    if (cd) {  // t is the root: its row of KJ for every root, this column
+      for (int r = 0; r < nt; ++r) pa.KJ[(int64_t)r * nt + s] = 0.0;
+      if (pa.slot_cidx[t] >= 0) pa.KJ[(int64_t)(t - ts0) * nt + s] = J;
+    }
   }
   __syncthreads();
   for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
@@ -1575,7 +1667,7 @@ __global__ __launch_bounds__(64) void k_pc_gbuild(PcArgs pa) {
       const int p = pa.slot_parent[u];
       double num = sJ[u - ts0];
       if (p >= ts0) num += sZ[p - ts0] / pa.chain_T[pa.slot_pchain[u]];
-      sZ[u - ts0] = num / pa.slot_D[u];
+      sZ[u - ts0] = (cd && p < ts0 && pa.slot_cidx[u] >= 0) ? 0.0 : num / pa.slot_D[u];
     }
     __syncthreads();
   }
@@ -1633,6 +1725,11 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __
       sZ[j] = (sJ[j] + (p >= 0 ? G[j] * sZ[p] : 0.0)) / sD[j];
     }
     __syncthreads();
+  }
+  if (pa.mdense && mode == 0) {  // the down kernels evaluate the top part (dense rows)
+    for (int j = threadIdx.x; j < nC; j += kTopThreads) pa.zc[j] = sZ[j];
+    if (threadIdx.x == 0) partB[pa.n_jobs] = 0.0;
+    return;
   }
   double part = 0.0;
   for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
@@ -1934,7 +2031,9 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
       if (h->pc_jobs > 0)
         hipLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
                            h->stream, h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
-      if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
+      if (MULTI && h->pa.mdense && mode == 0)  // dense top: the coarse partials only
+        hipLaunchKernelGGL(k_pc_cpart, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, st, mode);
+      else if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
         hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream,
                            h->pa, y, r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
     } else {
@@ -2370,17 +2469,24 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
     CHECK(team_pc(t, 0, 1));
     for (int r = 0; r < t.P; ++r) {  // coefficients of this assembly's D (fixed per solve)
       nx_network* h = t.hs[r];
-      if (!multi && h->pa.dc_kappa) {
+      if (h->pa.dc_kappa) {
         const int nmax = (int)std::max<int64_t>(h->pc_ndc, h->pc_slots);
         if (nmax > 0)
           hipLaunchKernelGGL(k_pc_factor, dim3(grid_of(nmax, 256)), dim3(256), 0, h->stream,
                              h->pa, (int)h->pc_ndc, (int)h->pc_slots);
       }
-      if (h->pa.dense && !multi)
+      const bool md = multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin;
+      if (h->pa.dense && (!multi || md))
         hipLaunchKernelGGL(k_pc_gbuild, dim3(h->pa.n_top), dim3(64), 0, h->stream, h->pa);
+      if (md) hipLaunchKernelGGL(k_pc_wroot, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa);
     }
     // the iterations use them (the start above computed D)
-    for (int r = 0; r < t.P; ++r) t.hs[r]->pa.factored = (!multi && t.hs[r]->pa.dc_kappa) ? 1 : 0;
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      h->pa.factored = h->pa.dc_kappa ? 1 : 0;
+      h->pa.mdense =
+          (multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin) ? 1 : 0;
+    }
   } else {
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
@@ -2450,9 +2556,15 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
     last = &h0->h_st[0];
     for (int r = 1; r < t.P; ++r) {  // the ranks run the same recurrence on the same scalars
       const MrState& o = t.hs[r]->h_st[0];
-      if (o.it != last->it || o.done != last->done || o.relres != last->relres)
-        return fail(NX_ERR_STATE, "ranks diverged: rank " + std::to_string(r) + " at iteration " +
-                                      std::to_string(o.it) + " vs " + std::to_string(last->it));
+      if (o.it != last->it || o.done != last->done || o.relres != last->relres) {
+        char msg[256];
+        std::snprintf(msg, sizeof(msg),
+                      "ranks diverged: rank %d it %d done %d relres %.17g beta %.17g alfa %.17g "
+                      "vs rank 0 it %d done %d relres %.17g beta %.17g alfa %.17g",
+                      r, o.it, o.done, o.relres, o.beta, o.alfa, last->it, last->done,
+                      last->relres, last->beta, last->alfa);
+        return fail(NX_ERR_STATE, msg);
+      }
     }
     if (prof) {
       const int ran = last->nb - nb_before;
@@ -2486,6 +2598,16 @@ NX_API int nx_get_solution(nx_network_t* h, double* xo) {
   if (!h || !xo) return fail(NX_ERR_ARG, "null argument");
   CHECK(set_device(h));
   HIPCALL(hipMemcpyAsync(xo, h->x, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_get_vector(nx_network_t* h, int32_t which, double* out) {
+  if (!h || !out) return fail(NX_ERR_ARG, "null argument");
+  CHECK(set_device(h));
+  const double* src = which == 0 ? h->x : which == 1 ? h->rhs : which == 2 ? h->z : nullptr;
+  if (!src) return fail(NX_ERR_ARG, "which: 0 = solution, 1 = rhs, 2 = preconditioned residual");
+  HIPCALL(hipMemcpyAsync(out, src, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
   HIPCALL(hipStreamSynchronize(h->stream));
   return NX_OK;
 }
@@ -2790,6 +2912,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.lin = 0;
   pa.dense = 0;
   pa.factored = 0;  // set by solve after k_pc_factor
+  pa.mdense = 0;
+  pa.KJ = nullptr;
   pa.dc_kappa = scratch(slot_dc_off[n_slots]);
   pa.slot_invD = scratch(n_slots);
   if (const char* e = std::getenv("NXHIP_PC_FACTOR"))
@@ -2876,7 +3000,7 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
         (job_root_u[j] >= 0 && job_root_dc[j] < 0))
       return fail(NX_ERR_ARG, "job_root_u / job_root_dc out of range");
   // dense mode: single rank, LDS kernels, a top part that fits
-  if (!fits || h->nranks > 1 || !h->pc_lds || nt < 1 || nt > kCapT || n_jobs < 1) return NX_OK;
+  if (!fits || !h->pc_lds || nt < 1 || nt > kCapT || n_jobs < 1) return NX_OK;
   if (const char* e = std::getenv("NXHIP_PC_DENSE"))
     if (std::atoi(e) == 0) return NX_OK;
   auto up = [&](const int32_t* src, int64_t n) -> const int* {
@@ -2907,6 +3031,23 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
   HIPCALL(hipMalloc((void**)&G, sizeof(double) * (size_t)nt * nt));
   h->pc_bufs.push_back(G);
   pa.G = G;
+  pa.KJ = nullptr;
+  if (h->nranks > 1) {  // several ranks: top trees rooted at coarse junctions (Dirichlet)
+    double *kj = nullptr, *w = nullptr, *at = nullptr;
+    int* rc = nullptr;
+    HIPCALL(hipMalloc((void**)&kj, sizeof(double) * (size_t)nt * nt));
+    h->pc_bufs.push_back(kj);
+    HIPCALL(hipMalloc((void**)&w, sizeof(double) * nt));
+    h->pc_bufs.push_back(w);
+    HIPCALL(hipMalloc((void**)&at, sizeof(double) * nt));
+    h->pc_bufs.push_back(at);
+    HIPCALL(hipMalloc((void**)&rc, sizeof(int) * nt));
+    h->pc_bufs.push_back(rc);
+    pa.KJ = kj;
+    pa.top_w = w;
+    pa.atop = at;
+    pa.top_rootc = rc;
+  }
   if (!pa.job_tslot_off || !pa.job_tslot || !pa.job_need_off || !pa.job_need || !pa.top_uoff ||
       !pa.slot_uy || !pa.chain_uit || !pa.chain_uib || !pa.job_root_u || !pa.job_root_dc)
     return fail(NX_ERR_HIP, "dense top upload failed");
@@ -2982,6 +3123,10 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   h->pc_bufs.push_back(cb);
   pa.cbuf = cb;
   pa.xalpha = cb + 3 * n_coarse;
+  double* zc = nullptr;  // coarse solution (dense top with several ranks)
+  HIPCALL(hipMalloc((void**)&zc, sizeof(double) * n_coarse));
+  h->pc_bufs.push_back(zc);
+  pa.zc = zc;
   // linear form needs the LDS kernels; NXHIP_PC_LIN=0 keeps alpha's own all-reduce
   pa.lin = h->pc_lds ? 1 : 0;
   if (const char* e = std::getenv("NXHIP_PC_LIN")) pa.lin = pa.lin && std::atoi(e) != 0;

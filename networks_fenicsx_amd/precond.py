@@ -529,6 +529,48 @@ def _dense_top_lists(pc: TreePreconditioner) -> None:
     pc.job_root_u, pc.job_root_dc = job_root_u, job_root_dc
 
 
+def top_dense_multi_model(pc: TreePreconditioner, T: np.ndarray, Dj: np.ndarray):
+    """Several ranks: (G_loc, KJ, w, rootc) of the dense top with coarse roots held at 0
+    (k_pc_gbuild with KJ, k_pc_wroot): z_top = G_loc a + w * zc[rootc], J_root = KJ a."""
+    ts0, ts1 = int(pc.top_lvl_off[0]), int(pc.top_lvl_off[-1])
+    nt = ts1 - ts0
+    G = np.zeros((nt, nt))
+    KJ = np.zeros((nt, nt))
+    lv = pc.top_lvl_off
+    for s in range(nt):
+        J = np.zeros(nt)
+        J[s] = 1.0
+        t = ts0 + s
+        while pc.slot_parent[t] >= ts0:
+            p = pc.slot_parent[t]
+            J[p - ts0] += J[t - ts0] / T[pc.slot_pchain[t]] / Dj[t]
+            t = p
+        if pc.slot_cidx[t] >= 0:
+            KJ[t - ts0, s] = J[t - ts0]
+        z = np.zeros(nt)
+        for li in range(lv.size - 1):
+            for u in range(lv[li], lv[li + 1]):
+                p = pc.slot_parent[u]
+                if p < ts0 and pc.slot_cidx[u] >= 0:
+                    z[u - ts0] = 0.0
+                    continue
+                num = J[u - ts0] + (z[p - ts0] / T[pc.slot_pchain[u]] if p >= ts0 else 0.0)
+                z[u - ts0] = num / Dj[u]
+        G[:, s] = z
+    w = np.zeros(nt)
+    rootc = np.full(nt, -1)
+    for li in range(lv.size - 1):
+        for t in range(lv[li], lv[li + 1]):
+            p = pc.slot_parent[t]
+            if p < ts0:
+                rootc[t - ts0] = pc.slot_cidx[t]
+                w[t - ts0] = 1.0 if pc.slot_cidx[t] >= 0 else 0.0
+            else:
+                rootc[t - ts0] = rootc[p - ts0]
+                w[t - ts0] = w[p - ts0] / T[pc.slot_pchain[t]] / Dj[t]
+    return G, KJ, w, rootc
+
+
 def top_inverse_model(pc: TreePreconditioner, T: np.ndarray, Dj: np.ndarray) -> np.ndarray:
     """G (n_top x n_top): column s = the top part's response to a unit J at top slot s
     (J up the ancestors with kappa = g_up / D, then the root-to-leaf back-substitution),

@@ -9,8 +9,9 @@ from cases import CASES
 from networks_fenicsx_amd import NetworkMesh
 from networks_fenicsx_amd import network_generation as ng
 from networks_fenicsx_amd.layout import build_local_problem
-from networks_fenicsx_amd.precond import (apply_model, build_tree_preconditioner, lumped_mass,
-                                          pc_finish_model, pc_up_model, top_inverse_model)
+from networks_fenicsx_amd.precond import (apply_model, build_tree_preconditioner, coarse_solve_model,
+                                          lumped_mass, pc_finish_model, pc_up_model,
+                                          top_dense_multi_model, top_inverse_model)
 from oracle import nx_oracle as O
 
 
@@ -107,3 +108,41 @@ def test_dense_top_inverse_matches_back_substitution(depth, jobs):
             u[pc.job_root_u[j]] = It[c] + Jj[root] / T[c] / Dj[root]
     a_u = np.add.reduceat(u, pc.top_uoff[:-1]) if u.size else u
     np.testing.assert_allclose(a_u, a, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("case,P", [("depth6_N40", 2), ("depth6_N40", 4), ("arterial5_N40", 3)])
+def test_dense_top_several_ranks(case, P):
+    """Several ranks: coarse partial J = KJ a, top values = G_loc a + w zc[root] against
+    the exact multi-rank back-substitution of the model."""
+    make, N, strategy, _ = CASES[case]
+    m, Ab, lp1 = _problem(make(), N, strategy)
+    src, dst = m.edges
+    dqg = lumped_mass(Ab, lp1)
+    lps = [build_local_problem(m.node_coordinates, src, dst, m.degrees, N, r, P) for r in range(P)]
+    pcs = [build_tree_preconditioner(lp, src, dst, m.degrees) for lp in lps]
+    rng = np.random.default_rng(5)
+    sts = []
+    for lp, pc in zip(lps, pcs):
+        sts.append(pc_up_model(pc, lp, dqg[lp.edges], rng.standard_normal(lp.n_own)))
+    total = sum(st["partial"] for st in sts)
+    zc = coarse_solve_model(pcs[0], total)
+    for lp, pc, st in zip(lps, pcs, sts):
+        z = pc_finish_model(pc, lp, dqg[lp.edges], st, total)
+        T, Dj, Jj = st["T"], st["Dj"], st["Jj"]
+        ts0, ts1 = int(pc.top_lvl_off[0]), int(pc.top_lvl_off[-1])
+        a = Jj[ts0:ts1].copy()
+        for t in range(ts0, ts1):
+            p = pc.slot_parent[t]
+            if p >= ts0:
+                a[p - ts0] -= Jj[t] / T[pc.slot_pchain[t]] / Dj[t]
+        G, KJ, w, rootc = top_dense_multi_model(pc, T, Dj)
+        roots = [t - ts0 for t in range(ts0, ts1)
+                 if pc.slot_parent[t] < ts0 and pc.slot_cidx[t] >= 0]
+        assert roots
+        np.testing.assert_allclose((KJ @ a)[roots], Jj[ts0:ts1][roots], rtol=1e-12, atol=1e-13)
+        zt = G @ a + np.where(rootc >= 0, w * zc[np.maximum(rootc, 0)], 0.0)
+        zfull = np.zeros(lp.n_own + lp.n_ghost)
+        zfull[:lp.n_own] = z
+        own = pc.slot_lam[ts0:ts1] < lp.n_own
+        np.testing.assert_allclose(zt[own], zfull[pc.slot_lam[ts0:ts1]][own], rtol=1e-11,
+                                   atol=1e-13)
