@@ -61,7 +61,9 @@ def pmc_traffic(kernel_prefix: str):
     """Per-launch HBM bytes of a kernel from the newest committed PMC summary
     (profiles/<tag>_summary.json, written by scripts/summarize_profile.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same workload)."""
-    cands = sorted((REPO / "profiles").glob("*_summary.json"), key=lambda p: p.stat().st_mtime)
+    # profile tags sort by round and letter (r01b < r01i < r02a); file mtimes are not
+    # meaningful in a fresh checkout
+    cands = sorted((REPO / "profiles").glob("*_summary.json"), key=lambda p: p.name)
     for path in reversed(cands):
         doc = json.loads(path.read_text())
         for name, d in doc.get("kernels", {}).items():
@@ -99,7 +101,7 @@ def main() -> int:
     ap.add_argument("--levels", type=int, default=15, help="tree generations at 1 GPU")
     ap.add_argument("--N", type=int, default=15, help="cells per edge")
     ap.add_argument("--rtol", type=float, default=1e-12)
-    ap.add_argument("--check-every", type=int, default=32)
+    ap.add_argument("--check-every", type=int, default=4)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")

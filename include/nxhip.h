@@ -163,6 +163,16 @@ int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs, const int32
                     const int32_t* job_root_u, const int32_t* job_root_dc);
 
 /*
+ * Flux mass of the preconditioner: 1 (default) = the consistent P1 mass M, i.e. the exact
+ * Schur complement P = blockdiag(M, G^T M^{-1} G) -- P^{-1} A has three distinct eigenvalues
+ * and MINRES converges in 3 iterations; 0 = the lumped mass D (O(30) iterations). The
+ * junction elimination is the same for both (precond.py, "Exact variant"); only the chain
+ * outputs differ. NXHIP_PC_EXACT=0 makes 0 the default. Call after nx_set_preconditioner.
+ */
+int nx_set_pc_exact(nx_network_t* h, int32_t enable);
+int nx_get_pc_exact(nx_network_t* h, int32_t* enabled);
+
+/*
  * Coarse step of the preconditioner on a partitioned problem (precond.py derives it): the
  * coarse junctions (interface junctions + the junctions on paths between them inside a
  * rank) form a forest that every rank solves redundantly from one all-reduce of

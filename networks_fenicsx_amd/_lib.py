@@ -65,6 +65,8 @@ _SIGS = {
     "nx_set_halo": (C.c_int, [_h, _i32, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
     "nx_set_pc_dense": (C.c_int, [_h, _i32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                   _pi32, _pi32, _pi32, _pi32]),
+    "nx_set_pc_exact": (C.c_int, [_h, _i32]),
+    "nx_get_pc_exact": (C.c_int, [_h, _pi32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
     "nx_group_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
     "nx_group_destroy": (C.c_int, [_h]),
@@ -180,7 +182,7 @@ class Handle:
     def assemble(self, lhs: bool = True, rhs: bool = True) -> None:
         check(lib().nx_assemble(self.ptr, int(bool(lhs)), int(bool(rhs))))
 
-    def solve(self, rtol: float, maxit: int, check_every: int = 32):
+    def solve(self, rtol: float, maxit: int, check_every: int = 4):
         it, rr, conv = C.c_int32(), C.c_double(), C.c_int32()
         check(lib().nx_solve(self.ptr, float(rtol), int(maxit), int(check_every), C.byref(it),
                              C.byref(rr), C.byref(conv)))
@@ -299,6 +301,15 @@ class Handle:
                 q["cc_bot"], q["c_parent"], q["c_child_off"], q["c_child"],
                 int(pc.c_lvl_off.size - 1), q["c_lvl_off"]))
 
+    def set_pc_exact(self, enable: bool) -> None:
+        """Consistent (exact Schur complement, default) or lumped flux mass in P."""
+        check(lib().nx_set_pc_exact(self.ptr, int(bool(enable))))
+
+    def pc_exact(self) -> bool:
+        e = C.c_int32(0)
+        check(lib().nx_get_pc_exact(self.ptr, C.byref(e)))
+        return bool(e.value)
+
     def set_halo(self, nranks: int, rank: int, peers, send_off, send_idx, recv_off):
         """Halo plan without a transport (in-process group members)."""
         peers = np.ascontiguousarray(peers, dtype=np.int32)
@@ -335,7 +346,7 @@ class Group:
         check(lib().nx_group_create(len(self._handles), arr, C.byref(out)))
         self._g = out
 
-    def solve(self, rtol: float = 1e-12, maxit: int = 50000, check_every: int = 32):
+    def solve(self, rtol: float = 1e-12, maxit: int = 50000, check_every: int = 4):
         it = C.c_int32(0)
         rr = C.c_double(0.0)
         conv = C.c_int32(0)

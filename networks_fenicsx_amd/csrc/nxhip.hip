@@ -756,6 +756,13 @@ struct PcArgs {
   int* top_rootc;
   double* atop;
   double* zc;
+  // exact Schur complement (default): P = blockdiag(M, G^T M^{-1} G) with the consistent
+  // flux mass M instead of its lumped D (precond.py: "Exact variant"). The junction system
+  // is the same; only the chain outputs change: z_q = M_e^{-1} r_q (M_e = mo T per edge,
+  // mo = R h / 6, Tinv = T^{-1}, (N+1)^2, host-computed) and z_p = z_p(lumped) - mo r_p.
+  // MINRES then converges in 3 iterations (3 distinct eigenvalues of P^{-1} A).
+  int exact;
+  const double* Tinv;
 };
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
@@ -818,6 +825,7 @@ struct ChainLane {
   int64_t dof_qN;
   double rhoN;
   double T;
+  double mo;  // R h / 6 of the edge (its end flux's lumped mass is R h / 2)
 
   __device__ __forceinline__ void setup(const PcArgs& pa, int c, bool active) {
     const int N = pa.N;
@@ -826,6 +834,7 @@ struct ChainLane {
     const int flip = active ? pa.chain_flip[c] : 0;
     const int64_t base = (int64_t)e * (2 * N + 1);
     const double* dqe = pa.dq + (int64_t)e * (N + 1);
+    mo = active ? dqe[0] / 3.0 : 1.0;
     double acc = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
@@ -848,6 +857,62 @@ struct ChainLane {
     T = seg_sum<W>(acc + rhoN);
   }
 };
+
+// LDS doubles pc_flux_block needs per workgroup of BS threads (N + 1 <= W CPL + 1 per chain)
+template <int BS, int W, int CPL>
+constexpr int flux_lds() {
+  return BS / W * (W * CPL + 1);
+}
+
+// Flux block of P^{-1} on the block's current chains: z_q = r_q / rho (lumped D) or, exact,
+// z_q = M_e^{-1} r_q. rq[t] is the lane's r at chain flux k = l CPL + t, rqN at q_N (the
+// has_last lane). T^{-1} is symmetric and persymmetric, so chain direction (flip) does not
+// matter, and Tinv[i (N+1) + k] is read unit-stride across the lanes of a segment. Every
+// thread of the block must call this (barriers); returns the lane's share of r . z.
+template <int W, int CPL>
+__device__ __forceinline__ double pc_flux_block(const PcArgs& pa, const ChainLane<W, CPL>& ch,
+                                                const double* rq, double rqN, double* sQ,
+                                                double* __restrict__ z) {
+  double part = 0.0;
+  if (!pa.exact) {
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      if (!ch.valid[t]) continue;
+      const double zq = rq[t] / ch.rho[t];
+      z[ch.dof_q[t]] = zq;
+      part += rq[t] * zq;
+    }
+    if (ch.has_last) {
+      const double zq = rqN / ch.rhoN;
+      z[ch.dof_qN] = zq;
+      part += rqN * zq;
+    }
+    return part;
+  }
+  const int N = pa.N, n1 = N + 1;
+  const int l = threadIdx.x & (W - 1);
+  double* q = sQ + (threadIdx.x / W) * n1;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t)
+    if (ch.valid[t]) q[l * CPL + t] = rq[t];
+  if (ch.has_last) q[N] = rqN;
+  __syncthreads();
+  const double imo = 1.0 / ch.mo;
+  const double* __restrict__ Ti = pa.Tinv;
+#pragma unroll
+  for (int t = 0; t < CPL + 1; ++t) {
+    const bool on = t < CPL ? ch.valid[t] : ch.has_last;
+    if (!on) continue;
+    const int k = t < CPL ? l * CPL + t : N;
+    double acc = 0.0;
+    for (int i = 0; i < n1; ++i) acc += Ti[i * n1 + k] * q[i];
+    const double zq = acc * imo;
+    z[t < CPL ? ch.dof_q[t] : ch.dof_qN] = zq;
+    part += (t < CPL ? rq[t] : rqN) * zq;
+  }
+  __syncthreads();  // sQ is reused by the next chains
+  return part;
+}
 
 template <int BS>
 __device__ __forceinline__ void pc_eliminate(const PcArgs& pa, const double* __restrict__ y,
@@ -1001,6 +1066,7 @@ __global__ __launch_bounds__(kBlock) void k_pc_down(PcArgs pa, const double* __r
                                                     double* __restrict__ z,
                                                     const MrState* __restrict__ st,
                                                     double* __restrict__ partB, int mode) {
+  __shared__ double sQ[flux_lds<kBlock, W, CPL>()];
   if (mode == 0 && st->done) return;
   const int job = blockIdx.x;
   double part = 0.0;
@@ -1022,7 +1088,7 @@ __global__ __launch_bounds__(kBlock) void k_pc_down(PcArgs pa, const double* __r
     const double zt = up >= 0 ? z[pa.slot_lam[up]] : 0.0;
     const double zb = lo >= 0 ? z[pa.slot_lam[lo]] : 0.0;
     const double T = ch.T, iT = 1.0 / T;
-    double rc[CPL], a[CPL], b[CPL];
+    double rc[CPL], a[CPL], b[CPL], rq[CPL];
     double sa = 0.0, sb = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
@@ -1041,22 +1107,17 @@ __global__ __launch_bounds__(kBlock) void k_pc_down(PcArgs pa, const double* __r
       const double suffix = Atot - pa_ + a[t];
       const double prefix = pb_;  // sum_{j<k} b_j
       pb_ += b[t];
+      rq[t] = 0.0;
       if (!ch.valid[t]) continue;
       const double Dk = ch.D[t];
-      const double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      if (pa.exact) zk -= ch.mo * rc[t];
       z[ch.dof_c[t]] = zk;
       part += rc[t] * zk;
-      const double rq = y[ch.dof_q[t]];
-      const double zq = rq / ch.rho[t];
-      z[ch.dof_q[t]] = zq;
-      part += rq * zq;
+      rq[t] = y[ch.dof_q[t]];
     }
-    if (ch.has_last) {
-      const double rq = y[ch.dof_qN];
-      const double zq = rq / ch.rhoN;
-      z[ch.dof_qN] = zq;
-      part += rq * zq;
-    }
+    const double rqN = ch.has_last ? y[ch.dof_qN] : 0.0;
+    part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, sQ, z);
   }
   block_sum_store(part, partB + blockIdx.x);
 }
@@ -1396,6 +1457,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sTa[kCapT];  // dense top: a_s of every top slot
   __shared__ int sNs[kMaxNeed];
   __shared__ double sNz[kMaxNeed];
+  __shared__ double sQ[flux_lds<kPcThreads, W, CPL>()];
   if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
@@ -1510,7 +1572,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : outside(up);
     const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : outside(lo);
     const double T = ch.T, iT = 1.0 / T;
-    double rc[CPL], a[CPL], b[CPL];
+    double rc[CPL], a[CPL], b[CPL], rq[CPL];
     double sa = 0.0, sb = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
@@ -1529,9 +1591,11 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       const double suffix = Atot - pa_ + a[t];
       const double prefix = pb_;
       pb_ += b[t];
+      rq[t] = 0.0;
       if (!ch.valid[t]) continue;
       const double Dk = ch.D[t];
       double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      if (pa.exact) zk -= ch.mo * rc[t];  // P^{-1} of the consistent-mass Schur complement
       double rk = rc[t];
       if (lin) {
         zk -= c2 * z[ch.dof_c[t]];
@@ -1540,25 +1604,24 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       }
       z[ch.dof_c[t]] = zk;
       part += rk * zk;
-      double rq = y[ch.dof_q[t]];
+      // flux: P^{-1} r' = P^{-1} y - c2 P^{-1} r2 and z_old = P^{-1} r2, so the block is
+      // applied to r' directly (z_q needs no separate linear-form correction)
+      double r = y[ch.dof_q[t]];
       if (lin) {
-        rq -= c2 * r2[ch.dof_q[t]];
-        y[ch.dof_q[t]] = rq;
+        r -= c2 * r2[ch.dof_q[t]];
+        y[ch.dof_q[t]] = r;
       }
-      const double zq = rq / ch.rho[t];
-      z[ch.dof_q[t]] = zq;
-      part += rq * zq;
+      rq[t] = r;
     }
+    double rqN = 0.0;
     if (ch.has_last) {
-      double rq = y[ch.dof_qN];
+      rqN = y[ch.dof_qN];
       if (lin) {
-        rq -= c2 * r2[ch.dof_qN];
-        y[ch.dof_qN] = rq;
+        rqN -= c2 * r2[ch.dof_qN];
+        y[ch.dof_qN] = rqN;
       }
-      const double zq = rq / ch.rhoN;
-      z[ch.dof_qN] = zq;
-      part += rq * zq;
     }
+    part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, sQ, z);
   }
   NX_PHASE(51);
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
@@ -2214,6 +2277,35 @@ int build_chunk_graph(const Team& t, int len) {
 int set_device(nx_network* h) {
   HIPCALL(hipSetDevice(h->device));
   return NX_OK;
+}
+
+// T^{-1} for the P1 mass matrix of one edge, M_e = (R h / 6) T, T = tridiag(1, 4, 1) of
+// size N+1 with 2 at both ends (assembly.py:253 on equal cells). Columns by the Thomas
+// algorithm (T is SPD and diagonally dominant); row-major (N+1)^2, symmetric.
+std::vector<double> mass_tinv(int N) {
+  const int n = N + 1;
+  std::vector<double> inv((size_t)n * n, 0.0), cp(n), dp(n);
+  auto diag = [&](int i) { return (i == 0 || i == N) ? 2.0 : 4.0; };
+  for (int k = 0; k < n; ++k) {
+    for (int i = 0; i < n; ++i) {  // forward sweep on e_k
+      const double a = i > 0 ? 1.0 : 0.0;
+      const double den = diag(i) - a * (i > 0 ? cp[i - 1] : 0.0);
+      cp[i] = (i < N ? 1.0 : 0.0) / den;
+      dp[i] = ((i == k ? 1.0 : 0.0) - a * (i > 0 ? dp[i - 1] : 0.0)) / den;
+    }
+    double x = dp[N];
+    inv[(size_t)N * n + k] = x;
+    for (int i = N - 1; i >= 0; --i) {
+      x = dp[i] - cp[i] * x;
+      inv[(size_t)i * n + k] = x;
+    }
+  }
+  for (int i = 0; i < n; ++i)  // exact symmetry (the sweeps differ in the last bits)
+    for (int j = i + 1; j < n; ++j) {
+      const double s = 0.5 * (inv[(size_t)i * n + j] + inv[(size_t)j * n + i]);
+      inv[(size_t)i * n + j] = inv[(size_t)j * n + i] = s;
+    }
+  return inv;
 }
 
 }  // namespace
@@ -2918,6 +3010,17 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.slot_invD = scratch(n_slots);
   if (const char* e = std::getenv("NXHIP_PC_FACTOR"))
     if (std::atoi(e) == 0) pa.dc_kappa = nullptr;  // keep the per-iteration eliminations
+  {  // consistent-mass flux block: T^{-1}, T = tridiag(1, 4, 1) with 2 at both ends
+    const std::vector<double> ti = mass_tinv(N);
+    double* d = scratch((int64_t)ti.size());
+    if (d == nullptr || hipMemcpy(d, ti.data(), sizeof(double) * ti.size(), hipMemcpyHostToDevice) !=
+                            hipSuccess)
+      return fail(NX_ERR_HIP, "preconditioner upload failed");
+    pa.Tinv = d;
+    pa.exact = 1;
+    if (const char* e = std::getenv("NXHIP_PC_EXACT"))
+      if (std::atoi(e) == 0) pa.exact = 0;  // lumped D: P = blockdiag(D, G^T D^{-1} G)
+  }
   for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
                         (const void*)pa.chain_lo, (const void*)pa.slot_lam, (const void*)pa.slot_pchain,
                         (const void*)pa.slot_parent, (const void*)pa.slot_dc_off, (const void*)pa.slot_dc,
@@ -3053,6 +3156,25 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
     return fail(NX_ERR_HIP, "dense top upload failed");
   pa.n_top = nt;
   pa.dense = 1;
+  return NX_OK;
+}
+
+NX_API int nx_set_pc_exact(nx_network_t* h, int32_t enable) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  {
+    nx_network* hs[1] = {h};
+    CHECK(drop_graph(graph_slot(Team{hs, 1, nullptr})));
+  }
+  h->pa.exact = enable ? 1 : 0;
+  return NX_OK;
+}
+
+NX_API int nx_get_pc_exact(nx_network_t* h, int32_t* enabled) {
+  if (!h || !enabled) return fail(NX_ERR_ARG, "null argument");
+  *enabled = h->pc ? h->pa.exact : 0;
   return NX_OK;
 }
 

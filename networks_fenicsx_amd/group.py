@@ -59,7 +59,7 @@ class RankGroup:
         for a in self.assemblers:
             a.set_preconditioner(enable)
 
-    def solve(self, rtol: float = 1e-12, maxit: int = 50000, check_every: int = 32):
+    def solve(self, rtol: float = 1e-12, maxit: int = 50000, check_every: int = 4):
         """MINRES over all ranks; returns ``(iterations, relres, converged)``."""
         if self._group is None:
             self._group = _lib.Group([a.handle for a in self.assemblers])

@@ -30,6 +30,20 @@ junction levels) number a few hundred and the *top* part (all junctions above th
 one workgroup, junction math only) stays small; chains whose lower end is in the top part
 are handed round-robin to the lower jobs (one workgroup per job, no extra launches).
 
+Exact variant (the default). With the *consistent* mass ``M`` instead of ``D`` the
+preconditioner ``P = blockdiag(M, G^T M^{-1} G)`` makes ``P^{-1} A`` have exactly three
+eigenvalues ``{1, (1 +- sqrt 5)/2}`` (Murphy, Golub & Wathen 2000), so MINRES converges
+in 3 iterations. On one edge the flux constraint ``-B u = r_p`` fixes ``u`` up to its
+start value ``u_0``, and ``1^T M = 1^T D = d^T`` (the column sums of the P1 mass are the
+lumped mass), so ``u_0`` -- hence the whole junction system -- is identical for ``M`` and
+``D``. Only the chain outputs change: the cell values are prefix sums of ``M u`` instead
+of ``D u``, and ``(M - D) u`` telescopes (``u_{k+1} - u_k = -r_p[k]``) to
+
+    (G^T M^{-1} G)^{-1} = (G^T D^{-1} G)^{-1} - (R h / 6) I   on the pressure cells,
+
+while the flux block becomes ``M_e^{-1} r_q = (6 / (R h)) T^{-1} r_q`` with the fixed
+``T = tridiag(1, 4, 1)`` (2 at both ends) of size N+1.
+
 Graphs that are not trees use the same machinery on a spanning forest: a chain that
 would close a cycle is grounded at one end. ``P`` stays SPD (a grounded Laplacian block);
 only its quality drops.
@@ -53,7 +67,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-__all__ = ["CoarseStructure", "TreePreconditioner", "build_tree_preconditioner",
+__all__ = ["CoarseStructure", "TreePreconditioner", "build_tree_preconditioner", "mass_tinv",
            "coarse_structure", "apply_model", "pc_up_model", "pc_finish_model"]
 
 _EMPTY_I = np.zeros(0, dtype=np.int32)
@@ -614,12 +628,23 @@ def lumped_mass(Ab, lp) -> np.ndarray:
     return d.reshape(E, N + 1)
 
 
-def apply_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray) -> np.ndarray:
+def mass_tinv(N: int) -> np.ndarray:
+    """``T^{-1}`` for the P1 mass of one edge, ``M_e = (R h / 6) T``, ``T = tridiag(1, 4, 1)``
+    of size N+1 with 2 at both ends (``assembly.py:253`` on N equal cells)."""
+    T = (np.diag(np.r_[2.0, np.full(N - 1, 4.0), 2.0]) if N > 0 else np.eye(1))
+    T += np.diag(np.ones(N), 1) + np.diag(np.ones(N), -1)
+    Ti = np.linalg.inv(T)
+    return 0.5 * (Ti + Ti.T)
+
+
+def apply_model(pc: TreePreconditioner, lp, dq: np.ndarray, r: np.ndarray,
+                exact: bool = True) -> np.ndarray:
     """numpy model of the device application ``z = P^{-1} r`` on one rank (no coarse
     exchange: with several ranks use :func:`pc_up_model` / :func:`pc_finish_model` around
-    a sum of the partials over ranks)."""
+    a sum of the partials over ranks). ``exact``: consistent flux mass (the device
+    default), else the lumped one."""
     st = pc_up_model(pc, lp, dq, r)
-    return pc_finish_model(pc, lp, dq, st, st["partial"])
+    return pc_finish_model(pc, lp, dq, st, st["partial"], exact=exact)
 
 
 def _chain_dofs(pc, dq, c):
@@ -716,10 +741,11 @@ def coarse_solve_model(pc: TreePreconditioner, total: np.ndarray) -> np.ndarray:
 
 
 def pc_finish_model(pc: TreePreconditioner, lp, dq: np.ndarray, st: dict,
-                    total: np.ndarray) -> np.ndarray:
+                    total: np.ndarray, exact: bool = True) -> np.ndarray:
     """Coarse solve, back-substitution and chain cells (k_pc_coarse / top + k_pc_down).
-    Returns z on the owned DoFs."""
+    Returns z on the owned DoFs. ``exact``: the consistent-mass variant (module doc)."""
     N = pc.N
+    Ti = mass_tinv(N) if exact else None
     rr, T, Dj, Jj = st["r"], st["T"], st["Dj"], st["Jj"]
     z = np.zeros_like(rr)
     zc = coarse_solve_model(pc, total) if pc.n_coarse else np.zeros(0)
@@ -756,5 +782,10 @@ def pc_finish_model(pc: TreePreconditioner, lp, dq: np.ndarray, st: dict,
         b = Dk * rp  # prefix sums j < k
         pre = np.concatenate([[0.0], np.cumsum(b)[:-1]])
         z[cells] = zt * (Tc - Dk) / Tc + zb * Dk / Tc + (Dk / Tc) * suf + ((Tc - Dk) / Tc) * pre
-        z[qs] = rr[qs] / rho
+        if exact:
+            mo = rho[0] / 3.0  # R h / 6
+            z[cells] -= mo * rp
+            z[qs] = (Ti @ rr[qs]) / mo
+        else:
+            z[qs] = rr[qs] / rho
     return z[:lp.n_own]

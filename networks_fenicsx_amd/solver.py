@@ -15,11 +15,14 @@ PETSc options understood (with or without the options prefix):
 ``ksp_max_it``                    iteration cap (default 50000)
 ``ksp_error_if_not_converged``    raise :class:`NxNotConverged` (default True)
 ``ksp_monitor``                   print iterations / residual after each solve
-``ksp_check_every``               iterations per host convergence check (default 32)
+``ksp_check_every``               iterations per host convergence check (default 4: the exact
+                                  preconditioner converges in 3, + 1 launch for the last update)
 
 ``pc_type``                       ``"none"`` runs plain MINRES; anything else (the reference's
                                   default ``"lu"`` included) uses the tree Schur-complement
                                   preconditioner (``precond.py``)
+``pc_mass``                       ``"consistent"`` (default: exact Schur complement, 3 MINRES
+                                  iterations) or ``"lumped"``
 
 ``ksp_type`` and ``pc_factor_mat_solver_type`` are accepted and recorded: whatever they
 say, the device solve is MINRES (a direct LU has no place on this path); the tolerance
@@ -108,11 +111,12 @@ class Solver:
             clean[key.lstrip("-")] = v
         self._rtol = float(clean.get("ksp_rtol", 1e-12))
         self._maxit = int(clean.get("ksp_max_it", 50000))
-        self._check_every = int(clean.get("ksp_check_every", 32))
+        self._check_every = int(clean.get("ksp_check_every", 4))
         self._raise = _truthy(clean.get("ksp_error_if_not_converged", True))
         self._monitor = "ksp_monitor" in clean and _truthy(clean["ksp_monitor"])
         self._ksp = KSPInfo(petsc_options_prefix, clean)
         self._pc = str(clean.get("pc_type", "lu")).lower() != "none"
+        self._pc_exact = str(clean.get("pc_mass", "consistent")).lower() != "lumped"
         self._kind = kind
         self._A = DeviceMatrix(assembler.handle, kind)
         self._b = DeviceVector(assembler.handle)
@@ -152,6 +156,8 @@ class Solver:
         h = self.assembler.handle
         if self.assembler.preconditioned != self._pc:
             self.assembler.set_preconditioner(self._pc)
+        if self.assembler.preconditioned and h.pc_exact() != self._pc_exact:
+            h.set_pc_exact(self._pc_exact)
         it, relres, conv = h.solve(self._rtol, self._maxit, self._check_every)
         self._ksp.iterations, self._ksp.residual_estimate, self._ksp.converged = it, relres, conv
         if self._monitor:

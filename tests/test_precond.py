@@ -27,8 +27,10 @@ def _problem(G, N, strategy=None):
 
 @pytest.mark.parametrize("case", ["depth6_N40", "arterial5_N40", "tree6_2d_N70", "Y_N4"])
 @pytest.mark.parametrize("jobs", [4, 16, 256])
-def test_exact_schur_solve_on_trees(case, jobs):
-    """P^{-1} from the decomposition equals a direct solve of blockdiag(D, G^T D^-1 G)."""
+@pytest.mark.parametrize("exact", [False, True])
+def test_exact_schur_solve_on_trees(case, jobs, exact):
+    """P^{-1} from the decomposition equals a direct solve of blockdiag(D, G^T D^-1 G)
+    (lumped) or of blockdiag(M, G^T M^-1 G) (consistent mass, the exact Schur complement)."""
     make, N, strategy, _ = CASES[case]
     m, Ab, lp = _problem(make(), N, strategy)
     src, dst = m.edges
@@ -41,12 +43,43 @@ def test_exact_schur_solve_on_trees(case, jobs):
     other = np.setdiff1d(np.arange(n), qrows)
     Dq = dq.ravel()
     Gm = Ab[qrows][:, other].toarray()
-    S = Gm.T @ (Gm / Dq[:, None])
     r = np.random.default_rng(3).standard_normal(n)
-    z = apply_model(pc, lp, dq, r)
-    np.testing.assert_allclose(z[qrows], r[qrows] / Dq, rtol=1e-13)
+    z = apply_model(pc, lp, dq, r, exact=exact)
+    if exact:
+        M = Ab[qrows][:, qrows].toarray()
+        S = Gm.T @ np.linalg.solve(M, Gm)
+        zq = np.linalg.solve(M, r[qrows])
+        assert np.linalg.norm(z[qrows] - zq) <= 1e-12 * np.linalg.norm(zq)
+    else:
+        S = Gm.T @ (Gm / Dq[:, None])
+        np.testing.assert_allclose(z[qrows], r[qrows] / Dq, rtol=1e-13)
     zs = np.linalg.solve(S, r[other])
     assert np.linalg.norm(z[other] - zs) <= 1e-11 * np.linalg.norm(zs)
+
+
+@pytest.mark.parametrize("case", ["depth6_N40", "arterial5_N40", "Y_N4"])
+def test_exact_preconditioner_three_iterations(case):
+    """With the consistent-mass Schur complement, P^{-1} A has three distinct eigenvalues
+    (Murphy-Golub-Wathen): preconditioned MINRES reaches the direct solution in 3 steps."""
+    import scipy.sparse.linalg as spla
+
+    make, N, strategy, _ = CASES[case]
+    m, Ab, lp = _problem(make(), N, strategy)
+    src, dst = m.edges
+    pc = build_tree_preconditioner(lp, src, dst, m.degrees, target_jobs=16)
+    dq = lumped_mass(Ab, lp)
+    n = Ab.shape[0]
+    b = np.random.default_rng(5).standard_normal(n)
+    x_direct = spla.spsolve(Ab.tocsc(), b)
+    its = [0]
+
+    def count(_x):
+        its[0] += 1
+
+    P = spla.LinearOperator((n, n), matvec=lambda r: apply_model(pc, lp, dq, r, exact=True))
+    x, info = spla.minres(Ab, b, M=P, rtol=1e-12, maxiter=50, callback=count)
+    assert info == 0 and its[0] <= 4
+    assert np.linalg.norm(x - x_direct) <= 1e-10 * np.linalg.norm(x_direct)
 
 
 @pytest.mark.parametrize("depth,jobs", [(6, 8), (8, 16), (9, 64)])
