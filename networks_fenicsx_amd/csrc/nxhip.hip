@@ -25,6 +25,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -546,20 +547,55 @@ struct MrVecs {
   double* v;         // preconditioned: v_{k-1} in, v_k = z_k / beta_k out (in place)
 };
 
+// Initial state from beta_1^2 (k_mr_init, or k_mr_a of iteration 1 in the single-rank head
+// graph, which folds the initialisation in).
+__device__ __forceinline__ MrState mr_initial(double bb, double rtol, int maxit) {
+  const double beta1 = sqrt(bb);
+  MrState s{};
+  s.beta1 = beta1;
+  s.beta = beta1;
+  s.phibar = beta1;
+  s.cs = -1.0;
+  s.rtol = rtol;
+  s.maxit = maxit;
+  s.relres = beta1 > 0.0 ? 1.0 : 0.0;
+  if (beta1 == 0.0) {
+    s.done = 1;
+    s.converged = 1;
+  }
+  return s;
+}
+
+struct MrInit {  // on = 1: iteration 1 starts the solve from beta_1^2 = sum(part[0..np))
+  int on;
+  int np;
+  int maxit;
+  double rtol;
+  const double* part;
+};
+
+// w_{k-3}, w_{k-2} and x are not initialised in memory: the first rotations read them as
+// zero (it0 = completed rotations before this one), so the solve needs no memsets.
 template <bool MULTI, bool PC>
 __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState* __restrict__ sin,
                                                  MrState* __restrict__ sout,
                                                  const double* __restrict__ partB, int nB,
                                                  const double* __restrict__ red,
-                                                 double* __restrict__ partA, int chunksA) {
-  if (sin->done) return;
+                                                 double* __restrict__ partA, int chunksA,
+                                                 MrInit ini) {
+  if (!ini.on && sin->done) return;
   NX_PHASE_START(0);
-  MrState s = *sin;
+  MrState s = ini.on ? mr_initial(block_allsum(ini.part, ini.np), ini.rtol, ini.maxit) : *sin;
   Rot rot{0.0, 0.0, 0.0, 0.0};
   const bool upd = s.nb > 0;  // a Lanczos step is waiting for its rotation
+  const int it0 = s.it;
   if (upd) rot = mr_rotate(s, MULTI ? red[1] : block_allsum(partB, nB));
   NX_PHASE(1);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *sout = s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *sout = s;
+    if (ini.on) *const_cast<MrState*>(sin) = s;  // both buffers start identical
+  }
+  if (ini.on && s.done) return;  // b = 0
   const double beta = s.beta, oldb = s.oldb;  // beta_k, beta_{k-1}
   const double sc = 1.0 / beta;
   const double c1 = upd ? beta / oldb : 0.0;
@@ -573,12 +609,14 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
     const double Ay = spmv ? spmv_row_sum(A, g, r0, nr) : 0.0;
     if ((int)threadIdx.x < nr) {
       const int64_t r = r0 + threadIdx.x;
-      const double r1v = v.r1[r];
+      const double r1v = upd ? v.r1[r] : 0.0;  // c1 = 0 in iteration 1
       if (upd) {  // w = (v - oldeps w1 - delta w2) / gamma ; x += phi w
         const double vk = PC ? v.v[r] : r1v / oldb;
-        const double wn = (vk - rot.oldeps * v.w1[r] - rot.delta * v.w2[r]) * rot.denom;
+        const double w1v = it0 >= 2 ? v.w1[r] : 0.0;  // w_{k-3}, w_{k-2}: zero at first
+        const double w2v = it0 >= 1 ? v.w2[r] : 0.0;
+        const double wn = (vk - rot.oldeps * w1v - rot.delta * w2v) * rot.denom;
         v.w1[r] = wn;
-        v.x[r] += rot.phi * wn;
+        v.x[r] = (it0 >= 1 ? v.x[r] : 0.0) + rot.phi * wn;
       }
       if (spmv) {
         const double vn = sc * g[r];
@@ -642,22 +680,7 @@ __global__ __launch_bounds__(kBlock) void k_mr_init(const double* __restrict__ p
                                                     MrState* __restrict__ st, double rtol,
                                                     int maxit) {
   const double bb = MULTI ? red[2] : block_allsum(part, np);
-  if (threadIdx.x == 0) {
-    const double beta1 = sqrt(bb);
-    MrState s{};
-    s.beta1 = beta1;
-    s.beta = beta1;
-    s.phibar = beta1;
-    s.cs = -1.0;
-    s.rtol = rtol;
-    s.maxit = maxit;
-    s.relres = beta1 > 0.0 ? 1.0 : 0.0;
-    if (beta1 == 0.0) {
-      s.done = 1;
-      s.converged = 1;
-    }
-    *st = s;
-  }
+  if (threadIdx.x == 0) *st = mr_initial(bb, rtol, maxit);
 }
 
 // Reduce partials into red[slot] (multi-rank: then all-reduced).
@@ -759,10 +782,11 @@ struct PcArgs {
   // exact Schur complement (default): P = blockdiag(M, G^T M^{-1} G) with the consistent
   // flux mass M instead of its lumped D (precond.py: "Exact variant"). The junction system
   // is the same; only the chain outputs change: z_q = M_e^{-1} r_q (M_e = mo T per edge,
-  // mo = R h / 6, Tinv = T^{-1}, (N+1)^2, host-computed) and z_p = z_p(lumped) - mo r_p.
+  // mo = R h / 6, T = tridiag(1, 4, 1), 2 at both ends, solved by Thomas scans with the
+  // host-computed pivots Tlu = [l_k | 1/u_k]) and z_p = z_p(lumped) - mo r_p.
   // MINRES then converges in 3 iterations (3 distinct eigenvalues of P^{-1} A).
   int exact;
-  const double* Tinv;
+  const double* Tlu;
 };
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
@@ -858,20 +882,16 @@ struct ChainLane {
   }
 };
 
-// LDS doubles pc_flux_block needs per workgroup of BS threads (N + 1 <= W CPL + 1 per chain)
-template <int BS, int W, int CPL>
-constexpr int flux_lds() {
-  return BS / W * (W * CPL + 1);
-}
-
 // Flux block of P^{-1} on the block's current chains: z_q = r_q / rho (lumped D) or, exact,
-// z_q = M_e^{-1} r_q. rq[t] is the lane's r at chain flux k = l CPL + t, rqN at q_N (the
-// has_last lane). T^{-1} is symmetric and persymmetric, so chain direction (flip) does not
-// matter, and Tinv[i (N+1) + k] is read unit-stride across the lanes of a segment. Every
-// thread of the block must call this (barriers); returns the lane's share of r . z.
+// z_q = M_e^{-1} r_q = T^{-1} r_q / mo by the Thomas algorithm run as two segment scans of
+// affine maps (T = L U with pivots fixed by N: forward y_k = r_k - l_k y_{k-1}, backward
+// x_k = (y_k - x_{k+1}) / u_k; pa.Tlu = [l_0..l_N | 1/u_0..1/u_N], l_0 = 0). T is
+// persymmetric, so the chain direction (flip) does not matter. rq[t] is the lane's r at
+// chain flux k = l CPL + t, rqN at q_N (the has_last lane, right after its last cell's
+// flux). No LDS, no barriers; returns the lane's share of r . z.
 template <int W, int CPL>
 __device__ __forceinline__ double pc_flux_block(const PcArgs& pa, const ChainLane<W, CPL>& ch,
-                                                const double* rq, double rqN, double* sQ,
+                                                const double* rq, double rqN,
                                                 double* __restrict__ z) {
   double part = 0.0;
   if (!pa.exact) {
@@ -889,28 +909,73 @@ __device__ __forceinline__ double pc_flux_block(const PcArgs& pa, const ChainLan
     }
     return part;
   }
-  const int N = pa.N, n1 = N + 1;
+  constexpr int NE = CPL + 1;  // the lane's elements: its cells' fluxes, then q_N
+  const int N = pa.N;
   const int l = threadIdx.x & (W - 1);
-  double* q = sQ + (threadIdx.x / W) * n1;
+  const double* __restrict__ lu = pa.Tlu;
+  bool on[NE];
+  double v[NE], lk[NE], iu[NE];
 #pragma unroll
-  for (int t = 0; t < CPL; ++t)
-    if (ch.valid[t]) q[l * CPL + t] = rq[t];
-  if (ch.has_last) q[N] = rqN;
-  __syncthreads();
-  const double imo = 1.0 / ch.mo;
-  const double* __restrict__ Ti = pa.Tinv;
-#pragma unroll
-  for (int t = 0; t < CPL + 1; ++t) {
-    const bool on = t < CPL ? ch.valid[t] : ch.has_last;
-    if (!on) continue;
+  for (int t = 0; t < NE; ++t) {
+    on[t] = t < CPL ? ch.valid[t] : ch.has_last;
     const int k = t < CPL ? l * CPL + t : N;
-    double acc = 0.0;
-    for (int i = 0; i < n1; ++i) acc += Ti[i * n1 + k] * q[i];
-    const double zq = acc * imo;
-    z[t < CPL ? ch.dof_q[t] : ch.dof_qN] = zq;
-    part += (t < CPL ? rq[t] : rqN) * zq;
+    v[t] = t < CPL ? rq[t] : rqN;
+    lk[t] = on[t] ? lu[k] : 0.0;
+    iu[t] = on[t] ? lu[N + 1 + k] : 0.0;
   }
-  __syncthreads();  // sQ is reused by the next chains
+  // forward: y_k = -l_k y_{k-1} + r_k; the lane's composite map, then an inclusive scan
+  double A = 1.0, B = 0.0;
+#pragma unroll
+  for (int t = 0; t < NE; ++t)
+    if (on[t]) {
+      B = -lk[t] * B + v[t];
+      A = -lk[t] * A;
+    }
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) {
+    const double Ap = __shfl_up(A, o, W), Bp = __shfl_up(B, o, W);
+    if (l >= o) {
+      B = A * Bp + B;
+      A = A * Ap;
+    }
+  }
+  double y = __shfl_up(B, 1, W);  // y at the end of the previous lane (0 before q_0)
+  if (l == 0) y = 0.0;
+#pragma unroll
+  for (int t = 0; t < NE; ++t)
+    if (on[t]) {
+      y = -lk[t] * y + v[t];
+      v[t] = y;
+    }
+  // backward: x_k = (y_k - x_{k+1}) / u_k; composite over the lane (last element first),
+  // then a suffix scan across lanes
+  A = 1.0;
+  B = 0.0;
+#pragma unroll
+  for (int t = NE - 1; t >= 0; --t)
+    if (on[t]) {
+      B = iu[t] * (v[t] - B);
+      A = -iu[t] * A;
+    }
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) {
+    const double An = __shfl_down(A, o, W), Bn = __shfl_down(B, o, W);
+    if (l + o < W) {
+      B = A * Bn + B;
+      A = A * An;
+    }
+  }
+  double x = __shfl_down(B, 1, W);  // x at the start of the next lane (0 after q_N)
+  if (l == W - 1) x = 0.0;
+  const double imo = 1.0 / ch.mo;
+#pragma unroll
+  for (int t = NE - 1; t >= 0; --t)
+    if (on[t]) {
+      x = iu[t] * (v[t] - x);
+      const double zq = x * imo;
+      z[t < CPL ? ch.dof_q[t] : ch.dof_qN] = zq;
+      part += (t < CPL ? rq[t] : rqN) * zq;
+    }
   return part;
 }
 
@@ -1066,7 +1131,6 @@ __global__ __launch_bounds__(kBlock) void k_pc_down(PcArgs pa, const double* __r
                                                     double* __restrict__ z,
                                                     const MrState* __restrict__ st,
                                                     double* __restrict__ partB, int mode) {
-  __shared__ double sQ[flux_lds<kBlock, W, CPL>()];
   if (mode == 0 && st->done) return;
   const int job = blockIdx.x;
   double part = 0.0;
@@ -1117,7 +1181,7 @@ __global__ __launch_bounds__(kBlock) void k_pc_down(PcArgs pa, const double* __r
       rq[t] = y[ch.dof_q[t]];
     }
     const double rqN = ch.has_last ? y[ch.dof_qN] : 0.0;
-    part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, sQ, z);
+    part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, z);
   }
   block_sum_store(part, partB + blockIdx.x);
 }
@@ -1457,7 +1521,6 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sTa[kCapT];  // dense top: a_s of every top slot
   __shared__ int sNs[kMaxNeed];
   __shared__ double sNz[kMaxNeed];
-  __shared__ double sQ[flux_lds<kPcThreads, W, CPL>()];
   if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
@@ -1621,7 +1684,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
         y[ch.dof_qN] = rqN;
       }
     }
-    part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, sQ, z);
+    part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, z);
   }
   NX_PHASE(51);
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
@@ -1704,10 +1767,33 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_cpart(PcArgs pa, const MrSta
 // Dense top: column s of G = response of the top part to a unit J at top slot s (J up the
 // ancestors with kappa = g_up / D, then the root-to-leaf back-substitution). One wave per
 // column; once per solve (D is fixed by the assembly).
-__global__ __launch_bounds__(64) void k_pc_gbuild(PcArgs pa) {
+__device__ void pc_gbuild_column(const PcArgs& pa, int s);
+
+__global__ __launch_bounds__(64) void k_pc_gbuild(PcArgs pa) { pc_gbuild_column(pa, blockIdx.x); }
+
+// Single-rank head graph, once per solve and concurrent with the start application's down
+// sweep (they touch disjoint data): the factored coefficients (k_pc_factor), G's columns
+// (k_pc_gbuild, n_gcols = n_top or 0) and r2 = b for iteration 1 (the start condensed b
+// straight from the rhs, so this replaces the two vector copies of the general path).
+__global__ __launch_bounds__(64) void k_pc_prep(PcArgs pa, int n_dc, int n_slots, int n_gcols,
+                                                const double* __restrict__ b,
+                                                double* __restrict__ r2, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  const int64_t i0 = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  for (int64_t i = i0; i < n; i += stride) r2[i] = b[i];
+  for (int64_t i = i0; i < n_dc || i < n_slots; i += stride) {
+    if (i < n_dc) {
+      const int lo = pa.dc_lo[i];
+      pa.dc_kappa[i] = lo >= 0 ? 1.0 / pa.chain_T[pa.slot_dc[i]] / pa.slot_D[lo] : 0.0;
+    }
+    if (i < n_slots) pa.slot_invD[i] = 1.0 / pa.slot_D[i];
+  }
+  if ((int)blockIdx.x < n_gcols) pc_gbuild_column(pa, blockIdx.x);
+}
+
+__device__ void pc_gbuild_column(const PcArgs& pa, int s) {
   __shared__ double sJ[kCapT], sZ[kCapT];
   const int nt = pa.n_top, ts0 = pa.top_lvl_off[0];
-  const int s = blockIdx.x;
   for (int i = threadIdx.x; i < nt; i += 64) sJ[i] = 0.0;
   __syncthreads();
   const bool cd = pa.KJ != nullptr;  // several ranks: coarse roots are Dirichlet nodes
@@ -1927,6 +2013,18 @@ struct nx_network {
   hipGraphExec_t chunk_exec = nullptr;
   hipGraph_t chunk_graph = nullptr;
   int chunk_len = 0;
+  // single rank with the preconditioner (solve_lean): the head graph (start application,
+  // k_pc_prep on the side stream, iterations 1..L) and its continuation chunks
+  hipGraphExec_t head_exec = nullptr;
+  hipGraph_t head_graph = nullptr;
+  int head_len = 0;
+  double head_rtol = 0.0;
+  int head_maxit = 0;
+  hipGraphExec_t lchunk_exec = nullptr;
+  hipGraph_t lchunk_graph = nullptr;
+  int lchunk_len = 0;
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // profiling
   bool prof = false;
   double spmv_ms = 0.0, asm_ms = 0.0;
@@ -2203,7 +2301,8 @@ int launch_iteration(const Team& t, int64_t k) {
 #define NX_LAUNCH_A(M, P)                                                                        \
   hipExtLaunchKernelGGL((k_mr_a<M, P>), dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,     \
                         csr_of(h), mv, sin, sout, p2p_beta ? h->gath : h->partB,              \
-                        p2p_beta ? h->nranks : nB, h->red, h->partA, h->chunksA)
+                        p2p_beta ? h->nranks : nB, h->red, h->partA, h->chunksA,             \
+                        MrInit{0, 0, 0, 0.0, nullptr})
     if (multi && !p2p_beta) {
       if (pc) NX_LAUNCH_A(true, true); else NX_LAUNCH_A(true, false);
     } else {
@@ -2239,20 +2338,30 @@ struct GraphSlot {
   hipGraphExec_t* exec;
   hipGraph_t* graph;
   int* len;
+  nx_network* lean;  // single handle: its head / continuation graphs go too
 };
 
 GraphSlot graph_slot(const Team& t) {
-  if (t.g) return GraphSlot{&t.g->chunk_exec, &t.g->chunk_graph, &t.g->chunk_len};
+  if (t.g) return GraphSlot{&t.g->chunk_exec, &t.g->chunk_graph, &t.g->chunk_len, nullptr};
   nx_network* h = t.hs[0];
-  return GraphSlot{&h->chunk_exec, &h->chunk_graph, &h->chunk_len};
+  return GraphSlot{&h->chunk_exec, &h->chunk_graph, &h->chunk_len, h};
+}
+
+int drop_one(hipGraphExec_t* exec, hipGraph_t* graph, int* len) {
+  if (*exec) HIPCALL(hipGraphExecDestroy(*exec));
+  if (*graph) HIPCALL(hipGraphDestroy(*graph));
+  *exec = nullptr;
+  *graph = nullptr;
+  *len = 0;
+  return NX_OK;
 }
 
 int drop_graph(GraphSlot gs) {
-  if (*gs.exec) HIPCALL(hipGraphExecDestroy(*gs.exec));
-  if (*gs.graph) HIPCALL(hipGraphDestroy(*gs.graph));
-  *gs.exec = nullptr;
-  *gs.graph = nullptr;
-  *gs.len = 0;
+  CHECK(drop_one(gs.exec, gs.graph, gs.len));
+  if (gs.lean) {
+    CHECK(drop_one(&gs.lean->head_exec, &gs.lean->head_graph, &gs.lean->head_len));
+    CHECK(drop_one(&gs.lean->lchunk_exec, &gs.lean->lchunk_graph, &gs.lean->lchunk_len));
+  }
   return NX_OK;
 }
 
@@ -2279,33 +2388,22 @@ int set_device(nx_network* h) {
   return NX_OK;
 }
 
-// T^{-1} for the P1 mass matrix of one edge, M_e = (R h / 6) T, T = tridiag(1, 4, 1) of
-// size N+1 with 2 at both ends (assembly.py:253 on equal cells). Columns by the Thomas
-// algorithm (T is SPD and diagonally dominant); row-major (N+1)^2, symmetric.
-std::vector<double> mass_tinv(int N) {
+// Pivots of the P1 mass matrix of one edge, M_e = (R h / 6) T, T = tridiag(1, 4, 1) of size
+// N+1 with 2 at both ends (assembly.py:253 on equal cells): T = L U with unit lower
+// multipliers l_k = 1 / u_{k-1} (l_0 = 0) and pivots u_0 = 2, u_k = d_k - l_k.
+// Returns [l_0..l_N | 1/u_0..1/u_N].
+std::vector<double> mass_lu(int N) {
   const int n = N + 1;
-  std::vector<double> inv((size_t)n * n, 0.0), cp(n), dp(n);
-  auto diag = [&](int i) { return (i == 0 || i == N) ? 2.0 : 4.0; };
-  for (int k = 0; k < n; ++k) {
-    for (int i = 0; i < n; ++i) {  // forward sweep on e_k
-      const double a = i > 0 ? 1.0 : 0.0;
-      const double den = diag(i) - a * (i > 0 ? cp[i - 1] : 0.0);
-      cp[i] = (i < N ? 1.0 : 0.0) / den;
-      dp[i] = ((i == k ? 1.0 : 0.0) - a * (i > 0 ? dp[i - 1] : 0.0)) / den;
-    }
-    double x = dp[N];
-    inv[(size_t)N * n + k] = x;
-    for (int i = N - 1; i >= 0; --i) {
-      x = dp[i] - cp[i] * x;
-      inv[(size_t)i * n + k] = x;
-    }
+  std::vector<double> lu(2 * (size_t)n, 0.0);
+  double u = 2.0;
+  lu[n] = 1.0 / u;
+  for (int k = 1; k < n; ++k) {
+    const double l = 1.0 / u;
+    u = (k == N ? 2.0 : 4.0) - l;
+    lu[k] = l;
+    lu[n + k] = 1.0 / u;
   }
-  for (int i = 0; i < n; ++i)  // exact symmetry (the sweeps differ in the last bits)
-    for (int j = i + 1; j < n; ++j) {
-      const double s = 0.5 * (inv[(size_t)i * n + j] + inv[(size_t)j * n + i]);
-      inv[(size_t)i * n + j] = inv[(size_t)j * n + i] = s;
-    }
-  return inv;
+  return lu;
 }
 
 }  // namespace
@@ -2446,8 +2544,11 @@ NX_API int nx_destroy(nx_network_t* h) {
   if (h->group) return fail(NX_ERR_STATE, "destroy the group (nx_group_destroy) first");
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->chunk_exec) (void)hipGraphExecDestroy(h->chunk_exec);
-  if (h->chunk_graph) (void)hipGraphDestroy(h->chunk_graph);
+  {
+    nx_network* hs[1] = {h};
+    (void)drop_graph(graph_slot(Team{hs, 1, nullptr}));
+  }
+  if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val, h->dq,
                   h->z, h->vv,
@@ -2464,6 +2565,9 @@ NX_API int nx_destroy(nx_network_t* h) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : h->ev_pool)
     if (e) (void)hipEventDestroy(e);
+  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
+  if (h->side) (void)hipStreamDestroy(h->side);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return NX_OK;
@@ -2531,6 +2635,108 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
 
 namespace {
 
+// ---- single rank with the preconditioner: the whole solve is one graph launch in the
+// common case. Head graph = start application z = P^{-1} b (condensed straight from the
+// rhs) with k_pc_prep beside its down sweep, then k_mr_a(1) (which initialises the state
+// from beta_1^2), then (preconditioner k, k_mr_a(k+1)) for k = 1..L-1. It ends with
+// k_mr_a(L), L even, so S[0] holds the latest state; the exact preconditioner converges
+// in 3 iterations and k_mr_a(4) applies the last update. Continuation chunks (rarely
+// needed) are (preconditioner k, k_mr_a(k+1)) for L consecutive k.
+void launch_a_lean(nx_network* h, int64_t k, bool init, double rtol, int maxit) {
+  MrVecs mv{h->vb[(k - 1) & 1], h->vb[k & 1], h->wb[k & 1], h->wb[(k - 1) & 1], h->x, h->z, h->vv};
+  const MrInit ini{init ? 1 : 0, nB_of(h), maxit, rtol, h->partB};
+  hipLaunchKernelGGL((k_mr_a<false, true>), dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv,
+                     h->st + ((k + 1) & 1), h->st + (k & 1), h->partB, nB_of(h), h->red, h->partA,
+                     h->chunksA, ini);
+}
+
+int launch_head_lean(nx_network* h, int L, double rtol, int maxit) {
+  nx_network* hs[1] = {h};
+  const Team t{hs, 1, nullptr};
+  // start: mode 1 only reads y, so it condenses the rhs itself
+  launch_pc<false>(h, h->rhs, h->vb[1], h->st, h->st + 1, 1, 0);
+  HIPCALL(hipEventRecord(h->fork_ev, h->stream));
+  HIPCALL(hipStreamWaitEvent(h->side, h->fork_ev, 0));
+  const bool fac = h->pa.dc_kappa != nullptr;
+  const int ncols = h->pa.dense ? h->pa.n_top : 0;
+  const int grid = std::max(ncols, std::min(2048, std::max(1, grid_of(h->n_own, 512))));
+  hipLaunchKernelGGL(k_pc_prep, dim3(grid), dim3(64), 0, h->side, h->pa, fac ? (int)h->pc_ndc : 0,
+                     fac ? (int)h->pc_slots : 0, ncols, h->rhs, h->vb[1], h->n_own);
+  HIPCALL(hipEventRecord(h->join_ev, h->side));
+  launch_pc<false>(h, h->rhs, h->vb[1], h->st, h->st + 1, 1, 1);
+  HIPCALL(hipStreamWaitEvent(h->stream, h->join_ev, 0));
+  launch_a_lean(h, 1, true, rtol, maxit);
+  for (int k = 1; k < L; ++k) {
+    CHECK(team_pc(t, k, 0));
+    launch_a_lean(h, k + 1, false, rtol, maxit);
+  }
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+int capture(nx_network* h, hipGraph_t* graph, hipGraphExec_t* exec,
+            const std::function<int()>& body) {
+  HIPCALL(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  const int rc = body();
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(h->stream, &g);
+  if (rc != NX_OK) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return fail(NX_ERR_HIP, std::string("capture: ") + hipGetErrorString(e));
+  *graph = g;
+  HIPCALL(hipGraphInstantiate(exec, g, nullptr, nullptr, 0));
+  return NX_OK;
+}
+
+int solve_lean(nx_network* h, double rtol, int32_t maxit, int L, int32_t* iters, double* relres,
+               int32_t* converged) {
+  if (!h->side) {
+    HIPCALL(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIPCALL(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+    HIPCALL(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+  }
+  // the iterations use the factored coefficients (k_pc_prep computes them)
+  h->pa.factored = h->pa.dc_kappa ? 1 : 0;
+  h->pa.mdense = 0;
+  if (!h->head_exec || h->head_len != L || h->head_rtol != rtol || h->head_maxit != maxit) {
+    CHECK(drop_one(&h->head_exec, &h->head_graph, &h->head_len));
+    CHECK(capture(h, &h->head_graph, &h->head_exec,
+                  [&] { return launch_head_lean(h, L, rtol, maxit); }));
+    h->head_len = L;
+    h->head_rtol = rtol;
+    h->head_maxit = maxit;
+  }
+  h->last_graph = true;
+  HIPCALL(hipGraphLaunch(h->head_exec, h->stream));
+  for (;;) {
+    HIPCALL(hipMemcpyAsync(h->h_st, h->st, 2 * sizeof(MrState), hipMemcpyDeviceToHost, h->stream));
+    HIPCALL(hipStreamSynchronize(h->stream));
+    if (h->h_st[0].done) break;
+    if (!h->lchunk_exec || h->lchunk_len != L) {
+      CHECK(drop_one(&h->lchunk_exec, &h->lchunk_graph, &h->lchunk_len));
+      nx_network* hs[1] = {h};
+      const Team t{hs, 1, nullptr};
+      CHECK(capture(h, &h->lchunk_graph, &h->lchunk_exec, [&] {
+        for (int k = L; k < 2 * L; ++k) {
+          CHECK(team_pc(t, k, 0));
+          launch_a_lean(h, k + 1, false, rtol, maxit);
+        }
+        HIPCALL(hipGetLastError());
+        return NX_OK;
+      }));
+      h->lchunk_len = L;
+    }
+    HIPCALL(hipGraphLaunch(h->lchunk_exec, h->stream));
+  }
+  const MrState& s = h->h_st[0];
+  if (iters) *iters = s.it;
+  if (relres) *relres = s.relres;
+  if (converged) *converged = s.converged;
+  return NX_OK;
+}
+
 // MINRES of every rank of the team (nx_solve / nx_group_solve).
 int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, int32_t* iters,
                double* relres, int32_t* converged) {
@@ -2544,6 +2750,12 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   if (check_every & 1) ++check_every;
   CHECK(set_device(t.hs[0]));
   const bool multi = team_multi(t);
+  static const bool lean_env = [] {
+    const char* e = std::getenv("NXHIP_LEAN");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (!multi && t.hs[0]->pc && !t.hs[0]->prof && lean_env)
+    return solve_lean(t.hs[0], rtol, maxit, check_every, iters, relres, converged);
   hipStream_t s = t.hs[0]->stream;
   // r1 = r2 = b, w1 = w2 = x = 0
   for (int r = 0; r < t.P; ++r) {
@@ -3010,13 +3222,13 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.slot_invD = scratch(n_slots);
   if (const char* e = std::getenv("NXHIP_PC_FACTOR"))
     if (std::atoi(e) == 0) pa.dc_kappa = nullptr;  // keep the per-iteration eliminations
-  {  // consistent-mass flux block: T^{-1}, T = tridiag(1, 4, 1) with 2 at both ends
-    const std::vector<double> ti = mass_tinv(N);
+  {  // consistent-mass flux block: pivots of T = tridiag(1, 4, 1), 2 at both ends
+    const std::vector<double> ti = mass_lu(N);
     double* d = scratch((int64_t)ti.size());
     if (d == nullptr || hipMemcpy(d, ti.data(), sizeof(double) * ti.size(), hipMemcpyHostToDevice) !=
                             hipSuccess)
       return fail(NX_ERR_HIP, "preconditioner upload failed");
-    pa.Tinv = d;
+    pa.Tlu = d;
     pa.exact = 1;
     if (const char* e = std::getenv("NXHIP_PC_EXACT"))
       if (std::atoi(e) == 0) pa.exact = 0;  // lumped D: P = blockdiag(D, G^T D^{-1} G)
