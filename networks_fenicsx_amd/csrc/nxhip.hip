@@ -215,6 +215,12 @@ struct AsmArgs {
   double* rhs;
   double* dq;  // E*(N+1) lumped flux mass (preconditioner), or nullptr
   int lhs, do_rhs;
+  // multiplier rows (k_assemble_lm's work, done by the blocks after the edge blocks)
+  int edge_blocks;
+  int64_t nnz_lm, B;
+  const double* lm_val;
+  double* val_lm;
+  double* rhs_lm;
 };
 
 __device__ __forceinline__ void vertex(const double* x0, const double* x1, int k, int N,
@@ -238,6 +244,13 @@ __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
 #pragma clang fp contract(off)
   __shared__ double s_md[kBlock / 64][65];
   __shared__ double s_mo[kBlock / 64][65];
+  if ((int)blockIdx.x >= a.edge_blocks) {  // multiplier rows: +-1 values, zero rhs
+    // (assembly.py:271-277; L[lm] = 0)
+    const int64_t i = (int64_t)(blockIdx.x - a.edge_blocks) * kBlock + threadIdx.x;
+    if (a.lhs && i < a.nnz_lm) a.val_lm[i] = a.lm_val[i];
+    if (a.do_rhs && i < a.B) a.rhs_lm[i] = 0.0;
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * (kBlock / 64) + w;
@@ -322,14 +335,6 @@ __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
   }
 }
 
-// Multiplier rows: constant +-1 values and zero rhs (assembly.py:271-277; L[lm] = 0).
-__global__ void k_assemble_lm(int64_t nnz_lm, const double* __restrict__ lm_val,
-                              double* __restrict__ val_lm, int64_t B, double* __restrict__ rhs_lm,
-                              int lhs, int do_rhs) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (lhs && i < nnz_lm) val_lm[i] = lm_val[i];
-  if (do_rhs && i < B) rhs_lm[i] = 0.0;
-}
 
 // ------------------------------------------------------------------------------------
 // Reductions: deterministic (fixed grid, fixed order), no atomics.
@@ -538,7 +543,8 @@ __device__ __forceinline__ void block_sum_store_n(double v, double* out) {
 }
 
 struct MrVecs {
-  double* r1;        // in: r_{k-1} (b at k = 1); out: y
+  double* r1;        // out: y
+  const double* r1in;  // in: r_{k-1} (usually r1; the rhs at k = 2 of the head graph)
   const double* r2;  // r_k; without preconditioner r_k = beta_k v_k and it is gathered
   double* w1;        // w_{k-3} in, w_{k-1} out (in place)
   const double* w2;  // w_{k-2}
@@ -609,13 +615,14 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
     const double Ay = spmv ? spmv_row_sum(A, g, r0, nr) : 0.0;
     if ((int)threadIdx.x < nr) {
       const int64_t r = r0 + threadIdx.x;
-      const double r1v = upd ? v.r1[r] : 0.0;  // c1 = 0 in iteration 1
+      // c1 = 0 in iteration 1; after the last rotation only the solution update remains
+      const double r1v = (upd && (spmv || !PC)) ? v.r1in[r] : 0.0;
       if (upd) {  // w = (v - oldeps w1 - delta w2) / gamma ; x += phi w
         const double vk = PC ? v.v[r] : r1v / oldb;
         const double w1v = it0 >= 2 ? v.w1[r] : 0.0;  // w_{k-3}, w_{k-2}: zero at first
         const double w2v = it0 >= 1 ? v.w2[r] : 0.0;
         const double wn = (vk - rot.oldeps * w1v - rot.delta * w2v) * rot.denom;
-        v.w1[r] = wn;
+        if (spmv) v.w1[r] = wn;  // no later rotation reads it once the solve stopped
         v.x[r] = (it0 >= 1 ? v.x[r] : 0.0) + rot.phi * wn;
       }
       if (spmv) {
@@ -787,6 +794,7 @@ struct PcArgs {
   // MINRES then converges in 3 iterations (3 distinct eigenvalues of P^{-1} A).
   int exact;
   const double* Tlu;
+  int n_dc_all, n_slots_all;  // hanging-chain entries / junction slots (k_pc_factor sizes)
 };
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
@@ -1510,6 +1518,10 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   NX_PHASE_END(32);
 }
 
+template <int BS>
+__device__ void pc_prep_in_block(const PcArgs& pa, double* sJ, double* sZ, int* sPar,
+                                 double* sTp, double* sDt);
+
 template <bool MULTI, int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* __restrict__ y,
                                                             const double* __restrict__ r2,
@@ -1521,6 +1533,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sTa[kCapT];  // dense top: a_s of every top slot
   __shared__ int sNs[kMaxNeed];
   __shared__ double sNz[kMaxNeed];
+  __shared__ double sGz[kCapT], sGt[kCapT], sGd[kCapT];  // start only: G columns (prep)
+  __shared__ int sGp[kCapT];
   if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
@@ -1689,6 +1703,12 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   NX_PHASE(51);
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
   NX_PHASE_END(48);
+  // single rank, start application: D is final -> factored coefficients and G here, so the
+  // iterations need no separate k_pc_factor / k_pc_gbuild launches (sTa is free in mode 1)
+  if (!MULTI && mode == 1) {
+    __syncthreads();
+    pc_prep_in_block<kPcThreads>(pa, sTa, sGz, sGp, sGt, sGd);
+  }
 }
 
 // Factored coefficients from this solve's D (after the start application).
@@ -1771,10 +1791,9 @@ __device__ void pc_gbuild_column(const PcArgs& pa, int s);
 
 __global__ __launch_bounds__(64) void k_pc_gbuild(PcArgs pa) { pc_gbuild_column(pa, blockIdx.x); }
 
-// Single-rank head graph, once per solve and concurrent with the start application's down
-// sweep (they touch disjoint data): the factored coefficients (k_pc_factor), G's columns
-// (k_pc_gbuild, n_gcols = n_top or 0) and r2 = b for iteration 1 (the start condensed b
-// straight from the rhs, so this replaces the two vector copies of the general path).
+// Single-rank head graph with the global-memory preconditioner kernels, once per solve:
+// the factored coefficients (k_pc_factor), G's columns (k_pc_gbuild, n_gcols = n_top or
+// 0) and optionally a copy r2 = b (n > 0). (The LDS path does this in k_pc_down_lds.)
 __global__ __launch_bounds__(64) void k_pc_prep(PcArgs pa, int n_dc, int n_slots, int n_gcols,
                                                 const double* __restrict__ b,
                                                 double* __restrict__ r2, int64_t n) {
@@ -1821,6 +1840,61 @@ __device__ void pc_gbuild_column(const PcArgs& pa, int s) {
     __syncthreads();
   }
   for (int t = threadIdx.x; t < nt; t += 64) pa.G[(int64_t)t * nt + s] = sZ[t];
+}
+
+// Single rank, start application (k_pc_down_lds, mode 1): the factored coefficients and the
+// columns s0, s0 + step, ... of G (same arithmetic as k_pc_factor / pc_gbuild_column), with
+// the top part's parents, chain resistances and D staged in LDS once. D is final here: the
+// start's up and top kernels wrote it.
+template <int BS>
+__device__ void pc_prep_in_block(const PcArgs& pa, double* sJ, double* sZ, int* sPar,
+                                 double* sTp, double* sDt) {
+  if (pa.dc_kappa) {
+    const int64_t stride = (int64_t)gridDim.x * BS;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < pa.n_dc_all || i < pa.n_slots_all;
+         i += stride) {
+      if (i < pa.n_dc_all) {
+        const int lo = pa.dc_lo[i];
+        pa.dc_kappa[i] = lo >= 0 ? 1.0 / pa.chain_T[pa.slot_dc[i]] / pa.slot_D[lo] : 0.0;
+      }
+      if (i < pa.n_slots_all) pa.slot_invD[i] = 1.0 / pa.slot_D[i];
+    }
+  }
+  if (!pa.dense || (int)blockIdx.x >= pa.n_top) return;  // block-uniform
+  const int nt = pa.n_top, ts0 = pa.top_lvl_off[0];
+  for (int u = threadIdx.x; u < nt; u += BS) {
+    const int p = pa.slot_parent[ts0 + u];
+    sPar[u] = p >= ts0 ? p - ts0 : -1;
+    const int pc = pa.slot_pchain[ts0 + u];
+    sTp[u] = pc >= 0 ? pa.chain_T[pc] : 1.0;
+    sDt[u] = pa.slot_D[ts0 + u];
+  }
+  __syncthreads();
+  for (int s = blockIdx.x; s < nt; s += gridDim.x) {
+    for (int i = threadIdx.x; i < nt; i += BS) sJ[i] = 0.0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double J = 1.0;
+      sJ[s] = 1.0;
+      for (int t = s, p = sPar[s]; p >= 0; t = p, p = sPar[t]) {
+        J = J / sTp[t] / sDt[t];
+        sJ[p] = J;
+      }
+    }
+    __syncthreads();
+    for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
+      const int a = pa.top_lvl_off[lv] - ts0, b = pa.top_lvl_off[lv + 1] - ts0;
+      for (int u = a + threadIdx.x; u < b; u += BS) {
+        const int p = sPar[u];
+        double num = sJ[u];
+        if (p >= 0) num += sZ[p] / sTp[u];
+        sZ[u] = num / sDt[u];
+      }
+      __syncthreads();
+    }
+    for (int t = threadIdx.x; t < nt; t += BS) pa.G[(int64_t)t * nt + s] = sZ[t];
+    __syncthreads();
+  }
 }
 
 // Second half of the top part with several ranks: solve the coarse forest from the
@@ -2014,7 +2088,7 @@ struct nx_network {
   hipGraph_t chunk_graph = nullptr;
   int chunk_len = 0;
   // single rank with the preconditioner (solve_lean): the head graph (start application,
-  // k_pc_prep on the side stream, iterations 1..L) and its continuation chunks
+  // iterations 1..L) and its continuation chunks
   hipGraphExec_t head_exec = nullptr;
   hipGraph_t head_graph = nullptr;
   int head_len = 0;
@@ -2023,8 +2097,6 @@ struct nx_network {
   hipGraphExec_t lchunk_exec = nullptr;
   hipGraph_t lchunk_graph = nullptr;
   int lchunk_len = 0;
-  hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // profiling
   bool prof = false;
   double spmv_ms = 0.0, asm_ms = 0.0;
@@ -2291,7 +2363,7 @@ int launch_iteration(const Team& t, int64_t k) {
     double* w2 = h->wb[(k - 1) & 1];
     MrState* sin = h->st + ((k + 1) & 1);
     MrState* sout = h->st + (k & 1);
-    MrVecs mv{r1, r2, w1, w2, h->x, h->z, h->vv};
+    MrVecs mv{r1, r1, r2, w1, w2, h->x, h->z, h->vv};
     const int nB = nB_of(h);
     // profiling (single handle): events bound to the kernel's own dispatch packet
     // (hipExtLaunchKernel), so the interval is the kernel's execution like rocprofv3's
@@ -2548,7 +2620,6 @@ NX_API int nx_destroy(nx_network_t* h) {
     nx_network* hs[1] = {h};
     (void)drop_graph(graph_slot(Team{hs, 1, nullptr}));
   }
-  if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val, h->dq,
                   h->z, h->vv,
@@ -2565,9 +2636,6 @@ NX_API int nx_destroy(nx_network_t* h) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : h->ev_pool)
     if (e) (void)hipEventDestroy(e);
-  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
-  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
-  if (h->side) (void)hipStreamDestroy(h->side);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return NX_OK;
@@ -2610,16 +2678,17 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   if (!h->have_coeffs) return fail(NX_ERR_STATE, "nx_set_coefficients must be called first");
   CHECK(set_device(h));
   if (!lhs && !rhs) return NX_OK;
-  if (h->E > 0) {
+  // one launch: edge blocks (4 edges each) then the multiplier-row blocks
+  const int64_t nlm = std::max(h->nnz_lm, h->B);
+  const int eb = grid_of(h->E, kBlock / 64);
+  const int lb = grid_of(nlm, kBlock);
+  if (eb + lb > 0) {
     AsmArgs a{EdgeArgs{h->edge_x, h->edge_lm, h->edge_seg, h->E, h->N},
-              h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs ? h->dq : nullptr, lhs, rhs};
-    hipExtLaunchKernelGGL(k_assemble, dim3(grid_of(h->E, kBlock / 64)), dim3(kBlock), 0, h->stream,
+              h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs ? h->dq : nullptr, lhs, rhs,
+              eb, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges, h->rhs + h->n_edge_dofs};
+    hipExtLaunchKernelGGL(k_assemble, dim3(eb + lb), dim3(kBlock), 0, h->stream,
                           h->prof ? h->ev[0] : nullptr, h->prof ? h->ev[1] : nullptr, 0, a);
   }
-  const int64_t nlm = std::max(h->nnz_lm, h->B);
-  if (nlm > 0)
-    hipLaunchKernelGGL(k_assemble_lm, dim3(grid_of(nlm, 256)), dim3(256), 0, h->stream, h->nnz_lm,
-                       h->lm_val, h->val + h->nnz_edges, h->B, h->rhs + h->n_edge_dofs, lhs, rhs);
   HIPCALL(hipGetLastError());
   if (h->prof && h->E > 0) {
     HIPCALL(hipEventSynchronize(h->ev[1]));
@@ -2637,13 +2706,15 @@ namespace {
 
 // ---- single rank with the preconditioner: the whole solve is one graph launch in the
 // common case. Head graph = start application z = P^{-1} b (condensed straight from the
-// rhs) with k_pc_prep beside its down sweep, then k_mr_a(1) (which initialises the state
-// from beta_1^2), then (preconditioner k, k_mr_a(k+1)) for k = 1..L-1. It ends with
+// rhs; its down sweep also builds the factored coefficients and G), then k_mr_a(1) (which
+// initialises the state from beta_1^2), then (preconditioner k, k_mr_a(k+1)) for k = 1..L-1. It ends with
 // k_mr_a(L), L even, so S[0] holds the latest state; the exact preconditioner converges
 // in 3 iterations and k_mr_a(4) applies the last update. Continuation chunks (rarely
 // needed) are (preconditioner k, k_mr_a(k+1)) for L consecutive k.
-void launch_a_lean(nx_network* h, int64_t k, bool init, double rtol, int maxit) {
-  MrVecs mv{h->vb[(k - 1) & 1], h->vb[k & 1], h->wb[k & 1], h->wb[(k - 1) & 1], h->x, h->z, h->vv};
+void launch_a_lean(nx_network* h, int64_t k, bool init, double rtol, int maxit,
+                   const double* r1in = nullptr) {
+  double* r1 = h->vb[(k - 1) & 1];
+  MrVecs mv{r1, r1in ? r1in : r1, h->vb[k & 1], h->wb[k & 1], h->wb[(k - 1) & 1], h->x, h->z, h->vv};
   const MrInit ini{init ? 1 : 0, nB_of(h), maxit, rtol, h->partB};
   hipLaunchKernelGGL((k_mr_a<false, true>), dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv,
                      h->st + ((k + 1) & 1), h->st + (k & 1), h->partB, nB_of(h), h->red, h->partA,
@@ -2651,24 +2722,29 @@ void launch_a_lean(nx_network* h, int64_t k, bool init, double rtol, int maxit) 
 }
 
 int launch_head_lean(nx_network* h, int L, double rtol, int maxit) {
-  nx_network* hs[1] = {h};
-  const Team t{hs, 1, nullptr};
-  // start: mode 1 only reads y, so it condenses the rhs itself
-  launch_pc<false>(h, h->rhs, h->vb[1], h->st, h->st + 1, 1, 0);
-  HIPCALL(hipEventRecord(h->fork_ev, h->stream));
-  HIPCALL(hipStreamWaitEvent(h->side, h->fork_ev, 0));
-  const bool fac = h->pa.dc_kappa != nullptr;
-  const int ncols = h->pa.dense ? h->pa.n_top : 0;
-  const int grid = std::max(ncols, std::min(2048, std::max(1, grid_of(h->n_own, 512))));
-  hipLaunchKernelGGL(k_pc_prep, dim3(grid), dim3(64), 0, h->side, h->pa, fac ? (int)h->pc_ndc : 0,
-                     fac ? (int)h->pc_slots : 0, ncols, h->rhs, h->vb[1], h->n_own);
-  HIPCALL(hipEventRecord(h->join_ev, h->side));
-  launch_pc<false>(h, h->rhs, h->vb[1], h->st, h->st + 1, 1, 1);
-  HIPCALL(hipStreamWaitEvent(h->stream, h->join_ev, 0));
+  // start: mode 1 only reads y, so it condenses the rhs itself; with the LDS kernels its
+  // down sweep also computes the factored coefficients and G (k_pc_down_lds, mode 1)
+  launch_pc<false>(h, h->rhs, h->rhs, h->st, h->st + 1, 1, 0);
+  launch_pc<false>(h, h->rhs, h->rhs, h->st, h->st + 1, 1, 1);
+  if (!h->pc_lds) {
+    const bool fac = h->pa.dc_kappa != nullptr;
+    const int ncols = h->pa.dense ? h->pa.n_top : 0;
+    const int nmax = (int)std::max<int64_t>(h->pc_ndc, h->pc_slots);
+    const int grid = std::max(ncols, std::max(1, grid_of(nmax, 64)));
+    hipLaunchKernelGGL(k_pc_prep, dim3(grid), dim3(64), 0, h->stream, h->pa, fac ? (int)h->pc_ndc : 0,
+                       fac ? (int)h->pc_slots : 0, ncols, nullptr, nullptr, (int64_t)0);
+  }
   launch_a_lean(h, 1, true, rtol, maxit);
+  // iteration 1 reads r_1 = b straight from the rhs (no copy): as r2 in the preconditioner
+  // of k = 1 and as r_{k-1} in k_mr_a(2)
   for (int k = 1; k < L; ++k) {
-    CHECK(team_pc(t, k, 0));
-    launch_a_lean(h, k + 1, false, rtol, maxit);
+    double* y = h->vb[(k - 1) & 1];
+    const double* r2 = k == 1 ? h->rhs : h->vb[k & 1];
+    MrState* st = h->st + (k & 1);
+    MrState* other = h->st + ((k + 1) & 1);
+    launch_pc<false>(h, y, r2, st, other, 0, 0);
+    launch_pc<false>(h, y, r2, st, other, 0, 1);
+    launch_a_lean(h, k + 1, false, rtol, maxit, k == 1 ? h->rhs : nullptr);
   }
   HIPCALL(hipGetLastError());
   return NX_OK;
@@ -2692,11 +2768,6 @@ int capture(nx_network* h, hipGraph_t* graph, hipGraphExec_t* exec,
 
 int solve_lean(nx_network* h, double rtol, int32_t maxit, int L, int32_t* iters, double* relres,
                int32_t* converged) {
-  if (!h->side) {
-    HIPCALL(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-    HIPCALL(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-    HIPCALL(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
-  }
   // the iterations use the factored coefficients (k_pc_prep computes them)
   h->pa.factored = h->pa.dc_kappa ? 1 : 0;
   h->pa.mdense = 0;
@@ -2773,14 +2844,15 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
     CHECK(team_pc(t, 0, 1));
     for (int r = 0; r < t.P; ++r) {  // coefficients of this assembly's D (fixed per solve)
       nx_network* h = t.hs[r];
-      if (h->pa.dc_kappa) {
+      const bool fused = !multi && h->pc_lds;  // k_pc_down_lds (start) did factor + G
+      if (h->pa.dc_kappa && !fused) {
         const int nmax = (int)std::max<int64_t>(h->pc_ndc, h->pc_slots);
         if (nmax > 0)
           hipLaunchKernelGGL(k_pc_factor, dim3(grid_of(nmax, 256)), dim3(256), 0, h->stream,
                              h->pa, (int)h->pc_ndc, (int)h->pc_slots);
       }
       const bool md = multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin;
-      if (h->pa.dense && (!multi || md))
+      if (h->pa.dense && (md || (!multi && !fused)))
         hipLaunchKernelGGL(k_pc_gbuild, dim3(h->pa.n_top), dim3(64), 0, h->stream, h->pa);
       if (md) hipLaunchKernelGGL(k_pc_wroot, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa);
     }
@@ -3204,6 +3276,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.top_lvl_off = up(top_lvl_off, n_top_lvl + 1);
   pa.n_top_lvl = n_top_lvl;
   pa.n_jobs = n_jobs;
+  pa.n_dc_all = (int)slot_dc_off[n_slots];
+  pa.n_slots_all = (int)n_slots;
   pa.dq = h->dq;
   pa.chain_T = scratch(n_chains);
   pa.chain_It = scratch(n_chains);
