@@ -203,9 +203,10 @@ __global__ __launch_bounds__(kBlock) void k_pattern(EdgeArgs ea, int* __restrict
 // ------------------------------------------------------------------------------------
 // Assembly: one wave per edge. Cells are processed in chunks of 64 (lane = cell):
 // each lane regenerates its cell's vertices exactly like the reference mesh
-// generator, computes the P1 mass element tensor (R h/3, R h/6) and stages it in
-// LDS; then the wave writes the chunk's CSR values (unit stride) reading the staged
-// tensors. Slot 0 of the staging row carries the previous chunk's last cell.
+// generator and computes the P1 mass element tensor (R h/3, R h/6); then the wave
+// writes the chunk's CSR values (unit stride), fetching neighbouring cells' tensors by
+// cross-lane permutes (no LDS, no barriers). A register carries the previous chunk's
+// last cell.
 struct AsmArgs {
   EdgeArgs ea;
   const double* edge_R;   // E (per-edge R)
@@ -242,8 +243,6 @@ __device__ __forceinline__ void vertex(const double* x0, const double* x1, int k
 
 __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
 #pragma clang fp contract(off)
-  __shared__ double s_md[kBlock / 64][65];
-  __shared__ double s_mo[kBlock / 64][65];
   if ((int)blockIdx.x >= a.edge_blocks) {  // multiplier rows: +-1 values, zero rhs
     // (assembly.py:271-277; L[lm] = 0)
     const int64_t i = (int64_t)(blockIdx.x - a.edge_blocks) * kBlock + threadIdx.x;
@@ -252,86 +251,85 @@ __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
     return;
   }
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * (kBlock / 64) + w;
-  const bool active = e < a.ea.E;  // all waves run the chunk loop (block barriers)
+  const int64_t e = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (e >= a.ea.E) return;  // wave-uniform; the waves of a block never synchronise
   const int N = a.ea.N;
   const double invN = 1.0 / (double)N;
-  double x0[3] = {0, 0, 0}, x1[3] = {0, 0, 0};
-  double R = 0.0, bc0 = 0.0, bc1 = 0.0;
-  int s = 0, seg = 0, seglen = 0, lm0 = -1, lm1 = -1;
-  int64_t base = 0;
-  if (active) {
+  double x0[3], x1[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      x0[c] = a.ea.edge_x[6 * e + c];
-      x1[c] = a.ea.edge_x[6 * e + 3 + c];
-    }
-    R = a.edge_R[e];
-    lm0 = a.ea.edge_lm[2 * e];
-    lm1 = a.ea.edge_lm[2 * e + 1];
-    s = lm0 >= 0;
-    seg = a.ea.edge_seg[e];
-    seglen = a.ea.edge_seg[e + 1] - seg;
-    base = e * (2 * N + 1);
-    bc0 = a.edge_bc[2 * e];
-    bc1 = a.edge_bc[2 * e + 1];
+  for (int c = 0; c < 3; ++c) {
+    x0[c] = a.ea.edge_x[6 * e + c];
+    x1[c] = a.ea.edge_x[6 * e + 3 + c];
   }
-  (void)lm1;
+  const double R = a.edge_R[e];
+  const int s = a.ea.edge_lm[2 * e] >= 0;
+  const int seg = a.ea.edge_seg[e];
+  const int seglen = a.ea.edge_seg[e + 1] - seg;
+  const int64_t base = e * (2 * N + 1);
+  const double bc0 = a.edge_bc[2 * e], bc1 = a.edge_bc[2 * e + 1];
+  // the previous chunk's last cell (slot 0 of the chunk)
+  double md_prev = 0.0, mo_prev = 0.0;
   for (int c0 = 0; c0 < N; c0 += 64) {
     const int nc = min(64, N - c0);
-    if (active && lane < nc) {
+    double md = 0.0, mo = 0.0;  // this lane's cell c0 + lane: R h/3, R h/6
+    if (lane < nc) {
       const int k = c0 + lane;
       double pa[3], pb[3];
       vertex(x0, x1, k, N, invN, pa);
       vertex(x0, x1, k + 1, N, invN, pb);
       const double d0 = pb[0] - pa[0], d1 = pb[1] - pa[1], d2 = pb[2] - pa[2];
       const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-      s_md[w][lane + 1] = R * h / 3.0;
-      s_mo[w][lane + 1] = R * h / 6.0;
+      md = R * h / 3.0;
+      mo = R * h / 6.0;
       if (a.do_rhs) {
         a.rhs[base + 2 * k + 1] = -(a.f * h);  // negated pressure row: -(f h)
         a.rhs[base + 2 * k] = (k == 0) ? bc0 : 0.0;
       }
     }
-    if (active && a.do_rhs && lane == 0 && c0 + nc == N) a.rhs[base + 2 * N] = bc1;
-    __syncthreads();
-    if (active && a.lhs) {
+    if (a.do_rhs && lane == 0 && c0 + nc == N) a.rhs[base + 2 * N] = bc1;
+    if (a.lhs) {
+      // the chunk's CSR entries, unit stride; element tensors of neighbouring lanes come
+      // by cross-lane permutes (slot = cell - c0 + 1, slot 0 = previous chunk's last cell)
       const int i0 = q_row_start(c0, s);
       const int i1 = (c0 + nc == N) ? seglen : q_row_start(c0 + nc, s);
-      for (int i = i0 + lane; i < i1; i += 64) {
-        const Entry en = decode_entry(i, N, s);
-        const int slot = en.cell - c0 + 1;  // in [0, 64]
+      for (int ib = i0; ib < i1; ib += 64) {  // uniform trip count across the wave
+        const int i = ib + lane;
+        const Entry en = decode_entry(i < i1 ? i : i0, N, s);
+        const int slot = en.cell - c0 + 1;  // in [0, nc]
+        const double mdA = __shfl(md, max(slot - 1, 0), 64);
+        const double moA = __shfl(mo, max(slot - 1, 0), 64);
+        const double mdB = __shfl(md, min(slot, 63), 64);
+        const double md_s = slot == 0 ? md_prev : mdA, mo_s = slot == 0 ? mo_prev : moA;
         double v;
         switch (en.vk) {
           case V_P1: v = 1.0; break;
           case V_M1: v = -1.0; break;
-          case V_MD: v = s_md[w][slot]; break;
-          case V_MO: v = s_mo[w][slot]; break;
-          default: v = s_md[w][slot] + s_md[w][slot + 1]; break;  // interior diagonal
+          case V_MD: v = md_s; break;
+          case V_MO: v = mo_s; break;
+          default: v = md_s + mdB; break;  // interior diagonal: cells g and g+1
         }
-        a.val[seg + i] = v;
+        if (i < i1) a.val[seg + i] = v;
       }
       // lumped (row-sum) flux mass of q_k, k in the chunk (and q_N in the last chunk):
       // the preconditioner's D block
+      const double mdL = __shfl(md, max(lane - 1, 0), 64), moL = __shfl(mo, max(lane - 1, 0), 64);
+      const double mdLast = __shfl(md, nc - 1, 64), moLast = __shfl(mo, nc - 1, 64);
       if (a.dq != nullptr) {
         const int64_t qb = e * (int64_t)(N + 1);
         if (lane < nc) {
           const int k = c0 + lane;
-          const int sl = lane + 1;  // cell k; cell k-1 is sl-1
-          double d = s_md[w][sl] + s_mo[w][sl];
-          if (k > 0) d = (s_mo[w][sl - 1] + s_md[w][sl - 1]) + d;
+          double d = md + mo;
+          if (k > 0) d = (lane > 0 ? moL + mdL : mo_prev + md_prev) + d;
           a.dq[qb + k] = d;
         }
-        if (lane == 0 && c0 + nc == N) a.dq[qb + N] = s_mo[w][nc] + s_md[w][nc];
+        if (lane == 0 && c0 + nc == N) a.dq[qb + N] = moLast + mdLast;
       }
+      md_prev = mdLast;
+      mo_prev = moLast;
+    } else {
+      md_prev = __shfl(md, nc - 1, 64);
+      mo_prev = __shfl(mo, nc - 1, 64);
     }
-    __syncthreads();
-    if (lane == 0) {
-      s_md[w][0] = s_md[w][nc];
-      s_mo[w][0] = s_mo[w][nc];
-    }
-    __syncthreads();
   }
 }
 
@@ -578,7 +576,22 @@ struct MrInit {  // on = 1: iteration 1 starts the solve from beta_1^2 = sum(par
   int maxit;
   double rtol;
   const double* part;
+  // lean path: the last k_mr_a of a graph publishes the state it ends with to a host-
+  // coherent mapped mirror, stamped with a sequence number (pad) the host waits for --
+  // the host learns the outcome without a stream synchronisation or a copy
+  int mark;
+  int* seq;         // device counter of published states
+  MrState* mirror;
 };
+
+__device__ __forceinline__ void mr_publish(MrState s, const MrInit& ini) {
+  const int q = *ini.seq + 1;
+  *ini.seq = q;
+  s.pad = 0;
+  *ini.mirror = s;
+  __threadfence_system();
+  __hip_atomic_store(&ini.mirror->pad, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // w_{k-3}, w_{k-2} and x are not initialised in memory: the first rotations read them as
 // zero (it0 = completed rotations before this one), so the solve needs no memsets.
@@ -589,7 +602,10 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
                                                  const double* __restrict__ red,
                                                  double* __restrict__ partA, int chunksA,
                                                  MrInit ini) {
-  if (!ini.on && sin->done) return;
+  if (!ini.on && sin->done) {
+    if (ini.mark && blockIdx.x == 0 && threadIdx.x == 0) mr_publish(*sin, ini);
+    return;
+  }
   NX_PHASE_START(0);
   MrState s = ini.on ? mr_initial(block_allsum(ini.part, ini.np), ini.rtol, ini.maxit) : *sin;
   Rot rot{0.0, 0.0, 0.0, 0.0};
@@ -600,6 +616,7 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *sout = s;
     if (ini.on) *const_cast<MrState*>(sin) = s;  // both buffers start identical
+    if (ini.mark) mr_publish(s, ini);
   }
   if (ini.on && s.done) return;  // b = 0
   const double beta = s.beta, oldb = s.oldb;  // beta_k, beta_{k-1}
@@ -2083,6 +2100,10 @@ struct nx_network {
   double* z = nullptr;  // P^{-1} r, n_col
   double* vv = nullptr; // Lanczos vector v, n_own
   MrState* h_st = nullptr;             // pinned host mirror of both
+  MrState* h_last = nullptr;           // host-coherent, mapped: the state published by the
+  MrState* d_last = nullptr;           // last k_mr_a of a lean graph (mr_publish)
+  int* d_seq = nullptr;                // device count of published states
+  int seq = 0;                         // host count of lean graph launches
   // graph chunk
   hipGraphExec_t chunk_exec = nullptr;
   hipGraph_t chunk_graph = nullptr;
@@ -2374,7 +2395,7 @@ int launch_iteration(const Team& t, int64_t k) {
   hipExtLaunchKernelGGL((k_mr_a<M, P>), dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,     \
                         csr_of(h), mv, sin, sout, p2p_beta ? h->gath : h->partB,              \
                         p2p_beta ? h->nranks : nB, h->red, h->partA, h->chunksA,             \
-                        MrInit{0, 0, 0, 0.0, nullptr})
+                        MrInit{0, 0, 0, 0.0, nullptr, 0, nullptr, nullptr})
     if (multi && !p2p_beta) {
       if (pc) NX_LAUNCH_A(true, true); else NX_LAUNCH_A(true, false);
     } else {
@@ -2583,6 +2604,14 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   if ((rc = dalloc(&h->red, 4))) return bail(rc);
   if (hipMalloc((void**)&h->st, 2 * sizeof(MrState)) != hipSuccess)
     return bail(fail(NX_ERR_HIP, "hipMalloc state failed"));
+  if (hipHostMalloc((void**)&h->h_last, sizeof(MrState),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&h->d_last, h->h_last, 0) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "mapped host state allocation failed"));
+  std::memset(h->h_last, 0, sizeof(MrState));
+  if ((rc = dalloc(&h->d_seq, 1))) return bail(rc);
+  if (hipMemsetAsync(h->d_seq, 0, sizeof(int), h->stream) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "memset failed"));
   if (hipHostMalloc((void**)&h->h_st, 2 * sizeof(MrState), hipHostMallocDefault) != hipSuccess)
     return bail(fail(NX_ERR_HIP, "hipHostMalloc failed"));
   for (auto& e : h->ev)
@@ -2626,12 +2655,13 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
                   h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
                   h->partA,  h->partB,   h->red,
-                  h->send_idx, h->send_buf, h->gath};
+                  h->send_idx, h->send_buf, h->gath, h->d_seq};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
     if (p) (void)hipFree(p);
   if (h->h_st) (void)hipHostFree(h->h_st);
+  if (h->h_last) (void)hipHostFree(h->h_last);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : h->ev_pool)
@@ -2712,10 +2742,10 @@ namespace {
 // in 3 iterations and k_mr_a(4) applies the last update. Continuation chunks (rarely
 // needed) are (preconditioner k, k_mr_a(k+1)) for L consecutive k.
 void launch_a_lean(nx_network* h, int64_t k, bool init, double rtol, int maxit,
-                   const double* r1in = nullptr) {
+                   const double* r1in = nullptr, bool mark = false) {
   double* r1 = h->vb[(k - 1) & 1];
   MrVecs mv{r1, r1in ? r1in : r1, h->vb[k & 1], h->wb[k & 1], h->wb[(k - 1) & 1], h->x, h->z, h->vv};
-  const MrInit ini{init ? 1 : 0, nB_of(h), maxit, rtol, h->partB};
+  const MrInit ini{init ? 1 : 0, nB_of(h), maxit, rtol, h->partB, mark ? 1 : 0, h->d_seq, h->d_last};
   hipLaunchKernelGGL((k_mr_a<false, true>), dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv,
                      h->st + ((k + 1) & 1), h->st + (k & 1), h->partB, nB_of(h), h->red, h->partA,
                      h->chunksA, ini);
@@ -2744,10 +2774,29 @@ int launch_head_lean(nx_network* h, int L, double rtol, int maxit) {
     MrState* other = h->st + ((k + 1) & 1);
     launch_pc<false>(h, y, r2, st, other, 0, 0);
     launch_pc<false>(h, y, r2, st, other, 0, 1);
-    launch_a_lean(h, k + 1, false, rtol, maxit, k == 1 ? h->rhs : nullptr);
+    launch_a_lean(h, k + 1, false, rtol, maxit, k == 1 ? h->rhs : nullptr, k + 1 == L);
   }
   HIPCALL(hipGetLastError());
   return NX_OK;
+}
+
+// Wait for the state published by the last k_mr_a of the graph just launched (sequence
+// number h->seq). Spins on host-coherent memory; checks the stream now and then so a
+// failed launch cannot hang the host.
+int wait_published(nx_network* h) {
+  const int want = h->seq;
+  for (uint64_t spin = 1;; ++spin) {
+    if (__atomic_load_n(&h->h_last->pad, __ATOMIC_ACQUIRE) == want) return NX_OK;
+    if ((spin & 1023) == 0) {
+      const hipError_t e = hipStreamQuery(h->stream);
+      if (e == hipSuccess) {  // stream idle: the stamp must be there now
+        if (__atomic_load_n(&h->h_last->pad, __ATOMIC_ACQUIRE) == want) return NX_OK;
+        return fail(NX_ERR_STATE, "solve graph finished without publishing its state");
+      }
+      if (e != hipErrorNotReady) return fail(NX_ERR_HIP, std::string("solve graph: ") +
+                                                             hipGetErrorString(e));
+    }
+  }
 }
 
 int capture(nx_network* h, hipGraph_t* graph, hipGraphExec_t* exec,
@@ -2781,10 +2830,13 @@ int solve_lean(nx_network* h, double rtol, int32_t maxit, int L, int32_t* iters,
   }
   h->last_graph = true;
   HIPCALL(hipGraphLaunch(h->head_exec, h->stream));
+  h->seq += 1;
   for (;;) {
-    HIPCALL(hipMemcpyAsync(h->h_st, h->st, 2 * sizeof(MrState), hipMemcpyDeviceToHost, h->stream));
-    HIPCALL(hipStreamSynchronize(h->stream));
-    if (h->h_st[0].done) break;
+    // the graph's last k_mr_a published the state it ends with (the final one once done);
+    // the solution update may still be running -- later work on the stream is ordered
+    // after it and every host read of device data synchronises the stream
+    CHECK(wait_published(h));
+    if (h->h_last->done) break;
     if (!h->lchunk_exec || h->lchunk_len != L) {
       CHECK(drop_one(&h->lchunk_exec, &h->lchunk_graph, &h->lchunk_len));
       nx_network* hs[1] = {h};
@@ -2792,7 +2844,7 @@ int solve_lean(nx_network* h, double rtol, int32_t maxit, int L, int32_t* iters,
       CHECK(capture(h, &h->lchunk_graph, &h->lchunk_exec, [&] {
         for (int k = L; k < 2 * L; ++k) {
           CHECK(team_pc(t, k, 0));
-          launch_a_lean(h, k + 1, false, rtol, maxit);
+          launch_a_lean(h, k + 1, false, rtol, maxit, nullptr, k + 1 == 2 * L);
         }
         HIPCALL(hipGetLastError());
         return NX_OK;
@@ -2800,8 +2852,9 @@ int solve_lean(nx_network* h, double rtol, int32_t maxit, int L, int32_t* iters,
       h->lchunk_len = L;
     }
     HIPCALL(hipGraphLaunch(h->lchunk_exec, h->stream));
+    h->seq += 1;
   }
-  const MrState& s = h->h_st[0];
+  const MrState s = *h->h_last;
   if (iters) *iters = s.it;
   if (relres) *relres = s.relres;
   if (converged) *converged = s.converged;
