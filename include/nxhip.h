@@ -173,6 +173,17 @@ int nx_set_pc_exact(nx_network_t* h, int32_t enable);
 int nx_get_pc_exact(nx_network_t* h, int32_t* enabled);
 
 /*
+ * Process-wide solve mode. 1 (default): with the preconditioner a solve is ONE HIP graph
+ * launch -- start application, per-solve coefficients and the first iterations (also with
+ * several ranks, RCCL or group, when beta^2 travels point-to-point) -- whose last k_mr_a
+ * publishes the MINRES state to host-coherent memory; nx_solve returns once it is
+ * published (the final solution update may still run: every host read of device data
+ * synchronises the stream). 0: eager prologue, chunked iteration graphs, a stream
+ * synchronisation per chunk (the path profiling always uses). NXHIP_LEAN=0 sets 0.
+ */
+int nx_set_lean(int32_t enable);
+
+/*
  * Coarse step of the preconditioner on a partitioned problem (precond.py derives it): the
  * coarse junctions (interface junctions + the junctions on paths between them inside a
  * rank) form a forest that every rank solves redundantly from one all-reduce of

@@ -67,6 +67,7 @@ _SIGS = {
                                   _pi32, _pi32, _pi32, _pi32]),
     "nx_set_pc_exact": (C.c_int, [_h, _i32]),
     "nx_get_pc_exact": (C.c_int, [_h, _pi32]),
+    "nx_set_lean": (C.c_int, [_i32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
     "nx_group_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
     "nx_group_destroy": (C.c_int, [_h]),
@@ -364,6 +365,11 @@ class Group:
             self.close()
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
+
+
+def set_lean(enable: bool) -> None:
+    """Process-wide: one graph per solve (default) or the general chunked path."""
+    check(lib().nx_set_lean(int(bool(enable))))
 
 
 def comm_unique_id() -> bytes:

@@ -2053,6 +2053,17 @@ __global__ void k_group_sum(GroupPtrs g, int P, int n) {
 // Host side
 // ======================================================================================
 
+struct LeanGraphs {
+  hipGraphExec_t head_exec = nullptr;
+  hipGraph_t head_graph = nullptr;
+  int head_len = 0;
+  double head_rtol = 0.0;
+  int head_maxit = 0;
+  hipGraphExec_t lchunk_exec = nullptr;
+  hipGraph_t lchunk_graph = nullptr;
+  int lchunk_len = 0;
+};
+
 struct nx_network {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -2108,16 +2119,9 @@ struct nx_network {
   hipGraphExec_t chunk_exec = nullptr;
   hipGraph_t chunk_graph = nullptr;
   int chunk_len = 0;
-  // single rank with the preconditioner (solve_lean): the head graph (start application,
-  // iterations 1..L) and its continuation chunks
-  hipGraphExec_t head_exec = nullptr;
-  hipGraph_t head_graph = nullptr;
-  int head_len = 0;
-  double head_rtol = 0.0;
-  int head_maxit = 0;
-  hipGraphExec_t lchunk_exec = nullptr;
-  hipGraph_t lchunk_graph = nullptr;
-  int lchunk_len = 0;
+  // with the preconditioner (solve_lean): the head graph (start application, iterations
+  // 1..L) and its continuation chunks; a group keeps its own
+  LeanGraphs lean;
   // profiling
   bool prof = false;
   double spmv_ms = 0.0, asm_ms = 0.0;
@@ -2151,6 +2155,7 @@ struct nx_group {
   hipGraphExec_t chunk_exec = nullptr;
   hipGraph_t chunk_graph = nullptr;
   int chunk_len = 0;
+  LeanGraphs lean;
 };
 
 namespace {
@@ -2336,12 +2341,12 @@ bool team_lin(const Team& t) {
 
 
 // Whole preconditioner application for every rank of the team, with the coarse exchange.
-int team_pc(const Team& t, int64_t k, int mode) {
+int team_pc(const Team& t, int64_t k, int mode, int start_vb = 0) {
   const bool multi = team_multi(t);
   for (int half = 0; half < 2; ++half) {
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
-      double* y = mode ? h->vb[0] : h->vb[(k - 1) & 1];
+      double* y = mode ? h->vb[start_vb] : h->vb[(k - 1) & 1];
       const double* r2 = mode ? h->vb[1] : h->vb[k & 1];
       MrState* st = mode ? h->st : h->st + (k & 1);
       MrState* other = mode ? h->st + 1 : h->st + ((k + 1) & 1);
@@ -2368,8 +2373,17 @@ int team_reduce_slot(const Team& t, bool from_a, int slot, bool allreduce = true
   return (to_coarse || !allreduce) ? NX_OK : team_allreduce(t, slot, 1);
 }
 
-// One MINRES iteration of every rank on the stream; `k` = 1-based iteration index.
-int launch_iteration(const Team& t, int64_t k) {
+// Lean graphs: k_mr_a of iteration 1 initialises the state; the graph's last k_mr_a
+// publishes its state (MrInit).
+struct LeanOpt {
+  bool init, mark;
+  double rtol;
+  int maxit;
+};
+
+// First part of MINRES iteration k (1-based) of every rank on the stream: the halo (with
+// several ranks also the previous beta^2 partial), then k_mr_a.
+int launch_part_a(const Team& t, int64_t k, const LeanOpt* lo = nullptr) {
   const bool multi = team_multi(t);
   const bool pc = t.hs[0]->pc;
   // beta^2 of the previous iteration travels with the halo (point-to-point gather)
@@ -2391,11 +2405,15 @@ int launch_iteration(const Team& t, int64_t k) {
     const bool prof = h->prof && t.g == nullptr;
     hipEvent_t e0 = prof ? h->ev_pool[2 * h->prof_k] : nullptr;
     hipEvent_t e1 = prof ? h->ev_pool[2 * h->prof_k + 1] : nullptr;
+    const double* bpart = p2p_beta ? h->gath : h->partB;
+    const int nbp = p2p_beta ? h->nranks : nB;
+    MrInit ini{0, 0, 0, 0.0, nullptr, 0, nullptr, nullptr};
+    if (lo)
+      ini = MrInit{lo->init ? 1 : 0, nbp, lo->maxit, lo->rtol, bpart, lo->mark ? 1 : 0,
+                   h->d_seq, h->d_last};
 #define NX_LAUNCH_A(M, P)                                                                        \
   hipExtLaunchKernelGGL((k_mr_a<M, P>), dim3(h->nA), dim3(kBlock), 0, h->stream, e0, e1, 0,     \
-                        csr_of(h), mv, sin, sout, p2p_beta ? h->gath : h->partB,              \
-                        p2p_beta ? h->nranks : nB, h->red, h->partA, h->chunksA,             \
-                        MrInit{0, 0, 0, 0.0, nullptr, 0, nullptr, nullptr})
+                        csr_of(h), mv, sin, sout, bpart, nbp, h->red, h->partA, h->chunksA, ini)
     if (multi && !p2p_beta) {
       if (pc) NX_LAUNCH_A(true, true); else NX_LAUNCH_A(true, false);
     } else {
@@ -2405,6 +2423,16 @@ int launch_iteration(const Team& t, int64_t k) {
     if (prof) h->prof_k += 1;
   }
   if (multi) CHECK(team_reduce_slot(t, true, 0));
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+// Second part of iteration k: the preconditioner (or the Lanczos step without it) and,
+// with several ranks and beta^2 by all-reduce, that reduction.
+int launch_part_pc(const Team& t, int64_t k) {
+  const bool multi = team_multi(t);
+  const bool pc = t.hs[0]->pc;
+  const bool p2p_beta = multi && t.hs[0]->beta_p2p;
   if (pc) {
     CHECK(team_pc(t, k, 0));
   } else {
@@ -2427,17 +2455,23 @@ int launch_iteration(const Team& t, int64_t k) {
   return NX_OK;
 }
 
+// One MINRES iteration of every rank on the stream; `k` = 1-based iteration index.
+int launch_iteration(const Team& t, int64_t k) {
+  CHECK(launch_part_a(t, k));
+  return launch_part_pc(t, k);
+}
+
 struct GraphSlot {
   hipGraphExec_t* exec;
   hipGraph_t* graph;
   int* len;
-  nx_network* lean;  // single handle: its head / continuation graphs go too
+  LeanGraphs* lean;  // the head / continuation graphs of the same handle or group go too
 };
 
 GraphSlot graph_slot(const Team& t) {
-  if (t.g) return GraphSlot{&t.g->chunk_exec, &t.g->chunk_graph, &t.g->chunk_len, nullptr};
+  if (t.g) return GraphSlot{&t.g->chunk_exec, &t.g->chunk_graph, &t.g->chunk_len, &t.g->lean};
   nx_network* h = t.hs[0];
-  return GraphSlot{&h->chunk_exec, &h->chunk_graph, &h->chunk_len, h};
+  return GraphSlot{&h->chunk_exec, &h->chunk_graph, &h->chunk_len, &h->lean};
 }
 
 int drop_one(hipGraphExec_t* exec, hipGraph_t* graph, int* len) {
@@ -2454,6 +2488,18 @@ int drop_graph(GraphSlot gs) {
   if (gs.lean) {
     CHECK(drop_one(&gs.lean->head_exec, &gs.lean->head_graph, &gs.lean->head_len));
     CHECK(drop_one(&gs.lean->lchunk_exec, &gs.lean->lchunk_graph, &gs.lean->lchunk_len));
+  }
+  return NX_OK;
+}
+
+// Captured launches bake in a handle's arguments: after a change, drop the handle's graphs
+// and those of the group it belongs to.
+int drop_handle_graphs(nx_network* h) {
+  nx_network* hs[1] = {h};
+  CHECK(drop_graph(graph_slot(Team{hs, 1, nullptr})));
+  if (h->group) {
+    nx_group* g = h->group;
+    CHECK(drop_graph(GraphSlot{&g->chunk_exec, &g->chunk_graph, &g->chunk_len, &g->lean}));
   }
   return NX_OK;
 }
@@ -2591,6 +2637,9 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   for (int i = 0; i < 2; ++i) {
     if ((rc = dalloc(&h->vb[i], n_col))) return bail(rc);
     if ((rc = dalloc(&h->wb[i], n_own))) return bail(rc);
+    // the ghost slots of r are read (junction slots of ghost junctions) and must stay zero
+    if (n_col > 0 && hipMemsetAsync(h->vb[i], 0, sizeof(double) * n_col, h->stream) != hipSuccess)
+      return bail(fail(NX_ERR_HIP, "memset failed"));
   }
   if ((rc = dalloc(&h->x, n_col))) return bail(rc);
   if ((rc = dalloc(&h->tmp, n_col))) return bail(rc);
@@ -2815,46 +2864,129 @@ int capture(nx_network* h, hipGraph_t* graph, hipGraphExec_t* exec,
   return NX_OK;
 }
 
-int solve_lean(nx_network* h, double rtol, int32_t maxit, int L, int32_t* iters, double* relres,
-               int32_t* converged) {
-  // the iterations use the factored coefficients (k_pc_prep computes them)
-  h->pa.factored = h->pa.dc_kappa ? 1 : 0;
-  h->pa.mdense = 0;
-  if (!h->head_exec || h->head_len != L || h->head_rtol != rtol || h->head_maxit != maxit) {
-    CHECK(drop_one(&h->head_exec, &h->head_graph, &h->head_len));
-    CHECK(capture(h, &h->head_graph, &h->head_exec,
-                  [&] { return launch_head_lean(h, L, rtol, maxit); }));
-    h->head_len = L;
-    h->head_rtol = rtol;
-    h->head_maxit = maxit;
+// ---- several ranks (RCCL, one process per GPU; or an in-process group) with the
+// preconditioner: the same one-graph solve. Head = b -> vb[1] (owned rows; ghost slots of
+// vb are zero from allocation and stay zero), the start application with its coarse
+// all-reduce, the per-solve coefficients, iterations 1..L-1, then the halo and k_mr_a of
+// iteration L (published). beta_1^2 travels with the halo of iteration 1 like every later
+// beta^2 (point-to-point gather), so k_mr_a(1) initialises the state itself.
+int launch_head_multi(const Team& t, int L, double rtol, int maxit) {
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    if (h->n_own > 0)
+      HIPCALL(hipMemcpyAsync(h->vb[1], h->rhs, sizeof(double) * h->n_own, hipMemcpyDeviceToDevice,
+                             h->stream));
   }
-  h->last_graph = true;
-  HIPCALL(hipGraphLaunch(h->head_exec, h->stream));
-  h->seq += 1;
+  CHECK(team_pc(t, 0, 1, 1));
+  for (int r = 0; r < t.P; ++r) {  // coefficients of this assembly's D (fixed per solve)
+    nx_network* h = t.hs[r];
+    if (h->pa.dc_kappa) {
+      const int nmax = (int)std::max<int64_t>(h->pc_ndc, h->pc_slots);
+      if (nmax > 0)
+        hipLaunchKernelGGL(k_pc_factor, dim3(grid_of(nmax, 256)), dim3(256), 0, h->stream, h->pa,
+                           (int)h->pc_ndc, (int)h->pc_slots);
+    }
+    if (h->pa.mdense) {
+      hipLaunchKernelGGL(k_pc_gbuild, dim3(h->pa.n_top), dim3(64), 0, h->stream, h->pa);
+      hipLaunchKernelGGL(k_pc_wroot, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa);
+    }
+  }
+  const LeanOpt first{true, L == 1, rtol, maxit};
+  CHECK(launch_part_a(t, 1, &first));
+  for (int k = 1; k < L; ++k) {
+    CHECK(launch_part_pc(t, k));
+    const LeanOpt next{false, k + 1 == L, rtol, maxit};
+    CHECK(launch_part_a(t, k + 1, &next));
+  }
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+LeanGraphs& lean_of(const Team& t) { return t.g ? t.g->lean : t.hs[0]->lean; }
+
+// 1: one graph per solve where possible (default; NXHIP_LEAN=0 or nx_set_lean(0): the
+// general path with eager prologue and chunked iterations)
+int& lean_flag() {
+  static int f = [] {
+    const char* e = std::getenv("NXHIP_LEAN");
+    return (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
+  }();
+  return f;
+}
+bool lean_mode() { return lean_flag() != 0; }
+
+// The lean solve of a team (single rank, group or RCCL rank). Returns NX_ERR_RCCL if the
+// RCCL capture failed (the caller falls back to eager launches).
+int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters, double* relres,
+               int32_t* converged) {
+  const bool multi = team_multi(t);
+  nx_network* h0 = t.hs[0];
+  for (int r = 0; r < t.P; ++r) {  // the iterations use the factored coefficients
+    nx_network* h = t.hs[r];
+    h->pa.factored = h->pa.dc_kappa ? 1 : 0;
+    h->pa.mdense = (multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin) ? 1 : 0;
+  }
+  LeanGraphs& lg = lean_of(t);
+  auto cap = [&](hipGraph_t* graph, hipGraphExec_t* exec, const std::function<int()>& body) {
+    const int rc = capture(h0, graph, exec, body);
+    if (rc != NX_OK && h0->comm) {  // RCCL refused the capture: eager from now on
+      (void)hipGetLastError();
+      h0->rccl_graph_ok = false;
+      return (int)NX_ERR_RCCL;
+    }
+    return rc;
+  };
+  if (!lg.head_exec || lg.head_len != L || lg.head_rtol != rtol || lg.head_maxit != maxit) {
+    CHECK(drop_one(&lg.head_exec, &lg.head_graph, &lg.head_len));
+    CHECK(cap(&lg.head_graph, &lg.head_exec, [&] {
+      return multi ? launch_head_multi(t, L, rtol, maxit) : launch_head_lean(h0, L, rtol, maxit);
+    }));
+    lg.head_len = L;
+    lg.head_rtol = rtol;
+    lg.head_maxit = maxit;
+  }
+  h0->last_graph = true;
+  HIPCALL(hipGraphLaunch(lg.head_exec, h0->stream));
+  for (int r = 0; r < t.P; ++r) t.hs[r]->seq += 1;
   for (;;) {
     // the graph's last k_mr_a published the state it ends with (the final one once done);
     // the solution update may still be running -- later work on the stream is ordered
     // after it and every host read of device data synchronises the stream
-    CHECK(wait_published(h));
-    if (h->h_last->done) break;
-    if (!h->lchunk_exec || h->lchunk_len != L) {
-      CHECK(drop_one(&h->lchunk_exec, &h->lchunk_graph, &h->lchunk_len));
-      nx_network* hs[1] = {h};
-      const Team t{hs, 1, nullptr};
-      CHECK(capture(h, &h->lchunk_graph, &h->lchunk_exec, [&] {
+    for (int r = 0; r < t.P; ++r) CHECK(wait_published(t.hs[r]));
+    const MrState& s0 = *h0->h_last;
+    for (int r = 1; r < t.P; ++r) {  // the ranks run the same recurrence on the same scalars
+      const MrState& o = *t.hs[r]->h_last;
+      if (o.it != s0.it || o.done != s0.done || o.relres != s0.relres) {
+        char msg[256];
+        std::snprintf(msg, sizeof(msg), "ranks diverged: rank %d it %d done %d relres %.17g vs "
+                      "rank 0 it %d done %d relres %.17g", r, o.it, o.done, o.relres, s0.it,
+                      s0.done, s0.relres);
+        return fail(NX_ERR_STATE, msg);
+      }
+    }
+    if (s0.done) break;
+    if (!lg.lchunk_exec || lg.lchunk_len != L) {
+      CHECK(drop_one(&lg.lchunk_exec, &lg.lchunk_graph, &lg.lchunk_len));
+      CHECK(cap(&lg.lchunk_graph, &lg.lchunk_exec, [&] {
         for (int k = L; k < 2 * L; ++k) {
-          CHECK(team_pc(t, k, 0));
-          launch_a_lean(h, k + 1, false, rtol, maxit, nullptr, k + 1 == 2 * L);
+          if (multi) {
+            CHECK(launch_part_pc(t, k));
+            const LeanOpt next{false, k + 1 == 2 * L, rtol, maxit};
+            CHECK(launch_part_a(t, k + 1, &next));
+          } else {
+            CHECK(team_pc(t, k, 0));
+            launch_a_lean(h0, k + 1, false, rtol, maxit, nullptr, k + 1 == 2 * L);
+          }
         }
         HIPCALL(hipGetLastError());
         return NX_OK;
       }));
-      h->lchunk_len = L;
+      lg.lchunk_len = L;
     }
-    HIPCALL(hipGraphLaunch(h->lchunk_exec, h->stream));
-    h->seq += 1;
+    HIPCALL(hipGraphLaunch(lg.lchunk_exec, h0->stream));
+    for (int r = 0; r < t.P; ++r) t.hs[r]->seq += 1;
   }
-  const MrState s = *h->h_last;
+  const MrState s = *h0->h_last;
   if (iters) *iters = s.it;
   if (relres) *relres = s.relres;
   if (converged) *converged = s.converged;
@@ -2874,12 +3006,16 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   if (check_every & 1) ++check_every;
   CHECK(set_device(t.hs[0]));
   const bool multi = team_multi(t);
-  static const bool lean_env = [] {
-    const char* e = std::getenv("NXHIP_LEAN");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  if (!multi && t.hs[0]->pc && !t.hs[0]->prof && lean_env)
-    return solve_lean(t.hs[0], rtol, maxit, check_every, iters, relres, converged);
+  const bool lean_env = lean_mode();
+  {  // one graph per solve (profiling and the all-reduce beta^2 variant keep the general path)
+    nx_network* h0 = t.hs[0];
+    const bool prof = h0->prof && t.g == nullptr;
+    const bool ok_multi = !multi || (h0->beta_p2p && (!h0->comm || h0->rccl_graph_ok));
+    if (h0->pc && !prof && lean_env && ok_multi) {
+      const int rc = solve_lean(t, rtol, maxit, check_every, iters, relres, converged);
+      if (rc != NX_ERR_RCCL || !h0->comm) return rc;  // RCCL capture refused: eager below
+    }
+  }
   hipStream_t s = t.hs[0]->stream;
   // r1 = r2 = b, w1 = w2 = x = 0
   for (int r = 0; r < t.P; ++r) {
@@ -3241,12 +3377,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   if (!h) return fail(NX_ERR_ARG, "null handle");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
-  {  // captured launches depend on the preconditioner: recapture
-    nx_network* hs[1] = {h};
-    CHECK(drop_graph(graph_slot(Team{hs, 1, nullptr})));
-    if (h->group) CHECK(drop_graph(GraphSlot{&h->group->chunk_exec, &h->group->chunk_graph,
-                                             &h->group->chunk_len}));
-  }
+  CHECK(drop_handle_graphs(h));  // captured launches depend on the preconditioner
   if (!enable) {
     h->pc = false;
     return NX_OK;
@@ -3411,10 +3542,7 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
   if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
-  {
-    nx_network* hs[1] = {h};
-    CHECK(drop_graph(graph_slot(Team{hs, 1, nullptr})));
-  }
+  CHECK(drop_handle_graphs(h));
   h->pa.dense = 0;
   if (!enable) return NX_OK;
   if (n_jobs != h->pc_jobs) return fail(NX_ERR_ARG, "n_jobs differs from the preconditioner's");
@@ -3503,11 +3631,13 @@ NX_API int nx_set_pc_exact(nx_network_t* h, int32_t enable) {
   if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
-  {
-    nx_network* hs[1] = {h};
-    CHECK(drop_graph(graph_slot(Team{hs, 1, nullptr})));
-  }
+  CHECK(drop_handle_graphs(h));
   h->pa.exact = enable ? 1 : 0;
+  return NX_OK;
+}
+
+NX_API int nx_set_lean(int32_t enable) {
+  lean_flag() = enable ? 1 : 0;
   return NX_OK;
 }
 
@@ -3530,6 +3660,7 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
                                 std::to_string(kCapCoarse) + ")");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
+  CHECK(drop_handle_graphs(h));
   const int64_t ns = h->pc_slots;
   if (n_coarse == 0) {
     h->pa.n_coarse = 0;
@@ -3730,7 +3861,7 @@ NX_API int nx_group_destroy(nx_group_t* g) {
   if (!g) return NX_OK;
   (void)hipSetDevice(g->hs[0]->device);
   (void)hipStreamSynchronize(g->stream);
-  (void)drop_graph(GraphSlot{&g->chunk_exec, &g->chunk_graph, &g->chunk_len});
+  (void)drop_graph(GraphSlot{&g->chunk_exec, &g->chunk_graph, &g->chunk_len, &g->lean});
   for (nx_network* h : g->hs) {
     h->stream = h->own_stream;
     h->own_stream = nullptr;

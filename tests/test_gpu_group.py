@@ -119,6 +119,35 @@ def test_group_alternative_kernel_paths(env, monkeypatch):
         grp.close()
 
 
+@pytest.mark.parametrize("case,P", [("depth6_N40", 4), ("arterial5_N40", 3), ("tree6_2d_N70", 5)])
+def test_group_lean_graph_matches_general_path(case, P):
+    """One graph per solve (start, coefficients, iterations, published state) vs the
+    general path (eager prologue, chunked iterations): same iterations and solution."""
+    from networks_fenicsx_amd import _lib
+
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.assemble()
+        out = {}
+        for lean in (True, False):
+            _lib.set_lean(lean)
+            it, relres, conv = grp.solve(1e-12, 50000, 4)
+            assert conv
+            x = np.zeros(Ab.shape[0])
+            for a, xl in zip(grp.assemblers, grp.solutions()):
+                x[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
+            assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+            out[lean] = (it, x)
+        assert out[True][0] == out[False][0]
+        assert np.linalg.norm(out[True][1] - out[False][1]) <= 1e-12 * np.linalg.norm(x_ref)
+    finally:
+        _lib.set_lean(True)
+        grp.close()
+
+
 def test_group_large_tree_iterations_flat():
     """Depth-10 binary tree (N=15, ~61k DoF) on 8 ranks: same iteration count as 1 rank
     (block-Jacobi grounding of the cuts would need ~5x more)."""
