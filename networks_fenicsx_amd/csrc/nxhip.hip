@@ -241,6 +241,109 @@ __device__ __forceinline__ void vertex(const double* x0, const double* x1, int k
   }
 }
 
+// Small N (N < S <= 32): 64 / S edges per wave, one S-lane segment per edge (lane = cell).
+// The wave's edges own one contiguous CSR range, written unit-stride by all 64 lanes;
+// entry -> edge by the (at most 4) segment boundaries. Same arithmetic as k_assemble.
+template <int S>
+__global__ __launch_bounds__(kBlock) void k_assemble_seg(AsmArgs a) {
+#pragma clang fp contract(off)
+  constexpr int EPW = 64 / S;
+  if ((int)blockIdx.x >= a.edge_blocks) {  // multiplier rows: +-1 values, zero rhs
+    const int64_t i = (int64_t)(blockIdx.x - a.edge_blocks) * kBlock + threadIdx.x;
+    if (a.lhs && i < a.nnz_lm) a.val_lm[i] = a.lm_val[i];
+    if (a.do_rhs && i < a.B) a.rhs_lm[i] = 0.0;
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / S, cl = lane % S;
+  const int64_t e0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * EPW;
+  if (e0 >= a.ea.E) return;  // wave-uniform
+  const int64_t E = a.ea.E;
+  const int ne = (int)min<int64_t>(EPW, E - e0);
+  const int64_t e = e0 + min(sub, ne - 1);  // idle segments shadow the last edge
+  const bool mine = sub < ne;
+  const int N = a.ea.N;
+  const double invN = 1.0 / (double)N;
+  double x0[3], x1[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    x0[c] = a.ea.edge_x[6 * e + c];
+    x1[c] = a.ea.edge_x[6 * e + 3 + c];
+  }
+  const double R = a.edge_R[e];
+  const int s = a.ea.edge_lm[2 * e] >= 0;
+  const int seg = a.ea.edge_seg[e];
+  const int64_t base = e * (2 * N + 1);
+  double md = 0.0, mo = 0.0;
+  if (mine && cl < N) {
+    double pa[3], pb[3];
+    vertex(x0, x1, cl, N, invN, pa);
+    vertex(x0, x1, cl + 1, N, invN, pb);
+    const double d0 = pb[0] - pa[0], d1 = pb[1] - pa[1], d2 = pb[2] - pa[2];
+    const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    md = R * h / 3.0;
+    mo = R * h / 6.0;
+    if (a.do_rhs) {
+      a.rhs[base + 2 * cl + 1] = -(a.f * h);  // negated pressure row: -(f h)
+      a.rhs[base + 2 * cl] = (cl == 0) ? a.edge_bc[2 * e] : 0.0;
+    }
+  }
+  if (mine && a.do_rhs && cl == N) a.rhs[base + 2 * N] = a.edge_bc[2 * e + 1];
+  // neighbours' tensors: cell cl - 1 (the lumped mass) and the last cell (q_N)
+  const int sb = sub * S;
+  const double mdL = __shfl(md, sb + max(cl - 1, 0), 64), moL = __shfl(mo, sb + max(cl - 1, 0), 64);
+  if (a.lhs) {
+    if (a.dq != nullptr && mine && cl <= N) {
+      double d;
+      if (cl < N) {
+        d = md + mo;
+        if (cl > 0) d = (moL + mdL) + d;
+      } else {
+        d = moL + mdL;  // q_N: the last cell only
+      }
+      a.dq[e * (int64_t)(N + 1) + cl] = d;
+    }
+    // the wave's contiguous CSR range [b_0, b_ne)
+    int bnd[EPW + 1], sfl[EPW];
+#pragma unroll
+    for (int j = 0; j < EPW; ++j) {
+      bnd[j] = __shfl(seg, j * S, 64);
+      sfl[j] = __shfl(s, j * S, 64);
+    }
+    const int last = a.ea.edge_seg[e0 + ne];
+    bnd[EPW] = last;
+#pragma unroll
+    for (int j = 0; j < EPW; ++j)
+      if (j >= ne) bnd[j] = last;
+    for (int ib = bnd[0]; ib < last; ib += 64) {  // uniform trip count across the wave
+      const int i = ib + lane;
+      int j = 0;
+#pragma unroll
+      for (int t = 1; t < EPW; ++t) j += (i >= bnd[t]) ? 1 : 0;
+      int sj = sfl[0], b0 = bnd[0];
+#pragma unroll
+      for (int t = 1; t < EPW; ++t)
+        if (t == j) {
+          sj = sfl[t];
+          b0 = bnd[t];
+        }
+      const Entry en = decode_entry(i < last ? i - b0 : 0, N, sj);
+      const int src = j * S + en.cell;
+      const double mdA = __shfl(md, src, 64), moA = __shfl(mo, src, 64);
+      const double mdB = __shfl(md, min(src + 1, 63), 64);
+      double v;
+      switch (en.vk) {
+        case V_P1: v = 1.0; break;
+        case V_M1: v = -1.0; break;
+        case V_MD: v = mdA; break;
+        case V_MO: v = moA; break;
+        default: v = mdA + mdB; break;  // interior diagonal: cells g and g+1
+      }
+      if (i < last) a.val[i] = v;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
 #pragma clang fp contract(off)
   if ((int)blockIdx.x >= a.edge_blocks) {  // multiplier rows: +-1 values, zero rhs
@@ -2759,14 +2862,21 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   if (!lhs && !rhs) return NX_OK;
   // one launch: edge blocks (4 edges each) then the multiplier-row blocks
   const int64_t nlm = std::max(h->nnz_lm, h->B);
-  const int eb = grid_of(h->E, kBlock / 64);
+  // edges per wave: 4 for N < 16, 2 for N < 32, else 1 (k_assemble, 64-cell chunks)
+  const int epw = h->N < 16 ? 4 : h->N < 32 ? 2 : 1;
+  const int eb = grid_of(grid_of(h->E, epw), kBlock / 64);
   const int lb = grid_of(nlm, kBlock);
   if (eb + lb > 0) {
     AsmArgs a{EdgeArgs{h->edge_x, h->edge_lm, h->edge_seg, h->E, h->N},
               h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs ? h->dq : nullptr, lhs, rhs,
               eb, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges, h->rhs + h->n_edge_dofs};
-    hipExtLaunchKernelGGL(k_assemble, dim3(eb + lb), dim3(kBlock), 0, h->stream,
-                          h->prof ? h->ev[0] : nullptr, h->prof ? h->ev[1] : nullptr, 0, a);
+    hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
+    if (epw == 4)
+      hipExtLaunchKernelGGL(k_assemble_seg<16>, dim3(eb + lb), dim3(kBlock), 0, h->stream, e0, e1, 0, a);
+    else if (epw == 2)
+      hipExtLaunchKernelGGL(k_assemble_seg<32>, dim3(eb + lb), dim3(kBlock), 0, h->stream, e0, e1, 0, a);
+    else
+      hipExtLaunchKernelGGL(k_assemble, dim3(eb + lb), dim3(kBlock), 0, h->stream, e0, e1, 0, a);
   }
   HIPCALL(hipGetLastError());
   if (h->prof && h->E > 0) {

@@ -61,6 +61,10 @@ CASES = {
     "edge_info_N10": (edge_info_graph, 10, None, p_y),
     "tree6_2d_N70": (lambda: ng.make_tree(6, 2, 1, dim=2), 70, "smallest_last", p_y),
     "linear_alt_N3": (lambda: linear_graph(12, ordered=lambda k: k % 2), 3, None, p_x),
+    # assembly layouts: 4 edges per wave (N < 16), 2 (N < 32), and the boundaries
+    "tree5_N15": (lambda: ng.make_tree(5, 5, 5), 15, "smallest_last", p_y),
+    "tree5_N16": (lambda: ng.make_tree(5, 5, 5), 16, "smallest_last", p_y),
+    "tree5_3d_N31": (lambda: ng.make_tree(5, 2, 3), 31, "smallest_last", p_x),
 }
 
 
