@@ -915,7 +915,22 @@ struct PcArgs {
   int exact;
   const double* Tlu;
   int n_dc_all, n_slots_all;  // hanging-chain entries / junction slots (k_pc_factor sizes)
+  // several ranks, dense top, LDS kernels, small coarse forest (nx_set_coarse): the up
+  // sweep's last workgroup does k_pc_cpart's work (ticket[0]) and every down workgroup
+  // solves the coarse forest itself, so neither one-workgroup kernel runs per iteration;
+  // fuse_pack (one-graph solve): the down sweep's last workgroup (ticket[1]) also packs the
+  // halo and this rank's beta^2 (k_pack_beta's work)
+  int fused;
+  int fuse_pack;
+  int* ticket;
+  const int* send_idx;
+  int n_send;
+  double* send_buf;
+  double* red1;
+  double* gath_self;
 };
+
+constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve in LDS
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
 // in the top part, level 0) and the chains joining two coarse junctions. sD/sJ are indexed
@@ -1328,6 +1343,8 @@ constexpr int kCapTDC = 2304; // top down-chain entries
 constexpr int kMaxTopLvl = 255;
 constexpr int kMaxNeed = 64;   // dense top: top values one job reads
 
+__device__ void pc_cpart_last(const PcArgs& pa, double* sA);
+
 template <bool MULTI, int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __restrict__ y,
                                                           const double* __restrict__ r2,
@@ -1341,6 +1358,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   __shared__ int sChild[kCapDC];
   __shared__ double sG[kCapDC];
   __shared__ int sOff[kCapS + 1];
+  __shared__ double sAtop[MULTI ? kCapT : 1];  // fused k_pc_cpart (last workgroup)
   double c2 = 0.0;
   if (mode == 0) {
     if (st->done) {
@@ -1415,10 +1433,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     }
   }
   const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
-  if (lv1 == lv0) {
-    NX_PHASE_END(16);
-    return;
-  }
+  if (lv1 > lv0) {  // the job's junction levels (block-uniform)
   const int js0 = pa.lvl_slot_off[lv0], js1 = pa.lvl_slot_off[lv1];
   const int ns = js1 - js0;
   const int dc0 = pa.slot_dc_off[js0];
@@ -1500,8 +1515,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     const double kap = fac ? pa.dc_kappa[k] : 1.0 / sT[pcn - c0] / sD[0];
     pa.u[pa.job_root_u[job]] = sIt[pcn - c0] + kap * sJ[0];
   }
+  }  // junction levels
   NX_PHASE(19);
   NX_PHASE_END(16);
+  if (MULTI && dense && pa.fused) pc_cpart_last(pa, sAtop);
 }
 
 template <bool MULTI>
@@ -1642,6 +1659,61 @@ template <int BS>
 __device__ void pc_prep_in_block(const PcArgs& pa, double* sJ, double* sZ, int* sPar,
                                  double* sTp, double* sDt);
 
+// The coarse forest solve of k_pc_coarse (same arithmetic, same order) inside one
+// workgroup, into sZc (n_coarse <= kCapCoarseLds); sD / sJ are scratch.
+__device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* sZc) {
+  const int nC = pa.n_coarse;
+  const double* __restrict__ G = pa.cbuf + 2 * nC;
+  for (int i = threadIdx.x; i < nC; i += kPcThreads) {
+    sD[i] = pa.cbuf[i];
+    sJ[i] = pa.cbuf[nC + i];
+  }
+  __syncthreads();
+  for (int lv = pa.n_clvl - 1; lv >= 0; --lv) {  // deepest level first
+    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kPcThreads) {
+      double D = sD[j], J = sJ[j];
+      for (int i = pa.c_child_off[j]; i < pa.c_child_off[j + 1]; ++i) {
+        const int k = pa.c_child[i];
+        const double g = G[k], Dk = sD[k];
+        D -= g * g / Dk;
+        J += g * sJ[k] / Dk;
+      }
+      sD[j] = D;
+      sJ[j] = J;
+    }
+    __syncthreads();
+  }
+  for (int lv = 0; lv < pa.n_clvl; ++lv) {  // root level first
+    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kPcThreads) {
+      const int p = pa.c_parent[j];
+      sZc[j] = (sJ[j] + (p >= 0 ? G[j] * sZc[p] : 0.0)) / sD[j];
+    }
+    __syncthreads();
+  }
+}
+
+// The fused halo pack (k_pack_beta's work) of the one-graph multi-rank solve: the last
+// workgroup of the down sweep to finish sums this rank's beta^2 partials into red[1] and
+// its slot of the gathered array, and packs the halo values of z. Resets its ticket.
+__device__ void pc_pack_last(const PcArgs& pa, const double* partB, const double* z) {
+  __shared__ int sLast;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    sLast = atomicAdd(pa.ticket + 1, 1) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!sLast) return;
+  __threadfence();
+  const double t = block_allsum<kPcThreads>(partB, pa.n_jobs + 1);
+  if (threadIdx.x == 0) {
+    *pa.red1 = t;
+    *pa.gath_self = t;
+    pa.ticket[1] = 0;
+  }
+  for (int i = threadIdx.x; i < pa.n_send; i += kPcThreads) pa.send_buf[i] = z[pa.send_idx[i]];
+}
+
 template <bool MULTI, int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* __restrict__ y,
                                                             const double* __restrict__ r2,
@@ -1655,6 +1727,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sNz[kMaxNeed];
   __shared__ double sGz[kCapT], sGt[kCapT], sGd[kCapT];  // start only: G columns (prep)
   __shared__ int sGp[kCapT];
+  __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
   if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
@@ -1668,6 +1741,19 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int ns = js1 - js0;
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
+  // several ranks, fused: every workgroup solves the coarse forest (k_pc_coarse's job)
+  const bool cfused = MULTI && dense && pa.fused;
+  if (cfused) {
+    pc_coarse_lds(pa, sGz, sGt, sCz);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (lin) {
+        MrState* s = const_cast<MrState*>(st);
+        s->alfa = pa.xalpha[0];
+        s->nb += 1;
+      }
+      partB[pa.n_jobs] = 0.0;  // no top kernel
+    }
+  }
   int nneed = 0;
   if (dense) {
     const int ts0 = pa.top_lvl_off[0], nt = pa.n_top;
@@ -1693,7 +1779,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       if (ln == 0) {
         if (MULTI) {  // + the coarse root's value through the tree
           const int rc = pa.top_rootc[t - ts0];
-          if (rc >= 0) acc += pa.top_w[t - ts0] * pa.zc[rc];
+          if (rc >= 0) acc += pa.top_w[t - ts0] * (cfused ? sCz[rc] : pa.zc[rc]);
         }
         sNs[k] = t;
         sNz[k] = acc;
@@ -1823,6 +1909,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   NX_PHASE(51);
   block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
   NX_PHASE_END(48);
+  if (MULTI && cfused && pa.fuse_pack) pc_pack_last(pa, partB, z);
   // single rank, start application: D is final -> factored coefficients and G here, so the
   // iterations need no separate k_pc_factor / k_pc_gbuild launches (sTa is free in mode 1)
   if (!MULTI && mode == 1) {
@@ -1864,10 +1951,34 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_wroot(PcArgs pa) {
 
 // Several ranks, dense top, every iteration: a = the summed top inputs, then this rank's
 // coarse partials [D | J | G] (D fixed by the assembly, J = KJ[root,:] a, coarse chains).
+// One workgroup of kTopThreads threads (its own kernel, or the up sweep's last workgroup).
+__device__ void pc_cpart_body(const PcArgs& pa, double* sA);
+
 __global__ __launch_bounds__(kTopThreads) void k_pc_cpart(PcArgs pa, const MrState* __restrict__ st,
                                                           int mode) {
   __shared__ double sA[kCapT];
   if (mode == 0 && st->done) return;
+  pc_cpart_body(pa, sA);
+}
+
+// The fused k_pc_cpart: the last workgroup of the up sweep to finish (atomic ticket; every
+// workgroup fences its writes first, the last one fences before reading) runs the body and
+// resets the ticket for the next launch.
+__device__ void pc_cpart_last(const PcArgs& pa, double* sA) {
+  __shared__ int sLast;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    sLast = atomicAdd(pa.ticket, 1) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!sLast) return;
+  __threadfence();
+  pc_cpart_body(pa, sA);
+  if (threadIdx.x == 0) *pa.ticket = 0;
+}
+
+__device__ void pc_cpart_body(const PcArgs& pa, double* sA) {
   const int ts0 = pa.top_lvl_off[0], nt = pa.n_top, nC = pa.n_coarse;
   for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
     double a = 0.0;
@@ -2301,9 +2412,9 @@ double* vec_of(nx_network* h, VecSel s, int64_t k) {
 // fill the ghost slots of the selected vector (n_col) from the owning ranks
 int nB_of(const nx_network* h);
 
-int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false) {
+int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false, bool packed = false) {
   if (!team_multi(t)) return NX_OK;
-  for (int r = 0; r < t.P; ++r) {
+  for (int r = 0; r < t.P && !packed; ++r) {  // packed: the down sweep's last workgroup did it
     nx_network* h = t.hs[r];
     const int nsend = h->send_off.back();
     if (beta)  // with the previous iteration's beta^2 partial sum
@@ -2393,9 +2504,10 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
       if (h->pc_jobs > 0)
         hipLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
                            h->stream, h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
-      if (MULTI && h->pa.mdense && mode == 0)  // dense top: the coarse partials only
-        hipLaunchKernelGGL(k_pc_cpart, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, st, mode);
-      else if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
+      if (MULTI && h->pa.mdense && mode == 0) {  // dense top: the coarse partials only
+        if (!h->pa.fused)  // else the up sweep's last workgroup computes them
+          hipLaunchKernelGGL(k_pc_cpart, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, st, mode);
+      } else if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
         hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream,
                            h->pa, y, r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
     } else {
@@ -2407,7 +2519,9 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
     }
     return;
   }
-  if (coarse)
+  // fused (dense top, LDS kernels): every down workgroup solves the coarse forest itself
+  const bool cfused = MULTI && h->pc_lds && h->pa.fused && h->pa.mdense && mode == 0;
+  if (coarse && !cfused)
     hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2, h->z,
                        st, h->partB, mode);
   if (h->pc_jobs > 0) {
@@ -2491,7 +2605,8 @@ int launch_part_a(const Team& t, int64_t k, const LeanOpt* lo = nullptr) {
   const bool pc = t.hs[0]->pc;
   // beta^2 of the previous iteration travels with the halo (point-to-point gather)
   const bool p2p_beta = multi && t.hs[0]->beta_p2p;
-  if (multi) CHECK(team_halo(t, pc ? VS_Z : VS_R2, k, p2p_beta));
+  const bool packed = lo != nullptr && k >= 2 && pc && t.hs[0]->pa.fuse_pack;
+  if (multi) CHECK(team_halo(t, pc ? VS_Z : VS_R2, k, p2p_beta, packed));
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
     double* r1 = h->vb[(k - 1) & 1];
@@ -3035,6 +3150,14 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
     nx_network* h = t.hs[r];
     h->pa.factored = h->pa.dc_kappa ? 1 : 0;
     h->pa.mdense = (multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin) ? 1 : 0;
+    // the down sweep of iteration k packs the halo of iteration k+1 (fused coarse solve and
+    // point-to-point beta^2 only)
+    h->pa.fuse_pack = (multi && h->pa.fused && h->pa.mdense && h->beta_p2p && h->pc_lds) ? 1 : 0;
+    h->pa.send_idx = h->send_idx;
+    h->pa.n_send = h->send_off.empty() ? 0 : h->send_off.back();
+    h->pa.send_buf = h->send_buf;
+    h->pa.red1 = h->red + 1;
+    h->pa.gath_self = h->gath ? h->gath + h->rank : nullptr;
   }
   LeanGraphs& lg = lean_of(t);
   auto cap = [&](hipGraph_t* graph, hipGraphExec_t* exec, const std::function<int()>& body) {
@@ -3126,6 +3249,7 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
       if (rc != NX_ERR_RCCL || !h0->comm) return rc;  // RCCL capture refused: eager below
     }
   }
+  for (int r = 0; r < t.P; ++r) t.hs[r]->pa.fuse_pack = 0;  // the general path packs itself
   hipStream_t s = t.hs[0]->stream;
   // r1 = r2 = b, w1 = w2 = x = 0
   for (int r = 0; r < t.P; ++r) {
@@ -3832,6 +3956,18 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   // linear form needs the LDS kernels; NXHIP_PC_LIN=0 keeps alpha's own all-reduce
   pa.lin = h->pc_lds ? 1 : 0;
   if (const char* e = std::getenv("NXHIP_PC_LIN")) pa.lin = pa.lin && std::atoi(e) != 0;
+  // fused one-workgroup steps (k_pc_cpart in the up sweep's last workgroup, the coarse solve
+  // in every down workgroup); NXHIP_PC_FUSE=0 keeps the separate kernels
+  pa.fused = (h->pc_lds && h->pc_jobs > 0 && n_coarse <= kCapCoarseLds) ? 1 : 0;
+  if (const char* e = std::getenv("NXHIP_PC_FUSE")) pa.fused = pa.fused && std::atoi(e) != 0;
+  pa.fuse_pack = 0;  // set per solve path (solve_lean)
+  {
+    int* tk = nullptr;
+    HIPCALL(hipMalloc((void**)&tk, 2 * sizeof(int)));
+    HIPCALL(hipMemset(tk, 0, 2 * sizeof(int)));
+    h->pc_bufs.push_back(tk);
+    pa.ticket = tk;
+  }
   for (const void* q : {(const void*)pa.slot_cidx, (const void*)pa.cc_chain, (const void*)pa.cc_top,
                         (const void*)pa.cc_bot, (const void*)pa.c_parent, (const void*)pa.c_child_off,
                         (const void*)pa.c_child, (const void*)pa.c_lvl_off})
