@@ -1656,8 +1656,8 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
 }
 
 template <int BS>
-__device__ void pc_prep_in_block(const PcArgs& pa, double* sJ, double* sZ, int* sPar,
-                                 double* sTp, double* sDt);
+__device__ void pc_prep_in_block(const PcArgs& pa, bool gcols, double* sJ, double* sZ, int* sPar,
+                                 double* sTp, double* sDt, int* sCid);
 
 // The coarse forest solve of k_pc_coarse (same arithmetic, same order) inside one
 // workgroup, into sZc (n_coarse <= kCapCoarseLds); sD / sJ are scratch.
@@ -1726,7 +1726,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ int sNs[kMaxNeed];
   __shared__ double sNz[kMaxNeed];
   __shared__ double sGz[kCapT], sGt[kCapT], sGd[kCapT];  // start only: G columns (prep)
-  __shared__ int sGp[kCapT];
+  __shared__ int sGp[kCapT], sGc[kCapT];
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
   if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
@@ -1912,9 +1912,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   if (MULTI && cfused && pa.fuse_pack) pc_pack_last(pa, partB, z);
   // single rank, start application: D is final -> factored coefficients and G here, so the
   // iterations need no separate k_pc_factor / k_pc_gbuild launches (sTa is free in mode 1)
-  if (!MULTI && mode == 1) {
+  if (mode == 1 && (!MULTI || pa.fused)) {
     __syncthreads();
-    pc_prep_in_block<kPcThreads>(pa, sTa, sGz, sGp, sGt, sGd);
+    pc_prep_in_block<kPcThreads>(pa, MULTI ? pa.mdense != 0 : pa.dense != 0, sTa, sGz, sGp, sGt,
+                                 sGd, sGc);
   }
 }
 
@@ -2073,13 +2074,14 @@ __device__ void pc_gbuild_column(const PcArgs& pa, int s) {
   for (int t = threadIdx.x; t < nt; t += 64) pa.G[(int64_t)t * nt + s] = sZ[t];
 }
 
-// Single rank, start application (k_pc_down_lds, mode 1): the factored coefficients and the
-// columns s0, s0 + step, ... of G (same arithmetic as k_pc_factor / pc_gbuild_column), with
-// the top part's parents, chain resistances and D staged in LDS once. D is final here: the
-// start's up and top kernels wrote it.
+// Start application (k_pc_down_lds, mode 1; several ranks: fused mode): the factored
+// coefficients and the columns s0, s0 + step, ... of G (same arithmetic as k_pc_factor /
+// pc_gbuild_column), with the top part's parents, chain resistances, D and coarse indices
+// staged in LDS once; several ranks also the KJ columns and, in workgroup 0, the roots and
+// weights of k_pc_wroot. D is final here: the start's up and top (and coarse) kernels wrote it.
 template <int BS>
-__device__ void pc_prep_in_block(const PcArgs& pa, double* sJ, double* sZ, int* sPar,
-                                 double* sTp, double* sDt) {
+__device__ void pc_prep_in_block(const PcArgs& pa, bool gcols, double* sJ, double* sZ, int* sPar,
+                                 double* sTp, double* sDt, int* sCid) {
   if (pa.dc_kappa) {
     const int64_t stride = (int64_t)gridDim.x * BS;
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < pa.n_dc_all || i < pa.n_slots_all;
@@ -2091,26 +2093,33 @@ __device__ void pc_prep_in_block(const PcArgs& pa, double* sJ, double* sZ, int* 
       if (i < pa.n_slots_all) pa.slot_invD[i] = 1.0 / pa.slot_D[i];
     }
   }
-  if (!pa.dense || (int)blockIdx.x >= pa.n_top) return;  // block-uniform
+  if (!gcols || (int)blockIdx.x >= pa.n_top) return;  // block-uniform
   const int nt = pa.n_top, ts0 = pa.top_lvl_off[0];
+  const bool cd = pa.KJ != nullptr;  // several ranks: coarse roots are Dirichlet nodes
   for (int u = threadIdx.x; u < nt; u += BS) {
     const int p = pa.slot_parent[ts0 + u];
     sPar[u] = p >= ts0 ? p - ts0 : -1;
     const int pc = pa.slot_pchain[ts0 + u];
     sTp[u] = pc >= 0 ? pa.chain_T[pc] : 1.0;
     sDt[u] = pa.slot_D[ts0 + u];
+    sCid[u] = cd ? pa.slot_cidx[ts0 + u] : -1;
   }
   __syncthreads();
   for (int s = blockIdx.x; s < nt; s += gridDim.x) {
-    for (int i = threadIdx.x; i < nt; i += BS) sJ[i] = 0.0;
+    for (int i = threadIdx.x; i < nt; i += BS) {
+      sJ[i] = 0.0;
+      if (cd) pa.KJ[(int64_t)i * nt + s] = 0.0;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       double J = 1.0;
       sJ[s] = 1.0;
-      for (int t = s, p = sPar[s]; p >= 0; t = p, p = sPar[t]) {
+      int t = s;
+      for (int p = sPar[s]; p >= 0; t = p, p = sPar[t]) {
         J = J / sTp[t] / sDt[t];
         sJ[p] = J;
       }
+      if (cd && sCid[t] >= 0) pa.KJ[(int64_t)t * nt + s] = J;  // t is the root
     }
     __syncthreads();
     for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
@@ -2119,12 +2128,33 @@ __device__ void pc_prep_in_block(const PcArgs& pa, double* sJ, double* sZ, int* 
         const int p = sPar[u];
         double num = sJ[u];
         if (p >= 0) num += sZ[p] / sTp[u];
-        sZ[u] = num / sDt[u];
+        sZ[u] = (cd && p < 0 && sCid[u] >= 0) ? 0.0 : num / sDt[u];
       }
       __syncthreads();
     }
     for (int t = threadIdx.x; t < nt; t += BS) pa.G[(int64_t)t * nt + s] = sZ[t];
     __syncthreads();
+  }
+  if (cd && blockIdx.x == 0) {  // k_pc_wroot: coarse root and weight of every top slot
+    for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
+      const int a = pa.top_lvl_off[lv] - ts0, b = pa.top_lvl_off[lv + 1] - ts0;
+      for (int t = a + threadIdx.x; t < b; t += BS) {
+        const int p = sPar[t];
+        if (p < 0) {
+          const int c = sCid[t];
+          sCid[t] = c;  // own root index (already there)
+          sJ[t] = c >= 0 ? 1.0 : 0.0;
+        } else {
+          sCid[t] = sCid[p];
+          sJ[t] = sJ[p] / sTp[t] / sDt[t];
+        }
+      }
+      __syncthreads();
+    }
+    for (int t = threadIdx.x; t < nt; t += BS) {
+      pa.top_rootc[t] = sCid[t];
+      pa.top_w[t] = sJ[t];
+    }
   }
 }
 
@@ -3105,6 +3135,7 @@ int launch_head_multi(const Team& t, int L, double rtol, int maxit) {
   CHECK(team_pc(t, 0, 1, 1));
   for (int r = 0; r < t.P; ++r) {  // coefficients of this assembly's D (fixed per solve)
     nx_network* h = t.hs[r];
+    if (h->pc_lds && h->pa.fused && h->pc_jobs > 0) continue;  // the start's down sweep did it
     if (h->pa.dc_kappa) {
       const int nmax = (int)std::max<int64_t>(h->pc_ndc, h->pc_slots);
       if (nmax > 0)
@@ -3264,10 +3295,19 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
     HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, h->stream));
   }
   if (t.hs[0]->pc) {  // beta_1^2 = b . P^{-1} b
+    // the flags of the iterations (mode-1 kernels ignore them, except that the start's down
+    // sweep builds G when the dense top is on)
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      h->pa.factored = h->pa.dc_kappa ? 1 : 0;
+      h->pa.mdense =
+          (multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin) ? 1 : 0;
+    }
     CHECK(team_pc(t, 0, 1));
     for (int r = 0; r < t.P; ++r) {  // coefficients of this assembly's D (fixed per solve)
       nx_network* h = t.hs[r];
-      const bool fused = !multi && h->pc_lds;  // k_pc_down_lds (start) did factor + G
+      // k_pc_down_lds (start) did factor + G (+ KJ, roots and weights with several ranks)
+      const bool fused = h->pc_lds && h->pc_jobs > 0 && (!multi || h->pa.fused);
       if (h->pa.dc_kappa && !fused) {
         const int nmax = (int)std::max<int64_t>(h->pc_ndc, h->pc_slots);
         if (nmax > 0)
@@ -3275,16 +3315,9 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
                              h->pa, (int)h->pc_ndc, (int)h->pc_slots);
       }
       const bool md = multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin;
-      if (h->pa.dense && (md || (!multi && !fused)))
+      if (h->pa.dense && (md || !multi) && !fused)
         hipLaunchKernelGGL(k_pc_gbuild, dim3(h->pa.n_top), dim3(64), 0, h->stream, h->pa);
-      if (md) hipLaunchKernelGGL(k_pc_wroot, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa);
-    }
-    // the iterations use them (the start above computed D)
-    for (int r = 0; r < t.P; ++r) {
-      nx_network* h = t.hs[r];
-      h->pa.factored = h->pa.dc_kappa ? 1 : 0;
-      h->pa.mdense =
-          (multi && h->pa.dense && h->pa.KJ && h->pa.n_coarse > 0 && h->pa.lin) ? 1 : 0;
+      if (md && !fused) hipLaunchKernelGGL(k_pc_wroot, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa);
     }
   } else {
     for (int r = 0; r < t.P; ++r) {
