@@ -2588,13 +2588,15 @@ bool team_lin(const Team& t) {
 
 
 // Whole preconditioner application for every rank of the team, with the coarse exchange.
-int team_pc(const Team& t, int64_t k, int mode, int start_vb = 0) {
+// from_rhs: the start condenses the rhs itself and iteration 1 reads r_1 = b from it (the
+// one-graph solve; the rhs is read-only for both)
+int team_pc(const Team& t, int64_t k, int mode, bool from_rhs = false) {
   const bool multi = team_multi(t);
   for (int half = 0; half < 2; ++half) {
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
-      double* y = mode ? h->vb[start_vb] : h->vb[(k - 1) & 1];
-      const double* r2 = mode ? h->vb[1] : h->vb[k & 1];
+      double* y = mode ? (from_rhs ? h->rhs : h->vb[0]) : h->vb[(k - 1) & 1];
+      const double* r2 = mode ? h->vb[1] : (from_rhs && k == 1) ? h->rhs : h->vb[k & 1];
       MrState* st = mode ? h->st : h->st + (k & 1);
       MrState* other = mode ? h->st + 1 : h->st + ((k + 1) & 1);
       if (multi) launch_pc<true>(h, y, r2, st, other, mode, half);
@@ -2646,7 +2648,8 @@ int launch_part_a(const Team& t, int64_t k, const LeanOpt* lo = nullptr) {
     double* w2 = h->wb[(k - 1) & 1];
     MrState* sin = h->st + ((k + 1) & 1);
     MrState* sout = h->st + (k & 1);
-    MrVecs mv{r1, r1, r2, w1, w2, h->x, h->z, h->vv};
+    // one-graph solve: k_mr_a(2) reads r_1 = b from the rhs
+    MrVecs mv{r1, (lo && pc && k == 2) ? h->rhs : r1, r2, w1, w2, h->x, h->z, h->vv};
     const int nB = nB_of(h);
     // profiling (single handle): events bound to the kernel's own dispatch packet
     // (hipExtLaunchKernel), so the interval is the kernel's execution like rocprofv3's
@@ -2677,12 +2680,12 @@ int launch_part_a(const Team& t, int64_t k, const LeanOpt* lo = nullptr) {
 
 // Second part of iteration k: the preconditioner (or the Lanczos step without it) and,
 // with several ranks and beta^2 by all-reduce, that reduction.
-int launch_part_pc(const Team& t, int64_t k) {
+int launch_part_pc(const Team& t, int64_t k, bool from_rhs = false) {
   const bool multi = team_multi(t);
   const bool pc = t.hs[0]->pc;
   const bool p2p_beta = multi && t.hs[0]->beta_p2p;
   if (pc) {
-    CHECK(team_pc(t, k, 0));
+    CHECK(team_pc(t, k, 0, from_rhs));
   } else {
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
@@ -2881,7 +2884,12 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   if ((rc = dalloc(&h->rowptr, n_own + 1))) return bail(rc);
   if ((rc = dalloc(&h->col, h->nnz))) return bail(rc);
   if ((rc = dalloc(&h->val, h->nnz))) return bail(rc);
-  if ((rc = dalloc(&h->rhs, n_own))) return bail(rc);
+  // rhs has ghost slots (zero): the one-graph solve reads b as r_1 straight from it, and the
+  // junction slots of ghost junctions index past the owned rows
+  if ((rc = dalloc(&h->rhs, n_col))) return bail(rc);
+  if (n_col > n_own && hipMemsetAsync(h->rhs + n_own, 0, sizeof(double) * (n_col - n_own),
+                                      h->stream) != hipSuccess)
+    return bail(fail(NX_ERR_HIP, "memset failed"));
   for (int i = 0; i < 2; ++i) {
     if ((rc = dalloc(&h->vb[i], n_col))) return bail(rc);
     if ((rc = dalloc(&h->wb[i], n_own))) return bail(rc);
@@ -3120,19 +3128,13 @@ int capture(nx_network* h, hipGraph_t* graph, hipGraphExec_t* exec,
 }
 
 // ---- several ranks (RCCL, one process per GPU; or an in-process group) with the
-// preconditioner: the same one-graph solve. Head = b -> vb[1] (owned rows; ghost slots of
-// vb are zero from allocation and stay zero), the start application with its coarse
-// all-reduce, the per-solve coefficients, iterations 1..L-1, then the halo and k_mr_a of
-// iteration L (published). beta_1^2 travels with the halo of iteration 1 like every later
+// preconditioner: the same one-graph solve. Head = the start application from the rhs
+// (ghost slots of the rhs and of r are zero from allocation and stay zero) with its coarse
+// all-reduce, the per-solve coefficients (or the fused start), iterations 1..L-1, then the
+// halo and k_mr_a of iteration L (published). beta_1^2 travels with the halo of iteration 1 like every later
 // beta^2 (point-to-point gather), so k_mr_a(1) initialises the state itself.
 int launch_head_multi(const Team& t, int L, double rtol, int maxit) {
-  for (int r = 0; r < t.P; ++r) {
-    nx_network* h = t.hs[r];
-    if (h->n_own > 0)
-      HIPCALL(hipMemcpyAsync(h->vb[1], h->rhs, sizeof(double) * h->n_own, hipMemcpyDeviceToDevice,
-                             h->stream));
-  }
-  CHECK(team_pc(t, 0, 1, 1));
+  CHECK(team_pc(t, 0, 1, true));
   for (int r = 0; r < t.P; ++r) {  // coefficients of this assembly's D (fixed per solve)
     nx_network* h = t.hs[r];
     if (h->pc_lds && h->pa.fused && h->pc_jobs > 0) continue;  // the start's down sweep did it
@@ -3150,7 +3152,7 @@ int launch_head_multi(const Team& t, int L, double rtol, int maxit) {
   const LeanOpt first{true, L == 1, rtol, maxit};
   CHECK(launch_part_a(t, 1, &first));
   for (int k = 1; k < L; ++k) {
-    CHECK(launch_part_pc(t, k));
+    CHECK(launch_part_pc(t, k, true));
     const LeanOpt next{false, k + 1 == L, rtol, maxit};
     CHECK(launch_part_a(t, k + 1, &next));
   }
