@@ -117,10 +117,11 @@ int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
              int32_t* iters, double* relres, int32_t* converged);
 
 /*
- * Tree Schur-complement preconditioner for MINRES, P = blockdiag(D, G^T D^{-1} G) with D the
- * lumped flux mass (networks_fenicsx_amd/precond.py derives it and builds these arrays).
- * There is no reference counterpart: the reference factorises with MUMPS
- * (solver.py:456-463); this makes the iterative replacement converge in O(10) iterations.
+ * Tree Schur-complement preconditioner for MINRES: by default the exact one,
+ * P = blockdiag(M, G^T M^{-1} G) with M the consistent flux mass (3 iterations), or with the
+ * lumped mass D (nx_set_pc_exact; networks_fenicsx_amd/precond.py derives both and builds
+ * these arrays). There is no reference counterpart: the reference factorises with MUMPS
+ * (solver.py:456-463); this makes the iterative replacement converge in 3 iterations.
  * enable = 0 switches back to unpreconditioned MINRES. Chains (one per local edge, in job
  * order): edge slot, flip (chain runs target -> source), top / bottom junction slot (-1 =
  * ground). Junction slots (one per owned multiplier, level order per job): multiplier row,
@@ -128,7 +129,7 @@ int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
  * entry, slot_plam: the parent's multiplier row -- both derivable, passed to save the
  * kernels a dependent load). Jobs (one workgroup each):
  * chain ranges and level ranges; lvl_slot_off / top_lvl_off: slot offsets per level (root
- * level first) of the lower jobs / of the single top workgroup. Requires N <= 256.
+ * level first) of the lower jobs / of the single top workgroup. Requires N <= 1024.
  * With several ranks the slots also cover the ghost junctions at the ends of local edges
  * (slot_lam = their ghost column) and nx_set_coarse must follow.
  */

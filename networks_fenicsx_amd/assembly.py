@@ -167,7 +167,7 @@ class HydraulicNetworkAssembler:
             self._init_comm()
         # MINRES preconditioner (tree Schur complement); topology-only, built once
         self._pc: TreePreconditioner | None = None
-        if mesh.N <= 256:
+        if mesh.N <= 1024:
             jobs = int(os.environ.get("NXHIP_PC_JOBS", "256"))  # swept: 64..1024
             self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=jobs)
         self.set_preconditioner(True)

@@ -2575,6 +2575,8 @@ void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState*
     case 5: launch_pc_wc<MULTI, 8, 2>(h, y, r2, st, other, mode, half); break;
     case 6: launch_pc_wc<MULTI, 4, 4>(h, y, r2, st, other, mode, half); break;
     case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half); break;
+    case 8: launch_pc_wc<MULTI, 64, 8>(h, y, r2, st, other, mode, half); break;
+    case 9: launch_pc_wc<MULTI, 64, 16>(h, y, r2, st, other, mode, half); break;
     default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half); break;
   }
 }
@@ -3658,11 +3660,13 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   else if (N <= 64) variant = 2;
   else if (N <= 128) variant = 3;
   else if (N <= 256) variant = 4;
-  else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 256 cells per edge");
+  else if (N <= 512) variant = 8;
+  else if (N <= 1024) variant = 9;
+  else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 1024 cells per edge");
   if (const char* e = std::getenv("NXHIP_PC_VARIANT")) {  // tuning: (W, CPL) override
     const int v = std::atoi(e);
-    const int cap[8] = {16, 32, 64, 128, 256, 16, 16, 32};
-    if (v >= 0 && v < 8 && N <= cap[v]) variant = v;
+    const int cap[10] = {16, 32, 64, 128, 256, 16, 16, 32, 512, 1024};
+    if (v >= 0 && v < 10 && N <= cap[v]) variant = v;
   }
   if (n_chains != h->E) return fail(NX_ERR_ARG, "one chain per local edge expected");
   // one slot per owned multiplier, plus (several ranks) the ghost junctions at the ends of

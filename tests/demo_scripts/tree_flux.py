@@ -19,7 +19,7 @@ from networks_fenicsx.post_processing import export_functions, extract_global_fl
 out = Path(sys.argv[1])
 graph = network_generation.make_tree(n=2, H=1, W=1)
 expect = (2 - math.sqrt(2), 4 - 2 * math.sqrt(2), math.sqrt(2) / (0.5 + math.sqrt(2)))
-for N in (2, 4, 8):
+for N in (2, 4, 8, 64, 512, 1024):  # demo_tree.py doubles N up to 1024
     net = NetworkMesh(graph, N=N)
     asm = HydraulicNetworkAssembler(net)
     asm.compute_forms(p_bc_ex=lambda x: x[1])

@@ -168,6 +168,28 @@ def test_large_tree_properties():
     assert err <= SOL_TOL, err
 
 
+@pytest.mark.parametrize("N", [300, 700, 1024])
+def test_preconditioner_long_edges(N):
+    """N > 256 cells per edge (demo_tree.py doubles N up to 1024): the (64, 8) / (64, 16)
+    chain layouts keep the exact preconditioner, 3 iterations to the direct solution."""
+    G = ng.make_tree(3, 1, 1)
+    mesh = NetworkMesh(G, N=N)
+    asm = HydraulicNetworkAssembler(mesh)
+    asm.compute_forms(p_bc_ex=lambda x: x[1])
+    assert asm.preconditioned
+    solver = Solver(asm)
+    solver.assemble()
+    solver.solve()
+    assert solver.ksp.getIterationNumber() <= 4
+    src, dst = mesh.edges
+    P = O.build_problem(mesh.node_coordinates, src, dst, N, mesh.edge_colors)
+    A, b = O.assemble_reference(P, lambda x: x[1])
+    _, _, perm, _ = O.to_build_layout(P, A, b)
+    x_ref = O.solve_reference(A, b)
+    x = solver.solution_vector()
+    assert np.linalg.norm(x - x_ref[perm]) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
 def test_not_converged_raises():
     from networks_fenicsx_amd._lib import NxNotConverged
 
