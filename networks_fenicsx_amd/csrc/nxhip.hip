@@ -3655,7 +3655,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   }
   const int N = h->N;
   int variant;
-  if (N <= 16) variant = 0;
+  if (N <= 16) variant = 5;  // 8 lanes x 2 cells: one chain round per job (swept: 16x1 +8%)
   else if (N <= 32) variant = 1;
   else if (N <= 64) variant = 2;
   else if (N <= 128) variant = 3;

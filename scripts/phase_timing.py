@@ -43,6 +43,7 @@ def main() -> int:
     lib = _lib.lib()
     fn = lib.nx_debug_phases
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int32]
+    _lib.set_lean(False)  # the general path: k_mr_a stamps of full iterations too
     for _ in range(3):
         it, rr, conv = h.solve(1e-12, 50000, 32)
     buf = (C.c_ulonglong * 128)()
