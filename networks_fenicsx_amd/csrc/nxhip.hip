@@ -1345,6 +1345,8 @@ constexpr int kMaxNeed = 64;   // dense top: top values one job reads
 
 __device__ void pc_cpart_last(const PcArgs& pa, double* sA);
 
+constexpr int kCapLvl = 64;  // job levels whose slot offsets are staged in LDS
+
 template <bool MULTI, int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __restrict__ y,
                                                           const double* __restrict__ r2,
@@ -1358,6 +1360,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   __shared__ int sChild[kCapDC];
   __shared__ double sG[kCapDC];
   __shared__ int sOff[kCapS + 1];
+  __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sAtop[MULTI ? kCapT : 1];  // fused k_pc_cpart (last workgroup)
   double c2 = 0.0;
   if (mode == 0) {
@@ -1470,10 +1473,14 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     sJ0[sl] = J0;
   }
   if (threadIdx.x == 0) sOff[ns] = pa.slot_dc_off[js1] - dc0;
+  if ((int)threadIdx.x <= min(lv1 - lv0, kCapLvl)) sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
   __syncthreads();
   NX_PHASE(18);
   for (int lv = lv1 - 1; lv >= lv0; --lv) {  // phase B, deepest level first
-    for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kPcThreads) {
+    // level offsets staged in LDS with phase A (a global load per level costs a round trip)
+    const int la = lv - lv0 <= kCapLvl ? sLvl[lv - lv0] : pa.lvl_slot_off[lv];
+    const int lb = lv - lv0 < kCapLvl ? sLvl[lv - lv0 + 1] : pa.lvl_slot_off[lv + 1];
+    for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
       const int sl = j - js0;
       double D = sD0[sl], J = sJ0[sl];
       if (fac) {
@@ -1727,6 +1734,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sNz[kMaxNeed];
   __shared__ double sGz[kCapT], sGt[kCapT], sGd[kCapT];  // start only: G columns (prep)
   __shared__ int sGp[kCapT], sGc[kCapT];
+  __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
   if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
@@ -1821,10 +1829,14 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     sP[sl] = local ? p - js0 : -1;
     sZ[sl] = (!local && p >= 0) ? outside(p) : 0.0;  // an outside parent is a top slot
   }
+  if (lv1 > lv0 && (int)threadIdx.x <= min(lv1 - lv0, kCapLvl))
+    sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
   __syncthreads();
   NX_PHASE(49);
   for (int lv = lv0; lv < lv1; ++lv) {  // phase B, root level first, LDS only
-    for (int j = pa.lvl_slot_off[lv] + threadIdx.x; j < pa.lvl_slot_off[lv + 1]; j += kPcThreads) {
+    const int la = lv - lv0 <= kCapLvl ? sLvl[lv - lv0] : pa.lvl_slot_off[lv];
+    const int lb = lv - lv0 < kCapLvl ? sLvl[lv - lv0 + 1] : pa.lvl_slot_off[lv + 1];
+    for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
       const int sl = j - js0;
       const int p = sP[sl];
       sZ[sl] = sA[sl] + sB[sl] * (p >= 0 ? sZ[p] : sZ[sl]);
