@@ -48,13 +48,28 @@ def spmv_bytes(n_rows: int, nnz: int) -> int:
     return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
-def mr_spmv_bytes(n_rows: int, nnz: int, preconditioned: bool) -> int:
-    """Algorithmic bytes of one fused ``k_mr_a`` launch: the CSR SpMV (matrix, row
-    pointers, the gathered vector read once) plus the fused vector traffic -- r1
-    read+write, w1 read+write, w2 read, x read+write (7 passes of 8 B per row), and with
-    the preconditioner the Lanczos vector v read+write (2 more passes)."""
-    passes = 9 if preconditioned else 7
-    return 12 * nnz + 4 * (n_rows + 1) + 8 * n_rows + 8 * passes * n_rows
+K_MAX_V = 8  # stored Lanczos vectors (csrc/nxhip.hip kMaxV)
+
+
+def mr_spmv_bytes(n_rows: int, nnz: int, preconditioned: bool, iterations: int = 1) -> float:
+    """Algorithmic bytes of one fused ``k_mr_a`` launch that ran a Lanczos step, averaged
+    over the ``iterations`` launches of a solve: the CSR SpMV (matrix, row pointers, the
+    gathered vector read once) plus the fused vector traffic.
+
+    With the preconditioner the first ``K_MAX_V`` Lanczos vectors are stored and the solution
+    is formed once at the end (csrc/nxhip.hip, MrVecs::vs): launch 1 writes y and v
+    (2 passes of 8 B per row), launches 2..8 also read r_{k-1} (3 passes); launch 9 hands
+    over to the w recurrence (reads v_1..v_8, writes x, w_7, w_8: 12 more passes); later
+    launches run the recurrence (r1 r/w, v r/w, w1 r/w, w2 r, x r/w: 9 passes). Without the
+    preconditioner every launch runs the recurrence on r (7 passes)."""
+    spmv = 12 * nnz + 4 * (n_rows + 1) + 8 * n_rows
+    if not preconditioned:
+        return spmv + 8 * 7 * n_rows
+    its = max(1, iterations)
+    passes = 0
+    for k in range(1, its + 1):
+        passes += 2 if k == 1 else 3 if k <= K_MAX_V else 15 if k == K_MAX_V + 1 else 9
+    return spmv + 8 * n_rows * passes / its
 
 
 def pmc_traffic(kernel_prefix: str):
@@ -176,7 +191,7 @@ def main() -> int:
     warm_spmv_ms = h.bench_spmv(200)
     cold_spmv_ms, cold_copies = h.bench_spmv_cold(120)
     pc_on = asm.preconditioned
-    nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on)
+    nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on, max(int(prof["spmv_count"]), 1))
     achieved = nbytes / (spmv_ms * 1e-3) / 1e9
     sbytes = spmv_bytes(h.n_rows, h.nnz)
     kname = f"k_mr_a<{str(world > 1).lower()}, {str(pc_on).lower()}>"

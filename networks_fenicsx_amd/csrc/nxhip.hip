@@ -652,7 +652,15 @@ struct MrVecs {
   double* x;
   const double* z;   // preconditioned: z_k = P^{-1} r_k, gathered (has ghost slots)
   double* v;         // preconditioned: v_{k-1} in, v_k = z_k / beta_k out (in place)
+  // preconditioned, stored Lanczos vectors (or null): v_1..v_kMaxV live in vs (stride
+  // vstride); the first kMaxV rotations only record (oldeps, delta, 1/gamma, phi) in hist
+  // and the solution is formed once, x = sum c_i v_i, when the solve stops -- or, past
+  // kMaxV iterations, x, w_{m-1}, w_m are formed and the w recurrence takes over
+  double* vs;
+  int64_t vstride;
+  double* hist;
 };
+constexpr int kMaxV = 8;
 
 // Initial state from beta_1^2 (k_mr_init, or k_mr_a of iteration 1 in the single-rank head
 // graph, which folds the initialisation in).
@@ -699,7 +707,7 @@ __device__ __forceinline__ void mr_publish(MrState s, const MrInit& ini) {
 // w_{k-3}, w_{k-2} and x are not initialised in memory: the first rotations read them as
 // zero (it0 = completed rotations before this one), so the solve needs no memsets.
 template <bool MULTI, bool PC>
-__global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState* __restrict__ sin,
+__global__ __launch_bounds__(kBlock, 8) void k_mr_a(Csr A, MrVecs v, const MrState* __restrict__ sin,
                                                  MrState* __restrict__ sout,
                                                  const double* __restrict__ partB, int nB,
                                                  const double* __restrict__ red,
@@ -727,6 +735,43 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
   const double c1 = upd ? beta / oldb : 0.0;
   const bool spmv = !s.done;
   const double* g = PC ? v.z : v.r2;  // v_k = g / beta_k
+  // stored Lanczos vectors: rotation j = s.it uses v_j = vs[j - 1]
+  const bool sv = PC && v.vs != nullptr;
+  const int jr = s.it;
+  const bool stored = sv && upd && jr <= kMaxV;
+  const bool trans = stored && !s.done && jr == kMaxV;  // hand over to the w recurrence
+  const bool comb = stored && (s.done || trans);        // form x (and w) from v_1..v_j
+  __shared__ double sM[kMaxV][kMaxV], sCx[kMaxV], sH[kMaxV][4];
+  if (stored && blockIdx.x == 0 && threadIdx.x == 0) {
+    double* hst = v.hist + 4 * (jr - 1);
+    hst[0] = rot.oldeps;
+    hst[1] = rot.delta;
+    hst[2] = rot.denom;
+    hst[3] = rot.phi;
+  }
+  if (comb) {  // w_i = sum_c M[i][c] v_c (the recurrence in coefficients), x = sum phi_i w_i
+    // (LDS work arrays: a private 8x8 array would cost every launch its registers)
+    const int t = threadIdx.x;
+    if (t < 4 * kMaxV) {
+      const int i = t >> 2, f = t & 3;
+      if (i + 1 < jr) sH[i][f] = v.hist[t];
+      else if (i + 1 == jr) sH[i][f] = f == 0 ? rot.oldeps : f == 1 ? rot.delta : f == 2 ? rot.denom : rot.phi;
+    }
+    __syncthreads();
+    if (t < kMaxV) {  // column t of M, rows in order
+      double cx = 0.0, m2 = 0.0, m1 = 0.0;
+      for (int i = 0; i < jr; ++i) {
+        const double m = ((t == i ? 1.0 : 0.0) - sH[i][0] * m2 - sH[i][1] * m1) * sH[i][2];
+        sM[i][t] = m;
+        cx += sH[i][3] * m;
+        m2 = m1;
+        m1 = m;
+      }
+      sCx[t] = cx;
+    }
+    __syncthreads();
+  }
+  double* vout = (sv && s.nb < kMaxV) ? v.vs + (int64_t)s.nb * v.vstride : v.v;
   double part = 0.0;
   for (int c = 0; c < chunksA; ++c) {
     const int64_t r0 = ((int64_t)blockIdx.x * chunksA + c) * kRowsPerBlock;
@@ -737,7 +782,23 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
       const int64_t r = r0 + threadIdx.x;
       // c1 = 0 in iteration 1; after the last rotation only the solution update remains
       const double r1v = (upd && (spmv || !PC)) ? v.r1in[r] : 0.0;
-      if (upd) {  // w = (v - oldeps w1 - delta w2) / gamma ; x += phi w
+      if (comb) {  // x (and, handing over, w_{j-1} -> w2's buffer, w_j -> w1's) from v_1..v_j
+        double xs = 0.0, wa = 0.0, wb = 0.0;
+#pragma unroll 1
+        for (int i = 0; i < jr; ++i) {
+          const double vi = v.vs[(int64_t)i * v.vstride + r];
+          xs += sCx[i] * vi;
+          if (trans) {
+            wa += sM[jr - 2][i] * vi;  // w_{j-1}
+            wb += sM[jr - 1][i] * vi;  // w_j
+          }
+        }
+        v.x[r] = xs;
+        if (trans) {
+          const_cast<double*>(v.w2)[r] = wa;
+          v.w1[r] = wb;
+        }
+      } else if (upd && !stored) {  // w = (v - oldeps w1 - delta w2) / gamma ; x += phi w
         const double vk = PC ? v.v[r] : r1v / oldb;
         const double w1v = it0 >= 2 ? v.w1[r] : 0.0;  // w_{k-3}, w_{k-2}: zero at first
         const double w2v = it0 >= 1 ? v.w2[r] : 0.0;
@@ -750,7 +811,7 @@ __global__ __launch_bounds__(kBlock) void k_mr_a(Csr A, MrVecs v, const MrState*
         const double y = sc * Ay - c1 * r1v;
         part += vn * y;
         v.r1[r] = y;
-        if (PC) v.v[r] = vn;
+        if (PC) vout[r] = vn;
       }
     }
     __syncthreads();  // LDS of spmv_row_sum is reused by the next chunk
@@ -2366,6 +2427,8 @@ struct nx_network {
   std::vector<void*> pc_bufs;
   double* z = nullptr;  // P^{-1} r, n_col
   double* vv = nullptr; // Lanczos vector v, n_own
+  double* vs = nullptr;   // stored Lanczos vectors v_1..v_kMaxV (kMaxV * n_own), or null
+  double* hist = nullptr; // their rotations (4 * kMaxV)
   MrState* h_st = nullptr;             // pinned host mirror of both
   MrState* h_last = nullptr;           // host-coherent, mapped: the state published by the
   MrState* d_last = nullptr;           // last k_mr_a of a lean graph (mr_publish)
@@ -2663,7 +2726,8 @@ int launch_part_a(const Team& t, int64_t k, const LeanOpt* lo = nullptr) {
     MrState* sin = h->st + ((k + 1) & 1);
     MrState* sout = h->st + (k & 1);
     // one-graph solve: k_mr_a(2) reads r_1 = b from the rhs
-    MrVecs mv{r1, (lo && pc && k == 2) ? h->rhs : r1, r2, w1, w2, h->x, h->z, h->vv};
+    MrVecs mv{r1,   (lo && pc && k == 2) ? h->rhs : r1, r2, w1, w2, h->x, h->z, h->vv,
+              pc ? h->vs : nullptr, h->n_own, h->hist};
     const int nB = nB_of(h);
     // profiling (single handle): events bound to the kernel's own dispatch packet
     // (hipExtLaunchKernel), so the interval is the kernel's execution like rocprofv3's
@@ -2970,7 +3034,7 @@ NX_API int nx_destroy(nx_network_t* h) {
   }
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val, h->dq,
-                  h->z, h->vv,
+                  h->z, h->vv, h->vs, h->hist,
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
                   h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
                   h->partA,  h->partB,   h->red,
@@ -3070,7 +3134,8 @@ namespace {
 void launch_a_lean(nx_network* h, int64_t k, bool init, double rtol, int maxit,
                    const double* r1in = nullptr, bool mark = false) {
   double* r1 = h->vb[(k - 1) & 1];
-  MrVecs mv{r1, r1in ? r1in : r1, h->vb[k & 1], h->wb[k & 1], h->wb[(k - 1) & 1], h->x, h->z, h->vv};
+  MrVecs mv{r1,    r1in ? r1in : r1, h->vb[k & 1], h->wb[k & 1], h->wb[(k - 1) & 1],
+            h->x,  h->z,             h->vv,        h->vs,        h->n_own,         h->hist};
   const MrInit ini{init ? 1 : 0, nB_of(h), maxit, rtol, h->partB, mark ? 1 : 0, h->d_seq, h->d_last};
   hipLaunchKernelGGL((k_mr_a<false, true>), dim3(h->nA), dim3(kBlock), 0, h->stream, csr_of(h), mv,
                      h->st + ((k + 1) & 1), h->st + (k & 1), h->partB, nB_of(h), h->red, h->partA,
@@ -3788,6 +3853,13 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     if (p == nullptr) return fail(NX_ERR_HIP, "preconditioner upload failed");
   if (!h->z) CHECK(dalloc(&h->z, std::max<int64_t>(h->n_col, 1)));
   if (!h->vv) CHECK(dalloc(&h->vv, std::max<int64_t>(h->n_own, 1)));
+  {  // stored Lanczos vectors (NXHIP_STORED_V=0: the w recurrence from the first rotation)
+    const char* e = std::getenv("NXHIP_STORED_V");
+    if ((e == nullptr || std::atoi(e) != 0) && !h->vs) {
+      CHECK(dalloc(&h->vs, (int64_t)kMaxV * std::max<int64_t>(h->n_own, 1)));
+      CHECK(dalloc(&h->hist, 4 * (int64_t)kMaxV));
+    }
+  }
   HIPCALL(hipMemset(h->z, 0, sizeof(double) * std::max<int64_t>(h->n_col, 1)));
   if (n_jobs + 1 > h->nB) {  // partB holds one partial per job + the top block
     HIPCALL(hipFree(h->partB));
