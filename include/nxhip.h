@@ -78,6 +78,31 @@ int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
               const int32_t* lm_col, const double* lm_val, int64_t n_ghost,
               nx_network_t** out);
 
+/*
+ * General element degrees: HydraulicNetworkAssembler(mesh, flux_degree=k,
+ * pressure_degree=m) (assembly.py:121-146) -- P_k equispaced flux per edge, DG0 (m = 0)
+ * or continuous P_m pressure. One rank; no tree preconditioner (plain MINRES). The host
+ * (networks_fenicsx_amd/layout_fe.py) numbers the DoFs, gives the sorted CSR pattern and
+ * lists, for every nonzero and every rhs row, its terms in summation order; the device
+ * evaluates them on every nx_assemble (k_assemble_fe: one thread per nonzero / row):
+ *
+ *   term (idx, ent) = table_val[ent] x factor, factor by table_kind[ent]:
+ *     0 constant 1 | 1 R_e h_c (mass; idx = cell e*N + c) | 2 f h_c (source; idx = cell)
+ *     | 3 edge_bc[idx] (boundary rhs; idx = 2e + end)
+ *   h_c is the cell length from edge_x, computed like the reference mesh generator.
+ *
+ *   n_rows, rowptr (n_rows+1), col   the symmetric system's CSR pattern (sorted rows)
+ *   n_table, table_kind, table_val   the term table (reference element tensors, signs)
+ *   a_ptr (nnz+1), a_idx, a_ent      the terms of every nonzero
+ *   b_ptr (n_rows+1), b_idx, b_ent   the terms of every rhs row
+ * nx_set_coefficients, nx_assemble, nx_solve and the getters work as for nx_create.
+ */
+int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
+                 int64_t n_rows, const int32_t* rowptr, const int32_t* col, int32_t n_table,
+                 const int32_t* table_kind, const double* table_val, const int32_t* a_ptr,
+                 const int32_t* a_idx, const int32_t* a_ent, const int32_t* b_ptr,
+                 const int32_t* b_idx, const int32_t* b_ent, nx_network_t** out);
+
 /* Release every device buffer, graph and communicator of the handle. */
 int nx_destroy(nx_network_t* h);
 

@@ -37,6 +37,8 @@ _SIGS = {
     "nx_device_count": (C.c_int, [_pi32]),
     "nx_create": (C.c_int, [_i32, _i32, _i64, _pd, _pi32, _i64, _pi32, _pi32, _pd, _i64,
                             C.POINTER(_h)]),
+    "nx_create_fe": (C.c_int, [_i32, _i32, _i64, _pd, _i64, _pi32, _pi32, _i32, _pi32, _pd,
+                               _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, C.POINTER(_h)]),
     "nx_destroy": (C.c_int, [_h]),
     "nx_dims": (C.c_int, [_h, _pi64, _pi64, _pi64]),
     "nx_set_coefficients": (C.c_int, [_h, _pd, _f64, _f64, _pd]),
@@ -151,6 +153,36 @@ class Handle:
         r, c, z = C.c_int64(), C.c_int64(), C.c_int64()
         check(L.nx_dims(h, C.byref(r), C.byref(c), C.byref(z)))
         self.n_rows, self.n_cols, self.nnz = int(r.value), int(c.value), int(z.value)
+
+    @classmethod
+    def create_fe(cls, device: int, lay) -> "Handle":
+        """Handle for general element degrees from a :class:`layout_fe.FeLayout`
+        (``nx_create_fe``: one rank, CSR pattern and term tables from the host)."""
+        L = lib()
+        self = cls.__new__(cls)
+        self._keep = []
+        edge_x = np.ascontiguousarray(lay.edge_x, dtype=np.float64).reshape(-1)
+        h = C.c_void_p()
+        arrays = [np.ascontiguousarray(a, dtype=np.int32) for a in
+                  (lay.rowptr, lay.col, lay.table_kind, lay.a_ptr, lay.a_idx, lay.a_ent,
+                   lay.b_ptr, lay.b_idx, lay.b_ent)]
+        rp, col, kind, ap, ai, ae, bp, bi, be = arrays
+        tval = np.ascontiguousarray(lay.table_val, dtype=np.float64)
+        check(L.nx_create_fe(int(device), int(lay.N), int(lay.E), _ptr(edge_x, C.c_double),
+                             int(lay.n_rows), _ptr(rp, C.c_int32), _ptr(col, C.c_int32),
+                             int(kind.size), _ptr(kind, C.c_int32), _ptr(tval, C.c_double),
+                             _ptr(ap, C.c_int32), _ptr(ai, C.c_int32), _ptr(ae, C.c_int32),
+                             _ptr(bp, C.c_int32), _ptr(bi, C.c_int32), _ptr(be, C.c_int32),
+                             C.byref(h)))
+        self._h = h
+        self.device = int(device)
+        self.N = int(lay.N)
+        self.n_edges = int(lay.E)
+        self.n_lm = int(lay.lm_nodes.size)
+        r, c, z = C.c_int64(), C.c_int64(), C.c_int64()
+        check(L.nx_dims(h, C.byref(r), C.byref(c), C.byref(z)))
+        self.n_rows, self.n_cols, self.nnz = int(r.value), int(c.value), int(z.value)
+        return self
 
     # ------------------------------------------------------------------ lifecycle
     def close(self) -> None:

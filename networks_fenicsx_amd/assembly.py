@@ -34,7 +34,9 @@ import numpy as np
 from . import _lib
 from .comm import GroupRankComm
 from .fem import Constant, FunctionSpace
+from .element import stable_pair
 from .layout import LocalProblem, build_local_problem
+from .layout_fe import FeLayout, build_fe_layout
 from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
@@ -142,20 +144,23 @@ class HydraulicNetworkAssembler:
 
     Args:
         mesh: the :class:`NetworkMesh`
-        flux_degree: polynomial degree of the flux (only 1 is implemented)
-        pressure_degree: polynomial degree of the pressure (only 0 is implemented)
+        flux_degree: degree k of the equispaced Lagrange flux on every edge (default 1)
+        pressure_degree: 0 for DG0 pressure (default), m >= 1 for continuous P_m (needs
+            k > m); anything but (1, 0) runs on one rank without the tree preconditioner
     """
 
     @timed("nxfx:HydraulicNetworkAssembler:__init__")
     def __init__(self, mesh: NetworkMesh, flux_degree: int = 1, pressure_degree: int = 0):
-        if flux_degree != 1 or pressure_degree != 0:
-            raise NotImplementedError(
-                "the device path implements the reference defaults flux_degree=1, "
-                "pressure_degree=0 (assembly.py:121); other degrees are a later extension"
-            )
         self._network_mesh = mesh
         comm = mesh.comm
         self._rank, self._nranks = comm.rank, comm.size
+        self._degrees = (int(flux_degree), int(pressure_degree))
+        self._a = None
+        self._L = None
+        self._pc: TreePreconditioner | None = None
+        if self._degrees != (1, 0):
+            self._init_general_degrees()
+            return
         src, dst = mesh.edges
         self._local: LocalProblem = build_local_problem(
             mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, self._rank, self._nranks
@@ -165,15 +170,49 @@ class HydraulicNetworkAssembler:
                                    lp.lm_rowptr, lp.lm_col, lp.lm_val, lp.n_ghost)
         if self._nranks > 1:
             self._init_comm()
+        self._edge_ids = lp.edges
         # MINRES preconditioner (tree Schur complement); topology-only, built once
-        self._pc: TreePreconditioner | None = None
         if mesh.N <= 1024:
             jobs = int(os.environ.get("NXHIP_PC_JOBS", "256"))  # swept: 64..1024
             self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=jobs)
         self.set_preconditioner(True)
-        self._a = None
-        self._L = None
         self._make_spaces()
+
+    def _init_general_degrees(self) -> None:
+        """Flux P_k / pressure DG0 or continuous P_m (``layout_fe.py``): one rank, gather
+        assembly (``nx_create_fe``), plain MINRES -- the tree preconditioner is P1/DG0's."""
+        mesh = self._network_mesh
+        k, m = self._degrees
+        if not stable_pair(k, m):
+            raise ValueError(
+                f"flux_degree={k}, pressure_degree={m}: with continuous pressure the flux degree "
+                "must exceed the pressure degree (otherwise the system is singular)")
+        if self._nranks > 1:
+            raise NotImplementedError("flux_degree / pressure_degree other than (1, 0) run on "
+                                      "one rank; the partitioned path is P1/DG0")
+        src, dst = mesh.edges
+        self._local = None
+        self._fe = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, k, m)
+        self._handle = _lib.Handle.create_fe(_device_for_rank(), self._fe)
+        self._edge_ids = np.arange(mesh.num_edges)
+        self._pc_on = False
+        fe = self._fe
+        colors = mesh.edge_colors
+        self._flux_spaces, self._flux_idx = [], []
+        for c in range(mesh.num_edge_colors):
+            edges = np.flatnonzero(colors == c)  # graph.edges() order inside a colour
+            self._flux_spaces.append(
+                FunctionSpace(mesh, "flux", "P", k, False, edges.size * (k * mesh.N + 1), edges, c))
+            self._flux_idx.append(fe.flux_rows[edges].ravel())
+        if m == 0:
+            self._pressure_space = FunctionSpace(mesh, "pressure", "DG", 0, True,
+                                                 fe.p_rows.size, self._edge_ids)
+        else:
+            self._pressure_space = FunctionSpace(mesh, "pressure", "P", m, False,
+                                                 fe.p_rows.size, self._edge_ids)
+        self._lm_space = FunctionSpace(mesh, "multiplier", "DG", 0, True, fe.lm_nodes.size)
+        self._p_idx = fe.p_rows
+        self._lm_idx = fe.lm_rows
 
     def _init_comm(self) -> None:
         comm = self._network_mesh.comm
@@ -213,7 +252,8 @@ class HydraulicNetworkAssembler:
         self._lm_idx = lp.n_edge_dofs + np.arange(lp.lm_nodes.size)
 
     def set_preconditioner(self, enable: bool) -> bool:
-        """Switch the device MINRES between preconditioned and plain; returns the state."""
+        """Switch the device MINRES between preconditioned and plain; returns the state
+        (always plain for general degrees: the tree preconditioner is P1/DG0's)."""
         on = bool(enable) and self._pc is not None
         self._handle.set_preconditioner(self._pc if on else None)
         self._pc_on = on
@@ -246,7 +286,7 @@ class HydraulicNetworkAssembler:
                 element tensors are compiled into the HIP library ahead of time.
         """
         del jit_options, form_compiler_options
-        mesh, lp = self._network_mesh, self._local
+        mesh, edge_ids = self._network_mesh, self._edge_ids
         f_val = _scalar(f, "f", 0.0)
         R_const, R_edge = 1.0, None
         if R is not None:
@@ -255,17 +295,17 @@ class HydraulicNetworkAssembler:
             if Rv.ndim == 0:
                 R_const = float(Rv)
             elif Rv.size == mesh.num_edges:
-                R_edge = np.ascontiguousarray(Rv[lp.edges])
+                R_edge = np.ascontiguousarray(Rv[edge_ids])
             else:
                 raise ValueError("R must be a constant or one value per graph edge")
         pbc = evaluate_nodal(p_bc_ex, mesh.node_coordinates)
         src, dst = mesh.edges
-        s, d = src[lp.edges], dst[lp.edges]
+        s, d = src[edge_ids], dst[edge_ids]
         leaf = np.zeros(mesh.num_nodes, dtype=bool)
         leaf[mesh.boundary_in_nodes] = True
         root = np.zeros(mesh.num_nodes, dtype=bool)
         root[mesh.boundary_out_nodes] = True
-        edge_bc = np.zeros((lp.edges.size, 2), dtype=np.float64)
+        edge_bc = np.zeros((edge_ids.size, 2), dtype=np.float64)
         edge_bc[:, 0] = np.where(root[s], -pbc[s], 0.0)  # - p_bc ds(out_marker)
         edge_bc[:, 1] = np.where(leaf[d], pbc[d], 0.0)  # + p_bc ds(in_marker)
         self._handle.set_coefficients(R_edge, R_const, f_val, edge_bc)
@@ -298,8 +338,19 @@ class HydraulicNetworkAssembler:
         return self._handle
 
     @property
-    def local_problem(self) -> LocalProblem:
+    def local_problem(self) -> LocalProblem | None:
+        """The P1/DG0 rank layout (``layout.py``); None for general degrees."""
         return self._local
+
+    @property
+    def fe_layout(self) -> FeLayout | None:
+        """The general-degree layout (``layout_fe.py``); None for P1/DG0."""
+        return getattr(self, "_fe", None)
+
+    @property
+    def degrees(self) -> tuple[int, int]:
+        """``(flux_degree, pressure_degree)``."""
+        return self._degrees
 
     @property
     def lm_space(self) -> FunctionSpace:

@@ -2465,6 +2465,17 @@ struct nx_network {
   bool beta_p2p = true;
   bool rccl_graph_ok = true;  // capture of the RCCL iteration worked (or was not tried)
   bool last_graph = false;    // the last nx_solve replayed HIP graphs
+  // general element degrees (nx_create_fe): gather-assembly tables, one rank, no
+  // preconditioner
+  bool fe = false;
+  int* fe_kind = nullptr;
+  double* fe_tval = nullptr;
+  int* fe_aptr = nullptr;
+  int* fe_aidx = nullptr;
+  int* fe_aent = nullptr;
+  int* fe_bptr = nullptr;
+  int* fe_bidx = nullptr;
+  int* fe_bent = nullptr;
 };
 
 struct nx_group {
@@ -3023,6 +3034,149 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   return NX_OK;
 }
 
+// ---- general element degrees (HydraulicNetworkAssembler(flux_degree=k, pressure_degree=m),
+// assembly.py:121-146). The host lists every nonzero's and every rhs row's terms in a
+// fixed order (layout_fe.py); k_assemble_fe evaluates them, one thread per nonzero / row.
+// Deterministic: same terms, same order on every call, no atomics.
+namespace {
+
+enum FeKind : int { kFeConst = 0, kFeMass = 1, kFeSource = 2, kFeBc = 3 };
+
+struct FeArgs {
+  const double* edge_x;  // E*6
+  const double* edge_R;  // E
+  const double* edge_bc; // E*2
+  double f;
+  int N;
+  const int* kind;       // term table
+  const double* tval;
+  const int* a_ptr;      // nnz + 1
+  const int* a_idx;
+  const int* a_ent;
+  const int* b_ptr;      // n_rows + 1
+  const int* b_idx;
+  const int* b_ent;
+  int64_t nnz, n_rows;
+  double* val;
+  double* rhs;
+  int lhs, do_rhs;
+};
+
+// length of cell c of edge e, vertices generated like the reference mesh (mesh.py:300-316)
+__device__ __forceinline__ double fe_cell_h(const double* __restrict__ edge_x, int64_t cell, int N) {
+#pragma clang fp contract(off)
+  const int64_t e = cell / N;
+  const int c = (int)(cell - e * N);
+  const double invN = 1.0 / (double)N;
+  double x0[3], x1[3], pa[3], pb[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    x0[d] = edge_x[6 * e + d];
+    x1[d] = edge_x[6 * e + 3 + d];
+  }
+  vertex(x0, x1, c, N, invN, pa);
+  vertex(x0, x1, c + 1, N, invN, pb);
+  const double d0 = pb[0] - pa[0], d1 = pb[1] - pa[1], d2 = pb[2] - pa[2];
+  return sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+}
+
+__device__ __forceinline__ double fe_term(const FeArgs& a, int idx, int ent) {
+#pragma clang fp contract(off)
+  const double v = a.tval[ent];
+  switch (a.kind[ent]) {
+    case kFeMass: return (a.edge_R[idx / a.N] * fe_cell_h(a.edge_x, idx, a.N)) * v;
+    case kFeSource: return (a.f * fe_cell_h(a.edge_x, idx, a.N)) * v;
+    case kFeBc: return a.edge_bc[idx] * v;
+    default: return v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_assemble_fe(FeArgs a) {
+#pragma clang fp contract(off)
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a.lhs && t < a.nnz) {
+    double s = 0.0;
+    for (int c = a.a_ptr[t]; c < a.a_ptr[t + 1]; ++c) s += fe_term(a, a.a_idx[c], a.a_ent[c]);
+    a.val[t] = s;
+  }
+  if (a.do_rhs && t < a.n_rows) {
+    double s = 0.0;
+    for (int c = a.b_ptr[t]; c < a.b_ptr[t + 1]; ++c) s += fe_term(a, a.b_idx[c], a.b_ent[c]);
+    a.rhs[t] = s;
+  }
+}
+
+// terms [ptr[i], ptr[i+1]) of every output i must reference the table and the cell / edge
+// arrays in range
+int check_terms(const char* what, int64_t n_out, const int32_t* ptr, const int32_t* idx,
+                const int32_t* ent, int32_t n_table, const int32_t* kind, int64_t n_cells,
+                int64_t n_edges) {
+  if (ptr[0] != 0) return fail(NX_ERR_ARG, std::string(what) + ": ptr[0] must be 0");
+  for (int64_t i = 0; i < n_out; ++i)
+    if (ptr[i + 1] < ptr[i]) return fail(NX_ERR_ARG, std::string(what) + ": ptr not monotone");
+  for (int64_t t = 0; t < ptr[n_out]; ++t) {
+    if (ent[t] < 0 || ent[t] >= n_table)
+      return fail(NX_ERR_ARG, std::string(what) + ": table entry out of range");
+    const int k = kind[ent[t]];
+    const int64_t lim = (k == kFeMass || k == kFeSource) ? n_cells : k == kFeBc ? 2 * n_edges : 1;
+    if (k != kFeConst && (idx[t] < 0 || idx[t] >= lim))
+      return fail(NX_ERR_ARG, std::string(what) + ": term index out of range");
+  }
+  return NX_OK;
+}
+
+}  // namespace
+
+NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
+                        int64_t n_rows, const int32_t* rowptr, const int32_t* col,
+                        int32_t n_table, const int32_t* table_kind, const double* table_val,
+                        const int32_t* a_ptr, const int32_t* a_idx, const int32_t* a_ent,
+                        const int32_t* b_ptr, const int32_t* b_idx, const int32_t* b_ent,
+                        nx_network_t** out) {
+  if (out == nullptr) return fail(NX_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (N < 1 || n_edges < 1 || n_rows < 1 || n_table < 1)
+    return fail(NX_ERR_ARG, "N, n_edges, n_rows and n_table must be >= 1");
+  if (!edge_x || !rowptr || !col || !table_kind || !table_val || !a_ptr || !a_idx || !a_ent ||
+      !b_ptr || !b_idx || !b_ent)
+    return fail(NX_ERR_ARG, "NULL array");
+  for (int32_t i = 0; i < n_table; ++i)
+    if (table_kind[i] < kFeConst || table_kind[i] > kFeBc)
+      return fail(NX_ERR_ARG, "table_kind must be 0..3");
+  if (rowptr[0] != 0) return fail(NX_ERR_ARG, "rowptr[0] must be 0");
+  const int64_t nnz = rowptr[n_rows];
+  const int64_t n_cells = n_edges * (int64_t)N;
+  if (n_cells >= (int64_t)INT32_MAX) return fail(NX_ERR_ARG, "too many cells for 32-bit terms");
+  CHECK(check_terms("matrix terms", nnz, a_ptr, a_idx, a_ent, n_table, table_kind, n_cells,
+                    n_edges));
+  CHECK(check_terms("rhs terms", n_rows, b_ptr, b_idx, b_ent, n_table, table_kind, n_cells,
+                    n_edges));
+  // the CSR pattern rides on nx_create's host-given row path (no graph edges): it validates
+  // the pattern and allocates the solver; the edge data and term tables are added here
+  std::vector<double> zeros((size_t)std::max<int64_t>(nnz, 1), 0.0);
+  nx_network_t* h = nullptr;
+  CHECK(nx_create(device, N, 0, nullptr, nullptr, n_rows, rowptr, col, zeros.data(), 0, &h));
+  h->fe = true;
+  h->E = n_edges;
+  int rc = NX_OK;
+  if ((rc = upload(&h->edge_x, edge_x, 6 * n_edges, h->stream)) ||
+      (rc = dalloc(&h->edge_R, n_edges)) || (rc = dalloc(&h->edge_bc, 2 * n_edges)) ||
+      (rc = upload(&h->fe_kind, table_kind, (int64_t)n_table, h->stream)) ||
+      (rc = upload(&h->fe_tval, table_val, (int64_t)n_table, h->stream)) ||
+      (rc = upload(&h->fe_aptr, a_ptr, nnz + 1, h->stream)) ||
+      (rc = upload(&h->fe_aidx, a_idx, (int64_t)a_ptr[nnz], h->stream)) ||
+      (rc = upload(&h->fe_aent, a_ent, (int64_t)a_ptr[nnz], h->stream)) ||
+      (rc = upload(&h->fe_bptr, b_ptr, n_rows + 1, h->stream)) ||
+      (rc = upload(&h->fe_bidx, b_idx, (int64_t)b_ptr[n_rows], h->stream)) ||
+      (rc = upload(&h->fe_bent, b_ent, (int64_t)b_ptr[n_rows], h->stream)) ||
+      hipStreamSynchronize(h->stream) != hipSuccess) {
+    nx_destroy(h);
+    return rc ? rc : fail(NX_ERR_HIP, "upload of the element tables failed");
+  }
+  *out = h;
+  return NX_OK;
+}
+
 NX_API int nx_destroy(nx_network_t* h) {
   if (h == nullptr) return NX_OK;
   if (h->group) return fail(NX_ERR_STATE, "destroy the group (nx_group_destroy) first");
@@ -3038,7 +3192,9 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
                   h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
                   h->partA,  h->partB,   h->red,
-                  h->send_idx, h->send_buf, h->gath, h->d_seq};
+                  h->send_idx, h->send_buf, h->gath, h->d_seq,
+                  h->fe_kind, h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent,
+                  h->fe_bptr, h->fe_bidx, h->fe_bent};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -3091,6 +3247,18 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   if (!h->have_coeffs) return fail(NX_ERR_STATE, "nx_set_coefficients must be called first");
   CHECK(set_device(h));
   if (!lhs && !rhs) return NX_OK;
+  if (h->fe) {  // general degrees: one thread per nonzero / rhs row
+    FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->N, h->fe_kind, h->fe_tval,
+             h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
+             h->nnz, h->n_own, h->val, h->rhs, lhs, rhs};
+    hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
+    hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
+                          dim3(kBlock), 0, h->stream, e0, e1, 0, a);
+    HIPCALL(hipGetLastError());
+    if (lhs) h->have_lhs = true;
+    if (rhs) h->have_rhs = true;
+    return NX_OK;
+  }
   // one launch: edge blocks (4 edges each) then the multiplier-row blocks
   const int64_t nlm = std::max(h->nnz_lm, h->B);
   // edges per wave: 4 for N < 16, 2 for N < 32, else 1 (k_assemble, 64-cell chunks)
@@ -3730,6 +3898,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     h->pc = false;
     return NX_OK;
   }
+  if (h->fe)
+    return fail(NX_ERR_STATE, "the tree preconditioner needs the P1/DG0 layout (nx_create)");
   const int N = h->N;
   int variant;
   if (N <= 16) variant = 5;  // 8 lanes x 2 cells: one chain round per job (swept: 16x1 +8%)
@@ -4116,6 +4286,7 @@ NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_
   if (!h) return fail(NX_ERR_ARG, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(NX_ERR_ARG, "bad rank/nranks");
   if (nranks > 1 && h->pc) return fail(NX_ERR_STATE, "set the halo plan before the preconditioner");
+  if (nranks > 1 && h->fe) return fail(NX_ERR_STATE, "general element degrees run on one rank");
   if (n_peers < 0 || (n_peers > 0 && (!peer_rank || !send_off || !recv_off)))
     return fail(NX_ERR_ARG, "bad halo plan");
   CHECK(set_device(h));

@@ -1,0 +1,86 @@
+"""Reference element tensors for general flux / pressure degrees.
+
+The reference builds its spaces with basix (``assembly.py:126-145``): equispaced Lagrange
+P_k for the flux on every edge, DG0 (``pressure_degree == 0``) or continuous Lagrange P_m
+for the pressure. FFCx then generates the element kernels for the forms of
+``compute_forms`` (``assembly.py:253-262``). Every kernel is a constant reference tensor
+times a per-cell factor, so they are tabulated once here, on the host, in closed form:
+each basis function is expanded in monomials with rational coefficients and the
+products are integrated exactly, then rounded once to double. The device gather
+assembly (``k_assemble_fe``) multiplies them by ``R h`` / ``f h`` per cell.
+"""
+
+from __future__ import annotations
+
+from fractions import Fraction
+
+import numpy as np
+
+__all__ = ["lagrange_monomials", "element_tensors", "stable_pair"]
+
+
+def lagrange_monomials(degree: int) -> list[list[Fraction]]:
+    """Exact monomial coefficients ``C[j][n]`` of the equispaced Lagrange basis on [0, 1]:
+    ``phi_j(x) = sum_n C[j][n] x^n`` with ``phi_j(i / degree) = delta_ij`` (rational
+    arithmetic: the tensors below are the correctly rounded exact integrals)."""
+    if degree == 0:
+        return [[Fraction(1)]]
+    nodes = [Fraction(i, degree) for i in range(degree + 1)]
+    out = []
+    for j, xj in enumerate(nodes):
+        coef = [Fraction(1)]  # running product, ascending powers
+        for i, xi in enumerate(nodes):
+            if i == j:
+                continue
+            # multiply by (x - xi) / (xj - xi)
+            d = xj - xi
+            nxt = [Fraction(0)] * (len(coef) + 1)
+            for n, c in enumerate(coef):
+                nxt[n + 1] += c / d
+                nxt[n] -= c * xi / d
+            coef = nxt
+        out.append(coef)
+    return out
+
+
+def _integral_of_products(A, B) -> np.ndarray:
+    """``int_0^1 a_i(x) b_j(x) dx`` for polynomials given by exact monomial coefficients."""
+    out = np.empty((len(A), len(B)))
+    for i, a in enumerate(A):
+        for j, b in enumerate(B):
+            s = Fraction(0)
+            for p, ap in enumerate(a):
+                for q, bq in enumerate(b):
+                    s += ap * bq / (p + q + 1)
+            out[i, j] = float(s)
+    return out
+
+
+def element_tensors(flux_degree: int, pressure_degree: int):
+    """``(Mref, Dref, wref)`` for the unit cell.
+
+    ``Mref[i, j] = int phi_i phi_j`` (flux mass), ``Dref[a, j] = int psi_a phi_j'`` (the
+    divergence form ``phi dq/ds``; ``h`` cancels), ``wref[a] = int psi_a`` (source).
+    Basis functions are ordered by node position along the cell (source side first).
+    """
+    k, m = int(flux_degree), int(pressure_degree)
+    if k < 1 or m < 0:
+        raise ValueError("flux_degree >= 1 and pressure_degree >= 0 required")
+    Cq = lagrange_monomials(k)
+    Cp = lagrange_monomials(m)
+    dCq = [[c * n for n, c in enumerate(row)][1:] for row in Cq]  # derivatives
+    Mref = _integral_of_products(Cq, Cq)
+    Dref = _integral_of_products(Cp, dCq)
+    wref = _integral_of_products(Cp, [[Fraction(1)]])[:, 0]
+    return Mref, Dref, wref
+
+
+def stable_pair(flux_degree: int, pressure_degree: int) -> bool:
+    """Whether the discrete saddle-point system is nonsingular on every graph.
+
+    DG0 pressure is stable with any flux degree. Continuous pressure of degree m needs
+    flux degree k > m: for k <= m the pressure space holds a function orthogonal to every
+    flux derivative (checked numerically on the reference's demo graphs: condition
+    numbers ~1e16-1e18), and the reference's direct solve would fail on it.
+    """
+    return pressure_degree == 0 or flux_degree > pressure_degree

@@ -1,0 +1,208 @@
+"""DoF layout and gather-assembly tables for general element degrees (one rank).
+
+``HydraulicNetworkAssembler(mesh, flux_degree=k, pressure_degree=m)`` (reference
+``assembly.py:121-146``) with ``(k, m) != (1, 0)``. The P1/DG0 default keeps its own layout
+and kernels (``layout.py``, ``k_assemble*``); this module serves every other stable pair.
+
+Device layout (``n_rows`` owned rows, no ghosts):
+
+* every graph edge ``e`` (``graph.edges()`` order) owns ``kN+1`` flux rows (the Lagrange
+  nodes along the edge, source -> target) followed by its edge-interior pressure rows:
+  ``N`` cell values for DG0, else the ``mN-1`` interior nodes of continuous P_m;
+* continuous pressure only: one row per graph node that has an edge (ascending id) --
+  the pressure value shared by every edge meeting there (``assembly.py:135-145``: the
+  pressure space lives on the whole network mesh);
+* one multiplier row per bifurcation (ascending node id).
+
+Pressure rows and their rhs are negated, as in the P1 path, so the matrix is symmetric.
+
+Assembly tables: every nonzero and every rhs entry is a short sum of terms
+``table_val[ent] x factor`` (factor ``R_e h_c``, ``f h_c``, ``edge_bc`` or 1; see
+``include/nxhip.h`` ``nx_create_fe``). The terms are generated cell by cell from the
+reference element tensors (:mod:`element`) and grouped per output in generation order,
+so the device sums them in a fixed order (``k_assemble_fe``).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .element import element_tensors, stable_pair
+
+__all__ = ["FeLayout", "build_fe_layout", "KIND_CONST", "KIND_MASS", "KIND_SOURCE", "KIND_BC"]
+
+KIND_CONST, KIND_MASS, KIND_SOURCE, KIND_BC = 0, 1, 2, 3
+
+
+@dataclass
+class FeLayout:
+    N: int
+    k: int
+    m: int
+    E: int
+    n_rows: int
+    rowptr: np.ndarray  # int32 (n_rows+1,)
+    col: np.ndarray  # int32 (nnz,)
+    table_kind: np.ndarray  # int32
+    table_val: np.ndarray  # f64
+    a_ptr: np.ndarray  # int32 (nnz+1,)
+    a_idx: np.ndarray  # int32
+    a_ent: np.ndarray  # int32
+    b_ptr: np.ndarray  # int32 (n_rows+1,)
+    b_idx: np.ndarray  # int32
+    b_ent: np.ndarray  # int32
+    flux_rows: np.ndarray  # (E, kN+1) device rows of each edge's flux nodes
+    p_rows: np.ndarray  # device row of every pressure DoF, in the function's order
+    p_nodes: np.ndarray  # graph nodes carrying a pressure DoF (m >= 1)
+    lm_nodes: np.ndarray  # bifurcations, ascending
+    lm_rows: np.ndarray
+    edge_x: np.ndarray  # (E, 6) source xyz, target xyz
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.size)
+
+
+def build_fe_layout(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
+                    N: int, k: int, m: int) -> FeLayout:
+    """Layout and term tables for flux degree ``k`` and pressure degree ``m``."""
+    if not stable_pair(k, m):
+        raise ValueError(
+            f"flux_degree={k}, pressure_degree={m}: continuous pressure needs a flux degree "
+            "above the pressure degree, otherwise the system is singular")
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    E = src.size
+    n_nodes = pos.shape[0]
+    nf = k * N + 1
+    npe = N if m == 0 else m * N - 1
+    per = nf + npe
+    base = np.arange(E, dtype=np.int64) * per
+    flux_rows = base[:, None] + np.arange(nf)[None, :]
+    p_nodes = np.flatnonzero(degree > 0) if m >= 1 else np.zeros(0, dtype=np.int64)
+    node_row = np.full(n_nodes, -1, dtype=np.int64)
+    node_row[p_nodes] = E * per + np.arange(p_nodes.size)
+    lm_nodes = np.flatnonzero(degree > 1)
+    lm_row = np.full(n_nodes, -1, dtype=np.int64)
+    lm_row[lm_nodes] = E * per + p_nodes.size + np.arange(lm_nodes.size)
+    n_rows = E * per + p_nodes.size + lm_nodes.size
+
+    c = np.arange(N)
+    qrow = base[:, None, None] + (c[:, None] * k + np.arange(k + 1)[None, :])[None]  # (E,N,k+1)
+    if m == 0:
+        prow = (base[:, None] + nf + c[None, :])[:, :, None]  # (E,N,1)
+    else:
+        ppos = c[:, None] * m + np.arange(m + 1)[None, :]  # (N, m+1) positions 0..mN
+        prow = np.broadcast_to(base[:, None, None] + nf + ppos[None] - 1, (E, N, m + 1)).copy()
+        prow = np.where(ppos[None] == 0, node_row[src][:, None, None], prow)
+        prow = np.where(ppos[None] == m * N, node_row[dst][:, None, None], prow)
+
+    Mref, Dref, wref = element_tensors(k, m)
+    nq, npl = k + 1, wref.size
+    ent_mass = np.arange(nq * nq).reshape(nq, nq)
+    ent_b = nq * nq + np.arange(npl * nq).reshape(npl, nq)
+    ent_plus = nq * nq + npl * nq
+    ent_minus = ent_plus + 1
+    ent_src = ent_minus + 1 + np.arange(npl)
+    ent_bc = int(ent_src[-1]) + 1
+    table_kind = np.concatenate([np.full(nq * nq, KIND_MASS), np.full(npl * nq, KIND_CONST),
+                                 [KIND_CONST, KIND_CONST], np.full(npl, KIND_SOURCE),
+                                 [KIND_BC]]).astype(np.int32)
+    # negated pressure rows: divergence -Dref (row p, col q); gradient -Dref^T (row q, col p)
+    table_val = np.concatenate([Mref.ravel(), -Dref.ravel(), [1.0, -1.0], -wref, [1.0]])
+
+    cell = np.arange(E, dtype=np.int64)[:, None] * N + c[None, :]  # (E, N)
+    rows, cols, idx, ent = [], [], [], []
+    for i in range(nq):
+        for j in range(nq):
+            rows.append(qrow[:, :, i]); cols.append(qrow[:, :, j])
+            idx.append(cell); ent.append(np.full((E, N), ent_mass[i, j]))
+    for a in range(npl):
+        for j in range(nq):
+            rows.append(prow[:, :, a]); cols.append(qrow[:, :, j])
+            idx.append(cell); ent.append(np.full((E, N), ent_b[a, j]))
+            rows.append(qrow[:, :, j]); cols.append(prow[:, :, a])
+            idx.append(cell); ent.append(np.full((E, N), ent_b[a, j]))
+    # junctions (assembly.py:268-277): +1 at in-edge ends, -1 at out-edge starts, both blocks
+    e_in = np.flatnonzero(lm_row[dst] >= 0)
+    e_out = np.flatnonzero(lm_row[src] >= 0)
+    for e_set, lam, qr, en in ((e_in, lm_row[dst[e_in]], flux_rows[e_in, -1], ent_plus),
+                               (e_out, lm_row[src[e_out]], flux_rows[e_out, 0], ent_minus)):
+        z = np.zeros(e_set.size, dtype=np.int64)
+        rows += [lam, qr]; cols += [qr, lam]
+        idx += [z, z]; ent += [np.full(e_set.size, en), np.full(e_set.size, en)]
+    R = np.concatenate([np.ravel(x) for x in rows])
+    C = np.concatenate([np.ravel(x) for x in cols])
+    Ix = np.concatenate([np.ravel(x) for x in idx])
+    T = np.concatenate([np.ravel(x) for x in ent])
+    order = np.lexsort((np.arange(R.size), C, R))  # by row, column, then generation order
+    R, C, Ix, T = R[order], C[order], Ix[order], T[order]
+    new = np.ones(R.size, dtype=bool)
+    new[1:] = (R[1:] != R[:-1]) | (C[1:] != C[:-1])
+    starts = np.flatnonzero(new)
+    a_ptr = np.append(starts, R.size)
+    col = C[starts]
+    rowptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(np.bincount(R[starts], minlength=n_rows), out=rowptr[1:])
+
+    # rhs: source on pressure rows, boundary data at both flux ends of every edge
+    e_ids = np.arange(E, dtype=np.int64)
+    br = [prow[:, :, a] for a in range(npl)] + [flux_rows[:, 0], flux_rows[:, -1]]
+    bi = [cell for _ in range(npl)] + [2 * e_ids, 2 * e_ids + 1]
+    be = [np.full((E, N), ent_src[a]) for a in range(npl)] + [np.full(E, ent_bc)] * 2
+    BR = np.concatenate([np.ravel(x) for x in br])
+    BI = np.concatenate([np.ravel(x) for x in bi])
+    BE = np.concatenate([np.ravel(x) for x in be])
+    border = np.argsort(BR, kind="stable")
+    b_ptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(np.bincount(BR, minlength=n_rows), out=b_ptr[1:])
+
+    if m == 0:
+        p_rows = (base[:, None] + nf + c[None, :]).ravel()
+    else:
+        p_rows = np.concatenate([node_row[p_nodes],
+                                 (base[:, None] + nf + np.arange(m * N - 1)[None, :]).ravel()])
+    pos3 = np.zeros((n_nodes, 3))
+    pos3[:, : pos.shape[1]] = pos
+    edge_x = np.concatenate([pos3[src], pos3[dst]], axis=1)
+    if max(a_ptr[-1], rowptr[-1], n_rows) >= np.iinfo(np.int32).max:
+        raise ValueError("problem too large for 32-bit CSR indices")
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+    return FeLayout(N, k, m, E, int(n_rows), i32(rowptr), i32(col), table_kind,
+                    np.ascontiguousarray(table_val), i32(a_ptr), i32(Ix), i32(T), i32(b_ptr),
+                    i32(BI[border]), i32(BE[border]), flux_rows, p_rows, p_nodes, lm_nodes,
+                    lm_row[lm_nodes], edge_x)
+
+
+def evaluate_terms(lay: FeLayout, R_edge: np.ndarray, f: float, edge_bc: np.ndarray,
+                   cell_h: np.ndarray):
+    """Host evaluation of the term tables (what ``k_assemble_fe`` computes), for tests and
+    debugging: returns ``(val, rhs)``. ``cell_h`` is ``(E, N)``."""
+    h = np.asarray(cell_h, dtype=np.float64).ravel()
+    Rc = np.repeat(np.asarray(R_edge, dtype=np.float64), lay.N)
+    bc = np.asarray(edge_bc, dtype=np.float64).ravel()
+
+    def term(i, e):
+        kind, v = lay.table_kind[e], lay.table_val[e]
+        if kind == KIND_MASS:
+            return (Rc[i] * h[i]) * v
+        if kind == KIND_SOURCE:
+            return (f * h[i]) * v
+        if kind == KIND_BC:
+            return bc[i] * v
+        return v
+
+    kind = lay.table_kind[lay.a_ent]
+    v = lay.table_val[lay.a_ent]
+    tv = np.where(kind == KIND_MASS, (Rc[np.where(kind == KIND_MASS, lay.a_idx, 0)]
+                                      * h[np.where(kind == KIND_MASS, lay.a_idx, 0)]) * v, v)
+    val = np.add.reduceat(tv, lay.a_ptr[:-1]) if tv.size else np.zeros(0)
+    rhs = np.zeros(lay.n_rows)
+    for r in range(lay.n_rows):
+        s = 0.0
+        for t in range(lay.b_ptr[r], lay.b_ptr[r + 1]):
+            s += term(lay.b_idx[t], lay.b_ent[t])
+        rhs[r] = s
+    return val, rhs

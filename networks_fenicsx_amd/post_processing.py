@@ -2,9 +2,9 @@
 
 Mirrors ``src/networks_fenicsx/post_processing.py``:
 
-* :func:`extract_global_flux` (reference ``:19-52``): the per-colour P1 fluxes gathered
-  into one discontinuous P1 ("DG1") field on the whole network, two values per cell
-  (its source-side and target-side vertex values), cells edge-major;
+* :func:`extract_global_flux` (reference ``:19-52``): the per-colour P_k fluxes gathered
+  into one discontinuous P_k ("DG_k") field on the whole network, ``k+1`` values per cell
+  (its nodes, source side first), cells edge-major;
 * :func:`export_functions` / :func:`export_submeshes` (reference ``:55-97``): the
   reference writes ADIOS2 ``.bp`` / XDMF files. ADIOS2 and DOLFINx IO are not
   available here; these write the same data as ``.npz`` archives (one per function /
@@ -24,32 +24,39 @@ __all__ = ["extract_global_flux", "export_functions", "export_submeshes", "integ
 
 
 def extract_global_flux(graph_mesh: NetworkMesh, functions: list[Function]) -> Function:
-    """Global DG1 flux on the network mesh from ``[flux_0, ..., flux_{M-1}, p, lm]``."""
+    """Global DG_k flux on the network mesh from ``[flux_0, ..., flux_{M-1}, p, lm]``.
+
+    ``k`` is the flux degree (reference ``:31-33``); every cell gets the ``k+1`` node values
+    of its edge's flux (source side first), cells edge-major."""
     flux_functions = functions[:-2]
     N = graph_mesh.N
     if not flux_functions:
         raise ValueError("no flux functions given")
-    # edges present in this rank's functions, and their values per vertex
+    degree = flux_functions[0].function_space.element.basix_element.degree
+    # edges present in this rank's functions, and their values per node
     edges = np.concatenate([f.function_space.edges for f in flux_functions])
-    vals = np.concatenate([f.x.array.reshape(-1, N + 1) for f in flux_functions])
+    vals = np.concatenate([f.x.array.reshape(-1, degree * N + 1) for f in flux_functions])
     order = np.argsort(edges, kind="stable")
     edges, vals = edges[order], vals[order]
-    degree = flux_functions[0].function_space.element.basix_element.degree
-    V = FunctionSpace(graph_mesh, "global_flux", "DG", degree, True, edges.size * 2 * N, edges)
+    V = FunctionSpace(graph_mesh, "global_flux", "DG", degree, True,
+                      edges.size * (degree + 1) * N, edges)
     g = Function(V, name="Global_Flux")
-    dg = np.empty((edges.size, N, 2), dtype=np.float64)
-    dg[:, :, 0] = vals[:, :-1]
-    dg[:, :, 1] = vals[:, 1:]
-    g.x.array[:] = dg.ravel()
+    nodes = np.arange(N)[:, None] * degree + np.arange(degree + 1)[None, :]  # (N, k+1)
+    g.x.array[:] = vals[:, nodes].ravel()
     return g
 
 
 def integrate_dg1(graph_mesh: NetworkMesh, g: Function) -> tuple[float, float]:
-    """``(integral of g, length)`` over the cells held in ``g`` (exact for DG1)."""
+    """``(integral of g, length)`` over the cells held in ``g`` (exact for the DG_k field
+    :func:`extract_global_flux` returns; the name is kept from the P1 default)."""
+    from .element import element_tensors
+
     N = graph_mesh.N
+    degree = g.function_space.element.basix_element.degree
+    weights = element_tensors(1, degree)[2]  # int_0^1 of the degree-k Lagrange basis
     h = graph_mesh.cell_lengths().reshape(-1, N)[g.function_space.edges]
-    v = g.x.array.reshape(-1, N, 2)
-    return float(np.sum(h * 0.5 * (v[:, :, 0] + v[:, :, 1]))), float(np.sum(h))
+    v = g.x.array.reshape(-1, N, degree + 1)
+    return float(np.sum(h * (v @ weights))), float(np.sum(h))
 
 
 def export_functions(functions: list[Function], outpath: Path | str) -> None:

@@ -15,8 +15,9 @@ PETSc options understood (with or without the options prefix):
 ``ksp_max_it``                    iteration cap (default 50000)
 ``ksp_error_if_not_converged``    raise :class:`NxNotConverged` (default True)
 ``ksp_monitor``                   print iterations / residual after each solve
-``ksp_check_every``               iterations per host convergence check (default 4: the exact
-                                  preconditioner converges in 3, + 1 launch for the last update)
+``ksp_check_every``               iterations per host convergence check (default 4 with the
+                                  preconditioner -- the exact one converges in 3, + 1 launch for
+                                  the last update -- and 32 for plain MINRES)
 
 ``pc_type``                       ``"none"`` runs plain MINRES; anything else (the reference's
                                   default ``"lu"`` included) uses the tree Schur-complement
@@ -111,7 +112,8 @@ class Solver:
             clean[key.lstrip("-")] = v
         self._rtol = float(clean.get("ksp_rtol", 1e-12))
         self._maxit = int(clean.get("ksp_max_it", 50000))
-        self._check_every = int(clean.get("ksp_check_every", 4))
+        ce = clean.get("ksp_check_every")
+        self._check_every = None if ce is None else int(ce)
         self._raise = _truthy(clean.get("ksp_error_if_not_converged", True))
         self._monitor = "ksp_monitor" in clean and _truthy(clean["ksp_monitor"])
         self._ksp = KSPInfo(petsc_options_prefix, clean)
@@ -158,7 +160,8 @@ class Solver:
             self.assembler.set_preconditioner(self._pc)
         if self.assembler.preconditioned and h.pc_exact() != self._pc_exact:
             h.set_pc_exact(self._pc_exact)
-        it, relres, conv = h.solve(self._rtol, self._maxit, self._check_every)
+        ce = self._check_every or (4 if self.assembler.preconditioned else 32)
+        it, relres, conv = h.solve(self._rtol, self._maxit, ce)
         self._ksp.iterations, self._ksp.residual_estimate, self._ksp.converged = it, relres, conv
         if self._monitor:
             print(f"  MINRES: {it} iterations, residual estimate {relres:.3e}"

@@ -1,0 +1,130 @@
+"""General element degrees on the GPU: ``k_assemble_fe`` + plain MINRES against the oracle.
+
+Tolerances:
+* CSR pattern: identical to the host layout; values and rhs bit-exact against the host
+  evaluation of the same term tables (same cell-length formula, same summation order);
+* values against the oracle's forms: <= 1e-14 relative (element tensors integrated two
+  ways: exact rationals vs Gauss-Legendre);
+* solution: <= 1e-10 relative 2-norm against the oracle's direct solve and, for
+  continuous pressure (m >= 1), against the analytic resistor-network answer.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from cases import CASES
+from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh, Solver
+from networks_fenicsx_amd.layout_fe import evaluate_terms
+from networks_fenicsx_amd.post_processing import extract_global_flux, integrate_dg1
+from oracle import nx_oracle as O
+from oracle import nx_oracle_fe as OF
+
+pytestmark = pytest.mark.gpu
+
+SOL_TOL = 1e-10
+PAIRS = [(2, 0), (3, 0), (2, 1), (3, 1), (3, 2)]
+
+
+def _setup(case, km, f=None, R=None):
+    make, N, strategy, pbc = CASES[case]
+    mesh = NetworkMesh(make(), N=N, color_strategy=strategy)
+    asm = HydraulicNetworkAssembler(mesh, flux_degree=km[0], pressure_degree=km[1])
+    asm.compute_forms(p_bc_ex=pbc, f=f, R=R)
+    src, dst = mesh.edges
+    F = OF.build_problem_fe(mesh.node_coordinates, src, dst, N, *km, mesh.edge_colors)
+    A, b = OF.assemble_reference_fe(F, pbc, f=0.0 if f is None else f,
+                                    R=1.0 if R is None else R)
+    return mesh, asm, F, A, b, pbc
+
+
+def _edge_bc(F, pbc):
+    pb = O._nodal(pbc, F.base.pos3)
+    src, dst = F.base.src, F.base.dst
+    leaf = np.zeros(pb.size, dtype=bool)
+    leaf[F.base.leaf_in] = True
+    root = np.zeros(pb.size, dtype=bool)
+    root[F.base.root_out] = True
+    bc = np.zeros((src.size, 2))
+    bc[:, 0] = np.where(root[src], -pb[src], 0.0)
+    bc[:, 1] = np.where(leaf[dst], pb[dst], 0.0)
+    return bc
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "edge_info_N10", "depth6_N40"])
+@pytest.mark.parametrize("km", PAIRS)
+def test_fe_csr_and_rhs(case, km):
+    R = 1.0 + np.arange(len(CASES[case][0]().edges())) % 3
+    mesh, asm, F, A, b, pbc = _setup(case, km, f=0.7, R=R)
+    asm.assemble()
+    lay = asm.fe_layout
+    rp, col, val = asm.handle.csr()
+    np.testing.assert_array_equal(rp, lay.rowptr)
+    np.testing.assert_array_equal(col, lay.col)
+    _, h = O.cell_geometry(F.base)
+    hv, hr = evaluate_terms(lay, R, 0.7, _edge_bc(F, pbc), h)
+    np.testing.assert_array_equal(val, hv)  # bit-exact: same terms, same order
+    np.testing.assert_array_equal(asm.handle.rhs(), hr)
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "edge_info_N10", "depth6_N40",
+                                  "arterial5_N40"])
+@pytest.mark.parametrize("km", PAIRS)
+def test_fe_solution(case, km):
+    mesh, asm, F, A, b, pbc = _setup(case, km)
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.converged and not asm.preconditioned
+    x_ref = O.solve_reference(A, b)
+    # functions in the oracle's block order: flux per colour, pressure, multipliers
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    if km[1] >= 1:
+        xa = OF.resistor_network_solution_fe(F, pbc)
+        assert np.linalg.norm(got - xa) / np.linalg.norm(xa) <= SOL_TOL
+    assert solver.true_residual() < 1e-9
+
+
+def test_fe_source_and_resistance():
+    case, km = "double_Y_N5", (2, 1)
+    R = np.array([1.0, 2.5, 0.5, 3.0, 1.5, 2.0, 1.0])[: len(CASES[case][0]().edges())]
+    mesh, asm, F, A, b, pbc = _setup(case, km, f=0.3, R=R)
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    x_ref = O.solve_reference(A, b)
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
+@pytest.mark.parametrize("km", [(2, 0), (3, 1)])
+def test_fe_global_flux(km):
+    """DG_k global flux: q is constant per edge (f = 0), so its integral is sum q_e L_e."""
+    mesh, asm, F, A, b, pbc = _setup("depth6_N40", km)
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    g = extract_global_flux(mesh, sol)
+    k = km[0]
+    assert g.function_space.element.basix_element.degree == k
+    assert g.x.array.size == mesh.num_edges * mesh.N * (k + 1)
+    total, length = integrate_dg1(mesh, g)
+    x1 = O.resistor_network_solution(O.build_problem(mesh.node_coordinates, *mesh.edges,
+                                                     mesh.N, mesh.edge_colors), pbc)
+    P1 = O.build_problem(mesh.node_coordinates, *mesh.edges, mesh.N, mesh.edge_colors)
+    _, h = O.cell_geometry(P1)
+    expect = float(np.sum(x1[P1.flux_offset] * h.sum(axis=1)))
+    assert abs(total - expect) <= 1e-9 * abs(expect)
+    assert abs(length - h.sum()) <= 1e-12 * h.sum()
+
+
+def test_fe_reassemble_idempotent():
+    mesh, asm, F, A, b, pbc = _setup("edge_info_N10", (3, 1))
+    asm.assemble()
+    v1 = asm.handle.csr()[2].copy()
+    r1 = asm.handle.rhs().copy()
+    asm.assemble()
+    np.testing.assert_array_equal(asm.handle.csr()[2], v1)
+    np.testing.assert_array_equal(asm.handle.rhs(), r1)
