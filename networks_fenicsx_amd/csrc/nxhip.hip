@@ -1424,50 +1424,90 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sAtop[MULTI ? kCapT : 1];  // fused k_pc_cpart (last workgroup)
   double c2 = 0.0;
-  if (mode == 0) {
-    if (st->done) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
-      return;
-    }
-    if (!(MULTI && pa.lin)) {  // linear form: alpha is not known yet (k_pc_coarse)
-      const double alfa = MULTI ? red[0] : block_allsum<kPcThreads>(partA, nA);
-      c2 = alfa / st->beta;
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->alfa = alfa;
-        st->nb += 1;
-      }
-    }
+  if (mode == 0 && st->done) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
+    return;
   }
   const bool upd = mode == 0 && !(MULTI && pa.lin);
+  const int job = blockIdx.x;
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  // prefetch, independent of alpha (its re-reduction below hides the latency): the first
+  // chain pass's lane setup and values, and this thread's junction slot of phase A
+  ChainLane<W, CPL> ch;
+  ch.setup(pa, c0 + seg, c0 + seg < c1);
+  double vc[CPL], wc[CPL], vq[CPL], wq[CPL], vN = 0.0, wN = 0.0;
+  auto load_lane = [&]() {
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      vc[t] = ch.valid[t] ? y[ch.dof_c[t]] : 0.0;
+      wc[t] = upd && ch.valid[t] ? r2[ch.dof_c[t]] : 0.0;
+      vq[t] = upd && ch.valid[t] ? y[ch.dof_q[t]] : 0.0;
+      wq[t] = upd && ch.valid[t] ? r2[ch.dof_q[t]] : 0.0;
+    }
+    vN = upd && ch.has_last ? y[ch.dof_qN] : 0.0;
+    wN = upd && ch.has_last ? r2[ch.dof_qN] : 0.0;
+  };
+  load_lane();
+  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
+  const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
+  const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
+  const bool fac = pa.factored && mode == 0;
+  constexpr int kPre = 4;  // down-chain entries of the slot prefetched
+  int p_lam = 0, p_pcn = -1, p_o0 = 0, p_o1 = 0, p_dc[kPre], p_lo[kPre];
+  double p_y = 0.0, p_r = 0.0, p_kap[kPre];
+  if ((int)threadIdx.x < js1 - js0) {
+    const int j = js0 + threadIdx.x;
+    p_lam = pa.slot_lam[j];
+    p_pcn = pa.slot_pchain[j];
+    p_o0 = pa.slot_dc_off[j];
+    p_o1 = pa.slot_dc_off[j + 1];
+    p_y = y[p_lam];
+    p_r = upd ? r2[p_lam] : 0.0;
+#pragma unroll
+    for (int q = 0; q < kPre; ++q) {
+      const bool in = p_o0 + q < p_o1;
+      p_dc[q] = in ? pa.slot_dc[p_o0 + q] : 0;
+      p_lo[q] = in ? pa.dc_lo[p_o0 + q] : -1;
+      p_kap[q] = in && fac ? pa.dc_kappa[p_o0 + q] : 0.0;
+    }
+  }
+  if (mode == 0 && !(MULTI && pa.lin)) {  // linear form: alpha is not known yet (k_pc_coarse)
+    const double alfa = MULTI ? red[0] : block_allsum<kPcThreads>(partA, nA);
+    c2 = alfa / st->beta;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->alfa = alfa;
+      st->nb += 1;
+    }
+  }
   if (MULTI && pa.lin && mode == 0 && blockIdx.x == 0) {  // this rank's alpha partial sum
     const double a = block_allsum<kPcThreads>(partA, nA);
     if (threadIdx.x == 0) const_cast<double*>(pa.xalpha)[0] = a;
   }
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;  // write the top inputs u
   NX_PHASE_START(16);
-  const int job = blockIdx.x;
-  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
-  constexpr int G = kPcThreads / W;
-  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
   for (int cb = c0; cb < c1; cb += G) {
     const int c = cb + seg;
     const bool active = c < c1;
-    ChainLane<W, CPL> ch;
-    ch.setup(pa, c, active);
+    if (cb != c0) {  // more chains than one pass: set up and load here
+      ch.setup(pa, c, active);
+      load_lane();
+    }
     double sr = 0.0, srd = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
       if (!ch.valid[t]) continue;
-      double rc = y[ch.dof_c[t]];
+      double rc = vc[t];
       if (upd) {
-        rc -= c2 * r2[ch.dof_c[t]];
+        rc -= c2 * wc[t];
         y[ch.dof_c[t]] = rc;
-        y[ch.dof_q[t]] -= c2 * r2[ch.dof_q[t]];
+        y[ch.dof_q[t]] = vq[t] - c2 * wq[t];
       }
       sr += rc;
       srd += rc * ch.D[t];
     }
-    if (upd && ch.has_last) y[ch.dof_qN] -= c2 * r2[ch.dof_qN];
+    if (upd && ch.has_last) y[ch.dof_qN] = vN - c2 * wN;
     sr = seg_sum<W>(sr);
     srd = seg_sum<W>(srd);
     if (active && l == 0) {
@@ -1496,35 +1536,44 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       pa.u[pa.slot_uy[t - ts0]] = yl;
     }
   }
-  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
   if (lv1 > lv0) {  // the job's junction levels (block-uniform)
-  const int js0 = pa.lvl_slot_off[lv0], js1 = pa.lvl_slot_off[lv1];
   const int ns = js1 - js0;
   const int dc0 = pa.slot_dc_off[js0];
   // factored: D is fixed by the assembly -> J += kappa J_child, no divisions, no D stores
-  const bool fac = pa.factored && mode == 0;
   __syncthreads();
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {  // phase A
     const int j = js0 + sl;
-    const int lam = pa.slot_lam[j];
-    double yl = y[lam];
+    const bool pre = sl == (int)threadIdx.x;  // the prefetched slot
+    const int lam = pre ? p_lam : pa.slot_lam[j];
+    double yl = pre ? p_y : y[lam];
     if (upd) {
-      yl -= c2 * r2[lam];
+      yl -= c2 * (pre ? p_r : r2[lam]);
       y[lam] = yl;
     }
-    const int pcn = pa.slot_pchain[j];
+    const int pcn = pre ? p_pcn : pa.slot_pchain[j];
     double D0 = pcn >= 0 ? 1.0 / sT[pcn - c0] : 0.0;
     double J0 = yl + (pcn >= 0 ? sIb[pcn - c0] : 0.0);
-    const int o0 = pa.slot_dc_off[j], o1 = pa.slot_dc_off[j + 1];
+    const int o0 = pre ? p_o0 : pa.slot_dc_off[j], o1 = pre ? p_o1 : pa.slot_dc_off[j + 1];
     sOff[sl] = o0 - dc0;
     for (int i = o0; i < o1; ++i) {
-      const int cl = pa.slot_dc[i] - c0;
-      const int lo = pa.dc_lo[i];
+      const int q = i - o0;
+      const bool pq = pre && q < kPre;
+      int dcq = 0, loq = -1;
+      double kq = 0.0;
+#pragma unroll
+      for (int r = 0; r < kPre; ++r)
+        if (r == q) {
+          dcq = p_dc[r];
+          loq = p_lo[r];
+          kq = p_kap[r];
+        }
+      const int cl = (pq ? dcq : pa.slot_dc[i]) - c0;
+      const int lo = pq ? loq : pa.dc_lo[i];
       const double g = 1.0 / sT[cl];
       J0 += sIt[cl];
       if (lo >= 0) {
         sChild[i - dc0] = lo - js0;
-        sG[i - dc0] = fac ? pa.dc_kappa[i] : g;
+        sG[i - dc0] = fac ? (pq ? kq : pa.dc_kappa[i]) : g;
       } else {
         sChild[i - dc0] = -1;
         D0 += g;
@@ -1808,6 +1857,36 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
   const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
   const int ns = js1 - js0;
+  // prefetch, independent of every z (the dense top and the level sweep below hide the
+  // latency): the first chain pass's lane setup and r values, this thread's junction slot
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W;
+  ChainLane<W, CPL> ch;
+  ch.setup(pa, c0 + seg, c0 + seg < c1);
+  double vc[CPL], vq[CPL], vN = 0.0;
+  int ch_up = -1, ch_lo = -1;
+  auto load_lane = [&](int c, bool active) {
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      vc[t] = ch.valid[t] ? y[ch.dof_c[t]] : 0.0;
+      vq[t] = ch.valid[t] ? y[ch.dof_q[t]] : 0.0;
+    }
+    vN = ch.has_last ? y[ch.dof_qN] : 0.0;
+    ch_up = active ? pa.chain_up[c] : -1;
+    ch_lo = active ? pa.chain_lo[c] : -1;
+  };
+  load_lane(c0 + seg, c0 + seg < c1);
+  int p_par = -1, p_lam = 0;
+  double p_A = 0.0, p_B = 0.0, p_y = 0.0;
+  if ((int)threadIdx.x < ns) {
+    const int j = js0 + threadIdx.x;
+    p_par = pa.slot_parent[j];
+    p_A = pa.slot_A[j];
+    p_B = pa.slot_B[j];
+    p_lam = pa.slot_lam[j];
+    p_y = y[p_lam];
+  }
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
   // several ranks, fused: every workgroup solves the coarse forest (k_pc_coarse's job)
@@ -1883,10 +1962,11 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   // phase A: every slot's A, B, parent (local index, or the parent's value for the root)
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
     const int j = js0 + sl;
-    const int p = pa.slot_parent[j];
+    const bool pre = sl == (int)threadIdx.x;  // the prefetched slot
+    const int p = pre ? p_par : pa.slot_parent[j];
     const bool local = p >= js0 && p < js1;
-    sA[sl] = pa.slot_A[j];
-    sB[sl] = pa.slot_B[j];
+    sA[sl] = pre ? p_A : pa.slot_A[j];
+    sB[sl] = pre ? p_B : pa.slot_B[j];
     sP[sl] = local ? p - js0 : -1;
     sZ[sl] = (!local && p >= 0) ? outside(p) : 0.0;  // an outside parent is a top slot
   }
@@ -1905,8 +1985,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     __syncthreads();
   }
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
-    const int lam = pa.slot_lam[js0 + sl];
-    double zl = sZ[sl], yl = y[lam];
+    const bool pre = sl == (int)threadIdx.x;
+    const int lam = pre ? p_lam : pa.slot_lam[js0 + sl];
+    double zl = sZ[sl], yl = pre ? p_y : y[lam];
     if (lin) {
       zl -= c2 * z[lam];
       yl -= c2 * r2[lam];
@@ -1916,15 +1997,14 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     part += yl * zl;
   }
   NX_PHASE(50);
-  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
-  constexpr int G = kPcThreads / W;
-  const int seg = threadIdx.x / W;
   for (int cb = c0; cb < c1; cb += G) {
     const int c = cb + seg;
     const bool active = c < c1;
-    ChainLane<W, CPL> ch;
-    ch.setup(pa, c, active);
-    const int up = active ? pa.chain_up[c] : -1, lo = active ? pa.chain_lo[c] : -1;
+    if (cb != c0) {  // more chains than one pass: set up and load here
+      ch.setup(pa, c, active);
+      load_lane(c, active);
+    }
+    const int up = ch_up, lo = ch_lo;
     const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : outside(up);
     const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : outside(lo);
     const double T = ch.T, iT = 1.0 / T;
@@ -1932,7 +2012,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     double sa = 0.0, sb = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
-      rc[t] = ch.valid[t] ? y[ch.dof_c[t]] : 0.0;
+      rc[t] = vc[t];
       a[t] = (T - ch.D[t]) * rc[t];
       b[t] = ch.D[t] * rc[t];
       sa += a[t];
@@ -1962,7 +2042,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       part += rk * zk;
       // flux: P^{-1} r' = P^{-1} y - c2 P^{-1} r2 and z_old = P^{-1} r2, so the block is
       // applied to r' directly (z_q needs no separate linear-form correction)
-      double r = y[ch.dof_q[t]];
+      double r = vq[t];
       if (lin) {
         r -= c2 * r2[ch.dof_q[t]];
         y[ch.dof_q[t]] = r;
@@ -1971,7 +2051,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     }
     double rqN = 0.0;
     if (ch.has_last) {
-      rqN = y[ch.dof_qN];
+      rqN = vN;
       if (lin) {
         rqN -= c2 * r2[ch.dof_qN];
         y[ch.dof_qN] = rqN;
