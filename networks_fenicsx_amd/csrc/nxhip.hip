@@ -610,11 +610,16 @@ __device__ __forceinline__ Rot mr_rotate(MrState& s, double b2) {
 
 // Sum of n values in a fixed order, identical in every block; returned to all threads.
 template <int BS = kBlock>
-__device__ __forceinline__ double block_allsum(const double* __restrict__ p, int n) {
+__device__ __forceinline__ double block_partial(const double* __restrict__ p, int n) {
+  double v = 0.0;  // this thread's share, in the fixed order every block uses
+  for (int i = threadIdx.x; i < n; i += BS) v += p[i];
+  return v;
+}
+
+template <int BS = kBlock>
+__device__ __forceinline__ double block_allsum_v(double v) {
   __shared__ double s_w[BS / 64];
   __shared__ double s_tot;
-  double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += BS) v += p[i];
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -626,6 +631,11 @@ __device__ __forceinline__ double block_allsum(const double* __restrict__ p, int
   }
   __syncthreads();
   return s_tot;
+}
+
+template <int BS = kBlock>
+__device__ __forceinline__ double block_allsum(const double* __restrict__ p, int n) {
+  return block_allsum_v<BS>(block_partial<BS>(p, n));
 }
 
 // Block sum of one value per thread -> *out (thread 0). Block size BS.
@@ -713,6 +723,8 @@ __global__ __launch_bounds__(kBlock, 8) void k_mr_a(Csr A, MrVecs v, const MrSta
                                                  const double* __restrict__ red,
                                                  double* __restrict__ partA, int chunksA,
                                                  MrInit ini) {
+  // the partials of beta^2 are loaded with the state, not after it (one round trip less)
+  const double pB = MULTI || ini.on ? 0.0 : block_partial(partB, nB);
   if (!ini.on && sin->done) {
     if (ini.mark && blockIdx.x == 0 && threadIdx.x == 0) mr_publish(*sin, ini);
     return;
@@ -722,7 +734,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_mr_a(Csr A, MrVecs v, const MrSta
   Rot rot{0.0, 0.0, 0.0, 0.0};
   const bool upd = s.nb > 0;  // a Lanczos step is waiting for its rotation
   const int it0 = s.it;
-  if (upd) rot = mr_rotate(s, MULTI ? red[1] : block_allsum(partB, nB));
+  if (upd) rot = mr_rotate(s, MULTI ? red[1] : block_allsum_v(pB));
   NX_PHASE(1);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *sout = s;
@@ -1424,6 +1436,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sAtop[MULTI ? kCapT : 1];  // fused k_pc_cpart (last workgroup)
   double c2 = 0.0;
+  // alpha's partials first: their loads overlap the state read and the prefetch below
+  const double pA = mode == 0 && !MULTI ? block_partial<kPcThreads>(partA, nA) : 0.0;
   if (mode == 0 && st->done) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
     return;
@@ -1474,7 +1488,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     }
   }
   if (mode == 0 && !(MULTI && pa.lin)) {  // linear form: alpha is not known yet (k_pc_coarse)
-    const double alfa = MULTI ? red[0] : block_allsum<kPcThreads>(partA, nA);
+    const double alfa = MULTI ? red[0] : block_allsum_v<kPcThreads>(pA);
     c2 = alfa / st->beta;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       st->alfa = alfa;
