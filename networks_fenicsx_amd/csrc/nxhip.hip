@@ -1438,10 +1438,6 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   double c2 = 0.0;
   // alpha's partials first: their loads overlap the state read and the prefetch below
   const double pA = mode == 0 && !MULTI ? block_partial<kPcThreads>(partA, nA) : 0.0;
-  if (mode == 0 && st->done) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
-    return;
-  }
   const bool upd = mode == 0 && !(MULTI && pa.lin);
   const int job = blockIdx.x;
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
@@ -1486,6 +1482,12 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       p_lo[q] = in ? pa.dc_lo[p_o0 + q] : -1;
       p_kap[q] = in && fac ? pa.dc_kappa[p_o0 + q] : 0.0;
     }
+  }
+  // the stop test after the prefetch: its load no longer delays the loads above (they are
+  // harmless when the solve has stopped; nothing is written before this point)
+  if (mode == 0 && st->done) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *other = *st;  // see k_mr_b
+    return;
   }
   if (mode == 0 && !(MULTI && pa.lin)) {  // linear form: alpha is not known yet (k_pc_coarse)
     const double alfa = MULTI ? red[0] : block_allsum_v<kPcThreads>(pA);
@@ -1860,10 +1862,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ int sGp[kCapT], sGc[kCapT];
   __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
-  if (mode == 0 && st->done) return;
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
-  const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
   NX_PHASE_START(48);
   const int job = blockIdx.x;
   double part = 0.0;
@@ -1901,6 +1901,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     p_lam = pa.slot_lam[j];
     p_y = y[p_lam];
   }
+  if (mode == 0 && st->done) return;  // after the prefetch (nothing written before)
+  const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
   // several ranks, fused: every workgroup solves the coarse forest (k_pc_coarse's job)
