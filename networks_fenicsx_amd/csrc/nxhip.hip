@@ -796,13 +796,22 @@ __global__ __launch_bounds__(kBlock, 8) void k_mr_a(Csr A, MrVecs v, const MrSta
       const double r1v = (upd && (spmv || !PC)) ? v.r1in[r] : 0.0;
       if (comb) {  // x (and, handing over, w_{j-1} -> w2's buffer, w_j -> w1's) from v_1..v_j
         double xs = 0.0, wa = 0.0, wb = 0.0;
+        // four stored vectors per round, their loads issued together (same summation order)
 #pragma unroll 1
-        for (int i = 0; i < jr; ++i) {
-          const double vi = v.vs[(int64_t)i * v.vstride + r];
-          xs += sCx[i] * vi;
-          if (trans) {
-            wa += sM[jr - 2][i] * vi;  // w_{j-1}
-            wb += sM[jr - 1][i] * vi;  // w_j
+        for (int i0 = 0; i0 < jr; i0 += 4) {
+          double vi[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            vi[u] = i0 + u < jr ? v.vs[(int64_t)(i0 + u) * v.vstride + r] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u;
+            if (i >= jr) break;
+            xs += sCx[i] * vi[u];
+            if (trans) {
+              wa += sM[jr - 2][i] * vi[u];  // w_{j-1}
+              wb += sM[jr - 1][i] * vi[u];  // w_j
+            }
           }
         }
         v.x[r] = xs;
