@@ -9,9 +9,12 @@ These classes keep the attributes the reference's callers use
 DoF order inside each function (documented, since DOLFINx's internal permutation is
 not reproduced):
 
-* flux colour ``c``: the edges of colour ``c`` in ``graph.edges()`` order, ``N+1``
-  vertex values each, source -> target;
-* pressure: ``N`` cell values per edge, edge-major, source -> target;
+* flux colour ``c``: the edges of colour ``c`` in ``graph.edges()`` order, ``kN+1``
+  node values each (flux degree k; ``N+1`` vertex values for the default P1), source ->
+  target;
+* pressure: ``N`` cell values per edge, edge-major, source -> target (DG0); continuous
+  P_m: one value per graph node with an edge (ascending id), then the ``mN-1`` interior
+  node values of every edge, edge-major;
 * multiplier: one value per bifurcation, ascending node id.
 
 On a multi-rank run each rank's arrays hold the edges / bifurcations that rank
