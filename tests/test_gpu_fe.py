@@ -128,3 +128,25 @@ def test_fe_reassemble_idempotent():
     asm.assemble()
     np.testing.assert_array_equal(asm.handle.csr()[2], v1)
     np.testing.assert_array_equal(asm.handle.rhs(), r1)
+
+
+@pytest.mark.parametrize("km", [(2, 0), (3, 2)])
+def test_fe_single_edge(km):
+    """One edge, one cell: no multipliers; the device solve equals the direct solve."""
+    import networkx as nx
+
+    G = nx.DiGraph()
+    G.add_node(0, pos=np.array([0.0, 0.0]))
+    G.add_node(1, pos=np.array([0.0, 2.0]))
+    G.add_edge(0, 1)
+    mesh = NetworkMesh(G, N=1)
+    pbc = CASES["Y_N4"][3]
+    asm = HydraulicNetworkAssembler(mesh, flux_degree=km[0], pressure_degree=km[1])
+    asm.compute_forms(p_bc_ex=pbc)
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    F = OF.build_problem_fe(mesh.node_coordinates, *mesh.edges, 1, *km, mesh.edge_colors)
+    x_ref = O.solve_reference(*OF.assemble_reference_fe(F, pbc))
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL

@@ -139,3 +139,30 @@ def test_layout_sizes():
     assert lay.p_rows.size == 4 + 9
     lay0 = build_fe_layout(m.node_coordinates, src, dst, m.degrees, 4, 3, 0)
     assert lay0.n_rows == 3 * 13 + 3 * 4 + 1
+
+
+@pytest.mark.parametrize("km", [(2, 0), (2, 1), (3, 2)])
+@pytest.mark.parametrize("N", [1, 2])
+def test_layout_single_edge(km, N):
+    """Edge cases: one edge (no bifurcation, no multiplier), one cell per edge."""
+    import networkx as nx
+
+    G = nx.DiGraph()
+    G.add_node(0, pos=np.array([0.0, 0.0]))
+    G.add_node(1, pos=np.array([0.0, 2.0]))
+    G.add_edge(0, 1)
+    m = NetworkMesh(G, N=N)
+    pbc = CASES["Y_N4"][3]
+    src, dst = m.edges
+    lay = build_fe_layout(m.node_coordinates, src, dst, m.degrees, N, *km)
+    assert lay.lm_nodes.size == 0
+    F, Ar, br, _ = _reference_in_device_layout(m, lay, pbc, 0.0, np.ones(1))
+    _, h = O.cell_geometry(F.base)
+    val, rhs = evaluate_terms(lay, np.ones(1), 0.0, _edge_bc(m, F, pbc), h)
+    Ad = sp.csr_matrix((val, lay.col, lay.rowptr), shape=(lay.n_rows, lay.n_rows))
+    assert abs(Ad - Ar).max() <= 1e-14 * abs(Ar).max()
+    np.testing.assert_allclose(rhs, br, rtol=0, atol=1e-15)
+    x = O.solve_reference(*OF.assemble_reference_fe(F, pbc))
+    if km[1] >= 1:
+        xa = OF.resistor_network_solution_fe(F, pbc)
+        assert np.linalg.norm(x - xa) / np.linalg.norm(xa) < 1e-12
