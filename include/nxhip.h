@@ -122,6 +122,14 @@ int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_const, d
                         const double* edge_bc);
 
 /*
+ * Spatially varying source of the mass-conservation equation (the `f` of compute_forms,
+ * assembly.py:201-202, 262, given as one value per local edge): edge_f[E] replaces the
+ * constant f of nx_set_coefficients in the pressure rhs (f_e h per cell, times the pressure
+ * basis integrals for general degrees); NULL returns to the constant.
+ */
+int nx_set_source(nx_network_t* h, const double* edge_f);
+
+/*
  * Assemble matrix values and/or rhs on the device into the resident CSR.
  * Replaces HydraulicNetworkAssembler.assemble (assembly.py:329-368) and
  * Solver.assemble (solver.py:488-499). Asynchronous on the handle's stream.

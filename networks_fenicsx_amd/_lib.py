@@ -42,6 +42,7 @@ _SIGS = {
     "nx_destroy": (C.c_int, [_h]),
     "nx_dims": (C.c_int, [_h, _pi64, _pi64, _pi64]),
     "nx_set_coefficients": (C.c_int, [_h, _pd, _f64, _f64, _pd]),
+    "nx_set_source": (C.c_int, [_h, _pd]),
     "nx_assemble": (C.c_int, [_h, _i32, _i32]),
     "nx_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
     "nx_get_solution": (C.c_int, [_h, _pd]),
@@ -211,6 +212,13 @@ class Handle:
             raise ValueError("edge_bc must be (E, 2) and edge_R (E,)")
         check(lib().nx_set_coefficients(self.ptr, _ptr(eR, C.c_double), float(R_const), float(f),
                                         _ptr(bc, C.c_double)))
+
+    def set_source(self, edge_f: np.ndarray | None) -> None:
+        """Per-edge source values (``nx_set_source``); None: the constant of set_coefficients."""
+        ef = None if edge_f is None else np.ascontiguousarray(edge_f, dtype=np.float64)
+        if ef is not None and ef.size != self.n_edges:
+            raise ValueError("edge_f must have one value per local edge")
+        check(lib().nx_set_source(self.ptr, _ptr(ef, C.c_double)))
 
     def assemble(self, lhs: bool = True, rhs: bool = True) -> None:
         check(lib().nx_assemble(self.ptr, int(bool(lhs)), int(bool(rhs))))

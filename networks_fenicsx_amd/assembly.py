@@ -278,8 +278,8 @@ class HydraulicNetworkAssembler:
         Args:
             p_bc_ex: pressure boundary data (callable ``x -> values``, object with
                 ``eval``, nodal array or scalar), imposed weakly at inlet/outlet nodes.
-            f: constant source of the mass-conservation equation (default 0,
-                ``assembly.py:201-202``).
+            f: source of the mass-conservation equation -- a constant (default 0,
+                ``assembly.py:201-202``) or one value per graph edge (``graph.edges()`` order).
             R: resistance -- a constant (default 1, ``assembly.py:204-205``) or one
                 value per graph edge (``graph.edges()`` order).
             jit_options, form_compiler_options: accepted for API compatibility; the
@@ -287,7 +287,15 @@ class HydraulicNetworkAssembler:
         """
         del jit_options, form_compiler_options
         mesh, edge_ids = self._network_mesh, self._edge_ids
-        f_val = _scalar(f, "f", 0.0)
+        f_val, f_edge = 0.0, None
+        fv = f.value if isinstance(f, Constant) else f
+        if fv is not None and np.ndim(fv) > 0:  # one value per graph edge
+            fv = np.asarray(fv, dtype=np.float64).reshape(-1)
+            if fv.size != mesh.num_edges:
+                raise ValueError("f must be a constant or one value per graph edge")
+            f_edge = np.ascontiguousarray(fv[edge_ids])
+        else:
+            f_val = _scalar(f, "f", 0.0)
         R_const, R_edge = 1.0, None
         if R is not None:
             Rv = R.value if isinstance(R, Constant) else R
@@ -309,7 +317,9 @@ class HydraulicNetworkAssembler:
         edge_bc[:, 0] = np.where(root[s], -pbc[s], 0.0)  # - p_bc ds(out_marker)
         edge_bc[:, 1] = np.where(leaf[d], pbc[d], 0.0)  # + p_bc ds(in_marker)
         self._handle.set_coefficients(R_edge, R_const, f_val, edge_bc)
-        self._a = ("device-forms", R_const if R_edge is None else "per-edge", f_val)
+        self._handle.set_source(f_edge)
+        self._a = ("device-forms", R_const if R_edge is None else "per-edge",
+                   f_val if f_edge is None else "per-edge")
         self._L = ("device-rhs", pbc)
 
     # ---------------------------------------------------------------- assemble

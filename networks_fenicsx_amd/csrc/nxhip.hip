@@ -212,6 +212,7 @@ struct AsmArgs {
   const double* edge_R;   // E (per-edge R)
   const double* edge_bc;  // E*2 rhs at q_0 / q_N
   double f;
+  const double* edge_f;   // E per-edge source, or nullptr: f everywhere
   double* val;
   double* rhs;
   double* dq;  // E*(N+1) lumped flux mass (preconditioner), or nullptr
@@ -284,7 +285,8 @@ __global__ __launch_bounds__(kBlock) void k_assemble_seg(AsmArgs a) {
     md = R * h / 3.0;
     mo = R * h / 6.0;
     if (a.do_rhs) {
-      a.rhs[base + 2 * cl + 1] = -(a.f * h);  // negated pressure row: -(f h)
+      const double fe = a.edge_f ? a.edge_f[e] : a.f;
+      a.rhs[base + 2 * cl + 1] = -(fe * h);  // negated pressure row: -(f h)
       a.rhs[base + 2 * cl] = (cl == 0) ? a.edge_bc[2 * e] : 0.0;
     }
   }
@@ -370,6 +372,7 @@ __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
   const int seglen = a.ea.edge_seg[e + 1] - seg;
   const int64_t base = e * (2 * N + 1);
   const double bc0 = a.edge_bc[2 * e], bc1 = a.edge_bc[2 * e + 1];
+  const double fe_src = a.edge_f ? a.edge_f[e] : a.f;
   // the previous chunk's last cell (slot 0 of the chunk)
   double md_prev = 0.0, mo_prev = 0.0;
   for (int c0 = 0; c0 < N; c0 += 64) {
@@ -385,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
       md = R * h / 3.0;
       mo = R * h / 6.0;
       if (a.do_rhs) {
-        a.rhs[base + 2 * k + 1] = -(a.f * h);  // negated pressure row: -(f h)
+        a.rhs[base + 2 * k + 1] = -(fe_src * h);  // negated pressure row: -(f h)
         a.rhs[base + 2 * k] = (k == 0) ? bc0 : 0.0;
       }
     }
@@ -2499,6 +2502,7 @@ struct nx_network {
   int* edge_seg = nullptr;
   double* edge_R = nullptr;
   double* edge_bc = nullptr;
+  double* edge_f = nullptr;  // per-edge source (nx_set_source), or null: f everywhere
   double* lm_val = nullptr;
   double* dq = nullptr;  // E*(N+1) lumped flux mass (preconditioner D block)
   double f = 0.0;
@@ -3152,6 +3156,7 @@ struct FeArgs {
   const double* edge_R;  // E
   const double* edge_bc; // E*2
   double f;
+  const double* edge_f;  // E per-edge source, or nullptr: f everywhere
   int N;
   const int* kind;       // term table
   const double* tval;
@@ -3190,7 +3195,8 @@ __device__ __forceinline__ double fe_term(const FeArgs& a, int idx, int ent) {
   const double v = a.tval[ent];
   switch (a.kind[ent]) {
     case kFeMass: return (a.edge_R[idx / a.N] * fe_cell_h(a.edge_x, idx, a.N)) * v;
-    case kFeSource: return (a.f * fe_cell_h(a.edge_x, idx, a.N)) * v;
+    case kFeSource:
+      return ((a.edge_f ? a.edge_f[idx / a.N] : a.f) * fe_cell_h(a.edge_x, idx, a.N)) * v;
     case kFeBc: return a.edge_bc[idx] * v;
     default: return v;
   }
@@ -3292,7 +3298,7 @@ NX_API int nx_destroy(nx_network_t* h) {
     (void)drop_graph(graph_slot(Team{hs, 1, nullptr}));
   }
   if (h->comm) ncclCommDestroy(h->comm);
-  void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->lm_val, h->dq,
+  void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->edge_f, h->lm_val, h->dq,
                   h->z, h->vv, h->vs, h->hist,
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
                   h->wb[0],  h->wb[1],   h->x,        h->tmp,    h->partials, h->st,
@@ -3347,13 +3353,30 @@ NX_API int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_c
   return NX_OK;
 }
 
+NX_API int nx_set_source(nx_network_t* h, const double* edge_f) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  CHECK(set_device(h));
+  if (edge_f == nullptr) {
+    if (h->edge_f) HIPCALL(hipFree(h->edge_f));
+    h->edge_f = nullptr;
+    return NX_OK;
+  }
+  if (h->E > 0) {
+    if (!h->edge_f) CHECK(dalloc(&h->edge_f, h->E));
+    HIPCALL(hipMemcpyAsync(h->edge_f, edge_f, sizeof(double) * h->E, hipMemcpyHostToDevice,
+                           h->stream));
+    HIPCALL(hipStreamSynchronize(h->stream));
+  }
+  return NX_OK;
+}
+
 NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->have_coeffs) return fail(NX_ERR_STATE, "nx_set_coefficients must be called first");
   CHECK(set_device(h));
   if (!lhs && !rhs) return NX_OK;
   if (h->fe) {  // general degrees: one thread per nonzero / rhs row
-    FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->N, h->fe_kind, h->fe_tval,
+    FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind, h->fe_tval,
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
              h->nnz, h->n_own, h->val, h->rhs, lhs, rhs};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
@@ -3372,7 +3395,7 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   const int lb = grid_of(nlm, kBlock);
   if (eb + lb > 0) {
     AsmArgs a{EdgeArgs{h->edge_x, h->edge_lm, h->edge_seg, h->E, h->N},
-              h->edge_R, h->edge_bc, h->f, h->val, h->rhs, lhs ? h->dq : nullptr, lhs, rhs,
+              h->edge_R, h->edge_bc, h->f, h->edge_f, h->val, h->rhs, lhs ? h->dq : nullptr, lhs, rhs,
               eb, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges, h->rhs + h->n_edge_dofs};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
     if (epw == 4)

@@ -176,12 +176,14 @@ def build_fe_layout(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degree: n
                     lm_row[lm_nodes], edge_x)
 
 
-def evaluate_terms(lay: FeLayout, R_edge: np.ndarray, f: float, edge_bc: np.ndarray,
+def evaluate_terms(lay: FeLayout, R_edge: np.ndarray, f, edge_bc: np.ndarray,
                    cell_h: np.ndarray):
     """Host evaluation of the term tables (what ``k_assemble_fe`` computes), for tests and
-    debugging: returns ``(val, rhs)``. ``cell_h`` is ``(E, N)``."""
+    debugging: returns ``(val, rhs)``. ``cell_h`` is ``(E, N)``; ``f`` a constant or one value
+    per edge."""
     h = np.asarray(cell_h, dtype=np.float64).ravel()
     Rc = np.repeat(np.asarray(R_edge, dtype=np.float64), lay.N)
+    fc = np.repeat(np.broadcast_to(np.asarray(f, dtype=np.float64), (lay.E,)), lay.N)
     bc = np.asarray(edge_bc, dtype=np.float64).ravel()
 
     def term(i, e):
@@ -189,7 +191,7 @@ def evaluate_terms(lay: FeLayout, R_edge: np.ndarray, f: float, edge_bc: np.ndar
         if kind == KIND_MASS:
             return (Rc[i] * h[i]) * v
         if kind == KIND_SOURCE:
-            return (f * h[i]) * v
+            return (fc[i] * h[i]) * v
         if kind == KIND_BC:
             return bc[i] * v
         return v

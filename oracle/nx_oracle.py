@@ -150,7 +150,7 @@ def _nodal(values_or_fn, pos3: np.ndarray) -> np.ndarray:
 def assemble_reference(prob: OracleProblem, p_bc, f: float = 0.0, R=1.0):
     """Assemble ``(A, b)`` exactly as the reference forms define them (non-symmetric).
 
-    ``R`` is a constant or one value per edge. Returns a CSR matrix with sorted
+    ``R`` and ``f`` are constants or one value per edge. Returns a CSR matrix with sorted
     column indices and duplicate contributions summed, and the rhs vector.
     """
     E, N = prob.src.size, prob.N
@@ -198,7 +198,8 @@ def assemble_reference(prob: OracleProblem, p_bc, f: float = 0.0, R=1.0):
     e_root = np.flatnonzero(is_root[prob.src])
     b[prob.flux_offset[e_leaf] + N] += pb[prob.dst[e_leaf]]
     b[prob.flux_offset[e_root]] -= pb[prob.src[e_root]]
-    b[pc.ravel()] += (f * h).ravel()
+    fe = np.broadcast_to(np.asarray(f, dtype=np.float64), (E,))[:, None]  # constant or per edge
+    b[pc.ravel()] += (fe * h).ravel()
     return A, b
 
 

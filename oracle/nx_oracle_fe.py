@@ -219,8 +219,9 @@ def assemble_reference_fe(prob: FeProblem, p_bc, f: float = 0.0, R=1.0):
     e_root = np.flatnonzero(is_root[b_.src])
     rhs[prob.flux_offset[e_leaf] + k * N] += pb[b_.dst[e_leaf]]
     rhs[prob.flux_offset[e_root]] -= pb[b_.src[e_root]]
+    fe = np.broadcast_to(np.asarray(f, dtype=np.float64), (E,))[:, None]  # constant or per edge
     for a in range(len(p)):
-        np.add.at(rhs, p[a].ravel(), (f * h * wref[a]).ravel())
+        np.add.at(rhs, p[a].ravel(), (fe * h * wref[a]).ravel())
     return A, rhs
 
 

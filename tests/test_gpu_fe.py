@@ -100,6 +100,23 @@ def test_fe_source_and_resistance():
 
 
 @pytest.mark.parametrize("km", [(2, 0), (3, 1)])
+def test_fe_per_edge_source(km):
+    case = "edge_info_N10"
+    E = len(CASES[case][0]().edges())
+    f = 0.2 + 0.1 * (np.arange(E) % 3)
+    mesh, asm, F, A, b, pbc = _setup(case, km, f=f)
+    asm.assemble()
+    _, h = O.cell_geometry(F.base)
+    _, hr = evaluate_terms(asm.fe_layout, np.ones(E), f, _edge_bc(F, pbc), h)
+    np.testing.assert_array_equal(asm.handle.rhs(), hr)
+    solver = Solver(asm)
+    sol = solver.solve()
+    x_ref = O.solve_reference(A, b)
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
+@pytest.mark.parametrize("km", [(2, 0), (3, 1)])
 def test_fe_global_flux(km):
     """DG_k global flux: q is constant per edge (f = 0), so its integral is sum q_e L_e."""
     mesh, asm, F, A, b, pbc = _setup("depth6_N40", km)

@@ -230,6 +230,31 @@ def test_per_edge_resistance_and_source():
     assert np.linalg.norm(x - x_ref[perm]) / np.linalg.norm(x_ref) <= SOL_TOL
 
 
+def test_per_edge_source():
+    """f given per graph edge (nx_set_source): CSR / rhs bit-exact, solution vs direct."""
+    make, N, strategy, pbc = CASES["depth6_N40"]
+    mesh = NetworkMesh(make(), N=N, color_strategy=strategy)
+    f = 0.1 + 0.05 * (np.arange(mesh.num_edges) % 7)
+    asm = HydraulicNetworkAssembler(mesh)
+    asm.compute_forms(p_bc_ex=pbc, f=f)
+    solver = Solver(asm)
+    solver.assemble()
+    solver.solve()
+    src, dst = mesh.edges
+    P = O.build_problem(mesh.node_coordinates, src, dst, N, mesh.edge_colors)
+    A, b = O.assemble_reference(P, pbc, f=f)
+    Ab, bb, perm, _ = O.to_build_layout(P, A, b)
+    np.testing.assert_array_equal(asm.handle.rhs(), bb)
+    x_ref = O.solve_reference(A, b)
+    x = solver.solution_vector()
+    assert np.linalg.norm(x - x_ref[perm]) / np.linalg.norm(x_ref) <= SOL_TOL
+    # back to a constant: the per-edge values are dropped
+    asm.compute_forms(p_bc_ex=pbc, f=0.2)
+    asm.assemble()
+    A2, b2 = O.assemble_reference(P, pbc, f=0.2)
+    np.testing.assert_array_equal(asm.handle.rhs(), O.to_build_layout(P, A2, b2)[1])
+
+
 def test_profiling_counters():
     mesh, asm, P, A, b, _ = _build("depth6_N40")
     h = asm.handle

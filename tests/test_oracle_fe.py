@@ -166,3 +166,15 @@ def test_layout_single_edge(km, N):
     if km[1] >= 1:
         xa = OF.resistor_network_solution_fe(F, pbc)
         assert np.linalg.norm(x - xa) / np.linalg.norm(xa) < 1e-12
+
+
+def test_per_edge_source_reduces_to_constant():
+    m, pbc = _mesh("edge_info_N10")
+    src, dst = m.edges
+    F = OF.build_problem_fe(m.node_coordinates, src, dst, m.N, 2, 1, m.edge_colors)
+    _, b1 = OF.assemble_reference_fe(F, pbc, f=0.4)
+    _, b2 = OF.assemble_reference_fe(F, pbc, f=np.full(src.size, 0.4))
+    np.testing.assert_array_equal(b1, b2)
+    P = O.build_problem(m.node_coordinates, src, dst, m.N, m.edge_colors)
+    np.testing.assert_array_equal(O.assemble_reference(P, pbc, f=0.4)[1],
+                                  O.assemble_reference(P, pbc, f=np.full(src.size, 0.4))[1])
