@@ -111,8 +111,8 @@ def cpu_baseline(mesh, budget_s: float):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--levels", type=int, default=15, help="tree generations at 1 GPU")
     ap.add_argument("--N", type=int, default=15, help="cells per edge")
     ap.add_argument("--rtol", type=float, default=1e-12)
