@@ -35,7 +35,7 @@
 
 namespace {
 
-constexpr int kVersion = 1 * 10000 + 0 * 100 + 0;
+constexpr int kVersion = 1 * 10000 + 1 * 100 + 0;  // 1.1: nx_create_fe, nx_set_source
 constexpr int kBlock = 256;         // threads per block (4 wave64)
 constexpr int kRowsPerBlock = 256;  // SpMV: one row per thread
 constexpr int kLdsCap = 2048;       // SpMV: products staged per block (16 KiB)
