@@ -53,3 +53,33 @@ def test_create_argument_errors():
     with pytest.raises(_lib.NxError, match="edge_lm"):
         _lib.Handle(0, 2, np.zeros((1, 6)), np.array([[0, -1]], np.int32),
                     np.zeros(1, np.int32), np.zeros(0, np.int32), np.zeros(0))
+
+
+def test_create_fe_argument_errors():
+    """nx_create_fe validates the layout and term tables before any device call."""
+    import copy
+
+    import numpy as np
+
+    from networks_fenicsx_amd import NetworkMesh
+    from networks_fenicsx_amd import network_generation as ng
+    from networks_fenicsx_amd.layout_fe import build_fe_layout
+
+    m = NetworkMesh(ng.make_tree(2, 1, 3), N=3)
+    src, dst = m.edges
+    lay = build_fe_layout(m.node_coordinates, src, dst, m.degrees, 3, 2, 1)
+    bad = copy.copy(lay)
+    bad.table_kind = lay.table_kind.copy()
+    bad.table_kind[0] = 7
+    with pytest.raises(_lib.NxError, match="table_kind"):
+        _lib.Handle.create_fe(0, bad)
+    bad = copy.copy(lay)
+    bad.a_idx = lay.a_idx.copy()
+    bad.a_idx[0] = 10 ** 6  # a mass term's cell out of range
+    with pytest.raises(_lib.NxError, match="out of range"):
+        _lib.Handle.create_fe(0, bad)
+    bad = copy.copy(lay)
+    bad.b_ptr = lay.b_ptr.copy()
+    bad.b_ptr[1], bad.b_ptr[2] = bad.b_ptr[2] + 1, bad.b_ptr[1]
+    with pytest.raises(_lib.NxError, match="monotone"):
+        _lib.Handle.create_fe(0, bad)
