@@ -217,7 +217,7 @@ struct AsmArgs {
   double* rhs;
   double* dq;  // E*(N+1) lumped flux mass (preconditioner), or nullptr
   int lhs, do_rhs;
-  // multiplier rows (k_assemble_lm's work, done by the blocks after the edge blocks)
+  // multiplier rows: +-1 values and zero rhs, done by the blocks after the edge blocks
   int edge_blocks;
   int64_t nnz_lm, B;
   const double* lm_val;
