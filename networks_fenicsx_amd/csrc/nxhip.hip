@@ -1682,6 +1682,20 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   __shared__ int sLv[kMaxTopLvl + 1];
   double c2 = 0.0;
   const bool upd = mode == 0 && !(MULTI && pa.lin);
+  // static indices of the first pass of phases A1 / A2, loaded before the stop test and
+  // alpha's re-reduction (they only depend on the decomposition)
+  const int nl = pa.n_top_lvl;
+  const int ts0 = pa.top_lvl_off[0], ts1 = pa.top_lvl_off[nl];
+  const int nt = ts1 - ts0;
+  const int dc0 = nt > 0 ? pa.slot_dc_off[ts0] : 0;
+  const int ndc = nt > 0 ? pa.slot_dc_off[ts1] - dc0 : 0;
+  const int tid = threadIdx.x;
+  const int p_c = tid < ndc ? pa.slot_dc[dc0 + tid] : 0;
+  const int p_lo = tid < ndc ? pa.dc_lo[dc0 + tid] : -1;
+  const int p_lam = tid < nt ? pa.slot_lam[ts0 + tid] : 0;
+  const int p_pcn = tid < nt ? pa.slot_pchain[ts0 + tid] : -1;
+  const int p_par = tid < nt ? pa.slot_parent[ts0 + tid] : -1;
+  const int p_off = tid < nt ? pa.slot_dc_off[ts0 + tid] : 0;
   if (mode == 0) {
     if (st->done) return;
     if (upd) {
@@ -1690,17 +1704,13 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     }
   }
   NX_PHASE_START(32);
-  const int nl = pa.n_top_lvl;
-  const int ts0 = pa.top_lvl_off[0], ts1 = pa.top_lvl_off[nl];
-  const int nt = ts1 - ts0;
-  const int dc0 = nt > 0 ? pa.slot_dc_off[ts0] : 0;
-  const int ndc = nt > 0 ? pa.slot_dc_off[ts1] - dc0 : 0;
   for (int i = threadIdx.x; i <= nl; i += kTopThreads) sLv[i] = pa.top_lvl_off[i];
   // phase A1, one thread per hanging chain: its conductance, its top current and, for a
   // lower-job root below it (final Norton pair) or ground, its whole contribution
   for (int i = threadIdx.x; i < ndc; i += kTopThreads) {
-    const int c = pa.slot_dc[dc0 + i];
-    const int lo = pa.dc_lo[dc0 + i];
+    const bool pre = i == tid;
+    const int c = pre ? p_c : pa.slot_dc[dc0 + i];
+    const int lo = pre ? p_lo : pa.dc_lo[dc0 + i];
     const double g = 1.0 / pa.chain_T[c];
     const double it = pa.chain_It[c];
     int child = -1;
@@ -1722,7 +1732,8 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   // phase A2, one thread per junction: own data + parent chain
   for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
     const int j = ts0 + sl;
-    const int lam = pa.slot_lam[j];
+    const bool pre = sl == tid;
+    const int lam = pre ? p_lam : pa.slot_lam[j];
     double yl = y[lam];
     if (upd) {
       yl -= c2 * r2[lam];
@@ -1730,14 +1741,14 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     }
     sLam[sl] = lam;
     sY[sl] = yl;
-    const int pcn = pa.slot_pchain[j];
+    const int pcn = pre ? p_pcn : pa.slot_pchain[j];
     const double gp = pcn >= 0 ? 1.0 / pa.chain_T[pcn] : 0.0;
     sD0[sl] = gp;
     sJ0[sl] = yl + (pcn >= 0 ? pa.chain_Ib[pcn] : 0.0);
-    const int par = pa.slot_parent[j];
+    const int par = pre ? p_par : pa.slot_parent[j];
     sPar[sl] = par >= 0 ? par - ts0 : -1;
     sGp[sl] = gp;
-    sOff[sl] = pa.slot_dc_off[j] - dc0;
+    sOff[sl] = (pre ? p_off : pa.slot_dc_off[j]) - dc0;
   }
   if (threadIdx.x == 0) sOff[nt] = ndc;
   __syncthreads();
