@@ -21,6 +21,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 from pathlib import Path
@@ -76,9 +77,13 @@ def pmc_traffic(kernel_prefix: str):
     """Per-launch HBM bytes of a kernel from the newest committed PMC summary
     (profiles/<tag>_summary.json, written by scripts/summarize_profile.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same workload)."""
-    # profile tags sort by round and letter (r01b < r01i < r02a); file mtimes are not
-    # meaningful in a fresh checkout
-    cands = sorted((REPO / "profiles").glob("*_summary.json"), key=lambda p: p.name)
+    # profile tags sort by round, then by letter suffix length, then letters
+    # (r01b < r01z < r01aa < r02a); file mtimes are not meaningful in a fresh checkout
+    def tag_key(p):
+        m = re.match(r"r(\d+)([a-z]*)_", p.name)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, p.name)
+
+    cands = sorted((REPO / "profiles").glob("*_summary.json"), key=tag_key)
     for path in reversed(cands):
         doc = json.loads(path.read_text())
         for name, d in doc.get("kernels", {}).items():
