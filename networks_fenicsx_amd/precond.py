@@ -259,6 +259,91 @@ class TreePreconditioner:
         return int(self.chain_edge.size)
 
 
+# LDS caps of the preconditioner kernels (csrc/nxhip.hip): chains, junction slots and
+# down-chain entries per job. The top part's chains ride along round-robin, hence the
+# margin on the chain cap.
+_CAP_CHAINS, _CAP_SLOTS, _CAP_DC = 512, 256, 768
+_CHAIN_MARGIN = 32
+
+
+@dataclass
+class _JobRoots:
+    roots: list
+    promoted: list
+
+
+def _split_job_roots(roots, children, chain_up_node, chain_lo_node, is_cc, E: int,
+                     n_top: int, max_top: int, balance: int = 0) -> _JobRoots:
+    """Replace every job root whose subtree exceeds the LDS caps by its children (the
+    root joins the top part), recursively, keeping the roots' order; stops promoting
+    when the top part would exceed ``max_top``. With ``balance`` > 0, first split the
+    root with the most chains while that keeps at most ``balance`` jobs."""
+    own_ch: dict[int, int] = {}
+    own_dc: dict[int, int] = {}
+    for e in range(E):
+        lo, up = int(chain_lo_node[e]), int(chain_up_node[e])
+        key = lo if lo != -1 else up
+        if key != -1:
+            own_ch[key] = own_ch.get(key, 0) + 1
+        if up != -1 and not is_cc[e]:
+            own_dc[up] = own_dc.get(up, 0) + 1
+    sizes: dict[int, tuple[int, int, int]] = {}
+
+    def size(v: int) -> tuple[int, int, int]:
+        if v not in sizes:  # iterative post-order (deep trees)
+            stack = [(v, False)]
+            while stack:
+                u, done = stack.pop()
+                if u in sizes:
+                    continue
+                if not done:
+                    stack.append((u, True))
+                    stack.extend((c, False) for c in children[u] if c not in sizes)
+                    continue
+                ch, sl, dc = own_ch.get(u, 0), 1, own_dc.get(u, 0)
+                for c in children[u]:
+                    a, b, d = sizes[c]
+                    ch, sl, dc = ch + a, sl + b, dc + d
+                sizes[u] = (ch, sl, dc)
+        return sizes[v]
+
+    def over(v: int) -> bool:
+        ch, sl, dc = size(v)
+        return ch > _CAP_CHAINS - _CHAIN_MARGIN or sl > _CAP_SLOTS or dc > _CAP_DC
+
+    promoted = []
+    if balance > 0:
+        import heapq
+
+        order = {v: i for i, v in enumerate(roots)}
+        heap = [(-size(v)[0], order[v], v) for v in roots]
+        heapq.heapify(heap)
+        live = set(roots)
+        while heap and n_top + len(promoted) < max_top:
+            negc, _, v = heap[0]
+            kids = children[v]
+            if not kids or len(live) - 1 + len(kids) > balance:
+                break
+            heapq.heappop(heap)
+            live.discard(v)
+            promoted.append(v)
+            for c in kids:
+                order[c] = len(order)
+                live.add(c)
+                heapq.heappush(heap, (-size(c)[0], order[c], c))
+        roots = sorted(live)  # slot_nodes order, as the depth cut's roots
+    out = []
+    todo = list(reversed(roots))
+    while todo:
+        r = todo.pop()
+        if children[r] and over(r) and n_top + len(promoted) < max_top:
+            promoted.append(r)
+            todo.extend(reversed(children[r]))
+        else:
+            out.append(r)
+    return _JobRoots(out, promoted)
+
+
 def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
                               target_jobs: int = 256, max_top: int = 1024,
                               coarse: CoarseStructure | None = None) -> TreePreconditioner:
@@ -376,11 +461,30 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         if p != -1:
             children[p].append(v)
 
+    # A lower subtree must fit one workgroup of the LDS kernels (csrc/nxhip.hip kCapC /
+    # kCapS / kCapDC); an uneven local forest (several ranks: pieces of different heights
+    # hang from the coarse junctions) can put 4x the typical subtree below one depth-L
+    # root. Such a root is promoted into the top part and its children become job roots.
+    if lp.nranks > 1 and croots and maxd >= 1:
+        # several ranks: the local forest's pieces differ in height, so a fixed cut depth
+        # gives uneven jobs; split the largest subtree first, from depth 1, until there are
+        # target_jobs jobs (a uniform binary tree gives the depth cut's decomposition)
+        L = 1
+        start = [v for v in slot_nodes if depth[v] == 1]
+        balance = target_jobs
+    else:
+        start = [v for v in slot_nodes if depth[v] == L]
+        balance = 0
+    job_roots = _split_job_roots(start, children, chain_up_node, chain_lo_node, is_cc, E,
+                                 n_top=int(counts[:L].sum()), max_top=max_top,
+                                 balance=balance)
+    promoted = set(job_roots.promoted)
+    job_roots = job_roots.roots
+
     # slots: lower subtrees (level order inside), then top levels
     slots: list[int] = []
     job_lvl_off = [0]
     lvl_slot_off = [0]
-    job_roots = [v for v in slot_nodes if depth[v] == L]
     for r in job_roots:
         level = [r]
         while level:
@@ -390,8 +494,9 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         job_lvl_off.append(len(lvl_slot_off) - 1)
     n_lower_slots = len(slots)
     top_lvl_off = [n_lower_slots]
-    for dlev in range(min(L, maxd + 1)):
-        slots.extend(v for v in slot_nodes if depth[v] == dlev)
+    top_depth = max([L - 1] + [depth[v] for v in promoted])
+    for dlev in range(min(top_depth + 1, maxd + 1)):
+        slots.extend(v for v in slot_nodes if depth[v] == dlev and (dlev < L or v in promoted))
         top_lvl_off.append(len(slots))
     assert len(slots) == len(slot_nodes)
     slot_of = {v: i for i, v in enumerate(slots)}
