@@ -2584,6 +2584,7 @@ struct nx_network {
   double* gath = nullptr;
   bool beta_p2p = true;
   bool rccl_graph_ok = true;  // capture of the RCCL iteration worked (or was not tried)
+  bool sched_checked = false; // RCCL: the ranks' kernel schedules were compared (per pc)
   bool last_graph = false;    // the last nx_solve replayed HIP graphs
   // general element degrees (nx_create_fe): gather-assembly tables, one rank, no
   // preconditioner
@@ -3646,6 +3647,56 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
 }
 
 // MINRES of every rank of the team (nx_solve / nx_group_solve).
+// What decides the exchange schedule of a multi-rank solve: every rank must run the same
+// one (a rank on the global-memory preconditioner kernels while another runs the LDS
+// kernels' linear form would pair different collectives). Each rank decides from its own
+// decomposition (LDS caps), so the ranks compare.
+constexpr int kSchedSig = 6;
+void sched_sig(const nx_network* h, int* s) {
+  s[0] = h->pc;
+  s[1] = h->pc && h->pc_lds;
+  s[2] = h->pc ? h->pa.lin : 0;
+  s[3] = h->pc ? h->pa.fused : 0;
+  s[4] = h->pc ? h->pc_variant : 0;
+  s[5] = h->beta_p2p;
+}
+
+int check_schedules(const Team& t) {
+  int s0[kSchedSig], s[kSchedSig];
+  sched_sig(t.hs[0], s0);
+  for (int r = 1; r < t.P; ++r) {
+    sched_sig(t.hs[r], s);
+    for (int i = 0; i < kSchedSig; ++i)
+      if (s[i] != s0[i])
+        return fail(NX_ERR_STATE, "ranks chose different kernel schedules (rank " +
+                                      std::to_string(r) + ", item " + std::to_string(i) + ")");
+  }
+  nx_network* h = t.hs[0];
+  if (!h->comm || h->sched_checked) return NX_OK;
+  int v[2 * kSchedSig];  // max of s and of -s over the ranks: equal iff all ranks agree
+  for (int i = 0; i < kSchedSig; ++i) {
+    v[i] = s0[i];
+    v[kSchedSig + i] = -s0[i];
+  }
+  int* d = nullptr;
+  HIPCALL(hipMalloc((void**)&d, sizeof(v)));
+  int rc = NX_OK;
+  if (hipMemcpy(d, v, sizeof(v), hipMemcpyHostToDevice) != hipSuccess ||
+      ncclAllReduce(d, d, 2 * kSchedSig, ncclInt32, ncclMax, h->comm, h->stream) != ncclSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess ||
+      hipMemcpy(v, d, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(NX_ERR_RCCL, "kernel schedule comparison across ranks failed");
+  (void)hipFree(d);
+  if (rc != NX_OK) return rc;
+  for (int i = 0; i < kSchedSig; ++i)
+    if (v[i] != -v[kSchedSig + i])
+      return fail(NX_ERR_STATE, "ranks chose different kernel schedules (item " +
+                                    std::to_string(i) + ": preconditioner decomposition "
+                                    "outside the LDS caps on some ranks)");
+  h->sched_checked = true;
+  return NX_OK;
+}
+
 int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, int32_t* iters,
                double* relres, int32_t* converged) {
   for (int r = 0; r < t.P; ++r) {
@@ -3658,6 +3709,7 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   if (check_every & 1) ++check_every;
   CHECK(set_device(t.hs[0]));
   const bool multi = team_multi(t);
+  if (multi) CHECK(check_schedules(t));
   const bool lean_env = lean_mode();
   {  // one graph per solve (profiling and the all-reduce beta^2 variant keep the general path)
     nx_network* h0 = t.hs[0];
@@ -4030,6 +4082,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
                                  int32_t n_lvl, const int32_t* lvl_slot_off, int32_t n_top_lvl,
                                  const int32_t* top_lvl_off) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
+  h->sched_checked = false;
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
   CHECK(drop_handle_graphs(h));  // captured launches depend on the preconditioner

@@ -194,3 +194,26 @@ def test_rccl_single_rank_communicator(pc):
         assert asm.handle.true_residual() < 1e-9
     finally:
         asm.close()
+
+
+def test_group_ranks_with_different_schedules_fail_loudly(monkeypatch):
+    """A rank whose preconditioner runs another kernel schedule (here: the global-memory
+    kernels on rank 1 only) must make the solve fail, not pair mismatched exchanges."""
+    from networks_fenicsx_amd._lib import NxError
+
+    make, N, strategy, pbc = CASES["depth6_N40"]
+    grp = RankGroup(make(), N, 2, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.assemble()
+        monkeypatch.setenv("NXHIP_PC_GLOBAL", "1")
+        grp.assemblers[1].set_preconditioner(True)
+        monkeypatch.delenv("NXHIP_PC_GLOBAL")
+        with pytest.raises(NxError, match="different kernel schedules"):
+            grp.solve(1e-12, 50000, 32)
+        grp._close_group()
+        grp.assemblers[1].set_preconditioner(True)  # same schedule again: solves
+        it, _, conv = grp.solve(1e-12, 50000, 32)
+        assert conv
+    finally:
+        grp.close()
