@@ -1818,19 +1818,30 @@ __device__ void pc_prep_in_block(const PcArgs& pa, bool gcols, double* sJ, doubl
 // The coarse forest solve of k_pc_coarse (same arithmetic, same order) inside one
 // workgroup, into sZc (n_coarse <= kCapCoarseLds); sD / sJ are scratch.
 __device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* sZc) {
-  const int nC = pa.n_coarse;
+  // the forest's structure is staged in LDS first (two round trips): its level sweeps
+  // (13 levels each way for the 8-rank depth-17 tree) then touch no global memory
+  __shared__ int sCo[kCapCoarseLds + 1], sCc[kCapCoarseLds], sCp[kCapCoarseLds];
+  __shared__ int sCl[kCapCoarseLds + 1];
+  __shared__ double sCg[kCapCoarseLds];
+  const int nC = pa.n_coarse, nl = pa.n_clvl;
   const double* __restrict__ G = pa.cbuf + 2 * nC;
+  for (int i = threadIdx.x; i <= nC; i += kPcThreads) sCo[i] = pa.c_child_off[i];
+  for (int i = threadIdx.x; i <= nl; i += kPcThreads) sCl[i] = pa.c_lvl_off[i];
   for (int i = threadIdx.x; i < nC; i += kPcThreads) {
     sD[i] = pa.cbuf[i];
     sJ[i] = pa.cbuf[nC + i];
+    sCg[i] = G[i];
+    sCp[i] = pa.c_parent[i];
   }
   __syncthreads();
-  for (int lv = pa.n_clvl - 1; lv >= 0; --lv) {  // deepest level first
-    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kPcThreads) {
+  for (int i = threadIdx.x; i < sCo[nC]; i += kPcThreads) sCc[i] = pa.c_child[i];
+  __syncthreads();
+  for (int lv = nl - 1; lv >= 0; --lv) {  // deepest level first
+    for (int j = sCl[lv] + threadIdx.x; j < sCl[lv + 1]; j += kPcThreads) {
       double D = sD[j], J = sJ[j];
-      for (int i = pa.c_child_off[j]; i < pa.c_child_off[j + 1]; ++i) {
-        const int k = pa.c_child[i];
-        const double g = G[k], Dk = sD[k];
+      for (int i = sCo[j]; i < sCo[j + 1]; ++i) {
+        const int k = sCc[i];
+        const double g = sCg[k], Dk = sD[k];
         D -= g * g / Dk;
         J += g * sJ[k] / Dk;
       }
@@ -1839,10 +1850,10 @@ __device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* 
     }
     __syncthreads();
   }
-  for (int lv = 0; lv < pa.n_clvl; ++lv) {  // root level first
-    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kPcThreads) {
-      const int p = pa.c_parent[j];
-      sZc[j] = (sJ[j] + (p >= 0 ? G[j] * sZc[p] : 0.0)) / sD[j];
+  for (int lv = 0; lv < nl; ++lv) {  // root level first
+    for (int j = sCl[lv] + threadIdx.x; j < sCl[lv + 1]; j += kPcThreads) {
+      const int p = sCp[j];
+      sZc[j] = (sJ[j] + (p >= 0 ? sCg[j] * sZc[p] : 0.0)) / sD[j];
     }
     __syncthreads();
   }
@@ -2195,8 +2206,39 @@ __device__ void pc_cpart_body(const PcArgs& pa, double* sA) {
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // chains joining two coarse junctions (serial: fixed order)
-    for (int i = 0; i < pa.n_cc; ++i) {
+  const int ncc = pa.n_cc;
+  if (ncc > 0 && nC <= kCapCoarseLds && ncc <= kCapCoarseLds) {
+    // chains joining two coarse junctions: their data gathered in parallel, then summed
+    // in LDS by one thread in the fixed order (same bits as summing in global memory,
+    // without a dependent global round trip per chain)
+    __shared__ double sCb[3 * kCapCoarseLds], sQg[kCapCoarseLds], sQt[kCapCoarseLds],
+        sQb[kCapCoarseLds];
+    __shared__ int sQi[kCapCoarseLds], sQo[kCapCoarseLds];
+    for (int i = threadIdx.x; i < 3 * nC; i += kTopThreads) sCb[i] = pa.cbuf[i];
+    for (int i = threadIdx.x; i < ncc; i += kTopThreads) {
+      const int c = pa.cc_chain[i];
+      sQg[i] = 1.0 / pa.chain_T[c];
+      sQt[i] = pa.chain_It[c];
+      sQb[i] = pa.chain_Ib[c];
+      sQi[i] = pa.cc_top[i];
+      sQo[i] = pa.cc_bot[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < ncc; ++i) {
+        const int t = sQi[i], b = sQo[i];
+        const double g = sQg[i];
+        sCb[t] += g;
+        sCb[b] += g;
+        sCb[nC + t] += sQt[i];
+        sCb[nC + b] += sQb[i];
+        sCb[2 * nC + b] = g;
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * nC; i += kTopThreads) pa.cbuf[i] = sCb[i];
+  } else if (threadIdx.x == 0) {  // (large coarse sets) serial in global memory
+    for (int i = 0; i < ncc; ++i) {
       const int c = pa.cc_chain[i], t = pa.cc_top[i], b = pa.cc_bot[i];
       const double g = 1.0 / pa.chain_T[c];
       pa.cbuf[t] += g;
