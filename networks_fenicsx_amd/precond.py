@@ -315,6 +315,22 @@ def _split_job_roots(roots, children, chain_up_node, chain_lo_node, is_cc, E: in
     if balance > 0:
         import heapq
 
+        # pieces far below the average job (small subtrees hanging from the coarse
+        # junctions) join the top part whole: they would take a workgroup each and leave
+        # too few jobs to split the largest subtrees (257-chain jobs at 8 ranks)
+        avg = sum(size(v)[0] for v in roots) / max(balance, 1)
+        keep = []
+        for v in roots:
+            sub = [v]
+            k = 0
+            while k < len(sub):
+                sub.extend(children[sub[k]])
+                k += 1
+            if 2 * size(v)[0] < avg and n_top + len(promoted) + len(sub) <= max_top:
+                promoted.extend(sub)
+            else:
+                keep.append(v)
+        roots = keep
         order = {v: i for i, v in enumerate(roots)}
         heap = [(-size(v)[0], order[v], v) for v in roots]
         heapq.heapify(heap)
