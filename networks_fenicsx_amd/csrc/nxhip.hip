@@ -958,6 +958,10 @@ struct PcArgs {
   // so alpha's partial rides in the coarse all-reduce (xalpha = cbuf + 3 n_coarse)
   int lin;
   const double* xalpha;
+  // dense inverse of the coarse forest system (n_coarse^2, built per solve by k_pc_gc in
+  // the start application; null when n_coarse > kCapCoarseLds): the fused down sweeps form
+  // z_c = Gc J_c by dot products instead of the level sweeps
+  double* Gc;
   double* slot_z;  // P^{-1}y at every junction slot (written by the top part, read across jobs)
   // dense top part (single rank, LDS kernels; precond.py: _dense_top_lists): G = inverse
   // of the top tree Schur matrix (n_top^2, built once per solve by k_pc_gbuild); per job
@@ -1942,7 +1946,21 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   // several ranks, fused: every workgroup solves the coarse forest (k_pc_coarse's job)
   const bool cfused = MULTI && dense && pa.fused;
   if (cfused) {
-    pc_coarse_lds(pa, sGz, sGt, sCz);
+    if (pa.Gc != nullptr) {  // z_c = Gc J_c, one wave per coarse value (fixed order)
+      const int nC = pa.n_coarse;
+      const double* __restrict__ Jc = pa.cbuf + nC;
+      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+      for (int j = wv; j < nC; j += kPcThreads / 64) {
+        const double* __restrict__ g = pa.Gc + (int64_t)j * nC;
+        double acc = 0.0;
+        for (int i = ln; i < nC; i += 64) acc += g[i] * Jc[i];
+        acc = wave_sum(acc);
+        if (ln == 0) sCz[j] = acc;
+      }
+      __syncthreads();
+    } else {
+      pc_coarse_lds(pa, sGz, sGt, sCz);
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       if (lin) {
         MrState* s = const_cast<MrState*>(st);
@@ -2769,6 +2787,43 @@ int team_allreduce(const Team& t, int slot, int n) {
   return NX_OK;
 }
 
+// Columns of Gc (several ranks, once per solve after the start's coarse all-reduce): the
+// coarse forest solve of e_k with this solve's D and G (k_pc_coarse's arithmetic), one
+// workgroup per column. D and G are fixed for the solve, so z_c = Gc J_c afterwards.
+constexpr int kGcThreads = 256;
+__global__ __launch_bounds__(kGcThreads) void k_pc_gc(PcArgs pa) {
+  __shared__ double sD[kCapCoarseLds], sJ[kCapCoarseLds], sZ[kCapCoarseLds];
+  const int nC = pa.n_coarse, k = blockIdx.x;
+  const double* __restrict__ G = pa.cbuf + 2 * nC;
+  for (int i = threadIdx.x; i < nC; i += kGcThreads) {
+    sD[i] = pa.cbuf[i];
+    sJ[i] = i == k ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int lv = pa.n_clvl - 1; lv >= 0; --lv) {  // deepest level first
+    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kGcThreads) {
+      double D = sD[j], J = sJ[j];
+      for (int i = pa.c_child_off[j]; i < pa.c_child_off[j + 1]; ++i) {
+        const int c = pa.c_child[i];
+        const double g = G[c], Dc = sD[c];
+        D -= g * g / Dc;
+        J += g * sJ[c] / Dc;
+      }
+      sD[j] = D;
+      sJ[j] = J;
+    }
+    __syncthreads();
+  }
+  for (int lv = 0; lv < pa.n_clvl; ++lv) {  // root level first
+    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kGcThreads) {
+      const int p = pa.c_parent[j];
+      sZ[j] = (sJ[j] + (p >= 0 ? G[j] * sZ[p] : 0.0)) / sD[j];
+    }
+    __syncthreads();
+  }
+  for (int j = threadIdx.x; j < nC; j += kGcThreads) pa.Gc[(int64_t)j * nC + k] = sZ[j];
+}
+
 // Preconditioner application on the stream: z = P^{-1} r' where r' = y - (alpha/beta) r2
 // (mode 0, written back into y) or r' = y (mode 1, start). Partials of r'.z -> partB.
 // half 0: chain condensation + junction elimination (up, top); half 1: back-substitution
@@ -2811,6 +2866,8 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
       hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
                          h->pa, y, h->z, st, h->partB, mode);
   }
+  if (MULTI && coarse && mode == 1 && h->pa.Gc != nullptr)  // the iterations' dense coarse step
+    hipLaunchKernelGGL(k_pc_gc, dim3(h->pa.n_coarse), dim3(kGcThreads), 0, h->stream, h->pa);
 }
 
 template <bool MULTI>
@@ -4476,6 +4533,17 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   h->pc_bufs.push_back(cb);
   pa.cbuf = cb;
   pa.xalpha = cb + 3 * n_coarse;
+  pa.Gc = nullptr;
+  if (n_coarse > 0 && n_coarse <= kCapCoarseLds) {
+    const char* e = std::getenv("NXHIP_PC_GC");  // 0: level sweeps in every down workgroup
+    if (!e || std::atoi(e) != 0) {
+      double* gc = nullptr;
+      HIPCALL(hipMalloc((void**)&gc, sizeof(double) * n_coarse * n_coarse));
+      HIPCALL(hipMemset(gc, 0, sizeof(double) * n_coarse * n_coarse));
+      h->pc_bufs.push_back(gc);
+      pa.Gc = gc;
+    }
+  }
   double* zc = nullptr;  // coarse solution (dense top with several ranks)
   HIPCALL(hipMalloc((void**)&zc, sizeof(double) * n_coarse));
   h->pc_bufs.push_back(zc);
