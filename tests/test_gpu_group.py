@@ -93,14 +93,16 @@ def test_group_solve_matches_direct(case, P, pc):
 
 @pytest.mark.parametrize("env", [{"NXHIP_PC_LIN": "0"}, {"NXHIP_PC_GLOBAL": "1"},
                                  {"NXHIP_BETA_P2P": "0"}, {"NXHIP_PC_DENSE": "0"},
-                                 {"NXHIP_PC_FACTOR": "0"}, {"NXHIP_PC_FUSE": "0"}])
+                                 {"NXHIP_PC_FACTOR": "0"}, {"NXHIP_PC_FUSE": "0"},
+                                 {"NXHIP_PC_GC": "0"}])
 def test_group_alternative_kernel_paths(env, monkeypatch):
     """Alternative multi-rank paths: alpha with its own all-reduce (NXHIP_PC_LIN=0), the
     global-memory preconditioner kernels (NXHIP_PC_GLOBAL=1), beta^2 by all-reduce
     (NXHIP_BETA_P2P=0), the per-iteration top kernel instead of the dense top
     (NXHIP_PC_DENSE=0), per-iteration eliminations instead of factored ones (NXHIP_PC_FACTOR=0),
     separate k_pc_cpart / k_pc_coarse / halo-pack kernels instead of the fused ones
-    (NXHIP_PC_FUSE=0)."""
+    (NXHIP_PC_FUSE=0), the coarse level sweeps in every down workgroup instead of the dense
+    Gc product (NXHIP_PC_GC=0)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     case, P = "depth6_N40", 4
