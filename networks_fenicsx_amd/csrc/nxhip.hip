@@ -2201,19 +2201,32 @@ __device__ void pc_cpart_last(const PcArgs& pa, double* sA) {
 }
 
 __device__ void pc_cpart_body(const PcArgs& pa, double* sA) {
+  // the coarse roots among the top slots, found by all threads at once (one round trip)
+  // and listed in LDS: the waves then only visit those (any order: each writes its own
+  // coarse slot)
+  __shared__ int sRoot[kCapT], sRootC[kCapT];
+  __shared__ int sNr;
+  if (threadIdx.x == 0) sNr = 0;
+  __syncthreads();
   const int ts0 = pa.top_lvl_off[0], nt = pa.n_top, nC = pa.n_coarse;
   for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
+    const int c = pa.slot_cidx[ts0 + sl];
+    const int par = pa.slot_parent[ts0 + sl];
     double a = 0.0;
     for (int i = pa.top_uoff[sl]; i < pa.top_uoff[sl + 1]; ++i) a += pa.u[i];
     sA[sl] = a;
     pa.atop[sl] = a;
+    if (c >= 0 && par < ts0) {
+      const int q = atomicAdd(&sNr, 1);
+      sRoot[q] = sl;
+      sRootC[q] = c;
+    }
   }
   for (int i = threadIdx.x; i < 3 * nC; i += kTopThreads) pa.cbuf[i] = 0.0;
   __syncthreads();
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  for (int r = wv; r < nt; r += kTopThreads / 64) {  // one wave per coarse root
-    const int c = pa.slot_cidx[ts0 + r];
-    if (c < 0 || pa.slot_parent[ts0 + r] >= ts0) continue;
+  for (int q = wv; q < sNr; q += kTopThreads / 64) {  // one wave per coarse root
+    const int r = sRoot[q], c = sRootC[q];
     const double* __restrict__ k = pa.KJ + (int64_t)r * nt;
     double acc = 0.0;
     for (int sl = ln; sl < nt; sl += 64) acc += k[sl] * sA[sl];
