@@ -219,3 +219,26 @@ def test_group_ranks_with_different_schedules_fail_loudly(monkeypatch):
         assert conv
     finally:
         grp.close()
+
+
+def test_group_rehearsal_four_ranks_depth16():
+    """4 ranks x make_tree(17) (1 M rows per rank): the size at which the depth-cut
+    decomposition put a job over the LDS caps on some ranks and the ranks diverged
+    (DESIGN.md section 6). Exact preconditioner: 3 iterations, analytic answer."""
+    G = ng.make_tree(17, 17, 17)
+    grp = RankGroup(G, 15, 4, color_strategy="smallest_last")
+    try:
+        grp.compute_forms(p_bc_ex=lambda x: x[1])
+        grp.assemble()
+        it, _, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and it == 3
+        m0 = grp.meshes[0]
+        src, dst = m0.edges
+        P = O.build_problem(m0.node_coordinates, src, dst, 15)
+        xa = O.resistor_network_solution(P, lambda x: x[1])[O.build_permutation(P)[0]]
+        x = np.full(xa.size, np.nan)
+        for a, xl in zip(grp.assemblers, grp.solutions()):
+            x[DM.global_rows(a.local_problem, m0.num_edges, m0.bifurcation_index)] = xl
+        assert np.linalg.norm(x - xa) / np.linalg.norm(xa) < 1e-10
+    finally:
+        grp.close()
