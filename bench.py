@@ -5,14 +5,22 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload: ``make_tree(15 + log2(N), ...)`` with N=15 cells per edge, p_bc = y, f = 0,
-R = 1. At one GPU this is the depth-14 tree (1,032,160 DoF, BASELINE
-configs[3]); every doubling of the GPU count adds one tree generation, so the work
-per GPU stays fixed (weak scaling) and 8 GPUs run the depth-17 tree (configs[4]).
+``--gpus N > 1`` without a launcher starts the ``torch.distributed.run`` line above as a
+child process (before torch or ``libnxhip.so`` is loaded) and exits with its code; a run
+whose ``WORLD_SIZE`` differs from ``--gpus`` fails instead of measuring something else.
 
-One step = device assembly of the CSR matrix and rhs (``nx_assemble``) + MINRES to
-rtol 1e-12 (``nx_solve``), inputs resident in HBM, solution left in HBM. Rank 0
-prints one JSON line.
+Workload (p_bc = y, f = 0, R = 1, ``color_strategy="smallest_last"``):
+
+* 1 GPU: ``make_tree(15,15,15)``, N = 15 -- the depth-14 tree, 1,032,160 DoF (configs[3],
+  the configuration the metric is quoted on);
+* P = 2^k GPUs: ``make_tree(15+k, 15+k, 15+k)``, N = 19 -- one tree generation per GPU
+  doubling (weak scaling, ~1.28 M rows per GPU); at 8 GPUs this is SURVEY's C4,
+  ``make_tree(18,18,18)``, N = 19, 10,354,648 DoF (configs[4]). Rank 0 also times the SAME
+  workload on its GPU alone (``strong_scaling``), so T1 / TP is measured in the same run.
+
+One step = device assembly of the CSR matrix and rhs (``nx_assemble``) + MINRES to rtol
+1e-12 (``nx_solve``), inputs resident in HBM, solution left in HBM. Rank 0 prints one JSON
+line.
 """
 
 from __future__ import annotations
@@ -21,7 +29,10 @@ import argparse
 import json
 import math
 import os
+import platform
 import re
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -29,18 +40,8 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
-# torch bundles its own HIP runtime / RCCL. Import it BEFORE libnxhip.so is loaded so
-# the library binds to those same copies (by SONAME); loading libnxhip.so first would
-# put two HIP runtimes in the process (they collide at exit).
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-from networks_fenicsx_amd import _lib  # noqa: E402
-
-_lib.lib()
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+METRIC = "assemble+solve ms and SpMV HBM GB/s, depth-14 tree, 1/2/4/8 GPU"
 
 
 def spmv_bytes(n_rows: int, nnz: int) -> int:
@@ -92,103 +93,204 @@ def pmc_traffic(kernel_prefix: str):
     return None, None, None
 
 
-def cpu_baseline(mesh, budget_s: float):
-    """CPU restatement of the reference path on the host: oracle assembly + SuperLU
-    direct solve (the MUMPS stand-in), repeated up to ``budget_s`` seconds."""
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(mesh, asm, dof: int, budget_s: float):
+    """The hot path on the host cores (rank 0, one GPU only), two legs:
+
+    * ``port``: ``oracle/nx_cpu.c`` -- OpenMP assembly in the device layout + MINRES with the
+      same exact tree preconditioner, on all threads OpenMP is given (OMP_NUM_THREADS);
+    * ``superlu``: the oracle's numpy assembly of the reference forms + SuperLU ``spsolve``
+      (1 thread; the stand-in for the reference's MUMPS direct solve).
+
+    The headline ``value`` is the all-cores port; each leg runs about ``budget_s / 2``."""
+    from networks_fenicsx_amd.assembly import edge_boundary_rhs, evaluate_nodal
+    from oracle import nx_cpu
     from oracle import nx_oracle as O
 
+    legs = []
+    lp = asm.local_problem
+    bc = edge_boundary_rhs(mesh, lp.edges, evaluate_nodal(lambda x: x[1], mesh.node_coordinates))
+    port = nx_cpu.CpuStep(lp, asm.tree_preconditioner, bc)
+    port.assemble()
+    port.solve()  # first touch of every buffer outside the timing
+    ms, runs, its = port.time_steps(budget_s / 2)
+    threads = nx_cpu.threads()
+    legs.append({"leg": "port", "ms_per_step": ms, "value": dof / (ms / 1e3), "cores": threads,
+                 "minres_iterations": its,
+                 "sample": f"{runs} full steps of the same workload ({dof} DoF): OpenMP assembly "
+                           f"+ MINRES with the exact tree preconditioner (oracle/nx_cpu.c), "
+                           f"{threads} threads"})
+    del port
     src, dst = mesh.edges
     P = O.build_problem(mesh.node_coordinates, src, dst, mesh.N, mesh.edge_colors)
     runs, t_total = 0, 0.0
-    while runs < 1 or (t_total < budget_s and runs < 40):  # ~10-30 s of CPU work
+    while runs < 1 or (t_total < budget_s / 2 and runs < 40):
         t0 = time.perf_counter()
         A, b = O.assemble_reference(P, lambda x: x[1])
         O.solve_reference(A, b)
         t_total += time.perf_counter() - t0
         runs += 1
-    ms = 1e3 * t_total / runs
-    return {"value": P.n_dofs / (ms / 1e3), "unit": "DoF/s", "cores": 1, "kind": "port",
-            "ms_per_step": ms,
-            "sample": f"{runs} full run(s) of the same workload ({P.n_dofs} DoF): numpy "
-                      f"assembly of the reference forms + scipy SuperLU spsolve (1 thread)"}
+    ms1 = 1e3 * t_total / runs
+    legs.append({"leg": "superlu", "ms_per_step": ms1, "value": dof / (ms1 / 1e3), "cores": 1,
+                 "sample": f"{runs} full run(s) of the same workload: numpy assembly of the "
+                           "reference forms + scipy SuperLU spsolve (1 thread, the MUMPS "
+                           "stand-in)"})
+    head = legs[0]
+    return {"value": head["value"], "unit": "DoF/s", "cores": head["cores"], "kind": "port",
+            "ms_per_step": head["ms_per_step"], "sample": head["sample"],
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "legs": legs}
 
 
-def main() -> int:
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--levels", type=int, default=15, help="tree generations at 1 GPU")
-    ap.add_argument("--N", type=int, default=15, help="cells per edge")
+    ap.add_argument("--levels", type=int, default=None,
+                    help="tree generations (default: 15 at 1 GPU, 15 + log2(P) at P GPUs)")
+    ap.add_argument("--N", type=int, default=None,
+                    help="cells per edge (default: 15 at 1 GPU, 19 at P > 1 GPUs)")
     ap.add_argument("--rtol", type=float, default=1e-12)
     ap.add_argument("--check-every", type=int, default=4)
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="P > 1: skip rank 0's one-GPU time of the same workload")
+    ap.add_argument("--api-steps", type=int, default=10,
+                    help="steps through the public Solver.assemble/solve surface (0: skip)")
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def main() -> int:
+    args = parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # one process per GPU: start the launcher as a child (nothing has touched the GPU)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), str(Path(__file__).resolve()), *sys.argv[1:]]
+        return subprocess.call(cmd)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to measure a "
+              "different configuration", file=sys.stderr)
+        return 2
+    return run(args, world)
+
+
+def run(args, world: int) -> int:
+    # torch first: libnxhip.so binds to torch's HIP runtime / RCCL (networks_fenicsx_amd._lib)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from networks_fenicsx_amd import _lib
+
+    _lib.lib()
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local_rank)
 
-    from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh
+    from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh, Solver
     from networks_fenicsx_amd import network_generation as ng
     from networks_fenicsx_amd.comm import SerialComm, TorchComm
 
     extra = int(round(math.log2(world))) if world > 1 else 0
     if world > 1 and 2**extra != world:
         raise SystemExit("world size must be a power of two")
-    levels = args.levels + extra
+    levels = args.levels if args.levels is not None else 15 + extra
+    N = args.N if args.N is not None else (15 if world == 1 else 19)
     comm = TorchComm() if world > 1 else SerialComm()
-    G = ng.make_tree(levels, levels, levels) if rank == 0 else None
-    mesh = NetworkMesh(G, N=args.N, color_strategy="smallest_last", comm=comm)
-    del G
-    asm = HydraulicNetworkAssembler(mesh)
-    asm.compute_forms(p_bc_ex=lambda x: x[1])
-    if args.no_pc:
-        asm.set_preconditioner(False)
-    h = asm.handle
-    E, B = mesh.num_edges, len(mesh.bifurcation_values)
-    dof_total = E * (2 * args.N + 1) + B
-
-    state = {}
-
-    def step():
-        h.assemble(True, True)
-        it, rr, conv = h.solve(args.rtol, 50000, args.check_every)
-        state["it"], state["relres"], state["conv"] = it, rr, conv
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    h.sync()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
+    def allmax(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
+
+    def allsum(vals):
+        if world == 1:
+            return list(vals)
+        t = torch.tensor(list(vals), dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.tolist()
+
+    # ---- setup (host: graph, topology, layout, preconditioner decomposition; device:
+    # pattern, coefficient upload) -- reported, not part of the step
+    barrier()
+    t0 = time.perf_counter()
+    G = ng.make_tree(levels, levels, levels) if rank == 0 else None
+    t_graph = time.perf_counter() - t0
+    mesh = NetworkMesh(G, N=N, color_strategy="smallest_last", comm=comm)
+    del G
+    t_mesh = time.perf_counter() - t0 - t_graph
+    asm = HydraulicNetworkAssembler(mesh)
+    t_asm = time.perf_counter() - t0 - t_graph - t_mesh
+    asm.compute_forms(p_bc_ex=lambda x: x[1])
+    if args.no_pc:
+        asm.set_preconditioner(False)
+    torch.cuda.synchronize()
+    setup = {"total": time.perf_counter() - t0, "graph": t_graph, "mesh": t_mesh,
+             "assembler": t_asm}
+    setup["forms"] = setup["total"] - t_graph - t_mesh - t_asm
+    setup = {k: allmax(v) for k, v in setup.items()}
+    h = asm.handle
+    E, B = mesh.num_edges, len(mesh.bifurcation_values)
+    dof_total = E * (2 * N + 1) + B
+    state = {}
+
+    def step(hd):
+        hd.assemble(True, True)
+        it, rr, conv = hd.solve(args.rtol, 50000, args.check_every)
+        state["it"], state["relres"], state["conv"] = it, rr, conv
+
+    def timed_steps(hd, steps, warmup, collective):
+        for _ in range(warmup):
+            step(hd)
+        if collective:
+            barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(steps):
+            step(hd)
+        hd.sync()
+        torch.cuda.synchronize()
+        if collective:
+            barrier()
+        el = time.perf_counter() - ts
+        return allmax(el) if collective else el
+
+    elapsed = timed_steps(h, args.steps, args.warmup, True)
     ms_per_step = 1e3 * elapsed / args.steps
+    iters = state["it"]
 
     # --- per-kernel timing with HIP events on the library's stream (one profiled step)
     h.set_profiling(True)
     h.reset_profile()
-    step()
+    step(h)
     prof = h.profile()
     h.set_profiling(False)
     spmv_ms = prof["spmv_ms"] / max(prof["spmv_count"], 1)
@@ -199,32 +301,74 @@ def main() -> int:
     nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on, max(int(prof["spmv_count"]), 1))
     achieved = nbytes / (spmv_ms * 1e-3) / 1e9
     sbytes = spmv_bytes(h.n_rows, h.nnz)
-    kname = f"k_mr_a<{str(world > 1).lower()}, {str(pc_on).lower()}>"
+    # beta^2 travels point-to-point with the halo, so the multi-rank k_mr_a is MULTI = false
+    kname = f"k_mr_a<false, {str(pc_on).lower()}>"
     # the committed PMC summaries profile the default workload (C3) on one GPU only
-    default_workload = world == 1 and (args.levels, args.N) == (15, 15) and not args.no_pc
+    default_workload = world == 1 and (levels, N) == (15, 15) and not args.no_pc
     traffic, traffic_src, rocprof_ns = pmc_traffic(kname) if default_workload else (None, None, None)
 
-    # --- parity outside the timed region
+    # --- the public surface: Solver.assemble() + Solver.solve() returning the Functions
+    # (the reference's nxfx:Solver:solve includes the assign into Functions, solver.py:107-135)
+    api_ms = None
+    if args.api_steps > 0:
+        solver = Solver(asm)
+        solver.assemble()
+        solver.solve()
+        barrier()
+        ts = time.perf_counter()
+        for _ in range(args.api_steps):
+            solver.assemble()
+            fns = solver.solve()
+        barrier()
+        api_ms = 1e3 * allmax(time.perf_counter() - ts) / args.api_steps
+        del fns, solver
+
+    # --- parity outside the timed region: true residual and error vs the analytic answer
+    from oracle import nx_oracle as O
+
     true_rr = h.true_residual()
     parity = {"true_relres": true_rr, "minres_relres": state["relres"], "converged": state["conv"]}
-    if world == 1:
-        from oracle import nx_oracle as O
+    src, dst = mesh.edges
+    P = O.build_problem(mesh.node_coordinates, src, dst, mesh.N)
+    xa = O.resistor_network_solution(P, lambda x: x[1])
+    perm, _ = O.build_permutation(P)
+    xa_b = xa[perm]  # build layout in global edge order
+    lp = asm.local_problem
+    per = 2 * N + 1
+    rows = np.concatenate([(lp.edges[:, None] * per + np.arange(per)[None, :]).ravel(),
+                           E * per + mesh.bifurcation_index[lp.lm_nodes]])
+    x = h.solution()
+    d2, r2 = allsum([float(np.sum((x - xa_b[rows]) ** 2)), float(np.sum(xa_b[rows] ** 2))])
+    parity["relerr_vs_analytic"] = math.sqrt(d2 / r2)
+    del xa, xa_b, P
 
-        src, dst = mesh.edges
-        P = O.build_problem(mesh.node_coordinates, src, dst, mesh.N)
-        xa = O.resistor_network_solution(P, lambda x: x[1])
-        perm, _ = O.build_permutation(P)
-        x = h.solution()
-        parity["relerr_vs_analytic"] = float(np.linalg.norm(x - xa[perm]) / np.linalg.norm(xa))
+    # --- rank 0 alone on the same workload (strong scaling T1), the others wait
+    strong = None
+    if world > 1 and not args.no_strong:
+        barrier()
+        if rank == 0:
+            ts = time.perf_counter()
+            asm1 = HydraulicNetworkAssembler(mesh.with_comm(None))
+            asm1.compute_forms(p_bc_ex=lambda x: x[1])
+            torch.cuda.synchronize()
+            setup1 = time.perf_counter() - ts
+            el1 = timed_steps(asm1.handle, args.steps, args.warmup, False)
+            t1 = 1e3 * el1 / args.steps
+            it1 = state["it"]
+            asm1.close()
+            strong = {"workload": "same tree, one GPU (rank 0)", "n_gpus": world,
+                      "t1_ms_per_step": t1, "tP_ms_per_step": ms_per_step,
+                      "speedup_t1_over_tP": t1 / ms_per_step, "t1_minres_iterations": it1,
+                      "t1_setup_s": setup1}
+        barrier()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(mesh, args.cpu_budget)
-        cpu["cores"] = 1
+        cpu = cpu_baseline(mesh, asm, dof_total, args.cpu_budget)
 
     if rank == 0:
         out = {
-            "metric": "assemble+solve ms and SpMV HBM GB/s, depth-14 tree, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": dof_total / (ms_per_step / 1e3),
             "unit": "DoF/s",
             "n_gpus": world,
@@ -238,14 +382,19 @@ def main() -> int:
             "data": "synthetic (make_tree binary tree, p_bc = y, f = 0, R = 1)",
             "config": {
                 "workload": f"make_tree({levels},{levels},{levels}) depth-{levels - 1} binary "
-                            f"tree, N={args.N} cells/edge, assemble + MINRES rtol {args.rtol:g}",
+                            f"tree, N={N} cells/edge, assemble + MINRES rtol {args.rtol:g}",
                 "dofs": dof_total,
-                "nnz": E * (7 * args.N + 1) + 6 * B,
+                "nnz": E * (7 * N + 1) + 6 * B,
                 "edges": E,
-                "minres_iterations": state["it"],
+                "N": N,
+                "minres_iterations": iters,
                 "parallelism": f"edge-partition x{world}" if world > 1 else "single GPU",
+                "rccl_ranks": h.comm_count() if world > 1 else None,
                 "preconditioner": "tree Schur complement" if pc_on else "none",
             },
+            "setup_s": setup,
+            "api_ms_per_step": api_ms,
+            "strong_scaling": strong,
             "roofline": {
                 "bound": "hbm",
                 "kernel": f"{kname} (CSR SpMV fused with the Lanczos step, Givens rotation and "
@@ -271,7 +420,7 @@ def main() -> int:
             "cpu_baseline": cpu,
             "parity": parity,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

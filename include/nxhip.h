@@ -295,6 +295,10 @@ int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned c
                  int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
                  const int32_t* send_idx, const int32_t* recv_off);
 
+/* Ranks of the handle's RCCL communicator (ncclCommCount); without one, the rank count of
+ * its halo plan (1 for a single-GPU handle). bench.py reports it next to the timing. */
+int nx_comm_count(nx_network_t* h, int32_t* nranks);
+
 /*
  * In-process rank group: the ranks of a partitioned problem as handles on ONE device,
  * driven in lock-step from one host thread, with the halo exchange as device copies and

@@ -65,6 +65,7 @@ _SIGS = {
     "nx_comm_init": (C.c_int, [_h, _i32, _i32, _pu8, _i32, _pi32, _pi32, _pi32, _pi32]),
     "nx_set_coarse": (C.c_int, [_h, _i32, _pi32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                 _i32, _pi32]),
+    "nx_comm_count": (C.c_int, [_h, _pi32]),
     "nx_set_halo": (C.c_int, [_h, _i32, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
     "nx_set_pc_dense": (C.c_int, [_h, _i32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                   _pi32, _pi32, _pi32, _pi32]),
@@ -86,6 +87,31 @@ class NxNotConverged(NxError):
     """MINRES did not reach the tolerance (mirrors ``ksp_error_if_not_converged``)."""
 
 
+def _import_torch_first() -> bool:
+    """Load torch's HIP runtime and RCCL before ``libnxhip.so``.
+
+    torch bundles its own ``libamdhip64`` / ``librccl`` (same SONAMEs as ``/opt/rocm``), and
+    a process that maps ``libnxhip.so`` before torch's HIP libraries aborts at exit ("double
+    free or corruption"), even when both bind to the same runtime copy (measured: preloading
+    torch's runtime libraries by path does not avoid it; importing torch first does). So when
+    torch is importable it is imported here, before the library is mapped, whatever order
+    the caller imports things in (``tests/test_lib.py`` runs the "wrong" order in a
+    subprocess). ``NXHIP_NO_TORCH=1`` skips this for processes that never import torch."""
+    import importlib.util
+    import sys
+
+    if "torch" in sys.modules or os.environ.get("NXHIP_NO_TORCH", "0") not in ("", "0"):
+        return False
+    try:
+        if importlib.util.find_spec("torch") is None:
+            return False
+    except (ImportError, ValueError):
+        return False
+    import torch  # noqa: F401
+
+    return True
+
+
 def lib():
     """Load ``libnxhip.so`` once; raise loudly if it is missing."""
     global _lib
@@ -98,6 +124,7 @@ def lib():
                     f"{_LIB_PATH} is missing: build it with "
                     "`python -m networks_fenicsx_amd.build` (there is no CPU fallback)"
                 )
+            _import_torch_first()
             handle = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
             for name, (res, args) in _SIGS.items():
                 fn = getattr(handle, name)
@@ -363,6 +390,12 @@ class Handle:
                                 _ptr(send_idx if send_idx.size else np.zeros(1, np.int32),
                                      C.c_int32),
                                 _ptr(recv_off, C.c_int32)))
+
+    def comm_count(self) -> int:
+        """Ranks of the RCCL communicator (``ncclCommCount``), else the plan's rank count."""
+        n = C.c_int32(0)
+        check(lib().nx_comm_count(self.ptr, C.byref(n)))
+        return int(n.value)
 
     def comm_init(self, nranks: int, rank: int, uid: bytes, peers, send_off, send_idx, recv_off):
         uid_arr = (C.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid)

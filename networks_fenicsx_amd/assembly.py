@@ -41,7 +41,8 @@ from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
 
-__all__ = ["HydraulicNetworkAssembler", "DeviceMatrix", "DeviceVector", "evaluate_nodal"]
+__all__ = ["HydraulicNetworkAssembler", "DeviceMatrix", "DeviceVector", "evaluate_nodal",
+           "edge_boundary_rhs"]
 
 
 def _device_for_rank() -> int:
@@ -81,6 +82,23 @@ def evaluate_nodal(p_bc_ex, pos: np.ndarray) -> np.ndarray:
     if vals.size != n:
         raise ValueError(f"p_bc gave {vals.size} values for {n} nodes")
     return vals
+
+
+def edge_boundary_rhs(mesh: NetworkMesh, edge_ids: np.ndarray, pbc: np.ndarray) -> np.ndarray:
+    """rhs of the flux end rows of every listed edge, ``(E, 2)``: ``-p_bc(source)`` at an
+    inlet root's ``q_0`` and ``+p_bc(target)`` at an outlet leaf's ``q_N``, 0 elsewhere --
+    the weak boundary terms ``+p_bc v ds(in) - p_bc v ds(out)`` (``assembly.py:258-260``)
+    with the markers of ``mesh.py:402-420``."""
+    src, dst = mesh.edges
+    s, d = src[edge_ids], dst[edge_ids]
+    leaf = np.zeros(mesh.num_nodes, dtype=bool)
+    leaf[mesh.boundary_in_nodes] = True
+    root = np.zeros(mesh.num_nodes, dtype=bool)
+    root[mesh.boundary_out_nodes] = True
+    edge_bc = np.zeros((edge_ids.size, 2), dtype=np.float64)
+    edge_bc[:, 0] = np.where(root[s], -pbc[s], 0.0)  # - p_bc ds(out_marker)
+    edge_bc[:, 1] = np.where(leaf[d], pbc[d], 0.0)  # + p_bc ds(in_marker)
+    return edge_bc
 
 
 def _scalar(c, name: str, default: float) -> float:
@@ -307,15 +325,7 @@ class HydraulicNetworkAssembler:
             else:
                 raise ValueError("R must be a constant or one value per graph edge")
         pbc = evaluate_nodal(p_bc_ex, mesh.node_coordinates)
-        src, dst = mesh.edges
-        s, d = src[edge_ids], dst[edge_ids]
-        leaf = np.zeros(mesh.num_nodes, dtype=bool)
-        leaf[mesh.boundary_in_nodes] = True
-        root = np.zeros(mesh.num_nodes, dtype=bool)
-        root[mesh.boundary_out_nodes] = True
-        edge_bc = np.zeros((edge_ids.size, 2), dtype=np.float64)
-        edge_bc[:, 0] = np.where(root[s], -pbc[s], 0.0)  # - p_bc ds(out_marker)
-        edge_bc[:, 1] = np.where(leaf[d], pbc[d], 0.0)  # + p_bc ds(in_marker)
+        edge_bc = edge_boundary_rhs(mesh, edge_ids, pbc)
         self._handle.set_coefficients(R_edge, R_const, f_val, edge_bc)
         self._handle.set_source(f_edge)
         self._a = ("device-forms", R_const if R_edge is None else "per-edge",
@@ -351,6 +361,11 @@ class HydraulicNetworkAssembler:
     def local_problem(self) -> LocalProblem | None:
         """The P1/DG0 rank layout (``layout.py``); None for general degrees."""
         return self._local
+
+    @property
+    def tree_preconditioner(self) -> TreePreconditioner | None:
+        """The host decomposition of the tree preconditioner (``precond.py``), or None."""
+        return self._pc
 
     @property
     def fe_layout(self) -> FeLayout | None:

@@ -2879,7 +2879,9 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
       hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
                          h->pa, y, h->z, st, h->partB, mode);
   }
-  if (MULTI && coarse && mode == 1 && h->pa.Gc != nullptr)  // the iterations' dense coarse step
+  // the iterations' dense coarse step: Gc is read only by the fused dense down sweep
+  if (MULTI && coarse && mode == 1 && h->pa.Gc != nullptr && h->pc_lds && h->pa.fused &&
+      h->pa.mdense)
     hipLaunchKernelGGL(k_pc_gc, dim3(h->pa.n_coarse), dim3(kGcThreads), 0, h->stream, h->pa);
 }
 
@@ -3763,7 +3765,7 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
 // one (a rank on the global-memory preconditioner kernels while another runs the LDS
 // kernels' linear form would pair different collectives). Each rank decides from its own
 // decomposition (LDS caps), so the ranks compare.
-constexpr int kSchedSig = 6;
+constexpr int kSchedSig = 8;
 void sched_sig(const nx_network* h, int* s) {
   s[0] = h->pc;
   s[1] = h->pc && h->pc_lds;
@@ -3771,6 +3773,11 @@ void sched_sig(const nx_network* h, int* s) {
   s[3] = h->pc ? h->pa.fused : 0;
   s[4] = h->pc ? h->pc_variant : 0;
   s[5] = h->beta_p2p;
+  // the dense top (nx_set_pc_dense, decided per rank from its kMaxNeed fit) drives mdense
+  // and with it fuse_pack: who packs the halo and beta^2 -- a per-rank difference would
+  // leave peers reading stale halo values
+  s[6] = h->pc ? h->pa.dense : 0;
+  s[7] = h->pc ? (h->pa.n_coarse > 0) : 0;
 }
 
 int check_schedules(const Team& t) {
@@ -4371,6 +4378,7 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
                            const int32_t* job_root_u, const int32_t* job_root_dc) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
+  h->sched_checked = false;
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
   CHECK(drop_handle_graphs(h));
@@ -4489,6 +4497,7 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   if (n_coarse > kCapCoarse)
     return fail(NX_ERR_ARG, "coarse forest has " + std::to_string(n_coarse) + " junctions (cap " +
                                 std::to_string(kCapCoarse) + ")");
+  h->sched_checked = false;  // pa.lin / pa.fused change the exchange schedule
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
   CHECK(drop_handle_graphs(h));
@@ -4634,10 +4643,23 @@ NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_
   HIPCALL(hipMemsetAsync(h->gath, 0, sizeof(double) * nranks, h->stream));
   h->beta_p2p = true;
   if (const char* e = std::getenv("NXHIP_BETA_P2P")) h->beta_p2p = std::atoi(e) != 0;
+  h->sched_checked = false;  // beta_p2p is part of the schedule signature
   h->nranks = nranks;
   h->rank = rank;
   h->have_plan = true;
   HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_comm_count(nx_network_t* h, int32_t* nranks) {
+  if (!h || !nranks) return fail(NX_ERR_ARG, "null argument");
+  if (!h->comm) {  // no RCCL communicator: the handle's own view (1, or a group's size)
+    *nranks = h->nranks;
+    return NX_OK;
+  }
+  int n = 0;
+  NCCLCALL(ncclCommCount(h->comm, &n));
+  *nranks = n;
   return NX_OK;
 }
 

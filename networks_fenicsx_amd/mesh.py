@@ -33,7 +33,7 @@ import networkx as nx
 import numpy as np
 import numpy.typing as npt
 
-from .comm import Comm, as_comm
+from .comm import Comm, SerialComm, as_comm
 from .timing import timed
 
 __all__ = ["NetworkMesh", "color_graph", "IntervalMesh", "AdjacencyList"]
@@ -290,6 +290,19 @@ class NetworkMesh:
         in_pairs = (np.asarray(in_nodes, dtype=np.int64), np.asarray(in_cols, dtype=np.int32))
         out_pairs = (np.asarray(out_nodes, dtype=np.int64), np.asarray(out_cols, dtype=np.int32))
         return gdim, pos, src, dst, ecol, n_colors, deg, radius, in_pairs, out_pairs
+
+    def with_comm(self, comm: Any) -> "NetworkMesh":
+        """The same network seen through another communicator (shares the graph arrays).
+
+        Every rank holds the whole graph after the broadcast, so e.g. ``with_comm(None)``
+        on rank 0 gives the single-process problem of a partitioned run (``bench.py``'s
+        same-workload one-GPU time) without analysing the graph again."""
+        import copy
+
+        m = copy.copy(self)
+        m._comm = as_comm(comm) if comm is not None else SerialComm()
+        m._msh = None
+        return m
 
     # -------------------------------------------------------------- geometry
     @property

@@ -12,6 +12,6 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step gpu_tests 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS}
+step gpu_tests 1000 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS}
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py ${BENCH_ARGS}

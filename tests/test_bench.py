@@ -29,3 +29,23 @@ def test_profile_tags_order_by_suffix_length(tmp_path, monkeypatch):
 def test_committed_summary_has_the_bench_kernel():
     traffic, src, ns = bench.pmc_traffic("k_mr_a<false, true>")
     assert src is not None and traffic > 0 and ns > 0
+
+
+def test_world_size_mismatch_refuses_to_measure():
+    """WORLD_SIZE set by a launcher but different from --gpus: non-zero exit before any
+    GPU work (bench.py would otherwise measure another configuration)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    res = subprocess.run([sys.executable, str(Path(bench.__file__)), "--gpus", "4"],
+                         capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 2
+    assert "refusing" in res.stderr
+
+
+def test_default_workloads():
+    args = bench.parse_args([])
+    assert args.gpus == 1 and args.levels is None and args.N is None

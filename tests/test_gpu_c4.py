@@ -1,0 +1,95 @@
+"""SURVEY's C4 (BASELINE configs[4]): ``make_tree(18,18,18)``, N = 19 -- 262,143 edges,
+10,354,648 DoF, 35,913,588 nonzeros -- on one GPU through the HIP path, and as the 8-rank
+edge-partitioned problem of ``bench.py --gpus 8`` through the in-process rank group (same
+per-rank handles, halo plans, coarse step and kernels as the RCCL path; RCCL itself needs
+one GPU per rank).
+
+Size-independent checks (the oracle's direct solve does not fit a test at this size):
+closed-form nnz E(7N+1)+6B, exact symmetry of the assembled matrix, 3 MINRES iterations
+(exact Schur-complement preconditioner), and the analytic resistor-network answer to
+1e-10 relative 2-norm (SURVEY.md 8a "derived exactness")."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import distributed_model as DM
+from networks_fenicsx_amd import HydraulicNetworkAssembler
+from networks_fenicsx_amd import network_generation as ng
+from networks_fenicsx_amd.group import RankGroup
+from oracle import nx_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+LEVELS, N, P = 18, 19, 8
+TOL = 1e-10
+
+
+def p_y(x):
+    return x[1]
+
+
+@pytest.fixture(scope="module")
+def c4():
+    G = ng.make_tree(LEVELS, LEVELS, LEVELS)
+    grp = RankGroup(G, N, P, color_strategy="smallest_last")
+    del G
+    m0 = grp.meshes[0]
+    src, dst = m0.edges
+    prob = O.build_problem(m0.node_coordinates, src, dst, N)
+    xa = O.resistor_network_solution(prob, p_y)[O.build_permutation(prob)[0]]
+    yield grp, xa
+    grp.close()
+
+
+def test_c4_single_gpu(c4):
+    grp, xa = c4
+    mesh = grp.meshes[0].with_comm(None)
+    E, B = mesh.num_edges, len(mesh.bifurcation_values)
+    assert (E, B) == (262_143, 131_071)
+    asm = HydraulicNetworkAssembler(mesh)
+    try:
+        asm.compute_forms(p_bc_ex=p_y)
+        asm.assemble()
+        h = asm.handle
+        assert h.n_rows == E * (2 * N + 1) + B == 10_354_648
+        assert h.nnz == E * (7 * N + 1) + 6 * B == 35_913_588
+        it, relres, conv = h.solve(1e-12, 50000, 4)
+        assert conv and it == 3, (it, relres)
+        x = h.solution()
+        err = np.linalg.norm(x - xa) / np.linalg.norm(xa)
+        assert err <= TOL, err
+        assert h.true_residual() < 1e-9
+        rp, col, val = h.csr()
+        A = sp.csr_matrix((val, col, rp), shape=(h.n_rows, h.n_rows))
+        At = A.T.tocsr()
+        At.sort_indices()
+        np.testing.assert_array_equal(A.indptr, At.indptr)
+        np.testing.assert_array_equal(A.indices, At.indices)
+        np.testing.assert_array_equal(A.data, At.data)  # exactly symmetric
+    finally:
+        asm.close()
+
+
+def test_c4_eight_rank_group(c4):
+    grp, xa = c4
+    grp.compute_forms(p_bc_ex=p_y)
+    grp.assemble()
+    it, relres, conv = grp.solve(1e-12, 50000, 4)
+    assert conv and it == 3, (it, relres)
+    m0 = grp.meshes[0]
+    E = m0.num_edges
+    seen = np.zeros(xa.size, dtype=np.int64)
+    num = den = 0.0
+    for r, (a, xl) in enumerate(zip(grp.assemblers, grp.solutions())):
+        rows = DM.global_rows(a.local_problem, E, m0.bifurcation_index)
+        seen[rows] += 1
+        d = xl - xa[rows]
+        err_r = np.linalg.norm(d) / np.linalg.norm(xa[rows])
+        assert err_r <= TOL, (r, err_r)  # every rank's rows, not just the total
+        num += float(d @ d)
+        den += float(xa[rows] @ xa[rows])
+    assert np.all(seen == 1)  # the partition covers every DoF exactly once
+    assert np.sqrt(num / den) <= TOL

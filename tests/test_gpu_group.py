@@ -221,6 +221,30 @@ def test_group_ranks_with_different_schedules_fail_loudly(monkeypatch):
         grp.close()
 
 
+def test_group_rank_without_dense_top_fails_loudly(monkeypatch):
+    """The dense top part is decided per rank (nx_set_pc_dense); it drives who packs the
+    halo and beta^2 (fuse_pack). A rank without it must make the solve fail through the
+    schedule check, never run with peers reading stale halo values."""
+    from networks_fenicsx_amd._lib import NxError
+
+    make, N, strategy, pbc = CASES["depth6_N40"]
+    grp = RankGroup(make(), N, 2, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.assemble()
+        monkeypatch.setenv("NXHIP_PC_DENSE", "0")
+        grp.assemblers[1].set_preconditioner(True)
+        monkeypatch.delenv("NXHIP_PC_DENSE")
+        with pytest.raises(NxError, match="different kernel schedules"):
+            grp.solve(1e-12, 50000, 4)
+        grp._close_group()
+        grp.assemblers[1].set_preconditioner(True)
+        it, _, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and it <= 4
+    finally:
+        grp.close()
+
+
 def test_group_rehearsal_four_ranks_depth16():
     """4 ranks x make_tree(17) (1 M rows per rank): the size at which the depth-cut
     decomposition put a job over the LDS caps on some ranks and the ranks diverged

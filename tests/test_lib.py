@@ -83,3 +83,27 @@ def test_create_fe_argument_errors():
     bad.b_ptr[1], bad.b_ptr[2] = bad.b_ptr[2] + 1, bad.b_ptr[1]
     with pytest.raises(_lib.NxError, match="monotone"):
         _lib.Handle.create_fe(0, bad)
+
+
+def test_import_order_single_runtime_clean_exit():
+    """Loading ``libnxhip.so`` BEFORE importing torch (the "wrong" order) must still give
+    one HIP runtime in the process and a clean exit: ``_lib.lib()`` imports torch first
+    when it is importable (a process that maps the library before torch's HIP libraries
+    aborts at exit)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from networks_fenicsx_amd import _lib\n"
+        "_lib.lib()\n"
+        "import torch\n"
+        "maps = open('/proc/self/maps').read().splitlines()\n"
+        "libs = {l.split()[-1] for l in maps if 'libamdhip64' in l}\n"
+        "assert len(libs) == 1, libs\n"
+        "print('single runtime:', libs.pop())\n"
+    ) % str(HEADER.parent.parent)
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=600, cwd="/tmp")
+    assert res.returncode == 0, (res.returncode, res.stdout, res.stderr[-2000:])
+    assert "single runtime" in res.stdout
