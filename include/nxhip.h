@@ -58,7 +58,7 @@ int nx_device_count(int32_t* count);
 /*
  * Create a network handle on `device` and build the CSR sparsity pattern on it.
  * Replaces Solver.__init__'s fem.petsc.create_matrix / create_vector
- * (solver.py:441-447) and the DoF layout of HydraulicNetworkAssembler.__init__
+ * (solver.py:43-49) and the DoF layout of HydraulicNetworkAssembler.__init__
  * (assembly.py:121-162).
  *
  *   N          cells per edge (>= 1)
@@ -132,13 +132,13 @@ int nx_set_source(nx_network_t* h, const double* edge_f);
 /*
  * Assemble matrix values and/or rhs on the device into the resident CSR.
  * Replaces HydraulicNetworkAssembler.assemble (assembly.py:329-368) and
- * Solver.assemble (solver.py:488-499). Asynchronous on the handle's stream.
+ * Solver.assemble (solver.py:90-101). Asynchronous on the handle's stream.
  */
 int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs);
 
 /*
  * MINRES (Paige-Saunders) on the device; replaces the KSP solve of
- * Solver.solve (solver.py:505-533; default there: LU/MUMPS).
+ * Solver.solve (solver.py:107-135; default there: LU/MUMPS).
  *   rtol         stop when the MINRES residual estimate ||r_k|| / ||b|| <= rtol
  *   maxit        iteration cap
  *   check_every  iterations per host convergence check (graph chunk), >= 2, even
@@ -154,7 +154,7 @@ int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_every,
  * P = blockdiag(M, G^T M^{-1} G) with M the consistent flux mass (3 iterations), or with the
  * lumped mass D (nx_set_pc_exact; networks_fenicsx_amd/precond.py derives both and builds
  * these arrays). There is no reference counterpart: the reference factorises with MUMPS
- * (solver.py:456-463); this makes the iterative replacement converge in 3 iterations.
+ * (solver.py:58-65); this makes the iterative replacement converge in 3 iterations.
  * enable = 0 switches back to unpreconditioned MINRES. Chains (one per local edge, in job
  * order): edge slot, flip (chain runs target -> source), top / bottom junction slot (-1 =
  * ground). Junction slots (one per owned multiplier, level order per job): multiplier row,
@@ -279,7 +279,7 @@ int nx_bench_spmv_cold(nx_network_t* h, int32_t reps, int32_t* copies, double* m
  * Multi-GPU (one process per GPU). Rank 0 creates the RCCL unique id, the
  * host control plane (torch.distributed) broadcasts it, every rank calls
  * nx_comm_init with its halo plan. Replaces the MPI ghost updates
- * (assembly.py:363-367, solver.py:526-530) and MUMPS' internal communication.
+ * (assembly.py:363-367, solver.py:128-132) and MUMPS' internal communication.
  *   n_peers                 neighbouring ranks
  *   peer_rank[n_peers]
  *   send_off[n_peers+1], send_idx[...]   owned local rows to send to each peer

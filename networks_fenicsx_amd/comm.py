@@ -1,7 +1,7 @@
 """Minimal communicator used by the host-side classes.
 
-The reference passes an ``mpi4py`` communicator around (``mesh.py:114``) and uses
-``bcast``/``barrier``/``allreduce`` on it (``mesh.py:252-275``,
+The reference passes an ``mpi4py`` communicator around (``mesh.py:89, 113-115``) and uses
+``bcast``/``barrier``/``allreduce`` on it (``mesh.py:227-250``,
 ``demos/demo_tree.py:64-71``). There is no MPI here: one process per GPU is
 launched by ``torch.distributed.run`` and host-side control messages go over
 ``torch.distributed`` (gloo for objects). The device data path (Krylov dot

@@ -1,4 +1,4 @@
-"""``dolfinx.io.VTXWriter`` stand-in (``demos/demo_tree.py:56-62`` and the other demos).
+"""``dolfinx.io.VTXWriter`` stand-in (``demos/demo_tree.py:57-62`` and the other demos).
 
 ADIOS2 is not available, so the writer creates the ``.bp`` path as a directory and writes
 one ``step_<k>.npz`` per ``write(t)`` with every function's values, its graph edges and the

@@ -3,9 +3,9 @@
 //
 // Reference semantics (files under /root/reference/src/networks_fenicsx/):
 //   forms            assembly.py:243-277 (mass, divergence, gradient, junctions, rhs)
-//   assemble         assembly.py:328-368, solver.py:488-499
-//   solve            solver.py:505-533 (PETSc KSP; MUMPS LU by default) -> MINRES here
-//   mesh geometry    mesh.py:295-347 (interior points x_u (1-w) + x_v w, w = k/N)
+//   assemble         assembly.py:328-368, solver.py:90-101
+//   solve            solver.py:107-135 (PETSc KSP; MUMPS LU by default) -> MINRES here
+//   mesh geometry    mesh.py:269-322 (interior points x_u (1-w) + x_v w, w = k/N)
 //
 // Layout per rank (see include/nxhip.h): edge e owns rows [e(2N+1), (e+1)(2N+1)),
 // interleaved q_0 p_0 q_1 ... p_{N-1} q_N, then the owned multipliers. With this
@@ -233,7 +233,7 @@ __device__ __forceinline__ void vertex(const double* x0, const double* x1, int k
   } else if (k == N) {
     p[0] = x1[0]; p[1] = x1[1]; p[2] = x1[2];
   } else {
-    // numpy: w = k * (1/N); start * (1 - w) + end * w   (mesh.py:300, 315)
+    // numpy: w = k * (1/N); start * (1 - w) + end * w   (mesh.py:275, 290)
     const double w = (double)k * invN;
     const double om = 1.0 - w;
     p[0] = x0[0] * om + x1[0] * w;
@@ -3298,7 +3298,7 @@ struct FeArgs {
   int lhs, do_rhs;
 };
 
-// length of cell c of edge e, vertices generated like the reference mesh (mesh.py:300-316)
+// length of cell c of edge e, vertices generated like the reference mesh (mesh.py:275-291)
 __device__ __forceinline__ double fe_cell_h(const double* __restrict__ edge_x, int64_t cell, int N) {
 #pragma clang fp contract(off)
   const int64_t e = cell / N;

@@ -1,7 +1,7 @@
 """Light function-space / function objects returned by the solver.
 
 The reference returns DOLFINx ``fem.Function`` objects
-``[flux_color_0, ..., flux_color_{M-1}, pressure, global_flux]`` (``solver.py:518-533``).
+``[flux_color_0, ..., flux_color_{M-1}, pressure, global_flux]`` (``solver.py:120-135``).
 These classes keep the attributes the reference's callers use
 (``.x.array``, ``.name``, ``.function_space``, ``.function_space.mesh``,
 ``.function_space.element.basix_element.degree``) without DOLFINx.

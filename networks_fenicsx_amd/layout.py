@@ -3,7 +3,7 @@
 The reference's DoF layout is DOLFINx's: one P1 flux space per edge colour, one DG0
 pressure space and one DG0 multiplier space on the bifurcation point cloud
 (``assembly.py:121-162``), distributed by the DOLFINx graph partitioner
-(``mesh.py:356-373``). Here the layout is designed for the device instead:
+(``mesh.py:331-348``). Here the layout is designed for the device instead:
 
 * every graph edge owns ``2N+1`` consecutive DoFs, interleaved
   ``[q_0, p_0, q_1, p_1, ..., p_{N-1}, q_N]`` (flux vertices / pressure cells,

@@ -1,27 +1,27 @@
 """Graph -> 1-D network topology (host side).
 
-Re-designs the reference's ``NetworkMesh`` (``src/networks_fenicsx/mesh.py:70-563``)
+Re-designs the reference's ``NetworkMesh`` (``src/networks_fenicsx/mesh.py:45-538``)
 without DOLFINx. What the hot path needs from it is *topology*, not a general
 finite-element mesh:
 
 * the edge list in ``graph.edges()`` order and the node coordinates
-  (``mesh.py:205, 299``);
-* the edge colouring (``mesh.py:54-67``), which only decides how the solution is
+  (``mesh.py:180, 274``);
+* the edge colouring (``mesh.py:29-42``), which only decides how the solution is
   grouped into per-colour flux functions on output;
 * node degrees -> ``bifurcation_values`` (degree > 1, ascending) and
-  ``boundary_values`` (degree == 1) (``mesh.py:207-211``);
-* per-bifurcation in/out colour lists (``mesh.py:214-234``);
+  ``boundary_values`` (degree == 1) (``mesh.py:182-186``);
+* per-bifurcation in/out colour lists (``mesh.py:189-209``);
 * boundary nodes split into inlets/outlets with the ``in_marker = 3 * #nodes`` /
-  ``out_marker = 5 * #nodes`` tags (``mesh.py:236-250, 427-433``).
+  ``out_marker = 5 * #nodes`` tags (``mesh.py:211-225, 402-408``).
 
 The interval mesh itself (``N`` cells per edge, interior points
-``x_u (1 - k/N) + x_v (k/N)``, ``mesh.py:295-347``) is kept as a light
+``x_u (1 - k/N) + x_v (k/N)``, ``mesh.py:269-322``) is kept as a light
 :class:`IntervalMesh` built with vectorised numpy for tests and post-processing;
 the device kernels regenerate the same points on the fly from the two edge end
 points, so the mesh is never shipped to the GPU.
 
 Cells are always stored source -> target, so the orientation field
-(``mesh.py:390-425``) is identically +1 and the unit tangent of every cell is the
+(``mesh.py:365-400``) is identically +1 and the unit tangent of every cell is the
 source -> target direction of its graph edge.
 """
 
@@ -44,7 +44,7 @@ def color_graph(
     graph: nx.DiGraph,
     strategy: str | Callable[[nx.Graph, dict[int, int]], Iterable[int]] | None,
 ) -> dict[tuple[int, int], int]:
-    """Greedy colouring of the line graph (reference ``mesh.py:54-67``).
+    """Greedy colouring of the line graph (reference ``mesh.py:29-42``).
 
     ``strategy=None`` gives every edge its own colour (edge index in
     ``graph.edges()`` order). Otherwise the same networkx call as the reference
@@ -161,7 +161,7 @@ def interval_points(pos3: np.ndarray, src: np.ndarray, dst: np.ndarray, N: int) 
     """Interior points of every edge, exactly as the reference computes them.
 
     ``start * (1 - w) + end * w`` with ``w = np.linspace(0, 1, N, endpoint=False)[1:]``
-    (reference ``mesh.py:300, 315``). Returns ``(E * (N - 1), 3)``.
+    (reference ``mesh.py:275, 290``). Returns ``(E * (N - 1), 3)``.
     """
     w = np.linspace(0, 1, N, endpoint=False)[1:][None, :, None]  # (1, N-1, 1)
     start = pos3[src][:, None, :]
@@ -229,7 +229,7 @@ class NetworkMesh:
         deg = self._degree
         self._bifurcation_values = np.flatnonzero(deg > 1).astype(np.int32)
         self._boundary_values = np.flatnonzero(deg == 1).astype(np.int32)
-        # inlets/outlets (reference mesh.py:236-250): a degree-1 node with an
+        # inlets/outlets (reference mesh.py:211-225): a degree-1 node with an
         # in-edge is an outlet leaf (in_marker), with an out-edge a root (out_marker)
         indeg = np.bincount(self._dst, minlength=n_nodes)
         bnd = self._boundary_values
@@ -277,7 +277,7 @@ class NetworkMesh:
         if src.size and all("radius" in graph.edges[e] for e in graph.edges):
             radius = np.fromiter((graph.edges[e]["radius"] for e in graph.edges),
                                  dtype=np.float64, count=src.size)
-        # in/out colours per node in networkx adjacency order (reference mesh.py:218-234)
+        # in/out colours per node in networkx adjacency order (reference mesh.py:193-209)
         in_nodes, in_cols, out_nodes, out_cols = [], [], [], []
         for v, preds in graph.pred.items():
             for u in preds:
@@ -412,12 +412,12 @@ class NetworkMesh:
         return self._boundary_out_nodes
 
     def in_edges(self, bifurcation_idx: int) -> npt.NDArray[np.int32]:
-        """Colours of the in-edges of bifurcation ``bifurcation_idx`` (reference ``mesh.py:540``)."""
+        """Colours of the in-edges of bifurcation ``bifurcation_idx`` (reference ``mesh.py:515-519``)."""
         assert bifurcation_idx < len(self.bifurcation_values)
         return self._bifurcation_in_color.links(int(bifurcation_idx))
 
     def out_edges(self, bifurcation_idx: int) -> npt.NDArray[np.int32]:
-        """Colours of the out-edges of bifurcation ``bifurcation_idx`` (reference ``mesh.py:546``)."""
+        """Colours of the out-edges of bifurcation ``bifurcation_idx`` (reference ``mesh.py:521-525``)."""
         assert bifurcation_idx < len(self.bifurcation_values)
         return self._bifurcation_out_color.links(int(bifurcation_idx))
 
@@ -443,7 +443,7 @@ class NetworkMesh:
 
     @property
     def subdomains(self) -> MeshTags:
-        """Cell tags = edge colour (reference ``mesh.py:379-388``)."""
+        """Cell tags = edge colour (reference ``mesh.py:353-363``)."""
         if self._subdomains is None:
             vals = np.repeat(self._edge_color, self._N)
             self._subdomains = MeshTags(1, np.arange(vals.size), vals, "subdomains")
@@ -451,7 +451,7 @@ class NetworkMesh:
 
     @property
     def boundaries(self) -> MeshTags:
-        """Vertex tags: node id, or in/out marker on boundary nodes (``mesh.py:427-445``)."""
+        """Vertex tags: node id, or in/out marker on boundary nodes (``mesh.py:402-420``)."""
         if self._facet_markers is None:
             used = np.flatnonzero(self._degree > 0)
             vals = used.astype(np.int64).copy()

@@ -34,7 +34,7 @@ def tree_arrays(n: int, H: float, W: float, dim: int = 3):
 
     This is what the device path consumes; :func:`make_tree` wraps it into a
     ``networkx.DiGraph``. Node ``c >= 2`` is a child of ``c // 2``; nodes of each
-    generation are sorted by x (reference ``network_generation.py:78-95``).
+    generation are sorted by x (reference ``network_generation.py:77-95``).
     """
     assert n >= 1, "Number of generations must be at least 1"
     per_gen = [2**g for g in range(n)]

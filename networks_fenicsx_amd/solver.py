@@ -3,7 +3,7 @@
 Mirrors ``Solver`` of the reference (``src/networks_fenicsx/solver.py:16-143``):
 same constructor signature, ``assemble``, ``solve``, ``A``, ``b``, ``ksp`` and
 ``assembler`` accessors. The reference factorises the system with MUMPS
-(``preonly`` + ``lu``, ``solver.py:456-463``); here the symmetric-indefinite system is
+(``preonly`` + ``lu``, ``solver.py:58-65``); here the symmetric-indefinite system is
 solved by MINRES running entirely on the GPU (``nx_solve`` in ``csrc/nxhip.hip``):
 CSR SpMV, fused vector updates and deterministic reductions, chunked into HIP graphs
 with one host convergence check per chunk.

@@ -3,8 +3,8 @@
 The reference decorates its setup and hot-path functions with
 ``dolfinx.common.timed("nxfx:...")`` and reads them back with
 ``dolfinx.common.timing(name) -> (count, timedelta)``
-(reference ``demos/demo_perf.py:85-150``; timer names at ``mesh.py:54,142,163,450``,
-``assembly.py:28,120,164,328``, ``solver.py:505``, ``network_generation.py:41,157``).
+(reference ``demos/demo_perf.py:85-150``; timer names at ``mesh.py:29,117,138,425``,
+``assembly.py:28,120,164,328``, ``solver.py:107``, ``network_generation.py:41,157``).
 This module keeps the same names and the same read-back shape so that
 demo_perf-style scripts keep working without DOLFINx.
 

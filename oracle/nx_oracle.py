@@ -10,7 +10,7 @@ The reference assembles a mixed (M+2)x(M+2) block system with DOLFINx/FFCx and
 solves it with PETSc/MUMPS. Neither is in this image, so this is a line-by-line
 restatement of the *forms* in numpy, assembled cell by cell in the reference's
 block layout and solved with SuperLU (``scipy.sparse.linalg.spsolve``, the
-direct-solver stand-in for MUMPS, reference ``solver.py:456-463``):
+direct-solver stand-in for MUMPS, reference ``solver.py:58-65``):
 
 * mass       ``R q v dx``                     -> ``R h/3, R h/6``   (``assembly.py:253``)
 * divergence ``phi (grad q . t) dx``          -> ``[-1, +1]`` on (p_cell, q_up/q_down)
@@ -22,10 +22,10 @@ direct-solver stand-in for MUMPS, reference ``solver.py:456-463``):
 * junctions  ``+-mu q ds``, ``+-lmbda v ds``  -> ``+1`` at in-edge ends, ``-1`` at out-edge
                                                starts, both blocks (``assembly.py:271-277``)
 
-Geometry follows the reference mesh generator (``mesh.py:300-316``): interior points
+Geometry follows the reference mesh generator (``mesh.py:275-291``): interior points
 ``start * (1 - w) + end * w`` with ``w = linspace(0, 1, N, endpoint=False)[1:]``,
 cell length = Euclidean norm of the cell's vertex difference, tangent source->target
-(orientation semantics ``mesh.py:390-425``, pinned by ``tests/test_orientation.py`` of
+(orientation semantics ``mesh.py:365-400``, pinned by ``tests/test_orientation.py`` of
 the reference).
 
 Block layout (the reference's function-space order, ``assembly.py:317-321``):
@@ -88,7 +88,7 @@ class OracleProblem:
 
 
 def build_problem(pos, src, dst, N: int, colors=None) -> OracleProblem:
-    """Topology + reference block layout (reference ``mesh.py:200-250``, ``assembly.py:120-162``)."""
+    """Topology + reference block layout (reference ``mesh.py:175-225``, ``assembly.py:120-162``)."""
     pos = np.asarray(pos, dtype=np.float64)
     n_nodes = pos.shape[0]
     pos3 = np.zeros((n_nodes, 3))
@@ -127,7 +127,7 @@ def cell_geometry(prob: OracleProblem):
     """Per-cell vertex coordinates and lengths, edge-major ``(E, N)``.
 
     Vertex k of edge e: ``x_u`` (k=0), ``x_v`` (k=N), else ``x_u (1-w_k) + x_v w_k``
-    with the reference's ``np.linspace`` weights (``mesh.py:300, 315``).
+    with the reference's ``np.linspace`` weights (``mesh.py:275, 290``).
     """
     N = prob.N
     start = prob.pos3[prob.src][:, None, :]
@@ -204,7 +204,7 @@ def assemble_reference(prob: OracleProblem, p_bc, f: float = 0.0, R=1.0):
 
 
 def solve_reference(A, b) -> np.ndarray:
-    """Direct sparse solve (SuperLU standing in for MUMPS LU, ``solver.py:456-463``)."""
+    """Direct sparse solve (SuperLU standing in for MUMPS LU, ``solver.py:58-65``)."""
     return spla.spsolve(A.tocsc(), b)
 
 
