@@ -243,6 +243,20 @@ int nx_get_graph_mode(nx_network_t* h, int32_t* graph);
 int nx_get_solution(nx_network_t* h, double* x);
 int nx_get_rhs(nx_network_t* h, double* b);
 
+/* The solution in the reference's function order -- what Solver.solve assigns into
+ * [flux_color_0 .. flux_color_{M-1}, pressure, global_flux] (solver.py:120-134,
+ * dolfinx.fem.petsc.assign). nx_set_output_map uploads once the permutation `rows`
+ * (n_rows entries, a permutation of the owned rows: output position -> device row);
+ * nx_get_solution_blocks gathers x into that order on the device and copies it to `out`
+ * (n_rows doubles; pinned memory from nx_host_alloc makes the copy one DMA at PCIe
+ * speed). Synchronous: `out` is complete when it returns. */
+int nx_set_output_map(nx_network_t* h, int64_t n, const int32_t* rows);
+int nx_get_solution_blocks(nx_network_t* h, double* out);
+
+/* Page-locked host memory for nx_get_solution_blocks (hipHostMalloc / hipHostFree). */
+int nx_host_alloc(int64_t bytes, void** out);
+int nx_host_free(void* p);
+
 /* Owned part of an internal vector (n_rows doubles): 0 = solution, 1 = rhs,
  * 2 = the latest preconditioned residual z = P^{-1} r (with the preconditioner). */
 int nx_get_vector(nx_network_t* h, int32_t which, double* out);

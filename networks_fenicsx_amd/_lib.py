@@ -10,11 +10,13 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
+import weakref
 from pathlib import Path
 
 import numpy as np
 
-__all__ = ["lib", "NxError", "NxNotConverged", "check", "Handle", "Group", "EXPORTED_SYMBOLS"]
+__all__ = ["lib", "NxError", "NxNotConverged", "check", "Handle", "Group", "PinnedPool",
+           "EXPORTED_SYMBOLS"]
 
 _LIB_PATH = Path(os.environ.get("NXHIP_LIB") or Path(__file__).resolve().parent / "libnxhip.so")
 _lock = threading.Lock()
@@ -47,6 +49,10 @@ _SIGS = {
     "nx_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
     "nx_get_solution": (C.c_int, [_h, _pd]),
     "nx_get_rhs": (C.c_int, [_h, _pd]),
+    "nx_set_output_map": (C.c_int, [_h, _i64, _pi32]),
+    "nx_get_solution_blocks": (C.c_int, [_h, C.c_void_p]),
+    "nx_host_alloc": (C.c_int, [_i64, C.POINTER(C.c_void_p)]),
+    "nx_host_free": (C.c_int, [C.c_void_p]),
     "nx_get_vector": (C.c_int, [_h, _i32, _pd]),
     "nx_get_csr": (C.c_int, [_h, _pi32, _pi32, _pd]),
     "nx_spmv_host": (C.c_int, [_h, _pd, _pd]),
@@ -261,6 +267,20 @@ class Handle:
         check(lib().nx_get_solution(self.ptr, _ptr(x, C.c_double)))
         return x
 
+    def set_output_map(self, rows: np.ndarray) -> None:
+        """Owned rows in output order (``nx_set_output_map``): the solver's function blocks."""
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        check(lib().nx_set_output_map(self.ptr, int(rows.size),
+                                      _ptr(rows if rows.size else np.zeros(1, np.int32), C.c_int32)))
+
+    def solution_blocks(self, out: np.ndarray) -> np.ndarray:
+        """The solution permuted by the output map into ``out`` (n_rows doubles; pinned
+        memory from :class:`PinnedPool` makes the device-to-host copy one DMA)."""
+        if out.dtype != np.float64 or out.size != self.n_rows or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a contiguous float64 array of {self.n_rows} entries")
+        check(lib().nx_get_solution_blocks(self.ptr, C.c_void_p(out.ctypes.data)))
+        return out
+
     def rhs(self) -> np.ndarray:
         b = np.empty(self.n_rows, dtype=np.float64)
         check(lib().nx_get_rhs(self.ptr, _ptr(b, C.c_double)))
@@ -438,6 +458,60 @@ class Group:
             self.close()
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
+
+
+class _PinnedView:
+    """numpy base object of one pinned buffer: while any array (or view of one) made from it
+    is alive, the pool does not hand the buffer out again."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False),
+                                    "version": 3}
+
+
+def _host_free(ptr: int) -> None:
+    try:
+        lib().nx_host_free(C.c_void_p(ptr))
+    except Exception:  # noqa: BLE001 - interpreter shutdown
+        pass
+
+
+class PinnedPool:
+    """Page-locked host buffers of ``n`` doubles (``nx_host_alloc``), reused once every array
+    handed out from a buffer has been dropped. The solver's output functions are views into
+    one such buffer, so a solve costs one gather kernel and one DMA instead of a pageable copy
+    plus a host-side split per colour."""
+
+    def __init__(self, n: int):
+        self._n = int(n)
+        self._slots: list[list] = []  # [ptr, weakref to the live _PinnedView or None]
+
+    def take(self) -> np.ndarray:
+        for s in self._slots:
+            if s[1] is None or s[1]() is None:
+                return self._wrap(s)
+        p = C.c_void_p()
+        check(lib().nx_host_alloc(8 * max(self._n, 1), C.byref(p)))
+        s = [int(p.value), None]
+        self._slots.append(s)
+        return self._wrap(s)
+
+    def _wrap(self, s) -> np.ndarray:
+        v = _PinnedView(s[0], self._n)
+        s[1] = weakref.ref(v)
+        return np.asarray(v)
+
+    def close(self) -> None:
+        for ptr, ref in self._slots:
+            v = ref() if ref is not None else None
+            if v is None:
+                _host_free(ptr)
+            else:  # still viewed by a caller's arrays: free when the last one goes
+                weakref.finalize(v, _host_free, ptr)
+        self._slots = []
+
+    def __del__(self):
+        self.close()
 
 
 def set_lean(enable: bool) -> None:

@@ -33,7 +33,7 @@ import numpy as np
 
 from . import _lib
 from .comm import GroupRankComm
-from .fem import Constant, FunctionSpace
+from .fem import Constant, Function, FunctionSpace
 from .element import stable_pair
 from .layout import LocalProblem, build_local_problem
 from .layout_fe import FeLayout, build_fe_layout
@@ -154,6 +154,52 @@ class DeviceMatrix:
         return self._handle.spmv(x)
 
 
+class FormBlock:
+    """Block ``a[i][j]`` (bilinear, ``j`` given) or ``L[i]`` (linear) of the reference's
+    nested forms (``assembly.py:194-299``: row block = test space ``i``, column block =
+    trial space ``j``, spaces ordered ``[flux_color_0 .., pressure, multiplier]``).
+
+    ``kind`` names the term of ``compute_forms`` it holds: ``"mass"`` (``R q v dx``, a[c][c],
+    ``:253``), ``"divergence"`` (``phi dq/ds``, a[M][c], ``:254``), ``"gradient"``
+    (``-p dv/ds``, a[c][M], ``:255``), ``"junction"`` (``+-mu q`` / ``+-lambda v``,
+    a[M+1][c] and a[c][M+1], ``:271-277``), ``"boundary"`` (``+-p_bc v ds``, L[c], ``:258``),
+    ``"source"`` (``f phi dx``, L[M], ``:262``) or ``"zero"`` (L[M+1]). Blocks the reference
+    sets to ``None`` (``:284-287``) are ``None`` here too.
+
+    :meth:`assemble` extracts the block from the device-assembled system in the reference's
+    signs (the device stores the pressure rows negated, which makes the system symmetric):
+    a ``scipy.sparse.csr_matrix`` over this rank's owned rows/columns, or the rhs slice."""
+
+    def __init__(self, assembler: "HydraulicNetworkAssembler", kind: str, i: int,
+                 j: int | None = None):
+        self._asm = assembler
+        self.kind = kind
+        self.i, self.j = i, j
+        self.rank = 2 if j is not None else 1
+
+    @property
+    def function_spaces(self):
+        V = self._asm.function_spaces
+        return [V[self.i]] if self.j is None else [V[self.i], V[self.j]]
+
+    def assemble(self):
+        asm = self._asm
+        rows = asm._block_rows(self.i)
+        sign = -1.0 if self.i == len(asm.function_spaces) - 2 else 1.0  # pressure rows
+        if self.j is None:
+            return sign * asm.handle.rhs()[rows]
+        import scipy.sparse as sp
+
+        h = asm.handle
+        rp, col, val = h.csr()
+        A = sp.csr_matrix((val, col, rp), shape=(h.n_rows, h.n_cols))
+        return (sign * A[rows][:, asm._block_rows(self.j)]).tocsr()
+
+    def __repr__(self) -> str:
+        idx = f"[{self.i}]" if self.j is None else f"[{self.i}][{self.j}]"
+        return f"FormBlock{idx}({self.kind})"
+
+
 class HydraulicNetworkAssembler:
     """Assembler for the mixed hydraulic network problem
 
@@ -231,6 +277,7 @@ class HydraulicNetworkAssembler:
         self._lm_space = FunctionSpace(mesh, "multiplier", "DG", 0, True, fe.lm_nodes.size)
         self._p_idx = fe.p_rows
         self._lm_idx = fe.lm_rows
+        self._set_output_map()
 
     def _init_comm(self) -> None:
         comm = self._network_mesh.comm
@@ -268,6 +315,16 @@ class HydraulicNetworkAssembler:
         self._p_idx = (np.arange(lp.edges.size)[:, None] * per
                        + 2 * np.arange(N)[None, :] + 1).ravel()
         self._lm_idx = lp.n_edge_dofs + np.arange(lp.lm_nodes.size)
+        self._set_output_map()
+
+    def _set_output_map(self) -> None:
+        """Upload the function-block order of the owned rows (``nx_set_output_map``): the
+        solution then reaches the host already split into ``[flux_color_0 .., pressure,
+        global_flux]`` (``solver.py:120-134``), each function a slice of one buffer."""
+        blocks = [*self._flux_idx, self._p_idx, self._lm_idx]
+        self._out_off = np.concatenate([[0], np.cumsum([b.size for b in blocks])]).astype(np.int64)
+        self._handle.set_output_map(np.concatenate(blocks))
+        self._out_pool = _lib.PinnedPool(self._handle.n_rows)
 
     def set_preconditioner(self, enable: bool) -> bool:
         """Switch the device MINRES between preconditioned and plain; returns the state
@@ -328,9 +385,20 @@ class HydraulicNetworkAssembler:
         edge_bc = edge_boundary_rhs(mesh, edge_ids, pbc)
         self._handle.set_coefficients(R_edge, R_const, f_val, edge_bc)
         self._handle.set_source(f_edge)
-        self._a = ("device-forms", R_const if R_edge is None else "per-edge",
-                   f_val if f_edge is None else "per-edge")
-        self._L = ("device-rhs", pbc)
+        self._coefficients = {"R": R_const if R_edge is None else "per-edge",
+                              "f": f_val if f_edge is None else "per-edge", "p_bc": pbc}
+        M = len(self._flux_spaces)
+        n = M + 2
+        a: list[list[FormBlock | None]] = [[None] * n for _ in range(n)]
+        for c in range(M):
+            a[c][c] = FormBlock(self, "mass", c, c)
+            a[M][c] = FormBlock(self, "divergence", M, c)
+            a[c][M] = FormBlock(self, "gradient", c, M)
+            a[M + 1][c] = FormBlock(self, "junction", M + 1, c)
+            a[c][M + 1] = FormBlock(self, "junction", c, M + 1)
+        self._a = a
+        self._L = [FormBlock(self, "boundary", c) for c in range(M)]
+        self._L += [FormBlock(self, "source", M), FormBlock(self, "zero", M + 1)]
 
     # ---------------------------------------------------------------- assemble
     @timed("nxfx:HydraulicNetworkAssembler:assemble")
@@ -344,8 +412,9 @@ class HydraulicNetworkAssembler:
         """
         if self._a is None:
             raise RuntimeError("compute_forms() must be called before assemble()")
+        # enqueued on the handle's stream: the solve (same stream) and every host read of
+        # the matrix / rhs order after it, so the host does not wait here
         self._handle.assemble(assemble_lhs, assemble_rhs)
-        self._handle.sync()
         if A is None and assemble_lhs:
             A = DeviceMatrix(self._handle, kind)
         if b is None and assemble_rhs:
@@ -405,10 +474,14 @@ class HydraulicNetworkAssembler:
         return self._a
 
     def bilinear_form(self, i: int, j: int):
-        n = len(self.function_spaces)
-        if i >= n or j >= n:
+        """Block ``a[i][j]`` (reference ``assembly.py:378-383``): a :class:`FormBlock`, or
+        None where the reference's block is None; out of range logs an error and raises."""
+        a = self.bilinear_forms
+        if a is None:
+            return None
+        if i >= len(a) or j >= len(a[i]):
             logging.error("Bilinear form a[%d][%d] out of range", i, j)
-        return self.bilinear_forms
+        return a[i][j]
 
     @property
     def linear_forms(self):
@@ -418,17 +491,49 @@ class HydraulicNetworkAssembler:
         return self._L
 
     def linear_form(self, i: int):
-        if i >= len(self.function_spaces):
+        """Block ``L[i]`` (reference ``assembly.py:393-398``)."""
+        L = self.linear_forms
+        if L is None:
+            return None
+        if i >= len(L):
             logging.error("Linear form L[%d] out of range", i)
-        return self.linear_forms
+        return L[i]
+
+    def _block_rows(self, i: int) -> np.ndarray:
+        """Owned device rows of function block ``i`` in the block's DoF order."""
+        blocks = [*self._flux_idx, self._p_idx, self._lm_idx]
+        return np.asarray(blocks[i], dtype=np.int64)
 
     def scatter_solution(self, x: np.ndarray, functions: list) -> list:
-        """Split the device-layout vector into ``[flux..., pressure, multiplier]``."""
+        """Split a host device-layout vector into ``[flux..., pressure, multiplier]``."""
         for fn, idx in zip(functions[:-2], self._flux_idx):
             fn.x.array[:] = x[idx]
         functions[-2].x.array[:] = x[self._p_idx]
         functions[-1].x.array[:] = x[self._lm_idx]
         return functions
 
+    def solution_functions(self, functions: list | None = None) -> list:
+        """The device solution as ``[flux_color_0 .., pressure, global_flux]`` (the
+        reference's ``assign``, ``solver.py:120-134``): one gather kernel into the block
+        order and one DMA into a pinned buffer. New functions are views of that buffer;
+        given ``functions`` are filled from it."""
+        buf = self._out_pool.take()
+        self._handle.solution_blocks(buf)
+        off = self._out_off
+        spaces = self.function_spaces
+        if functions is None:
+            names = [f"flux_color_{i}" for i in range(len(self._flux_spaces))]
+            names += ["pressure", "global_flux"]
+            return [Function(V, name=nm, array=buf[off[i]:off[i + 1]])
+                    for i, (V, nm) in enumerate(zip(spaces, names))]
+        if len(functions) != len(spaces):
+            raise ValueError(f"expected {len(spaces)} functions, got {len(functions)}")
+        for i, fn in enumerate(functions):
+            np.copyto(fn.x.array, buf[off[i]:off[i + 1]])
+        return functions
+
     def close(self) -> None:
+        pool = getattr(self, "_out_pool", None)
+        if pool is not None:
+            pool.close()
         self._handle.close()

@@ -2515,6 +2515,15 @@ __global__ void k_pack(const double* __restrict__ x, const int* __restrict__ idx
   if (i < n) buf[i] = x[idx[i]];
 }
 
+// Solution in the reference's block order (nx_get_solution_blocks): out[i] = x[idx[i]],
+// idx = the [flux colour 0 .. M-1 | pressure | multiplier] permutation of the owned rows.
+__global__ __launch_bounds__(kBlock) void k_gather_out(const double* __restrict__ x,
+                                                       const int* __restrict__ idx, int64_t n,
+                                                       double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = x[idx[i]];
+}
+
 // Halo pack + this rank's beta^2 (sum of the previous iteration's partials, block 0) into
 // red[1] and its own slot of the gathered array: saves a reduction launch per iteration.
 __global__ __launch_bounds__(kBlock) void k_pack_beta(const double* __restrict__ x,
@@ -2661,6 +2670,9 @@ struct nx_network {
   bool last_graph = false;    // the last nx_solve replayed HIP graphs
   // general element degrees (nx_create_fe): gather-assembly tables, one rank, no
   // preconditioner
+  // nx_set_output_map: owned rows in the reference's function order (Solver.solve output)
+  int* out_idx = nullptr;
+  int64_t n_out = 0;
   bool fe = false;
   int* fe_kind = nullptr;
   double* fe_tval = nullptr;
@@ -3431,7 +3443,7 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->partA,  h->partB,   h->red,
                   h->send_idx, h->send_buf, h->gath, h->d_seq,
                   h->fe_kind, h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent,
-                  h->fe_bptr, h->fe_bidx, h->fe_bent};
+                  h->fe_bptr, h->fe_bidx, h->fe_bent, h->out_idx};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -3990,6 +4002,57 @@ NX_API int nx_get_solution(nx_network_t* h, double* xo) {
   CHECK(set_device(h));
   HIPCALL(hipMemcpyAsync(xo, h->x, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
   HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_set_output_map(nx_network_t* h, int64_t n, const int32_t* rows) {
+  if (!h || (n > 0 && !rows)) return fail(NX_ERR_ARG, "null argument");
+  if (n != h->n_own) return fail(NX_ERR_ARG, "the output map must list every owned row once");
+  std::vector<char> seen((size_t)n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (rows[i] < 0 || rows[i] >= n || seen[(size_t)rows[i]])
+      return fail(NX_ERR_ARG, "the output map is not a permutation of the owned rows");
+    seen[(size_t)rows[i]] = 1;
+  }
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  if (h->out_idx) HIPCALL(hipFree(h->out_idx));
+  h->out_idx = nullptr;
+  h->n_out = 0;
+  if (n > 0) {
+    HIPCALL(hipMalloc((void**)&h->out_idx, sizeof(int) * n));
+    HIPCALL(hipMemcpy(h->out_idx, rows, sizeof(int) * n, hipMemcpyHostToDevice));
+  }
+  h->n_out = n;
+  return NX_OK;
+}
+
+NX_API int nx_get_solution_blocks(nx_network_t* h, double* out) {
+  if (!h || !out) return fail(NX_ERR_ARG, "null argument");
+  if (!h->out_idx && h->n_own > 0) return fail(NX_ERR_STATE, "nx_set_output_map first");
+  CHECK(set_device(h));
+  if (h->n_own > 0) {
+    // tmp (n_col >= n_own) is free outside nx_solve / nx_spmv_host
+    hipLaunchKernelGGL(k_gather_out, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
+                       h->x, h->out_idx, h->n_own, h->tmp);
+    HIPCALL(hipGetLastError());
+    HIPCALL(hipMemcpyAsync(out, h->tmp, sizeof(double) * h->n_own, hipMemcpyDeviceToHost,
+                           h->stream));
+  }
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_host_alloc(int64_t bytes, void** out) {
+  if (!out || bytes < 0) return fail(NX_ERR_ARG, "bad argument");
+  *out = nullptr;
+  if (bytes == 0) return NX_OK;
+  HIPCALL(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+  return NX_OK;
+}
+
+NX_API int nx_host_free(void* p) {
+  if (p) HIPCALL(hipHostFree(p));
   return NX_OK;
 }
 

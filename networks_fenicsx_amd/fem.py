@@ -73,8 +73,10 @@ class FunctionSpace:
 class Vector:
     """``.x`` of a :class:`Function` (DOLFINx ``la.Vector`` subset)."""
 
-    def __init__(self, n: int):
-        self.array = np.zeros(n, dtype=np.float64)
+    def __init__(self, n: int, array: np.ndarray | None = None):
+        if array is not None and array.shape != (n,):
+            raise ValueError(f"array must have shape ({n},)")
+        self.array = np.zeros(n, dtype=np.float64) if array is None else array
 
     def scatter_forward(self) -> None:
         return None
@@ -84,10 +86,14 @@ class Vector:
 
 
 class Function:
-    def __init__(self, V: FunctionSpace, name: str | None = None):
+    """``array``: an existing float64 buffer to use as ``x.array`` (the solver passes views
+    of its pinned output buffer)."""
+
+    def __init__(self, V: FunctionSpace, name: str | None = None,
+                 array: np.ndarray | None = None):
         self.function_space = V
         self.name = name or "f"
-        self.x = Vector(V.num_dofs)
+        self.x = Vector(V.num_dofs, array)
 
     def __repr__(self) -> str:
         return f"Function({self.name!r}, {self.function_space!r})"

@@ -39,7 +39,6 @@ import numpy as np
 
 from . import _lib
 from .assembly import DeviceMatrix, DeviceVector, HydraulicNetworkAssembler
-from .fem import Function
 from .timing import timed
 
 __all__ = ["Solver", "KSPInfo"]
@@ -122,6 +121,7 @@ class Solver:
         self._kind = kind
         self._A = DeviceMatrix(assembler.handle, kind)
         self._b = DeviceVector(assembler.handle)
+        self._closed = False
 
     @property
     def assembler(self) -> HydraulicNetworkAssembler:
@@ -149,12 +149,12 @@ class Solver:
 
     @timed("nxfx:Solver:solve")
     def solve(self, functions: list | None = None) -> list:
-        """Solve on the device and return ``[flux_color_0.., pressure, global_flux]``."""
-        if functions is None:
-            functions = [Function(V, name=f"flux_color_{i}")
-                         for i, V in enumerate(self.assembler.flux_spaces)]
-            functions.append(Function(self.assembler.pressure_space, name="pressure"))
-            functions.append(Function(self.assembler.lm_space, name="global_flux"))
+        """Solve on the device and return ``[flux_color_0.., pressure, global_flux]``
+        (``solver.py:107-135``). The functions are filled by one gather kernel and one DMA
+        (``HydraulicNetworkAssembler.solution_functions``); new ones are views of a pinned
+        buffer that is reused only after every function of that solve is dropped."""
+        if self._closed:
+            raise RuntimeError("the solver has been destroyed")
         h = self.assembler.handle
         if self.assembler.preconditioned != self._pc:
             self.assembler.set_preconditioner(self._pc)
@@ -170,9 +170,7 @@ class Solver:
             raise _lib.NxNotConverged(
                 f"MINRES did not converge: {it} iterations, relative residual {relres:.3e} "
                 f"> rtol {self._rtol:.1e}")
-        x = h.solution()
-        self.assembler.scatter_solution(x, functions)
-        return functions
+        return self.assembler.solution_functions(functions)
 
     def solution_vector(self) -> np.ndarray:
         """Device-layout solution (owned DoFs of this rank)."""
@@ -181,5 +179,18 @@ class Solver:
     def true_residual(self) -> float:
         return self.assembler.handle.true_residual()
 
+    def destroy(self) -> None:
+        """Release what the solver owns (the reference destroys its KSP, b and x,
+        ``solver.py:137-143``). The device matrix, rhs and Krylov vectors belong to the
+        assembler's handle (shared by every solver of that assembler) and go with
+        ``assembler.close()``; functions returned by :meth:`solve` stay valid."""
+        self._closed = True
+        self._ksp.destroy()
+        self._A = None
+        self._b = None
+
     def __del__(self):
-        return None
+        try:
+            self.destroy()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass

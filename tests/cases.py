@@ -54,6 +54,7 @@ CASES = {
     "Y_N4": (lambda: ng.make_tree(2, 1, 3), 4, None, p_y),
     "demo_tree_N2": (lambda: ng.make_tree(2, 1, 1), 2, None, p_y),
     "demo_tree_N1": (lambda: ng.make_tree(2, 1, 1), 1, None, p_y),
+    "demo_tree_N4": (lambda: ng.make_tree(2, 1, 1), 4, None, p_y),
     "double_Y_N5": (lambda: ng.make_tree(2, 3.1, 7.3), 5, None, p_x),
     "depth6_N40": (lambda: ng.make_tree(7, 7, 7), 40, "smallest_last", p_y),
     "arterial5_N40": (lambda: ng.make_arterial_tree(5, direction=np.array([0.1, 1, 0])), 40,
@@ -66,6 +67,10 @@ CASES = {
     "tree5_N16": (lambda: ng.make_tree(5, 5, 5), 16, "smallest_last", p_y),
     "tree5_3d_N31": (lambda: ng.make_tree(5, 2, 3), 31, "smallest_last", p_x),
 }
+
+# every configuration of tests/golden/systems.npz (tests/golden/make_golden.py)
+GOLDEN_CASES = ["Y_N4", "demo_tree_N2", "demo_tree_N4", "double_Y_N5", "depth6_N40",
+                "arterial5_N40"]
 
 
 def graph_arrays(G):

@@ -88,7 +88,8 @@ def main() -> None:
 
     systems = {}
     cases = {"Y_N4": ("Y", 4), "demo_tree_N2": ("demo_tree", 2), "demo_tree_N4": ("demo_tree", 4),
-             "double_Y_N5": ("double_Y", 5), "depth6_N40": ("depth6", 40)}
+             "double_Y_N5": ("double_Y", 5), "depth6_N40": ("depth6", 40),
+             "arterial5_N40": ("arterial5", 40)}  # C2, N = 40
     for case, (g, N) in cases.items():
         pos, edges = out[f"{g}/pos"], out[f"{g}/edges"]
         P = O.build_problem(pos, edges[:, 0], edges[:, 1], N)
@@ -104,6 +105,21 @@ def main() -> None:
         systems[f"{case}/rhs_build"] = bb
         systems[f"{case}/x_build"] = x[perm]
         systems[f"{case}/x_analytic_build"] = xa[perm]
+        if g.startswith("arterial"):
+            # C2 as demo_arterial_tree.py runs it (largest_first colouring): the solution in
+            # the reference's function order [flux colour blocks, pressure, multipliers]
+            import networkx as nx
+
+            G = ref.make_arterial_tree(**{**ARTERIAL[g],
+                                          "direction": np.asarray(ARTERIAL[g]["direction"])})
+            col = nx.coloring.greedy_color(nx.line_graph(G.to_undirected()),
+                                           strategy=nx.coloring.strategy_largest_first)
+            colors = np.asarray([col.get((u, v), col.get((v, u))) for u, v in G.edges()])
+            Pc = O.build_problem(pos, edges[:, 0], edges[:, 1], N, colors)
+            Ac, bc = O.assemble_reference(Pc, pbc)
+            systems[f"{case}/colors"] = colors
+            systems[f"{case}/x_ref_blocks"] = O.solve_reference(Ac, bc)
+            systems[f"{case}/radius"] = out[f"{g}/radius"]
     np.savez_compressed(HERE / "systems.npz", **systems)
     print("wrote", HERE / "graphs.npz", "and", HERE / "systems.npz")
 

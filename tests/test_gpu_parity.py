@@ -13,7 +13,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from cases import CASES, edge_info_graph, graph_arrays  # noqa: F401
+from cases import CASES, GOLDEN_CASES, edge_info_graph, graph_arrays  # noqa: F401
 from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh, Solver
 from networks_fenicsx_amd import network_generation as ng
 from networks_fenicsx_amd.post_processing import extract_global_flux, integrate_dg1
@@ -124,23 +124,33 @@ def test_demo_tree_closed_form(N):
     assert abs(sol[-1].x.array[0] + (2 - s2)) < tol
 
 
-def test_golden_systems(systems):
-    """Device system and solution against the committed oracle fixtures."""
-    make, N, strategy, pbc = CASES["Y_N4"]
-    mesh = NetworkMesh(make(), N=N)
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_golden_systems(systems, case):
+    """Device system and solution against every committed oracle fixture
+    (tests/golden/systems.npz): CSR bit-exact where stored, rhs bit-exact, solution
+    <= 1e-10 against the fixture's direct solve and its analytic answer."""
+    make, N, strategy, pbc = CASES[case]
+    mesh = NetworkMesh(make(), N=N, color_strategy=strategy)
     asm = HydraulicNetworkAssembler(mesh)
     asm.compute_forms(p_bc_ex=pbc)
     solver = Solver(asm)
     solver.assemble()
-    solver.solve()
-    rp, col, val = asm.handle.csr()
-    np.testing.assert_array_equal(rp, systems["Y_N4/indptr"])
-    np.testing.assert_array_equal(col, systems["Y_N4/indices"])
-    np.testing.assert_array_equal(val, systems["Y_N4/data"])
-    np.testing.assert_array_equal(asm.handle.rhs(), systems["Y_N4/rhs_build"])
+    sol = solver.solve()
+    if f"{case}/indptr" in systems:
+        rp, col, val = asm.handle.csr()
+        np.testing.assert_array_equal(rp, systems[f"{case}/indptr"])
+        np.testing.assert_array_equal(col, systems[f"{case}/indices"])
+        np.testing.assert_array_equal(val, systems[f"{case}/data"])
+    np.testing.assert_array_equal(asm.handle.rhs(), systems[f"{case}/rhs_build"])
     x = solver.solution_vector()
-    ref = systems["Y_N4/x_build"]
-    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= SOL_TOL
+    for key in ("x_build", "x_analytic_build"):
+        ref = systems[f"{case}/{key}"]
+        assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= SOL_TOL, key
+    if f"{case}/x_ref_blocks" in systems:  # C2: the functions in the reference's order
+        np.testing.assert_array_equal(mesh.edge_colors, systems[f"{case}/colors"])
+        ref = systems[f"{case}/x_ref_blocks"]
+        got = np.concatenate([f.x.array for f in sol])
+        assert np.linalg.norm(got - ref) / np.linalg.norm(ref) <= SOL_TOL
 
 
 def test_large_tree_properties():

@@ -3,7 +3,7 @@
 import numpy as np
 import pytest
 
-from cases import CASES
+from cases import CASES, GOLDEN_CASES
 from networks_fenicsx_amd import NetworkMesh
 from oracle import nx_oracle as O
 
@@ -76,7 +76,7 @@ def test_demo_tree_closed_form(N):
     assert abs(x[P.lm_offset] + (2 - s2)) < 1e-12
 
 
-@pytest.mark.parametrize("case", ["Y_N4", "demo_tree_N2", "double_Y_N5", "depth6_N40"])
+@pytest.mark.parametrize("case", GOLDEN_CASES)
 def test_golden_systems_reproduce(systems, case):
     m, P, pbc = _problem(case)
     A, b = O.assemble_reference(P, pbc)
@@ -90,6 +90,20 @@ def test_golden_systems_reproduce(systems, case):
     np.testing.assert_allclose(x, systems[f"{case}/x_build"], rtol=0, atol=1e-12)
     np.testing.assert_allclose(systems[f"{case}/x_analytic_build"], systems[f"{case}/x_build"],
                                rtol=0, atol=1e-11)
+
+
+def test_golden_arterial_reference_order(systems):
+    """C2 (demo_arterial_tree.py: largest_first colouring, N = 40): the fixture's solution in
+    the reference's function order is the oracle's, and equals the build-layout solution
+    regrouped per colour; the fixture's radii are the generator's."""
+    m, P, pbc = _problem("arterial5_N40")
+    np.testing.assert_array_equal(m.edge_colors, systems["arterial5_N40/colors"])
+    np.testing.assert_array_equal(m.edge_radius, systems["arterial5_N40/radius"])
+    A, b = O.assemble_reference(P, pbc)
+    x = O.solve_reference(A, b)
+    np.testing.assert_allclose(x, systems["arterial5_N40/x_ref_blocks"], rtol=0, atol=1e-12)
+    _, _, perm, _ = O.to_build_layout(P, A, b)
+    np.testing.assert_allclose(x[perm], systems["arterial5_N40/x_build"], rtol=0, atol=1e-12)
 
 
 def test_per_edge_R_and_source():
