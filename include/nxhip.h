@@ -207,6 +207,22 @@ int nx_set_pc_exact(nx_network_t* h, int32_t enable);
 int nx_get_pc_exact(nx_network_t* h, int32_t* enabled);
 
 /*
+ * Which solve nx_solve runs. solver = 0 (default): MINRES. solver = 1: the direct solve
+ * the reference's default options ask for (ksp_type=preonly + pc_type=lu + MUMPS,
+ * solver.py:58-65), specialised to the network: a block LU of [[M, K], [K^T, 0]] whose
+ * Schur complement K^T M^{-1} K is inverted by the tree preconditioner's sweeps --
+ *   y = M^{-1} b_q,  x_s = S^{-1} (K^T y - b_s),  x_q = M^{-1} (b_q - K x_s)
+ * -- one HIP graph, followed by the true residual ||b - A x|| / ||b|| (one CSR SpMV),
+ * which is what nx_solve reports (iters = 1). It runs when it is exact: one rank, the
+ * consistent-mass preconditioner (nx_set_pc_exact 1) and tree_exact != 0 (the host
+ * decomposition grounded no cycle-closing chain; precond.py TreePreconditioner.tree_exact).
+ * Otherwise, or if the residual misses rtol, nx_solve runs MINRES. nx_get_solver returns
+ * the requested solver and what the last nx_solve ran (0 MINRES, 1 direct).
+ */
+int nx_set_solver(nx_network_t* h, int32_t solver, int32_t tree_exact);
+int nx_get_solver(nx_network_t* h, int32_t* requested, int32_t* last_run);
+
+/*
  * Process-wide solve mode. 1 (default): with the preconditioner a solve is ONE HIP graph
  * launch -- start application, per-solve coefficients and the first iterations (also with
  * several ranks, RCCL or group, when beta^2 travels point-to-point) -- whose last k_mr_a

@@ -77,6 +77,8 @@ _SIGS = {
                                   _pi32, _pi32, _pi32, _pi32]),
     "nx_set_pc_exact": (C.c_int, [_h, _i32]),
     "nx_get_pc_exact": (C.c_int, [_h, _pi32]),
+    "nx_set_solver": (C.c_int, [_h, _i32, _i32]),
+    "nx_get_solver": (C.c_int, [_h, _pi32, _pi32]),
     "nx_set_lean": (C.c_int, [_i32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
     "nx_group_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
@@ -397,6 +399,16 @@ class Handle:
         e = C.c_int32(0)
         check(lib().nx_get_pc_exact(self.ptr, C.byref(e)))
         return bool(e.value)
+
+    def set_solver(self, direct: bool, tree_exact: bool) -> None:
+        """``nx_set_solver``: the direct tree solve (where exact) or MINRES."""
+        check(lib().nx_set_solver(self.ptr, int(bool(direct)), int(bool(tree_exact))))
+
+    def solver(self):
+        """(requested, last run): 0 = MINRES, 1 = direct tree solve."""
+        a, b = C.c_int32(0), C.c_int32(0)
+        check(lib().nx_get_solver(self.ptr, C.byref(a), C.byref(b)))
+        return int(a.value), int(b.value)
 
     def set_halo(self, nranks: int, rank: int, peers, send_off, send_idx, recv_off):
         """Halo plan without a transport (in-process group members)."""

@@ -338,6 +338,15 @@ class HydraulicNetworkAssembler:
     def preconditioned(self) -> bool:
         return self._pc_on
 
+    def set_direct(self, enable: bool) -> None:
+        """Ask ``nx_solve`` for the direct tree solve (``nx_set_solver``); the device runs it
+        only where it is exact -- one rank, exact preconditioner, no cycle (the
+        decomposition's ``tree_exact``) -- and MINRES otherwise."""
+        want = (bool(enable), bool(self._pc is not None and self._pc.tree_exact))
+        if getattr(self, "_direct_state", None) != want:
+            self._handle.set_solver(*want)
+            self._direct_state = want
+
     # ------------------------------------------------------------------ forms
     @timed("nxfx:HydraulicNetworkAssembler:compute_forms")
     def compute_forms(

@@ -530,10 +530,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv(Csr A, const double* __restrict
   if ((int)threadIdx.x < nr) y[r0 + threadIdx.x] = s;
 }
 
-// residual r = b - A x, partial ||r||^2 and ||b||^2
+// residual r = b - A x, partial ||r||^2 and ||b||^2; r itself into rout when given
 __global__ __launch_bounds__(kBlock) void k_residual(Csr A, const double* __restrict__ x,
                                                      const double* __restrict__ b,
-                                                     double* __restrict__ partials, int nblk) {
+                                                     double* __restrict__ partials, int nblk,
+                                                     double* __restrict__ rout) {
   const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
   const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
   const double s = spmv_row_sum(A, x, r0, nr);
@@ -541,6 +542,7 @@ __global__ __launch_bounds__(kBlock) void k_residual(Csr A, const double* __rest
   if ((int)threadIdx.x < nr) {
     const double bv = b[r0 + threadIdx.x];
     const double rv = bv - s;
+    if (rout) rout[r0 + threadIdx.x] = rv;
     rr = rv * rv;
     bb = bv * bv;
   }
@@ -1121,27 +1123,16 @@ struct ChainLane {
 // persymmetric, so the chain direction (flip) does not matter. rq[t] is the lane's r at
 // chain flux k = l CPL + t, rqN at q_N (the has_last lane, right after its last cell's
 // flux). No LDS, no barriers; returns the lane's share of r . z.
+// M_e^{-1} r on the lane's elements (its cells' fluxes, then q_N on the has_last lane) by
+// the Thomas algorithm run as two segment scans of affine maps (T = L U with pivots fixed
+// by N: forward y_k = r_k - l_k y_{k-1}, backward x_k = (y_k - x_{k+1}) / u_k; pa.Tlu =
+// [l_0..l_N | 1/u_0..1/u_N], l_0 = 0); T is persymmetric, so the chain direction (flip)
+// does not matter. out[t] = the solution at element t (0 where the lane has none).
 template <int W, int CPL>
-__device__ __forceinline__ double pc_flux_block(const PcArgs& pa, const ChainLane<W, CPL>& ch,
-                                                const double* rq, double rqN,
-                                                double* __restrict__ z) {
-  double part = 0.0;
-  if (!pa.exact) {
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) {
-      if (!ch.valid[t]) continue;
-      const double zq = rq[t] / ch.rho[t];
-      z[ch.dof_q[t]] = zq;
-      part += rq[t] * zq;
-    }
-    if (ch.has_last) {
-      const double zq = rqN / ch.rhoN;
-      z[ch.dof_qN] = zq;
-      part += rqN * zq;
-    }
-    return part;
-  }
-  constexpr int NE = CPL + 1;  // the lane's elements: its cells' fluxes, then q_N
+__device__ __forceinline__ void chain_mass_solve(const PcArgs& pa, const ChainLane<W, CPL>& ch,
+                                                 const double* rq, double rqN,
+                                                 double (&out)[CPL + 1]) {
+  constexpr int NE = CPL + 1;
   const int N = pa.N;
   const int l = threadIdx.x & (W - 1);
   const double* __restrict__ lu = pa.Tlu;
@@ -1201,13 +1192,49 @@ __device__ __forceinline__ double pc_flux_block(const PcArgs& pa, const ChainLan
   if (l == W - 1) x = 0.0;
   const double imo = 1.0 / ch.mo;
 #pragma unroll
-  for (int t = NE - 1; t >= 0; --t)
+  for (int t = NE - 1; t >= 0; --t) {
+    out[t] = 0.0;
     if (on[t]) {
       x = iu[t] * (v[t] - x);
-      const double zq = x * imo;
-      z[t < CPL ? ch.dof_q[t] : ch.dof_qN] = zq;
-      part += (t < CPL ? rq[t] : rqN) * zq;
+      out[t] = x * imo;
     }
+  }
+}
+
+// Flux block of P^{-1} on the block's current chains: z_q = r_q / rho (lumped D) or, exact,
+// z_q = M_e^{-1} r_q = T^{-1} r_q / mo (chain_mass_solve). rq[t] is the lane's r at chain
+// flux k = l CPL + t, rqN at q_N (the has_last lane, right after its last cell's flux). No
+// LDS, no barriers; returns the lane's share of r . z.
+template <int W, int CPL>
+__device__ __forceinline__ double pc_flux_block(const PcArgs& pa, const ChainLane<W, CPL>& ch,
+                                                const double* rq, double rqN,
+                                                double* __restrict__ z) {
+  double part = 0.0;
+  if (!pa.exact) {
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      if (!ch.valid[t]) continue;
+      const double zq = rq[t] / ch.rho[t];
+      z[ch.dof_q[t]] = zq;
+      part += rq[t] * zq;
+    }
+    if (ch.has_last) {
+      const double zq = rqN / ch.rhoN;
+      z[ch.dof_qN] = zq;
+      part += rqN * zq;
+    }
+    return part;
+  }
+  double zv[CPL + 1];
+  chain_mass_solve<W, CPL>(pa, ch, rq, rqN, zv);
+#pragma unroll
+  for (int t = CPL; t >= 0; --t) {
+    const bool on = t < CPL ? ch.valid[t] : ch.has_last;
+    if (on) {
+      z[t < CPL ? ch.dof_q[t] : ch.dof_qN] = zv[t];
+      part += (t < CPL ? rq[t] : rqN) * zv[t];
+    }
+  }
   return part;
 }
 
@@ -1434,6 +1461,69 @@ constexpr int kMaxNeed = 64;   // dense top: top values one job reads
 
 __device__ void pc_cpart_last(const PcArgs& pa, double* sA);
 
+// Direct solve (nx_set_solver; mode kModeDirect of the LDS sweeps, one rank): the sweeps
+// apply S^{-1} to w = K^T M^{-1} b_q - b_s and finish x_q = M^{-1} (b_q - K x_s) themselves.
+constexpr int kModeDirect = 3;
+
+// Cell inputs of one chain for the direct solve: y = M^{-1} b_q (Thomas scans), then
+// w_c = (K^T y)_c - b_c in place of vc (row p_g of the layout: +q_g - q_{g+1}; cell k of the
+// chain lies between chain fluxes k and k + 1, whose orientation flips the sign). ytop / ybot
+// (valid in every lane): the multiplier rows' K^T y at the chain's top / bottom end -- the
+// layout puts -1 at q_0 (source multiplier) and +1 at q_N (target multiplier).
+template <int W, int CPL>
+__device__ __forceinline__ void direct_cell_inputs(const PcArgs& pa, const ChainLane<W, CPL>& ch,
+                                                   int flip, const double* bq, double bqN,
+                                                   double* vc, double& ytop, double& ybot) {
+#pragma clang fp contract(off)
+  double yv[CPL + 1];
+  chain_mass_solve<W, CPL>(pa, ch, bq, bqN, yv);
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const double nxt0 = __shfl_down(yv[0], 1, W);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    const int k = l * CPL + t;
+    const double ynext = (k + 1 == N) ? yv[CPL] : (t + 1 < CPL ? yv[t + 1] : nxt0);
+    const double d = yv[t] - ynext;
+    vc[t] = ch.valid[t] ? (flip ? -d : d) - vc[t] : 0.0;
+  }
+  const double y0 = __shfl(yv[0], 0, W), yN = __shfl(yv[CPL], (N - 1) / CPL, W);
+  ytop = flip ? y0 : -y0;  // top = chain position 0 = the edge's source unless flipped
+  ybot = flip ? -yN : yN;
+}
+
+// Flux rows of the direct solve: rq = b_q - K x_s at the chain's fluxes (rq holds b_q on
+// entry), from the lane's cell values zc, the previous lane's last one and the end junction
+// values zt / zb. Row q_k of the layout: +p_k - p_{k-1} - lambda_src (k = 0) + lambda_dst
+// (k = N) in edge orientation; a flipped chain negates it (its position 0 is q_N).
+template <int W, int CPL>
+__device__ __forceinline__ void direct_flux_rhs(const PcArgs& pa, const ChainLane<W, CPL>& ch,
+                                                int flip, const double* zc, double zt, double zb,
+                                                double* rq, double& rqN) {
+#pragma clang fp contract(off)
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  double prev = __shfl_up(zc[CPL - 1], 1, W);  // cell k - 1 of element 0
+  if (l == 0) prev = 0.0;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    const int k = l * CPL + t;
+    const double bprev = t > 0 ? zc[t - 1] : prev;
+    double kz = zc[t] - bprev;  // zc = 0 past the last cell
+    if (k == 0) kz -= zt;
+    if (ch.valid[t]) rq[t] -= flip ? -kz : kz;
+  }
+  if (ch.has_last) {
+    const int tl = (N - 1) - l * CPL;  // the lane's element of cell N - 1
+    double last = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t)
+      if (t == tl) last = zc[t];
+    const double kz = zb - last;  // k = N: -p_{N-1} + the bottom junction
+    rqN -= flip ? -kz : kz;
+  }
+}
+
 constexpr int kCapLvl = 64;  // job levels whose slot offsets are staged in LDS
 
 template <bool MULTI, int W, int CPL>
@@ -1455,6 +1545,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   // alpha's partials first: their loads overlap the state read and the prefetch below
   const double pA = mode == 0 && !MULTI ? block_partial<kPcThreads>(partA, nA) : 0.0;
   const bool upd = mode == 0 && !(MULTI && pa.lin);
+  // direct solve (mode 3, single rank): y holds b; the chains condense w = K^T M^{-1} b_q - b
+  // (formed here from b) and their It / Ib carry the multiplier rows' share of K^T M^{-1} b_q
+  const bool dir = !MULTI && mode == kModeDirect;
   const int job = blockIdx.x;
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
@@ -1464,18 +1557,20 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   ChainLane<W, CPL> ch;
   ch.setup(pa, c0 + seg, c0 + seg < c1);
   double vc[CPL], wc[CPL], vq[CPL], wq[CPL], vN = 0.0, wN = 0.0;
-  auto load_lane = [&]() {
+  int flip = 0;
+  auto load_lane = [&](int c, bool active) {
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
       vc[t] = ch.valid[t] ? y[ch.dof_c[t]] : 0.0;
       wc[t] = upd && ch.valid[t] ? r2[ch.dof_c[t]] : 0.0;
-      vq[t] = upd && ch.valid[t] ? y[ch.dof_q[t]] : 0.0;
+      vq[t] = (upd || dir) && ch.valid[t] ? y[ch.dof_q[t]] : 0.0;
       wq[t] = upd && ch.valid[t] ? r2[ch.dof_q[t]] : 0.0;
     }
-    vN = upd && ch.has_last ? y[ch.dof_qN] : 0.0;
+    vN = (upd || dir) && ch.has_last ? y[ch.dof_qN] : 0.0;
     wN = upd && ch.has_last ? r2[ch.dof_qN] : 0.0;
+    flip = dir && active ? pa.chain_flip[c] : 0;
   };
-  load_lane();
+  load_lane(c0 + seg, c0 + seg < c1);
   const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
   const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
   const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
@@ -1524,8 +1619,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     const bool active = c < c1;
     if (cb != c0) {  // more chains than one pass: set up and load here
       ch.setup(pa, c, active);
-      load_lane();
+      load_lane(c, active);
     }
+    double ytop = 0.0, ybot = 0.0;
+    if (dir) direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
     double sr = 0.0, srd = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
@@ -1544,12 +1641,13 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     srd = seg_sum<W>(srd);
     if (active && l == 0) {
       const double ib = srd / ch.T;
+      const double it = (sr - ib) + ytop, ibe = ib + ybot;  // dir: + the multiplier rows' share
       sT[c - c0] = ch.T;
-      sIb[c - c0] = ib;
-      sIt[c - c0] = sr - ib;
+      sIb[c - c0] = dir ? ibe : ib;
+      sIt[c - c0] = dir ? it : sr - ib;
       pa.chain_T[c] = ch.T;
-      pa.chain_Ib[c] = ib;
-      pa.chain_It[c] = sr - ib;
+      pa.chain_Ib[c] = dir ? ibe : ib;
+      pa.chain_It[c] = dir ? it : sr - ib;
       if (dense) {
         const int ui = pa.chain_uit[c], ub = pa.chain_uib[c];
         if (ui >= 0) pa.u[ui] = sr - ib;
@@ -1582,6 +1680,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       yl -= c2 * (pre ? p_r : r2[lam]);
       y[lam] = yl;
     }
+    if (dir) yl = -yl;  // w_lambda = (K^T M^{-1} b_q)_lambda - b_lambda; the first part is in It / Ib
     const int pcn = pre ? p_pcn : pa.slot_pchain[j];
     double D0 = pcn >= 0 ? 1.0 / sT[pcn - c0] : 0.0;
     double J0 = yl + (pcn >= 0 ? sIb[pcn - c0] : 0.0);
@@ -1743,6 +1842,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
       yl -= c2 * r2[lam];
       y[lam] = yl;
     }
+    if (!MULTI && mode == kModeDirect) yl = -yl;  // direct solve: see k_pc_up_lds
     sLam[sl] = lam;
     sY[sl] = yl;
     const int pcn = pre ? p_pcn : pa.slot_pchain[j];
@@ -1902,6 +2002,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
+  // direct solve (mode 3, single rank): y holds b, z is the solution x; the chains form the
+  // cell inputs w from b again (as k_pc_up_lds did) and finish x_q = M^{-1} (b_q - K x_s)
+  const bool dir = !MULTI && mode == kModeDirect;
   NX_PHASE_START(48);
   const int job = blockIdx.x;
   double part = 0.0;
@@ -1917,7 +2020,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   ChainLane<W, CPL> ch;
   ch.setup(pa, c0 + seg, c0 + seg < c1);
   double vc[CPL], vq[CPL], vN = 0.0;
-  int ch_up = -1, ch_lo = -1;
+  int ch_up = -1, ch_lo = -1, flip = 0;
   auto load_lane = [&](int c, bool active) {
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
@@ -1927,6 +2030,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     vN = ch.has_last ? y[ch.dof_qN] : 0.0;
     ch_up = active ? pa.chain_up[c] : -1;
     ch_lo = active ? pa.chain_lo[c] : -1;
+    flip = dir && active ? pa.chain_flip[c] : 0;
   };
   load_lane(c0 + seg, c0 + seg < c1);
   int p_par = -1, p_lam = 0;
@@ -2076,8 +2180,12 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : outside(up);
     const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : outside(lo);
     const double T = ch.T, iT = 1.0 / T;
-    double rc[CPL], a[CPL], b[CPL], rq[CPL];
+    double rc[CPL], a[CPL], b[CPL], rq[CPL], zc[CPL];
     double sa = 0.0, sb = 0.0;
+    if (dir) {
+      double ytop, ybot;
+      direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
+    }
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
       rc[t] = vc[t];
@@ -2096,10 +2204,12 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       const double prefix = pb_;
       pb_ += b[t];
       rq[t] = 0.0;
+      zc[t] = 0.0;
       if (!ch.valid[t]) continue;
       const double Dk = ch.D[t];
       double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
       if (pa.exact) zk -= ch.mo * rc[t];  // P^{-1} of the consistent-mass Schur complement
+      zc[t] = zk;
       double rk = rc[t];
       if (lin) {
         zk -= c2 * z[ch.dof_c[t]];
@@ -2125,6 +2235,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
         y[ch.dof_qN] = rqN;
       }
     }
+    if (dir) direct_flux_rhs<W, CPL>(pa, ch, flip, zc, zt, zb, rq, rqN);
     part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, z);
   }
   NX_PHASE(51);
@@ -2524,6 +2635,150 @@ __global__ __launch_bounds__(kBlock) void k_gather_out(const double* __restrict_
   if (i < n) out[i] = x[idx[i]];
 }
 
+// ---- Direct solve on a tree (nx_set_solver(h, 1), one rank): block LU of the symmetric
+// system A = [[M, K], [K^T, 0]] (flux rows q; pressure cells and multipliers s), whose Schur
+// complement S = K^T M^{-1} K is exactly what the tree preconditioner inverts (P =
+// blockdiag(M, S); precond.py). Three steps, each a sweep the preconditioner already has:
+//   y   = M^{-1} b_q                      k_dir_pre  (per chain: Thomas scans)
+//   w_s = K^T y - b_s                     k_dir_pre (cells), k_dir_wl (multipliers)
+//   x_s = S^{-1} w_s                      up / top / down sweeps, mode 2 (apply only)
+//   x_q = M^{-1} (b_q - K x_s)            k_dir_post (per chain)
+// then the true residual ||b - A x|| / ||b|| (k_residual + k_dir_publish). This is the
+// reference's default ksp_type=preonly + pc_type=lu (a direct factorisation, solver.py:
+// 58-65) specialised to the network's tree structure; a graph with cycles, where the tree
+// preconditioner grounds a chain and S^{-1} is only approximate, runs MINRES instead.
+template <int W, int CPL>
+__global__ __launch_bounds__(kBlock) void k_dir_pre(PcArgs pa, int n_chains,
+                                                    const double* __restrict__ b,
+                                                    double* __restrict__ yq,
+                                                    double* __restrict__ w) {
+#pragma clang fp contract(off)
+  constexpr int G = kBlock / W;
+  const int c = blockIdx.x * G + (int)threadIdx.x / W;
+  const bool active = c < n_chains;
+  const int l = threadIdx.x & (W - 1);
+  ChainLane<W, CPL> ch;
+  ch.setup(pa, active ? c : 0, active);
+  const int flip = active ? pa.chain_flip[c] : 0;
+  double rq[CPL], bc[CPL];
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    rq[t] = ch.valid[t] ? b[ch.dof_q[t]] : 0.0;
+    bc[t] = ch.valid[t] ? b[ch.dof_c[t]] : 0.0;
+  }
+  const double rqN = ch.has_last ? b[ch.dof_qN] : 0.0;
+  double yv[CPL + 1];
+  chain_mass_solve<W, CPL>(pa, ch, rq, rqN, yv);
+  // y at the fluxes (the multiplier rows read the edge ends); the cell rows of K^T y - b
+  // from the lane's values and the next lane's first: cell k lies between chain fluxes k
+  // and k + 1 (q_N is the has_last lane's element CPL); row p_g = +q_g - q_{g+1}
+  const double nxt0 = __shfl_down(yv[0], 1, W);
+  const int N = pa.N;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    if (!ch.valid[t]) continue;
+    yq[ch.dof_q[t]] = yv[t];
+    const int k = l * CPL + t;
+    const double ynext = (k + 1 == N) ? yv[CPL] : (t + 1 < CPL ? yv[t + 1] : nxt0);
+    const double d = yv[t] - ynext;
+    w[ch.dof_c[t]] = (flip ? -d : d) - bc[t];
+  }
+  if (ch.has_last) yq[ch.dof_qN] = yv[CPL];
+}
+
+// Multiplier rows of w = K^T y - b (+-1 at the flux ends of the edges meeting there).
+__global__ __launch_bounds__(kBlock) void k_dir_wl(Csr A, int64_t n_edge_dofs,
+                                                   const double* __restrict__ y,
+                                                   const double* __restrict__ b,
+                                                   double* __restrict__ w) {
+#pragma clang fp contract(off)
+  const int64_t i = n_edge_dofs + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n_rows) return;
+  double acc = 0.0;
+  for (int k = A.rowptr[i]; k < A.rowptr[i + 1]; ++k) acc += A.val[k] * y[A.col[k]];
+  w[i] = acc - b[i];
+}
+
+// x_q = M^{-1} (b_q - K z_s) per chain, x_s = z_s. Row q_k of the layout (k_pattern):
+// +1 at p_k (k < N), -1 at p_{k-1} (k > 0), -1 at the source multiplier (k = 0), +1 at the
+// target multiplier (k = N). Blocks past the chains copy the multiplier rows.
+template <int W, int CPL, bool ACC>
+__global__ __launch_bounds__(kBlock) void k_dir_post(PcArgs pa, int n_chains, int chain_blocks,
+                                                     const int* __restrict__ edge_lm,
+                                                     int64_t n_edge_dofs, int64_t n_own,
+                                                     const double* __restrict__ b,
+                                                     const double* __restrict__ z,
+                                                     double* __restrict__ x) {
+#pragma clang fp contract(off)
+  if ((int)blockIdx.x >= chain_blocks) {
+    const int64_t i = n_edge_dofs + (int64_t)(blockIdx.x - chain_blocks) * kBlock + threadIdx.x;
+    if (i < n_own) x[i] = ACC ? x[i] + z[i] : z[i];
+    return;
+  }
+  constexpr int G = kBlock / W;
+  const int c = blockIdx.x * G + (int)threadIdx.x / W;
+  const bool active = c < n_chains;
+  ChainLane<W, CPL> ch;
+  ch.setup(pa, active ? c : 0, active);
+  const int N = pa.N;
+  const int e = active ? pa.chain_edge[c] : 0;
+  const int64_t base = (int64_t)e * (2 * N + 1);
+  const int ls = active ? edge_lm[2 * e] : -1, lt = active ? edge_lm[2 * e + 1] : -1;
+  const double zsrc = ls >= 0 ? z[ls] : 0.0, zdst = lt >= 0 ? z[lt] : 0.0;
+  auto rhs_q = [&](int64_t q) {
+    const int k = (int)((q - base) >> 1);
+    double kx = 0.0;
+    if (k < N) kx += z[q + 1];
+    if (k > 0) kx -= z[q - 1];
+    if (k == 0) kx -= zsrc;
+    if (k == N) kx += zdst;
+    return b[q] - kx;
+  };
+  double rq[CPL];
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    rq[t] = ch.valid[t] ? rhs_q(ch.dof_q[t]) : 0.0;
+    if (ch.valid[t]) x[ch.dof_c[t]] = ACC ? x[ch.dof_c[t]] + z[ch.dof_c[t]] : z[ch.dof_c[t]];
+  }
+  const double rqN = ch.has_last ? rhs_q(ch.dof_qN) : 0.0;
+  double xv[CPL + 1];
+  chain_mass_solve<W, CPL>(pa, ch, rq, rqN, xv);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t)
+    if (ch.valid[t]) x[ch.dof_q[t]] = ACC ? x[ch.dof_q[t]] + xv[t] : xv[t];
+  if (ch.has_last) x[ch.dof_qN] = ACC ? x[ch.dof_qN] + xv[CPL] : xv[CPL];
+}
+
+// x += d (the refinement step of the fused direct solve)
+__global__ __launch_bounds__(kBlock) void k_axpy1(int64_t n, const double* __restrict__ d,
+                                                  double* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] += d[i];
+}
+
+// ||b - A x|| / ||b|| from k_residual's partials (fixed order), published like a MINRES
+// state (it = 1, done) to the host-coherent mirror the host spins on.
+__global__ __launch_bounds__(kReduceThreads) void k_dir_publish(const double* __restrict__ p,
+                                                                int nblk, double rtol, int* seq,
+                                                                MrState* mirror) {
+  const double rr = reduce_partials(p, nblk);
+  __syncthreads();
+  const double bb = reduce_partials(p + nblk, nblk);
+  if (threadIdx.x == 0) {
+    MrState s{};
+    s.beta1 = sqrt(bb);
+    s.relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
+    s.rtol = rtol;
+    s.it = 1;
+    s.done = 1;
+    s.converged = s.relres <= rtol ? 1 : 0;
+    MrInit ini{};
+    ini.seq = seq;
+    ini.mirror = mirror;
+    mr_publish(s, ini);
+  }
+}
+
 // Halo pack + this rank's beta^2 (sum of the previous iteration's partials, block 0) into
 // red[1] and its own slot of the gathered array: saves a reduction launch per iteration.
 __global__ __launch_bounds__(kBlock) void k_pack_beta(const double* __restrict__ x,
@@ -2580,6 +2835,11 @@ struct LeanGraphs {
   hipGraphExec_t lchunk_exec = nullptr;
   hipGraph_t lchunk_graph = nullptr;
   int lchunk_len = 0;
+  // direct tree solve (nx_set_solver(h, 1)): one graph per solve
+  hipGraphExec_t direct_exec = nullptr;
+  hipGraph_t direct_graph = nullptr;
+  int direct_len = 0;
+  double direct_rtol = 0.0;
 };
 
 struct nx_network {
@@ -2668,6 +2928,11 @@ struct nx_network {
   bool rccl_graph_ok = true;  // capture of the RCCL iteration worked (or was not tried)
   bool sched_checked = false; // RCCL: the ranks' kernel schedules were compared (per pc)
   bool last_graph = false;    // the last nx_solve replayed HIP graphs
+  // solver (nx_set_solver): 0 = MINRES, 1 = direct tree solve where it is exact (one rank,
+  // exact preconditioner on a forest: tree_exact from the host decomposition), else MINRES
+  int solver = 0;
+  bool tree_exact = false;
+  int last_solver = 0;        // what the last nx_solve ran (0 MINRES, 1 direct)
   // general element degrees (nx_create_fe): gather-assembly tables, one rank, no
   // preconditioner
   // nx_set_output_map: owned rows in the reference's function order (Solver.solve output)
@@ -2856,8 +3121,9 @@ __global__ __launch_bounds__(kGcThreads) void k_pc_gc(PcArgs pa) {
 // buffer is all-reduced between the halves and k_pc_coarse finishes the top part.
 template <bool MULTI, int W, int CPL>
 void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other,
-                  int mode, int half) {
+                  int mode, int half, double* zout) {
   const bool coarse = MULTI && h->pa.n_coarse > 0;
+  double* const z = zout ? zout : h->z;
   if (half == 0) {
     if (h->pc_lds) {
       if (h->pc_jobs > 0)
@@ -2868,28 +3134,28 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
           hipLaunchKernelGGL(k_pc_cpart, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, st, mode);
       } else if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
         hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream,
-                           h->pa, y, r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
+                           h->pa, y, r2, z, st, h->partA, h->nA, h->red, h->partB, mode);
     } else {
       if (h->pc_jobs > 0)
         hipLaunchKernelGGL((k_pc_up<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
                            h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
       hipLaunchKernelGGL((k_pc_top<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y,
-                         r2, h->z, st, h->partA, h->nA, h->red, h->partB, mode);
+                         r2, z, st, h->partA, h->nA, h->red, h->partB, mode);
     }
     return;
   }
   // fused (dense top, LDS kernels): every down workgroup solves the coarse forest itself
   const bool cfused = MULTI && h->pc_lds && h->pa.fused && h->pa.mdense && mode == 0;
   if (coarse && !cfused)
-    hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2, h->z,
+    hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2, z,
                        st, h->partB, mode);
   if (h->pc_jobs > 0) {
     if (h->pc_lds)
       hipLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
-                         h->stream, h->pa, y, r2, h->z, st, h->partB, mode);
+                         h->stream, h->pa, y, r2, z, st, h->partB, mode);
     else
       hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
-                         h->pa, y, h->z, st, h->partB, mode);
+                         h->pa, y, z, st, h->partB, mode);
   }
   // the iterations' dense coarse step: Gc is read only by the fused dense down sweep
   if (MULTI && coarse && mode == 1 && h->pa.Gc != nullptr && h->pc_lds && h->pa.fused &&
@@ -2899,18 +3165,18 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
 
 template <bool MULTI>
 void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other, int mode,
-               int half) {
+               int half, double* zout = nullptr) {
   switch (h->pc_variant) {
-    case 0: launch_pc_wc<MULTI, 16, 1>(h, y, r2, st, other, mode, half); break;
-    case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode, half); break;
-    case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode, half); break;
-    case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode, half); break;
-    case 5: launch_pc_wc<MULTI, 8, 2>(h, y, r2, st, other, mode, half); break;
-    case 6: launch_pc_wc<MULTI, 4, 4>(h, y, r2, st, other, mode, half); break;
-    case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half); break;
-    case 8: launch_pc_wc<MULTI, 64, 8>(h, y, r2, st, other, mode, half); break;
-    case 9: launch_pc_wc<MULTI, 64, 16>(h, y, r2, st, other, mode, half); break;
-    default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half); break;
+    case 0: launch_pc_wc<MULTI, 16, 1>(h, y, r2, st, other, mode, half, zout); break;
+    case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode, half, zout); break;
+    case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode, half, zout); break;
+    case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode, half, zout); break;
+    case 5: launch_pc_wc<MULTI, 8, 2>(h, y, r2, st, other, mode, half, zout); break;
+    case 6: launch_pc_wc<MULTI, 4, 4>(h, y, r2, st, other, mode, half, zout); break;
+    case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half, zout); break;
+    case 8: launch_pc_wc<MULTI, 64, 8>(h, y, r2, st, other, mode, half, zout); break;
+    case 9: launch_pc_wc<MULTI, 64, 16>(h, y, r2, st, other, mode, half, zout); break;
+    default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half, zout); break;
   }
 }
 
@@ -3075,6 +3341,7 @@ int drop_graph(GraphSlot gs) {
   if (gs.lean) {
     CHECK(drop_one(&gs.lean->head_exec, &gs.lean->head_graph, &gs.lean->head_len));
     CHECK(drop_one(&gs.lean->lchunk_exec, &gs.lean->lchunk_graph, &gs.lean->lchunk_len));
+    CHECK(drop_one(&gs.lean->direct_exec, &gs.lean->direct_graph, &gs.lean->direct_len));
   }
   return NX_OK;
 }
@@ -3675,6 +3942,117 @@ int launch_head_multi(const Team& t, int L, double rtol, int maxit) {
 
 LeanGraphs& lean_of(const Team& t) { return t.g ? t.g->lean : t.hs[0]->lean; }
 
+// ---- direct tree solve (k_dir_*): y in vb[1], w in vb[0], S^{-1} w in z, x
+// refine = 0: x = A^{-1} b; refine = 1: one step of iterative refinement, r = b - A x
+// (into tmp), x += A^{-1} r. Both end with the true residual published.
+template <int W, int CPL>
+void launch_direct_wc(nx_network* h, double rtol, int refine) {
+  constexpr int G = kBlock / W;
+  const int cb = grid_of(h->E, G);
+  double* yq = h->vb[1];
+  double* w = h->vb[0];
+  const double* bin = h->rhs;
+  if (refine) {
+    hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, h->nblk, h->tmp);
+    bin = h->tmp;
+  }
+  if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
+    double* xo = refine ? w : h->x;  // refinement: the correction, then x += it
+    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, xo);
+    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, xo);
+    if (refine)
+      hipLaunchKernelGGL(k_axpy1, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
+                         h->n_own, (const double*)w, h->x);
+  } else {
+  const int64_t n_lm = h->n_own - h->n_edge_dofs;
+  if (cb > 0)
+    hipLaunchKernelGGL((k_dir_pre<W, CPL>), dim3(cb), dim3(kBlock), 0, h->stream, h->pa, (int)h->E,
+                       bin, yq, w);
+  if (n_lm > 0)
+    hipLaunchKernelGGL(k_dir_wl, dim3(grid_of(n_lm, kBlock)), dim3(kBlock), 0, h->stream,
+                       csr_of(h), h->n_edge_dofs, yq, bin, w);
+  launch_pc<false>(h, w, w, h->st, h->st + 1, 2, 0);
+  launch_pc<false>(h, w, w, h->st, h->st + 1, 2, 1);
+  const int lb = grid_of(n_lm, kBlock);
+  if (cb + lb > 0) {
+    if (refine)
+      hipLaunchKernelGGL((k_dir_post<W, CPL, true>), dim3(cb + lb), dim3(kBlock), 0, h->stream,
+                         h->pa, (int)h->E, cb, h->edge_lm, h->n_edge_dofs, h->n_own, bin, h->z, h->x);
+    else
+      hipLaunchKernelGGL((k_dir_post<W, CPL, false>), dim3(cb + lb), dim3(kBlock), 0, h->stream,
+                         h->pa, (int)h->E, cb, h->edge_lm, h->n_edge_dofs, h->n_own, bin, h->z, h->x);
+  }
+  }  // unfused
+  hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                     h->rhs, h->partials, h->nblk, nullptr);
+  hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                     h->nblk, rtol, h->d_seq, h->d_last);
+}
+
+int launch_direct(nx_network* h, double rtol, int refine) {
+  switch (h->pc_variant) {
+    case 0: launch_direct_wc<16, 1>(h, rtol, refine); break;
+    case 1: launch_direct_wc<16, 2>(h, rtol, refine); break;
+    case 2: launch_direct_wc<16, 4>(h, rtol, refine); break;
+    case 3: launch_direct_wc<64, 2>(h, rtol, refine); break;
+    case 5: launch_direct_wc<8, 2>(h, rtol, refine); break;
+    case 6: launch_direct_wc<4, 4>(h, rtol, refine); break;
+    case 7: launch_direct_wc<8, 4>(h, rtol, refine); break;
+    case 8: launch_direct_wc<64, 8>(h, rtol, refine); break;
+    case 9: launch_direct_wc<64, 16>(h, rtol, refine); break;
+    default: launch_direct_wc<64, 4>(h, rtol, refine); break;
+  }
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+// Exact on this handle: one rank (no communicator, no group), the exact Schur-complement
+// preconditioner (consistent mass) on a decomposition without grounded cycle chains.
+bool direct_applicable(const nx_network* h) {
+  return h->solver == 1 && h->pc && h->pa.exact && h->tree_exact && h->nranks == 1 &&
+         h->comm == nullptr && h->group == nullptr && h->E > 0;
+}
+
+// One graph: pre, multiplier rows, S^{-1} (up / top / down, mode 2), post, residual,
+// publish. The tree formula is exact but not backward stable to the last digits (its true
+// residual is ~1e-13 .. 1e-11 where a sparse LU reaches ~1e-15; the forward error stays
+// ~1e-12): when the residual misses rtol, a second graph applies one step of iterative
+// refinement (residual -> direct solve -> x += correction; ~1e-15 after it). Returns NX_OK
+// with *converged = 0 if that is still above rtol (the caller runs MINRES).
+int solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
+                 int32_t* converged) {
+  LeanGraphs& lg = h->lean;
+  if (!lg.direct_exec || lg.direct_rtol != rtol) {
+    CHECK(drop_one(&lg.direct_exec, &lg.direct_graph, &lg.direct_len));
+    CHECK(drop_one(&lg.lchunk_exec, &lg.lchunk_graph, &lg.lchunk_len));
+    CHECK(capture(h, &lg.direct_graph, &lg.direct_exec, [&] { return launch_direct(h, rtol, 0); }));
+    lg.direct_len = 1;
+    lg.direct_rtol = rtol;
+  }
+  h->last_graph = true;
+  HIPCALL(hipGraphLaunch(lg.direct_exec, h->stream));
+  h->seq += 1;
+  CHECK(wait_published(h));
+  MrState s = *h->h_last;
+  if (!s.converged && s.relres == s.relres) {  // one refinement step (graph kept in lchunk)
+    if (!lg.lchunk_exec || lg.lchunk_len != -1) {
+      CHECK(drop_one(&lg.lchunk_exec, &lg.lchunk_graph, &lg.lchunk_len));
+      CHECK(capture(h, &lg.lchunk_graph, &lg.lchunk_exec, [&] { return launch_direct(h, rtol, 1); }));
+      lg.lchunk_len = -1;  // marks the refinement graph (MINRES continuation chunks use L > 0)
+    }
+    HIPCALL(hipGraphLaunch(lg.lchunk_exec, h->stream));
+    h->seq += 1;
+    CHECK(wait_published(h));
+    s = *h->h_last;
+    s.it = 2;
+  }
+  if (iters) *iters = s.it;
+  if (relres) *relres = s.relres;
+  if (converged) *converged = s.converged;
+  return NX_OK;
+}
+
 // 1: one graph per solve where possible (default; NXHIP_LEAN=0 or nx_set_lean(0): the
 // general path with eager prologue and chunked iterations)
 int& lean_flag() {
@@ -3837,6 +4215,18 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   }
   if (maxit < 1) return fail(NX_ERR_ARG, "maxit must be >= 1");
   if (check_every < 2) check_every = 2;
+  t.hs[0]->last_solver = 0;
+  if (t.P == 1 && t.g == nullptr && direct_applicable(t.hs[0])) {
+    CHECK(set_device(t.hs[0]));
+    int32_t conv = 0;
+    CHECK(solve_direct(t.hs[0], rtol, iters, relres, &conv));
+    if (conv) {
+      t.hs[0]->last_solver = 1;
+      if (converged) *converged = 1;
+      return NX_OK;
+    }
+    // residual above rtol (e.g. rounding on an ill-conditioned tree): MINRES from scratch
+  }
   if (check_every & 1) ++check_every;
   CHECK(set_device(t.hs[0]));
   const bool multi = team_multi(t);
@@ -4115,7 +4505,7 @@ NX_API int nx_true_residual(nx_network_t* h, double* relres) {
     CHECK(team_halo(Team{hs, 1, nullptr}, VS_X, 0));
   }
   hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                     h->rhs, h->partials, h->nblk);
+                     h->rhs, h->partials, h->nblk, nullptr);
   double* d = h->red + 2;  // slots 2, 3 are free outside nx_solve
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials, h->nblk, d);
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials + h->nblk,
@@ -4535,6 +4925,23 @@ NX_API int nx_set_pc_exact(nx_network_t* h, int32_t enable) {
   HIPCALL(hipStreamSynchronize(h->stream));
   CHECK(drop_handle_graphs(h));
   h->pa.exact = enable ? 1 : 0;
+  return NX_OK;
+}
+
+NX_API int nx_set_solver(nx_network_t* h, int32_t solver, int32_t tree_exact) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (solver != 0 && solver != 1) return fail(NX_ERR_ARG, "solver: 0 = MINRES, 1 = direct");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  h->solver = solver;
+  h->tree_exact = tree_exact != 0;
+  return NX_OK;
+}
+
+NX_API int nx_get_solver(nx_network_t* h, int32_t* requested, int32_t* last_run) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (requested) *requested = h->solver;
+  if (last_run) *last_run = h->last_solver;
   return NX_OK;
 }
 

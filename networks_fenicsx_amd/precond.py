@@ -253,6 +253,9 @@ class TreePreconditioner:
     c_child_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
     c_child: np.ndarray = field(default_factory=lambda: _EMPTY_I)
     c_lvl_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
+    # no chain closes a cycle (grounded at one end): P^{-1} is the exact block inverse, so
+    # the direct tree solve (nx_set_solver) is exact
+    tree_exact: bool = False
 
     @property
     def n_chains(self) -> int:
@@ -430,6 +433,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     chain_lo_node = np.full(E, -1, dtype=np.int64)
     is_cc = np.zeros(E, dtype=bool)  # joins two coarse junctions (coarse step)
     flip = np.zeros(E, dtype=np.int8)
+    n_cycle = 0  # chains grounded to break a cycle
     for e in range(E):
         a, b = int(es[e]), int(ed[e])
         ja, jb = is_j(a), is_j(b)
@@ -437,6 +441,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         if is_c(a) and is_c(b):
             if coarse.demoted[ge]:  # closes a cycle of the coarse graph: ground one end
                 up, lo = a, -1
+                n_cycle += 1
             else:  # coarse forest edge: top = parent end, bottom = child end
                 child = b if coarse.pedge[coarse.cidx[b]] == ge else a
                 up, lo = (a if child == b else b), child
@@ -449,6 +454,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
                 up, lo = b, a
         elif ja and jb:  # closes a cycle: hang from the shallower end, ground the other
             up, lo = (a, -1) if depth[a] <= depth[b] else (b, -1)
+            n_cycle += 1
         elif ja:
             up, lo = a, -1
         elif jb:
@@ -580,7 +586,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         job_chain_off=job_chain_off, job_lvl_off=np.asarray(job_lvl_off, dtype=np.int32),
         lvl_slot_off=np.asarray(lvl_slot_off, dtype=np.int32),
         top_lvl_off=np.asarray(top_lvl_off, dtype=np.int32), n_jobs=int(n_jobs),
-        n_slots=n_slots)
+        n_slots=n_slots, tree_exact=n_cycle == 0)
     _dense_top_lists(pc)
     if coarse is not None and coarse.n > 0:
         cid = coarse.cidx

@@ -3,10 +3,15 @@
 Mirrors ``Solver`` of the reference (``src/networks_fenicsx/solver.py:16-143``):
 same constructor signature, ``assemble``, ``solve``, ``A``, ``b``, ``ksp`` and
 ``assembler`` accessors. The reference factorises the system with MUMPS
-(``preonly`` + ``lu``, ``solver.py:58-65``); here the symmetric-indefinite system is
-solved by MINRES running entirely on the GPU (``nx_solve`` in ``csrc/nxhip.hip``):
-CSR SpMV, fused vector updates and deterministic reductions, chunked into HIP graphs
-with one host convergence check per chunk.
+(``preonly`` + ``lu``, ``solver.py:58-65``). Here both KSP types run on the GPU
+(``nx_solve`` in ``csrc/nxhip.hip``):
+
+* ``ksp_type="preonly"`` (the reference default): a direct solve -- the block LU of the
+  saddle-point system whose Schur complement the tree preconditioner inverts exactly
+  (``nx_set_solver``), one HIP graph, checked by the true residual. Used where it is exact
+  (one rank, trees); a graph with cycles, or a residual above ``ksp_rtol``, runs MINRES;
+* ``ksp_type="minres"`` (or any other iterative type): preconditioned MINRES -- CSR SpMV,
+  fused vector updates and deterministic reductions in HIP graphs.
 
 PETSc options understood (with or without the options prefix):
 
@@ -25,9 +30,10 @@ PETSc options understood (with or without the options prefix):
 ``pc_mass``                       ``"consistent"`` (default: exact Schur complement, 3 MINRES
                                   iterations) or ``"lumped"``
 
-``ksp_type`` and ``pc_factor_mat_solver_type`` are accepted and recorded: whatever they
-say, the device solve is MINRES (a direct LU has no place on this path); the tolerance
-above makes the result agree with the direct solve.
+``ksp_type``                      ``"preonly"`` (default): the direct tree solve where exact,
+                                  else MINRES; anything else: MINRES.
+``pc_factor_mat_solver_type`` is accepted and recorded. ``ksp.solver_used`` tells which
+solve ran last (``"direct"`` or ``"minres"``).
 """
 
 from __future__ import annotations
@@ -61,6 +67,7 @@ class KSPInfo:
         self.iterations = 0
         self.residual_estimate = float("nan")
         self.converged = False
+        self.solver_used = ""
 
     def getOptionsPrefix(self) -> str:  # noqa: N802
         return self.prefix
@@ -118,6 +125,7 @@ class Solver:
         self._ksp = KSPInfo(petsc_options_prefix, clean)
         self._pc = str(clean.get("pc_type", "lu")).lower() != "none"
         self._pc_exact = str(clean.get("pc_mass", "consistent")).lower() != "lumped"
+        self._direct = str(clean.get("ksp_type", "preonly")).lower() == "preonly"
         self._kind = kind
         self._A = DeviceMatrix(assembler.handle, kind)
         self._b = DeviceVector(assembler.handle)
@@ -160,12 +168,17 @@ class Solver:
             self.assembler.set_preconditioner(self._pc)
         if self.assembler.preconditioned and h.pc_exact() != self._pc_exact:
             h.set_pc_exact(self._pc_exact)
+        self.assembler.set_direct(self._direct and self.assembler.preconditioned)
         ce = self._check_every or (4 if self.assembler.preconditioned else 32)
         it, relres, conv = h.solve(self._rtol, self._maxit, ce)
         self._ksp.iterations, self._ksp.residual_estimate, self._ksp.converged = it, relres, conv
+        used = "direct" if h.solver()[1] == 1 else "minres"
+        self._ksp.solver_used = used
         if self._monitor:
-            print(f"  MINRES: {it} iterations, residual estimate {relres:.3e}"
-                  f" ({'converged' if conv else 'NOT converged'})", file=sys.stdout)
+            what = ("direct tree solve, true residual" if used == "direct"
+                    else f"MINRES: {it} iterations, residual estimate")
+            print(f"  {what} {relres:.3e} ({'converged' if conv else 'NOT converged'})",
+                  file=sys.stdout)
         if not conv and self._raise:
             raise _lib.NxNotConverged(
                 f"MINRES did not converge: {it} iterations, relative residual {relres:.3e} "

@@ -208,12 +208,13 @@ def test_not_converged_raises():
     asm = HydraulicNetworkAssembler(mesh)
     asm.compute_forms(p_bc_ex=pbc)
     # the exact preconditioner needs 3 iterations: a cap of 2 cannot converge
-    solver = Solver(asm, petsc_options={"ksp_max_it": 2, "ksp_error_if_not_converged": True})
+    solver = Solver(asm, petsc_options={"ksp_type": "minres", "ksp_max_it": 2,
+                                        "ksp_error_if_not_converged": True})
     solver.assemble()
     with pytest.raises(NxNotConverged):
         solver.solve()
-    quiet = Solver(asm, petsc_options={"ksp_max_it": 10, "ksp_error_if_not_converged": False,
-                                       "pc_mass": "lumped"})
+    quiet = Solver(asm, petsc_options={"ksp_type": "minres", "ksp_max_it": 10,
+                                       "ksp_error_if_not_converged": False, "pc_mass": "lumped"})
     quiet.solve()
     assert not quiet.ksp.converged and quiet.ksp.getIterationNumber() == 10
 
