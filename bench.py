@@ -18,9 +18,14 @@ Workload (p_bc = y, f = 0, R = 1, ``color_strategy="smallest_last"
   ``make_tree(18,18,18)``, N = 19, 10,354,648 DoF (configs[4]). Rank 0 also times the SAME
   workload on its GPU alone (``strong_scaling``), so T1 / TP is measured in the same run.
 
-One step = device assembly of the CSR matrix and rhs (``nx_assemble``) + MINRES to rtol
-1e-12 (``nx_solve``), inputs resident in HBM, solution left in HBM. Rank 0 prints one JSON
-line.
+One step = device assembly of the CSR matrix and rhs (``nx_assemble``) + the solve
+(``nx_solve``), inputs resident in HBM, solution left in HBM. The solve is what the
+reference's default options ask for (``ksp_type=preonly`` + ``pc_type=lu``: a direct
+factorisation, solver.py:58-65): on one GPU the direct tree solve (block LU through the
+tree sweeps, true residual checked, rtol 1e-12, one refinement step if it misses), with
+``--solver minres`` preconditioned MINRES to rtol 1e-12. Partitioned runs (P > 1) use MINRES.
+The other single-GPU solver is timed on the same workload and reported beside. Rank 0
+prints one JSON line.
 """
 
 from __future__ import annotations
@@ -72,6 +77,25 @@ def mr_spmv_bytes(n_rows: int, nnz: int, preconditioned: bool, iterations: int =
     for k in range(1, its + 1):
         passes += 2 if k == 1 else 3 if k <= K_MAX_V else 15 if k == K_MAX_V + 1 else 9
     return spmv + 8 * n_rows * passes / its
+
+
+def direct_kernel_bytes(n: int, nnz: int, n_e: int, E: int, N: int, B: int, nblk: int) -> dict:
+    """Algorithmic bytes per launch of the direct solve's kernels:
+    f64 vectors, int32 indices, the lumped mass dq (E (N+1)) read by every chain sweep."""
+    dq = 8 * E * (N + 1)
+    return {
+        # CSR SpMV of x, b read, r not stored; two partials per block
+        "k_residual": 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n + 16 * nblk,
+        # b at the edge DoFs + dq, chain T / It / Ib written, junction slots (b, D, J, A, B
+        # and their static indices: ~64 B each), chain statics (edge, flip: 8 B)
+        "k_pc_up_lds": 8 * n_e + dq + 24 * E + 8 * E + 64 * B,
+        # b at the edge DoFs + dq read, x written (edge DoFs + multipliers), chain and slot
+        # statics (up, lo, edge, flip: 16 B; A, B, parent, lambda: 24 B)
+        "k_pc_down_lds": 8 * n_e + dq + 8 * n + 16 * E + 24 * B,
+        "k_pc_top_lds": 64 * 1024,  # <= 1024 junctions above the cut
+        # values + rhs written, dq written, edge inputs read (edge_x 48, R, bc 16, lm 8, seg 4)
+        "k_assemble_seg": 8 * nnz + 8 * n + dq + 80 * E,
+    }
 
 
 def pmc_traffic(kernel_prefix: str):
@@ -174,6 +198,9 @@ def parse_args(argv=None):
     ap.add_argument("--api-steps", type=int, default=10,
                     help="steps through the public Solver.assemble/solve surface (0: skip)")
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
+    ap.add_argument("--solver", choices=("direct", "minres"), default="direct",
+                    help="one GPU: the direct tree solve (reference default preonly + lu) or "
+                         "MINRES; several GPUs always run MINRES")
     return ap.parse_args(argv)
 
 
@@ -283,29 +310,116 @@ def run(args, world: int) -> int:
         el = time.perf_counter() - ts
         return allmax(el) if collective else el
 
+    pc_on = asm.preconditioned
+    direct = args.solver == "direct" and world == 1 and pc_on
+    asm.set_direct(direct)
     elapsed = timed_steps(h, args.steps, args.warmup, True)
     ms_per_step = 1e3 * elapsed / args.steps
     iters = state["it"]
-
-    # --- per-kernel timing with HIP events on the library's stream (one profiled step)
-    h.set_profiling(True)
-    h.reset_profile()
-    step(h)
-    prof = h.profile()
-    h.set_profiling(False)
-    spmv_ms = prof["spmv_ms"] / max(prof["spmv_count"], 1)
-    asm_ms = prof["asm_ms"] / max(prof["asm_count"], 1)
-    warm_spmv_ms = h.bench_spmv(200)
-    cold_spmv_ms, cold_copies = h.bench_spmv_cold(120)
-    pc_on = asm.preconditioned
-    nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on, max(int(prof["spmv_count"]), 1))
-    achieved = nbytes / (spmv_ms * 1e-3) / 1e9
-    sbytes = spmv_bytes(h.n_rows, h.nnz)
-    # beta^2 travels point-to-point with the halo, so the multi-rank k_mr_a is MULTI = false
-    kname = f"k_mr_a<false, {str(pc_on).lower()}>"
+    solver_used = "direct" if h.solver()[1] == 1 else "minres"
     # the committed PMC summaries profile the default workload (C3) on one GPU only
     default_workload = world == 1 and (levels, N) == (15, 15) and not args.no_pc
-    traffic, traffic_src, rocprof_ns = pmc_traffic(kname) if default_workload else (None, None, None)
+
+    def minres_roofline():
+        """k_mr_a: HIP events bound to its dispatches over one profiled MINRES step."""
+        h.set_profiling(True)
+        h.reset_profile()
+        step(h)
+        prof = h.profile()
+        h.set_profiling(False)
+        spmv_ms = prof["spmv_ms"] / max(prof["spmv_count"], 1)
+        nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on, max(int(prof["spmv_count"]), 1))
+        # beta^2 travels point-to-point with the halo, so the multi-rank k_mr_a is MULTI = false
+        kname = f"k_mr_a<false, {str(pc_on).lower()}>"
+        traffic, tsrc, rocprof_ns = (pmc_traffic(kname) if default_workload
+                                     else (None, None, None))
+        achieved = nbytes / (spmv_ms * 1e-3) / 1e9
+        return {"bound": "hbm",
+                "kernel": f"{kname} (CSR SpMV fused with the Lanczos step, Givens rotation "
+                          "and solution update)",
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+                "traffic_source": tsrc,
+                "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
+                "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": spmv_ms,
+                "assembly_kernel_ms": prof["asm_ms"] / max(prof["asm_count"], 1)}
+
+    def direct_roofline():
+        """The direct solve's kernels (events bound to each dispatch, one profiled step):
+        the dominant one by time is the roofline kernel; all are listed."""
+        h.set_profiling(True)
+        h.reset_profile()
+        step(h)
+        pd = h.profile_direct()
+        prof = h.profile()
+        h.set_profiling(False)
+        cnt = max(pd["count"], 1)
+        n, nnz = h.n_rows, h.nnz
+        n_e = E * (2 * N + 1)
+        nblk = (n + 255) // 256
+        kb = direct_kernel_bytes(n, nnz, n_e, E, N, B, nblk)
+        ms = {"k_residual": pd["residual_ms"] / cnt, "k_pc_up_lds": pd["up_ms"] / cnt,
+              "k_pc_top_lds": pd["top_ms"] / cnt, "k_pc_down_lds": pd["down_ms"] / cnt,
+              "k_assemble_seg": prof["asm_ms"] / max(prof["asm_count"], 1)}
+        kernels = {}
+        for k, t in ms.items():
+            if t > 0:
+                ach = kb[k] / (t * 1e-3) / 1e9
+                kernels[k] = {"avg_launch_ms": t, "algorithmic_bytes_per_launch": kb[k],
+                              "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
+        dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
+        d = kernels[dom]
+        names = {"k_residual": "k_residual (CSR SpMV r = b - A x: the direct solve's true-residual "
+                               "check)",
+                 "k_pc_up_lds": "k_pc_up_lds<false, 8, 2> (direct mode: M^-1 b_q per chain, "
+                                "chain condensation, junction elimination)",
+                 "k_pc_down_lds": "k_pc_down_lds<false, 8, 2> (direct mode: back-substitution, "
+                                  "cells, x_q = M^-1 (b_q - K x_s))",
+                 "k_pc_top_lds": "k_pc_top_lds<false> (junctions above the cut)",
+                 "k_assemble_seg": "k_assemble_seg<16> (CSR values + rhs)"}
+        rocname = {"k_residual": "(anonymous namespace)::k_residual",
+                   "k_pc_up_lds": "void (anonymous namespace)::k_pc_up_lds<false, 8, 2>",
+                   "k_pc_down_lds": "void (anonymous namespace)::k_pc_down_lds<false, 8, 2>",
+                   "k_pc_top_lds": "void (anonymous namespace)::k_pc_top_lds<false>",
+                   "k_assemble_seg": "void (anonymous namespace)::k_assemble_seg<16>"}[dom]
+        traffic, tsrc, rocprof_ns = (pmc_traffic(rocname) if default_workload
+                                     else (None, None, None))
+        return {"bound": "hbm", "kernel": names.get(dom, dom),
+                "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": d["frac"], "traffic": traffic,
+                "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+                "traffic_source": tsrc,
+                "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
+                "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+                "avg_launch_ms": d["avg_launch_ms"], "kernels": kernels,
+                "assembly_kernel_ms": ms["k_assemble_seg"]}
+
+    roof = direct_roofline() if solver_used == "direct" else minres_roofline()
+    warm_spmv_ms = h.bench_spmv(200)
+    cold_spmv_ms, cold_copies = h.bench_spmv_cold(120)
+    sbytes = spmv_bytes(h.n_rows, h.nnz)
+    roof.update({"spmv_algorithmic_bytes": sbytes,
+                 "isolated_warm_spmv_ms": warm_spmv_ms,
+                 "isolated_warm_spmv_GBs": sbytes / (warm_spmv_ms * 1e-3) / 1e9,
+                 "isolated_cold_spmv_ms": cold_spmv_ms,
+                 "isolated_cold_spmv_GBs": sbytes / (cold_spmv_ms * 1e-3) / 1e9,
+                 "cold_rotation_copies": cold_copies})
+
+    # --- the other single-GPU solver on the same workload (same steps, same clock)
+    other = None
+    if world == 1 and pc_on:
+        asm.set_direct(solver_used != "direct")
+        el2 = timed_steps(h, args.steps, args.warmup, False)
+        used2 = "direct" if h.solver()[1] == 1 else "minres"
+        other = {"solver": used2, "ms_per_step": 1e3 * el2 / args.steps,
+                 "value": dof_total / (el2 / args.steps), "iterations": state["it"],
+                 "relres": state["relres"]}
+        if used2 == "minres":
+            other["roofline"] = minres_roofline()
+        asm.set_direct(direct)
+        step(h)  # leave the headline solver's solution in place for the parity check
+        state["it"] = iters
 
     # --- the public surface: Solver.assemble() + Solver.solve() returning the Functions
     # (the reference's nxfx:Solver:solve includes the assign into Functions, solver.py:107-135)
@@ -355,10 +469,16 @@ def run(args, world: int) -> int:
             el1 = timed_steps(asm1.handle, args.steps, args.warmup, False)
             t1 = 1e3 * el1 / args.steps
             it1 = state["it"]
+            # the same tree by the one-GPU default solver (direct tree solve)
+            asm1.set_direct(True)
+            el1d = timed_steps(asm1.handle, args.steps, args.warmup, False)
+            t1d = 1e3 * el1d / args.steps
             asm1.close()
             strong = {"workload": "same tree, one GPU (rank 0)", "n_gpus": world,
                       "t1_ms_per_step": t1, "tP_ms_per_step": ms_per_step,
                       "speedup_t1_over_tP": t1 / ms_per_step, "t1_minres_iterations": it1,
+                      "t1_direct_ms_per_step": t1d,
+                      "speedup_t1_direct_over_tP": t1d / ms_per_step,
                       "t1_setup_s": setup1}
         barrier()
 
@@ -387,7 +507,8 @@ def run(args, world: int) -> int:
                 "nnz": E * (7 * N + 1) + 6 * B,
                 "edges": E,
                 "N": N,
-                "minres_iterations": iters,
+                "solver": solver_used,
+                "iterations": iters,
                 "parallelism": f"edge-partition x{world}" if world > 1 else "single GPU",
                 "rccl_ranks": h.comm_count() if world > 1 else None,
                 "preconditioner": "tree Schur complement" if pc_on else "none",
@@ -395,28 +516,9 @@ def run(args, world: int) -> int:
             "setup_s": setup,
             "api_ms_per_step": api_ms,
             "strong_scaling": strong,
-            "roofline": {
-                "bound": "hbm",
-                "kernel": f"{kname} (CSR SpMV fused with the Lanczos step, Givens rotation and "
-                          "solution update)",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
-                "traffic_source": traffic_src,
-                "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
-                "algorithmic_bytes_per_launch": nbytes,
-                "avg_launch_ms": spmv_ms,
-                "spmv_algorithmic_bytes": sbytes,
-                "isolated_warm_spmv_ms": warm_spmv_ms,
-                "isolated_warm_spmv_GBs": sbytes / (warm_spmv_ms * 1e-3) / 1e9,
-                "isolated_cold_spmv_ms": cold_spmv_ms,
-                "isolated_cold_spmv_GBs": sbytes / (cold_spmv_ms * 1e-3) / 1e9,
-                "cold_rotation_copies": cold_copies,
-                "assembly_kernel_ms": asm_ms,
-            },
+            "solver": solver_used,
+            "roofline": roof,
+            "other_solver": other,
             "cpu_baseline": cpu,
             "parity": parity,
         }

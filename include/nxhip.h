@@ -137,8 +137,10 @@ int nx_set_source(nx_network_t* h, const double* edge_f);
 int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs);
 
 /*
- * MINRES (Paige-Saunders) on the device; replaces the KSP solve of
- * Solver.solve (solver.py:107-135; default there: LU/MUMPS).
+ * Solve on the device; replaces the KSP solve of Solver.solve (solver.py:107-135; default
+ * there: preonly + LU/MUMPS). MINRES (Paige-Saunders) by default, or the direct tree solve
+ * where nx_set_solver asked for it and it is exact (then iters = 1, or 2 after one
+ * refinement step, and relres is the true residual ||b - A x|| / ||b||).
  *   rtol         stop when the MINRES residual estimate ||r_k|| / ||b|| <= rtol
  *   maxit        iteration cap
  *   check_every  iterations per host convergence check (graph chunk), >= 2, even
@@ -299,6 +301,10 @@ int nx_sync(nx_network_t* h);
 int nx_set_profiling(nx_network_t* h, int32_t enable);
 int nx_get_profile(nx_network_t* h, double* spmv_ms, int64_t* spmv_count, double* asm_ms,
                    int64_t* asm_count);
+/* Direct solve (nx_set_solver 1, profiling on): summed kernel times (ms) of the up, top and
+ * down sweeps (mode kModeDirect) and of the residual SpMV, over `count` direct solves, each
+ * from events bound to the kernel's own dispatch (no graph while profiling). */
+int nx_get_profile_direct(nx_network_t* h, double* ms4, int64_t* count);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
 /* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,

@@ -60,6 +60,7 @@ _SIGS = {
     "nx_sync": (C.c_int, [_h]),
     "nx_set_profiling": (C.c_int, [_h, _i32]),
     "nx_get_profile": (C.c_int, [_h, _pd, _pi64, _pd, _pi64]),
+    "nx_get_profile_direct": (C.c_int, [_h, _pd, _pi64]),
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
     "nx_bench_spmv_cold": (C.c_int, [_h, _i32, _pi32, _pd]),
@@ -319,6 +320,14 @@ class Handle:
         a, b, c, d = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
         check(lib().nx_get_profile(self.ptr, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return {"spmv_ms": a.value, "spmv_count": b.value, "asm_ms": c.value, "asm_count": d.value}
+
+    def profile_direct(self):
+        """Direct solves under profiling: summed ms of up / top / down sweeps and residual."""
+        ms = (C.c_double * 4)()
+        n = C.c_int64(0)
+        check(lib().nx_get_profile_direct(self.ptr, ms, C.byref(n)))
+        return {"up_ms": ms[0], "top_ms": ms[1], "down_ms": ms[2], "residual_ms": ms[3],
+                "count": int(n.value)}
 
     def reset_profile(self) -> None:
         check(lib().nx_reset_profile(self.ptr))

@@ -1525,6 +1525,7 @@ __device__ __forceinline__ void direct_flux_rhs(const PcArgs& pa, const ChainLan
 }
 
 constexpr int kCapLvl = 64;  // job levels whose slot offsets are staged in LDS
+constexpr int kWaveKids = 4;  // junction children per slot of the one-wave level sweeps
 
 template <bool MULTI, int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __restrict__ y,
@@ -1536,6 +1537,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
                                                           int mode) {
   __shared__ double sT[kCapC], sIt[kCapC], sIb[kCapC];
   __shared__ double sD0[kCapS], sJ0[kCapS], sD[kCapS], sJ[kCapS];
+  __shared__ double sIv[kCapS];  // direct mode: 1 / D of every slot (one division per slot)
   __shared__ int sChild[kCapDC];
   __shared__ double sG[kCapDC];
   __shared__ int sOff[kCapS + 1];
@@ -1545,9 +1547,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   // alpha's partials first: their loads overlap the state read and the prefetch below
   const double pA = mode == 0 && !MULTI ? block_partial<kPcThreads>(partA, nA) : 0.0;
   const bool upd = mode == 0 && !(MULTI && pa.lin);
-  // direct solve (mode 3, single rank): y holds b; the chains condense w = K^T M^{-1} b_q - b
+  // direct solve (mode 3): y holds b; the chains condense w = K^T M^{-1} b_q - b
   // (formed here from b) and their It / Ib carry the multiplier rows' share of K^T M^{-1} b_q
-  const bool dir = !MULTI && mode == kModeDirect;
+  const bool dir = mode == kModeDirect;
   const int job = blockIdx.x;
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
@@ -1717,6 +1719,73 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   if ((int)threadIdx.x <= min(lv1 - lv0, kCapLvl)) sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
   __syncthreads();
   NX_PHASE(18);
+  // phase B by one wave when the job has <= 64 slots with <= kWaveKids junction children
+  // each (every job of the binary trees): lane = slot, the children's values by shuffles,
+  // no workgroup barrier per level (~0.5 us each). Same arithmetic in the same order.
+  int nkids = 0;
+  if ((int)threadIdx.x < ns)
+    for (int i = sOff[threadIdx.x]; i < sOff[threadIdx.x + 1]; ++i) nkids += sChild[i] >= 0;
+  const bool wave_lv = __syncthreads_or(nkids > kWaveKids) == 0 && ns <= 64 &&
+                       lv1 - lv0 <= kCapLvl;
+  if (wave_lv) {
+    if (threadIdx.x < 64) {
+      const int sl = threadIdx.x;
+      const bool mine = sl < ns;
+      int mylv = -1;
+      for (int q = 0; q < lv1 - lv0; ++q)
+        if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
+      int cl[kWaveKids];
+      double cg[kWaveKids];
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k) {
+        cl[k] = sl;
+        cg[k] = 0.0;
+      }
+      int nk = 0;
+      if (mine)
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int chd = sChild[i];
+          if (chd < 0) continue;
+#pragma unroll
+          for (int k = 0; k < kWaveKids; ++k)
+            if (k == nk) {
+              cl[k] = chd;
+              cg[k] = sG[i];
+            }
+          ++nk;
+        }
+      int kmax = nk;
+      for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+      double D = mine ? sD0[sl] : 1.0, J = mine ? sJ0[sl] : 0.0, iv = 1.0;
+      for (int q = lv1 - lv0 - 1; q >= 0; --q) {
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          if (k >= kmax) break;
+          const double Jc = __shfl(J, cl[k]);
+          const double Dc = __shfl(dir ? iv : D, cl[k]);
+          if (mylv == q && k < nk) {
+            const double g = cg[k];
+            if (fac) {
+              J += g * Jc;
+            } else if (dir) {
+              D += g * (1.0 - g * Dc);
+              J += g * Jc * Dc;
+            } else {
+              D += g * (1.0 - g / Dc);
+              J += g * Jc / Dc;
+            }
+          }
+        }
+        if (dir && mylv == q) iv = 1.0 / D;
+      }
+      if (mine) {
+        sD[sl] = D;
+        sJ[sl] = J;
+        if (dir) sIv[sl] = iv;
+      }
+    }
+    __syncthreads();
+  } else
   for (int lv = lv1 - 1; lv >= lv0; --lv) {  // phase B, deepest level first
     // level offsets staged in LDS with phase A (a global load per level costs a round trip)
     const int la = lv - lv0 <= kCapLvl ? sLvl[lv - lv0] : pa.lvl_slot_off[lv];
@@ -1729,6 +1798,15 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
           const int ch = sChild[i];
           if (ch >= 0) J += sG[i] * sJ[ch];
         }
+      } else if (dir) {  // the children's 1 / D: no division on the level's critical path
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int ch = sChild[i];
+          if (ch < 0) continue;
+          const double g = sG[i], iv = sIv[ch];
+          D += g * (1.0 - g * iv);
+          J += g * sJ[ch] * iv;
+        }
+        sIv[sl] = 1.0 / D;
       } else {
         for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
           const int ch = sChild[i];
@@ -1749,6 +1827,12 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     pa.slot_J[j] = J;
     if (fac) {
       pa.slot_A[j] = J * pa.slot_invD[j];
+    } else if (dir) {
+      const int pcn = pa.slot_pchain[j];
+      const double iv = sIv[sl];
+      pa.slot_D[j] = sD[sl];
+      pa.slot_A[j] = J * iv;
+      pa.slot_B[j] = pcn >= 0 ? iv / sT[pcn - c0] : 0.0;
     } else {
       const int pcn = pa.slot_pchain[j];
       const double D = sD[sl];
@@ -1842,7 +1926,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
       yl -= c2 * r2[lam];
       y[lam] = yl;
     }
-    if (!MULTI && mode == kModeDirect) yl = -yl;  // direct solve: see k_pc_up_lds
+    if (mode == kModeDirect) yl = -yl;  // direct solve: see k_pc_up_lds
     sLam[sl] = lam;
     sY[sl] = yl;
     const int pcn = pre ? p_pcn : pa.slot_pchain[j];
@@ -1868,16 +1952,30 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   }
   __syncthreads();
   NX_PHASE(34);
+  // direct mode: sY holds 1 / D of every slot once its level is done (one division per
+  // slot instead of two per child on the level's critical path; sY's partial is not needed)
+  const bool dir = mode == kModeDirect;
   for (int lv = nl - 1; lv >= 0; --lv) {
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
       const int sl = j - ts0;
       double D = sD0[sl], J = sJ0[sl];
-      for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
-        const int ch = sChild[i];
-        if (ch < 0) continue;
-        const double g = sG[i], Dc = sD[ch];
-        D += g * (1.0 - g / Dc);
-        J += g * sJ[ch] / Dc;
+      if (dir) {
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int ch = sChild[i];
+          if (ch < 0) continue;
+          const double g = sG[i], iv = sY[ch];
+          D += g * (1.0 - g * iv);
+          J += g * sJ[ch] * iv;
+        }
+        sY[sl] = 1.0 / D;
+      } else {
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int ch = sChild[i];
+          if (ch < 0) continue;
+          const double g = sG[i], Dc = sD[ch];
+          D += g * (1.0 - g / Dc);
+          J += g * sJ[ch] / Dc;
+        }
       }
       sD[sl] = D;
       sJ[sl] = J;
@@ -1898,11 +1996,12 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
       const int sl = j - ts0;
       const int p = sPar[sl];
-      const double zj = (sJ[sl] + (p >= 0 ? sGp[sl] * sJ0[p] : 0.0)) / sD[sl];
+      const double num = sJ[sl] + (p >= 0 ? sGp[sl] * sJ0[p] : 0.0);
+      const double zj = dir ? num * sY[sl] : num / sD[sl];
       sJ0[sl] = zj;  // reuse: z of top slots
       z[sLam[sl]] = zj;
       pa.slot_z[ts0 + sl] = zj;
-      part += sY[sl] * zj;
+      if (!dir) part += sY[sl] * zj;
     }
     __syncthreads();
   }
@@ -1911,7 +2010,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     pa.slot_D[ts0 + sl] = sD[sl];
     pa.slot_J[ts0 + sl] = sJ[sl];
   }
-  block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
+  if (!dir) block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
   NX_PHASE_END(32);
 }
 
@@ -2002,9 +2101,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
-  // direct solve (mode 3, single rank): y holds b, z is the solution x; the chains form the
+  // direct solve (mode 3): y holds b, z is the solution x; the chains form the
   // cell inputs w from b again (as k_pc_up_lds did) and finish x_q = M^{-1} (b_q - K x_s)
-  const bool dir = !MULTI && mode == kModeDirect;
+  const bool dir = mode == kModeDirect;
   NX_PHASE_START(48);
   const int job = blockIdx.x;
   double part = 0.0;
@@ -2146,6 +2245,24 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
   __syncthreads();
   NX_PHASE(49);
+  if (ns <= 64 && lv1 - lv0 <= kCapLvl) {  // one wave: lane = slot, parent by shuffle
+    if (threadIdx.x < 64) {
+      const int sl = threadIdx.x;
+      const bool mine = sl < ns;
+      int mylv = -1;
+      for (int q = 0; q < lv1 - lv0; ++q)
+        if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
+      const double A = mine ? sA[sl] : 0.0, Bv = mine ? sB[sl] : 0.0;
+      const int p = mine ? sP[sl] : -1;
+      double zv = mine ? sZ[sl] : 0.0;  // an outside parent's value for the job root
+      for (int q = 0; q < lv1 - lv0; ++q) {
+        const double zp = __shfl(zv, p >= 0 ? p : sl);
+        if (mylv == q) zv = A + Bv * zp;
+      }
+      if (mine) sZ[sl] = zv;
+    }
+    __syncthreads();
+  } else
   for (int lv = lv0; lv < lv1; ++lv) {  // phase B, root level first, LDS only
     const int la = lv - lv0 <= kCapLvl ? sLvl[lv - lv0] : pa.lvl_slot_off[lv];
     const int lb = lv - lv0 < kCapLvl ? sLvl[lv - lv0 + 1] : pa.lvl_slot_off[lv + 1];
@@ -2239,7 +2356,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, z);
   }
   NX_PHASE(51);
-  block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
+  if (!dir) block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
   NX_PHASE_END(48);
   if (MULTI && cfused && pa.fuse_pack) pc_pack_last(pa, partB, z);
   // single rank, start application: D is final -> factored coefficients and G here, so the
@@ -2749,6 +2866,52 @@ __global__ __launch_bounds__(kBlock) void k_dir_post(PcArgs pa, int n_chains, in
   if (ch.has_last) x[ch.dof_qN] = ACC ? x[ch.dof_qN] + xv[CPL] : xv[CPL];
 }
 
+// Several ranks: this rank's ||r||^2 and ||b||^2 partial sums -> out[0], out[1] (then
+// all-reduced and published by k_dir_publish_red).
+__global__ __launch_bounds__(kReduceThreads) void k_dir_reduce2(const double* __restrict__ p,
+                                                                int nblk, double* __restrict__ out) {
+  __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
+  double rr = 0.0, bb = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += kReduceThreads) {
+    rr += p[i];
+    bb += p[nblk + i];
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_r[threadIdx.x >> 6] = rr;
+    s_b[threadIdx.x >> 6] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    rr = 0.0;
+    bb = 0.0;
+    for (int w = 0; w < kReduceThreads / 64; ++w) {
+      rr += s_r[w];
+      bb += s_b[w];
+    }
+    out[0] = rr;
+    out[1] = bb;
+  }
+}
+
+__global__ void k_dir_publish_red(const double* __restrict__ rb, double rtol, int* seq,
+                                  MrState* mirror) {
+  if (threadIdx.x != 0) return;
+  const double rr = rb[0], bb = rb[1];
+  MrState s{};
+  s.beta1 = sqrt(bb);
+  s.relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
+  s.rtol = rtol;
+  s.it = 1;
+  s.done = 1;
+  s.converged = s.relres <= rtol ? 1 : 0;
+  MrInit ini{};
+  ini.seq = seq;
+  ini.mirror = mirror;
+  mr_publish(s, ini);
+}
+
 // x += d (the refinement step of the fused direct solve)
 __global__ __launch_bounds__(kBlock) void k_axpy1(int64_t n, const double* __restrict__ d,
                                                   double* __restrict__ x) {
@@ -2761,10 +2924,27 @@ __global__ __launch_bounds__(kBlock) void k_axpy1(int64_t n, const double* __res
 __global__ __launch_bounds__(kReduceThreads) void k_dir_publish(const double* __restrict__ p,
                                                                 int nblk, double rtol, int* seq,
                                                                 MrState* mirror) {
-  const double rr = reduce_partials(p, nblk);
+  // both sums in one pass (fixed order: thread-strided, then waves, then thread 0)
+  __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
+  double rr = 0.0, bb = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += kReduceThreads) {
+    rr += p[i];
+    bb += p[nblk + i];
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_r[threadIdx.x >> 6] = rr;
+    s_b[threadIdx.x >> 6] = bb;
+  }
   __syncthreads();
-  const double bb = reduce_partials(p + nblk, nblk);
   if (threadIdx.x == 0) {
+    rr = 0.0;
+    bb = 0.0;
+    for (int w = 0; w < kReduceThreads / 64; ++w) {
+      rr += s_r[w];
+      bb += s_b[w];
+    }
     MrState s{};
     s.beta1 = sqrt(bb);
     s.relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
@@ -2835,11 +3015,17 @@ struct LeanGraphs {
   hipGraphExec_t lchunk_exec = nullptr;
   hipGraph_t lchunk_graph = nullptr;
   int lchunk_len = 0;
-  // direct tree solve (nx_set_solver(h, 1)): one graph per solve
+  double lchunk_rtol = 0.0;  // the direct solve's refinement graph (lchunk_len = -1)
+  // direct tree solve (nx_set_solver(h, 1)): one graph per solve; the _asm one starts with
+  // the deferred assembly of values and rhs
   hipGraphExec_t direct_exec = nullptr;
   hipGraph_t direct_graph = nullptr;
   int direct_len = 0;
   double direct_rtol = 0.0;
+  hipGraphExec_t direct_asm_exec = nullptr;
+  hipGraph_t direct_asm_graph = nullptr;
+  int direct_asm_len = 0;
+  double direct_asm_rtol = 0.0;
 };
 
 struct nx_network {
@@ -2908,6 +3094,10 @@ struct nx_network {
   double spmv_ms = 0.0, asm_ms = 0.0;
   int64_t spmv_cnt = 0, asm_cnt = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  // direct solve profiling: event pairs of up, top, down, residual; summed times, launches
+  hipEvent_t dev[8] = {};
+  double dir_ms[4] = {0.0, 0.0, 0.0, 0.0};
+  int64_t dir_cnt = 0;
   std::vector<hipEvent_t> ev_pool;  // SpMV timing pairs inside one convergence chunk
   int prof_k = 0;
   // multi-rank: halo plan (nx_set_halo) and transport -- an RCCL communicator (one
@@ -2927,12 +3117,14 @@ struct nx_network {
   bool beta_p2p = true;
   bool rccl_graph_ok = true;  // capture of the RCCL iteration worked (or was not tried)
   bool sched_checked = false; // RCCL: the ranks' kernel schedules were compared (per pc)
+  bool direct_all = false;    // RCCL: every rank can run the direct solve (check_schedules)
   bool last_graph = false;    // the last nx_solve replayed HIP graphs
   // solver (nx_set_solver): 0 = MINRES, 1 = direct tree solve where it is exact (one rank,
   // exact preconditioner on a forest: tree_exact from the host decomposition), else MINRES
   int solver = 0;
   bool tree_exact = false;
   int last_solver = 0;        // what the last nx_solve ran (0 MINRES, 1 direct)
+  int pend_lhs = 0, pend_rhs = 0;  // deferred nx_assemble (flush_assembly)
   // general element degrees (nx_create_fe): gather-assembly tables, one rank, no
   // preconditioner
   // nx_set_output_map: owned rows in the reference's function order (Solver.solve output)
@@ -2960,6 +3152,8 @@ struct nx_group {
 };
 
 namespace {
+
+int flush_assembly(nx_network* h);  // a deferred nx_assemble (defined with nx_assemble)
 
 int grid_of(int64_t n, int per) { return (int)((n + per - 1) / per); }
 
@@ -3121,20 +3315,25 @@ __global__ __launch_bounds__(kGcThreads) void k_pc_gc(PcArgs pa) {
 // buffer is all-reduced between the halves and k_pc_coarse finishes the top part.
 template <bool MULTI, int W, int CPL>
 void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other,
-                  int mode, int half, double* zout) {
+                  int mode, int half, double* zout, const hipEvent_t* evs) {
+  // evs (profiling, LDS kernels): event pairs bound to the up / top / down dispatches
   const bool coarse = MULTI && h->pa.n_coarse > 0;
   double* const z = zout ? zout : h->z;
+  hipEvent_t e[6] = {};
+  if (evs)
+    for (int i = 0; i < 6; ++i) e[i] = evs[i];
   if (half == 0) {
     if (h->pc_lds) {
       if (h->pc_jobs > 0)
-        hipLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
-                           h->stream, h->pa, y, r2, st, other, h->partA, h->nA, h->red, mode);
+        hipExtLaunchKernelGGL((k_pc_up_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
+                              h->stream, e[0], e[1], 0, h->pa, y, r2, st, other, h->partA, h->nA,
+                              h->red, mode);
       if (MULTI && h->pa.mdense && mode == 0) {  // dense top: the coarse partials only
         if (!h->pa.fused)  // else the up sweep's last workgroup computes them
           hipLaunchKernelGGL(k_pc_cpart, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, st, mode);
       } else if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
-        hipLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream,
-                           h->pa, y, r2, z, st, h->partA, h->nA, h->red, h->partB, mode);
+        hipExtLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, e[2],
+                              e[3], 0, h->pa, y, r2, z, st, h->partA, h->nA, h->red, h->partB, mode);
     } else {
       if (h->pc_jobs > 0)
         hipLaunchKernelGGL((k_pc_up<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
@@ -3151,8 +3350,8 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
                        st, h->partB, mode);
   if (h->pc_jobs > 0) {
     if (h->pc_lds)
-      hipLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
-                         h->stream, h->pa, y, r2, z, st, h->partB, mode);
+      hipExtLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
+                            h->stream, e[4], e[5], 0, h->pa, y, r2, z, st, h->partB, mode);
     else
       hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
                          h->pa, y, z, st, h->partB, mode);
@@ -3165,18 +3364,18 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
 
 template <bool MULTI>
 void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState* other, int mode,
-               int half, double* zout = nullptr) {
+               int half, double* zout = nullptr, const hipEvent_t* evs = nullptr) {
   switch (h->pc_variant) {
-    case 0: launch_pc_wc<MULTI, 16, 1>(h, y, r2, st, other, mode, half, zout); break;
-    case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode, half, zout); break;
-    case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode, half, zout); break;
-    case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode, half, zout); break;
-    case 5: launch_pc_wc<MULTI, 8, 2>(h, y, r2, st, other, mode, half, zout); break;
-    case 6: launch_pc_wc<MULTI, 4, 4>(h, y, r2, st, other, mode, half, zout); break;
-    case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half, zout); break;
-    case 8: launch_pc_wc<MULTI, 64, 8>(h, y, r2, st, other, mode, half, zout); break;
-    case 9: launch_pc_wc<MULTI, 64, 16>(h, y, r2, st, other, mode, half, zout); break;
-    default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half, zout); break;
+    case 0: launch_pc_wc<MULTI, 16, 1>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 1: launch_pc_wc<MULTI, 16, 2>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 2: launch_pc_wc<MULTI, 16, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 3: launch_pc_wc<MULTI, 64, 2>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 5: launch_pc_wc<MULTI, 8, 2>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 6: launch_pc_wc<MULTI, 4, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 8: launch_pc_wc<MULTI, 64, 8>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 9: launch_pc_wc<MULTI, 64, 16>(h, y, r2, st, other, mode, half, zout, evs); break;
+    default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
   }
 }
 
@@ -3342,6 +3541,8 @@ int drop_graph(GraphSlot gs) {
     CHECK(drop_one(&gs.lean->head_exec, &gs.lean->head_graph, &gs.lean->head_len));
     CHECK(drop_one(&gs.lean->lchunk_exec, &gs.lean->lchunk_graph, &gs.lean->lchunk_len));
     CHECK(drop_one(&gs.lean->direct_exec, &gs.lean->direct_graph, &gs.lean->direct_len));
+    CHECK(drop_one(&gs.lean->direct_asm_exec, &gs.lean->direct_asm_graph,
+                   &gs.lean->direct_asm_len));
   }
   return NX_OK;
 }
@@ -3694,6 +3895,7 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
 }
 
 NX_API int nx_destroy(nx_network_t* h) {
+  if (h) h->pend_lhs = h->pend_rhs = 0;  // nothing to assemble for a dying handle
   if (h == nullptr) return NX_OK;
   if (h->group) return fail(NX_ERR_STATE, "destroy the group (nx_group_destroy) first");
   (void)hipSetDevice(h->device);
@@ -3721,6 +3923,8 @@ NX_API int nx_destroy(nx_network_t* h) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : h->ev_pool)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : h->dev)
+    if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return NX_OK;
@@ -3736,6 +3940,7 @@ NX_API int nx_dims(nx_network_t* h, int64_t* n_rows, int64_t* n_cols, int64_t* n
 
 NX_API int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_const, double f,
                                const double* edge_bc) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (h->E > 0 && edge_bc == nullptr) return fail(NX_ERR_ARG, "edge_bc is NULL");
   CHECK(set_device(h));
@@ -3759,6 +3964,7 @@ NX_API int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_c
 }
 
 NX_API int nx_set_source(nx_network_t* h, const double* edge_f) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   CHECK(set_device(h));
   if (edge_f == nullptr) {
@@ -3775,11 +3981,10 @@ NX_API int nx_set_source(nx_network_t* h, const double* edge_f) {
   return NX_OK;
 }
 
-NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
-  if (!h) return fail(NX_ERR_ARG, "null handle");
-  if (!h->have_coeffs) return fail(NX_ERR_STATE, "nx_set_coefficients must be called first");
-  CHECK(set_device(h));
-  if (!lhs && !rhs) return NX_OK;
+namespace {
+
+// Launch the assembly kernel (values and / or rhs) on the handle's stream.
+int launch_assembly(nx_network* h, int lhs, int rhs) {
   if (h->fe) {  // general degrees: one thread per nonzero / rhs row
     FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind, h->fe_tval,
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
@@ -3788,8 +3993,6 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
     hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
                           dim3(kBlock), 0, h->stream, e0, e1, 0, a);
     HIPCALL(hipGetLastError());
-    if (lhs) h->have_lhs = true;
-    if (rhs) h->have_rhs = true;
     return NX_OK;
   }
   // one launch: edge blocks (4 edges each) then the multiplier-row blocks
@@ -3811,12 +4014,49 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
       hipExtLaunchKernelGGL(k_assemble, dim3(eb + lb), dim3(kBlock), 0, h->stream, e0, e1, 0, a);
   }
   HIPCALL(hipGetLastError());
-  if (h->prof && h->E > 0) {
-    HIPCALL(hipEventSynchronize(h->ev[1]));
-    float ms = 0.f;
-    HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-    h->asm_ms += ms;
-    h->asm_cnt += 1;
+  return NX_OK;
+}
+
+// Deferred assembly: on one rank (no group, no communicator, P1/DG0) nx_assemble only
+// records what to assemble, and the next call that uses the device -- every NX_API entry
+// point flushes it first -- launches it; the direct solve captures it as the head of its
+// own graph instead (one launch per step less). NXHIP_DEFER=0 launches at once.
+bool defer_ok(const nx_network* h) {
+  static const bool env = [] {
+    const char* e = std::getenv("NXHIP_DEFER");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return env && !h->fe && !h->prof && h->nranks == 1 && h->comm == nullptr && h->group == nullptr;
+}
+
+int flush_assembly(nx_network* h) {
+  if (!h || !(h->pend_lhs || h->pend_rhs)) return NX_OK;
+  const int lhs = h->pend_lhs, rhs = h->pend_rhs;
+  h->pend_lhs = h->pend_rhs = 0;
+  CHECK(set_device(h));
+  return launch_assembly(h, lhs, rhs);
+}
+
+}  // namespace
+
+NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->have_coeffs) return fail(NX_ERR_STATE, "nx_set_coefficients must be called first");
+  if (!lhs && !rhs) return NX_OK;
+  if (defer_ok(h)) {
+    h->pend_lhs |= lhs ? 1 : 0;
+    h->pend_rhs |= rhs ? 1 : 0;
+  } else {
+    CHECK(flush_assembly(h));
+    CHECK(set_device(h));
+    CHECK(launch_assembly(h, lhs, rhs));
+    if (h->prof && h->E > 0) {
+      HIPCALL(hipEventSynchronize(h->ev[1]));
+      float ms = 0.f;
+      HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+      h->asm_ms += ms;
+      h->asm_cnt += 1;
+    }
   }
   if (lhs) h->have_lhs = true;
   if (rhs) h->have_rhs = true;
@@ -3946,7 +4186,8 @@ LeanGraphs& lean_of(const Team& t) { return t.g ? t.g->lean : t.hs[0]->lean; }
 // refine = 0: x = A^{-1} b; refine = 1: one step of iterative refinement, r = b - A x
 // (into tmp), x += A^{-1} r. Both end with the true residual published.
 template <int W, int CPL>
-void launch_direct_wc(nx_network* h, double rtol, int refine) {
+void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
+  const hipEvent_t* evs = prof ? h->dev : nullptr;
   constexpr int G = kBlock / W;
   const int cb = grid_of(h->E, G);
   double* yq = h->vb[1];
@@ -3959,8 +4200,8 @@ void launch_direct_wc(nx_network* h, double rtol, int refine) {
   }
   if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
     double* xo = refine ? w : h->x;  // refinement: the correction, then x += it
-    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, xo);
-    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, xo);
+    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, xo, evs);
+    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, xo, evs);
     if (refine)
       hipLaunchKernelGGL(k_axpy1, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
                          h->n_own, (const double*)w, h->x);
@@ -3984,24 +4225,25 @@ void launch_direct_wc(nx_network* h, double rtol, int refine) {
                          h->pa, (int)h->E, cb, h->edge_lm, h->n_edge_dofs, h->n_own, bin, h->z, h->x);
   }
   }  // unfused
-  hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                     h->rhs, h->partials, h->nblk, nullptr);
+  hipExtLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream,
+                        prof ? h->dev[6] : nullptr, prof ? h->dev[7] : nullptr, 0, csr_of(h), h->x,
+                        h->rhs, h->partials, h->nblk, (double*)nullptr);
   hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
                      h->nblk, rtol, h->d_seq, h->d_last);
 }
 
-int launch_direct(nx_network* h, double rtol, int refine) {
+int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
   switch (h->pc_variant) {
-    case 0: launch_direct_wc<16, 1>(h, rtol, refine); break;
-    case 1: launch_direct_wc<16, 2>(h, rtol, refine); break;
-    case 2: launch_direct_wc<16, 4>(h, rtol, refine); break;
-    case 3: launch_direct_wc<64, 2>(h, rtol, refine); break;
-    case 5: launch_direct_wc<8, 2>(h, rtol, refine); break;
-    case 6: launch_direct_wc<4, 4>(h, rtol, refine); break;
-    case 7: launch_direct_wc<8, 4>(h, rtol, refine); break;
-    case 8: launch_direct_wc<64, 8>(h, rtol, refine); break;
-    case 9: launch_direct_wc<64, 16>(h, rtol, refine); break;
-    default: launch_direct_wc<64, 4>(h, rtol, refine); break;
+    case 0: launch_direct_wc<16, 1>(h, rtol, refine, prof); break;
+    case 1: launch_direct_wc<16, 2>(h, rtol, refine, prof); break;
+    case 2: launch_direct_wc<16, 4>(h, rtol, refine, prof); break;
+    case 3: launch_direct_wc<64, 2>(h, rtol, refine, prof); break;
+    case 5: launch_direct_wc<8, 2>(h, rtol, refine, prof); break;
+    case 6: launch_direct_wc<4, 4>(h, rtol, refine, prof); break;
+    case 7: launch_direct_wc<8, 4>(h, rtol, refine, prof); break;
+    case 8: launch_direct_wc<64, 8>(h, rtol, refine, prof); break;
+    case 9: launch_direct_wc<64, 16>(h, rtol, refine, prof); break;
+    default: launch_direct_wc<64, 4>(h, rtol, refine, prof); break;
   }
   HIPCALL(hipGetLastError());
   return NX_OK;
@@ -4009,41 +4251,154 @@ int launch_direct(nx_network* h, double rtol, int refine) {
 
 // Exact on this handle: one rank (no communicator, no group), the exact Schur-complement
 // preconditioner (consistent mass) on a decomposition without grounded cycle chains.
-bool direct_applicable(const nx_network* h) {
-  return h->solver == 1 && h->pc && h->pa.exact && h->tree_exact && h->nranks == 1 &&
-         h->comm == nullptr && h->group == nullptr && h->E > 0;
+// This rank can run the direct solve exactly: the exact Schur-complement preconditioner
+// (consistent mass) on a decomposition without grounded cycle chains; with several ranks
+// also the LDS sweeps (their mode kModeDirect) and the coarse step.
+bool direct_local(const nx_network* h) {
+  if (!(h->solver == 1 && h->pc && h->pa.exact && h->tree_exact && h->E > 0)) return false;
+  const bool multi = h->comm != nullptr || h->group != nullptr || h->nranks > 1;
+  return !multi || (h->pc_lds && h->pc_jobs > 0 && h->pa.n_coarse > 0 &&
+                    h->pa.n_coarse <= kCapCoarse);
 }
 
-// One graph: pre, multiplier rows, S^{-1} (up / top / down, mode 2), post, residual,
-// publish. The tree formula is exact but not backward stable to the last digits (its true
-// residual is ~1e-13 .. 1e-11 where a sparse LU reaches ~1e-15; the forward error stays
-// ~1e-12): when the residual misses rtol, a second graph applies one step of iterative
-// refinement (residual -> direct solve -> x += correction; ~1e-15 after it). Returns NX_OK
-// with *converged = 0 if that is still above rtol (the caller runs MINRES).
-int solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
-                 int32_t* converged) {
-  LeanGraphs& lg = h->lean;
-  if (!lg.direct_exec || lg.direct_rtol != rtol) {
-    CHECK(drop_one(&lg.direct_exec, &lg.direct_graph, &lg.direct_len));
-    CHECK(drop_one(&lg.lchunk_exec, &lg.lchunk_graph, &lg.lchunk_len));
-    CHECK(capture(h, &lg.direct_graph, &lg.direct_exec, [&] { return launch_direct(h, rtol, 0); }));
-    lg.direct_len = 1;
-    lg.direct_rtol = rtol;
-  }
-  h->last_graph = true;
-  HIPCALL(hipGraphLaunch(lg.direct_exec, h->stream));
-  h->seq += 1;
-  CHECK(wait_published(h));
-  MrState s = *h->h_last;
-  if (!s.converged && s.relres == s.relres) {  // one refinement step (graph kept in lchunk)
-    if (!lg.lchunk_exec || lg.lchunk_len != -1) {
-      CHECK(drop_one(&lg.lchunk_exec, &lg.lchunk_graph, &lg.lchunk_len));
-      CHECK(capture(h, &lg.lchunk_graph, &lg.lchunk_exec, [&] { return launch_direct(h, rtol, 1); }));
-      lg.lchunk_len = -1;  // marks the refinement graph (MINRES continuation chunks use L > 0)
+// The ranks decide together: a group compares its handles here, RCCL ranks agreed in
+// check_schedules (all-reduced with the schedule signature).
+bool direct_applicable(const Team& t) {
+  if (t.hs[0]->comm) return t.hs[0]->sched_checked && t.hs[0]->direct_all;
+  for (int r = 0; r < t.P; ++r)
+    if (!direct_local(t.hs[r])) return false;
+  return true;
+}
+
+// Several ranks (RCCL, one process per GPU; or an in-process group): every rank's fused
+// sweeps in mode kModeDirect with the coarse all-reduce between the halves (every rank then
+// solves the coarse forest redundantly -- same inputs, same order, same bits -- and
+// back-substitutes from it), the halo of x (remote flux ends read by the multiplier rows),
+// and one all-reduce of the residual sums, published by every rank.
+int launch_direct_team(const Team& t, double rtol, int refine) {
+  nx_network* h0 = t.hs[0];
+  if (refine) {  // r = b - A x (x's ghosts from the owners first); ghost slots of r are 0
+    CHECK(team_halo(t, VS_X, 0));
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                         h->rhs, h->partials, h->nblk, h->tmp);
+      if (h->n_col > h->n_own)
+        HIPCALL(hipMemsetAsync(h->tmp + h->n_own, 0, sizeof(double) * (h->n_col - h->n_own),
+                               h->stream));
     }
-    HIPCALL(hipGraphLaunch(lg.lchunk_exec, h->stream));
+  }
+  for (int half = 0; half < 2; ++half) {
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      double* bin = refine ? h->tmp : h->rhs;
+      launch_pc<true>(h, bin, bin, h->st, h->st + 1, kModeDirect, half, refine ? h->vb[0] : h->x);
+    }
+    if (half == 0) CHECK(team_allreduce(t, -1, 3 * h0->pa.n_coarse));
+  }
+  for (int r = 0; r < t.P && refine; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_axpy1, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
+                       h->n_own, (const double*)h->vb[0], h->x);
+  }
+  CHECK(team_halo(t, VS_X, 0));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, h->nblk, (double*)nullptr);
+    hipLaunchKernelGGL(k_dir_reduce2, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                       h->nblk, h->red + 2);
+  }
+  CHECK(team_allreduce(t, 2, 2));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_dir_publish_red, dim3(1), dim3(64), 0, h->stream, h->red + 2, rtol,
+                       h->d_seq, h->d_last);
+  }
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+// The direct solve of a team (one rank, a group or an RCCL rank): one graph -- on one rank
+// headed by the deferred assembly -- then the published true residual. The tree formula is
+// exact but not backward stable to the last digits (its true residual is ~1e-13 .. 1e-11
+// where a sparse LU reaches ~1e-15; the forward error stays ~1e-12): when the residual misses
+// rtol, a second graph applies one step of iterative refinement (residual -> direct solve
+// -> x += correction; ~1e-15 after it). Returns NX_OK with *converged = 0 if that is still
+// above rtol (the caller runs MINRES). RCCL that refuses the capture: eager launches.
+int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
+                 int32_t* converged) {
+  const bool multi = team_multi(t);
+  nx_network* h = t.hs[0];
+  LeanGraphs& lg = lean_of(t);
+  if (!multi && h->prof) {  // eager, with events bound to the sweeps' and the residual's dispatches
+    if (!h->dev[0])
+      for (auto& e : h->dev) HIPCALL(hipEventCreate(&e));
+    CHECK(launch_direct(h, rtol, 0, true));
     h->seq += 1;
     CHECK(wait_published(h));
+    HIPCALL(hipStreamSynchronize(h->stream));
+    const bool fused = h->pc_lds;
+    for (int k = 0; k < 4; ++k) {
+      if (k < 3 && !fused) continue;
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, h->dev[2 * k], h->dev[2 * k + 1]) == hipSuccess)
+        h->dir_ms[k] += ms;
+    }
+    h->dir_cnt += 1;
+    const MrState s = *h->h_last;
+    if (iters) *iters = s.it;
+    if (relres) *relres = s.relres;
+    if (converged) *converged = s.converged;
+    return NX_OK;
+  }
+  const bool with_asm = !multi && h->pend_lhs && h->pend_rhs;  // deferred assembly heads it
+  for (int r = 0; r < t.P; ++r)
+    if (!with_asm) CHECK(flush_assembly(t.hs[r]));
+  auto body = [&](int refine, bool asmb) -> int {
+    if (multi) return launch_direct_team(t, rtol, refine);
+    if (asmb) CHECK(launch_assembly(h, 1, 1));
+    return launch_direct(h, rtol, refine);
+  };
+  const bool graphs = !h->comm || h->rccl_graph_ok;
+  auto run = [&](hipGraphExec_t* exec, hipGraph_t* graph, int* len, double* grtol, int key,
+                 int refine, bool asmb) -> int {
+    if (graphs && (!*exec || *grtol != rtol || *len != key)) {
+      CHECK(drop_one(exec, graph, len));
+      const int rc = capture(h, graph, exec, [&] { return body(refine, asmb); });
+      if (rc != NX_OK && h->comm) {  // RCCL refused the capture: eager from now on
+        (void)hipGetLastError();
+        h->rccl_graph_ok = false;
+      } else {
+        CHECK(rc);
+        *len = key;
+        *grtol = rtol;
+      }
+    }
+    h->last_graph = graphs && h->rccl_graph_ok;
+    if (h->last_graph) {
+      HIPCALL(hipGraphLaunch(*exec, h->stream));
+    } else {
+      CHECK(body(refine, asmb));
+    }
+    for (int r = 0; r < t.P; ++r) t.hs[r]->seq += 1;
+    for (int r = 0; r < t.P; ++r) CHECK(wait_published(t.hs[r]));
+    const MrState& s0 = *h->h_last;
+    for (int r = 1; r < t.P; ++r)  // every rank published the same all-reduced sums
+      if (t.hs[r]->h_last->relres != s0.relres && s0.relres == s0.relres)
+        return fail(NX_ERR_STATE, "ranks disagree on the direct solve's residual");
+    return NX_OK;
+  };
+  hipGraphExec_t* exec = with_asm ? &lg.direct_asm_exec : &lg.direct_exec;
+  hipGraph_t* graph = with_asm ? &lg.direct_asm_graph : &lg.direct_graph;
+  int* len = with_asm ? &lg.direct_asm_len : &lg.direct_len;
+  double* grtol = with_asm ? &lg.direct_asm_rtol : &lg.direct_rtol;
+  CHECK(run(exec, graph, len, grtol, 1, 0, with_asm));
+  h->pend_lhs = h->pend_rhs = 0;
+  MrState s = *h->h_last;
+  if (!s.converged && s.relres == s.relres) {  // one refinement step (graph kept in lchunk;
+                                                // MINRES continuation chunks use len > 0)
+    CHECK(run(&lg.lchunk_exec, &lg.lchunk_graph, &lg.lchunk_len, &lg.lchunk_rtol, -1, 1, false));
     s = *h->h_last;
     s.it = 2;
   }
@@ -4156,6 +4511,7 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
 // kernels' linear form would pair different collectives). Each rank decides from its own
 // decomposition (LDS caps), so the ranks compare.
 constexpr int kSchedSig = 8;
+bool direct_local(const nx_network* h);
 void sched_sig(const nx_network* h, int* s) {
   s[0] = h->pc;
   s[1] = h->pc && h->pc_lds;
@@ -4182,16 +4538,19 @@ int check_schedules(const Team& t) {
   }
   nx_network* h = t.hs[0];
   if (!h->comm || h->sched_checked) return NX_OK;
-  int v[2 * kSchedSig];  // max of s and of -s over the ranks: equal iff all ranks agree
+  // max of s and of -s over the ranks: equal iff all ranks agree; the last entry is the
+  // max of -direct_local: the direct solve runs only if every rank can run it
+  int v[2 * kSchedSig + 1];
   for (int i = 0; i < kSchedSig; ++i) {
     v[i] = s0[i];
     v[kSchedSig + i] = -s0[i];
   }
+  v[2 * kSchedSig] = direct_local(h) ? -1 : 0;
   int* d = nullptr;
   HIPCALL(hipMalloc((void**)&d, sizeof(v)));
   int rc = NX_OK;
   if (hipMemcpy(d, v, sizeof(v), hipMemcpyHostToDevice) != hipSuccess ||
-      ncclAllReduce(d, d, 2 * kSchedSig, ncclInt32, ncclMax, h->comm, h->stream) != ncclSuccess ||
+      ncclAllReduce(d, d, 2 * kSchedSig + 1, ncclInt32, ncclMax, h->comm, h->stream) != ncclSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess ||
       hipMemcpy(v, d, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(NX_ERR_RCCL, "kernel schedule comparison across ranks failed");
@@ -4202,6 +4561,7 @@ int check_schedules(const Team& t) {
       return fail(NX_ERR_STATE, "ranks chose different kernel schedules (item " +
                                     std::to_string(i) + ": preconditioner decomposition "
                                     "outside the LDS caps on some ranks)");
+  h->direct_all = v[2 * kSchedSig] == -1;
   h->sched_checked = true;
   return NX_OK;
 }
@@ -4215,18 +4575,23 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   }
   if (maxit < 1) return fail(NX_ERR_ARG, "maxit must be >= 1");
   if (check_every < 2) check_every = 2;
-  t.hs[0]->last_solver = 0;
-  if (t.P == 1 && t.g == nullptr && direct_applicable(t.hs[0])) {
+  for (int r = 0; r < t.P; ++r) t.hs[r]->last_solver = 0;
+  if (team_multi(t)) {  // every rank must take the same path (the signature holds it)
+    CHECK(set_device(t.hs[0]));
+    CHECK(check_schedules(t));
+  }
+  if (direct_applicable(t)) {
     CHECK(set_device(t.hs[0]));
     int32_t conv = 0;
-    CHECK(solve_direct(t.hs[0], rtol, iters, relres, &conv));
+    CHECK(solve_direct(t, rtol, iters, relres, &conv));
     if (conv) {
-      t.hs[0]->last_solver = 1;
+      for (int r = 0; r < t.P; ++r) t.hs[r]->last_solver = 1;
       if (converged) *converged = 1;
       return NX_OK;
     }
-    // residual above rtol (e.g. rounding on an ill-conditioned tree): MINRES from scratch
+    // residual above rtol after a refinement step: MINRES from scratch
   }
+  for (int r = 0; r < t.P; ++r) CHECK(flush_assembly(t.hs[r]));  // MINRES: no deferred work
   if (check_every & 1) ++check_every;
   CHECK(set_device(t.hs[0]));
   const bool multi = team_multi(t);
@@ -4388,6 +4753,7 @@ NX_API int nx_solve(nx_network_t* h, double rtol, int32_t maxit, int32_t check_e
 }
 
 NX_API int nx_get_solution(nx_network_t* h, double* xo) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !xo) return fail(NX_ERR_ARG, "null argument");
   CHECK(set_device(h));
   HIPCALL(hipMemcpyAsync(xo, h->x, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
@@ -4396,6 +4762,7 @@ NX_API int nx_get_solution(nx_network_t* h, double* xo) {
 }
 
 NX_API int nx_set_output_map(nx_network_t* h, int64_t n, const int32_t* rows) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || (n > 0 && !rows)) return fail(NX_ERR_ARG, "null argument");
   if (n != h->n_own) return fail(NX_ERR_ARG, "the output map must list every owned row once");
   std::vector<char> seen((size_t)n, 0);
@@ -4418,6 +4785,7 @@ NX_API int nx_set_output_map(nx_network_t* h, int64_t n, const int32_t* rows) {
 }
 
 NX_API int nx_get_solution_blocks(nx_network_t* h, double* out) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !out) return fail(NX_ERR_ARG, "null argument");
   if (!h->out_idx && h->n_own > 0) return fail(NX_ERR_STATE, "nx_set_output_map first");
   CHECK(set_device(h));
@@ -4447,6 +4815,7 @@ NX_API int nx_host_free(void* p) {
 }
 
 NX_API int nx_get_vector(nx_network_t* h, int32_t which, double* out) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !out) return fail(NX_ERR_ARG, "null argument");
   CHECK(set_device(h));
   const double* src = which == 0 ? h->x : which == 1 ? h->rhs : which == 2 ? h->z : nullptr;
@@ -4457,6 +4826,7 @@ NX_API int nx_get_vector(nx_network_t* h, int32_t which, double* out) {
 }
 
 NX_API int nx_get_rhs(nx_network_t* h, double* b) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !b) return fail(NX_ERR_ARG, "null argument");
   CHECK(set_device(h));
   HIPCALL(hipMemcpyAsync(b, h->rhs, sizeof(double) * h->n_own, hipMemcpyDeviceToHost, h->stream));
@@ -4465,6 +4835,7 @@ NX_API int nx_get_rhs(nx_network_t* h, double* b) {
 }
 
 NX_API int nx_get_csr(nx_network_t* h, int32_t* rowptr, int32_t* col, double* val) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   CHECK(set_device(h));
   if (rowptr)
@@ -4479,6 +4850,7 @@ NX_API int nx_get_csr(nx_network_t* h, int32_t* rowptr, int32_t* col, double* va
 }
 
 NX_API int nx_spmv_host(nx_network_t* h, const double* xh, double* yh) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !xh || !yh) return fail(NX_ERR_ARG, "null argument");
   if (!h->have_lhs) return fail(NX_ERR_STATE, "assemble the matrix first");
   CHECK(set_device(h));
@@ -4496,6 +4868,7 @@ NX_API int nx_spmv_host(nx_network_t* h, const double* xh, double* yh) {
 }
 
 NX_API int nx_true_residual(nx_network_t* h, double* relres) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !relres) return fail(NX_ERR_ARG, "null argument");
   if (!h->have_lhs || !h->have_rhs) return fail(NX_ERR_STATE, "assemble first");
   if (h->group) return fail(NX_ERR_STATE, "group member: compute the residual from the solutions");
@@ -4520,6 +4893,7 @@ NX_API int nx_true_residual(nx_network_t* h, double* relres) {
 }
 
 NX_API int nx_sync(nx_network_t* h) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
@@ -4527,6 +4901,7 @@ NX_API int nx_sync(nx_network_t* h) {
 }
 
 NX_API int nx_set_profiling(nx_network_t* h, int32_t enable) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   h->prof = enable != 0;
   return NX_OK;
@@ -4542,14 +4917,24 @@ NX_API int nx_get_profile(nx_network_t* h, double* spmv_ms, int64_t* spmv_count,
   return NX_OK;
 }
 
+NX_API int nx_get_profile_direct(nx_network_t* h, double* ms4, int64_t* count) {
+  if (!h || !ms4) return fail(NX_ERR_ARG, "null argument");
+  for (int k = 0; k < 4; ++k) ms4[k] = h->dir_ms[k];
+  if (count) *count = h->dir_cnt;
+  return NX_OK;
+}
+
 NX_API int nx_reset_profile(nx_network_t* h) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
   h->spmv_ms = h->asm_ms = 0.0;
   h->spmv_cnt = h->asm_cnt = 0;
+  for (double& v : h->dir_ms) v = 0.0;
+  h->dir_cnt = 0;
   return NX_OK;
 }
 
 NX_API int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !ms_per_spmv || reps < 1) return fail(NX_ERR_ARG, "bad argument");
   if (!h->have_lhs) return fail(NX_ERR_STATE, "assemble the matrix first");
   CHECK(set_device(h));
@@ -4581,6 +4966,7 @@ NX_API int nx_get_graph_mode(nx_network_t* h, int32_t* graph) {
 
 NX_API int nx_bench_spmv_cold(nx_network_t* h, int32_t reps, int32_t* copies_out,
                               double* ms_per_spmv) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !ms_per_spmv || reps < 1) return fail(NX_ERR_ARG, "bad argument");
   if (!h->have_lhs) return fail(NX_ERR_STATE, "assemble the matrix first");
   CHECK(set_device(h));
@@ -4653,6 +5039,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
                                  const int32_t* job_chain_off, const int32_t* job_lvl_off,
                                  int32_t n_lvl, const int32_t* lvl_slot_off, int32_t n_top_lvl,
                                  const int32_t* top_lvl_off) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   h->sched_checked = false;
   CHECK(set_device(h));
@@ -4829,6 +5216,7 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
                            const int32_t* top_uoff, const int32_t* slot_uy,
                            const int32_t* chain_uit, const int32_t* chain_uib,
                            const int32_t* job_root_u, const int32_t* job_root_dc) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
   h->sched_checked = false;
@@ -4919,6 +5307,7 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
 }
 
 NX_API int nx_set_pc_exact(nx_network_t* h, int32_t enable) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
   CHECK(set_device(h));
@@ -4929,12 +5318,14 @@ NX_API int nx_set_pc_exact(nx_network_t* h, int32_t enable) {
 }
 
 NX_API int nx_set_solver(nx_network_t* h, int32_t solver, int32_t tree_exact) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (solver != 0 && solver != 1) return fail(NX_ERR_ARG, "solver: 0 = MINRES, 1 = direct");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
   h->solver = solver;
   h->tree_exact = tree_exact != 0;
+  h->sched_checked = false;  // the solver choice is part of the ranks' schedule signature
   return NX_OK;
 }
 
@@ -4961,6 +5352,7 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
                          const int32_t* cc_bot, const int32_t* c_parent,
                          const int32_t* c_child_off, const int32_t* c_child, int32_t n_clvl,
                          const int32_t* c_lvl_off) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
   if (n_coarse < 0 || n_cc < 0 || n_clvl < 0) return fail(NX_ERR_ARG, "negative sizes");
@@ -5077,6 +5469,7 @@ NX_API int nx_comm_unique_id(unsigned char* id_out) {
 NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_peers,
                        const int32_t* peer_rank, const int32_t* send_off,
                        const int32_t* send_idx, const int32_t* recv_off) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h) return fail(NX_ERR_ARG, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(NX_ERR_ARG, "bad rank/nranks");
   if (nranks > 1 && h->pc) return fail(NX_ERR_STATE, "set the halo plan before the preconditioner");
@@ -5136,6 +5529,7 @@ NX_API int nx_comm_count(nx_network_t* h, int32_t* nranks) {
 NX_API int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned char* id,
                         int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
                         const int32_t* send_idx, const int32_t* recv_off) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
   if (!h || !id) return fail(NX_ERR_ARG, "null argument");
   if (h->group) return fail(NX_ERR_STATE, "the handle belongs to a group");
   CHECK(nx_set_halo(h, nranks, rank, n_peers, peer_rank, send_off, send_idx, recv_off));
@@ -5153,6 +5547,7 @@ NX_API int nx_group_create(int32_t nranks, nx_network_t* const* handles, nx_grou
   for (int r = 0; r < nranks; ++r) {
     nx_network* h = handles[r];
     if (!h) return fail(NX_ERR_ARG, "null handle in group");
+    CHECK(flush_assembly(h));
     if (h->group || h->comm) return fail(NX_ERR_STATE, "handle already has a transport");
     if (h->device != handles[0]->device) return fail(NX_ERR_ARG, "group members share one device");
     if (nranks > 1 && (!h->have_plan || h->rank != r || h->nranks != nranks))

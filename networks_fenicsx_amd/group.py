@@ -59,8 +59,20 @@ class RankGroup:
         for a in self.assemblers:
             a.set_preconditioner(enable)
 
+    def set_direct(self, enable: bool) -> None:
+        """The direct tree solve over all ranks (``nx_set_solver`` on every handle; it runs
+        where every rank can run it exactly, else MINRES)."""
+        for a in self.assemblers:
+            a.set_direct(enable)
+
+    @property
+    def solver_used(self) -> str:
+        """What the last solve ran: ``"direct"`` or ``"minres"``."""
+        return "direct" if self.assemblers[0].handle.solver()[1] == 1 else "minres"
+
     def solve(self, rtol: float = 1e-12, maxit: int = 50000, check_every: int = 4):
-        """MINRES over all ranks; returns ``(iterations, relres, converged)``."""
+        """MINRES (or the direct solve, see :meth:`set_direct`) over all ranks; returns
+        ``(iterations, relres, converged)``."""
         if self._group is None:
             self._group = _lib.Group([a.handle for a in self.assemblers])
         it, rr, conv = self._group.solve(rtol, maxit, check_every)

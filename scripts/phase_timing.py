@@ -6,7 +6,10 @@ build.build(phase_timing=True)'``), solves the bench workload and prints, for th
 complete iteration, workgroup 0's phase stamps and every kernel's latest workgroup start
 and end (wall_clock64, 100 MHz), relative to k_mr_a's start.
 
-    python scripts/phase_timing.py [levels] [N]
+    python scripts/phase_timing.py [levels] [N] [direct]
+
+With ``direct`` the direct tree solve runs (its sweeps in mode 3; times relative to the up
+sweep's start).
 """
 
 from __future__ import annotations
@@ -43,14 +46,17 @@ def main() -> int:
     lib = _lib.lib()
     fn = lib.nx_debug_phases
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int32]
+    direct = len(sys.argv) > 3 and sys.argv[3] == "direct"
+    asm.set_direct(direct)
     _lib.set_lean(False)  # the general path: k_mr_a stamps of full iterations too
     for _ in range(3):
         it, rr, conv = h.solve(1e-12, 50000, 32)
     buf = (C.c_ulonglong * 128)()
     _lib.check(fn(buf, 128))
     g = list(buf)
-    t0 = g[0]
-    print(f"iterations {it}, converged {conv}; times in us relative to k_mr_a start (wg 0)")
+    t0 = g[16] if direct else g[0]
+    ref = "k_pc_up_lds" if direct else "k_mr_a"
+    print(f"iterations {it}, converged {conv}; times in us relative to {ref} start (wg 0)")
     for base, name in KERNELS.items():
         stamps = [g[base + i] for i in range(len(PHASES[base]))]
         rel = [(x - t0) / 100.0 if x else float("nan") for x in stamps]

@@ -4,6 +4,7 @@ edge-partitioned problem of ``bench.py --gpus 8`` through the in-process rank gr
 per-rank handles, halo plans, coarse step and kernels as the RCCL path; RCCL itself needs
 one GPU per rank).
 
+Both solvers: preconditioned MINRES and the direct tree solve (one GPU and 8 ranks).
 Size-independent checks (the oracle's direct solve does not fit a test at this size):
 closed-form nnz E(7N+1)+6B, exact symmetry of the assembled matrix, 3 MINRES iterations
 (exact Schur-complement preconditioner), and the analytic resistor-network answer to
@@ -62,6 +63,12 @@ def test_c4_single_gpu(c4):
         err = np.linalg.norm(x - xa) / np.linalg.norm(xa)
         assert err <= TOL, err
         assert h.true_residual() < 1e-9
+        # the direct tree solve (the reference's default preonly + lu) on the same system
+        asm.set_direct(True)
+        it_d, relres_d, conv_d = h.solve(1e-12, 50000, 4)
+        assert conv_d and it_d in (1, 2) and h.solver()[1] == 1, (it_d, relres_d)
+        xd = h.solution()
+        assert np.linalg.norm(xd - xa) / np.linalg.norm(xa) <= TOL
         rp, col, val = h.csr()
         A = sp.csr_matrix((val, col, rp), shape=(h.n_rows, h.n_rows))
         At = A.T.tocsr()
@@ -93,3 +100,11 @@ def test_c4_eight_rank_group(c4):
         den += float(xa[rows] @ xa[rows])
     assert np.all(seen == 1)  # the partition covers every DoF exactly once
     assert np.sqrt(num / den) <= TOL
+    # the direct tree solve across the 8 ranks (coarse all-reduce, halo of x)
+    grp.set_direct(True)
+    it, relres, conv = grp.solve(1e-12, 50000, 4)
+    assert conv and it in (1, 2) and grp.solver_used == "direct", (it, relres)
+    for r, (a, xl) in enumerate(zip(grp.assemblers, grp.solutions())):
+        rows = DM.global_rows(a.local_problem, E, m0.bifurcation_index)
+        err_r = np.linalg.norm(xl - xa[rows]) / np.linalg.norm(xa[rows])
+        assert err_r <= TOL, (r, err_r)

@@ -128,3 +128,29 @@ def test_direct_large_tree_analytic(levels, N):
     xa = O.resistor_network_solution(P, lambda x: x[1])[O.build_permutation(P)[0]]
     assert np.linalg.norm(x1 - xa) / np.linalg.norm(xa) <= SOL_TOL
     asm.close()
+
+
+def test_deferred_assembly_keeps_call_order():
+    """nx_assemble is deferred on one rank (it heads the direct solve's graph), but every
+    other call flushes it first: an assembly followed by new coefficients still holds the
+    old ones, exactly as if it had run at once."""
+    mesh, asm, P, A, b, pbc = _setup("depth6_N40")
+    h = asm.handle
+    asm.assemble()
+    asm.compute_forms(p_bc_ex=pbc, R=2.0)  # uploads R = 2 after the pending assembly ran
+    Ab, bb, _, _ = O.to_build_layout(P, A, b)
+    np.testing.assert_array_equal(h.csr()[2], Ab.data)
+    np.testing.assert_array_equal(h.rhs(), bb)
+    asm.assemble()
+    A2, b2 = O.assemble_reference(P, pbc, R=2.0)
+    Ab2, bb2, perm, _ = O.to_build_layout(P, A2, b2)
+    np.testing.assert_array_equal(h.csr()[2], Ab2.data)
+    asm.assemble()  # deferred into the solve's graph
+    asm.set_direct(True)
+    it, relres, conv = h.solve(1e-12, 100, 4)
+    assert conv and h.solver()[1] == 1
+    x_ref = O.solve_reference(A2, b2)[perm]
+    assert np.linalg.norm(h.solution() - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    asm.assemble(assemble_lhs=False)  # rhs only: flushed, then the plain direct graph
+    it, relres, conv = h.solve(1e-12, 100, 4)
+    assert conv and np.linalg.norm(h.solution() - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL

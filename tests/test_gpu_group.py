@@ -266,3 +266,39 @@ def test_group_rehearsal_four_ranks_depth16():
         assert np.linalg.norm(x - xa) / np.linalg.norm(xa) < 1e-10
     finally:
         grp.close()
+
+
+@pytest.mark.parametrize("case,P", [("depth6_N40", 2), ("depth6_N40", 4), ("depth6_N40", 8),
+                                    ("arterial5_N40", 3), ("tree6_2d_N70", 5),
+                                    ("linear_alt_N3", 3), ("Y_N4", 2), ("edge_info_N10", 2)])
+def test_group_direct_solve(case, P):
+    """The direct tree solve across ranks (mode kModeDirect of the multi-rank sweeps, coarse
+    all-reduce between the halves, halo of x, all-reduced true residual): the oracle's
+    direct solution to 1e-10; graphs with a cycle fall back to MINRES on every rank."""
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.assemble()
+        grp.set_direct(True)
+        it, relres, conv = grp.solve(1e-12, 50000, 4)
+        assert conv, (it, relres)
+        is_tree = mesh.num_edges == mesh.num_nodes - 1
+        assert grp.solver_used == ("direct" if is_tree else "minres")
+        if is_tree:
+            assert it in (1, 2) and relres <= 1e-12
+        x = np.zeros(Ab.shape[0])
+        for a, xl in zip(grp.assemblers, grp.solutions()):
+            x[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
+        err = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
+        assert err <= SOL_TOL, err
+        # again: the captured graphs are reused and the result does not move
+        grp.assemble()
+        grp.solve(1e-12, 50000, 4)
+        x2 = np.zeros(Ab.shape[0])
+        for a, xl in zip(grp.assemblers, grp.solutions()):
+            x2[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
+        np.testing.assert_array_equal(x2, x)
+    finally:
+        grp.close()
