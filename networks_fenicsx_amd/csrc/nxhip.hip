@@ -1821,6 +1821,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
     }
     __syncthreads();
   }
+  NX_PHASE(20);
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
     const int j = js0 + sl;
     const double J = sJ[sl];
