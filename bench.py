@@ -377,11 +377,11 @@ def run(args, world: int) -> int:
                                   "cells, x_q = M^-1 (b_q - K x_s))",
                  "k_pc_top_lds": "k_pc_top_lds<false> (junctions above the cut)",
                  "k_assemble_seg": "k_assemble_seg<16> (CSR values + rhs)"}
-        rocname = {"k_residual": "(anonymous namespace)::k_residual",
-                   "k_pc_up_lds": "void (anonymous namespace)::k_pc_up_lds<false, 8, 2>",
-                   "k_pc_down_lds": "void (anonymous namespace)::k_pc_down_lds<false, 8, 2>",
-                   "k_pc_top_lds": "void (anonymous namespace)::k_pc_top_lds<false>",
-                   "k_assemble_seg": "void (anonymous namespace)::k_assemble_seg<16>"}[dom]
+        # kernel names as scripts/summarize_profile.py writes them (short form)
+        rocname = {"k_residual": "k_residual", "k_pc_up_lds": "k_pc_up_lds<false, 8, 2>",
+                   "k_pc_down_lds": "k_pc_down_lds<false, 8, 2>",
+                   "k_pc_top_lds": "k_pc_top_lds<false>",
+                   "k_assemble_seg": "k_assemble_seg<16>"}[dom]
         traffic, tsrc, rocprof_ns = (pmc_traffic(rocname) if default_workload
                                      else (None, None, None))
         return {"bound": "hbm", "kernel": names.get(dom, dom),
@@ -440,7 +440,7 @@ def run(args, world: int) -> int:
     from oracle import nx_oracle as O
 
     true_rr = h.true_residual()
-    parity = {"true_relres": true_rr, "minres_relres": state["relres"], "converged": state["conv"]}
+    parity = {"true_relres": true_rr, "solver_relres": state["relres"], "converged": state["conv"]}
     src, dst = mesh.edges
     P = O.build_problem(mesh.node_coordinates, src, dst, mesh.N)
     xa = O.resistor_network_solution(P, lambda x: x[1])

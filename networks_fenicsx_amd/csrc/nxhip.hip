@@ -294,17 +294,19 @@ __global__ __launch_bounds__(kBlock) void k_assemble_seg(AsmArgs a) {
   // neighbours' tensors: cell cl - 1 (the lumped mass) and the last cell (q_N)
   const int sb = sub * S;
   const double mdL = __shfl(md, sb + max(cl - 1, 0), 64), moL = __shfl(mo, sb + max(cl - 1, 0), 64);
-  if (a.lhs) {
-    if (a.dq != nullptr && mine && cl <= N) {
-      double d;
-      if (cl < N) {
-        d = md + mo;
-        if (cl > 0) d = (moL + mdL) + d;
-      } else {
-        d = moL + mdL;  // q_N: the last cell only
-      }
-      a.dq[e * (int64_t)(N + 1) + cl] = d;
+  // lumped flux mass (the preconditioner's D block): with the values or on its own (the
+  // direct solve's graph writes rhs + dq first and the values on a second branch)
+  if (a.dq != nullptr && mine && cl <= N) {
+    double d;
+    if (cl < N) {
+      d = md + mo;
+      if (cl > 0) d = (moL + mdL) + d;
+    } else {
+      d = moL + mdL;  // q_N: the last cell only
     }
+    a.dq[e * (int64_t)(N + 1) + cl] = d;
+  }
+  if (a.lhs) {
     // the wave's contiguous CSR range [b_0, b_ne)
     int bnd[EPW + 1], sfl[EPW];
 #pragma unroll
@@ -416,26 +418,23 @@ __global__ __launch_bounds__(kBlock) void k_assemble(AsmArgs a) {
         }
         if (i < i1) a.val[seg + i] = v;
       }
-      // lumped (row-sum) flux mass of q_k, k in the chunk (and q_N in the last chunk):
-      // the preconditioner's D block
-      const double mdL = __shfl(md, max(lane - 1, 0), 64), moL = __shfl(mo, max(lane - 1, 0), 64);
-      const double mdLast = __shfl(md, nc - 1, 64), moLast = __shfl(mo, nc - 1, 64);
-      if (a.dq != nullptr) {
-        const int64_t qb = e * (int64_t)(N + 1);
-        if (lane < nc) {
-          const int k = c0 + lane;
-          double d = md + mo;
-          if (k > 0) d = (lane > 0 ? moL + mdL : mo_prev + md_prev) + d;
-          a.dq[qb + k] = d;
-        }
-        if (lane == 0 && c0 + nc == N) a.dq[qb + N] = moLast + mdLast;
-      }
-      md_prev = mdLast;
-      mo_prev = moLast;
-    } else {
-      md_prev = __shfl(md, nc - 1, 64);
-      mo_prev = __shfl(mo, nc - 1, 64);
     }
+    // lumped (row-sum) flux mass of q_k, k in the chunk (and q_N in the last chunk):
+    // the preconditioner's D block (with the values or on its own, see k_assemble_seg)
+    const double mdL = __shfl(md, max(lane - 1, 0), 64), moL = __shfl(mo, max(lane - 1, 0), 64);
+    const double mdLast = __shfl(md, nc - 1, 64), moLast = __shfl(mo, nc - 1, 64);
+    if (a.dq != nullptr) {
+      const int64_t qb = e * (int64_t)(N + 1);
+      if (lane < nc) {
+        const int k = c0 + lane;
+        double d = md + mo;
+        if (k > 0) d = (lane > 0 ? moL + mdL : mo_prev + md_prev) + d;
+        a.dq[qb + k] = d;
+      }
+      if (lane == 0 && c0 + nc == N) a.dq[qb + N] = moLast + mdLast;
+    }
+    md_prev = mdLast;
+    mo_prev = moLast;
   }
 }
 
@@ -3984,15 +3983,18 @@ NX_API int nx_set_source(nx_network_t* h, const double* edge_f) {
 
 namespace {
 
-// Launch the assembly kernel (values and / or rhs) on the handle's stream.
-int launch_assembly(nx_network* h, int lhs, int rhs) {
+// Launch the assembly kernel (values and / or rhs; the lumped mass dq with the values unless
+// dq says otherwise) on stream s (the handle's by default).
+int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s = nullptr) {
+  if (!s) s = h->stream;
+  if (dq < 0) dq = lhs;
   if (h->fe) {  // general degrees: one thread per nonzero / rhs row
     FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind, h->fe_tval,
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
              h->nnz, h->n_own, h->val, h->rhs, lhs, rhs};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
     hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
-                          dim3(kBlock), 0, h->stream, e0, e1, 0, a);
+                          dim3(kBlock), 0, s, e0, e1, 0, a);
     HIPCALL(hipGetLastError());
     return NX_OK;
   }
@@ -4004,15 +4006,15 @@ int launch_assembly(nx_network* h, int lhs, int rhs) {
   const int lb = grid_of(nlm, kBlock);
   if (eb + lb > 0) {
     AsmArgs a{EdgeArgs{h->edge_x, h->edge_lm, h->edge_seg, h->E, h->N},
-              h->edge_R, h->edge_bc, h->f, h->edge_f, h->val, h->rhs, lhs ? h->dq : nullptr, lhs, rhs,
+              h->edge_R, h->edge_bc, h->f, h->edge_f, h->val, h->rhs, dq ? h->dq : nullptr, lhs, rhs,
               eb, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges, h->rhs + h->n_edge_dofs};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
     if (epw == 4)
-      hipExtLaunchKernelGGL(k_assemble_seg<16>, dim3(eb + lb), dim3(kBlock), 0, h->stream, e0, e1, 0, a);
+      hipExtLaunchKernelGGL(k_assemble_seg<16>, dim3(eb + lb), dim3(kBlock), 0, s, e0, e1, 0, a);
     else if (epw == 2)
-      hipExtLaunchKernelGGL(k_assemble_seg<32>, dim3(eb + lb), dim3(kBlock), 0, h->stream, e0, e1, 0, a);
+      hipExtLaunchKernelGGL(k_assemble_seg<32>, dim3(eb + lb), dim3(kBlock), 0, s, e0, e1, 0, a);
     else
-      hipExtLaunchKernelGGL(k_assemble, dim3(eb + lb), dim3(kBlock), 0, h->stream, e0, e1, 0, a);
+      hipExtLaunchKernelGGL(k_assemble, dim3(eb + lb), dim3(kBlock), 0, s, e0, e1, 0, a);
   }
   HIPCALL(hipGetLastError());
   return NX_OK;
@@ -4356,6 +4358,9 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   const bool with_asm = !multi && h->pend_lhs && h->pend_rhs;  // deferred assembly heads it
   for (int r = 0; r < t.P; ++r)
     if (!with_asm) CHECK(flush_assembly(t.hs[r]));
+  // (measured and kept out: forking the CSR values' assembly onto a second graph branch
+  // beside the sweeps -- the cross-queue dependencies cost ~13 us at the fork and ~9 us at
+  // the join, more than the 17 us assembly they would hide; r02 trace)
   auto body = [&](int refine, bool asmb) -> int {
     if (multi) return launch_direct_team(t, rtol, refine);
     if (asmb) CHECK(launch_assembly(h, 1, 1));
