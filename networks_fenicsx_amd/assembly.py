@@ -200,6 +200,57 @@ class FormBlock:
         return f"FormBlock{idx}({self.kind})"
 
 
+def _block_kind(i: int, j: int, M: int) -> str | None:
+    """Which term of compute_forms block a[i][j] holds (None: the reference's None)."""
+    if i < M and j == i:
+        return "mass"
+    if i == M and j < M:
+        return "divergence"
+    if i < M and j == M:
+        return "gradient"
+    if (i == M + 1 and j < M) or (i < M and j == M + 1):
+        return "junction"
+    return None
+
+
+class _BilinearBlocks:
+    """The nested ``a[i][j]`` of the reference (``assembly.py:194-196, 284-293``) without
+    storing its (M + 2)^2 entries: with ``color_strategy=None`` M is the edge count, and a
+    list of lists would need O(E^2) memory (the reference's own structure)."""
+
+    def __init__(self, asm: "HydraulicNetworkAssembler", M: int):
+        self._asm, self._M = asm, M
+
+    def __len__(self) -> int:
+        return self._M + 2
+
+    def __getitem__(self, i: int) -> "_BilinearRow":
+        if not -len(self) <= i < len(self):
+            raise IndexError(i)
+        return _BilinearRow(self._asm, i % len(self), self._M)
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
+class _BilinearRow:
+    def __init__(self, asm, i: int, M: int):
+        self._asm, self._i, self._M = asm, i, M
+
+    def __len__(self) -> int:
+        return self._M + 2
+
+    def __getitem__(self, j: int):
+        if not -len(self) <= j < len(self):
+            raise IndexError(j)
+        j %= len(self)
+        kind = _block_kind(self._i, j, self._M)
+        return None if kind is None else FormBlock(self._asm, kind, self._i, j)
+
+    def __iter__(self):
+        return (self[j] for j in range(len(self)))
+
+
 class HydraulicNetworkAssembler:
     """Assembler for the mixed hydraulic network problem
 
@@ -397,15 +448,7 @@ class HydraulicNetworkAssembler:
         self._coefficients = {"R": R_const if R_edge is None else "per-edge",
                               "f": f_val if f_edge is None else "per-edge", "p_bc": pbc}
         M = len(self._flux_spaces)
-        n = M + 2
-        a: list[list[FormBlock | None]] = [[None] * n for _ in range(n)]
-        for c in range(M):
-            a[c][c] = FormBlock(self, "mass", c, c)
-            a[M][c] = FormBlock(self, "divergence", M, c)
-            a[c][M] = FormBlock(self, "gradient", c, M)
-            a[M + 1][c] = FormBlock(self, "junction", M + 1, c)
-            a[c][M + 1] = FormBlock(self, "junction", c, M + 1)
-        self._a = a
+        self._a = _BilinearBlocks(self, M)  # (M + 2)^2 blocks, materialised on access
         self._L = [FormBlock(self, "boundary", c) for c in range(M)]
         self._L += [FormBlock(self, "source", M), FormBlock(self, "zero", M + 1)]
 

@@ -42,10 +42,16 @@ class _Element:
         self.basix_element = _BasixElement(degree, family, discontinuous)
 
 
+class _IndexMap:
+    def __init__(self, n: int):
+        self.size_local = n
+        self.size_global = n
+        self.num_ghosts = 0
+
+
 class _DofMap:
     def __init__(self, n: int):
-        self.index_map = type("IndexMap", (), {"size_local": n, "size_global": n,
-                                               "num_ghosts": 0})()
+        self.index_map = _IndexMap(n)
         self.index_map_bs = 1
 
 

@@ -1,15 +1,15 @@
 #!/usr/bin/env python3
 """Rehearsal of the driver's multi-GPU bench workload on ONE GPU.
 
-``bench.py --gpus P`` weak-scales to ``make_tree(15 + log2 P)`` with N = 15 (P = 8: the
-depth-17 tree, 8.26 M DoF). RCCL refuses several ranks on one device, so this script runs
+``bench.py --gpus P`` weak-scales to ``make_tree(15 + log2 P)`` with N = 19 (P = 8: the
+depth-17 tree, SURVEY's C4, 10.35 M DoF). RCCL refuses several ranks on one device, so this script runs
 the same P per-rank handles -- same partition, halo plans, coarse step, kernels and MINRES
 schedule -- through the in-process group transport (``RankGroup``) and checks the gathered
 solution against the analytic resistor-network answer (oracle). Group solve
 times are printed for information only: the group transport serialises all ranks on one
 stream, so they are not multi-GPU timings.
 
-    python scripts/group_rehearsal.py [--ranks 8] [--levels 15] [--N 15]
+    python scripts/group_rehearsal.py [--ranks 8] [--levels 15] [--N 19] [--solver direct]
 """
 
 from __future__ import annotations
@@ -37,7 +37,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--levels", type=int, default=15, help="tree generations at one rank")
-    ap.add_argument("--N", type=int, default=15)
+    ap.add_argument("--N", type=int, default=19)
+    ap.add_argument("--solver", choices=("direct", "minres"), default="direct")
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     levels = args.levels + int(round(math.log2(args.ranks)))
@@ -48,6 +49,7 @@ def main() -> int:
           flush=True)
     try:
         grp.compute_forms(p_bc_ex=lambda x: x[1])
+        grp.set_direct(args.solver == "direct")
         grp.assemble()
         it, rr, conv = grp.solve(1e-12, 50000, 4)
         print(f"first solve: {it} iterations, relres {rr:.3e}, converged {conv}", flush=True)
@@ -71,7 +73,9 @@ def main() -> int:
         print(f"DoF {xa.size}, rows per rank {min(rows)}..{max(rows)}, "
               f"group assemble+solve median {1e3 * sorted(ts)[len(ts) // 2]:.2f} ms "
               f"(serialised ranks), rel. error vs analytic {err:.3e}", flush=True)
-        ok = conv and it == 3 and err < 1e-10 and not np.isnan(x).any()
+        print(f"solver {grp.solver_used}", flush=True)
+        want = (1, 2) if grp.solver_used == "direct" else (3,)
+        ok = conv and it in want and err < 1e-10 and not np.isnan(x).any()
         print("REHEARSAL OK" if ok else "REHEARSAL FAILED", flush=True)
         return 0 if ok else 1
     finally:
