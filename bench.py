@@ -128,14 +128,15 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(mesh, asm, dof: int, budget_s: float):
-    """The hot path on the host cores (rank 0, one GPU only), two legs:
+    """The hot path on the host cores (rank 0, one GPU only), three legs:
 
-    * ``port``: ``oracle/nx_cpu.c`` -- OpenMP assembly in the device layout + MINRES with the
-      same exact tree preconditioner, on all threads OpenMP is given (OMP_NUM_THREADS);
+    * ``port-direct`` / ``port``: ``oracle/nx_cpu.c`` -- OpenMP assembly in the device layout
+      + the direct tree solve (the GPU default's algorithm) / MINRES with the same exact tree
+      preconditioner, on all threads OpenMP is given (OMP_NUM_THREADS);
     * ``superlu``: the oracle's numpy assembly of the reference forms + SuperLU ``spsolve``
       (1 thread; the stand-in for the reference's MUMPS direct solve).
 
-    The headline ``value`` is the all-cores port; each leg runs about ``budget_s / 2``."""
+    The headline ``value`` is the all-cores direct port; each leg runs about ``budget_s / 3``."""
     from networks_fenicsx_amd.assembly import edge_boundary_rhs, evaluate_nodal
     from oracle import nx_cpu
     from oracle import nx_oracle as O
@@ -146,18 +147,19 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
     port = nx_cpu.CpuStep(lp, asm.tree_preconditioner, bc)
     port.assemble()
     port.solve()  # first touch of every buffer outside the timing
-    ms, runs, its = port.time_steps(budget_s / 2)
     threads = nx_cpu.threads()
-    legs.append({"leg": "port", "ms_per_step": ms, "value": dof / (ms / 1e3), "cores": threads,
-                 "minres_iterations": its,
-                 "sample": f"{runs} full steps of the same workload ({dof} DoF): OpenMP assembly "
-                           f"+ MINRES with the exact tree preconditioner (oracle/nx_cpu.c), "
-                           f"{threads} threads"})
+    for direct, leg, what in ((True, "port-direct", "the direct tree solve (as the GPU's default)"),
+                              (False, "port", "MINRES with the exact tree preconditioner")):
+        ms, runs, its = port.time_steps(budget_s / 3, direct=direct)
+        legs.append({"leg": leg, "ms_per_step": ms, "value": dof / (ms / 1e3), "cores": threads,
+                     "iterations": its,
+                     "sample": f"{runs} full steps of the same workload ({dof} DoF): OpenMP "
+                               f"assembly + {what} (oracle/nx_cpu.c), {threads} threads"})
     del port
     src, dst = mesh.edges
     P = O.build_problem(mesh.node_coordinates, src, dst, mesh.N, mesh.edge_colors)
     runs, t_total = 0, 0.0
-    while runs < 1 or (t_total < budget_s / 2 and runs < 40):
+    while runs < 1 or (t_total < budget_s / 3 and runs < 40):
         t0 = time.perf_counter()
         A, b = O.assemble_reference(P, lambda x: x[1])
         O.solve_reference(A, b)

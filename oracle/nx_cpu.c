@@ -317,6 +317,122 @@ static double pc_apply(const Pc* p, const double* r, double* z) {
   return part;
 }
 
+/* ---- direct tree solve (the GPU's kModeDirect sweeps, csrc/nxhip.hip): block LU of
+ * [[M, K], [K^T, 0]] -- y = M^{-1} b_q, x_s = S^{-1}(K^T y - b_s), x_q = M^{-1}(b_q - K x_s) ---- */
+static void chain_thomas(const Pc* p, const double* rhs, double* out) {  /* T^{-1} rhs */
+  const int N = p->N;
+  const double* l = p->lu;
+  const double* iu = p->lu + N + 1;
+  double yk = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    yk = rhs[k] - (k ? l[k] * yk : 0.0);
+    out[k] = yk;
+  }
+  double xk = 0.0;
+  for (int k = N; k >= 0; --k) {
+    xk = iu[k] * (out[k] - (k < N ? xk : 0.0));
+    out[k] = xk;
+  }
+}
+
+/* x = A^{-1} b (owned rows; x also receives the multipliers). mb: scratch of n doubles. */
+static void pc_direct(const Pc* p, const double* b, double* x, double* mb, int64_t n) {
+  const int N = p->N;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) mb[i] = -b[i];  /* multiplier rows: -b_lambda */
+#pragma omp parallel
+  {
+    double* rho = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+    double* t = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+    double* y = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+#pragma omp for schedule(static)
+    for (int64_t c = 0; c < p->n_chains; ++c) {  /* y, cell inputs w, condensation */
+      chain_rho(p, c, rho);
+      const double mo = rho[0] / 3.0;
+      const int flip = p->chain_flip[c];
+      for (int k = 0; k <= N; ++k) t[k] = b[q_dof(p, c, k)];
+      chain_thomas(p, t, y);
+      for (int k = 0; k <= N; ++k) y[k] /= mo;
+      double T = 0.0, acc = 0.0, sr = 0.0, srd = 0.0;
+      for (int k = 0; k <= N; ++k) T += rho[k];
+      for (int k = 0; k < N; ++k) {
+        acc += rho[k];
+        const double d = y[k] - y[k + 1];
+        const double w = (flip ? -d : d) - b[cell_dof(p, c, k)];
+        sr += w;
+        srd += w * acc;
+      }
+      const double ib = srd / T;
+      p->T[c] = T;
+      p->Ib[c] = ib + (flip ? -y[N] : y[N]);
+      p->It[c] = (sr - ib) + (flip ? y[0] : -y[0]);
+    }
+    free(rho);
+    free(t);
+    free(y);
+  }
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int jb = 0; jb < p->n_jobs; ++jb)
+    for (int lv = p->job_lvl_off[jb + 1] - 1; lv >= p->job_lvl_off[jb]; --lv)
+      for (int j = p->lvl_slot_off[lv]; j < p->lvl_slot_off[lv + 1]; ++j) eliminate(p, mb, j);
+  for (int lv = p->n_top_lvl - 1; lv >= 0; --lv)
+    for (int j = p->top_lvl_off[lv]; j < p->top_lvl_off[lv + 1]; ++j) eliminate(p, mb, j);
+  for (int lv = 0; lv < p->n_top_lvl; ++lv)
+    for (int j = p->top_lvl_off[lv]; j < p->top_lvl_off[lv + 1]; ++j) backsub(p, x, j);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int jb = 0; jb < p->n_jobs; ++jb)
+    for (int lv = p->job_lvl_off[jb]; lv < p->job_lvl_off[jb + 1]; ++lv)
+      for (int j = p->lvl_slot_off[lv]; j < p->lvl_slot_off[lv + 1]; ++j) backsub(p, x, j);
+#pragma omp parallel
+  {
+    double* rho = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+    double* Dk = (double*)malloc(sizeof(double) * (size_t)N);
+    double* w = (double*)malloc(sizeof(double) * (size_t)N);
+    double* zc = (double*)malloc(sizeof(double) * (size_t)N);
+    double* suf = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+    double* t = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+    double* y = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+#pragma omp for schedule(static)
+    for (int64_t c = 0; c < p->n_chains; ++c) {  /* cells, then x_q = M^{-1}(b_q - K x_s) */
+      chain_rho(p, c, rho);
+      const double mo = rho[0] / 3.0;
+      const int flip = p->chain_flip[c];
+      for (int k = 0; k <= N; ++k) t[k] = b[q_dof(p, c, k)];
+      chain_thomas(p, t, y);
+      for (int k = 0; k <= N; ++k) y[k] /= mo;
+      const double T = p->T[c], iT = 1.0 / T;
+      const double zt = p->chain_up[c] >= 0 ? p->z_slot[p->chain_up[c]] : 0.0;
+      const double zb = p->chain_lo[c] >= 0 ? p->z_slot[p->chain_lo[c]] : 0.0;
+      double acc = 0.0;
+      for (int k = 0; k < N; ++k) {
+        acc += rho[k];
+        Dk[k] = acc;
+        const double d = y[k] - y[k + 1];
+        w[k] = (flip ? -d : d) - b[cell_dof(p, c, k)];
+      }
+      suf[N] = 0.0;
+      for (int k = N - 1; k >= 0; --k) suf[k] = suf[k + 1] + (T - Dk[k]) * w[k];
+      double pre = 0.0;
+      for (int k = 0; k < N; ++k) {
+        double zk = zt * (T - Dk[k]) * iT + zb * Dk[k] * iT + Dk[k] * iT * suf[k] +
+                    (T - Dk[k]) * iT * pre - mo * w[k];
+        pre += Dk[k] * w[k];
+        zc[k] = zk;
+        x[cell_dof(p, c, k)] = zk;
+      }
+      for (int k = 0; k <= N; ++k) {  /* row q_k: +p_k - p_{k-1} - lambda_top + lambda_bottom */
+        double kz = (k < N ? zc[k] : 0.0) - (k > 0 ? zc[k - 1] : 0.0);
+        if (k == 0) kz -= zt;
+        if (k == N) kz += zb;
+        t[k] = b[q_dof(p, c, k)] - (flip ? -kz : kz);
+      }
+      chain_thomas(p, t, y);
+      for (int k = 0; k <= N; ++k) x[q_dof(p, c, k)] = y[k] / mo;
+    }
+    free(rho); free(Dk); free(w); free(zc); free(suf); free(t); free(y);
+  }
+}
+
 /* ---- CSR SpMV and vector kernels ---- */
 static void spmv(int64_t n, const int* rp, const int* col, const double* val, const double* x,
                  double* y) {
@@ -429,4 +545,67 @@ API int nxc_minres(int64_t n, const int* rp, const int* col, const double* val, 
   free(r1); free(r2); free(y); free(v); free(w1); free(w2);
   free(p.T); free(p.It); free(p.Ib); free(p.D); free(p.J); free(p.z_slot); free(p.lu);
   return itn;
+}
+
+/*
+ * The direct tree solve on the host (csrc/nxhip.hip kModeDirect, the GPU's default): one
+ * pass, the true residual ||b - A x|| / ||b||, one refinement step when it exceeds rtol.
+ * Returns the passes run (1 or 2); *relres = the final true residual.
+ */
+API int nxc_direct(int64_t n, const int* rp, const int* col, const double* val, const double* b,
+                   double rtol, int N, const double* dq, int64_t n_chains,
+                   const int* chain_edge, const int* chain_flip, const int* chain_up,
+                   const int* chain_lo, int64_t n_slots, const int* slot_lam,
+                   const int* slot_pchain, const int* slot_parent, const int* slot_dc_off,
+                   const int* slot_dc, int n_jobs, const int* job_chain_off,
+                   const int* job_lvl_off, const int* lvl_slot_off, int n_top_lvl,
+                   const int* top_lvl_off, double* x, double* relres) {
+  Pc p = {N, 1, n_chains, n_slots, n_jobs, n_top_lvl, chain_edge, chain_flip, chain_up,
+          chain_lo, slot_lam, slot_pchain, slot_parent, slot_dc_off, slot_dc, job_chain_off,
+          job_lvl_off, lvl_slot_off, top_lvl_off, dq, NULL, NULL, NULL, NULL, NULL, NULL, NULL};
+  const size_t nc = (size_t)(n_chains > 0 ? n_chains : 1), ns = (size_t)(n_slots > 0 ? n_slots : 1);
+  p.T = (double*)malloc(sizeof(double) * nc);
+  p.It = (double*)malloc(sizeof(double) * nc);
+  p.Ib = (double*)malloc(sizeof(double) * nc);
+  p.D = (double*)malloc(sizeof(double) * ns);
+  p.J = (double*)malloc(sizeof(double) * ns);
+  p.z_slot = (double*)malloc(sizeof(double) * ns);
+  p.lu = (double*)malloc(sizeof(double) * 2 * (size_t)(N + 1));
+  {
+    double u = 2.0;
+    p.lu[0] = 0.0;
+    p.lu[N + 1] = 1.0 / u;
+    for (int k = 1; k <= N; ++k) {
+      const double l = 1.0 / u;
+      u = (k == N ? 2.0 : 4.0) - l;
+      p.lu[k] = l;
+      p.lu[N + 1 + k] = 1.0 / u;
+    }
+  }
+  const size_t nb = sizeof(double) * (size_t)(n > 0 ? n : 1);
+  double *mb = malloc(nb), *r = malloc(nb), *d = malloc(nb);
+  int passes = 0;
+  for (;;) {
+    if (passes == 0) {
+      pc_direct(&p, b, x, mb, n);
+    } else {  /* refinement: x += A^{-1} (b - A x) */
+      pc_direct(&p, r, d, mb, n);
+#pragma omp parallel for schedule(static)
+      for (int64_t i = 0; i < n; ++i) x[i] += d[i];
+    }
+    ++passes;
+    spmv(n, rp, col, val, x, r);
+    double rr = 0.0, bb = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : rr, bb)
+    for (int64_t i = 0; i < n; ++i) {
+      r[i] = b[i] - r[i];
+      rr += r[i] * r[i];
+      bb += b[i] * b[i];
+    }
+    *relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
+    if (*relres <= rtol || passes == 2) break;
+  }
+  free(mb); free(r); free(d);
+  free(p.T); free(p.It); free(p.Ib); free(p.D); free(p.J); free(p.z_slot); free(p.lu);
+  return passes;
 }

@@ -3,7 +3,8 @@
 ctypes binding of ``oracle/libnxcpu.so`` (``oracle/nx_cpu.c``, built by ``oracle/Makefile``):
 an OpenMP restatement of one full step of the hot path on the host cores -- assembly of
 the reference's forms in the device layout (``assembly.py:243-277``, pressure rows negated)
-plus MINRES with the same exact tree Schur-complement preconditioner as the GPU. Only
+plus MINRES with the same exact tree Schur-complement preconditioner as the GPU, or the
+same direct tree solve as the GPU's default (``nxc_direct``). Only
 ``bench.py``'s ``cpu_baseline`` leg and ``tests/`` use it; the product path never does.
 """
 
@@ -35,6 +36,10 @@ def lib():
         L.nxc_assemble.restype = None
         L.nxc_assemble.argtypes = [C.c_int, C.c_int64, _pd, _pi, _pd, C.c_double, _pd, C.c_double,
                                    C.c_int64, _pi, _pi, _pd, C.c_int, _pi, _pi, _pd, _pd, _pd]
+        L.nxc_direct.restype = C.c_int
+        L.nxc_direct.argtypes = ([C.c_int64, _pi, _pi, _pd, _pd, C.c_double, C.c_int, _pd,
+                                  C.c_int64] + [_pi] * 4 + [C.c_int64] + [_pi] * 5
+                                 + [C.c_int] + [_pi] * 3 + [C.c_int, _pi, _pd, _pd])
         L.nxc_minres.restype = C.c_int
         L.nxc_minres.argtypes = ([C.c_int64, _pi, _pi, _pd, _pd, C.c_double, C.c_int, C.c_int, _pd,
                                   C.c_int, C.c_int64] + [_pi] * 4 + [C.c_int64] + [_pi] * 5
@@ -112,13 +117,32 @@ class CpuStep:
             _p(q["top_lvl_off"], C.c_int32), _p(self.x, C.c_double), C.byref(rr))
         return int(it), float(rr.value)
 
-    def time_steps(self, budget_s: float, rtol: float = 1e-12, max_runs: int = 200):
+    def solve_direct(self, rtol: float = 1e-12):
+        """The direct tree solve (``nxc_direct``): (passes, true relative residual)."""
+        q = self._pc
+        pc = self.pc
+        rr = C.c_double(0.0)
+        it = lib().nxc_direct(
+            self.n, _p(self.rowptr, C.c_int32), _p(self.col, C.c_int32), _p(self.val, C.c_double),
+            _p(self.rhs, C.c_double), float(rtol), self.N, _p(self.dq, C.c_double),
+            int(pc.n_chains), _p(q["chain_edge"], C.c_int32),
+            _p(q["chain_flip"], C.c_int32), _p(q["chain_up"], C.c_int32),
+            _p(q["chain_lo"], C.c_int32), int(pc.n_slots), _p(q["slot_lam"], C.c_int32),
+            _p(q["slot_pchain"], C.c_int32), _p(q["slot_parent"], C.c_int32),
+            _p(q["slot_dc_off"], C.c_int32), _p(q["slot_dc"], C.c_int32), int(pc.n_jobs),
+            _p(q["job_chain_off"], C.c_int32), _p(q["job_lvl_off"], C.c_int32),
+            _p(q["lvl_slot_off"], C.c_int32), int(q["top_lvl_off"].size - 1),
+            _p(q["top_lvl_off"], C.c_int32), _p(self.x, C.c_double), C.byref(rr))
+        return int(it), float(rr.value)
+
+    def time_steps(self, budget_s: float, rtol: float = 1e-12, max_runs: int = 200,
+                   direct: bool = False):
         """Repeat assemble + solve for about ``budget_s`` seconds; (ms per step, runs, its)."""
         runs, total, its = 0, 0.0, 0
         while runs < 1 or (total < budget_s and runs < max_runs):
             t0 = time.perf_counter()
             self.assemble()
-            its, _ = self.solve(rtol)
+            its, _ = self.solve_direct(rtol) if direct else self.solve(rtol)
             total += time.perf_counter() - t0
             runs += 1
         return 1e3 * total / runs, runs, its

@@ -59,3 +59,33 @@ def test_cpu_port_medium_tree_analytic():
     xa = O.resistor_network_solution(P, lambda x: x[1])[O.build_permutation(P)[0]]
     assert it == 3
     assert np.linalg.norm(st.x - xa) / np.linalg.norm(xa) < 1e-10
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "depth6_N40", "arterial5_N40", "tree5_N15",
+                                  "linear_alt_N3", "tree6_2d_N70", "demo_tree_N1"])
+def test_cpu_direct_matches_oracle(case):
+    """The host port of the GPU's direct tree solve (nxc_direct): the oracle's direct
+    solution to 1e-10, true residual <= 1e-12 after at most one refinement step."""
+    make, N, strategy, pbc = CASES[case]
+    m, lp, pc, st = _setup(make(), N, strategy, pbc)
+    assert pc.tree_exact
+    src, dst = m.edges
+    P = O.build_problem(m.node_coordinates, src, dst, N, m.edge_colors)
+    A, b = O.assemble_reference(P, pbc)
+    _, _, perm, _ = O.to_build_layout(P, A, b)
+    passes, rr = st.solve_direct(1e-12)
+    assert passes in (1, 2) and rr <= 1e-12, (passes, rr)
+    x_ref = O.solve_reference(A, b)[perm]
+    assert np.linalg.norm(st.x - x_ref) / np.linalg.norm(x_ref) <= 1e-10
+
+
+def test_cpu_direct_medium_tree_analytic():
+    G = ng.make_tree(12, 12, 12)
+    m, lp, pc, st = _setup(G, 15, "smallest_last", lambda x: x[1])
+    st.assemble()
+    passes, rr = st.solve_direct(1e-12)
+    src, dst = m.edges
+    P = O.build_problem(m.node_coordinates, src, dst, 15)
+    xa = O.resistor_network_solution(P, lambda x: x[1])[O.build_permutation(P)[0]]
+    assert passes in (1, 2) and rr <= 1e-12
+    assert np.linalg.norm(st.x - xa) / np.linalg.norm(xa) < 1e-10
