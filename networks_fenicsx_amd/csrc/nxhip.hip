@@ -4186,8 +4186,9 @@ int launch_head_multi(const Team& t, int L, double rtol, int maxit) {
 LeanGraphs& lean_of(const Team& t) { return t.g ? t.g->lean : t.hs[0]->lean; }
 
 // ---- direct tree solve (k_dir_*): y in vb[1], w in vb[0], S^{-1} w in z, x
-// refine = 0: x = A^{-1} b; refine = 1: one step of iterative refinement, r = b - A x
-// (into tmp), x += A^{-1} r. Both end with the true residual published.
+// refine = 0: x = A^{-1} b; refine = 1: one step of iterative refinement, x += A^{-1} r with
+// r = b - A x as the previous pass's residual check left it in tmp. Both end with the true
+// residual (r kept in tmp again) published.
 template <int W, int CPL>
 void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const hipEvent_t* evs = prof ? h->dev : nullptr;
@@ -4195,12 +4196,8 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const int cb = grid_of(h->E, G);
   double* yq = h->vb[1];
   double* w = h->vb[0];
-  const double* bin = h->rhs;
-  if (refine) {
-    hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                       h->rhs, h->partials, h->nblk, h->tmp);
-    bin = h->tmp;
-  }
+  // refine: the previous pass's residual check left r = b - A x in tmp
+  const double* bin = refine ? h->tmp : h->rhs;
   if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
     double* xo = refine ? w : h->x;  // refinement: the correction, then x += it
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, xo, evs);
@@ -4230,7 +4227,7 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   }  // unfused
   hipExtLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream,
                         prof ? h->dev[6] : nullptr, prof ? h->dev[7] : nullptr, 0, csr_of(h), h->x,
-                        h->rhs, h->partials, h->nblk, (double*)nullptr);
+                        h->rhs, h->partials, h->nblk, h->tmp);  // r kept for a refinement
   hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
                      h->nblk, rtol, h->d_seq, h->d_last);
 }
@@ -4280,12 +4277,9 @@ bool direct_applicable(const Team& t) {
 // and one all-reduce of the residual sums, published by every rank.
 int launch_direct_team(const Team& t, double rtol, int refine) {
   nx_network* h0 = t.hs[0];
-  if (refine) {  // r = b - A x (x's ghosts from the owners first); ghost slots of r are 0
-    CHECK(team_halo(t, VS_X, 0));
+  if (refine) {  // the previous pass's check left r = b - A x in tmp; its ghost slots 0
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
-      hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                         h->rhs, h->partials, h->nblk, h->tmp);
       if (h->n_col > h->n_own)
         HIPCALL(hipMemsetAsync(h->tmp + h->n_own, 0, sizeof(double) * (h->n_col - h->n_own),
                                h->stream));
@@ -4308,7 +4302,7 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
     hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                       h->rhs, h->partials, h->nblk, (double*)nullptr);
+                       h->rhs, h->partials, h->nblk, h->tmp);  // r kept for a refinement
     hipLaunchKernelGGL(k_dir_reduce2, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
                        h->nblk, h->red + 2);
   }
