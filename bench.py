@@ -79,13 +79,19 @@ def mr_spmv_bytes(n_rows: int, nnz: int, preconditioned: bool, iterations: int =
     return spmv + 8 * n_rows * passes / its
 
 
+def res_chunks(n: int) -> int:
+    """256-row chunks per k_residual_ck block: csrc/nxhip.hip res_chunks()."""
+    env = int(os.environ.get("NXHIP_RES_CHUNKS", "0") or 0)
+    return max(1, env) if env > 0 else (4 if n > (4 << 20) else 2)
+
+
 def direct_kernel_bytes(n: int, nnz: int, n_e: int, E: int, N: int, B: int, nblk: int) -> dict:
     """Algorithmic bytes per launch of the direct solve's kernels:
     f64 vectors, int32 indices, the lumped mass dq (E (N+1)) read by every chain sweep."""
     dq = 8 * E * (N + 1)
     return {
-        # CSR SpMV of x, b read, r not stored; two partials per block
-        "k_residual": 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n + 16 * nblk,
+        # CSR SpMV of x, b read, r stored (for a refinement step); two partials per block
+        "k_residual_ck": 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n + 8 * n + 16 * nblk,
         # b at the edge DoFs + dq, chain T / It / Ib written, junction slots (b, D, J, A, B
         # and their static indices: ~64 B each), chain statics (edge, flip: 8 B)
         "k_pc_up_lds": 8 * n_e + dq + 24 * E + 8 * E + 64 * B,
@@ -358,9 +364,9 @@ def run(args, world: int) -> int:
         cnt = max(pd["count"], 1)
         n, nnz = h.n_rows, h.nnz
         n_e = E * (2 * N + 1)
-        nblk = (n + 255) // 256
+        nblk = -(-n // (256 * res_chunks(n)))  # k_residual_ck blocks (partials)
         kb = direct_kernel_bytes(n, nnz, n_e, E, N, B, nblk)
-        ms = {"k_residual": pd["residual_ms"] / cnt, "k_pc_up_lds": pd["up_ms"] / cnt,
+        ms = {"k_residual_ck": pd["residual_ms"] / cnt, "k_pc_up_lds": pd["up_ms"] / cnt,
               "k_pc_top_lds": pd["top_ms"] / cnt, "k_pc_down_lds": pd["down_ms"] / cnt,
               "k_assemble_seg": prof["asm_ms"] / max(prof["asm_count"], 1)}
         kernels = {}
@@ -371,8 +377,8 @@ def run(args, world: int) -> int:
                               "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
         dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
         d = kernels[dom]
-        names = {"k_residual": "k_residual (CSR SpMV r = b - A x: the direct solve's true-residual "
-                               "check)",
+        names = {"k_residual_ck": "k_residual_ck (CSR SpMV r = b - A x: the direct solve's "
+                                  "true-residual check)",
                  "k_pc_up_lds": "k_pc_up_lds<false, 8, 2> (direct mode: M^-1 b_q per chain, "
                                 "chain condensation, junction elimination)",
                  "k_pc_down_lds": "k_pc_down_lds<false, 8, 2> (direct mode: back-substitution, "
@@ -380,7 +386,7 @@ def run(args, world: int) -> int:
                  "k_pc_top_lds": "k_pc_top_lds<false> (junctions above the cut)",
                  "k_assemble_seg": "k_assemble_seg<16> (CSR values + rhs)"}
         # kernel names as scripts/summarize_profile.py writes them (short form)
-        rocname = {"k_residual": "k_residual", "k_pc_up_lds": "k_pc_up_lds<false, 8, 2>",
+        rocname = {"k_residual_ck": "k_residual_ck", "k_pc_up_lds": "k_pc_up_lds<false, 8, 2>",
                    "k_pc_down_lds": "k_pc_down_lds<false, 8, 2>",
                    "k_pc_top_lds": "k_pc_top_lds<false>",
                    "k_assemble_seg": "k_assemble_seg<16>"}[dom]

@@ -550,6 +550,41 @@ __global__ __launch_bounds__(kBlock) void k_residual(Csr A, const double* __rest
   block_sum_store(bb, partials + nblk + blockIdx.x);
 }
 
+// The direct solve's check: the same residual, `ck` 256-row chunks per block (fewer partials
+// for the publish step to sum). Swept on MI355X (r02g, profiles/r02g_sweep.log): C3 (1 M rows)
+// 1: 0.0883-0.0896, 2: 0.0855-0.0876, 4: 0.089 ms/step; C4 (10 M rows) 1: 1.136, 4: 1.105.
+// NXHIP_RES_CHUNKS overrides.
+int res_chunks(int64_t n) {
+  static const int c = [] {
+    const char* e = std::getenv("NXHIP_RES_CHUNKS");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  return c > 0 ? c : (n > (int64_t(4) << 20) ? 4 : 2);
+}
+__global__ __launch_bounds__(kBlock) void k_residual_ck(Csr A, const double* __restrict__ x,
+                                                        const double* __restrict__ b,
+                                                        double* __restrict__ partials, int nblk,
+                                                        double* __restrict__ rout, int ck) {
+  double rr = 0.0, bb = 0.0;
+  for (int c = 0; c < ck; ++c) {
+    const int64_t r0 = ((int64_t)blockIdx.x * ck + c) * kRowsPerBlock;
+    if (r0 >= A.n_rows) break;  // block-uniform
+    const int nr = (int)min<int64_t>(kRowsPerBlock, A.n_rows - r0);
+    const double s = spmv_row_sum(A, x, r0, nr);
+    if ((int)threadIdx.x < nr) {
+      const double bv = b[r0 + threadIdx.x];
+      const double rv = bv - s;
+      if (rout) rout[r0 + threadIdx.x] = rv;
+      rr += rv * rv;
+      bb += bv * bv;
+    }
+    __syncthreads();  // spmv_row_sum's LDS is reused by the next chunk
+  }
+  block_sum_store(rr, partials + blockIdx.x);
+  __syncthreads();
+  block_sum_store(bb, partials + nblk + blockIdx.x);
+}
+
 // ------------------------------------------------------------------------------------
 // MINRES: Paige & Saunders (1975) recurrences in the form of scipy.sparse.linalg.minres
 // (unpreconditioned, shift 0). One iteration k (1-based) = 2 launches on one GPU:
@@ -1012,6 +1047,8 @@ struct PcArgs {
   // halo and this rank's beta^2 (k_pack_beta's work)
   int fused;
   int fuse_pack;
+  // direct solve, refinement pass: the sweeps add their output to x instead of storing it
+  int accum;
   int* ticket;
   const int* send_idx;
   int n_send;
@@ -1999,7 +2036,10 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
       const double num = sJ[sl] + (p >= 0 ? sGp[sl] * sJ0[p] : 0.0);
       const double zj = dir ? num * sY[sl] : num / sD[sl];
       sJ0[sl] = zj;  // reuse: z of top slots
-      z[sLam[sl]] = zj;
+      if (dir && pa.accum)
+        z[sLam[sl]] += zj;
+      else
+        z[sLam[sl]] = zj;
       pa.slot_z[ts0 + sl] = zj;
       if (!dir) part += sY[sl] * zj;
     }
@@ -2282,7 +2322,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       yl -= c2 * r2[lam];
       y[lam] = yl;
     }
-    z[lam] = zl;
+    if (dir && pa.accum)
+      z[lam] += zl;
+    else
+      z[lam] = zl;
     part += yl * zl;
   }
   NX_PHASE(50);
@@ -2333,7 +2376,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
         rk -= c2 * r2[ch.dof_c[t]];
         y[ch.dof_c[t]] = rk;
       }
-      z[ch.dof_c[t]] = zk;
+      if (dir && pa.accum)
+        z[ch.dof_c[t]] += zk;
+      else
+        z[ch.dof_c[t]] = zk;
       part += rk * zk;
       // flux: P^{-1} r' = P^{-1} y - c2 P^{-1} r2 and z_old = P^{-1} r2, so the block is
       // applied to r' directly (z_q needs no separate linear-form correction)
@@ -2352,8 +2398,23 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
         y[ch.dof_qN] = rqN;
       }
     }
-    if (dir) direct_flux_rhs<W, CPL>(pa, ch, flip, zc, zt, zb, rq, rqN);
-    part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, z);
+    if (dir) {  // x_q = M^{-1} (b_q - K x_s)
+      direct_flux_rhs<W, CPL>(pa, ch, flip, zc, zt, zb, rq, rqN);
+      double xv[CPL + 1];
+      chain_mass_solve<W, CPL>(pa, ch, rq, rqN, xv);
+#pragma unroll
+      for (int t = 0; t <= CPL; ++t) {
+        const bool on = t < CPL ? ch.valid[t] : ch.has_last;
+        if (!on) continue;
+        const int64_t d = t < CPL ? ch.dof_q[t] : ch.dof_qN;
+        if (pa.accum)
+          z[d] += xv[t];
+        else
+          z[d] = xv[t];
+      }
+    } else {
+      part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, z);
+    }
   }
   NX_PHASE(51);
   if (!dir) block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
@@ -2729,7 +2790,10 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __
         yl -= c2 * r2[lam];
         y[lam] = yl;
       }
-      z[lam] = zj;
+      if (mode == kModeDirect && pa.accum)
+        z[lam] += zj;
+      else
+        z[lam] = zj;
       part += yl * zj;
     }
     __syncthreads();
@@ -2910,13 +2974,6 @@ __global__ void k_dir_publish_red(const double* __restrict__ rb, double rtol, in
   ini.seq = seq;
   ini.mirror = mirror;
   mr_publish(s, ini);
-}
-
-// x += d (the refinement step of the fused direct solve)
-__global__ __launch_bounds__(kBlock) void k_axpy1(int64_t n, const double* __restrict__ d,
-                                                  double* __restrict__ x) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[i] += d[i];
 }
 
 // ||b - A x|| / ||b|| from k_residual's partials (fixed order), published like a MINRES
@@ -4199,12 +4256,10 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   // refine: the previous pass's residual check left r = b - A x in tmp
   const double* bin = refine ? h->tmp : h->rhs;
   if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
-    double* xo = refine ? w : h->x;  // refinement: the correction, then x += it
-    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, xo, evs);
-    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, xo, evs);
-    if (refine)
-      hipLaunchKernelGGL(k_axpy1, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
-                         h->n_own, (const double*)w, h->x);
+    h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
+    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, h->x, evs);
+    launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, h->x, evs);
+    h->pa.accum = 0;
   } else {
   const int64_t n_lm = h->n_own - h->n_edge_dofs;
   if (cb > 0)
@@ -4225,11 +4280,12 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
                          h->pa, (int)h->E, cb, h->edge_lm, h->n_edge_dofs, h->n_own, bin, h->z, h->x);
   }
   }  // unfused
-  hipExtLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream,
+  const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
+  hipExtLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream,
                         prof ? h->dev[6] : nullptr, prof ? h->dev[7] : nullptr, 0, csr_of(h), h->x,
-                        h->rhs, h->partials, h->nblk, h->tmp);  // r kept for a refinement
+                        h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));  // r kept: refinement
   hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                     h->nblk, rtol, h->d_seq, h->d_last);
+                     nrb, rtol, h->d_seq, h->d_last);
 }
 
 int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
@@ -4289,22 +4345,20 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
       double* bin = refine ? h->tmp : h->rhs;
-      launch_pc<true>(h, bin, bin, h->st, h->st + 1, kModeDirect, half, refine ? h->vb[0] : h->x);
+      h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
+      launch_pc<true>(h, bin, bin, h->st, h->st + 1, kModeDirect, half, h->x);
+      h->pa.accum = 0;
     }
     if (half == 0) CHECK(team_allreduce(t, -1, 3 * h0->pa.n_coarse));
-  }
-  for (int r = 0; r < t.P && refine; ++r) {
-    nx_network* h = t.hs[r];
-    hipLaunchKernelGGL(k_axpy1, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
-                       h->n_own, (const double*)h->vb[0], h->x);
   }
   CHECK(team_halo(t, VS_X, 0));
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
-    hipLaunchKernelGGL(k_residual, dim3(h->nblk), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                       h->rhs, h->partials, h->nblk, h->tmp);  // r kept for a refinement
+    const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
+    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));  // r kept: refinement
     hipLaunchKernelGGL(k_dir_reduce2, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                       h->nblk, h->red + 2);
+                       nrb, h->red + 2);
   }
   CHECK(team_allreduce(t, 2, 2));
   for (int r = 0; r < t.P; ++r) {

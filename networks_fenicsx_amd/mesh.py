@@ -33,6 +33,7 @@ import networkx as nx
 import numpy as np
 import numpy.typing as npt
 
+from .coloring import fast_edge_coloring, fast_path_available
 from .comm import Comm, SerialComm, as_comm
 from .timing import timed
 
@@ -47,13 +48,18 @@ def color_graph(
     """Greedy colouring of the line graph (reference ``mesh.py:29-42``).
 
     ``strategy=None`` gives every edge its own colour (edge index in
-    ``graph.edges()`` order). Otherwise the same networkx call as the reference
-    is made. The line graph of an undirected graph names each edge by its end
+    ``graph.edges()`` order). Otherwise the colouring of the reference's networkx call,
+    computed by :mod:`.coloring` for ``largest_first`` / ``smallest_last`` (the same
+    operations without networkx's graph classes) and by networkx itself otherwise. The line graph of an undirected graph names each edge by its end
     nodes in node order; both spellings of an edge are accepted here.
     """
     if strategy is None:
         return {edge: i for i, edge in enumerate(graph.edges)}
-    colouring = nx.coloring.greedy_color(nx.line_graph(graph.to_undirected()), strategy=strategy)
+    if fast_path_available(graph, strategy):  # same result, ~4x faster (coloring.py)
+        colouring = fast_edge_coloring(graph, strategy)
+    else:
+        colouring = nx.coloring.greedy_color(nx.line_graph(graph.to_undirected()),
+                                             strategy=strategy)
     out: dict[tuple[int, int], int] = {}
     for u, v in graph.edges:
         c = colouring.get((u, v))

@@ -54,9 +54,10 @@ def test_default_workloads():
 def test_direct_kernel_bytes_c3():
     """The residual SpMV of the direct solve reads the CSR, x and b once (SURVEY 8(d) + b)."""
     n, nnz, E, N, B = 1_032_160, 3_571_600, 32_767, 15, 16_383
-    kb = bench.direct_kernel_bytes(n, nnz, E * (2 * N + 1), E, N, B, (n + 255) // 256)
-    assert kb["k_residual"] == bench.spmv_bytes(n, nnz) + 16 * ((n + 255) // 256)
-    assert set(kb) == {"k_residual", "k_pc_up_lds", "k_pc_down_lds", "k_pc_top_lds",
+    nblk = (n + 255) // 256
+    kb = bench.direct_kernel_bytes(n, nnz, E * (2 * N + 1), E, N, B, nblk)
+    assert kb["k_residual_ck"] == bench.spmv_bytes(n, nnz) + 8 * n + 16 * nblk  # + r stored
+    assert set(kb) == {"k_residual_ck", "k_pc_up_lds", "k_pc_down_lds", "k_pc_top_lds",
                        "k_assemble_seg"}
     assert 13e6 < kb["k_pc_up_lds"] < 16e6 and 20e6 < kb["k_pc_down_lds"] < 23e6
 
