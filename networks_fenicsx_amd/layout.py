@@ -190,11 +190,6 @@ def build_local_problem(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degre
     n_own = v.n_edge_dofs + v.lm_nodes.size
     ghost_col = {k: n_own + i for i, k in enumerate(gkeys)}
 
-    def lm_col_of(b: int) -> int:
-        if lm_owner[b] == rank:
-            return int(lm_local[b])
-        return ghost_col[("lm", int(b))]
-
     # edge arrays
     Er = v.edges.size
     edge_x = np.empty((Er, 6), dtype=np.float64)
@@ -206,11 +201,14 @@ def build_local_problem(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degre
         edge_lm[:, 0] = np.where(is_bif[s_nodes], lm_local[s_nodes], -1)
         edge_lm[:, 1] = np.where(is_bif[d_nodes], lm_local[d_nodes], -1)
     else:
-        for j in range(Er):
-            if is_bif[s_nodes[j]]:
-                edge_lm[j, 0] = lm_col_of(int(s_nodes[j]))
-            if is_bif[d_nodes[j]]:
-                edge_lm[j, 1] = lm_col_of(int(d_nodes[j]))
+        # column of every multiplier this rank touches: owned, else its ghost column
+        col_of = np.where(lm_owner == rank, lm_local, -1)
+        for k, c in ghost_col.items():
+            if k[0] == "lm":
+                col_of[k[1]] = c
+        edge_lm[:, 0] = np.where(is_bif[s_nodes], col_of[s_nodes], -1)
+        edge_lm[:, 1] = np.where(is_bif[d_nodes], col_of[d_nodes], -1)
+        assert (edge_lm[is_bif[np.stack([s_nodes, d_nodes], axis=1)]] >= 0).all()
 
     # multiplier rows of this rank
     mine = lm_owner[inc_node] == rank
@@ -220,13 +218,9 @@ def build_local_problem(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degre
     if nranks == 1:
         cols = v.edge_local[e_inc] + np.where(end_inc == 1, 2 * N, 0)
     else:
-        cols = np.empty(n_inc.size, dtype=np.int64)
-        for j in range(n_inc.size):
-            e, end = int(e_inc[j]), int(end_inc[j])
-            if owner[e] == rank:
-                cols[j] = v.edge_local[e] + (2 * N if end else 0)
-            else:
-                cols[j] = ghost_col[key_edge_end(e, end)]
+        cols = v.edge_local[e_inc] + np.where(end_inc == 1, 2 * N, 0)
+        for j in np.flatnonzero(owner[e_inc] != rank).tolist():  # remote flux ends only
+            cols[j] = ghost_col[key_edge_end(int(e_inc[j]), int(end_inc[j]))]
     vals = np.where(end_inc == 1, 1.0, -1.0)
     row = lm_local[n_inc] - v.n_edge_dofs
     o = np.lexsort((cols, row))

@@ -128,21 +128,20 @@ def coarse_structure(src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
             alive = np.ones(er.size, dtype=bool)
             term = terminal[nodes]
             # prune non-terminal leaves: what stays is the Steiner forest of the terminals
-            stack = np.flatnonzero((deg == 1) & ~term).tolist()
-            while stack:
-                v = stack.pop()
-                if deg[v] != 1:
-                    continue
-                for i in range(off[v], off[v + 1]):
-                    e = inc_e[i]
-                    if alive[e]:
-                        break
+            # (the fixpoint does not depend on the order, so all current leaves go at once;
+            # only the far ends of the removed edges can become leaves next)
+            cand = np.flatnonzero((deg == 1) & ~term)
+            while cand.size:
+                leaf = np.unique(cand[(deg[cand] == 1) & ~term[cand]])
+                if not leaf.size:
+                    break
+                rep, pos = _ragged(off, leaf)
+                e = inc_e[pos]
+                e = np.unique(e[alive[e]])  # the one live edge of each leaf (shared: once)
                 alive[e] = False
-                deg[v] = 0
-                w = a[e] if b[e] == v else b[e]
-                deg[w] -= 1
-                if deg[w] == 1 and not term[w]:
-                    stack.append(w)
+                np.subtract.at(deg, a[e], 1)
+                np.subtract.at(deg, b[e], 1)
+                cand = np.concatenate([a[e], b[e]])
             keep = (deg > 0) & is_bif[nodes]
             coarse[nodes[keep]] = True
     cn = np.flatnonzero(coarse)
@@ -269,50 +268,69 @@ _CAP_CHAINS, _CAP_SLOTS, _CAP_DC = 512, 256, 768
 _CHAIN_MARGIN = 32
 
 
+def _ragged(off: np.ndarray, items: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenation of the CSR rows ``items`` (in order): (row position, entry index)."""
+    starts = off[items]
+    lens = off[items + 1] - starts
+    total = int(lens.sum())
+    if total == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    rep = np.repeat(np.arange(items.size), lens)
+    first = np.cumsum(lens) - lens
+    return rep, np.arange(total) - first[rep] + starts[rep]
+
+
+def _csr(keys: np.ndarray, n: int) -> tuple[np.ndarray, np.ndarray]:
+    """Stable grouping of positions by ``keys`` (0 <= key < n): (offsets, positions)."""
+    order = np.argsort(keys, kind="stable")
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(keys, minlength=n), out=off[1:])
+    return off, order
+
+
+def _bfs(frontier, adj_off, adj_e, adj_w, isj, depth, parent, pchain, tree_edge) -> None:
+    """Level-synchronous breadth-first search from the junctions ``frontier`` (depth already
+    set), through local edges to unvisited junctions. A node's parent is its first
+    discoverer in frontier order, adjacency order -- exactly what a FIFO queue gives, and
+    for several roots the same as one search per root as long as no unvisited junction is
+    reachable from two of them (true for the roots used here: see the caller)."""
+    F = np.asarray(frontier, dtype=np.int64)
+    while F.size:
+        rep, pos = _ragged(adj_off, F)
+        w = adj_w[pos]
+        m = isj[w] & (depth[w] < 0)
+        if not m.any():
+            break
+        w, e, u = w[m], adj_e[pos][m], F[rep][m]
+        _, first = np.unique(w, return_index=True)
+        first.sort()
+        w, e, u = w[first], e[first], u[first]
+        depth[w] = depth[u] + 1
+        parent[w] = u
+        pchain[w] = e
+        tree_edge[e] = True
+        F = w
+
+
 @dataclass
 class _JobRoots:
     roots: list
     promoted: list
 
 
-def _split_job_roots(roots, children, chain_up_node, chain_lo_node, is_cc, E: int,
-                     n_top: int, max_top: int, balance: int = 0) -> _JobRoots:
+def _split_job_roots(roots, kids, sizes, n_top: int, max_top: int,
+                     balance: int = 0) -> _JobRoots:
     """Replace every job root whose subtree exceeds the LDS caps by its children (the
     root joins the top part), recursively, keeping the roots' order; stops promoting
     when the top part would exceed ``max_top``. With ``balance`` > 0, first split the
-    root with the most chains while that keeps at most ``balance`` jobs."""
-    own_ch: dict[int, int] = {}
-    own_dc: dict[int, int] = {}
-    for e in range(E):
-        lo, up = int(chain_lo_node[e]), int(chain_up_node[e])
-        key = lo if lo != -1 else up
-        if key != -1:
-            own_ch[key] = own_ch.get(key, 0) + 1
-        if up != -1 and not is_cc[e]:
-            own_dc[up] = own_dc.get(up, 0) + 1
-    sizes: dict[int, tuple[int, int, int]] = {}
-
-    def size(v: int) -> tuple[int, int, int]:
-        if v not in sizes:  # iterative post-order (deep trees)
-            stack = [(v, False)]
-            while stack:
-                u, done = stack.pop()
-                if u in sizes:
-                    continue
-                if not done:
-                    stack.append((u, True))
-                    stack.extend((c, False) for c in children[u] if c not in sizes)
-                    continue
-                ch, sl, dc = own_ch.get(u, 0), 1, own_dc.get(u, 0)
-                for c in children[u]:
-                    a, b, d = sizes[c]
-                    ch, sl, dc = ch + a, sl + b, dc + d
-                sizes[u] = (ch, sl, dc)
-        return sizes[v]
+    root with the most chains while that keeps at most ``balance`` jobs. ``kids(v)`` lists
+    the children of junction ``v``; ``sizes`` = (chains, slots, down-chain entries) of
+    every junction's subtree (arrays over node ids)."""
+    s_ch, s_sl, s_dc = sizes
 
     def over(v: int) -> bool:
-        ch, sl, dc = size(v)
-        return ch > _CAP_CHAINS - _CHAIN_MARGIN or sl > _CAP_SLOTS or dc > _CAP_DC
+        return (s_ch[v] > _CAP_CHAINS - _CHAIN_MARGIN or s_sl[v] > _CAP_SLOTS
+                or s_dc[v] > _CAP_DC)
 
     promoted = []
     if balance > 0:
@@ -321,43 +339,44 @@ def _split_job_roots(roots, children, chain_up_node, chain_lo_node, is_cc, E: in
         # pieces far below the average job (small subtrees hanging from the coarse
         # junctions) join the top part whole: they would take a workgroup each and leave
         # too few jobs to split the largest subtrees (257-chain jobs at 8 ranks)
-        avg = sum(size(v)[0] for v in roots) / max(balance, 1)
+        avg = float(sum(int(s_ch[v]) for v in roots)) / max(balance, 1)
         keep = []
         for v in roots:
-            sub = [v]
-            k = 0
-            while k < len(sub):
-                sub.extend(children[sub[k]])
-                k += 1
-            if 2 * size(v)[0] < avg and n_top + len(promoted) + len(sub) <= max_top:
+            if 2 * int(s_ch[v]) < avg and n_top + len(promoted) + int(s_sl[v]) <= max_top:
+                sub = [v]  # level order of the subtree
+                k = 0
+                while k < len(sub):
+                    sub.extend(kids(sub[k]))
+                    k += 1
                 promoted.extend(sub)
             else:
                 keep.append(v)
         roots = keep
         order = {v: i for i, v in enumerate(roots)}
-        heap = [(-size(v)[0], order[v], v) for v in roots]
+        heap = [(-int(s_ch[v]), order[v], v) for v in roots]
         heapq.heapify(heap)
         live = set(roots)
         while heap and n_top + len(promoted) < max_top:
             negc, _, v = heap[0]
-            kids = children[v]
-            if not kids or len(live) - 1 + len(kids) > balance:
+            ks = kids(v)
+            if not ks or len(live) - 1 + len(ks) > balance:
                 break
             heapq.heappop(heap)
             live.discard(v)
             promoted.append(v)
-            for c in kids:
+            for c in ks:
                 order[c] = len(order)
                 live.add(c)
-                heapq.heappush(heap, (-size(c)[0], order[c], c))
+                heapq.heappush(heap, (-int(s_ch[c]), order[c], c))
         roots = sorted(live)  # slot_nodes order, as the depth cut's roots
     out = []
     todo = list(reversed(roots))
     while todo:
         r = todo.pop()
-        if children[r] and over(r) and n_top + len(promoted) < max_top:
+        ks = kids(r)
+        if ks and over(r) and n_top + len(promoted) < max_top:
             promoted.append(r)
-            todo.extend(reversed(children[r]))
+            todo.extend(reversed(ks))
         else:
             out.append(r)
     return _JobRoots(out, promoted)
@@ -370,103 +389,109 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
 
     ``src``/``dst`` are the global node ids of all edges, ``degree`` the global degrees.
     With several ranks the coarse forest is derived from ``lp.edge_owner`` unless given.
+    Array code throughout (arrays over global node ids); the only Python loops run over
+    job roots and the few junctions above the cut.
     """
     N = lp.N
     E = lp.edges.size
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    n_nodes = max(int(np.asarray(degree).size),
+                  int(max(src.max(initial=-1), dst.max(initial=-1))) + 1)
     es, ed = src[lp.edges], dst[lp.edges]
     if coarse is None and lp.nranks > 1:
         coarse = coarse_structure(src, dst, degree, lp.edge_owner, lp.nranks)
-    is_c = (lambda v: coarse.cidx[v] >= 0) if coarse is not None else (lambda v: False)  # noqa: E731
+    isc = np.zeros(n_nodes, dtype=bool)
+    if coarse is not None:
+        isc[: coarse.cidx.size] = coarse.cidx >= 0
     # junction slots: owned multipliers + ghost junctions at the ends of local edges (the
-    # latter are interface junctions, hence coarse)
-    lam_of = {int(v): lp.n_edge_dofs + i for i, v in enumerate(lp.lm_nodes)}
-    if lp.nranks > 1:
-        for j in range(E):
-            for end, v in ((0, int(es[j])), (1, int(ed[j]))):
-                col = int(lp.edge_lm[j, end])
-                if col >= lp.n_own and v not in lam_of:
-                    lam_of[v] = col
-    owned = lam_of
-    is_j = lambda v: v in owned  # noqa: E731
-    # junction adjacency through local edges
-    adj: dict[int, list[tuple[int, int]]] = {v: [] for v in owned}
-    for e in range(E):
-        a, b = int(es[e]), int(ed[e])
-        if is_j(a):
-            adj[a].append((e, b))
-        if is_j(b):
-            adj[b].append((e, a))
+    # latter are interface junctions, hence coarse); lam = local DoF of the multiplier
+    lam = np.full(n_nodes, -1, dtype=np.int64)
+    lm_nodes = np.asarray(lp.lm_nodes, dtype=np.int64)
+    lam[lm_nodes] = lp.n_edge_dofs + np.arange(lm_nodes.size)
+    if lp.nranks > 1 and E:
+        ends = np.stack([es, ed], axis=1).ravel()  # (edge, end) order
+        cols = np.asarray(lp.edge_lm, dtype=np.int64).ravel()
+        g = (cols >= lp.n_own) & (lam[ends] < 0)
+        gv, first = np.unique(ends[g], return_index=True)  # first occurrence wins
+        lam[gv] = cols[g][first]
+    isj = lam >= 0
+    slot_nodes = np.flatnonzero(isj)  # ascending node id
+    # junction adjacency through local edges: per junction, (edge, other end) by edge
+    e_ar = np.arange(E, dtype=np.int64)
+    ma, mb = isj[es], isj[ed]
+    a_u = np.concatenate([es[ma], ed[mb]])
+    a_e = np.concatenate([e_ar[ma], e_ar[mb]])
+    a_w = np.concatenate([ed[ma], es[mb]])
+    o = np.lexsort((a_e, a_u))
+    a_u, a_e, a_w = a_u[o], a_e[o], a_w[o]
+    adj_off = np.zeros(n_nodes + 1, dtype=np.int64)
+    np.cumsum(np.bincount(a_u, minlength=n_nodes), out=adj_off[1:])
 
     # spanning forest: coarse junctions are the roots (BFS never enters another coarse
-    # junction: a path between two would make its junctions coarse too); the rest from
-    # junctions touching ground first
-    depth = {}
-    parent_j = {}
-    pchain = {}
+    # junction: a path between two would make its junctions coarse too, so every other
+    # piece hangs from at most one coarse root and the roots' searches can run together);
+    # each remaining component from its first junction touching ground, else its first
+    depth = np.full(n_nodes, -1, dtype=np.int64)
+    parent_j = np.full(n_nodes, -1, dtype=np.int64)
+    pchain = np.full(n_nodes, -1, dtype=np.int64)
     tree_edge = np.zeros(E, dtype=bool)
-    slot_nodes = sorted(owned)
-    croots = [v for v in slot_nodes if is_c(v)]
-    for r in croots:
-        depth[r], parent_j[r], pchain[r] = 0, -1, -1
-    ground_touch = [v for v in slot_nodes if any(not is_j(w) for _, w in adj[v])]
-    grown = set()
-    for r in croots + ground_touch + slot_nodes:
-        r = int(r)
-        if r in grown or (r in depth and not is_c(r)):
-            continue
-        grown.add(r)
-        if r not in depth:
-            depth[r], parent_j[r], pchain[r] = 0, -1, -1
-        q = deque([r])
-        while q:
-            u = q.popleft()
-            for e, w in adj[u]:
-                if is_j(w) and w not in depth:
-                    depth[w] = depth[u] + 1
-                    parent_j[w] = u
-                    pchain[w] = e
-                    tree_edge[e] = True
-                    q.append(w)
+    croots = slot_nodes[isc[slot_nodes]]
+    depth[croots] = 0
+    _bfs(croots, adj_off, a_e, a_w, isj, depth, parent_j, pchain, tree_edge)
+    rest = slot_nodes[depth[slot_nodes] < 0]
+    if rest.size:
+        from scipy.sparse import coo_matrix
+        from scipy.sparse.csgraph import connected_components
+
+        jj = isj[es] & isj[ed]
+        A = coo_matrix((np.ones(int(jj.sum())), (es[jj], ed[jj])), shape=(n_nodes, n_nodes))
+        _, label = connected_components(A, directed=False)
+        touch = np.zeros(n_nodes, dtype=bool)
+        touch[a_u[~isj[a_w]]] = True
+        # first (lowest id) ground-touching junction of each component, else the lowest
+        key = np.where(touch[rest], 0, 1)
+        o = np.lexsort((rest, key, label[rest]))
+        lab = label[rest][o]
+        lead = np.ones(lab.size, dtype=bool)
+        lead[1:] = lab[1:] != lab[:-1]
+        roots2 = np.sort(rest[o][lead])
+        depth[roots2] = 0
+        _bfs(roots2, adj_off, a_e, a_w, isj, depth, parent_j, pchain, tree_edge)
 
     # chain ends: top = parent side (junction or ground), bottom = other
-    chain_up_node = np.full(E, -1, dtype=np.int64)
-    chain_lo_node = np.full(E, -1, dtype=np.int64)
+    up = np.full(E, -1, dtype=np.int64)
+    lo = np.full(E, -1, dtype=np.int64)
     is_cc = np.zeros(E, dtype=bool)  # joins two coarse junctions (coarse step)
-    flip = np.zeros(E, dtype=np.int8)
     n_cycle = 0  # chains grounded to break a cycle
-    for e in range(E):
-        a, b = int(es[e]), int(ed[e])
-        ja, jb = is_j(a), is_j(b)
-        ge = int(lp.edges[e])
-        if is_c(a) and is_c(b):
-            if coarse.demoted[ge]:  # closes a cycle of the coarse graph: ground one end
-                up, lo = a, -1
-                n_cycle += 1
-            else:  # coarse forest edge: top = parent end, bottom = child end
-                child = b if coarse.pedge[coarse.cidx[b]] == ge else a
-                up, lo = (a if child == b else b), child
-                is_cc[e] = True
-        elif tree_edge[e]:
-            # the child is the endpoint whose parent chain is e
-            if jb and pchain.get(b) == e:
-                up, lo = a, b
-            else:
-                up, lo = b, a
-        elif ja and jb:  # closes a cycle: hang from the shallower end, ground the other
-            up, lo = (a, -1) if depth[a] <= depth[b] else (b, -1)
-            n_cycle += 1
-        elif ja:
-            up, lo = a, -1
-        elif jb:
-            up, lo = b, -1
-        else:
-            up, lo = -1, -1
-        chain_up_node[e] = up
-        chain_lo_node[e] = lo
-        flip[e] = 1 if (up == b and up != -1) or (up == -1 and lo == a and lo != -1) else 0
+    ge = np.asarray(lp.edges, dtype=np.int64)
+    both_c = isc[es] & isc[ed] if coarse is not None else np.zeros(E, dtype=bool)
+    dem = both_c & coarse.demoted[ge] if coarse is not None else both_c
+    up[dem] = es[dem]  # closes a cycle of the coarse graph: ground one end
+    n_cycle += int(dem.sum())
+    fe = both_c & ~dem  # coarse forest edge: top = parent end, bottom = child end
+    if fe.any():
+        child_b = coarse.pedge[coarse.cidx[ed[fe]]] == ge[fe]
+        up[fe] = np.where(child_b, es[fe], ed[fe])
+        lo[fe] = np.where(child_b, ed[fe], es[fe])
+        is_cc[fe] = True
+    ja, jb = isj[es], isj[ed]
+    t = ~both_c & tree_edge  # the child is the endpoint whose parent chain is e
+    cb = jb & (pchain[ed] == e_ar)
+    up[t] = np.where(cb[t], es[t], ed[t])
+    lo[t] = np.where(cb[t], ed[t], es[t])
+    r = ~both_c & ~tree_edge
+    cyc = r & ja & jb  # closes a cycle: hang from the shallower end, ground the other
+    up[cyc] = np.where(depth[es[cyc]] <= depth[ed[cyc]], es[cyc], ed[cyc])
+    n_cycle += int(cyc.sum())
+    g1 = r & ja & ~jb
+    up[g1] = es[g1]
+    g2 = r & ~ja & jb
+    up[g2] = ed[g2]
+    flip = (((up == ed) & (up != -1)) | ((up == -1) & (lo == es) & (lo != -1))).astype(np.int8)
 
     # cut depth: lower subtrees rooted at depth L (coarse junctions, depth 0, stay on top)
-    dvals = np.array([depth[int(v)] for v in slot_nodes], dtype=np.int64)
+    dvals = depth[slot_nodes]
     maxd = int(dvals.max()) if dvals.size else -1
     counts = np.bincount(dvals, minlength=maxd + 1) if dvals.size else np.zeros(0, np.int64)
     L = maxd + 1  # default: everything in the top part
@@ -474,70 +499,102 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         if counts[cand] >= target_jobs or counts[:cand].sum() + counts[cand] > max_top:
             L = cand
             break
-    if croots:
+    if croots.size:
         L = max(L, 1)
 
-    children: dict[int, list[int]] = {v: [] for v in slot_nodes}
-    for v in slot_nodes:
-        p = parent_j[v]
-        if p != -1:
-            children[p].append(v)
+    # children of every junction (ascending node id) as CSR over node ids
+    has_p = slot_nodes[parent_j[slot_nodes] >= 0]
+    ch_off, o = _csr(parent_j[has_p], n_nodes)
+    ch = has_p[o]
+
+    def kids(v: int) -> list:
+        return ch[ch_off[v]:ch_off[v + 1]].tolist()
+
+    # subtree sizes (chains, slots, down-chain entries), deepest level first
+    key = np.where(lo != -1, lo, up)
+    s_ch = np.bincount(key[key != -1], minlength=n_nodes).astype(np.int64)
+    dcm = (up != -1) & ~is_cc
+    s_dc = np.bincount(up[dcm], minlength=n_nodes).astype(np.int64)
+    s_sl = isj.astype(np.int64)
+    by_d = slot_nodes[np.argsort(dvals, kind="stable")]
+    d_off = np.searchsorted(dvals[np.argsort(dvals, kind="stable")], np.arange(maxd + 2))
+    for dl in range(maxd, 0, -1):
+        vs = by_d[d_off[dl]:d_off[dl + 1]]
+        ps = parent_j[vs]
+        np.add.at(s_ch, ps, s_ch[vs])
+        np.add.at(s_sl, ps, s_sl[vs])
+        np.add.at(s_dc, ps, s_dc[vs])
 
     # A lower subtree must fit one workgroup of the LDS kernels (csrc/nxhip.hip kCapC /
     # kCapS / kCapDC); an uneven local forest (several ranks: pieces of different heights
     # hang from the coarse junctions) can put 4x the typical subtree below one depth-L
     # root. Such a root is promoted into the top part and its children become job roots.
-    if lp.nranks > 1 and croots and maxd >= 1:
+    if lp.nranks > 1 and croots.size and maxd >= 1:
         # several ranks: the local forest's pieces differ in height, so a fixed cut depth
         # gives uneven jobs; split the largest subtree first, from depth 1, until there are
         # target_jobs jobs (a uniform binary tree gives the depth cut's decomposition)
         L = 1
-        start = [v for v in slot_nodes if depth[v] == 1]
+        start = slot_nodes[dvals == 1].tolist()
         balance = target_jobs
     else:
-        start = [v for v in slot_nodes if depth[v] == L]
+        start = slot_nodes[dvals == L].tolist()
         balance = 0
-    job_roots = _split_job_roots(start, children, chain_up_node, chain_lo_node, is_cc, E,
-                                 n_top=int(counts[:L].sum()), max_top=max_top,
-                                 balance=balance)
-    promoted = set(job_roots.promoted)
-    job_roots = job_roots.roots
+    jr = _split_job_roots(start, kids, (s_ch, s_sl, s_dc), n_top=int(counts[:L].sum()),
+                          max_top=max_top, balance=balance)
+    promoted = np.zeros(n_nodes, dtype=bool)
+    promoted[np.asarray(jr.promoted, dtype=np.int64)] = True
+    job_roots = np.asarray(jr.roots, dtype=np.int64)
+    n_lower = job_roots.size
 
-    # slots: lower subtrees (level order inside), then top levels
-    slots: list[int] = []
-    job_lvl_off = [0]
-    lvl_slot_off = [0]
-    for r in job_roots:
-        level = [r]
-        while level:
-            slots.extend(level)
-            lvl_slot_off.append(len(slots))
-            level = [c for u in level for c in children[u]]
-        job_lvl_off.append(len(lvl_slot_off) - 1)
-    n_lower_slots = len(slots)
-    top_lvl_off = [n_lower_slots]
-    top_depth = max([L - 1] + [depth[v] for v in promoted])
-    for dlev in range(min(top_depth + 1, maxd + 1)):
-        slots.extend(v for v in slot_nodes if depth[v] == dlev and (dlev < L or v in promoted))
-        top_lvl_off.append(len(slots))
-    assert len(slots) == len(slot_nodes)
-    slot_of = {v: i for i, v in enumerate(slots)}
+    # slots: lower subtrees (level order inside), then top levels. All jobs' levels are
+    # expanded together; the frontier stays job-major, so a stable sort by (job, level)
+    # gives every job's level order
+    F, Jf, lv = job_roots, np.arange(n_lower, dtype=np.int64), 0
+    parts_v, parts_j, parts_l = [], [], []
+    while F.size:
+        parts_v.append(F)
+        parts_j.append(Jf)
+        parts_l.append(np.full(F.size, lv, dtype=np.int64))
+        rep, pos = _ragged(ch_off, F)
+        F, Jf, lv = ch[pos], Jf[rep], lv + 1
+    if parts_v:
+        v_all, j_all, l_all = (np.concatenate(x) for x in (parts_v, parts_j, parts_l))
+        o = np.lexsort((l_all, j_all))
+        lower, j_all, l_all = v_all[o], j_all[o], l_all[o]
+        brk = np.flatnonzero((j_all[1:] != j_all[:-1]) | (l_all[1:] != l_all[:-1])) + 1
+        lvl_slot_off = np.concatenate([[0], brk, [lower.size]])
+        lvl_job = j_all[lvl_slot_off[:-1]]
+        job_lvl_off = np.searchsorted(lvl_job, np.arange(n_lower + 1))
+    else:
+        lower = np.zeros(0, np.int64)
+        lvl_slot_off = np.zeros(1, np.int64)
+        job_lvl_off = np.zeros(1, np.int64)
+    n_lower_slots = lower.size
+    top_depth = max([L - 1] + depth[np.asarray(jr.promoted, dtype=np.int64)].tolist())
+    nlev = min(top_depth + 1, maxd + 1)
+    tm = (dvals < nlev) & ((dvals < L) | promoted[slot_nodes])
+    tn, td = slot_nodes[tm], dvals[tm]
+    o = np.argsort(td, kind="stable")
+    top = tn[o]
+    top_lvl_off = n_lower_slots + np.searchsorted(td[o], np.arange(nlev + 1))
+    slots = np.concatenate([lower, top])
+    assert slots.size == slot_nodes.size
+    slot_of = np.full(n_nodes, -1, dtype=np.int64)
+    slot_of[slots] = np.arange(slots.size)
 
     # chains: per lower job, the parent chains of its junctions + chains hanging from them
     # (grounded / cycle-closing); the rest (top part chains) go round-robin to the jobs
-    job_of_slot = np.full(len(slots), -1, dtype=np.int64)
-    for j in range(len(job_roots)):
-        a = lvl_slot_off[job_lvl_off[j]]
-        b = lvl_slot_off[job_lvl_off[j + 1]]
-        job_of_slot[a:b] = j
+    job_of_slot = np.full(slots.size, -1, dtype=np.int64)
+    if n_lower:
+        lv_len = np.diff(lvl_slot_off)
+        job_of_slot[:n_lower_slots] = np.repeat(lvl_job, lv_len)
     chain_job = np.full(E, -1, dtype=np.int64)
-    for e in range(E):
-        lo, up = chain_lo_node[e], chain_up_node[e]
-        if lo != -1 and job_of_slot[slot_of[lo]] >= 0:
-            chain_job[e] = job_of_slot[slot_of[lo]]
-        elif lo == -1 and up != -1 and job_of_slot[slot_of[up]] >= 0:
-            chain_job[e] = job_of_slot[slot_of[up]]
-    n_lower = len(job_roots)
+    jlo = np.where(lo != -1, job_of_slot[slot_of[np.maximum(lo, 0)]], -1)
+    jup = np.where(up != -1, job_of_slot[slot_of[np.maximum(up, 0)]], -1)
+    c1 = (lo != -1) & (jlo >= 0)
+    chain_job[c1] = jlo[c1]
+    c2 = (lo == -1) & (up != -1) & (jup >= 0)
+    chain_job[c2] = jup[c2]
     rest = np.flatnonzero(chain_job < 0)
     if n_lower > 0:
         # chains of the top part ride along with the lower jobs (round-robin): one
@@ -553,45 +610,40 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     order = np.lexsort((np.arange(E), chain_job))
     job_chain_off = np.searchsorted(chain_job[order], np.arange(n_jobs + 1)).astype(np.int32)
     # chain-only jobs have no levels
-    while len(job_lvl_off) < n_jobs + 1:
-        job_lvl_off.append(job_lvl_off[-1])
+    job_lvl_off = np.concatenate([job_lvl_off,
+                                  np.full(n_jobs + 1 - job_lvl_off.size, job_lvl_off[-1])])
 
     chain_index = np.empty(E, dtype=np.int64)
     chain_index[order] = np.arange(E)
-    to_slot = lambda v: slot_of[int(v)] if v != -1 else -1  # noqa: E731
-    c_up = np.array([to_slot(chain_up_node[e]) for e in order], dtype=np.int32)
-    c_lo = np.array([to_slot(chain_lo_node[e]) for e in order], dtype=np.int32)
+    c_up = np.where(up[order] != -1, slot_of[np.maximum(up[order], 0)], -1).astype(np.int32)
+    c_lo = np.where(lo[order] != -1, slot_of[np.maximum(lo[order], 0)], -1).astype(np.int32)
     cc = is_cc[order]
 
-    n_slots = len(slots)
-    slot_lam = np.array([lam_of[v] for v in slots], dtype=np.int32)
-    slot_pchain = np.array([chain_index[pchain[v]] if pchain[v] != -1 else -1 for v in slots],
-                           dtype=np.int32)
-    slot_parent = np.array([slot_of[parent_j[v]] if parent_j[v] != -1 else -1 for v in slots],
-                           dtype=np.int32)
-    down = [[] for _ in range(n_slots)]
-    for c in range(E):
-        if c_up[c] != -1 and not cc[c]:
-            down[c_up[c]].append(c)
-    slot_dc_off = np.zeros(n_slots + 1, dtype=np.int32)
-    np.cumsum([len(d) for d in down], out=slot_dc_off[1:])
-    slot_dc = np.array([c for d in down for c in d], dtype=np.int32)
+    n_slots = slots.size
+    slot_lam = lam[slots].astype(np.int32)
+    pcs = pchain[slots]
+    slot_pchain = np.where(pcs != -1, chain_index[np.maximum(pcs, 0)], -1).astype(np.int32)
+    pjs = parent_j[slots]
+    slot_parent = np.where(pjs != -1, slot_of[np.maximum(pjs, 0)], -1).astype(np.int32)
+    dm = np.flatnonzero((c_up != -1) & ~cc)
+    slot_dc_off, o = _csr(c_up[dm].astype(np.int64), n_slots)
+    slot_dc = dm[o].astype(np.int32)
     dc_lo = c_lo[slot_dc] if slot_dc.size else np.zeros(0, np.int32)
     slot_plam = np.where(slot_parent >= 0, slot_lam[np.maximum(slot_parent, 0)], -1).astype(np.int32)
     pc = TreePreconditioner(
         N=N, chain_edge=order.astype(np.int32), chain_flip=flip[order].astype(np.int32),
         chain_up=c_up, chain_lo=c_lo, slot_lam=slot_lam, slot_pchain=slot_pchain,
-        slot_parent=slot_parent, slot_dc_off=slot_dc_off, slot_dc=slot_dc,
+        slot_parent=slot_parent, slot_dc_off=slot_dc_off.astype(np.int32), slot_dc=slot_dc,
         dc_lo=dc_lo.astype(np.int32), slot_plam=slot_plam,
         job_chain_off=job_chain_off, job_lvl_off=np.asarray(job_lvl_off, dtype=np.int32),
         lvl_slot_off=np.asarray(lvl_slot_off, dtype=np.int32),
         top_lvl_off=np.asarray(top_lvl_off, dtype=np.int32), n_jobs=int(n_jobs),
-        n_slots=n_slots, tree_exact=n_cycle == 0)
+        n_slots=int(n_slots), tree_exact=n_cycle == 0)
     _dense_top_lists(pc)
     if coarse is not None and coarse.n > 0:
         cid = coarse.cidx
         pc.n_coarse = coarse.n
-        pc.slot_cidx = np.array([cid[v] for v in slots], dtype=np.int32)
+        pc.slot_cidx = cid[slots].astype(np.int32)
         ccs = np.flatnonzero(cc).astype(np.int32)
         pc.cc_chain = ccs
         pc.cc_top = pc.slot_cidx[c_up[ccs]] if ccs.size else _EMPTY_I
@@ -610,28 +662,23 @@ def _dense_top_lists(pc: TreePreconditioner) -> None:
     nj = pc.n_jobs
     if nj == 0 or ts1 == ts0:
         return
-    own: list[list[int]] = [[] for _ in range(nj)]
-    for i, t in enumerate(range(ts0, ts1)):
-        own[i % nj].append(t)
-    need: list[list[int]] = []
-    for j in range(nj):
-        ns = set(own[j])
-        for c in range(pc.job_chain_off[j], pc.job_chain_off[j + 1]):
-            for e in (pc.chain_up[c], pc.chain_lo[c]):
-                if e >= ts0:
-                    ns.add(int(e))
-        lv0, lv1 = pc.job_lvl_off[j], pc.job_lvl_off[j + 1]
-        for sl in range(pc.lvl_slot_off[lv0], pc.lvl_slot_off[lv1]) if lv1 > lv0 else []:
-            p = pc.slot_parent[sl]
-            if p >= ts0:
-                ns.add(int(p))
-        need.append(sorted(ns))
-    pc.job_tslot_off = np.zeros(nj + 1, dtype=np.int32)
-    np.cumsum([len(o) for o in own], out=pc.job_tslot_off[1:])
-    pc.job_tslot = np.array([t for o in own for t in o], dtype=np.int32)
-    pc.job_need_off = np.zeros(nj + 1, dtype=np.int32)
-    np.cumsum([len(n) for n in need], out=pc.job_need_off[1:])
-    pc.job_need = np.array([t for n in need for t in n], dtype=np.int32)
+    ts = np.arange(ts0, ts1, dtype=np.int64)
+    own_job = (ts - ts0) % nj  # round-robin
+    o = np.lexsort((ts, own_job))
+    pc.job_tslot = ts[o].astype(np.int32)
+    pc.job_tslot_off = np.searchsorted(own_job[o], np.arange(nj + 1)).astype(np.int32)
+    # needed top slots per job: its own, the top ends of its chains, its slots' parents
+    cj = np.repeat(np.arange(nj, dtype=np.int64), np.diff(pc.job_chain_off))
+    sl0 = pc.lvl_slot_off[pc.job_lvl_off[:-1]].astype(np.int64)
+    sl1 = pc.lvl_slot_off[pc.job_lvl_off[1:]].astype(np.int64)
+    sj = np.repeat(np.arange(nj, dtype=np.int64), np.where(sl1 > sl0, sl1 - sl0, 0))
+    sp = pc.slot_parent[:sj.size].astype(np.int64)  # lower slots come first, job-major
+    jj = np.concatenate([own_job, cj, cj, sj])
+    tt = np.concatenate([ts, pc.chain_up.astype(np.int64), pc.chain_lo.astype(np.int64), sp])
+    m = tt >= ts0
+    key = np.unique(jj[m] * (ts1 + 1) + tt[m])  # sorted by job, then slot
+    pc.job_need = (key % (ts1 + 1)).astype(np.int32)
+    pc.job_need_off = np.searchsorted(key // (ts1 + 1), np.arange(nj + 1)).astype(np.int32)
     # producer-side input layout: per top slot [y', I_bot(parent chain), one per dc entry]
     nt = ts1 - ts0
     cnt = np.zeros(nt, dtype=np.int64)

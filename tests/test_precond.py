@@ -215,18 +215,15 @@ def test_several_ranks_balanced_jobs(P):
 def test_split_job_roots_promotes_over_cap():
     from networks_fenicsx_amd.precond import _CAP_CHAINS, _split_job_roots
 
-    # root 0 with two children; 600 chains hang below child 1 -> root 0 is over the cap
+    # root 0 with two children; 600 chains hang below child 1 -> root 0 is over the cap.
+    # Subtree sizes (chains, slots, down-chain entries): chains whose bottom (else top)
+    # end is the junction, plus the children's
     children = {0: [1, 2], 1: [], 2: []}
-    E = 700
-    up = np.full(E, -1)
-    lo = np.full(E, -1)
-    lo[0], up[0] = 0, -1      # root's parent chain (to ground)
-    lo[1], up[1] = 1, 0
-    lo[2], up[2] = 2, 0
-    up[3:603] = 1             # hanging from 1
-    up[603:] = 2
-    cc = np.zeros(E, dtype=bool)
-    res = _split_job_roots([0], children, up, lo, cc, E, n_top=0, max_top=1024)
+    s_ch = np.array([1 + 601 + 98, 601, 98])
+    s_sl = np.array([3, 1, 1])
+    s_dc = np.array([2 + 600 + 97, 600, 97])
+    res = _split_job_roots([0], children.__getitem__, (s_ch, s_sl, s_dc), n_top=0,
+                           max_top=1024)
     assert res.promoted == [0] and res.roots == [1, 2]
     assert 601 > _CAP_CHAINS  # child 1 stays over the cap: a leaf junction cannot split
 
