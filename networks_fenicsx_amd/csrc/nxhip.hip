@@ -1528,36 +1528,54 @@ __device__ __forceinline__ void direct_cell_inputs(const PcArgs& pa, const Chain
   ybot = flip ? -yN : yN;
 }
 
-// Flux rows of the direct solve: rq = b_q - K x_s at the chain's fluxes (rq holds b_q on
-// entry), from the lane's cell values zc, the previous lane's last one and the end junction
-// values zt / zb. Row q_k of the layout: +p_k - p_{k-1} - lambda_src (k = 0) + lambda_dst
-// (k = N) in edge orientation; a flipped chain negates it (its position 0 is q_N).
+// Fluxes of one chain from its end and cell values, conservatively: x_q = M^{-1}(b_q - K x_s)
+// computed flux by flux takes differences of neighbouring pressures, whose rounding
+// (eps |p|) divided by the cell mass R h leaves the divergence rows a residual of
+// eps |p| / (R h) -- 1e-11 relative on the depth-17 tree. The exact solution satisfies the N
+// divergence rows exactly, so they fix every flux from the first one,
+//   x_q[k] = q_0 - s P_k,   P_k = sum_{j<k} b_c[j]   (s = -1 on a flipped chain),
+// and the d-weighted sum of the N + 1 flux rows (1^T M = d^T, d = lumped mass; 1^T K x_s
+// telescopes to s (z_bot - z_top)) fixes q_0:
+//   T q_0 = sum_k b_q[k] - s (z_bot - z_top) + s sum_k d_k P_k,   T = sum_k d_k.
+// Same solution in exact arithmetic; the divergence rows' residual is then exactly zero and
+// the flux / multiplier rows' stays at eps |p| (one pass: 2.9e-13 -> 3e-14 at C3).
+// bc / bq: the lane's b at its cells / fluxes (chain order), bqN at q_N (has_last lane).
 template <int W, int CPL>
-__device__ __forceinline__ void direct_flux_rhs(const PcArgs& pa, const ChainLane<W, CPL>& ch,
-                                                int flip, const double* zc, double zt, double zb,
-                                                double* rq, double& rqN) {
+__device__ __forceinline__ void direct_flux_cons(const ChainLane<W, CPL>& ch, int flip,
+                                                 const double* bc, const double* bq, double bqN,
+                                                 double zt, double zb, double (&out)[CPL + 1]) {
 #pragma clang fp contract(off)
-  const int N = pa.N;
   const int l = threadIdx.x & (W - 1);
-  double prev = __shfl_up(zc[CPL - 1], 1, W);  // cell k - 1 of element 0
-  if (l == 0) prev = 0.0;
+  double loc = 0.0;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t)
+    if (ch.valid[t]) loc += bc[t];
+  const double incl = seg_incl_scan<W>(loc);
+  double run = __shfl_up(incl, 1, W);  // cells before this lane's first
+  if (l == 0) run = 0.0;
+  double P[CPL + 1];
+  double s1 = 0.0, s2 = 0.0;
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
-    const int k = l * CPL + t;
-    const double bprev = t > 0 ? zc[t - 1] : prev;
-    double kz = zc[t] - bprev;  // zc = 0 past the last cell
-    if (k == 0) kz -= zt;
-    if (ch.valid[t]) rq[t] -= flip ? -kz : kz;
+    P[t] = run;
+    if (ch.valid[t]) {
+      s1 += bq[t];
+      s2 += ch.rho[t] * run;
+      run += bc[t];
+    }
   }
+  P[CPL] = run;  // q_N (the has_last lane holds cell N - 1): every cell
   if (ch.has_last) {
-    const int tl = (N - 1) - l * CPL;  // the lane's element of cell N - 1
-    double last = 0.0;
-#pragma unroll
-    for (int t = 0; t < CPL; ++t)
-      if (t == tl) last = zc[t];
-    const double kz = zb - last;  // k = N: -p_{N-1} + the bottom junction
-    rqN -= flip ? -kz : kz;
+    s1 += bqN;
+    s2 += ch.rhoN * run;
   }
+  s1 = seg_sum<W>(s1);
+  s2 = seg_sum<W>(s2);
+  const double sg = flip ? -1.0 : 1.0;
+  const double q0 = (s1 - sg * (zb - zt) + sg * s2) / ch.T;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) out[t] = ch.valid[t] ? q0 - sg * P[t] : 0.0;
+  out[CPL] = ch.has_last ? q0 - sg * P[CPL] : 0.0;
 }
 
 constexpr int kCapLvl = 64;  // job levels whose slot offsets are staged in LDS
@@ -2342,7 +2360,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     const double T = ch.T, iT = 1.0 / T;
     double rc[CPL], a[CPL], b[CPL], rq[CPL], zc[CPL];
     double sa = 0.0, sb = 0.0;
+    double bcv[CPL];  // direct: b at the cells (the conservative flux recovery reads it)
     if (dir) {
+#pragma unroll
+      for (int t = 0; t < CPL; ++t) bcv[t] = vc[t];
       double ytop, ybot;
       direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
     }
@@ -2398,10 +2419,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
         y[ch.dof_qN] = rqN;
       }
     }
-    if (dir) {  // x_q = M^{-1} (b_q - K x_s)
-      direct_flux_rhs<W, CPL>(pa, ch, flip, zc, zt, zb, rq, rqN);
+    if (dir) {  // x_q = M^{-1} (b_q - K x_s), conservatively (direct_flux_cons)
       double xv[CPL + 1];
-      chain_mass_solve<W, CPL>(pa, ch, rq, rqN, xv);
+      direct_flux_cons<W, CPL>(ch, flip, bcv, rq, rqN, zt, zb, xv);
 #pragma unroll
       for (int t = 0; t <= CPL; ++t) {
         const bool on = t < CPL ? ch.valid[t] : ch.has_last;
@@ -2880,9 +2900,8 @@ __global__ __launch_bounds__(kBlock) void k_dir_wl(Csr A, int64_t n_edge_dofs,
   w[i] = acc - b[i];
 }
 
-// x_q = M^{-1} (b_q - K z_s) per chain, x_s = z_s. Row q_k of the layout (k_pattern):
-// +1 at p_k (k < N), -1 at p_{k-1} (k > 0), -1 at the source multiplier (k = 0), +1 at the
-// target multiplier (k = N). Blocks past the chains copy the multiplier rows.
+// x_q = M^{-1} (b_q - K z_s) per chain (conservatively, direct_flux_cons), x_s = z_s.
+// Blocks past the chains copy the multiplier rows.
 template <int W, int CPL, bool ACC>
 __global__ __launch_bounds__(kBlock) void k_dir_post(PcArgs pa, int n_chains, int chain_blocks,
                                                      const int* __restrict__ edge_lm,
@@ -2901,29 +2920,20 @@ __global__ __launch_bounds__(kBlock) void k_dir_post(PcArgs pa, int n_chains, in
   const bool active = c < n_chains;
   ChainLane<W, CPL> ch;
   ch.setup(pa, active ? c : 0, active);
-  const int N = pa.N;
   const int e = active ? pa.chain_edge[c] : 0;
-  const int64_t base = (int64_t)e * (2 * N + 1);
   const int ls = active ? edge_lm[2 * e] : -1, lt = active ? edge_lm[2 * e + 1] : -1;
   const double zsrc = ls >= 0 ? z[ls] : 0.0, zdst = lt >= 0 ? z[lt] : 0.0;
-  auto rhs_q = [&](int64_t q) {
-    const int k = (int)((q - base) >> 1);
-    double kx = 0.0;
-    if (k < N) kx += z[q + 1];
-    if (k > 0) kx -= z[q - 1];
-    if (k == 0) kx -= zsrc;
-    if (k == N) kx += zdst;
-    return b[q] - kx;
-  };
-  double rq[CPL];
+  double bq[CPL], bc[CPL];
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
-    rq[t] = ch.valid[t] ? rhs_q(ch.dof_q[t]) : 0.0;
+    bq[t] = ch.valid[t] ? b[ch.dof_q[t]] : 0.0;
+    bc[t] = ch.valid[t] ? b[ch.dof_c[t]] : 0.0;
     if (ch.valid[t]) x[ch.dof_c[t]] = ACC ? x[ch.dof_c[t]] + z[ch.dof_c[t]] : z[ch.dof_c[t]];
   }
-  const double rqN = ch.has_last ? rhs_q(ch.dof_qN) : 0.0;
+  const double bqN = ch.has_last ? b[ch.dof_qN] : 0.0;
+  const int flip = active ? pa.chain_flip[c] : 0;  // chain top = the edge's source unless flipped
   double xv[CPL + 1];
-  chain_mass_solve<W, CPL>(pa, ch, rq, rqN, xv);
+  direct_flux_cons<W, CPL>(ch, flip, bc, bq, bqN, flip ? zdst : zsrc, flip ? zsrc : zdst, xv);
 #pragma unroll
   for (int t = 0; t < CPL; ++t)
     if (ch.valid[t]) x[ch.dof_q[t]] = ACC ? x[ch.dof_q[t]] + xv[t] : xv[t];

@@ -318,7 +318,8 @@ static double pc_apply(const Pc* p, const double* r, double* z) {
 }
 
 /* ---- direct tree solve (the GPU's kModeDirect sweeps, csrc/nxhip.hip): block LU of
- * [[M, K], [K^T, 0]] -- y = M^{-1} b_q, x_s = S^{-1}(K^T y - b_s), x_q = M^{-1}(b_q - K x_s) ---- */
+ * [[M, K], [K^T, 0]] -- y = M^{-1} b_q, x_s = S^{-1}(K^T y - b_s), x_q = M^{-1}(b_q - K x_s),
+ * the last one recovered conservatively (divergence rows exact) ---- */
 static void chain_thomas(const Pc* p, const double* rhs, double* out) {  /* T^{-1} rhs */
   const int N = p->N;
   const double* l = p->lu;
@@ -420,14 +421,19 @@ static void pc_direct(const Pc* p, const double* b, double* x, double* mb, int64
         zc[k] = zk;
         x[cell_dof(p, c, k)] = zk;
       }
-      for (int k = 0; k <= N; ++k) {  /* row q_k: +p_k - p_{k-1} - lambda_top + lambda_bottom */
-        double kz = (k < N ? zc[k] : 0.0) - (k > 0 ? zc[k - 1] : 0.0);
-        if (k == 0) kz -= zt;
-        if (k == N) kz += zb;
-        t[k] = b[q_dof(p, c, k)] - (flip ? -kz : kz);
+      /* fluxes, conservatively (csrc/nxhip.hip direct_flux_cons): the divergence rows give
+       * x_q[k] = q0 - s P_k, P_k = sum_{j<k} b_c[j]; the d-weighted sum of the flux rows
+       * gives T q0 = sum_k b_q[k] - s (zb - zt) + s sum_k d_k P_k */
+      const double sg = flip ? -1.0 : 1.0;
+      double s1 = 0.0, s2 = 0.0, P = 0.0;
+      for (int k = 0; k <= N; ++k) {
+        s1 += b[q_dof(p, c, k)];
+        s2 += rho[k] * P;
+        t[k] = P;
+        if (k < N) P += b[cell_dof(p, c, k)];
       }
-      chain_thomas(p, t, y);
-      for (int k = 0; k <= N; ++k) x[q_dof(p, c, k)] = y[k] / mo;
+      const double q0 = (s1 - sg * (zb - zt) + sg * s2) / T;
+      for (int k = 0; k <= N; ++k) x[q_dof(p, c, k)] = q0 - sg * t[k];
     }
     free(rho); free(Dk); free(w); free(zc); free(suf); free(t); free(y);
   }
