@@ -85,10 +85,23 @@ def res_chunks(n: int) -> int:
     return max(1, env) if env > 0 else (4 if n > (4 << 20) else 2)
 
 
-def direct_kernel_bytes(n: int, nnz: int, n_e: int, E: int, N: int, B: int, nblk: int) -> dict:
+def direct_kernel_bytes(n: int, nnz: int, n_e: int, E: int, N: int, B: int, nblk: int,
+                        fused: bool = False, n_jobs: int = 0, n_left: int = 0) -> dict:
     """Algorithmic bytes per launch of the direct solve's kernels:
-    f64 vectors, int32 indices, the lumped mass dq (E (N+1)) read by every chain sweep."""
+    f64 vectors, int32 indices, the lumped mass dq (E (N+1)) read by every chain sweep.
+    ``fused``: the down sweep forms the residual (reads the edge geometry and R to regenerate
+    the cell masses, stores r), k_dir_publish_fr sums its partials and forms the ``n_left``
+    multiplier rows of the top part from the CSR (3 entries each) instead of k_residual_ck."""
     dq = 8 * E * (N + 1)
+    if fused:
+        return {
+            "k_dir_publish_fr": 16 * n_jobs + n_left * (8 + 3 * 20 + 16),
+            "k_pc_up_lds": 8 * n_e + dq + 24 * E + 8 * E + 64 * B,
+            # + edge_x / R (56 B per edge) read, r stored at the edge DoFs and local multipliers
+            "k_pc_down_lds": 8 * n_e + dq + 8 * n + 16 * E + 24 * B + 56 * E + 8 * n_e + 8 * B,
+            "k_pc_top_lds": 64 * 1024,
+            "k_assemble_seg": 8 * nnz + 8 * n + dq + 80 * E,
+        }
     return {
         # CSR SpMV of x, b read, r stored (for a refinement step); two partials per block
         "k_residual_ck": 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n + 8 * n + 16 * nblk,
@@ -365,8 +378,12 @@ def run(args, world: int) -> int:
         n, nnz = h.n_rows, h.nnz
         n_e = E * (2 * N + 1)
         nblk = -(-n // (256 * res_chunks(n)))  # k_residual_ck blocks (partials)
-        kb = direct_kernel_bytes(n, nnz, n_e, E, N, B, nblk)
-        ms = {"k_residual_ck": pd["residual_ms"] / cnt, "k_pc_up_lds": pd["up_ms"] / cnt,
+        info = h.direct_info()
+        fused = info["fused_residual"]
+        rname = "k_dir_publish_fr" if fused else "k_residual_ck"
+        kb = direct_kernel_bytes(n, nnz, n_e, E, N, B, nblk, fused=fused,
+                                 n_jobs=asm.tree_preconditioner.n_jobs, n_left=info["n_left"])
+        ms = {rname: pd["residual_ms"] / cnt, "k_pc_up_lds": pd["up_ms"] / cnt,
               "k_pc_top_lds": pd["top_ms"] / cnt, "k_pc_down_lds": pd["down_ms"] / cnt,
               "k_assemble_seg": prof["asm_ms"] / max(prof["asm_count"], 1)}
         kernels = {}
@@ -379,15 +396,18 @@ def run(args, world: int) -> int:
         d = kernels[dom]
         names = {"k_residual_ck": "k_residual_ck (CSR SpMV r = b - A x: the direct solve's "
                                   "true-residual check)",
+                 "k_dir_publish_fr": "k_dir_publish_fr (the fused residual check's sums, the top "
+                                     "part's multiplier rows, the published state)",
                  "k_pc_up_lds": "k_pc_up_lds<false, 8, 2> (direct mode: M^-1 b_q per chain, "
                                 "chain condensation, junction elimination)",
-                 "k_pc_down_lds": "k_pc_down_lds<false, 8, 2> (direct mode: back-substitution, "
-                                  "cells, x_q = M^-1 (b_q - K x_s))",
+                 "k_pc_down_lds": "k_pc_down_lds<false, 8, 2, true> (direct mode: back-"
+                                  "substitution, cells, conservative x_q, the fused residual)",
                  "k_pc_top_lds": "k_pc_top_lds<false> (junctions above the cut)",
                  "k_assemble_seg": "k_assemble_seg<16> (CSR values + rhs)"}
         # kernel names as scripts/summarize_profile.py writes them (short form)
-        rocname = {"k_residual_ck": "k_residual_ck", "k_pc_up_lds": "k_pc_up_lds<false, 8, 2>",
-                   "k_pc_down_lds": "k_pc_down_lds<false, 8, 2>",
+        rocname = {"k_residual_ck": "k_residual_ck", "k_dir_publish_fr": "k_dir_publish_fr",
+                   "k_pc_up_lds": "k_pc_up_lds<false, 8, 2>",
+                   "k_pc_down_lds": "k_pc_down_lds<false, 8, 2, true>",
                    "k_pc_top_lds": "k_pc_top_lds<false>",
                    "k_assemble_seg": "k_assemble_seg<16>"}[dom]
         traffic, tsrc, rocprof_ns = (pmc_traffic(rocname) if default_workload

@@ -305,6 +305,11 @@ int nx_get_profile(nx_network_t* h, double* spmv_ms, int64_t* spmv_count, double
  * down sweeps (mode kModeDirect) and of the residual SpMV, over `count` direct solves, each
  * from events bound to the kernel's own dispatch (no graph while profiling). */
 int nx_get_profile_direct(nx_network_t* h, double* ms4, int64_t* count);
+/* How the direct solve checks its residual: *fused = 1 when the down sweep forms r = b - A x
+ * itself (one rank, LDS kernels; the 4th time of nx_get_profile_direct is then the publish
+ * kernel k_dir_publish_fr, which also forms the *n_left multiplier rows of the top part from
+ * the CSR), 0 when a separate CSR SpMV (k_residual_ck) does. */
+int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
 /* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,

@@ -61,6 +61,7 @@ _SIGS = {
     "nx_set_profiling": (C.c_int, [_h, _i32]),
     "nx_get_profile": (C.c_int, [_h, _pd, _pi64, _pd, _pi64]),
     "nx_get_profile_direct": (C.c_int, [_h, _pd, _pi64]),
+    "nx_get_direct_info": (C.c_int, [_h, _pi32, _pi32]),
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
     "nx_bench_spmv_cold": (C.c_int, [_h, _i32, _pi32, _pd]),
@@ -328,6 +329,12 @@ class Handle:
         check(lib().nx_get_profile_direct(self.ptr, ms, C.byref(n)))
         return {"up_ms": ms[0], "top_ms": ms[1], "down_ms": ms[2], "residual_ms": ms[3],
                 "count": int(n.value)}
+
+    def direct_info(self) -> dict:
+        """How the direct solve checks its residual (nx_get_direct_info)."""
+        f, n = C.c_int32(0), C.c_int32(0)
+        check(lib().nx_get_direct_info(self.ptr, C.byref(f), C.byref(n)))
+        return {"fused_residual": bool(f.value), "n_left": int(n.value)}
 
     def reset_profile(self) -> None:
         check(lib().nx_reset_profile(self.ptr))

@@ -1055,6 +1055,17 @@ struct PcArgs {
   double* send_buf;
   double* red1;
   double* gath_self;
+  // direct solve, one rank: the true residual r = b - A x is formed by the down sweep from
+  // the values it just computed (direct_residual): its chains' rows and the multiplier rows
+  // of the junctions whose chains are all in its job (slot_rloc); k_dir_publish_fr does the
+  // rest from the CSR. edge_x / edge_R regenerate the cell masses exactly as k_assemble does.
+  int fres;
+  const double* edge_x;
+  const double* edge_R;
+  const int* slot_rloc;
+  const double* rhs_b;  // the assembled rhs b (a refinement pass checks b - A (x + d))
+  double* rres;   // r (kept for a refinement step)
+  double* rpart;  // per job: partial ||r||^2, then (n_jobs on) partial ||b||^2
 };
 
 constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve in LDS
@@ -1111,12 +1122,12 @@ __device__ __forceinline__ double seg_sum(double v) {
 template <int W, int CPL>
 struct ChainLane {
   int valid[CPL];
-  int64_t dof_c[CPL];  // pressure DoF of chain cell k = l*CPL + t
-  int64_t dof_q[CPL];  // flux DoF of chain q_k (between cell k-1 and k)
+  int dof_c[CPL];  // pressure DoF of chain cell k = l*CPL + t (rows are int32, as in the CSR)
+  int dof_q[CPL];  // flux DoF of chain q_k (between cell k-1 and k)
   double rho[CPL];
   double D[CPL];       // resistance distance top -> cell k
   int has_last;        // this lane also owns q_N
-  int64_t dof_qN;
+  int dof_qN;
   double rhoN;
   double T;
   double mo;  // R h / 6 of the edge (its end flux's lumped mass is R h / 2)
@@ -1126,7 +1137,7 @@ struct ChainLane {
     const int l = threadIdx.x & (W - 1);
     const int e = active ? pa.chain_edge[c] : 0;
     const int flip = active ? pa.chain_flip[c] : 0;
-    const int64_t base = (int64_t)e * (2 * N + 1);
+    const int base = e * (2 * N + 1);
     const double* dqe = pa.dq + (int64_t)e * (N + 1);
     mo = active ? dqe[0] / 3.0 : 1.0;
     double acc = 0.0;
@@ -1576,6 +1587,107 @@ __device__ __forceinline__ void direct_flux_cons(const ChainLane<W, CPL>& ch, in
 #pragma unroll
   for (int t = 0; t < CPL; ++t) out[t] = ch.valid[t] ? q0 - sg * P[t] : 0.0;
   out[CPL] = ch.has_last ? q0 - sg * P[CPL] : 0.0;
+}
+
+// mo = R h / 6 of the lane's cells (chain order), with k_assemble's arithmetic: the CSR
+// values are R h / 3 and R h / 6 of the same h, bit for bit (direct_residual).
+template <int W, int CPL>
+__device__ __forceinline__ void chain_cell_mo(const PcArgs& pa, const ChainLane<W, CPL>& ch, int c,
+                                              bool active, int flip, double* mo) {
+#pragma clang fp contract(off)
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const int e = active ? pa.chain_edge[c] : 0;
+  double x0[3], x1[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    x0[i] = pa.edge_x[6 * (int64_t)e + i];
+    x1[i] = pa.edge_x[6 * (int64_t)e + 3 + i];
+  }
+  const double R = pa.edge_R[e];
+  const double invN = 1.0 / (double)N;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    mo[t] = 0.0;
+    if (!ch.valid[t]) continue;
+    const int k = l * CPL + t;
+    const int kp = flip ? N - 1 - k : k;  // the edge's cell
+    double va[3], vb[3];
+    vertex(x0, x1, kp, N, invN, va);
+    vertex(x0, x1, kp + 1, N, invN, vb);
+    const double d0 = vb[0] - va[0], d1 = vb[1] - va[1], d2 = vb[2] - va[2];
+    const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    mo[t] = R * h / 6.0;
+  }
+}
+
+// The direct solve's true residual on one chain's rows, r = vin - A out (pa.fres): vin = the
+// sweeps' input (b; the previous residual in a refinement pass, r' = r - A d), out = their
+// output (x; the correction d) -- cells xc, fluxes xq (q_N in xq[CPL] of the has_last lane),
+// end junctions zt / zb. The operator is the assembled one: the cell masses R h / 3, R h / 6
+// are regenerated with k_assemble's arithmetic (bit-identical CSR values), the pressure and
+// multiplier couplings are +-1 (k_pattern's rows, chain order: s = -1 on a flipped chain).
+// Stores r, adds r^2 and vin^2 to rr / bb, and posts the chain's shares of its end junctions'
+// multiplier rows (A[lam_top, q_0] = -s, A[lam_bot, q_N] = +s) to sQt / sQb[lc].
+template <int W, int CPL>
+__device__ __forceinline__ void direct_residual(const PcArgs& pa, const ChainLane<W, CPL>& ch,
+                                                bool active, int flip, const double* vc,
+                                                const double* vq, double vqN, const double* xc,
+                                                const double (&xq)[CPL + 1], double zt, double zb,
+                                                const double* mo, double& rr, double& bb,
+                                                double* sQt, double* sQb, int lc) {
+#pragma clang fp contract(off)
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const double sg = flip ? -1.0 : 1.0;
+  // md = R h / 3 = 2 mo exactly (mo = R h / 6: halving is exact in binary)
+  double md[CPL];
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) md[t] = 2.0 * mo[t];
+  // cell k - 1 of element 0 and flux k + 1 of the last element live in the neighbour lanes
+  const double mdP = __shfl_up(md[CPL - 1], 1, W), moP = __shfl_up(mo[CPL - 1], 1, W);
+  const double xcP = __shfl_up(xc[CPL - 1], 1, W), xqP = __shfl_up(xq[CPL - 1], 1, W);
+  const double xqX = __shfl_down(xq[0], 1, W);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    if (!ch.valid[t]) continue;
+    const int k = l * CPL + t;
+    const double qn = (k + 1 == N) ? xq[CPL] : (t + 1 < CPL ? xq[t + 1] : xqX);
+    const double rc = vc[t] - sg * (xq[t] - qn);  // cell row: s (q_k - q_{k+1})
+    double acc, xcl;
+    if (k == 0) {
+      acc = md[t] * xq[t] + mo[t] * qn;
+      xcl = zt;
+    } else {
+      const double mdl = t > 0 ? md[t - 1] : mdP, mol = t > 0 ? mo[t - 1] : moP;
+      const double xql = t > 0 ? xq[t - 1] : xqP;
+      xcl = t > 0 ? xc[t - 1] : xcP;
+      acc = mol * xql + (mdl + md[t]) * xq[t] + mo[t] * qn;
+    }
+    const double rq = vq[t] - (acc + sg * (xc[t] - xcl));  // flux row: mass + s (p_k - p_{k-1})
+    pa.rres[ch.dof_c[t]] = rc;
+    pa.rres[ch.dof_q[t]] = rq;
+    rr += rc * rc + rq * rq;
+    bb += vc[t] * vc[t] + vq[t] * vq[t];
+  }
+  if (ch.has_last) {  // q_N: cell N - 1 and the bottom junction
+    const int tl = (N - 1) - l * CPL;
+    double mdl = 0.0, mol = 0.0, xql = 0.0, xcl = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t)
+      if (t == tl) {
+        mdl = md[t];
+        mol = mo[t];
+        xql = xq[t];
+        xcl = xc[t];
+      }
+    const double rq = vqN - ((mol * xql + mdl * xq[CPL]) + sg * (zb - xcl));
+    pa.rres[ch.dof_qN] = rq;
+    rr += rq * rq;
+    bb += vqN * vqN;
+    sQb[lc] = sg * xq[CPL];
+  }
+  if (l == 0 && active) sQt[lc] = -sg * xq[0];
 }
 
 constexpr int kCapLvl = 64;  // job levels whose slot offsets are staged in LDS
@@ -2142,12 +2254,15 @@ __device__ void pc_pack_last(const PcArgs& pa, const double* partB, const double
   for (int i = threadIdx.x; i < pa.n_send; i += kPcThreads) pa.send_buf[i] = z[pa.send_idx[i]];
 }
 
-template <bool MULTI, int W, int CPL>
+// DIRK: the direct solve's instantiation (mode kModeDirect only; without the MINRES paths its
+// registers fit the fused residual without spills)
+template <bool MULTI, int W, int CPL, bool DIRK>
 __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* __restrict__ y,
                                                             const double* __restrict__ r2,
                                                             double* __restrict__ z,
                                                             const MrState* __restrict__ st,
-                                                            double* __restrict__ partB, int mode) {
+                                                            double* __restrict__ partB, int mode_in) {
+  const int mode = DIRK ? kModeDirect : mode_in;
   __shared__ double sZ[kCapS], sA[kCapS], sB[kCapS];
   __shared__ int sP[kCapS];
   __shared__ double sTa[kCapT];  // dense top: a_s of every top slot
@@ -2157,11 +2272,14 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ int sGp[kCapT], sGc[kCapT];
   __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
+  __shared__ double sQt[MULTI ? 1 : kCapC], sQb[MULTI ? 1 : kCapC];  // fused residual
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
   // direct solve (mode 3): y holds b, z is the solution x; the chains form the
   // cell inputs w from b again (as k_pc_up_lds did) and finish x_q = M^{-1} (b_q - K x_s)
-  const bool dir = mode == kModeDirect;
+  const bool dir = DIRK;
+  const bool fres = !MULTI && dir && pa.fres;  // the true residual of this job's rows
+  double rr = 0.0, bb = 0.0;
   NX_PHASE_START(48);
   const int job = blockIdx.x;
   double part = 0.0;
@@ -2177,6 +2295,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   ChainLane<W, CPL> ch;
   ch.setup(pa, c0 + seg, c0 + seg < c1);
   double vc[CPL], vq[CPL], vN = 0.0;
+  double mo_r[CPL];  // fused residual: the cells' R h / 6
   int ch_up = -1, ch_lo = -1, flip = 0;
   auto load_lane = [&](int c, bool active) {
 #pragma unroll
@@ -2347,6 +2466,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     part += yl * zl;
   }
   NX_PHASE(50);
+  if (fres && pa.accum) __syncthreads();  // the refined junction values above, for the check
   for (int cb = c0; cb < c1; cb += G) {
     const int c = cb + seg;
     const bool active = c < c1;
@@ -2354,9 +2474,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       ch.setup(pa, c, active);
       load_lane(c, active);
     }
+    if (fres) chain_cell_mo<W, CPL>(pa, ch, c, active, flip, mo_r);
     const int up = ch_up, lo = ch_lo;
-    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : outside(up);
-    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : outside(lo);
+    double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : outside(up);
+    double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : outside(lo);
     const double T = ch.T, iT = 1.0 / T;
     double rc[CPL], a[CPL], b[CPL], rq[CPL], zc[CPL];
     double sa = 0.0, sb = 0.0;
@@ -2426,17 +2547,56 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       for (int t = 0; t <= CPL; ++t) {
         const bool on = t < CPL ? ch.valid[t] : ch.has_last;
         if (!on) continue;
-        const int64_t d = t < CPL ? ch.dof_q[t] : ch.dof_qN;
+        const int d = t < CPL ? ch.dof_q[t] : ch.dof_qN;
         if (pa.accum)
           z[d] += xv[t];
         else
           z[d] = xv[t];
+      }
+      if (fres) {
+        if (pa.accum) {  // refinement pass: the true residual of the refined x, b - A (x + d)
+#pragma unroll
+          for (int t = 0; t < CPL; ++t)
+            if (ch.valid[t]) {
+              bcv[t] = pa.rhs_b[ch.dof_c[t]];
+              rq[t] = pa.rhs_b[ch.dof_q[t]];
+              zc[t] = z[ch.dof_c[t]];
+              xv[t] = z[ch.dof_q[t]];
+            }
+          if (ch.has_last) {
+            rqN = pa.rhs_b[ch.dof_qN];
+            xv[CPL] = z[ch.dof_qN];
+          }
+          zt = up < 0 ? 0.0 : z[pa.slot_lam[up]];
+          zb = lo < 0 ? 0.0 : z[pa.slot_lam[lo]];
+        }
+        direct_residual<W, CPL>(pa, ch, active, flip, bcv, rq, rqN, zc, xv, zt, zb, mo_r, rr, bb,
+                                sQt, sQb, c - c0);
       }
     } else {
       part += pc_flux_block<W, CPL>(pa, ch, rq, rqN, z);
     }
   }
   NX_PHASE(51);
+  if (fres) {  // multiplier rows of the junctions whose chains are all in this job
+    __syncthreads();
+    if ((int)threadIdx.x < ns) {
+      const int j = js0 + threadIdx.x;
+      if (pa.slot_rloc[j]) {
+        const int pc = pa.slot_pchain[j];
+        double acc = pc >= 0 ? sQb[pc - c0] : 0.0;
+        for (int i = pa.slot_dc_off[j]; i < pa.slot_dc_off[j + 1]; ++i) acc += sQt[pa.slot_dc[i] - c0];
+        const double bl = pa.accum ? pa.rhs_b[p_lam] : p_y;
+        const double rl = bl - acc;
+        pa.rres[p_lam] = rl;
+        rr += rl * rl;
+        bb += bl * bl;
+      }
+    }
+    block_sum_store_n<kPcThreads>(rr, pa.rpart + job);
+    __syncthreads();
+    block_sum_store_n<kPcThreads>(bb, pa.rpart + pa.n_jobs + job);
+  }
   if (!dir) block_sum_store_n<kPcThreads>(part, partB + blockIdx.x);
   NX_PHASE_END(48);
   if (MULTI && cfused && pa.fuse_pack) pc_pack_last(pa, partB, z);
@@ -3026,6 +3186,63 @@ __global__ __launch_bounds__(kReduceThreads) void k_dir_publish(const double* __
   }
 }
 
+// The fused check's publish step (pa.fres): the down sweeps' partials in job order, then the
+// rows no job could form (multiplier rows of junctions whose chains span jobs -- the top
+// part) from the CSR: r = b - A x, stored for a refinement step. ||b||^2 is that of the
+// first pass (bbst); a refinement pass (refine = 1) reuses it.
+__global__ __launch_bounds__(kReduceThreads) void k_dir_publish_fr(
+    const double* __restrict__ rpart, int nj, const int* __restrict__ left, int nleft, Csr A,
+    const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ rres,
+    double* __restrict__ bbst, int refine, double rtol, int* seq, MrState* mirror) {
+#pragma clang fp contract(off)
+  __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
+  double rr = 0.0, bb = 0.0;
+  for (int i = threadIdx.x; i < nj; i += kReduceThreads) {
+    rr += rpart[i];
+    bb += rpart[nj + i];
+  }
+  for (int i = threadIdx.x; i < nleft; i += kReduceThreads) {
+    const int row = left[i];
+    double acc = 0.0;
+    for (int k = A.rowptr[row]; k < A.rowptr[row + 1]; ++k) acc += A.val[k] * x[A.col[k]];
+    const double bv = b[row];
+    const double rv = bv - acc;
+    rres[row] = rv;
+    rr += rv * rv;
+    bb += bv * bv;
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_r[threadIdx.x >> 6] = rr;
+    s_b[threadIdx.x >> 6] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    rr = 0.0;
+    bb = 0.0;
+    for (int w = 0; w < kReduceThreads / 64; ++w) {
+      rr += s_r[w];
+      bb += s_b[w];
+    }
+    if (refine)
+      bb = bbst[0];
+    else
+      bbst[0] = bb;
+    MrState s{};
+    s.beta1 = sqrt(bb);
+    s.relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
+    s.rtol = rtol;
+    s.it = 1;
+    s.done = 1;
+    s.converged = s.relres <= rtol ? 1 : 0;
+    MrInit ini{};
+    ini.seq = seq;
+    ini.mirror = mirror;
+    mr_publish(s, ini);
+  }
+}
+
 // Halo pack + this rank's beta^2 (sum of the previous iteration's partials, block 0) into
 // red[1] and its own slot of the gathered array: saves a reduction launch per iteration.
 __global__ __launch_bounds__(kBlock) void k_pack_beta(const double* __restrict__ x,
@@ -3192,6 +3409,12 @@ struct nx_network {
   bool tree_exact = false;
   int last_solver = 0;        // what the last nx_solve ran (0 MINRES, 1 direct)
   int pend_lhs = 0, pend_rhs = 0;  // deferred nx_assemble (flush_assembly)
+  // direct solve, one rank: the residual check fused into the down sweep (PcArgs::fres);
+  // the rows it cannot form (left, n_left) and ||b||^2 of the first pass (dir_bb)
+  bool fres_ok = false;
+  int* d_left = nullptr;
+  int n_left = 0;
+  double* dir_bb = nullptr;
   // general element degrees (nx_create_fe): gather-assembly tables, one rank, no
   // preconditioner
   // nx_set_output_map: owned rows in the reference's function order (Solver.solve output)
@@ -3416,9 +3639,12 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
     hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2, z,
                        st, h->partB, mode);
   if (h->pc_jobs > 0) {
-    if (h->pc_lds)
-      hipExtLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0,
-                            h->stream, e[4], e[5], 0, h->pa, y, r2, z, st, h->partB, mode);
+    if (h->pc_lds && mode == kModeDirect)
+      hipExtLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL, true>), dim3(h->pc_jobs), dim3(kPcThreads),
+                            0, h->stream, e[4], e[5], 0, h->pa, y, r2, z, st, h->partB, mode);
+    else if (h->pc_lds)
+      hipExtLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL, false>), dim3(h->pc_jobs), dim3(kPcThreads),
+                            0, h->stream, e[4], e[5], 0, h->pa, y, r2, z, st, h->partB, mode);
     else
       hipLaunchKernelGGL((k_pc_down<MULTI, W, CPL>), dim3(h->pc_jobs), dim3(kBlock), 0, h->stream,
                          h->pa, y, z, st, h->partB, mode);
@@ -4267,9 +4493,18 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const double* bin = refine ? h->tmp : h->rhs;
   if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
     h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
+    h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the residual check
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, h->x, evs);
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, h->x, evs);
     h->pa.accum = 0;
+    h->pa.fres = 0;
+    if (h->fres_ok) {
+      hipExtLaunchKernelGGL(k_dir_publish_fr, dim3(1), dim3(kReduceThreads), 0, h->stream,
+                            prof ? h->dev[6] : nullptr, prof ? h->dev[7] : nullptr, 0, h->pa.rpart,
+                            h->pc_jobs, h->d_left, h->n_left, csr_of(h), h->x, h->rhs, h->tmp,
+                            h->dir_bb, refine, rtol, h->d_seq, h->d_last);
+      return;
+    }
   } else {
   const int64_t n_lm = h->n_own - h->n_edge_dofs;
   if (cb > 0)
@@ -4988,6 +5223,13 @@ NX_API int nx_get_profile_direct(nx_network_t* h, double* ms4, int64_t* count) {
   return NX_OK;
 }
 
+NX_API int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (fused) *fused = h->fres_ok ? 1 : 0;
+  if (n_left) *n_left = h->n_left;
+  return NX_OK;
+}
+
 NX_API int nx_reset_profile(nx_network_t* h) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
   h->spmv_ms = h->asm_ms = 0.0;
@@ -5264,6 +5506,56 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     }
   }
   if (const char* e = std::getenv("NXHIP_PC_GLOBAL")) lds = lds && std::atoi(e) == 0;
+  // fused residual of the direct solve (one rank, LDS kernels): a junction's multiplier row
+  // is formed by its job's down sweep when its chains -- the parent chain (lo = j) and the
+  // hanging ones (up = j) -- are exactly slot_pchain / slot_dc and all in that job; every
+  // other multiplier row goes to k_dir_publish_fr (the top part's)
+  pa.fres = 0;
+  pa.edge_x = h->edge_x;
+  pa.edge_R = h->edge_R;
+  h->fres_ok = false;
+  h->d_left = nullptr;
+  h->n_left = 0;
+  if (lds && h->nranks == 1 && h->comm == nullptr && n_jobs > 0) {
+    std::vector<int> job_of_chain(n_chains, -1), job_of_slot(n_slots, -1);
+    for (int jb = 0; jb < n_jobs; ++jb) {
+      for (int c = job_chain_off[jb]; c < job_chain_off[jb + 1]; ++c) job_of_chain[c] = jb;
+      for (int lv = job_lvl_off[jb]; lv < job_lvl_off[jb + 1]; ++lv)
+        for (int j = lvl_slot_off[lv]; j < lvl_slot_off[lv + 1]; ++j) job_of_slot[j] = jb;
+    }
+    std::vector<int> n_lo(n_slots, 0), n_up(n_slots, 0);
+    std::vector<char> far(n_slots, 0);  // a chain at this junction lies in another job
+    for (int64_t c = 0; c < n_chains; ++c) {
+      for (int end = 0; end < 2; ++end) {
+        const int j = end ? chain_lo[c] : chain_up[c];
+        if (j < 0) continue;
+        (end ? n_lo : n_up)[j] += 1;
+        if (job_of_chain[c] != job_of_slot[j]) far[j] = 1;
+      }
+    }
+    std::vector<int> rloc(n_slots, 0);
+    std::vector<char> done_row(h->n_own - h->n_edge_dofs, 0);
+    for (int64_t j = 0; j < n_slots; ++j) {
+      const int pcn = slot_pchain[j];
+      const bool ok = job_of_slot[j] >= 0 && !far[j] &&
+                      n_lo[j] == (pcn >= 0 ? 1 : 0) && (pcn < 0 || chain_lo[pcn] == j) &&
+                      n_up[j] == slot_dc_off[j + 1] - slot_dc_off[j];
+      rloc[j] = ok ? 1 : 0;
+      if (ok) done_row[slot_lam[j] - h->n_edge_dofs] = 1;
+    }
+    std::vector<int> left;
+    for (int64_t i = 0; i < (int64_t)done_row.size(); ++i)
+      if (!done_row[i]) left.push_back((int)(h->n_edge_dofs + i));
+    pa.slot_rloc = up(rloc.data(), n_slots);
+    h->d_left = const_cast<int*>(up(left.empty() ? nullptr : left.data(), (int64_t)left.size()));
+    pa.rpart = scratch(2 * (int64_t)n_jobs);
+    h->dir_bb = scratch(1);
+    pa.rres = h->tmp;
+    pa.rhs_b = h->rhs;
+    h->n_left = (int)left.size();
+    h->fres_ok = pa.slot_rloc && h->d_left && pa.rpart && h->dir_bb && h->tmp;
+    if (const char* e = std::getenv("NXHIP_DIR_FRES")) h->fres_ok = h->fres_ok && std::atoi(e) != 0;
+  }
   h->pc_lds = lds;
   h->pa = pa;
   h->pc_jobs = n_jobs;

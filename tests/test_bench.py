@@ -62,6 +62,19 @@ def test_direct_kernel_bytes_c3():
     assert 13e6 < kb["k_pc_up_lds"] < 16e6 and 20e6 < kb["k_pc_down_lds"] < 23e6
 
 
+def test_direct_kernel_bytes_fused_c3():
+    """Fused residual check: no residual SpMV; the down sweep also reads the edge geometry and
+    stores r (8 B per edge DoF and local multiplier), the publish step is small."""
+    n, nnz, E, N, B = 1_032_160, 3_571_600, 32_767, 15, 16_383
+    n_e = E * (2 * N + 1)
+    plain = bench.direct_kernel_bytes(n, nnz, n_e, E, N, B, 1)
+    kb = bench.direct_kernel_bytes(n, nnz, n_e, E, N, B, 1, fused=True, n_jobs=256, n_left=255)
+    assert set(kb) == {"k_dir_publish_fr", "k_pc_up_lds", "k_pc_down_lds", "k_pc_top_lds",
+                       "k_assemble_seg"}
+    assert kb["k_pc_down_lds"] - plain["k_pc_down_lds"] == 56 * E + 8 * n_e + 8 * B
+    assert kb["k_dir_publish_fr"] < 64 * 1024
+
+
 def test_solver_option_defaults_to_direct():
     assert bench.parse_args([]).solver == "direct"
     assert bench.parse_args(["--solver", "minres"]).solver == "minres"

@@ -154,3 +154,42 @@ def test_deferred_assembly_keeps_call_order():
     asm.assemble(assemble_lhs=False)  # rhs only: flushed, then the plain direct graph
     it, relres, conv = h.solve(1e-12, 100, 4)
     assert conv and np.linalg.norm(h.solution() - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
+@pytest.mark.parametrize("case", ["depth6_N40", "arterial5_N40", "tree6_2d_N70", "Y_N4",
+                                  "demo_tree_N1", "linear_alt_N3"])
+def test_fused_residual_is_the_true_residual(case, monkeypatch):
+    """The down sweep forms r = b - A x itself (PcArgs::fres; the top part's multiplier rows in
+    k_dir_publish_fr): the reported residual is the true one (host SpMV of the assembled CSR)
+    to 5%, the solution is bit-identical to the unfused check's (NXHIP_DIR_FRES=0), and a
+    forced refinement step (rtol just under the first pass's residual) converges with the
+    refined residual reported truthfully too."""
+    mesh, asm, P, A, b, pbc = _setup(case)
+    asm.set_direct(True)
+    h = asm.handle
+    asm.assemble()
+    it, rr, conv = h.solve(1e-12, 100, 4)
+    assert conv and it == 1 and h.solver() == (1, 1)
+    x_fused = h.solution()
+    true1 = h.true_residual()
+    assert abs(rr - true1) <= 0.05 * true1 + 5e-16, (rr, true1)  # 5e-16: see below
+    monkeypatch.setenv("NXHIP_DIR_FRES", "0")
+    asm.set_direct(True)
+    asm.set_preconditioner(True)
+    asm.assemble()
+    it0, rr0, _ = h.solve(1e-12, 100, 4)
+    np.testing.assert_array_equal(h.solution(), x_fused)
+    assert abs(rr0 - rr) <= 0.05 * rr0 + 5e-16
+    monkeypatch.delenv("NXHIP_DIR_FRES")
+    asm.set_preconditioner(True)
+    if rr > 4e-15:  # room for a refinement step below it
+        asm.assemble()
+        it2, rr2, conv2 = h.solve(rr / 2, 100, 4)
+        assert h.solver() == (1, 1) and it2 == 2 and conv2, (it2, rr2)
+        true2 = h.true_residual()
+        # at ~1e-16 the two evaluations (fused sweep / host CSR SpMV, different summation
+        # orders) differ by their own rounding, eps ||A|| ||x|| / ||b|| ~ 5e-16
+        assert rr2 <= rr / 2 and abs(rr2 - true2) <= 0.05 * true2 + 5e-16, (rr2, true2)
+        x_ref = O.solve_reference(A, b)
+        _, _, perm, _ = O.to_build_layout(P, A, b)
+        assert np.linalg.norm(h.solution() - x_ref[perm]) / np.linalg.norm(x_ref) <= SOL_TOL
