@@ -2272,13 +2272,13 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ int sGp[kCapT], sGc[kCapT];
   __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
-  __shared__ double sQt[MULTI ? 1 : kCapC], sQb[MULTI ? 1 : kCapC];  // fused residual
+  __shared__ double sQt[DIRK ? kCapC : 1], sQb[DIRK ? kCapC : 1];  // fused residual
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
   // direct solve (mode 3): y holds b, z is the solution x; the chains form the
   // cell inputs w from b again (as k_pc_up_lds did) and finish x_q = M^{-1} (b_q - K x_s)
   const bool dir = DIRK;
-  const bool fres = !MULTI && dir && pa.fres;  // the true residual of this job's rows
+  const bool fres = dir && pa.fres;  // the true residual of this job's rows
   double rr = 0.0, bb = 0.0;
   NX_PHASE_START(48);
   const int job = blockIdx.x;
@@ -2897,12 +2897,20 @@ __device__ void pc_prep_in_block(const PcArgs& pa, bool gcols, double* sJ, doubl
 // coarse slots take their coarse value -- and the partial r.z of the top slots.
 constexpr int kCapCoarse = 2048;
 
+// Coarse forest solve (redundant on every rank: same inputs, same order, same bits) and the
+// back-substitution of this rank's top part from the exact coarse values. Latency-bound, one
+// workgroup: the top part's per-solve inputs (J, D, the parent chain's T) and structure are
+// loaded into registers before the coarse solve (one slot per thread, the host caps the top
+// part at 1024) and staged in LDS after it, and a small coarse forest is solved from LDS
+// (pc_coarse_lds), so the level sweeps touch no global memory (8-rank depth-17 rehearsal:
+// 31.8 us per launch with per-level global loads).
 __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __restrict__ y,
                                                            const double* __restrict__ r2,
                                                            double* __restrict__ z,
                                                            MrState* __restrict__ st,
                                                            double* __restrict__ partB, int mode) {
   __shared__ double sD[kCapCoarse], sJ[kCapCoarse], sZ[kCapCoarse];
+  __shared__ int sTp[kTopThreads], sTl[kTopThreads];  // top slot: parent (local) or -2 - coarse index; lambda
   if (mode == 0 && st->done) return;
   // linear form: alpha arrived with the coarse partials; the Lanczos step is completed here
   double c2 = 0.0;
@@ -2917,66 +2925,124 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __
     }
   }
   const int nC = pa.n_coarse;
+  const bool backsub = !(pa.mdense && mode == 0);
+  const int ntl = pa.n_top_lvl;
+  const int ts0 = ntl > 0 ? pa.top_lvl_off[0] : 0;
+  const int nt = ntl > 0 ? pa.top_lvl_off[ntl] - ts0 : 0;
+  const bool staged = backsub && nt <= kTopThreads;
+  // this thread's top slot, loaded before the coarse solve (hides the global round trips)
+  const int sl0 = threadIdx.x;
+  int t_k = -1, t_lam = 0, t_par = -1;
+  double t_J = 0.0, t_D = 1.0, t_T = 1.0;
+  if (staged && sl0 < nt) {
+    const int j = ts0 + sl0;
+    t_k = pa.slot_cidx[j];
+    t_lam = pa.slot_lam[j];
+    if (t_k < 0) {
+      t_par = pa.slot_parent[j];
+      t_J = pa.slot_J[j];
+      t_D = pa.slot_D[j];
+      if (t_par >= 0) t_T = pa.chain_T[pa.slot_pchain[j]];
+    }
+  }
   const double* __restrict__ G = pa.cbuf + 2 * nC;
-  for (int i = threadIdx.x; i < nC; i += kTopThreads) {
-    sD[i] = pa.cbuf[i];
-    sJ[i] = pa.cbuf[nC + i];
-  }
-  __syncthreads();
-  for (int lv = pa.n_clvl - 1; lv >= 0; --lv) {  // deepest level first
-    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kTopThreads) {
-      double D = sD[j], J = sJ[j];
-      for (int i = pa.c_child_off[j]; i < pa.c_child_off[j + 1]; ++i) {
-        const int k = pa.c_child[i];
-        const double g = G[k], Dk = sD[k];
-        D -= g * g / Dk;
-        J += g * sJ[k] / Dk;
+  if (nC <= kCapCoarseLds) {
+    pc_coarse_lds(pa, sD, sJ, sZ);
+  } else {
+    for (int i = threadIdx.x; i < nC; i += kTopThreads) {
+      sD[i] = pa.cbuf[i];
+      sJ[i] = pa.cbuf[nC + i];
+    }
+    __syncthreads();
+    for (int lv = pa.n_clvl - 1; lv >= 0; --lv) {  // deepest level first
+      for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kTopThreads) {
+        double D = sD[j], J = sJ[j];
+        for (int i = pa.c_child_off[j]; i < pa.c_child_off[j + 1]; ++i) {
+          const int k = pa.c_child[i];
+          const double g = G[k], Dk = sD[k];
+          D -= g * g / Dk;
+          J += g * sJ[k] / Dk;
+        }
+        sD[j] = D;
+        sJ[j] = J;
       }
-      sD[j] = D;
-      sJ[j] = J;
+      __syncthreads();
     }
-    __syncthreads();
-  }
-  for (int lv = 0; lv < pa.n_clvl; ++lv) {  // root level first
-    for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kTopThreads) {
-      const int p = pa.c_parent[j];
-      sZ[j] = (sJ[j] + (p >= 0 ? G[j] * sZ[p] : 0.0)) / sD[j];
+    for (int lv = 0; lv < pa.n_clvl; ++lv) {  // root level first
+      for (int j = pa.c_lvl_off[lv] + threadIdx.x; j < pa.c_lvl_off[lv + 1]; j += kTopThreads) {
+        const int p = pa.c_parent[j];
+        sZ[j] = (sJ[j] + (p >= 0 ? G[j] * sZ[p] : 0.0)) / sD[j];
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
-  if (pa.mdense && mode == 0) {  // the down kernels evaluate the top part (dense rows)
+  if (!backsub) {  // the down kernels evaluate the top part (dense rows)
     for (int j = threadIdx.x; j < nC; j += kTopThreads) pa.zc[j] = sZ[j];
     if (threadIdx.x == 0) partB[pa.n_jobs] = 0.0;
     return;
   }
   double part = 0.0;
-  for (int lv = 0; lv < pa.n_top_lvl; ++lv) {
-    for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads) {
-      const int k = pa.slot_cidx[j];
-      const int lam = pa.slot_lam[j];
-      double zj;
-      if (k >= 0) {
-        zj = sZ[k];
-      } else {
-        const int p = pa.slot_parent[j];
-        double num = pa.slot_J[j];
-        if (p >= 0) num += pa.slot_z[p] / pa.chain_T[pa.slot_pchain[j]];
-        zj = num / pa.slot_D[j];
-      }
-      pa.slot_z[j] = zj;
-      double yl = y[lam];
-      if (lin) {  // ghost slots: y = r2 = 0 and the halo overwrites z
-        zj -= c2 * z[lam];
-        yl -= c2 * r2[lam];
-        y[lam] = yl;
-      }
-      if (mode == kModeDirect && pa.accum)
-        z[lam] += zj;
-      else
-        z[lam] = zj;
-      part += yl * zj;
+  auto finish = [&](int j, int lam, double zj) {
+    pa.slot_z[j] = zj;
+    double yl = y[lam];
+    if (lin) {  // ghost slots: y = r2 = 0 and the halo overwrites z
+      zj -= c2 * z[lam];
+      yl -= c2 * r2[lam];
+      y[lam] = yl;
+    }
+    if (mode == kModeDirect && pa.accum)
+      z[lam] += zj;
+    else
+      z[lam] = zj;
+    part += yl * zj;
+  };
+  if (staged) {  // sD / sJ are free now: J, D | T, z of the top slots
+    double* sTJ = sD;
+    double* sTD = sD + kTopThreads;
+    double* sTT = sJ;
+    double* sTZ = sJ + kTopThreads;
+    if (sl0 < nt) {
+      sTJ[sl0] = t_J;
+      sTD[sl0] = t_D;
+      sTT[sl0] = t_T;
+      sTp[sl0] = t_k >= 0 ? -2 - t_k : (t_par >= 0 ? t_par - ts0 : -1);
+      sTl[sl0] = t_lam;
     }
     __syncthreads();
+    for (int lv = 0; lv < ntl; ++lv) {
+      for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads) {
+        const int sl = j - ts0;
+        const int p = sTp[sl];
+        double zj;
+        if (p <= -2) {
+          zj = sZ[-2 - p];
+        } else {
+          double num = sTJ[sl];
+          if (p >= 0) num += sTZ[p] / sTT[sl];
+          zj = num / sTD[sl];
+        }
+        sTZ[sl] = zj;
+        finish(j, sTl[sl], zj);
+      }
+      __syncthreads();
+    }
+  } else {
+    for (int lv = 0; lv < ntl; ++lv) {
+      for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads) {
+        const int k = pa.slot_cidx[j];
+        double zj;
+        if (k >= 0) {
+          zj = sZ[k];
+        } else {
+          const int p = pa.slot_parent[j];
+          double num = pa.slot_J[j];
+          if (p >= 0) num += pa.slot_z[p] / pa.chain_T[pa.slot_pchain[j]];
+          zj = num / pa.slot_D[j];
+        }
+        finish(j, pa.slot_lam[j], zj);
+      }
+      __syncthreads();
+    }
   }
   block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
 }
@@ -3124,6 +3190,53 @@ __global__ __launch_bounds__(kReduceThreads) void k_dir_reduce2(const double* __
       rr += s_r[w];
       bb += s_b[w];
     }
+    out[0] = rr;
+    out[1] = bb;
+  }
+}
+
+// Several ranks, fused check: this rank's ||r||^2, ||b||^2 (the down sweeps' partials in job
+// order, then its owned rows no job could form -- the top part's and the cut junctions'
+// multiplier rows, after the halo of x -- from the CSR, r stored) -> out[0], out[1].
+__global__ __launch_bounds__(kReduceThreads) void k_dir_reduce2_fr(
+    const double* __restrict__ rpart, int nj, const int* __restrict__ left, int nleft, Csr A,
+    const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ rres,
+    double* __restrict__ bbst, int refine, double* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
+  double rr = 0.0, bb = 0.0;
+  for (int i = threadIdx.x; i < nj; i += kReduceThreads) {
+    rr += rpart[i];
+    bb += rpart[nj + i];
+  }
+  for (int i = threadIdx.x; i < nleft; i += kReduceThreads) {
+    const int row = left[i];
+    double acc = 0.0;
+    for (int k = A.rowptr[row]; k < A.rowptr[row + 1]; ++k) acc += A.val[k] * x[A.col[k]];
+    const double bv = b[row];
+    const double rv = bv - acc;
+    rres[row] = rv;
+    rr += rv * rv;
+    bb += bv * bv;
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_r[threadIdx.x >> 6] = rr;
+    s_b[threadIdx.x >> 6] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    rr = 0.0;
+    bb = 0.0;
+    for (int w = 0; w < kReduceThreads / 64; ++w) {
+      rr += s_r[w];
+      bb += s_b[w];
+    }
+    if (refine)
+      bb = bbst[0];
+    else
+      bbst[0] = bb;
     out[0] = rr;
     out[1] = bb;
   }
@@ -4591,14 +4704,22 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
       nx_network* h = t.hs[r];
       double* bin = refine ? h->tmp : h->rhs;
       h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
+      h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the local rows' residual
       launch_pc<true>(h, bin, bin, h->st, h->st + 1, kModeDirect, half, h->x);
       h->pa.accum = 0;
+      h->pa.fres = 0;
     }
     if (half == 0) CHECK(team_allreduce(t, -1, 3 * h0->pa.n_coarse));
   }
   CHECK(team_halo(t, VS_X, 0));
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
+    if (h->fres_ok) {  // the down sweeps formed the local rows; the rest need the halo of x
+      hipLaunchKernelGGL(k_dir_reduce2_fr, dim3(1), dim3(kReduceThreads), 0, h->stream,
+                         h->pa.rpart, h->pc_jobs, h->d_left, h->n_left, csr_of(h), h->x, h->rhs,
+                         h->tmp, h->dir_bb, refine, h->red + 2);
+      continue;
+    }
     const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
     hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
                        h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));  // r kept: refinement
@@ -5516,7 +5637,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->fres_ok = false;
   h->d_left = nullptr;
   h->n_left = 0;
-  if (lds && h->nranks == 1 && h->comm == nullptr && n_jobs > 0) {
+  if (lds && n_jobs > 0) {  // one rank or several (then only owned rows of lower jobs)
     std::vector<int> job_of_chain(n_chains, -1), job_of_slot(n_slots, -1);
     for (int jb = 0; jb < n_jobs; ++jb) {
       for (int c = job_chain_off[jb]; c < job_chain_off[jb + 1]; ++c) job_of_chain[c] = jb;
@@ -5537,11 +5658,11 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     std::vector<char> done_row(h->n_own - h->n_edge_dofs, 0);
     for (int64_t j = 0; j < n_slots; ++j) {
       const int pcn = slot_pchain[j];
-      const bool ok = job_of_slot[j] >= 0 && !far[j] &&
+      const bool ok = job_of_slot[j] >= 0 && !far[j] && slot_lam[j] < h->n_own &&
                       n_lo[j] == (pcn >= 0 ? 1 : 0) && (pcn < 0 || chain_lo[pcn] == j) &&
                       n_up[j] == slot_dc_off[j + 1] - slot_dc_off[j];
       rloc[j] = ok ? 1 : 0;
-      if (ok) done_row[slot_lam[j] - h->n_edge_dofs] = 1;
+      if (ok) done_row[slot_lam[j] - h->n_edge_dofs] = 1;  // owned: slot_lam < n_own
     }
     std::vector<int> left;
     for (int64_t i = 0; i < (int64_t)done_row.size(); ++i)
