@@ -271,6 +271,17 @@ int nx_get_rhs(nx_network_t* h, double* b);
 int nx_set_output_map(nx_network_t* h, int64_t n, const int32_t* rows);
 int nx_get_solution_blocks(nx_network_t* h, double* out);
 
+/* Deferred form of nx_get_solution_blocks (what Solver.solve returns by default):
+ * nx_snapshot_solution gathers x into the function order into the handle's device
+ * snapshot `slot` (0 <= slot < 64, allocated on first use) on the handle's stream and
+ * returns without waiting -- later solves do not disturb it; nx_fetch_snapshot copies a
+ * slot to `out` (n_rows doubles) on a separate copy stream once the gather has run and
+ * waits for that copy only. The caller owns the slot bookkeeping (a slot is rewritten by
+ * the next nx_snapshot_solution into it). Replaces the same assign as above
+ * (solver.py:120-134): the functions' host arrays are filled when first read. */
+int nx_snapshot_solution(nx_network_t* h, int32_t slot);
+int nx_fetch_snapshot(nx_network_t* h, int32_t slot, double* out);
+
 /* Page-locked host memory for nx_get_solution_blocks (hipHostMalloc / hipHostFree). */
 int nx_host_alloc(int64_t bytes, void** out);
 int nx_host_free(void* p);

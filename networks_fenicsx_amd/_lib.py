@@ -51,6 +51,8 @@ _SIGS = {
     "nx_get_rhs": (C.c_int, [_h, _pd]),
     "nx_set_output_map": (C.c_int, [_h, _i64, _pi32]),
     "nx_get_solution_blocks": (C.c_int, [_h, C.c_void_p]),
+    "nx_snapshot_solution": (C.c_int, [_h, _i32]),
+    "nx_fetch_snapshot": (C.c_int, [_h, _i32, C.c_void_p]),
     "nx_host_alloc": (C.c_int, [_i64, C.POINTER(C.c_void_p)]),
     "nx_host_free": (C.c_int, [C.c_void_p]),
     "nx_get_vector": (C.c_int, [_h, _i32, _pd]),
@@ -283,6 +285,17 @@ class Handle:
         if out.dtype != np.float64 or out.size != self.n_rows or not out.flags.c_contiguous:
             raise ValueError(f"out must be a contiguous float64 array of {self.n_rows} entries")
         check(lib().nx_get_solution_blocks(self.ptr, C.c_void_p(out.ctypes.data)))
+        return out
+
+    def snapshot_solution(self, slot: int) -> None:
+        """Gather the solution in the output order into device snapshot ``slot`` (async)."""
+        check(lib().nx_snapshot_solution(self.ptr, int(slot)))
+
+    def fetch_snapshot(self, slot: int, out: np.ndarray) -> np.ndarray:
+        """Copy device snapshot ``slot`` into ``out`` (n_rows doubles, ideally pinned)."""
+        if out.dtype != np.float64 or out.size != self.n_rows or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a contiguous float64 array of {self.n_rows} entries")
+        check(lib().nx_fetch_snapshot(self.ptr, int(slot), C.c_void_p(out.ctypes.data)))
         return out
 
     def rhs(self) -> np.ndarray:
@@ -540,6 +553,80 @@ class PinnedPool:
 
     def __del__(self):
         self.close()
+
+
+_MAX_SNAPSHOTS = 64  # csrc/nxhip.hip kMaxSnap
+
+
+class DeferredSolution:
+    """One solve's output, held in a device snapshot slot until it is first read.
+
+    ``array()`` copies the slot into a pinned buffer (one DMA, on the handle's copy stream)
+    and frees the slot; until then later solves on the handle do not disturb it."""
+
+    def __init__(self, pool: "SnapshotPool", slot: int):
+        self._pool = pool
+        self._slot = slot
+        self._buf = None
+
+    @property
+    def ready(self) -> bool:
+        return self._buf is not None
+
+    def array(self) -> np.ndarray:
+        if self._buf is None:
+            buf = self._pool.pinned.take()
+            self._pool.handle.fetch_snapshot(self._slot, buf)
+            self._buf = buf
+            self._pool.release(self._slot, self)
+        return self._buf
+
+    def __del__(self):
+        try:
+            if self._buf is None:
+                self._pool.release(self._slot, self)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+class SnapshotPool:
+    """Device snapshot slots of one handle (``nx_snapshot_solution``): ``take()`` gathers the
+    current solution into a free slot and returns its :class:`DeferredSolution`. With every
+    slot in use the oldest unread snapshot is read first (frees its slot)."""
+
+    def __init__(self, handle: "Handle", pinned: PinnedPool):
+        self.handle = handle
+        self.pinned = pinned
+        self._free = list(range(_MAX_SNAPSHOTS - 1, -1, -1))
+        self._live: dict[int, weakref.ref] = {}  # slot -> unread DeferredSolution (oldest first)
+
+    def take(self) -> DeferredSolution:
+        if not self._free:
+            oldest = next(iter(self._live.values()))()
+            if oldest is not None:
+                oldest.array()
+            else:  # collected without __del__ running yet
+                self._free.append(next(iter(self._live)))
+                del self._live[next(iter(self._live))]
+        slot = self._free.pop()
+        self.handle.snapshot_solution(slot)
+        d = DeferredSolution(self, slot)
+        self._live[slot] = weakref.ref(d)
+        return d
+
+    def release(self, slot: int, owner: DeferredSolution) -> None:
+        ref = self._live.get(slot)
+        if ref is not None and ref() in (owner, None):
+            del self._live[slot]
+            self._free.append(slot)
+
+    def materialize_all(self) -> None:
+        """Read every unread snapshot (before the handle goes away)."""
+        for ref in list(self._live.values()):
+            d = ref()
+            if d is not None:
+                d.array()
+        self._live.clear()
 
 
 def set_lean(enable: bool) -> None:

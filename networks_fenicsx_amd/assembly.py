@@ -376,6 +376,7 @@ class HydraulicNetworkAssembler:
         self._out_off = np.concatenate([[0], np.cumsum([b.size for b in blocks])]).astype(np.int64)
         self._handle.set_output_map(np.concatenate(blocks))
         self._out_pool = _lib.PinnedPool(self._handle.n_rows)
+        self._snap_pool = _lib.SnapshotPool(self._handle, self._out_pool)
 
     def set_preconditioner(self, enable: bool) -> bool:
         """Switch the device MINRES between preconditioned and plain; returns the state
@@ -564,27 +565,38 @@ class HydraulicNetworkAssembler:
         functions[-1].x.array[:] = x[self._lm_idx]
         return functions
 
-    def solution_functions(self, functions: list | None = None) -> list:
+    def solution_functions(self, functions: list | None = None, deferred: bool = True) -> list:
         """The device solution as ``[flux_color_0 .., pressure, global_flux]`` (the
-        reference's ``assign``, ``solver.py:120-134``): one gather kernel into the block
-        order and one DMA into a pinned buffer. New functions are views of that buffer;
-        given ``functions`` are filled from it."""
-        buf = self._out_pool.take()
-        self._handle.solution_blocks(buf)
+        reference's ``assign``, ``solver.py:120-134``), in the block order by one gather
+        kernel. New functions (``deferred``, the default) hold a device snapshot of it and
+        read it into a pinned buffer -- one DMA for all of them -- when the first one's
+        ``x.array`` is used; ``deferred=False`` copies at once. Given ``functions`` are
+        filled at once."""
         off = self._out_off
         spaces = self.function_spaces
         if functions is None:
             names = [f"flux_color_{i}" for i in range(len(self._flux_spaces))]
             names += ["pressure", "global_flux"]
+            if deferred:
+                src = self._snap_pool.take()
+                return [Function(V, name=nm, deferred=(src, int(off[i]), int(off[i + 1])))
+                        for i, (V, nm) in enumerate(zip(spaces, names))]
+            buf = self._out_pool.take()
+            self._handle.solution_blocks(buf)
             return [Function(V, name=nm, array=buf[off[i]:off[i + 1]])
                     for i, (V, nm) in enumerate(zip(spaces, names))]
         if len(functions) != len(spaces):
             raise ValueError(f"expected {len(spaces)} functions, got {len(functions)}")
+        buf = self._out_pool.take()
+        self._handle.solution_blocks(buf)
         for i, fn in enumerate(functions):
             np.copyto(fn.x.array, buf[off[i]:off[i + 1]])
         return functions
 
     def close(self) -> None:
+        snaps = getattr(self, "_snap_pool", None)
+        if snaps is not None and getattr(self._handle, "_h", None):
+            snaps.materialize_all()  # returned functions stay valid after close
         pool = getattr(self, "_out_pool", None)
         if pool is not None:
             pool.close()

@@ -3533,6 +3533,11 @@ struct nx_network {
   // nx_set_output_map: owned rows in the reference's function order (Solver.solve output)
   int* out_idx = nullptr;
   int64_t n_out = 0;
+  // nx_snapshot_solution / nx_fetch_snapshot: device copies of x in the output order, the
+  // event after each gather, the stream their device-to-host copies run on
+  std::vector<double*> snap;
+  std::vector<hipEvent_t> snap_ev;
+  hipStream_t copy_stream = nullptr;
   bool fe = false;
   int* fe_kind = nullptr;
   double* fe_tval = nullptr;
@@ -4331,6 +4336,11 @@ NX_API int nx_destroy(nx_network_t* h) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : h->dev)
     if (e) (void)hipEventDestroy(e);
+  for (double* p : h->snap)
+    if (p) (void)hipFree(p);
+  for (auto& e : h->snap_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return NX_OK;
@@ -5218,6 +5228,44 @@ NX_API int nx_get_solution_blocks(nx_network_t* h, double* out) {
                            h->stream));
   }
   HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+
+constexpr int kMaxSnap = 64;
+
+NX_API int nx_snapshot_solution(nx_network_t* h, int32_t slot) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (slot < 0 || slot >= kMaxSnap) return fail(NX_ERR_ARG, "snapshot slot out of range");
+  if (!h->out_idx && h->n_own > 0) return fail(NX_ERR_STATE, "nx_set_output_map first");
+  CHECK(set_device(h));
+  if ((int)h->snap.size() <= slot) {
+    h->snap.resize((size_t)slot + 1, nullptr);
+    h->snap_ev.resize((size_t)slot + 1, nullptr);
+  }
+  if (!h->snap_ev[slot]) HIPCALL(hipEventCreateWithFlags(&h->snap_ev[slot], hipEventDisableTiming));
+  if (h->n_own > 0) {
+    if (!h->snap[slot]) CHECK(dalloc(&h->snap[slot], h->n_own));
+    hipLaunchKernelGGL(k_gather_out, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
+                       h->x, h->out_idx, h->n_own, h->snap[slot]);
+    HIPCALL(hipGetLastError());
+  }
+  HIPCALL(hipEventRecord(h->snap_ev[slot], h->stream));
+  return NX_OK;
+}
+
+NX_API int nx_fetch_snapshot(nx_network_t* h, int32_t slot, double* out) {
+  if (!h || !out) return fail(NX_ERR_ARG, "null argument");
+  if (slot < 0 || slot >= (int)h->snap_ev.size() || !h->snap_ev[slot])
+    return fail(NX_ERR_STATE, "no snapshot in this slot (nx_snapshot_solution first)");
+  CHECK(set_device(h));
+  if (h->n_own > 0) {
+    if (!h->copy_stream) HIPCALL(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+    HIPCALL(hipStreamWaitEvent(h->copy_stream, h->snap_ev[slot], 0));
+    HIPCALL(hipMemcpyAsync(out, h->snap[slot], sizeof(double) * h->n_own, hipMemcpyDeviceToHost,
+                           h->copy_stream));
+    HIPCALL(hipStreamSynchronize(h->copy_stream));
+  }
   return NX_OK;
 }
 

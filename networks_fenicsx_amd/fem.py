@@ -77,12 +77,31 @@ class FunctionSpace:
 
 
 class Vector:
-    """``.x`` of a :class:`Function` (DOLFINx ``la.Vector`` subset)."""
+    """``.x`` of a :class:`Function` (DOLFINx ``la.Vector`` subset).
 
-    def __init__(self, n: int, array: np.ndarray | None = None):
+    ``deferred=(source, lo, hi)``: the values are ``source.array()[lo:hi]``, read when
+    ``array`` is first used (the solver's output stays on the device until then)."""
+
+    def __init__(self, n: int, array: np.ndarray | None = None, deferred=None):
         if array is not None and array.shape != (n,):
             raise ValueError(f"array must have shape ({n},)")
-        self.array = np.zeros(n, dtype=np.float64) if array is None else array
+        self._n = n
+        self._deferred = deferred if array is None else None
+        self._array = array if array is not None or deferred is not None else np.zeros(
+            n, dtype=np.float64)
+
+    @property
+    def array(self) -> np.ndarray:
+        if self._deferred is not None:
+            src, lo, hi = self._deferred
+            self._array = src.array()[lo:hi]
+            self._deferred = None
+        return self._array
+
+    @array.setter
+    def array(self, value: np.ndarray) -> None:
+        self._deferred = None
+        self._array = value
 
     def scatter_forward(self) -> None:
         return None
@@ -92,14 +111,14 @@ class Vector:
 
 
 class Function:
-    """``array``: an existing float64 buffer to use as ``x.array`` (the solver passes views
-    of its pinned output buffer)."""
+    """``array``: an existing float64 buffer to use as ``x.array``; ``deferred``: the
+    solver's device-held output (see :class:`Vector`)."""
 
     def __init__(self, V: FunctionSpace, name: str | None = None,
-                 array: np.ndarray | None = None):
+                 array: np.ndarray | None = None, deferred=None):
         self.function_space = V
         self.name = name or "f"
-        self.x = Vector(V.num_dofs, array)
+        self.x = Vector(V.num_dofs, array, deferred)
 
     def __repr__(self) -> str:
         return f"Function({self.name!r}, {self.function_space!r})"

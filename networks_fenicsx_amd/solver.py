@@ -158,9 +158,11 @@ class Solver:
     @timed("nxfx:Solver:solve")
     def solve(self, functions: list | None = None) -> list:
         """Solve on the device and return ``[flux_color_0.., pressure, global_flux]``
-        (``solver.py:107-135``). The functions are filled by one gather kernel and one DMA
-        (``HydraulicNetworkAssembler.solution_functions``); new ones are views of a pinned
-        buffer that is reused only after every function of that solve is dropped."""
+        (``solver.py:107-135``). One gather kernel snapshots the solution on the device in
+        the functions' order; new functions read it -- one DMA into a pinned buffer for all
+        of them -- when the first ``x.array`` is used, so later solves never change them
+        (``HydraulicNetworkAssembler.solution_functions``). Given ``functions`` are filled
+        at once."""
         if self._closed:
             raise RuntimeError("the solver has been destroyed")
         h = self.assembler.handle

@@ -7,7 +7,8 @@
 * ``Solver.solve`` output (``solver.py:107-135``): functions in the reference's order,
   filled by the device gather into pinned memory; buffers are reused only after the
   functions of a solve are dropped; given functions are filled in place;
-* ``Solver.destroy`` (``solver.py:137-143``).
+* ``Solver.destroy`` (``solver.py:137-143``);
+* deferred output: the functions of a solve read their device snapshot when first used.
 """
 
 from __future__ import annotations
@@ -115,3 +116,40 @@ def test_solution_functions_order_and_pinned_reuse():
     gc.collect()
     got = np.concatenate([f.x.array for f in out])
     assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= 1e-10
+
+
+def test_deferred_functions_keep_their_solve():
+    """Functions returned by ``solve`` hold a device snapshot until first read
+    (``nx_snapshot_solution``): later solves of a different problem do not change them,
+    more unread solves than device slots are read in order, and ``close`` reads the rest."""
+    mesh, asm, P, A, b = _setup("depth6_N40")
+    x_ref = O.solve_reference(A, b)
+    solver = Solver(asm)
+
+    def solve_scaled(s):
+        asm.compute_forms(p_bc_ex=lambda x, s=s: s * x[1])
+        solver.assemble()
+        return solver.solve()
+
+    held = [solve_scaled(s) for s in range(1, 71)]  # 70 unread solves > 64 slots
+    assert all(f.x._deferred is not None for f in held[-1])
+    for s, sol in reversed(list(enumerate(held, start=1))):
+        got = np.concatenate([f.x.array for f in sol])
+        assert np.linalg.norm(got - s * x_ref) / np.linalg.norm(s * x_ref) <= 1e-10, s
+    # the functions of one solve share one buffer after the read
+    assert all(f.x.array.base is held[0][0].x.array.base for f in held[0])
+    # unread functions survive the assembler's close
+    last = solve_scaled(3)
+    solver.destroy()
+    asm.close()
+    gc.collect()
+    got = np.concatenate([f.x.array for f in last])
+    assert np.linalg.norm(got - 3 * x_ref) / np.linalg.norm(3 * x_ref) <= 1e-10
+    # eager read on request
+    mesh, asm, P, A, b = _setup("Y_N4")
+    solver = Solver(asm)
+    solver.assemble()
+    solver.solve()
+    eager = asm.solution_functions(deferred=False)
+    assert all(f.x._deferred is None for f in eager)
+    asm.close()
