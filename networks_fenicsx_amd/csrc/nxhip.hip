@@ -1066,6 +1066,7 @@ struct PcArgs {
   const double* rhs_b;  // the assembled rhs b (a refinement pass checks b - A (x + d))
   double* rres;   // r (kept for a refinement step)
   double* rpart;  // per job: partial ||r||^2, then (n_jobs on) partial ||b||^2
+  int top_reg;    // k_pc_top_lds: register level sweeps allowed (NXHIP_TOP_REG)
 };
 
 constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve in LDS
@@ -2122,6 +2123,68 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   // direct mode: sY holds 1 / D of every slot once its level is done (one division per
   // slot instead of two per child on the level's critical path; sY's partial is not needed)
   const bool dir = mode == kModeDirect;
+  // register sweeps (top part <= kTopThreads slots with <= kWaveKids junction children
+  // each -- every binary tree's): thread = slot, its level, children and their g loaded
+  // into registers once, so a level costs one LDS round trip for the children's values
+  // (both issued together) and the division, instead of two dependent trips per child.
+  // Same arithmetic in the same order. NXHIP_TOP_REG=0: the loops over LDS below.
+  const int rsl = threadIdx.x;
+  const bool rmine = rsl < nt;
+  int rlv = -1, rnk = 0, rch[kWaveKids];
+  double rg[kWaveKids];
+#pragma unroll
+  for (int k = 0; k < kWaveKids; ++k) {
+    rch[k] = 0;
+    rg[k] = 0.0;
+  }
+  if (rmine) {
+    for (int q = 0; q < nl; ++q)
+      if (ts0 + rsl >= sLv[q] && ts0 + rsl < sLv[q + 1]) rlv = q;
+    for (int i = sOff[rsl]; i < sOff[rsl + 1]; ++i) {
+      const int chd = sChild[i];
+      if (chd < 0) continue;
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k)
+        if (k == rnk) {
+          rch[k] = chd;
+          rg[k] = sG[i];
+        }
+      ++rnk;
+    }
+  }
+  const bool reg = pa.top_reg && nt <= kTopThreads && __syncthreads_or(rnk > kWaveKids) == 0;
+  double rD = rmine ? sD0[rsl] : 1.0, rJ = rmine ? sJ0[rsl] : 0.0, riv = 1.0;
+  if (reg) {
+    for (int lv = nl - 1; lv >= 0; --lv) {
+      if (rlv == lv) {
+        double cv[kWaveKids], cj[kWaveKids];
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          cv[k] = k < rnk ? (dir ? sY[rch[k]] : sD[rch[k]]) : 1.0;
+          cj[k] = k < rnk ? sJ[rch[k]] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          if (k >= rnk) break;
+          const double g = rg[k];
+          if (dir) {
+            rD += g * (1.0 - g * cv[k]);
+            rJ += g * cj[k] * cv[k];
+          } else {
+            rD += g * (1.0 - g / cv[k]);
+            rJ += g * cj[k] / cv[k];
+          }
+        }
+        if (dir) {
+          riv = 1.0 / rD;
+          sY[rsl] = riv;
+        }
+        sD[rsl] = rD;
+        sJ[rsl] = rJ;
+      }
+      __syncthreads();
+    }
+  } else
   for (int lv = nl - 1; lv >= 0; --lv) {
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
       const int sl = j - ts0;
@@ -2159,6 +2222,25 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
     return;
   }
   double part = 0.0;
+  if (reg) {  // thread = slot: z_j = (J_j + g_par z_par) / D_j, root level first
+    const int p = rmine ? sPar[rsl] : -1;
+    const double gp = rmine ? sGp[rsl] : 0.0;
+    const int lam = rmine ? sLam[rsl] : 0;
+    for (int lv = 0; lv < nl; ++lv) {
+      if (rlv == lv) {
+        const double num = rJ + (p >= 0 ? gp * sJ0[p] : 0.0);
+        const double zj = dir ? num * riv : num / rD;
+        sJ0[rsl] = zj;  // reuse: z of top slots
+        if (dir && pa.accum)
+          z[lam] += zj;
+        else
+          z[lam] = zj;
+        pa.slot_z[ts0 + rsl] = zj;
+        if (!dir) part += sY[rsl] * zj;
+      }
+      __syncthreads();
+    }
+  } else
   for (int lv = 0; lv < nl; ++lv) {  // root level first: z_j = (J_j + g_par z_par) / D_j
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
       const int sl = j - ts0;
@@ -4753,6 +4835,21 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
 // rtol, a second graph applies one step of iterative refinement (residual -> direct solve
 // -> x += correction; ~1e-15 after it). Returns NX_OK with *converged = 0 if that is still
 // above rtol (the caller runs MINRES). RCCL that refuses the capture: eager launches.
+// One rank: the direct solve's five kernels are launched directly by default -- from an
+// idle stream the first starts ~3 us after the call and the host enqueues the rest while
+// it runs, where a graph replay costs ~10 us of fixed host time (C3: 0.0708 vs 0.0739
+// ms/step, r02n A/B). NXHIP_DIR_GRAPH=1 replays a graph instead. Several ranks: graphs.
+// (Measured and kept out: the down sweep's last workgroup publishing through an atomic
+// ticket instead of k_dir_publish_fr -- 0.079 vs 0.072 ms/step: every workgroup's release
+// fence writes back its XCD's L2, dirty with x, before the ticket.)
+int dir_graph_flag() {
+  static const int f = [] {
+    const char* e = std::getenv("NXHIP_DIR_GRAPH");
+    return (e != nullptr && std::atoi(e) != 0) ? 1 : 0;
+  }();
+  return f;
+}
+
 int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
                  int32_t* converged) {
   const bool multi = team_multi(t);
@@ -4790,7 +4887,8 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     if (asmb) CHECK(launch_assembly(h, 1, 1));
     return launch_direct(h, rtol, refine);
   };
-  const bool graphs = !h->comm || h->rccl_graph_ok;
+  // one rank: graph replay or the five launches issued directly (NXHIP_DIR_GRAPH)
+  const bool graphs = (!h->comm || h->rccl_graph_ok) && (multi || dir_graph_flag());
   auto run = [&](hipGraphExec_t* exec, hipGraph_t* graph, int* len, double* grtol, int key,
                  int refine, bool asmb) -> int {
     if (graphs && (!*exec || *grtol != rtol || *len != key)) {
@@ -5725,6 +5823,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     h->fres_ok = pa.slot_rloc && h->d_left && pa.rpart && h->dir_bb && h->tmp;
     if (const char* e = std::getenv("NXHIP_DIR_FRES")) h->fres_ok = h->fres_ok && std::atoi(e) != 0;
   }
+  pa.top_reg = 1;
+  if (const char* e = std::getenv("NXHIP_TOP_REG")) pa.top_reg = std::atoi(e) != 0;
   h->pc_lds = lds;
   h->pa = pa;
   h->pc_jobs = n_jobs;

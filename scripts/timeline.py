@@ -3,7 +3,8 @@
 kernel start offsets, durations and the idle gaps between consecutive dispatches.
 
 Usage: python scripts/timeline.py gpurun_out/prof_<tag>/trace/trace_kernel_trace.csv [anchor]
-(anchor = the kernel that starts a step, default k_assemble)
+(anchor = the kernel that starts a step, default k_assemble; optional third argument:
+the index of the anchor that starts the step to print)
 """
 
 import csv
@@ -22,7 +23,11 @@ def main() -> None:
     starts = [i for i, k in enumerate(ks) if k[2] == anchor]
     # a full timed step: between the third- and second-to-last anchors (the last one is
     # the bench's profiled step)
-    i0, i1 = starts[-3], starts[-2]
+    if len(sys.argv) > 3:  # explicit step index (the n-th anchor)
+        k = int(sys.argv[3])
+        i0, i1 = starts[k], starts[k + 1]
+    else:
+        i0, i1 = starts[-3], starts[-2]
     t0 = ks[i0][0]
     prev_end = t0
     busy = 0
