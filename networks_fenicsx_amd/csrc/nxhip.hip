@@ -1067,6 +1067,7 @@ struct PcArgs {
   double* rres;   // r (kept for a refinement step)
   double* rpart;  // per job: partial ||r||^2, then (n_jobs on) partial ||b||^2
   int top_reg;    // k_pc_top_lds: register level sweeps allowed (NXHIP_TOP_REG)
+  int topdown;    // one rank, direct: the top part solved in every down sweep workgroup
 };
 
 constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve in LDS
@@ -2021,20 +2022,32 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   if (MULTI && dense && pa.fused) pc_cpart_last(pa, sAtop);
 }
 
+// LDS of the top part's solve (k_pc_top_lds; with pa.topdown also every direct down sweep)
+struct TopLds {
+  double *sD0, *sJ0, *sD, *sJ, *sGp, *sY;
+  int *sPar, *sLam, *sOff, *sChild;
+  double *sG, *sDD, *sDJ;
+  int* sLv;
+};
+
+// The top part's elimination and back-substitution (one workgroup of kTopThreads). down = 1:
+// run inside a direct down sweep (pa.topdown, one rank): the top values stay in LDS (sJ0)
+// for the workgroup's own chains, workgroup 0 stores them in slot_z (k_dir_publish_fr moves
+// them into x after the sweep), nothing else is written.
 template <bool MULTI>
-__global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* __restrict__ y,
-                                                            const double* __restrict__ r2,
-                                                            double* __restrict__ z,
-                                                            const MrState* __restrict__ st,
-                                                            const double* __restrict__ partA,
-                                                            int nA, const double* __restrict__ red,
-                                                            double* __restrict__ partB, int mode) {
-  __shared__ double sD0[kCapT], sJ0[kCapT], sD[kCapT], sJ[kCapT], sGp[kCapT], sY[kCapT];
-  __shared__ int sPar[kCapT], sLam[kCapT];
-  __shared__ int sOff[kCapT + 1];
-  __shared__ int sChild[kCapTDC];
-  __shared__ double sG[kCapTDC], sDD[kCapTDC], sDJ[kCapTDC];
-  __shared__ int sLv[kMaxTopLvl + 1];
+__device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ y,
+                                         const double* __restrict__ r2, double* __restrict__ z,
+                                         const MrState* __restrict__ st,
+                                         const double* __restrict__ partA, int nA,
+                                         const double* __restrict__ red,
+                                         double* __restrict__ partB, int mode, const TopLds& L,
+                                         bool down) {
+  // no contraction: the kernel and every down workgroup (topdown) must agree bit for bit
+#pragma clang fp contract(off)
+  double *sD0 = L.sD0, *sJ0 = L.sJ0, *sD = L.sD, *sJ = L.sJ, *sGp = L.sGp, *sY = L.sY;
+  int *sPar = L.sPar, *sLam = L.sLam, *sOff = L.sOff, *sChild = L.sChild;
+  double *sG = L.sG, *sDD = L.sDD, *sDJ = L.sDJ;
+  int* sLv = L.sLv;
   double c2 = 0.0;
   const bool upd = mode == 0 && !(MULTI && pa.lin);
   // static indices of the first pass of phases A1 / A2, loaded before the stop test and
@@ -2231,11 +2244,13 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
         const double num = rJ + (p >= 0 ? gp * sJ0[p] : 0.0);
         const double zj = dir ? num * riv : num / rD;
         sJ0[rsl] = zj;  // reuse: z of top slots
-        if (dir && pa.accum)
-          z[lam] += zj;
-        else
-          z[lam] = zj;
-        pa.slot_z[ts0 + rsl] = zj;
+        if (!down) {
+          if (dir && pa.accum)
+            z[lam] += zj;
+          else
+            z[lam] = zj;
+        }
+        if (!down || blockIdx.x == 0) pa.slot_z[ts0 + rsl] = zj;
         if (!dir) part += sY[rsl] * zj;
       }
       __syncthreads();
@@ -2248,22 +2263,48 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
       const double num = sJ[sl] + (p >= 0 ? sGp[sl] * sJ0[p] : 0.0);
       const double zj = dir ? num * sY[sl] : num / sD[sl];
       sJ0[sl] = zj;  // reuse: z of top slots
-      if (dir && pa.accum)
-        z[sLam[sl]] += zj;
-      else
-        z[sLam[sl]] = zj;
-      pa.slot_z[ts0 + sl] = zj;
+      if (!down) {
+        if (dir && pa.accum)
+          z[sLam[sl]] += zj;
+        else
+          z[sLam[sl]] = zj;
+      }
+      if (!down || blockIdx.x == 0) pa.slot_z[ts0 + sl] = zj;
       if (!dir) part += sY[sl] * zj;
     }
     __syncthreads();
   }
   NX_PHASE(36);
+  if (down) {
+    __syncthreads();  // the top values (sJ0) for the caller's chains
+    return;
+  }
   for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {  // lower-job roots read these
     pa.slot_D[ts0 + sl] = sD[sl];
     pa.slot_J[ts0 + sl] = sJ[sl];
   }
   if (!dir) block_sum_store_n<kTopThreads>(part, partB + pa.n_jobs);
   NX_PHASE_END(32);
+}
+
+
+template <bool MULTI>
+__global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* __restrict__ y,
+                                                            const double* __restrict__ r2,
+                                                            double* __restrict__ z,
+                                                            const MrState* __restrict__ st,
+                                                            const double* __restrict__ partA,
+                                                            int nA, const double* __restrict__ red,
+                                                            double* __restrict__ partB, int mode) {
+  __shared__ double sD0[kCapT], sJ0[kCapT], sD[kCapT], sJ[kCapT], sGp[kCapT], sY[kCapT];
+  __shared__ int sPar[kCapT], sLam[kCapT];
+  __shared__ int sOff[kCapT + 1];
+  __shared__ int sChild[kCapTDC];
+  __shared__ double sG[kCapTDC], sDD[kCapTDC], sDJ[kCapTDC];
+  __shared__ int sLv[kMaxTopLvl + 1];
+  top_body<MULTI>(pa, y, r2, z, st, partA, nA, red, partB, mode,
+                  TopLds{sD0, sJ0, sD, sJ, sGp, sY, sPar, sLam, sOff, sChild, sG, sDD, sDJ, sLv},
+                  false);
 }
 
 template <int BS>
@@ -2347,11 +2388,18 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int mode = DIRK ? kModeDirect : mode_in;
   __shared__ double sZ[kCapS], sA[kCapS], sB[kCapS];
   __shared__ int sP[kCapS];
-  __shared__ double sTa[kCapT];  // dense top: a_s of every top slot
+  constexpr int kCT = DIRK ? 1 : kCapT;  // MINRES-only arrays (dense top, start's prep)
+  __shared__ double sTa[kCT];  // dense top: a_s of every top slot
   __shared__ int sNs[kMaxNeed];
   __shared__ double sNz[kMaxNeed];
-  __shared__ double sGz[kCapT], sGt[kCapT], sGd[kCapT];  // start only: G columns (prep)
-  __shared__ int sGp[kCapT], sGc[kCapT];
+  __shared__ double sGz[kCT], sGt[kCT], sGd[kCT];  // start only: G columns (prep)
+  __shared__ int sGp[kCT], sGc[kCT];
+  // one rank, direct (pa.topdown): the top part's solve in every workgroup (top_body)
+  constexpr int kTT = DIRK && !MULTI ? kCapT : 1, kTD = DIRK && !MULTI ? kCapTDC : 1;
+  __shared__ double tD0[kTT], tJ0[kTT], tD[kTT], tJ[kTT], tGp[kTT], tY[kTT];
+  __shared__ int tPar[kTT], tLam[kTT], tOff[kTT + 1], tChild[kTD];
+  __shared__ double tG[kTD], tDD[kTD], tDJ[kTD];
+  __shared__ int tLv[DIRK && !MULTI ? kMaxTopLvl + 1 : 1];
   __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
   __shared__ double sQt[DIRK ? kCapC : 1], sQb[DIRK ? kCapC : 1];  // fused residual
@@ -2403,6 +2451,16 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   }
   if (mode == 0 && st->done) return;  // after the prefetch (nothing written before)
   const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
+  // one rank, direct: the top part solved here (k_pc_top_lds's work, same arithmetic) while
+  // the prefetch above is in flight; its values stay in LDS (tJ0, by top position)
+  const bool tdir = DIRK && !MULTI && pa.topdown;
+  const int tts0 = tdir ? pa.top_lvl_off[0] : 0;
+  if constexpr (DIRK && !MULTI) {
+    if (tdir)
+      top_body<false>(pa, y, r2, z, st, nullptr, 0, nullptr, nullptr, kModeDirect,
+                      TopLds{tD0, tJ0, tD, tJ, tGp, tY, tPar, tLam, tOff, tChild, tG, tDD, tDJ, tLv},
+                      true);
+  }
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
   // several ranks, fused: every workgroup solves the coarse forest (k_pc_coarse's job)
@@ -2483,6 +2541,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     if (blockIdx.x == 0 && threadIdx.x == 0) partB[pa.n_jobs] = 0.0;  // no top kernel
   }
   auto outside = [&](int t) -> double {  // value of a top slot (outside this job)
+    if (tdir) return tJ0[t - tts0];
     if (!dense) return pa.slot_z[t];
     double v = 0.0;
     for (int k = 0; k < nneed; ++k)
@@ -2649,8 +2708,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
             rqN = pa.rhs_b[ch.dof_qN];
             xv[CPL] = z[ch.dof_qN];
           }
-          zt = up < 0 ? 0.0 : z[pa.slot_lam[up]];
-          zb = lo < 0 ? 0.0 : z[pa.slot_lam[lo]];
+          // (topdown: the top slots' x is refined by k_dir_publish_fr after this sweep, so
+          // their refined value is formed here as x + d, the same single addition)
+          zt = up < 0 ? 0.0 : z[pa.slot_lam[up]] + (tdir && (up < js0 || up >= js1) ? zt : 0.0);
+          zb = lo < 0 ? 0.0 : z[pa.slot_lam[lo]] + (tdir && (lo < js0 || lo >= js1) ? zb : 0.0);
         }
         direct_residual<W, CPL>(pa, ch, active, flip, bcv, rq, rqN, zc, xv, zt, zb, mo_r, rr, bb,
                                 sQt, sQb, c - c0);
@@ -3387,9 +3448,19 @@ __global__ __launch_bounds__(kReduceThreads) void k_dir_publish(const double* __
 // first pass (bbst); a refinement pass (refine = 1) reuses it.
 __global__ __launch_bounds__(kReduceThreads) void k_dir_publish_fr(
     const double* __restrict__ rpart, int nj, const int* __restrict__ left, int nleft, Csr A,
-    const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ rres,
-    double* __restrict__ bbst, int refine, double rtol, int* seq, MrState* mirror) {
+    double* __restrict__ x, const double* __restrict__ b, double* __restrict__ rres,
+    double* __restrict__ bbst, int refine, double rtol, int* seq, MrState* mirror,
+    const int* __restrict__ top_lam, const double* __restrict__ top_z, int ntop) {
 #pragma clang fp contract(off)
+  // topdown: the top part's values (solved in every down workgroup, workgroup 0's copy in
+  // slot_z) into x; the rows below read flux values only (multiplier rows)
+  for (int i = threadIdx.x; i < ntop; i += kReduceThreads) {
+    const int lam = top_lam[i];
+    if (refine)
+      x[lam] += top_z[i];
+    else
+      x[lam] = top_z[i];
+  }
   __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
   double rr = 0.0, bb = 0.0;
   for (int i = threadIdx.x; i < nj; i += kReduceThreads) {
@@ -3607,6 +3678,7 @@ struct nx_network {
   // direct solve, one rank: the residual check fused into the down sweep (PcArgs::fres);
   // the rows it cannot form (left, n_left) and ||b||^2 of the first pass (dir_bb)
   bool fres_ok = false;
+  int top_ts0 = 0, top_nt = 0;  // the top part's slots (host copy of top_lvl_off's ends)
   int* d_left = nullptr;
   int n_left = 0;
   double* dir_bb = nullptr;
@@ -3821,7 +3893,8 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
       if (MULTI && h->pa.mdense && mode == 0) {  // dense top: the coarse partials only
         if (!h->pa.fused)  // else the up sweep's last workgroup computes them
           hipLaunchKernelGGL(k_pc_cpart, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, st, mode);
-      } else if (!(!MULTI && h->pa.dense && mode == 0))  // dense top: k_pc_down_lds does it
+      } else if (!(!MULTI && h->pa.dense && mode == 0) &&  // dense top: k_pc_down_lds does it
+                 !(!MULTI && h->pa.topdown && mode == kModeDirect))  // so does topdown
         hipExtLaunchKernelGGL((k_pc_top_lds<MULTI>), dim3(1), dim3(kTopThreads), 0, h->stream, e[2],
                               e[3], 0, h->pa, y, r2, z, st, h->partA, h->nA, h->red, h->partB, mode);
     } else {
@@ -4687,6 +4760,14 @@ LeanGraphs& lean_of(const Team& t) { return t.g ? t.g->lean : t.hs[0]->lean; }
 // refine = 0: x = A^{-1} b; refine = 1: one step of iterative refinement, x += A^{-1} r with
 // r = b - A x as the previous pass's residual check left it in tmp. Both end with the true
 // residual (r kept in tmp again) published.
+int top_down_flag() {
+  static const int f = [] {
+    const char* e = std::getenv("NXHIP_TOP_DOWN");
+    return (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
+  }();
+  return f;
+}
+
 template <int W, int CPL>
 void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const hipEvent_t* evs = prof ? h->dev : nullptr;
@@ -4699,15 +4780,21 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
     h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
     h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the residual check
+    // and every down workgroup the top part (no k_pc_top_lds; NXHIP_TOP_DOWN=0 keeps it)
+    const bool td = h->fres_ok && h->top_nt > 0 && top_down_flag();
+    h->pa.topdown = td ? 1 : 0;
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, h->x, evs);
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, h->x, evs);
     h->pa.accum = 0;
     h->pa.fres = 0;
+    h->pa.topdown = 0;
     if (h->fres_ok) {
+      const int ntop = td ? h->top_nt : 0;
       hipExtLaunchKernelGGL(k_dir_publish_fr, dim3(1), dim3(kReduceThreads), 0, h->stream,
                             prof ? h->dev[6] : nullptr, prof ? h->dev[7] : nullptr, 0, h->pa.rpart,
                             h->pc_jobs, h->d_left, h->n_left, csr_of(h), h->x, h->rhs, h->tmp,
-                            h->dir_bb, refine, rtol, h->d_seq, h->d_last);
+                            h->dir_bb, refine, rtol, h->d_seq, h->d_last,
+                            h->pa.slot_lam + h->top_ts0, h->pa.slot_z + h->top_ts0, ntop);
       return;
     }
   } else {
@@ -4866,8 +4953,12 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     for (int k = 0; k < 4; ++k) {
       if (k < 3 && !fused) continue;
       float ms = 0.f;
+      if (k == 1 && fused && h->fres_ok && h->top_nt > 0 && top_down_flag())
+        continue;  // no k_pc_top_lds dispatch (topdown): its events were not recorded
       if (hipEventElapsedTime(&ms, h->dev[2 * k], h->dev[2 * k + 1]) == hipSuccess)
         h->dir_ms[k] += ms;
+      else
+        (void)hipGetLastError();  // an event pair this solve did not record
     }
     h->dir_cnt += 1;
     const MrState s = *h->h_last;
@@ -5703,6 +5794,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.lvl_slot_off = up(lvl_slot_off, n_lvl + 1);
   pa.top_lvl_off = up(top_lvl_off, n_top_lvl + 1);
   pa.n_top_lvl = n_top_lvl;
+  h->top_ts0 = top_lvl_off[0];
+  h->top_nt = top_lvl_off[n_top_lvl] - top_lvl_off[0];
   pa.n_jobs = n_jobs;
   pa.n_dc_all = (int)slot_dc_off[n_slots];
   pa.n_slots_all = (int)n_slots;
