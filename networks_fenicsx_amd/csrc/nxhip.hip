@@ -1078,27 +1078,63 @@ constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve 
 template <int BS>
 __device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const double* sD,
                                    const double* sJ) {
-  const int nC = pa.n_coarse;
-  for (int i = threadIdx.x; i < 3 * nC; i += BS) pa.cbuf[i] = 0.0;
+  // small coarse sets: the buffer is built in LDS and the coarse chains' data loaded in
+  // parallel (thread = chain) before one thread sums them in a fixed order, then copied out
+  // (was: built in global memory, two dependent round trips plus a read-modify-write per
+  // chain on thread 0 -- ~14 us on the ranks holding the tree's upper part, 8-rank rehearsal)
+  constexpr int kCapCC = 256;
+  __shared__ double sBuf[3 * kCapCC], sCg[kCapCC], sCit[kCapCC], sCib[kCapCC];
+  __shared__ int sCt[kCapCC], sCb[kCapCC];
+  const int nC = pa.n_coarse, ncc = pa.n_cc;
+  const bool lds = nC <= kCapCC && ncc <= kCapCC;
+  double* __restrict__ buf = lds ? sBuf : pa.cbuf;
+  for (int i = threadIdx.x; i < 3 * nC; i += BS) buf[i] = 0.0;
   __syncthreads();
   for (int sl = threadIdx.x; sl < nt; sl += BS) {
     const int k = pa.slot_cidx[ts0 + sl];
     if (k >= 0) {
-      pa.cbuf[k] = sD[sl];
-      pa.cbuf[nC + k] = sJ[sl];
+      buf[k] = sD[sl];
+      buf[nC + k] = sJ[sl];
     }
   }
+  if (lds)
+    for (int i = threadIdx.x; i < ncc; i += BS) {
+      const int c = pa.cc_chain[i];
+      sCt[i] = pa.cc_top[i];
+      sCb[i] = pa.cc_bot[i];
+      sCg[i] = 1.0 / pa.chain_T[c];
+      sCit[i] = pa.chain_It[c];
+      sCib[i] = pa.chain_Ib[c];
+    }
   __syncthreads();
   if (threadIdx.x == 0) {  // few chains; serial keeps the sums in a fixed order
-    for (int i = 0; i < pa.n_cc; ++i) {
-      const int c = pa.cc_chain[i], t = pa.cc_top[i], b = pa.cc_bot[i];
-      const double g = 1.0 / pa.chain_T[c];
-      pa.cbuf[t] += g;
-      pa.cbuf[b] += g;
-      pa.cbuf[nC + t] += pa.chain_It[c];
-      pa.cbuf[nC + b] += pa.chain_Ib[c];
-      pa.cbuf[2 * nC + b] = g;
+    for (int i = 0; i < ncc; ++i) {
+      int t, b;
+      double g, it, ib;
+      if (lds) {
+        t = sCt[i];
+        b = sCb[i];
+        g = sCg[i];
+        it = sCit[i];
+        ib = sCib[i];
+      } else {
+        const int c = pa.cc_chain[i];
+        t = pa.cc_top[i];
+        b = pa.cc_bot[i];
+        g = 1.0 / pa.chain_T[c];
+        it = pa.chain_It[c];
+        ib = pa.chain_Ib[c];
+      }
+      buf[t] += g;
+      buf[b] += g;
+      buf[nC + t] += it;
+      buf[nC + b] += ib;
+      buf[2 * nC + b] = g;
     }
+  }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * nC; i += BS) pa.cbuf[i] = sBuf[i];
   }
 }
 
@@ -2332,6 +2368,54 @@ __device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* 
   __syncthreads();
   for (int i = threadIdx.x; i < sCo[nC]; i += kPcThreads) sCc[i] = pa.c_child[i];
   __syncthreads();
+  // register sweeps (thread = coarse junction, <= kWaveKids children): its level, children
+  // and their g in registers, one LDS round trip per level for the children's D, J and
+  // the two divisions; same arithmetic in the same order as the loops below
+  const int cj = threadIdx.x;
+  const bool cmine = cj < nC;
+  int clv = -1, cnk = 0, cch[kWaveKids];
+#pragma unroll
+  for (int k = 0; k < kWaveKids; ++k) cch[k] = 0;
+  if (cmine) {
+    for (int q = 0; q < nl; ++q)
+      if (cj >= sCl[q] && cj < sCl[q + 1]) clv = q;
+    for (int i = sCo[cj]; i < sCo[cj + 1]; ++i) {
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k)
+        if (k == cnk) cch[k] = sCc[i];
+      ++cnk;
+    }
+  }
+  if (nC <= kPcThreads && __syncthreads_or(cnk > kWaveKids) == 0) {
+    double D = cmine ? sD[cj] : 1.0, J = cmine ? sJ[cj] : 0.0;
+    for (int lv = nl - 1; lv >= 0; --lv) {
+      if (clv == lv) {
+        double g[kWaveKids], dk[kWaveKids], jk[kWaveKids];
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          g[k] = k < cnk ? sCg[cch[k]] : 0.0;
+          dk[k] = k < cnk ? sD[cch[k]] : 1.0;
+          jk[k] = k < cnk ? sJ[cch[k]] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          if (k >= cnk) break;
+          D -= g[k] * g[k] / dk[k];
+          J += g[k] * jk[k] / dk[k];
+        }
+        sD[cj] = D;
+        sJ[cj] = J;
+      }
+      __syncthreads();
+    }
+    const int p = cmine ? sCp[cj] : -1;
+    const double gp = cmine ? sCg[cj] : 0.0;
+    for (int lv = 0; lv < nl; ++lv) {  // root level first
+      if (clv == lv) sZc[cj] = (J + (p >= 0 ? gp * sZc[p] : 0.0)) / D;
+      __syncthreads();
+    }
+    return;
+  }
   for (int lv = nl - 1; lv >= 0; --lv) {  // deepest level first
     for (int j = sCl[lv] + threadIdx.x; j < sCl[lv + 1]; j += kPcThreads) {
       double D = sD[j], J = sJ[j];
@@ -3054,6 +3138,7 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __
                                                            double* __restrict__ partB, int mode) {
   __shared__ double sD[kCapCoarse], sJ[kCapCoarse], sZ[kCapCoarse];
   __shared__ int sTp[kTopThreads], sTl[kTopThreads];  // top slot: parent (local) or -2 - coarse index; lambda
+  __shared__ int sTlv[kMaxTopLvl + 1];  // the top levels' slot offsets
   if (mode == 0 && st->done) return;
   // linear form: alpha arrived with the coarse partials; the Lanczos step is completed here
   double c2 = 0.0;
@@ -3077,10 +3162,14 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __
   const int sl0 = threadIdx.x;
   int t_k = -1, t_lam = 0, t_par = -1;
   double t_J = 0.0, t_D = 1.0, t_T = 1.0;
+  // the top levels' offsets (thread <= ntl), staged in LDS after the coarse solve
+  const int t_lvo = staged && (int)threadIdx.x <= ntl && ntl <= kMaxTopLvl ? pa.top_lvl_off[threadIdx.x] : 0;
+  double t_y = 0.0;  // y at this slot's multiplier (finish)
   if (staged && sl0 < nt) {
     const int j = ts0 + sl0;
     t_k = pa.slot_cidx[j];
     t_lam = pa.slot_lam[j];
+    t_y = y[t_lam];
     if (t_k < 0) {
       t_par = pa.slot_parent[j];
       t_J = pa.slot_J[j];
@@ -3125,9 +3214,9 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __
     return;
   }
   double part = 0.0;
-  auto finish = [&](int j, int lam, double zj) {
+  auto finish = [&](int j, int lam, double zj, bool pre = false) {
     pa.slot_z[j] = zj;
-    double yl = y[lam];
+    double yl = pre ? t_y : y[lam];
     if (lin) {  // ghost slots: y = r2 = 0 and the halo overwrites z
       zj -= c2 * z[lam];
       yl -= c2 * r2[lam];
@@ -3151,7 +3240,30 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_coarse(PcArgs pa, double* __
       sTp[sl0] = t_k >= 0 ? -2 - t_k : (t_par >= 0 ? t_par - ts0 : -1);
       sTl[sl0] = t_lam;
     }
+    if ((int)threadIdx.x <= ntl && ntl <= kMaxTopLvl) sTlv[threadIdx.x] = t_lvo;
     __syncthreads();
+    if (ntl <= kMaxTopLvl) {  // thread = slot: its level and inputs in registers
+      int mylv = -1;
+      if (sl0 < nt)
+        for (int q = 0; q < ntl; ++q)
+          if (ts0 + sl0 >= sTlv[q] && ts0 + sl0 < sTlv[q + 1]) mylv = q;
+      const int p = t_k >= 0 ? -2 - t_k : (t_par >= 0 ? t_par - ts0 : -1);
+      for (int lv = 0; lv < ntl; ++lv) {
+        if (mylv == lv) {
+          double zj;
+          if (p <= -2) {
+            zj = sZ[-2 - p];
+          } else {
+            double num = t_J;
+            if (p >= 0) num += sTZ[p] / t_T;
+            zj = num / t_D;
+          }
+          sTZ[sl0] = zj;
+          finish(ts0 + sl0, t_lam, zj, true);
+        }
+        __syncthreads();
+      }
+    } else
     for (int lv = 0; lv < ntl; ++lv) {
       for (int j = pa.top_lvl_off[lv] + threadIdx.x; j < pa.top_lvl_off[lv + 1]; j += kTopThreads) {
         const int sl = j - ts0;
