@@ -1068,6 +1068,7 @@ struct PcArgs {
   double* rpart;  // per job: partial ||r||^2, then (n_jobs on) partial ||b||^2
   int top_reg;    // k_pc_top_lds: register level sweeps allowed (NXHIP_TOP_REG)
   int topdown;    // one rank, direct: the top part solved in every down sweep workgroup
+  int top_ts0, top_nt, top_dc0, top_ndc;  // the top part's slots and hanging-chain entries
 };
 
 constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve in LDS
@@ -2066,6 +2067,41 @@ struct TopLds {
   int* sLv;
 };
 
+// This thread's first entries of the top part's phases A1 (hanging chain tid) and A2 (slot
+// tid): indices (top_pre_idx, one round trip: the top part's extent is host-known, PcArgs
+// top_*) and the values they point at (top_pre_val, one more), so a caller can issue both
+// among its own loads (the direct down sweep: beside its chain prefetch).
+struct TopPre {
+  int c, lo, lam, pcn, par, off;
+  double T, It, Dl, Jl, y, Tp, Ib;
+};
+
+__device__ __forceinline__ void top_pre_idx(const PcArgs& pa, TopPre& p) {
+  const int tid = threadIdx.x;
+  const int ts0 = pa.top_ts0, nt = pa.top_nt, dc0 = pa.top_dc0, ndc = pa.top_ndc;
+  p.c = tid < ndc ? pa.slot_dc[dc0 + tid] : 0;
+  p.lo = tid < ndc ? pa.dc_lo[dc0 + tid] : -1;
+  p.lam = tid < nt ? pa.slot_lam[ts0 + tid] : 0;
+  p.pcn = tid < nt ? pa.slot_pchain[ts0 + tid] : -1;
+  p.par = tid < nt ? pa.slot_parent[ts0 + tid] : -1;
+  p.off = tid < nt ? pa.slot_dc_off[ts0 + tid] : 0;
+}
+
+__device__ __forceinline__ void top_pre_val(const PcArgs& pa, const double* __restrict__ y,
+                                            TopPre& p) {
+  const int tid = threadIdx.x;
+  const int ts0 = pa.top_ts0, ts1 = pa.top_ts0 + pa.top_nt;
+  const bool dc = tid < pa.top_ndc, sl = tid < pa.top_nt;
+  const bool low = dc && p.lo >= 0 && !(p.lo >= ts0 && p.lo < ts1);  // a lower job's root
+  p.T = dc ? pa.chain_T[p.c] : 1.0;
+  p.It = dc ? pa.chain_It[p.c] : 0.0;
+  p.Dl = low ? pa.slot_D[p.lo] : 1.0;
+  p.Jl = low ? pa.slot_J[p.lo] : 0.0;
+  p.y = sl ? y[p.lam] : 0.0;
+  p.Tp = sl && p.pcn >= 0 ? pa.chain_T[p.pcn] : 1.0;
+  p.Ib = sl && p.pcn >= 0 ? pa.chain_Ib[p.pcn] : 0.0;
+}
+
 // The top part's elimination and back-substitution (one workgroup of kTopThreads). down = 1:
 // run inside a direct down sweep (pa.topdown, one rank): the top values stay in LDS (sJ0)
 // for the workgroup's own chains, workgroup 0 stores them in slot_z (k_dir_publish_fr moves
@@ -2077,7 +2113,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
                                          const double* __restrict__ partA, int nA,
                                          const double* __restrict__ red,
                                          double* __restrict__ partB, int mode, const TopLds& L,
-                                         bool down) {
+                                         bool down, const TopPre& pre_in) {
   // no contraction: the kernel and every down workgroup (topdown) must agree bit for bit
 #pragma clang fp contract(off)
   double *sD0 = L.sD0, *sJ0 = L.sJ0, *sD = L.sD, *sJ = L.sJ, *sGp = L.sGp, *sY = L.sY;
@@ -2086,20 +2122,15 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
   int* sLv = L.sLv;
   double c2 = 0.0;
   const bool upd = mode == 0 && !(MULTI && pa.lin);
-  // static indices of the first pass of phases A1 / A2, loaded before the stop test and
-  // alpha's re-reduction (they only depend on the decomposition)
+  // the first pass of phases A1 / A2 comes prefetched (top_pre_idx / top_pre_val, issued
+  // by the caller before the stop test and alpha's re-reduction)
   const int nl = pa.n_top_lvl;
-  const int ts0 = pa.top_lvl_off[0], ts1 = pa.top_lvl_off[nl];
-  const int nt = ts1 - ts0;
-  const int dc0 = nt > 0 ? pa.slot_dc_off[ts0] : 0;
-  const int ndc = nt > 0 ? pa.slot_dc_off[ts1] - dc0 : 0;
+  const int ts0 = pa.top_ts0, nt = pa.top_nt, ts1 = ts0 + nt;
+  const int dc0 = pa.top_dc0, ndc = pa.top_ndc;
   const int tid = threadIdx.x;
-  const int p_c = tid < ndc ? pa.slot_dc[dc0 + tid] : 0;
-  const int p_lo = tid < ndc ? pa.dc_lo[dc0 + tid] : -1;
-  const int p_lam = tid < nt ? pa.slot_lam[ts0 + tid] : 0;
-  const int p_pcn = tid < nt ? pa.slot_pchain[ts0 + tid] : -1;
-  const int p_par = tid < nt ? pa.slot_parent[ts0 + tid] : -1;
-  const int p_off = tid < nt ? pa.slot_dc_off[ts0 + tid] : 0;
+  const TopPre& pre_ = pre_in;
+  const int p_c = pre_.c, p_lo = pre_.lo, p_lam = pre_.lam, p_pcn = pre_.pcn, p_par = pre_.par,
+            p_off = pre_.off;
   if (mode == 0) {
     if (st->done) return;
     if (upd) {
@@ -2115,16 +2146,16 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     const bool pre = i == tid;
     const int c = pre ? p_c : pa.slot_dc[dc0 + i];
     const int lo = pre ? p_lo : pa.dc_lo[dc0 + i];
-    const double g = 1.0 / pa.chain_T[c];
-    const double it = pa.chain_It[c];
+    const double g = 1.0 / (pre ? pre_.T : pa.chain_T[c]);
+    const double it = pre ? pre_.It : pa.chain_It[c];
     int child = -1;
     double dD = 0.0, dJ = it;
     if (lo >= ts0 && lo < ts1) {  // child above the cut: solved in the level sweep
       child = lo - ts0;
     } else if (lo >= 0) {
-      const double Dl = pa.slot_D[lo];
+      const double Dl = pre ? pre_.Dl : pa.slot_D[lo];
       dD = g * (1.0 - g / Dl);
-      dJ += g * pa.slot_J[lo] / Dl;
+      dJ += g * (pre ? pre_.Jl : pa.slot_J[lo]) / Dl;
     } else {
       dD = g;
     }
@@ -2138,7 +2169,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     const int j = ts0 + sl;
     const bool pre = sl == tid;
     const int lam = pre ? p_lam : pa.slot_lam[j];
-    double yl = y[lam];
+    double yl = pre ? pre_.y : y[lam];
     if (upd) {
       yl -= c2 * r2[lam];
       y[lam] = yl;
@@ -2147,9 +2178,9 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     sLam[sl] = lam;
     sY[sl] = yl;
     const int pcn = pre ? p_pcn : pa.slot_pchain[j];
-    const double gp = pcn >= 0 ? 1.0 / pa.chain_T[pcn] : 0.0;
+    const double gp = pcn >= 0 ? 1.0 / (pre ? pre_.Tp : pa.chain_T[pcn]) : 0.0;
     sD0[sl] = gp;
-    sJ0[sl] = yl + (pcn >= 0 ? pa.chain_Ib[pcn] : 0.0);
+    sJ0[sl] = yl + (pcn >= 0 ? (pre ? pre_.Ib : pa.chain_Ib[pcn]) : 0.0);
     const int par = pre ? p_par : pa.slot_parent[j];
     sPar[sl] = par >= 0 ? par - ts0 : -1;
     sGp[sl] = gp;
@@ -2338,9 +2369,12 @@ __global__ __launch_bounds__(kTopThreads) void k_pc_top_lds(PcArgs pa, double* _
   __shared__ int sChild[kCapTDC];
   __shared__ double sG[kCapTDC], sDD[kCapTDC], sDJ[kCapTDC];
   __shared__ int sLv[kMaxTopLvl + 1];
+  TopPre pre;
+  top_pre_idx(pa, pre);
+  top_pre_val(pa, y, pre);
   top_body<MULTI>(pa, y, r2, z, st, partA, nA, red, partB, mode,
                   TopLds{sD0, sJ0, sD, sJ, sGp, sY, sPar, sLam, sOff, sChild, sG, sDD, sDJ, sLv},
-                  false);
+                  false, pre);
 }
 
 template <int BS>
@@ -2506,6 +2540,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
   const int seg = threadIdx.x / W;
+  // one rank, direct (pa.topdown): the top part's first indices ahead of the chain prefetch
+  const bool tdir = DIRK && !MULTI && pa.topdown;
+  TopPre tpre{};
+  if (tdir) top_pre_idx(pa, tpre);
   ChainLane<W, CPL> ch;
   ch.setup(pa, c0 + seg, c0 + seg < c1);
   double vc[CPL], vq[CPL], vN = 0.0;
@@ -2533,17 +2571,17 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     p_lam = pa.slot_lam[j];
     p_y = y[p_lam];
   }
+  if (tdir) top_pre_val(pa, y, tpre);  // the values they point at, beside the job's own
   if (mode == 0 && st->done) return;  // after the prefetch (nothing written before)
   const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
   // one rank, direct: the top part solved here (k_pc_top_lds's work, same arithmetic) while
   // the prefetch above is in flight; its values stay in LDS (tJ0, by top position)
-  const bool tdir = DIRK && !MULTI && pa.topdown;
-  const int tts0 = tdir ? pa.top_lvl_off[0] : 0;
+  const int tts0 = pa.top_ts0;
   if constexpr (DIRK && !MULTI) {
     if (tdir)
       top_body<false>(pa, y, r2, z, st, nullptr, 0, nullptr, nullptr, kModeDirect,
                       TopLds{tD0, tJ0, tD, tJ, tGp, tY, tPar, tLam, tOff, tChild, tG, tDD, tDJ, tLv},
-                      true);
+                      true, tpre);
   }
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
@@ -5908,6 +5946,10 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.n_top_lvl = n_top_lvl;
   h->top_ts0 = top_lvl_off[0];
   h->top_nt = top_lvl_off[n_top_lvl] - top_lvl_off[0];
+  pa.top_ts0 = h->top_ts0;
+  pa.top_nt = h->top_nt;
+  pa.top_dc0 = h->top_nt > 0 ? slot_dc_off[h->top_ts0] : 0;
+  pa.top_ndc = h->top_nt > 0 ? slot_dc_off[h->top_ts0 + h->top_nt] - pa.top_dc0 : 0;
   pa.n_jobs = n_jobs;
   pa.n_dc_all = (int)slot_dc_off[n_slots];
   pa.n_slots_all = (int)n_slots;
