@@ -46,6 +46,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+PROF_STEPS = 20  # eager steps with HIP events bound to each dispatch (the roofline entries)
 METRIC = "assemble+solve ms and SpMV HBM GB/s, depth-14 tree, 1/2/4/8 GPU"
 
 
@@ -98,6 +99,7 @@ def direct_kernel_bytes(n: int, nnz: int, n_e: int, E: int, N: int, B: int, nblk
             "k_dir_publish_fr": 16 * n_jobs + n_left * (8 + 3 * 20 + 16),
             "k_pc_up_lds": 8 * n_e + dq + 24 * E + 8 * E + 64 * B,
             # + edge_x / R (56 B per edge) read, r stored at the edge DoFs and local multipliers
+            # (+ the top part's inputs, ~40 B per top slot and hanging chain: < 0.1 MB)
             "k_pc_down_lds": 8 * n_e + dq + 8 * n + 16 * E + 24 * B + 56 * E + 8 * n_e + 8 * B,
             "k_pc_top_lds": 64 * 1024,
             "k_assemble_seg": 8 * nnz + 8 * n + dq + 80 * E,
@@ -341,14 +343,18 @@ def run(args, world: int) -> int:
     default_workload = world == 1 and (levels, N) == (15, 15) and not args.no_pc
 
     def minres_roofline():
-        """k_mr_a: HIP events bound to its dispatches over one profiled MINRES step."""
+        """k_mr_a: HIP events bound to its dispatches over PROF_STEPS profiled MINRES steps
+        (after a warm one)."""
         h.set_profiling(True)
-        h.reset_profile()
         step(h)
+        h.reset_profile()
+        for _ in range(PROF_STEPS):
+            step(h)
         prof = h.profile()
         h.set_profiling(False)
         spmv_ms = prof["spmv_ms"] / max(prof["spmv_count"], 1)
-        nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on, max(int(prof["spmv_count"]), 1))
+        nbytes = mr_spmv_bytes(h.n_rows, h.nnz, pc_on,
+                               max(int(prof["spmv_count"]) // PROF_STEPS, 1))
         # beta^2 travels point-to-point with the halo, so the multi-rank k_mr_a is MULTI = false
         kname = f"k_mr_a<false, {str(pc_on).lower()}>"
         traffic, tsrc, rocprof_ns = (pmc_traffic(kname) if default_workload
@@ -366,11 +372,14 @@ def run(args, world: int) -> int:
                 "assembly_kernel_ms": prof["asm_ms"] / max(prof["asm_count"], 1)}
 
     def direct_roofline():
-        """The direct solve's kernels (events bound to each dispatch, one profiled step):
-        the dominant one by time is the roofline kernel; all are listed."""
+        """The direct solve's kernels (events bound to each dispatch, PROF_STEPS profiled
+        steps after a warm one): the dominant one by time is the roofline kernel; all are
+        listed."""
         h.set_profiling(True)
+        step(h)  # the first profiled step runs cold (~1.5x); not averaged
         h.reset_profile()
-        step(h)
+        for _ in range(PROF_STEPS):
+            step(h)
         pd = h.profile_direct()
         prof = h.profile()
         h.set_profiling(False)
@@ -400,8 +409,9 @@ def run(args, world: int) -> int:
                                      "part's multiplier rows, the published state)",
                  "k_pc_up_lds": "k_pc_up_lds<false, 8, 2> (direct mode: M^-1 b_q per chain, "
                                 "chain condensation, junction elimination)",
-                 "k_pc_down_lds": "k_pc_down_lds<false, 8, 2, true> (direct mode: back-"
-                                  "substitution, cells, conservative x_q, the fused residual)",
+                 "k_pc_down_lds": "k_pc_down_lds<false, 8, 2, true> (direct mode: the top "
+                                  "part's solve in every workgroup, back-substitution, cells, "
+                                  "conservative x_q, the fused residual)",
                  "k_pc_top_lds": "k_pc_top_lds<false> (junctions above the cut)",
                  "k_assemble_seg": "k_assemble_seg<16> (CSR values + rhs)"}
         # kernel names as scripts/summarize_profile.py writes them (short form)
