@@ -347,6 +347,18 @@ int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned c
                  int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
                  const int32_t* send_idx, const int32_t* recv_off);
 
+/* Several ranks, direct solve: the multiplier rows of the K cut bifurcations (incident
+ * edges on several ranks; one global order, the same on every rank) are completed inside
+ * the residual's all-reduce of [||r||^2, ||b||^2, r_cut[K]] instead of a halo of x and a
+ * second all-reduce -- the MPI ghost update + norm of the reference's solve
+ * (solver.py:128-132, assembly.py:363-367) in one collective.
+ *   lm_cut[n_lm]        per owned multiplier row (local order): its cut index or -1
+ *   gk_off[K+1], gk_row, gk_coef   per cut index owned by another rank: this rank's flux
+ *                       end rows at it and their coupling coefficient (+-1)
+ * NXHIP_DIR_CUT=0 keeps the halo path. Part of the ranks' schedule signature. */
+int nx_set_cut(nx_network_t* h, int32_t K, const int32_t* lm_cut, const int32_t* gk_off,
+               const int32_t* gk_row, const double* gk_coef);
+
 /* Ranks of the handle's RCCL communicator (ncclCommCount); without one, the rank count of
  * its halo plan (1 for a single-GPU handle). bench.py reports it next to the timing. */
 int nx_comm_count(nx_network_t* h, int32_t* nranks);

@@ -77,6 +77,7 @@ _SIGS = {
                                 _i32, _pi32]),
     "nx_comm_count": (C.c_int, [_h, _pi32]),
     "nx_set_halo": (C.c_int, [_h, _i32, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
+    "nx_set_cut": (C.c_int, [_h, _i32, _pi32, _pi32, _pi32, _pd]),
     "nx_set_pc_dense": (C.c_int, [_h, _i32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                   _pi32, _pi32, _pi32, _pi32]),
     "nx_set_pc_exact": (C.c_int, [_h, _i32]),
@@ -451,6 +452,17 @@ class Handle:
                                 _ptr(send_idx if send_idx.size else np.zeros(1, np.int32),
                                      C.c_int32),
                                 _ptr(recv_off, C.c_int32)))
+
+    def set_cut(self, n_cut: int, lm_cut, gk_off, gk_row, gk_coef) -> None:
+        """Cut bifurcations of a multi-rank problem (``nx_set_cut``): their multiplier rows
+        are completed inside the direct solve's residual all-reduce."""
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in (
+            (lm_cut, np.int32), (gk_off, np.int32), (gk_row, np.int32), (gk_coef, np.float64))]
+        arrs = [a if a.size else np.zeros(1, a.dtype) for a in arrs]
+        self._cut_keep = arrs
+        check(lib().nx_set_cut(self.ptr, int(n_cut), _ptr(arrs[0], C.c_int32),
+                               _ptr(arrs[1], C.c_int32), _ptr(arrs[2], C.c_int32),
+                               _ptr(arrs[3], C.c_double)))
 
     def comm_count(self) -> int:
         """Ranks of the RCCL communicator (``ncclCommCount``), else the plan's rank count."""

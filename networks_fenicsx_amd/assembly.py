@@ -336,11 +336,13 @@ class HydraulicNetworkAssembler:
         if isinstance(comm, GroupRankComm):  # in-process group: plan only (RankGroup)
             self._handle.set_halo(self._nranks, self._rank, lp.peers, lp.send_off, lp.send_idx,
                                   lp.recv_off)
-            return
-        uid = _lib.comm_unique_id() if self._rank == 0 else None
-        uid = comm.bcast(uid, root=0)
-        self._handle.comm_init(self._nranks, self._rank, uid, lp.peers, lp.send_off,
-                               lp.send_idx, lp.recv_off)
+        else:
+            uid = _lib.comm_unique_id() if self._rank == 0 else None
+            uid = comm.bcast(uid, root=0)
+            self._handle.comm_init(self._nranks, self._rank, uid, lp.peers, lp.send_off,
+                                   lp.send_idx, lp.recv_off)
+        # the direct solve completes the cut multiplier rows in its residual all-reduce
+        self._handle.set_cut(lp.n_cut, lp.lm_cut, lp.gk_off, lp.gk_row, lp.gk_coef)
 
     def _make_spaces(self) -> None:
         mesh, lp, N = self._network_mesh, self._local, self._network_mesh.N

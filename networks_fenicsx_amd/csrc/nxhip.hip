@@ -3535,6 +3535,100 @@ __global__ __launch_bounds__(kReduceThreads) void k_dir_reduce2_fr(
   }
 }
 
+// Several ranks, fused check with the cut rows (nx_set_cut): as k_dir_reduce2_fr, but an
+// owned cut bifurcation's row is summed over its owned columns only and left as a partial
+// in out[2 + k], and this rank's share of every cut row it does not own (its flux ends
+// there, -(+-1) x_q in a fixed order) goes to out[2 + k] too; out[0], out[1] exclude the
+// cut rows' r^2 (k_dir_publish_cut adds them after the all-reduce of out).
+__global__ __launch_bounds__(kReduceThreads) void k_dir_reduce_cut(
+    const double* __restrict__ rpart, int nj, const int* __restrict__ left,
+    const int* __restrict__ left_k, int nleft, Csr A, const double* __restrict__ x,
+    const double* __restrict__ b, double* __restrict__ rres, double* __restrict__ bbst,
+    int refine, int K, const int* __restrict__ cut_own, const int* __restrict__ gk_off,
+    const int* __restrict__ gk_row, const double* __restrict__ gk_coef,
+    double* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
+  double rr = 0.0, bb = 0.0;
+  for (int i = threadIdx.x; i < nj; i += kReduceThreads) {
+    rr += rpart[i];
+    bb += rpart[nj + i];
+  }
+  for (int i = threadIdx.x; i < nleft; i += kReduceThreads) {
+    const int row = left[i];
+    double acc = 0.0;
+    for (int k = A.rowptr[row]; k < A.rowptr[row + 1]; ++k) {
+      const int c = A.col[k];
+      if (c < A.n_rows) acc += A.val[k] * x[c];  // ghost columns: their owners' share
+    }
+    const double bv = b[row];
+    const double rv = bv - acc;
+    bb += bv * bv;
+    const int kc = left_k[i];
+    if (kc >= 0) {
+      out[2 + kc] = rv;
+    } else {
+      rres[row] = rv;
+      rr += rv * rv;
+    }
+  }
+  // cut index k on thread kReduceThreads - 1 - k: beside the left rows' threads, not after
+  for (int k = kReduceThreads - 1 - (int)threadIdx.x; k >= 0 && k < K; k += kReduceThreads) {
+    if (cut_own[k] >= 0) continue;  // written above
+    double sh = 0.0;
+    for (int e = gk_off[k]; e < gk_off[k + 1]; ++e) sh -= gk_coef[e] * x[gk_row[e]];
+    out[2 + k] = sh;
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_r[threadIdx.x >> 6] = rr;
+    s_b[threadIdx.x >> 6] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    rr = 0.0;
+    bb = 0.0;
+    for (int w = 0; w < kReduceThreads / 64; ++w) {
+      rr += s_r[w];
+      bb += s_b[w];
+    }
+    if (refine)
+      bb = bbst[0];
+    else
+      bbst[0] = bb;
+    out[0] = rr;
+    out[1] = bb;
+  }
+}
+
+// After the all-reduce of [rr, bb, r_cut]: the cut rows' r^2 added in index order (every
+// rank the same bits), the owned ones' r stored for a refinement step, the state published.
+__global__ void k_dir_publish_cut(const double* __restrict__ rb, int K,
+                                  const int* __restrict__ cut_own, double* __restrict__ rres,
+                                  double rtol, int* seq, MrState* mirror) {
+#pragma clang fp contract(off)
+  if (threadIdx.x != 0) return;
+  double rr = rb[0];
+  for (int k = 0; k < K; ++k) {
+    const double r = rb[2 + k];
+    rr += r * r;
+    if (cut_own[k] >= 0) rres[cut_own[k]] = r;
+  }
+  const double bb = rb[1];
+  MrState s{};
+  s.beta1 = sqrt(bb);
+  s.relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
+  s.rtol = rtol;
+  s.it = 1;
+  s.done = 1;
+  s.converged = s.relres <= rtol ? 1 : 0;
+  MrInit ini{};
+  ini.seq = seq;
+  ini.mirror = mirror;
+  mr_publish(s, ini);
+}
+
 __global__ void k_dir_publish_red(const double* __restrict__ rb, double rtol, int* seq,
                                   MrState* mirror) {
   if (threadIdx.x != 0) return;
@@ -3832,6 +3926,18 @@ struct nx_network {
   int* d_left = nullptr;
   int n_left = 0;
   double* dir_bb = nullptr;
+  std::vector<int> left_host;  // the rows of d_left
+  // several ranks, direct (nx_set_cut): the multiplier rows of the K cut bifurcations are
+  // completed inside the residual's all-reduce (no halo of x): per left row its cut index,
+  // per cut index the owned row (or -1) and this rank's flux ends at it (row, +-1)
+  int n_cut = -1;  // -1: not set
+  std::vector<int> lm_cut;
+  int* d_left_k = nullptr;
+  int* d_cut_own = nullptr;
+  int* d_gk_off = nullptr;
+  int* d_gk_row = nullptr;
+  double* d_gk_coef = nullptr;
+  double* cutbuf = nullptr;  // [rr, bb, r_0 .. r_{K-1}] (all-reduced)
   // general element degrees (nx_create_fe): gather-assembly tables, one rank, no
   // preconditioner
   // nx_set_output_map: owned rows in the reference's function order (Solver.solve output)
@@ -3966,7 +4072,9 @@ int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false, bool pack
 }
 
 // sum-all-reduce of n doubles: red + slot (slot 0..3) or the coarse buffer (slot -1)
-double* xbuf_of(nx_network* h, int slot) { return slot < 0 ? h->pa.cbuf : h->red + slot; }
+double* xbuf_of(nx_network* h, int slot) {
+  return slot == -2 ? h->cutbuf : slot < 0 ? h->pa.cbuf : h->red + slot;
+}
 
 int team_allreduce(const Team& t, int slot, int n) {
   if (!team_multi(t) || n <= 0) return NX_OK;
@@ -4628,7 +4736,8 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->partA,  h->partB,   h->red,
                   h->send_idx, h->send_buf, h->gath, h->d_seq,
                   h->fe_kind, h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent,
-                  h->fe_bptr, h->fe_bidx, h->fe_bent, h->out_idx};
+                  h->fe_bptr, h->fe_bidx, h->fe_bent, h->out_idx,
+                  h->d_left_k, h->d_cut_own, h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -5018,6 +5127,15 @@ bool direct_applicable(const Team& t) {
 // solves the coarse forest redundantly -- same inputs, same order, same bits -- and
 // back-substitutes from it), the halo of x (remote flux ends read by the multiplier rows),
 // and one all-reduce of the residual sums, published by every rank.
+// Several ranks: the cut rows ride in the residual's all-reduce (nx_set_cut given, fused
+// check on, not disabled by NXHIP_DIR_CUT=0). Part of the schedule signature.
+int build_left_cut(nx_network* h);
+bool cut_mode(const nx_network* h) {
+  const char* e = std::getenv("NXHIP_DIR_CUT");  // read per solve: tests switch it
+  const bool env = e == nullptr || std::atoi(e) != 0;
+  return env && h->n_cut >= 0 && h->fres_ok && h->d_left_k != nullptr && h->cutbuf != nullptr;
+}
+
 int launch_direct_team(const Team& t, double rtol, int refine) {
   nx_network* h0 = t.hs[0];
   if (refine) {  // the previous pass's check left r = b - A x in tmp; its ghost slots 0
@@ -5039,6 +5157,23 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
       h->pa.fres = 0;
     }
     if (half == 0) CHECK(team_allreduce(t, -1, 3 * h0->pa.n_coarse));
+  }
+  if (cut_mode(h0)) {  // the cut rows ride in the residual's all-reduce: no halo of x
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      hipLaunchKernelGGL(k_dir_reduce_cut, dim3(1), dim3(kReduceThreads), 0, h->stream,
+                         h->pa.rpart, h->pc_jobs, h->d_left, h->d_left_k, h->n_left, csr_of(h),
+                         h->x, h->rhs, h->tmp, h->dir_bb, refine, h->n_cut, h->d_cut_own,
+                         h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf);
+    }
+    CHECK(team_allreduce(t, -2, 2 + h0->n_cut));
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      hipLaunchKernelGGL(k_dir_publish_cut, dim3(1), dim3(64), 0, h->stream, h->cutbuf,
+                         h->n_cut, h->d_cut_own, h->tmp, rtol, h->d_seq, h->d_last);
+    }
+    HIPCALL(hipGetLastError());
+    return NX_OK;
   }
   CHECK(team_halo(t, VS_X, 0));
   for (int r = 0; r < t.P; ++r) {
@@ -5279,8 +5414,9 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
 // one (a rank on the global-memory preconditioner kernels while another runs the LDS
 // kernels' linear form would pair different collectives). Each rank decides from its own
 // decomposition (LDS caps), so the ranks compare.
-constexpr int kSchedSig = 8;
+constexpr int kSchedSig = 9;
 bool direct_local(const nx_network* h);
+bool cut_mode(const nx_network* h);
 void sched_sig(const nx_network* h, int* s) {
   s[0] = h->pc;
   s[1] = h->pc && h->pc_lds;
@@ -5293,6 +5429,8 @@ void sched_sig(const nx_network* h, int* s) {
   // leave peers reading stale halo values
   s[6] = h->pc ? h->pa.dense : 0;
   s[7] = h->pc ? (h->pa.n_coarse > 0) : 0;
+  // the direct solve's residual: halo of x + all-reduce of 2, or one all-reduce of 2 + K
+  s[8] = cut_mode(h) ? 1 + h->n_cut : 0;
 }
 
 int check_schedules(const Team& t) {
@@ -6069,6 +6207,11 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     h->n_left = (int)left.size();
     h->fres_ok = pa.slot_rloc && h->d_left && pa.rpart && h->dir_bb && h->tmp;
     if (const char* e = std::getenv("NXHIP_DIR_FRES")) h->fres_ok = h->fres_ok && std::atoi(e) != 0;
+    h->left_host = left;
+    if (h->n_cut >= 0) {
+      const int rc = build_left_cut(h);
+      if (rc != NX_OK) return rc;
+    }
   }
   pa.top_reg = 1;
   if (const char* e = std::getenv("NXHIP_TOP_REG")) pa.top_reg = std::atoi(e) != 0;
@@ -6335,6 +6478,73 @@ NX_API int nx_comm_unique_id(unsigned char* id_out) {
   ncclUniqueId id;
   NCCLCALL(ncclGetUniqueId(&id));
   std::memcpy(id_out, &id, sizeof(id));
+  return NX_OK;
+}
+
+namespace {
+// d_left_k: the cut index of every left row (the owned multiplier rows the down sweeps do
+// not form), from the per-multiplier-row lm_cut of nx_set_cut
+int build_left_cut(nx_network* h) {
+  if (h->d_left_k) HIPCALL(hipFree(h->d_left_k));
+  h->d_left_k = nullptr;
+  std::vector<int> lk(std::max<size_t>(1, h->left_host.size()), -1);
+  for (size_t i = 0; i < h->left_host.size(); ++i) {
+    const int64_t m = h->left_host[i] - h->n_edge_dofs;
+    if (m < 0 || m >= (int64_t)h->lm_cut.size()) return fail(NX_ERR_STATE, "left row outside the multiplier rows");
+    lk[i] = h->lm_cut[m];
+  }
+  CHECK(upload(&h->d_left_k, lk.data(), (int64_t)lk.size(), h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+}  // namespace
+
+NX_API int nx_set_cut(nx_network_t* h, int32_t K, const int32_t* lm_cut, const int32_t* gk_off,
+                      const int32_t* gk_row, const double* gk_coef) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (K < 0 || (K > 0 && (!gk_off || (gk_off[K] > 0 && (!gk_row || !gk_coef)))))
+    return fail(NX_ERR_ARG, "bad cut lists");
+  const int64_t n_lm = h->n_own - h->n_edge_dofs;
+  if (n_lm > 0 && !lm_cut) return fail(NX_ERR_ARG, "lm_cut needed for the multiplier rows");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  CHECK(drop_handle_graphs(h));
+  std::vector<int> own(std::max(1, (int)K), -1);
+  for (int64_t m = 0; m < n_lm; ++m) {
+    if (lm_cut[m] < -1 || lm_cut[m] >= K) return fail(NX_ERR_ARG, "lm_cut out of range");
+    if (lm_cut[m] >= 0) {
+      if (own[lm_cut[m]] >= 0) return fail(NX_ERR_ARG, "a cut index owned twice");
+      own[lm_cut[m]] = (int)(h->n_edge_dofs + m);
+    }
+  }
+  const int ne = K > 0 ? gk_off[K] : 0;
+  for (int k = 0; k < K; ++k)
+    if (gk_off[k] > gk_off[k + 1] || (own[k] >= 0 && gk_off[k + 1] > gk_off[k]))
+      return fail(NX_ERR_ARG, "gk_off: an owned cut row takes no flux-end shares");
+  for (int e = 0; e < ne; ++e)
+    if (gk_row[e] < 0 || gk_row[e] >= h->n_edge_dofs) return fail(NX_ERR_ARG, "gk_row out of range");
+  for (void* p : {(void*)h->d_cut_own, (void*)h->d_gk_off, (void*)h->d_gk_row,
+                  (void*)h->d_gk_coef, (void*)h->cutbuf})
+    if (p) HIPCALL(hipFree(p));
+  h->d_cut_own = h->d_gk_off = h->d_gk_row = nullptr;
+  h->d_gk_coef = h->cutbuf = nullptr;
+  std::vector<int> off(gk_off ? gk_off : nullptr, gk_off ? gk_off + K + 1 : nullptr);
+  if (off.empty()) off.assign(1, 0);
+  std::vector<int> row(gk_row ? gk_row : nullptr, gk_row ? gk_row + ne : nullptr);
+  std::vector<double> coef(gk_coef ? gk_coef : nullptr, gk_coef ? gk_coef + ne : nullptr);
+  if (row.empty()) row.assign(1, 0);
+  if (coef.empty()) coef.assign(1, 0.0);
+  CHECK(upload(&h->d_cut_own, own.data(), (int64_t)own.size(), h->stream));
+  CHECK(upload(&h->d_gk_off, off.data(), (int64_t)off.size(), h->stream));
+  CHECK(upload(&h->d_gk_row, row.data(), (int64_t)row.size(), h->stream));
+  CHECK(upload(&h->d_gk_coef, coef.data(), (int64_t)coef.size(), h->stream));
+  CHECK(dalloc(&h->cutbuf, 2 + (int64_t)K));
+  h->lm_cut.assign(lm_cut ? lm_cut : nullptr, lm_cut ? lm_cut + n_lm : nullptr);
+  h->n_cut = K;
+  h->sched_checked = false;  // the residual's exchange is part of the schedule signature
+  if (!h->left_host.empty() || h->d_left) CHECK(build_left_cut(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
   return NX_OK;
 }
 

@@ -103,6 +103,14 @@ class LocalProblem:
     # owning rank of every global edge (the partition; the preconditioner's coarse step
     # needs the whole map)
     edge_owner: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    # cut bifurcations (incident edges on several ranks), one global order on every rank:
+    # per owned multiplier row its cut index or -1; per cut index this rank's flux end rows
+    # there and their coupling (+-1) when another rank owns the row (nx_set_cut)
+    n_cut: int = 0
+    lm_cut: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    gk_off: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int32))
+    gk_row: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    gk_coef: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float64))
 
     @property
     def n_edge_dofs(self) -> int:
@@ -260,4 +268,32 @@ def build_local_problem(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degre
         lp.send_off = np.asarray(send_off, dtype=np.int32)
         lp.send_idx = np.asarray(send_idx, dtype=np.int32)
         lp.recv_off = np.asarray(recv_off, dtype=np.int32)
+        _cut_lists(lp, v, src, dst, is_bif, inc_node, inc_edge, owner, lm_owner, rank, N)
     return lp
+
+
+def _cut_lists(lp: LocalProblem, v, src, dst, is_bif, inc_node, inc_edge, owner, lm_owner,
+               rank: int, N: int) -> None:
+    """The cut bifurcations (sorted node ids: the same K and order on every rank) and this
+    rank's part of their multiplier rows: the owner forms the row over its own flux ends,
+    every other rank adds -(+-1) x_q of its flux ends there (the coupling is symmetric:
+    A[q, lambda] = A[lambda, q] = -1 at a source end q_0, +1 at a target end q_N)."""
+    cut = np.unique(inc_node[owner[inc_edge] != lm_owner[inc_node]])
+    k_of = np.full(is_bif.size, -1, dtype=np.int64)
+    k_of[cut] = np.arange(cut.size)
+    lp.n_cut = int(cut.size)
+    lp.lm_cut = k_of[v.lm_nodes].astype(np.int32)
+    per = 2 * N + 1
+    ks, rows, coefs = [], [], []
+    for end, nodes in ((0, src[v.edges]), (1, dst[v.edges])):
+        m = is_bif[nodes] & (lm_owner[nodes] != rank)
+        loc = np.flatnonzero(m)
+        ks.append(k_of[nodes[loc]])
+        rows.append(loc * per + (2 * N if end else 0))
+        coefs.append(np.full(loc.size, 1.0 if end else -1.0))
+    ks, rows, coefs = np.concatenate(ks), np.concatenate(rows), np.concatenate(coefs)
+    assert (ks >= 0).all(), "a remote multiplier at a local edge end is a cut bifurcation"
+    o = np.lexsort((rows, ks))
+    lp.gk_row = rows[o].astype(np.int32)
+    lp.gk_coef = coefs[o].astype(np.float64)
+    lp.gk_off = np.searchsorted(ks[o], np.arange(cut.size + 1)).astype(np.int32)

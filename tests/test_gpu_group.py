@@ -170,6 +170,51 @@ def test_group_large_tree_iterations_flat():
         grp.close()
 
 
+@pytest.mark.parametrize("case,P", [("depth6_N40", 4), ("arterial5_N40", 3), ("Y_N4", 2)])
+def test_group_direct_cut_rows_in_one_allreduce(case, P, monkeypatch):
+    """The cut bifurcations' multiplier rows completed inside the residual's all-reduce
+    (nx_set_cut, default) against the halo of x + all-reduce of two (NXHIP_DIR_CUT=0): the
+    same solution bit for bit, the same reported residual to its rounding, and a forced
+    refinement pass (which starts from the stored cut rows' r) converges to the true
+    residual."""
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+
+    def gathered():
+        x = np.zeros(Ab.shape[0])
+        for a, xl in zip(grp.assemblers, grp.solutions()):
+            x[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
+        return x
+
+    try:
+        assert grp.assemblers[0].local_problem.n_cut > 0
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.set_direct(True)
+        grp.assemble()
+        it, rr, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and it == 1 and grp.solver_used == "direct"
+        x1 = gathered()
+        true1 = np.linalg.norm(bb - Ab @ x1) / np.linalg.norm(bb)
+        assert abs(rr - true1) <= 0.05 * true1 + 5e-16, (rr, true1)
+        monkeypatch.setenv("NXHIP_DIR_CUT", "0")
+        grp.assemble()
+        it0, rr0, _ = grp.solve(1e-12, 50000, 4)
+        np.testing.assert_array_equal(gathered(), x1)
+        assert abs(rr0 - rr) <= 1e-6 * rr0 + 5e-16, (rr0, rr)
+        monkeypatch.delenv("NXHIP_DIR_CUT")
+        if rr > 4e-15:  # room for a refinement step below the first pass's residual
+            grp.assemble()
+            it2, rr2, conv2 = grp.solve(rr / 2, 50000, 4)
+            assert it2 == 2 and conv2 and grp.solver_used == "direct", (it2, rr2)
+            x2 = gathered()
+            true2 = np.linalg.norm(bb - Ab @ x2) / np.linalg.norm(bb)
+            assert rr2 <= rr / 2 and abs(rr2 - true2) <= 0.05 * true2 + 5e-16, (rr2, true2)
+            assert np.linalg.norm(x2 - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    finally:
+        grp.close()
+
+
 @pytest.mark.parametrize("pc", [True, False])
 def test_rccl_single_rank_communicator(pc):
     """A one-rank RCCL communicator drives the RCCL transport code (unique id, comm init,

@@ -98,6 +98,50 @@ def test_partitioned_spmv_and_halo(case, P):
         assert max(lp.n_ghost for lp in lps) <= 4 * P
 
 
+@pytest.mark.parametrize("case,P", [("depth6_N40", 2), ("depth6_N40", 8), ("arterial5_N40", 3),
+                                    ("edge_info_N10", 2), ("tree6_2d_N70", 4)])
+def test_cut_rows_by_one_allreduce(case, P):
+    """nx_set_cut's lists (layout._cut_lists): the owner's row over its own columns plus
+    every other rank's -(+-1) x_q at its flux ends there, summed over the ranks, is the
+    global residual of each cut multiplier row (what k_dir_reduce_cut + the all-reduce form
+    on the device instead of a halo of x); the same K on every rank."""
+    m, Pr, A, b, Ab, bb, perm = _setup(case)
+    src, dst = m.edges
+    bif_idx = m.bifurcation_index
+    lps = [build_local_problem(m.node_coordinates, src, dst, m.degrees, m.N, r, P)
+           for r in range(P)]
+    K = lps[0].n_cut
+    assert K > 0 and all(lp.n_cut == K for lp in lps)
+    rng = np.random.default_rng(2)
+    xg = rng.uniform(-1, 1, Ab.shape[0])
+    rg = bb - Ab @ xg
+    total = np.zeros(K)
+    owner_row = np.full(K, -1)
+    for lp in lps:
+        Al, rws = DM.local_matrix(Ab, lp, m.num_edges, bif_idx)
+        part = np.zeros(K)
+        xl = xg[rws]
+        ne = lp.n_edge_dofs
+        for i, k in enumerate(lp.lm_cut):
+            if k < 0:
+                continue
+            row = ne + i
+            assert owner_row[k] < 0
+            owner_row[k] = rws[row]
+            lo, hi = Al.indptr[row], Al.indptr[row + 1]
+            cols, vals = Al.indices[lo:hi], Al.data[lo:hi]
+            own = cols < lp.n_own
+            part[k] = bb[rws[row]] - np.dot(vals[own], xl[cols[own]])
+        for k in range(K):
+            for e in range(lp.gk_off[k], lp.gk_off[k + 1]):
+                assert lp.lm_cut.size == 0 or k not in lp.lm_cut
+                # symmetric coupling: the flux end row's entry at the multiplier column
+                part[k] -= lp.gk_coef[e] * xl[lp.gk_row[e]]
+        total += part
+    assert (owner_row >= 0).all()
+    np.testing.assert_allclose(total, rg[owner_row], rtol=1e-13, atol=1e-13)
+
+
 class _ThreadComm:
     """P ranks as threads: barrier-synchronised all-reduce (fixed rank order) and halo."""
 
