@@ -1068,6 +1068,7 @@ struct PcArgs {
   double* rpart;  // per job: partial ||r||^2, then (n_jobs on) partial ||b||^2
   int top_reg;    // k_pc_top_lds: register level sweeps allowed (NXHIP_TOP_REG)
   int topdown;    // one rank, direct: the top part solved in every down sweep workgroup
+  int coarsedown;  // several ranks, direct: the coarse step (k_pc_coarse) in every one
   int top_ts0, top_nt, top_dc0, top_ndc;  // the top part's slots and hanging-chain entries
 };
 
@@ -2420,7 +2421,50 @@ __device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* 
       ++cnk;
     }
   }
-  if (nC <= kPcThreads && __syncthreads_or(cnk > kWaveKids) == 0) {
+  const bool creg = nC <= kPcThreads && __syncthreads_or(cnk > kWaveKids) == 0;
+  if (creg && nC <= 64) {
+    // one wave (lane = coarse junction; 63 for the 8-rank C4 tree): children's D, J and the
+    // parent's z by shuffles, no workgroup barrier per level; same arithmetic and order
+    if (threadIdx.x < 64) {
+      double D = cmine ? sD[cj] : 1.0, J = cmine ? sJ[cj] : 0.0;
+      const double g0 = cmine ? sCg[cj] : 0.0;
+      double gk[kWaveKids];
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k) gk[k] = __shfl(g0, cch[k]);
+      int kmax = cnk;
+      for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+      for (int lv = nl - 1; lv >= 0; --lv) {
+        double dk[kWaveKids], jk[kWaveKids];
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          dk[k] = k < kmax ? __shfl(D, cch[k]) : 1.0;
+          jk[k] = k < kmax ? __shfl(J, cch[k]) : 0.0;
+        }
+        if (clv == lv) {
+#pragma unroll
+          for (int k = 0; k < kWaveKids; ++k) {
+            if (k >= cnk) break;
+            D -= gk[k] * gk[k] / dk[k];
+            J += gk[k] * jk[k] / dk[k];
+          }
+        }
+      }
+      const int p = cmine ? sCp[cj] : -1;
+      double zc = 0.0;
+      for (int lv = 0; lv < nl; ++lv) {  // root level first
+        const double zp = __shfl(zc, p >= 0 ? p : cj);
+        if (clv == lv) zc = (J + (p >= 0 ? g0 * zp : 0.0)) / D;
+      }
+      if (cmine) {
+        sD[cj] = D;
+        sJ[cj] = J;
+        sZc[cj] = zc;
+      }
+    }
+    __syncthreads();
+    return;
+  }
+  if (creg) {
     double D = cmine ? sD[cj] : 1.0, J = cmine ? sJ[cj] : 0.0;
     for (int lv = nl - 1; lv >= 0; --lv) {
       if (clv == lv) {
@@ -2473,6 +2517,65 @@ __device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* 
   }
 }
 
+// Several ranks, direct solve (pa.coarsedown): k_pc_coarse's work in every down workgroup.
+// This thread's top slot (loaded at the sweep's start, beside its chain prefetch) ...
+struct CoarsePre {
+  int k, par, lvo;
+  double J, D, T;
+};
+
+__device__ __forceinline__ void coarse_top_pre(const PcArgs& pa, CoarsePre& p) {
+  const int sl = threadIdx.x, ts0 = pa.top_ts0, nt = pa.top_nt;
+  p.k = -1;
+  p.par = -1;
+  p.J = 0.0;
+  p.D = 1.0;
+  p.T = 1.0;
+  p.lvo = sl <= pa.n_top_lvl ? pa.top_lvl_off[sl] : 0;
+  if (sl < nt) {
+    const int j = ts0 + sl;
+    p.k = pa.slot_cidx[j];
+    if (p.k < 0) {
+      p.par = pa.slot_parent[j];
+      p.J = pa.slot_J[j];
+      p.D = pa.slot_D[j];
+      if (p.par >= 0) p.T = pa.chain_T[pa.slot_pchain[j]];
+    }
+  }
+}
+
+// ... then the coarse forest from the all-reduced [D | J | G] (pc_coarse_lds, the same bits
+// on every rank and workgroup) and the top part's back-substitution (k_pc_coarse's staged
+// arithmetic, thread = slot) into tZ; workgroup 0 stores the values in slot_z (the
+// residual's reduce kernel moves them into x after the sweep).
+__device__ void coarse_top_block(const PcArgs& pa, const CoarsePre& p, double* cD, double* cJ,
+                                 double* cZ, double* tZ, int* tLv) {
+  const int ntl = pa.n_top_lvl, ts0 = pa.top_ts0, nt = pa.top_nt;
+  const int sl = threadIdx.x;
+  if (sl <= ntl) tLv[sl] = p.lvo;
+  pc_coarse_lds(pa, cD, cJ, cZ);  // ends with a barrier (tLv is staged too)
+  int mylv = -1;
+  if (sl < nt)
+    for (int q = 0; q < ntl; ++q)
+      if (ts0 + sl >= tLv[q] && ts0 + sl < tLv[q + 1]) mylv = q;
+  const int par = p.k >= 0 ? -2 - p.k : (p.par >= 0 ? p.par - ts0 : -1);
+  for (int lv = 0; lv < ntl; ++lv) {
+    if (mylv == lv) {
+      double zj;
+      if (par <= -2) {
+        zj = cZ[-2 - par];
+      } else {
+        double num = p.J;
+        if (par >= 0) num += tZ[par] / p.T;
+        zj = num / p.D;
+      }
+      tZ[sl] = zj;
+      if (blockIdx.x == 0) pa.slot_z[ts0 + sl] = zj;
+    }
+    __syncthreads();
+  }
+}
+
 // The fused halo pack (k_pack_beta's work) of the one-graph multi-rank solve: the last
 // workgroup of the down sweep to finish sums this rank's beta^2 partials into red[1] and
 // its slot of the gathered array, and packs the halo values of z. Resets its ticket.
@@ -2513,11 +2616,13 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sGz[kCT], sGt[kCT], sGd[kCT];  // start only: G columns (prep)
   __shared__ int sGp[kCT], sGc[kCT];
   // one rank, direct (pa.topdown): the top part's solve in every workgroup (top_body)
-  constexpr int kTT = DIRK && !MULTI ? kCapT : 1, kTD = DIRK && !MULTI ? kCapTDC : 1;
+  constexpr int kTT = DIRK ? kCapT : 1, kTD = DIRK && !MULTI ? kCapTDC : 1;
   __shared__ double tD0[kTT], tJ0[kTT], tD[kTT], tJ[kTT], tGp[kTT], tY[kTT];
   __shared__ int tPar[kTT], tLam[kTT], tOff[kTT + 1], tChild[kTD];
   __shared__ double tG[kTD], tDD[kTD], tDJ[kTD];
-  __shared__ int tLv[DIRK && !MULTI ? kMaxTopLvl + 1 : 1];
+  __shared__ int tLv[DIRK ? kMaxTopLvl + 1 : 1];
+  // several ranks, direct (pa.coarsedown): the coarse forest and the top part solved here
+  // (k_pc_coarse's work) in tD0 / tJ0 / tD (coarse) and tJ (top values)
   __shared__ int sLvl[kCapLvl + 1];
   __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
   __shared__ double sQt[DIRK ? kCapC : 1], sQb[DIRK ? kCapC : 1];  // fused residual
@@ -2544,6 +2649,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const bool tdir = DIRK && !MULTI && pa.topdown;
   TopPre tpre{};
   if (tdir) top_pre_idx(pa, tpre);
+  const bool cdir = DIRK && MULTI && pa.coarsedown;
+  CoarsePre cpre{};
+  if (cdir) coarse_top_pre(pa, cpre);
   ChainLane<W, CPL> ch;
   ch.setup(pa, c0 + seg, c0 + seg < c1);
   double vc[CPL], vq[CPL], vN = 0.0;
@@ -2582,6 +2690,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
       top_body<false>(pa, y, r2, z, st, nullptr, 0, nullptr, nullptr, kModeDirect,
                       TopLds{tD0, tJ0, tD, tJ, tGp, tY, tPar, tLam, tOff, tChild, tG, tDD, tDJ, tLv},
                       true, tpre);
+  }
+  if constexpr (DIRK && MULTI) {
+    if (cdir) coarse_top_block(pa, cpre, tD0, tJ0, tD, tJ, tLv);
   }
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
@@ -2664,6 +2775,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   }
   auto outside = [&](int t) -> double {  // value of a top slot (outside this job)
     if (tdir) return tJ0[t - tts0];
+    if (cdir) return tJ[t - tts0];
     if (!dense) return pa.slot_z[t];
     double v = 0.0;
     for (int k = 0; k < nneed; ++k)
@@ -2832,8 +2944,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
           }
           // (topdown: the top slots' x is refined by k_dir_publish_fr after this sweep, so
           // their refined value is formed here as x + d, the same single addition)
-          zt = up < 0 ? 0.0 : z[pa.slot_lam[up]] + (tdir && (up < js0 || up >= js1) ? zt : 0.0);
-          zb = lo < 0 ? 0.0 : z[pa.slot_lam[lo]] + (tdir && (lo < js0 || lo >= js1) ? zb : 0.0);
+          const bool tv = tdir || cdir;  // the top values are not in x yet
+          zt = up < 0 ? 0.0 : z[pa.slot_lam[up]] + (tv && (up < js0 || up >= js1) ? zt : 0.0);
+          zb = lo < 0 ? 0.0 : z[pa.slot_lam[lo]] + (tv && (lo < js0 || lo >= js1) ? zb : 0.0);
         }
         direct_residual<W, CPL>(pa, ch, active, flip, bcv, rq, rqN, zc, xv, zt, zb, mo_r, rr, bb,
                                 sQt, sQb, c - c0);
@@ -3542,13 +3655,23 @@ __global__ __launch_bounds__(kReduceThreads) void k_dir_reduce2_fr(
 // cut rows' r^2 (k_dir_publish_cut adds them after the all-reduce of out).
 __global__ __launch_bounds__(kReduceThreads) void k_dir_reduce_cut(
     const double* __restrict__ rpart, int nj, const int* __restrict__ left,
-    const int* __restrict__ left_k, int nleft, Csr A, const double* __restrict__ x,
+    const int* __restrict__ left_k, int nleft, Csr A, double* __restrict__ x,
     const double* __restrict__ b, double* __restrict__ rres, double* __restrict__ bbst,
     int refine, int K, const int* __restrict__ cut_own, const int* __restrict__ gk_off,
     const int* __restrict__ gk_row, const double* __restrict__ gk_coef,
-    double* __restrict__ out) {
+    double* __restrict__ out, const int* __restrict__ top_lam,
+    const double* __restrict__ top_z, int ntop) {
 #pragma clang fp contract(off)
   __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
+  // coarsedown: the top part's values (every down workgroup solved them, workgroup 0's copy
+  // in slot_z) into x; the rows below read flux values only
+  for (int i = threadIdx.x; i < ntop; i += kReduceThreads) {
+    const int lam = top_lam[i];
+    if (refine)
+      x[lam] += top_z[i];
+    else
+      x[lam] = top_z[i];
+  }
   double rr = 0.0, bb = 0.0;
   for (int i = threadIdx.x; i < nj; i += kReduceThreads) {
     rr += rpart[i];
@@ -4166,7 +4289,7 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
   }
   // fused (dense top, LDS kernels): every down workgroup solves the coarse forest itself
   const bool cfused = MULTI && h->pc_lds && h->pa.fused && h->pa.mdense && mode == 0;
-  if (coarse && !cfused)
+  if (coarse && !cfused && !(mode == kModeDirect && h->pa.coarsedown))
     hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2, z,
                        st, h->partB, mode);
   if (h->pc_jobs > 0) {
@@ -5130,6 +5253,17 @@ bool direct_applicable(const Team& t) {
 // Several ranks: the cut rows ride in the residual's all-reduce (nx_set_cut given, fused
 // check on, not disabled by NXHIP_DIR_CUT=0). Part of the schedule signature.
 int build_left_cut(nx_network* h);
+bool cut_mode(const nx_network* h);
+// Several ranks, direct: k_pc_coarse's work in every down workgroup (pa.coarsedown; with the
+// cut rows in the residual's all-reduce, whose reduce kernel then moves the top values into
+// x). NXHIP_DIR_COARSE_DOWN=0 keeps the kernel. Part of the schedule signature.
+bool coarse_down(const nx_network* h) {
+  const char* e = std::getenv("NXHIP_DIR_COARSE_DOWN");
+  const bool env = e == nullptr || std::atoi(e) != 0;
+  return env && cut_mode(h) && h->pc_lds && h->pa.n_coarse > 0 &&
+         h->pa.n_coarse <= kCapCoarseLds && h->top_nt <= kTopThreads &&
+         h->pa.n_top_lvl <= kMaxTopLvl;
+}
 bool cut_mode(const nx_network* h) {
   const char* e = std::getenv("NXHIP_DIR_CUT");  // read per solve: tests switch it
   const bool env = e == nullptr || std::atoi(e) != 0;
@@ -5152,19 +5286,23 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
       double* bin = refine ? h->tmp : h->rhs;
       h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
       h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the local rows' residual
+      h->pa.coarsedown = coarse_down(h) ? 1 : 0;  // and the coarse step (no k_pc_coarse)
       launch_pc<true>(h, bin, bin, h->st, h->st + 1, kModeDirect, half, h->x);
       h->pa.accum = 0;
       h->pa.fres = 0;
+      h->pa.coarsedown = 0;
     }
     if (half == 0) CHECK(team_allreduce(t, -1, 3 * h0->pa.n_coarse));
   }
   if (cut_mode(h0)) {  // the cut rows ride in the residual's all-reduce: no halo of x
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
+      const int ntop = coarse_down(h) ? h->top_nt : 0;
       hipLaunchKernelGGL(k_dir_reduce_cut, dim3(1), dim3(kReduceThreads), 0, h->stream,
                          h->pa.rpart, h->pc_jobs, h->d_left, h->d_left_k, h->n_left, csr_of(h),
                          h->x, h->rhs, h->tmp, h->dir_bb, refine, h->n_cut, h->d_cut_own,
-                         h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf);
+                         h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf,
+                         h->pa.slot_lam + h->top_ts0, h->pa.slot_z + h->top_ts0, ntop);
     }
     CHECK(team_allreduce(t, -2, 2 + h0->n_cut));
     for (int r = 0; r < t.P; ++r) {
@@ -5414,9 +5552,10 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
 // one (a rank on the global-memory preconditioner kernels while another runs the LDS
 // kernels' linear form would pair different collectives). Each rank decides from its own
 // decomposition (LDS caps), so the ranks compare.
-constexpr int kSchedSig = 9;
+constexpr int kSchedSig = 10;
 bool direct_local(const nx_network* h);
 bool cut_mode(const nx_network* h);
+bool coarse_down(const nx_network* h);
 void sched_sig(const nx_network* h, int* s) {
   s[0] = h->pc;
   s[1] = h->pc && h->pc_lds;
@@ -5431,6 +5570,7 @@ void sched_sig(const nx_network* h, int* s) {
   s[7] = h->pc ? (h->pa.n_coarse > 0) : 0;
   // the direct solve's residual: halo of x + all-reduce of 2, or one all-reduce of 2 + K
   s[8] = cut_mode(h) ? 1 + h->n_cut : 0;
+  s[9] = coarse_down(h) ? 1 : 0;  // the coarse step in the down sweeps or k_pc_coarse
 }
 
 int check_schedules(const Team& t) {

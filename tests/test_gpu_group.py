@@ -173,10 +173,11 @@ def test_group_large_tree_iterations_flat():
 @pytest.mark.parametrize("case,P", [("depth6_N40", 4), ("arterial5_N40", 3), ("Y_N4", 2)])
 def test_group_direct_cut_rows_in_one_allreduce(case, P, monkeypatch):
     """The cut bifurcations' multiplier rows completed inside the residual's all-reduce
-    (nx_set_cut, default) against the halo of x + all-reduce of two (NXHIP_DIR_CUT=0): the
-    same solution bit for bit, the same reported residual to its rounding, and a forced
-    refinement pass (which starts from the stored cut rows' r) converges to the true
-    residual."""
+    (nx_set_cut, default) against the halo of x + all-reduce of two (NXHIP_DIR_CUT=0), and
+    the coarse step inside the down sweeps (default) against k_pc_coarse
+    (NXHIP_DIR_COARSE_DOWN=0): the same solution bit for bit, the same reported residual to
+    its rounding, and a forced refinement pass (which starts from the stored cut rows' r and
+    refines the top values in the down sweeps) converges to the true residual."""
     make, N, strategy, pbc = CASES[case]
     G, mesh, Ab, bb, x_ref = _reference(case)
     grp = RankGroup(G, N, P, color_strategy=strategy)
@@ -197,12 +198,19 @@ def test_group_direct_cut_rows_in_one_allreduce(case, P, monkeypatch):
         x1 = gathered()
         true1 = np.linalg.norm(bb - Ab @ x1) / np.linalg.norm(bb)
         assert abs(rr - true1) <= 0.05 * true1 + 5e-16, (rr, true1)
-        monkeypatch.setenv("NXHIP_DIR_CUT", "0")
+        monkeypatch.setenv("NXHIP_DIR_CUT", "0")  # (and so k_pc_coarse, see below)
         grp.assemble()
         it0, rr0, _ = grp.solve(1e-12, 50000, 4)
         np.testing.assert_array_equal(gathered(), x1)
         assert abs(rr0 - rr) <= 1e-6 * rr0 + 5e-16, (rr0, rr)
         monkeypatch.delenv("NXHIP_DIR_CUT")
+        # the coarse step in every down workgroup (default) against the k_pc_coarse kernel
+        monkeypatch.setenv("NXHIP_DIR_COARSE_DOWN", "0")
+        grp.assemble()
+        it0, rr0, _ = grp.solve(1e-12, 50000, 4)
+        np.testing.assert_array_equal(gathered(), x1)
+        assert rr0 == rr, (rr0, rr)
+        monkeypatch.delenv("NXHIP_DIR_COARSE_DOWN")
         if rr > 4e-15:  # room for a refinement step below the first pass's residual
             grp.assemble()
             it2, rr2, conv2 = grp.solve(rr / 2, 50000, 4)
