@@ -2645,13 +2645,31 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   constexpr int G = kPcThreads / W;
   const int seg = threadIdx.x / W;
-  // one rank, direct (pa.topdown): the top part's first indices ahead of the chain prefetch
+  // one rank, direct (pa.topdown): the top part solved here first (k_pc_top_lds's work, same
+  // arithmetic), its values left in LDS (tJ0, by top position); several ranks, direct
+  // (pa.coarsedown): the coarse forest and the top part's back-substitution (k_pc_coarse's
+  // work; values in tJ). Before the chain prefetch: nothing of it is live across them
+  // (spills otherwise).
   const bool tdir = DIRK && !MULTI && pa.topdown;
-  TopPre tpre{};
-  if (tdir) top_pre_idx(pa, tpre);
   const bool cdir = DIRK && MULTI && pa.coarsedown;
-  CoarsePre cpre{};
-  if (cdir) coarse_top_pre(pa, cpre);
+  const int tts0 = pa.top_ts0;
+  if constexpr (DIRK && !MULTI) {
+    if (tdir) {
+      TopPre tpre;
+      top_pre_idx(pa, tpre);
+      top_pre_val(pa, y, tpre);
+      top_body<false>(pa, y, r2, z, st, nullptr, 0, nullptr, nullptr, kModeDirect,
+                      TopLds{tD0, tJ0, tD, tJ, tGp, tY, tPar, tLam, tOff, tChild, tG, tDD, tDJ, tLv},
+                      true, tpre);
+    }
+  }
+  if constexpr (DIRK && MULTI) {
+    if (cdir) {
+      CoarsePre cpre;
+      coarse_top_pre(pa, cpre);
+      coarse_top_block(pa, cpre, tD0, tJ0, tD, tJ, tLv);
+    }
+  }
   ChainLane<W, CPL> ch;
   ch.setup(pa, c0 + seg, c0 + seg < c1);
   double vc[CPL], vq[CPL], vN = 0.0;
@@ -2679,21 +2697,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     p_lam = pa.slot_lam[j];
     p_y = y[p_lam];
   }
-  if (tdir) top_pre_val(pa, y, tpre);  // the values they point at, beside the job's own
   if (mode == 0 && st->done) return;  // after the prefetch (nothing written before)
   const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
-  // one rank, direct: the top part solved here (k_pc_top_lds's work, same arithmetic) while
-  // the prefetch above is in flight; its values stay in LDS (tJ0, by top position)
-  const int tts0 = pa.top_ts0;
-  if constexpr (DIRK && !MULTI) {
-    if (tdir)
-      top_body<false>(pa, y, r2, z, st, nullptr, 0, nullptr, nullptr, kModeDirect,
-                      TopLds{tD0, tJ0, tD, tJ, tGp, tY, tPar, tLam, tOff, tChild, tG, tDD, tDJ, tLv},
-                      true, tpre);
-  }
-  if constexpr (DIRK && MULTI) {
-    if (cdir) coarse_top_block(pa, cpre, tD0, tJ0, tD, tJ, tLv);
-  }
+
   // dense top (iterations, single rank): the top values this job needs, z_t = G[t,:] . a
   const bool dense = (MULTI ? pa.mdense : pa.dense) && mode == 0;
   // several ranks, fused: every workgroup solves the coarse forest (k_pc_coarse's job)
@@ -4322,6 +4328,7 @@ void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState*
     case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
     case 8: launch_pc_wc<MULTI, 64, 8>(h, y, r2, st, other, mode, half, zout, evs); break;
     case 9: launch_pc_wc<MULTI, 64, 16>(h, y, r2, st, other, mode, half, zout, evs); break;
+    case 10: launch_pc_wc<MULTI, 8, 3>(h, y, r2, st, other, mode, half, zout, evs); break;
     default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
   }
 }
@@ -5218,6 +5225,7 @@ int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
     case 7: launch_direct_wc<8, 4>(h, rtol, refine, prof); break;
     case 8: launch_direct_wc<64, 8>(h, rtol, refine, prof); break;
     case 9: launch_direct_wc<64, 16>(h, rtol, refine, prof); break;
+    case 10: launch_direct_wc<8, 3>(h, rtol, refine, prof); break;
     default: launch_direct_wc<64, 4>(h, rtol, refine, prof); break;
   }
   HIPCALL(hipGetLastError());
@@ -6155,8 +6163,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 1024 cells per edge");
   if (const char* e = std::getenv("NXHIP_PC_VARIANT")) {  // tuning: (W, CPL) override
     const int v = std::atoi(e);
-    const int cap[10] = {16, 32, 64, 128, 256, 16, 16, 32, 512, 1024};
-    if (v >= 0 && v < 10 && N <= cap[v]) variant = v;
+    const int cap[11] = {16, 32, 64, 128, 256, 16, 16, 32, 512, 1024, 24};
+    if (v >= 0 && v < 11 && N <= cap[v]) variant = v;
   }
   if (n_chains != h->E) return fail(NX_ERR_ARG, "one chain per local edge expected");
   // one slot per owned multiplier, plus (several ranks) the ghost junctions at the ends of
