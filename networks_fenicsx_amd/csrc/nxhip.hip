@@ -4328,7 +4328,6 @@ void launch_pc(nx_network* h, double* y, const double* r2, MrState* st, MrState*
     case 7: launch_pc_wc<MULTI, 8, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
     case 8: launch_pc_wc<MULTI, 64, 8>(h, y, r2, st, other, mode, half, zout, evs); break;
     case 9: launch_pc_wc<MULTI, 64, 16>(h, y, r2, st, other, mode, half, zout, evs); break;
-    case 10: launch_pc_wc<MULTI, 8, 3>(h, y, r2, st, other, mode, half, zout, evs); break;
     default: launch_pc_wc<MULTI, 64, 4>(h, y, r2, st, other, mode, half, zout, evs); break;
   }
 }
@@ -5225,7 +5224,6 @@ int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
     case 7: launch_direct_wc<8, 4>(h, rtol, refine, prof); break;
     case 8: launch_direct_wc<64, 8>(h, rtol, refine, prof); break;
     case 9: launch_direct_wc<64, 16>(h, rtol, refine, prof); break;
-    case 10: launch_direct_wc<8, 3>(h, rtol, refine, prof); break;
     default: launch_direct_wc<64, 4>(h, rtol, refine, prof); break;
   }
   HIPCALL(hipGetLastError());
@@ -6163,8 +6161,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 1024 cells per edge");
   if (const char* e = std::getenv("NXHIP_PC_VARIANT")) {  // tuning: (W, CPL) override
     const int v = std::atoi(e);
-    const int cap[11] = {16, 32, 64, 128, 256, 16, 16, 32, 512, 1024, 24};
-    if (v >= 0 && v < 11 && N <= cap[v]) variant = v;
+    const int cap[10] = {16, 32, 64, 128, 256, 16, 16, 32, 512, 1024};
+    if (v >= 0 && v < 10 && N <= cap[v]) variant = v;
   }
   if (n_chains != h->E) return fail(NX_ERR_ARG, "one chain per local edge expected");
   // one slot per owned multiplier, plus (several ranks) the ghost junctions at the ends of
