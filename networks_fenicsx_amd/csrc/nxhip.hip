@@ -1963,6 +1963,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       int kmax = nk;
       for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
       double D = mine ? sD0[sl] : 1.0, J = mine ? sJ0[sl] : 0.0, iv = 1.0;
+#ifdef NX_PHASE_TIMING
+      if (blockIdx.x == 0 && threadIdx.x == 0) g_phase[21] = wall_clock64();  // setup done
+#endif
       for (int q = lv1 - lv0 - 1; q >= 0; --q) {
 #pragma unroll
         for (int k = 0; k < kWaveKids; ++k) {
@@ -2607,6 +2610,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
                                                             const MrState* __restrict__ st,
                                                             double* __restrict__ partB, int mode_in) {
   const int mode = DIRK ? kModeDirect : mode_in;
+  // one rank, direct (pa.topdown): the top part's first indices before anything else (they
+  // need no per-job offsets; the scalar loads of the prologue below would hold them back)
+  TopPre tpre;
+  if (DIRK && !MULTI && pa.topdown) top_pre_idx(pa, tpre);
   __shared__ double sZ[kCapS], sA[kCapS], sB[kCapS];
   __shared__ int sP[kCapS];
   constexpr int kCT = DIRK ? 1 : kCapT;  // MINRES-only arrays (dense top, start's prep)
@@ -2655,8 +2662,6 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   const int tts0 = pa.top_ts0;
   if constexpr (DIRK && !MULTI) {
     if (tdir) {
-      TopPre tpre;
-      top_pre_idx(pa, tpre);
       top_pre_val(pa, y, tpre);
       top_body<false>(pa, y, r2, z, st, nullptr, 0, nullptr, nullptr, kModeDirect,
                       TopLds{tD0, tJ0, tD, tJ, tGp, tY, tPar, tLam, tOff, tChild, tG, tDD, tDJ, tLv},

@@ -29,7 +29,7 @@ from networks_fenicsx_amd import network_generation as ng  # noqa: E402
 KERNELS = {0: "k_mr_a", 16: "k_pc_up_lds", 32: "k_pc_top_lds", 48: "k_pc_down_lds"}
 PHASES = {
     0: ["start", "rotation", "spmv+update"],
-    16: ["start", "chains", "phase A", "levels+store", "levels"],
+    16: ["start", "chains", "phase A", "levels+store", "levels", "wave set-up"],
     32: ["start", "A1/A2 gathers", "A3 fold", "up levels", "back-sub"],
     48: ["start", "phase A", "levels+slots", "chains"],
 }
