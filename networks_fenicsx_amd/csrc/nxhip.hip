@@ -1067,6 +1067,11 @@ struct PcArgs {
   double* rres;   // r (kept for a refinement step)
   double* rpart;  // per job: partial ||r||^2, then (n_jobs on) partial ||b||^2
   int top_reg;    // k_pc_top_lds: register level sweeps allowed (NXHIP_TOP_REG)
+  // the up sweep's one-wave junction levels, set up by the host: per job kmax + 1 (0: the
+  // job runs the block-wide levels), per lower slot [level | nk << 8, child 0 | child 1 << 16,
+  // child 2 | child 3 << 16] with child = local slot | dc offset << 6
+  const int* job_wave;
+  const int* slot_wave;
   int topdown;    // one rank, direct: the top part solved in every down sweep workgroup
   int coarsedown;  // several ranks, direct: the coarse step (k_pc_coarse) in every one
   int top_ts0, top_nt, top_dc0, top_ndc;  // the top part's slots and hanging-chain entries
@@ -1874,6 +1879,15 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
       pa.u[pa.slot_uy[t - ts0]] = yl;
     }
   }
+  // the host-built one-wave set-up of this job's levels (loaded here, used after phase A)
+  const int jwave = (lv1 > lv0 && pa.job_wave) ? pa.job_wave[job] : 0;
+  int wv0 = 0, wv1 = 0, wv2 = 0;
+  if (jwave > 0 && (int)threadIdx.x < js1 - js0) {
+    const int* w = pa.slot_wave + 3 * (int64_t)(js0 + threadIdx.x);
+    wv0 = w[0];
+    wv1 = w[1];
+    wv2 = w[2];
+  }
   if (lv1 > lv0) {  // the job's junction levels (block-uniform)
   const int ns = js1 - js0;
   const int dc0 = pa.slot_dc_off[js0];
@@ -1928,18 +1942,18 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
   // phase B by one wave when the job has <= 64 slots with <= kWaveKids junction children
   // each (every job of the binary trees): lane = slot, the children's values by shuffles,
   // no workgroup barrier per level (~0.5 us each). Same arithmetic in the same order.
-  int nkids = 0;
-  if ((int)threadIdx.x < ns)
-    for (int i = sOff[threadIdx.x]; i < sOff[threadIdx.x + 1]; ++i) nkids += sChild[i] >= 0;
-  const bool wave_lv = __syncthreads_or(nkids > kWaveKids) == 0 && ns <= 64 &&
-                       lv1 - lv0 <= kCapLvl;
+  bool wave_lv = jwave > 0;  // host-built set-up (pa.slot_wave)
+  if (!wave_lv) {
+    int nkids = 0;
+    if ((int)threadIdx.x < ns)
+      for (int i = sOff[threadIdx.x]; i < sOff[threadIdx.x + 1]; ++i) nkids += sChild[i] >= 0;
+    wave_lv = __syncthreads_or(nkids > kWaveKids) == 0 && ns <= 64 && lv1 - lv0 <= kCapLvl;
+  }
   if (wave_lv) {
     if (threadIdx.x < 64) {
       const int sl = threadIdx.x;
       const bool mine = sl < ns;
       int mylv = -1;
-      for (int q = 0; q < lv1 - lv0; ++q)
-        if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
       int cl[kWaveKids];
       double cg[kWaveKids];
 #pragma unroll
@@ -1947,21 +1961,38 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_up_lds(PcArgs pa, double* __r
         cl[k] = sl;
         cg[k] = 0.0;
       }
-      int nk = 0;
-      if (mine)
-        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
-          const int chd = sChild[i];
-          if (chd < 0) continue;
+      int nk = 0, kmax;
+      if (jwave > 0) {  // level, children and their dc entries from the host
+        kmax = jwave - 1;
+        if (mine) {
+          mylv = wv0 & 0xff;
+          nk = (wv0 >> 8) & 0xff;
+          const int cw[kWaveKids] = {wv1 & 0xffff, wv1 >> 16, wv2 & 0xffff, wv2 >> 16};
 #pragma unroll
           for (int k = 0; k < kWaveKids; ++k)
-            if (k == nk) {
-              cl[k] = chd;
-              cg[k] = sG[i];
+            if (k < nk) {
+              cl[k] = cw[k] & 63;
+              cg[k] = sG[cw[k] >> 6];
             }
-          ++nk;
         }
-      int kmax = nk;
-      for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+      } else {
+        for (int q = 0; q < lv1 - lv0; ++q)
+          if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
+        if (mine)
+          for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+            const int chd = sChild[i];
+            if (chd < 0) continue;
+#pragma unroll
+            for (int k = 0; k < kWaveKids; ++k)
+              if (k == nk) {
+                cl[k] = chd;
+                cg[k] = sG[i];
+              }
+            ++nk;
+          }
+        kmax = nk;
+        for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+      }
       double D = mine ? sD0[sl] : 1.0, J = mine ? sJ0[sl] : 0.0, iv = 1.0;
 #ifdef NX_PHASE_TIMING
       if (blockIdx.x == 0 && threadIdx.x == 0) g_phase[21] = wall_clock64();  // setup done
@@ -6366,6 +6397,49 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   }
   pa.top_reg = 1;
   if (const char* e = std::getenv("NXHIP_TOP_REG")) pa.top_reg = std::atoi(e) != 0;
+  // the up sweep's one-wave level set-up (k_pc_up_lds): per eligible job (<= 64 slots, <=
+  // kCapLvl levels, <= kWaveKids junction children per slot) each slot's level, children
+  // (local slot) and their hanging-chain entries (offset from the job's first), packed
+  pa.job_wave = nullptr;
+  pa.slot_wave = nullptr;
+  if (lds && n_jobs > 0) {
+    std::vector<int> jw(n_jobs, 0), sw(3 * std::max<int64_t>(1, n_slots), 0);
+    int n_wave = 0;
+    for (int jb = 0; jb < n_jobs; ++jb) {
+      const int lv0 = job_lvl_off[jb], lv1 = job_lvl_off[jb + 1];
+      if (lv1 <= lv0) continue;
+      const int js0 = lvl_slot_off[lv0], js1 = lvl_slot_off[lv1];
+      if (js1 - js0 > 64 || lv1 - lv0 > kCapLvl) continue;
+      const int dc0 = slot_dc_off[js0];
+      bool ok = true;
+      int kmax = 0;
+      for (int lv = lv0; lv < lv1 && ok; ++lv)
+        for (int j = lvl_slot_off[lv]; j < lvl_slot_off[lv + 1] && ok; ++j) {
+          int nk = 0, cw[kWaveKids] = {0, 0, 0, 0};
+          for (int i = slot_dc_off[j]; i < slot_dc_off[j + 1]; ++i) {
+            if (dc_lo[i] < 0) continue;
+            const int cl = dc_lo[i] - js0, off = i - dc0;
+            if (nk >= kWaveKids || cl < 0 || cl >= 64 || off >= 1024) {
+              ok = false;
+              break;
+            }
+            cw[nk++] = cl | (off << 6);
+          }
+          kmax = std::max(kmax, nk);
+          sw[3 * j] = (lv - lv0) | (nk << 8);
+          sw[3 * j + 1] = cw[0] | (cw[1] << 16);
+          sw[3 * j + 2] = cw[2] | (cw[3] << 16);
+        }
+      if (ok) {
+        jw[jb] = kmax + 1;
+        ++n_wave;
+      }
+    }
+    if (n_wave > 0) {
+      pa.job_wave = up(jw.data(), n_jobs);
+      pa.slot_wave = up(sw.data(), (int64_t)sw.size());
+    }
+  }
   h->pc_lds = lds;
   h->pa = pa;
   h->pc_jobs = n_jobs;
