@@ -2723,8 +2723,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     flip = dir && active ? pa.chain_flip[c] : 0;
   };
   load_lane(c0 + seg, c0 + seg < c1);
-  int p_par = -1, p_lam = 0;
+  int p_par = -1, p_lam = 0, p_lv = -1;
   double p_A = 0.0, p_B = 0.0, p_y = 0.0;
+  const bool hwave = pa.job_wave != nullptr && lv1 > lv0 && pa.job_wave[job] > 0;
   if ((int)threadIdx.x < ns) {
     const int j = js0 + threadIdx.x;
     p_par = pa.slot_parent[j];
@@ -2732,6 +2733,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     p_B = pa.slot_B[j];
     p_lam = pa.slot_lam[j];
     p_y = y[p_lam];
+    if (hwave) p_lv = pa.slot_wave[3 * (int64_t)j] & 0xff;  // the host's level of the slot
   }
   if (mode == 0 && st->done) return;  // after the prefetch (nothing written before)
   const double c2 = lin ? pa.xalpha[0] / st->beta : 0.0;
@@ -2843,9 +2845,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     if (threadIdx.x < 64) {
       const int sl = threadIdx.x;
       const bool mine = sl < ns;
-      int mylv = -1;
-      for (int q = 0; q < lv1 - lv0; ++q)
-        if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
+      int mylv = hwave ? p_lv : -1;
+      if (!hwave)
+        for (int q = 0; q < lv1 - lv0; ++q)
+          if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
       const double A = mine ? sA[sl] : 0.0, Bv = mine ? sB[sl] : 0.0;
       const int p = mine ? sP[sl] : -1;
       double zv = mine ? sZ[sl] : 0.0;  // an outside parent's value for the job root
