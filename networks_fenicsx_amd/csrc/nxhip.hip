@@ -4091,6 +4091,7 @@ struct nx_network {
   // the rows it cannot form (left, n_left) and ||b||^2 of the first pass (dir_bb)
   bool fres_ok = false;
   int top_ts0 = 0, top_nt = 0;  // the top part's slots (host copy of top_lvl_off's ends)
+  int n_cu = 0;  // compute units of the device (topdown / coarsedown need one round of jobs)
   int* d_left = nullptr;
   int n_left = 0;
   double* dir_bb = nullptr;
@@ -4720,6 +4721,8 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   if (hipMemsetAsync(h->st, 0, 2 * sizeof(MrState), h->stream) != hipSuccess)
     return bail(fail(NX_ERR_HIP, "memset state failed"));
 
+  if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    h->n_cu = 0;
   // pattern: edge segments on the device; multiplier rows from the host lists
   if (n_edges > 0) {
     EdgeArgs ea{h->edge_x, h->edge_lm, h->edge_seg, n_edges, N};
@@ -5195,6 +5198,13 @@ int top_down_flag() {
   return f;
 }
 
+// One rank, direct: the top part in every down workgroup (pa.topdown) -- only when the jobs
+// run in one round (every workgroup repeats the top part; C4 on one GPU, 4 rounds, measured
+// 0.524 vs 0.488 ms/step with the top kernel)
+bool top_down_on(const nx_network* h) {
+  return h->fres_ok && h->top_nt > 0 && top_down_flag() && h->pc_jobs <= h->n_cu;
+}
+
 template <int W, int CPL>
 void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const hipEvent_t* evs = prof ? h->dev : nullptr;
@@ -5208,7 +5218,7 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
     h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
     h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the residual check
     // and every down workgroup the top part (no k_pc_top_lds; NXHIP_TOP_DOWN=0 keeps it)
-    const bool td = h->fres_ok && h->top_nt > 0 && top_down_flag();
+    const bool td = top_down_on(h);
     h->pa.topdown = td ? 1 : 0;
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, h->x, evs);
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 1, h->x, evs);
@@ -5305,7 +5315,7 @@ bool cut_mode(const nx_network* h);
 bool coarse_down(const nx_network* h) {
   const char* e = std::getenv("NXHIP_DIR_COARSE_DOWN");
   const bool env = e == nullptr || std::atoi(e) != 0;
-  return env && cut_mode(h) && h->pc_lds && h->pa.n_coarse > 0 &&
+  return env && cut_mode(h) && h->pc_lds && h->pa.n_coarse > 0 && h->pc_jobs <= h->n_cu &&
          h->pa.n_coarse <= kCapCoarseLds && h->top_nt <= kTopThreads &&
          h->pa.n_top_lvl <= kMaxTopLvl;
 }
@@ -5421,7 +5431,7 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     for (int k = 0; k < 4; ++k) {
       if (k < 3 && !fused) continue;
       float ms = 0.f;
-      if (k == 1 && fused && h->fres_ok && h->top_nt > 0 && top_down_flag())
+      if (k == 1 && fused && top_down_on(h))
         continue;  // no k_pc_top_lds dispatch (topdown): its events were not recorded
       if (hipEventElapsedTime(&ms, h->dev[2 * k], h->dev[2 * k + 1]) == hipSuccess)
         h->dir_ms[k] += ms;
