@@ -261,12 +261,20 @@ class Handle:
         check(lib().nx_set_source(self.ptr, _ptr(ef, C.c_double)))
 
     def assemble(self, lhs: bool = True, rhs: bool = True) -> None:
-        check(lib().nx_assemble(self.ptr, int(bool(lhs)), int(bool(rhs))))
+        rc = lib().nx_assemble(self.ptr, 1 if lhs else 0, 1 if rhs else 0)
+        if rc != NX_OK:
+            check(rc)
 
     def solve(self, rtol: float, maxit: int, check_every: int = 4):
-        it, rr, conv = C.c_int32(), C.c_double(), C.c_int32()
-        check(lib().nx_solve(self.ptr, float(rtol), int(maxit), int(check_every), C.byref(it),
-                             C.byref(rr), C.byref(conv)))
+        # out-parameters allocated once per handle: this call sits in every step's host path
+        out = self.__dict__.get("_solve_out")
+        if out is None:
+            vals = (C.c_int32(), C.c_double(), C.c_int32())
+            out = self._solve_out = (vals, tuple(C.byref(v) for v in vals))
+        rc = lib().nx_solve(self.ptr, float(rtol), int(maxit), int(check_every), *out[1])
+        if rc != NX_OK:
+            check(rc)
+        it, rr, conv = out[0]
         return int(it.value), float(rr.value), bool(conv.value)
 
     def solution(self) -> np.ndarray:
