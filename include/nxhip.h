@@ -209,6 +209,17 @@ int nx_set_pc_exact(nx_network_t* h, int32_t enable);
 int nx_get_pc_exact(nx_network_t* h, int32_t* enabled);
 
 /*
+ * Sweep kernels of the preconditioner / direct solve: nx_get_pc_kernels reports whether the
+ * uploaded decomposition runs the LDS kernels (1) or the global-memory ones (0, a job over
+ * the LDS caps); nx_set_pc_kernels(h, 1) makes the next nx_set_preconditioner take the
+ * global-memory kernels even where LDS fits. Several ranks must agree (their exchange
+ * schedules differ): the host reduces the ranks' choice (MIN) and re-uploads -- the
+ * reference's MPI-collective setup of the solver (solver.py:32-73) in one flag.
+ */
+int nx_set_pc_kernels(nx_network_t* h, int32_t global);
+int nx_get_pc_kernels(nx_network_t* h, int32_t* lds);
+
+/*
  * Which solve nx_solve runs. solver = 0 (default): MINRES. solver = 1: the direct solve
  * the reference's default options ask for (ksp_type=preonly + pc_type=lu + MUMPS,
  * solver.py:58-65), specialised to the network: a block LU of [[M, K], [K^T, 0]] whose

@@ -78,6 +78,8 @@ _SIGS = {
     "nx_comm_count": (C.c_int, [_h, _pi32]),
     "nx_set_halo": (C.c_int, [_h, _i32, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
     "nx_set_cut": (C.c_int, [_h, _i32, _pi32, _pi32, _pi32, _pd]),
+    "nx_set_pc_kernels": (C.c_int, [_h, _i32]),
+    "nx_get_pc_kernels": (C.c_int, [_h, _pi32]),
     "nx_set_pc_dense": (C.c_int, [_h, _i32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                   _pi32, _pi32, _pi32, _pi32]),
     "nx_set_pc_exact": (C.c_int, [_h, _i32]),
@@ -460,6 +462,16 @@ class Handle:
                                 _ptr(send_idx if send_idx.size else np.zeros(1, np.int32),
                                      C.c_int32),
                                 _ptr(recv_off, C.c_int32)))
+
+    def set_pc_kernels(self, global_kernels: bool) -> None:
+        """The next preconditioner upload takes the global-memory sweeps (ranks agreeing)."""
+        check(lib().nx_set_pc_kernels(self.ptr, int(bool(global_kernels))))
+
+    def pc_lds(self) -> bool:
+        """The uploaded preconditioner runs the LDS sweep kernels."""
+        v = C.c_int32(0)
+        check(lib().nx_get_pc_kernels(self.ptr, C.byref(v)))
+        return bool(v.value)
 
     def set_cut(self, n_cut: int, lm_cut, gk_off, gk_row, gk_coef) -> None:
         """Cut bifurcations of a multi-rank problem (``nx_set_cut``): their multiplier rows

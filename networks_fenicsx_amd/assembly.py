@@ -32,7 +32,7 @@ import typing
 import numpy as np
 
 from . import _lib
-from .comm import GroupRankComm
+from .comm import MIN, GroupRankComm
 from .fem import Constant, Function, FunctionSpace
 from .element import stable_pair
 from .layout import LocalProblem, build_local_problem
@@ -385,6 +385,15 @@ class HydraulicNetworkAssembler:
         (always plain for general degrees: the tree preconditioner is P1/DG0's)."""
         on = bool(enable) and self._pc is not None
         self._handle.set_preconditioner(self._pc if on else None)
+        comm = self._network_mesh.comm
+        if on and self._nranks > 1 and not isinstance(comm, GroupRankComm):
+            # the sweep kernels are chosen per rank from its decomposition (LDS caps); the
+            # ranks' exchange schedules must agree: global-memory kernels everywhere if any
+            # rank cannot run the LDS ones (RankGroup does the same for its ranks)
+            lds = int(self._handle.pc_lds())
+            if int(comm.allreduce(lds, MIN)) == 0 and lds:
+                self._handle.set_pc_kernels(True)
+                self._handle.set_preconditioner(self._pc)
         self._pc_on = on
         return on
 

@@ -4091,6 +4091,7 @@ struct nx_network {
   // the rows it cannot form (left, n_left) and ||b||^2 of the first pass (dir_bb)
   bool fres_ok = false;
   int top_ts0 = 0, top_nt = 0;  // the top part's slots (host copy of top_lvl_off's ends)
+  int force_global = 0;  // nx_set_pc_kernels: the global-memory sweeps even where LDS fits
   int n_cu = 0;  // compute units of the device (topdown / coarsedown need one round of jobs)
   int* d_left = nullptr;
   int n_left = 0;
@@ -6353,6 +6354,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     }
   }
   if (const char* e = std::getenv("NXHIP_PC_GLOBAL")) lds = lds && std::atoi(e) == 0;
+  lds = lds && !h->force_global;  // the ranks chose together (nx_set_pc_kernels)
   // fused residual of the direct solve (one rank, LDS kernels): a junction's multiplier row
   // is formed by its job's down sweep when its chains -- the parent chain (lo = j) and the
   // hanging ones (up = j) -- are exactly slot_pchain / slot_dc and all in that job; every
@@ -6591,6 +6593,19 @@ NX_API int nx_get_solver(nx_network_t* h, int32_t* requested, int32_t* last_run)
 
 NX_API int nx_set_lean(int32_t enable) {
   lean_flag() = enable ? 1 : 0;
+  return NX_OK;
+}
+
+NX_API int nx_set_pc_kernels(nx_network_t* h, int32_t global) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  h->force_global = global ? 1 : 0;
+  h->sched_checked = false;
+  return NX_OK;
+}
+
+NX_API int nx_get_pc_kernels(nx_network_t* h, int32_t* lds) {
+  if (!h || !lds) return fail(NX_ERR_ARG, "null argument");
+  *lds = (h->pc && h->pc_lds) ? 1 : 0;
   return NX_OK;
 }
 

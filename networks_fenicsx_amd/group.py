@@ -37,6 +37,7 @@ class RankGroup:
         self.meshes = [NetworkMesh(graph if r == 0 else None, N=N, color_strategy=color_strategy,
                                    comm=group.comm(r)) for r in range(nranks)]
         self.assemblers = [HydraulicNetworkAssembler(m) for m in self.meshes]
+        self._agree_kernels()
         self._group: _lib.Group | None = None
         self.iterations = 0
         self.relres = float("nan")
@@ -58,6 +59,24 @@ class RankGroup:
         self._close_group()
         for a in self.assemblers:
             a.set_preconditioner(enable)
+        if enable:
+            self._agree_kernels()
+
+    def _agree_kernels(self) -> None:
+        """The ranks' sweep kernels (LDS or global memory, chosen per rank from its
+        decomposition) must agree -- their exchange schedules differ: if any rank cannot run
+        the LDS kernels, every rank takes the global-memory ones (what
+        HydraulicNetworkAssembler.set_preconditioner does over a real communicator)."""
+        pcs = [a for a in self.assemblers if a.preconditioned]
+        if len(pcs) < 2:
+            return
+        lds = [a.handle.pc_lds() for a in pcs]
+        if all(lds) or not any(lds):
+            return
+        for a, on in zip(pcs, lds):
+            if on:
+                a.handle.set_pc_kernels(True)
+                a.handle.set_preconditioner(a.tree_preconditioner)
 
     def set_direct(self, enable: bool) -> None:
         """The direct tree solve over all ranks (``nx_set_solver`` on every handle; it runs

@@ -274,6 +274,35 @@ def test_group_ranks_with_different_schedules_fail_loudly(monkeypatch):
         grp.close()
 
 
+def test_group_ranks_agree_on_sweep_kernels(monkeypatch):
+    """A rank that cannot run the LDS sweeps (here forced: the global-memory kernels on rank 1
+    only) makes every rank take the global-memory kernels (RankGroup._agree_kernels, over a
+    communicator HydraulicNetworkAssembler.set_preconditioner's MIN all-reduce), so the
+    solve runs -- MINRES, the direct solve needs the LDS sweeps across ranks -- instead of
+    failing on mismatched schedules."""
+    make, N, strategy, pbc = CASES["depth6_N40"]
+    G, mesh, Ab, bb, x_ref = _reference("depth6_N40")
+    grp = RankGroup(G, N, 2, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.assemble()
+        monkeypatch.setenv("NXHIP_PC_GLOBAL", "1")
+        grp.assemblers[1].set_preconditioner(True)
+        monkeypatch.delenv("NXHIP_PC_GLOBAL")
+        assert [a.handle.pc_lds() for a in grp.assemblers] == [True, False]
+        grp._agree_kernels()
+        assert [a.handle.pc_lds() for a in grp.assemblers] == [False, False]
+        grp.set_direct(True)
+        it, relres, conv = grp.solve(1e-12, 50000, 32)
+        assert conv and grp.solver_used == "minres"
+        x = np.zeros(Ab.shape[0])
+        for a, xl in zip(grp.assemblers, grp.solutions()):
+            x[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
+        assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    finally:
+        grp.close()
+
+
 def test_group_rank_without_dense_top_fails_loudly(monkeypatch):
     """The dense top part is decided per rank (nx_set_pc_dense); it drives who packs the
     halo and beta^2 (fuse_pack). A rank without it must make the solve fail through the
