@@ -1549,7 +1549,7 @@ constexpr int kCapDC = 768;   // down-chain entries per job
 constexpr int kCapT = 1152;   // top junction slots (host caps the top part at 1024)
 constexpr int kCapTDC = 2304; // top down-chain entries
 constexpr int kMaxTopLvl = 255;
-constexpr int kMaxNeed = 64;   // dense top: top values one job reads
+constexpr int kMaxNeed = 128;  // dense top: top values one job reads (precond.K_MAX_NEED)
 
 __device__ void pc_cpart_last(const PcArgs& pa, double* sA);
 
@@ -2649,8 +2649,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ int sP[kCapS];
   constexpr int kCT = DIRK ? 1 : kCapT;  // MINRES-only arrays (dense top, start's prep)
   __shared__ double sTa[kCT];  // dense top: a_s of every top slot
-  __shared__ int sNs[kMaxNeed];
-  __shared__ double sNz[kMaxNeed];
+  __shared__ double sNv[kCT];  // dense top: the values this job reads, by top position
   __shared__ double sGz[kCT], sGt[kCT], sGd[kCT];  // start only: G columns (prep)
   __shared__ int sGp[kCT], sGc[kCT];
   // one rank, direct (pa.topdown): the top part's solve in every workgroup (top_body)
@@ -2781,6 +2780,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     }
     const int n0 = pa.job_need_off[job];
     nneed = pa.job_need_off[job + 1] - n0;
+    for (int sl = threadIdx.x; sl < nt; sl += kPcThreads) sNv[sl] = 0.0;  // (never read)
     __syncthreads();
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     for (int k = wv; k < nneed; k += kPcThreads / 64) {  // one wave per needed row
@@ -2794,17 +2794,14 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
           const int rc = pa.top_rootc[t - ts0];
           if (rc >= 0) acc += pa.top_w[t - ts0] * (cfused ? sCz[rc] : pa.zc[rc]);
         }
-        sNs[k] = t;
-        sNz[k] = acc;
+        sNv[t - ts0] = acc;
       }
     }
     __syncthreads();
     // the job's own top rows: z and their share of r'.z
     for (int i = pa.job_tslot_off[job] + threadIdx.x; i < pa.job_tslot_off[job + 1]; i += kPcThreads) {
       const int t = pa.job_tslot[i];
-      double zt = 0.0;
-      for (int k = 0; k < nneed; ++k)
-        if (sNs[k] == t) zt = sNz[k];
+      double zt = sNv[t - ts0];  // own top slots are among the needed ones
       const int lam = pa.slot_lam[t];
       double yl = y[lam];
       if (lin) {  // several ranks: linear form, as for every other row of this kernel
@@ -2821,10 +2818,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     if (tdir) return tJ0[t - tts0];
     if (cdir) return tJ[t - tts0];
     if (!dense) return pa.slot_z[t];
-    double v = 0.0;
-    for (int k = 0; k < nneed; ++k)
-      if (sNs[k] == t) v = sNz[k];
-    return v;
+    return sNv[t - pa.top_ts0];  // O(1): the job may read up to kMaxNeed top values
   };
   // phase A: every slot's A, B, parent (local index, or the parent's value for the root)
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {

@@ -62,6 +62,7 @@ step (cut junctions grounded per rank) MINRES needs 5x the iterations at 8 ranks
 
 from __future__ import annotations
 
+import heapq
 from collections import deque
 from dataclasses import dataclass, field
 
@@ -262,7 +263,7 @@ class TreePreconditioner:
 
 
 # LDS caps of the preconditioner kernels (csrc/nxhip.hip): chains, junction slots and
-# down-chain entries per job. The top part's chains ride along round-robin, hence the
+# down-chain entries per job. The top part's chains ride along (balanced), hence the
 # margin on the chain cap.
 _CAP_CHAINS, _CAP_SLOTS, _CAP_DC = 512, 256, 768
 _CHAIN_MARGIN = 32
@@ -384,7 +385,8 @@ def _split_job_roots(roots, kids, sizes, n_top: int, max_top: int,
 
 def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
                               target_jobs: int = 256, max_top: int = 1024,
-                              coarse: CoarseStructure | None = None) -> TreePreconditioner:
+                              coarse: CoarseStructure | None = None,
+                              balanced: bool = True) -> TreePreconditioner:
     """Decompose the rank-local problem ``lp`` (:class:`layout.LocalProblem`).
 
     ``src``/``dst`` are the global node ids of all edges, ``degree`` the global degrees.
@@ -583,7 +585,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     slot_of[slots] = np.arange(slots.size)
 
     # chains: per lower job, the parent chains of its junctions + chains hanging from them
-    # (grounded / cycle-closing); the rest (top part chains) go round-robin to the jobs
+    # (grounded / cycle-closing); the rest (top part chains) go to the jobs (balanced)
     job_of_slot = np.full(slots.size, -1, dtype=np.int64)
     if n_lower:
         lv_len = np.diff(lvl_slot_off)
@@ -597,11 +599,24 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     chain_job[c2] = jup[c2]
     rest = np.flatnonzero(chain_job < 0)
     if n_lower > 0:
-        # chains of the top part ride along with the lower jobs (round-robin): one
+        # chains of the top part ride along with the lower jobs: one
         # workgroup per job and no extra jobs, so a launch has exactly n_lower
         # workgroups (<= #CUs); two extra chain-only workgroups started ~10 us late on
         # the GPU (scripts/phase_timing.py)
-        chain_job[rest] = np.arange(rest.size) % n_lower
+        if balanced:
+            # each to the job with the fewest chains (ties: lowest job), so no job runs an
+            # extra chain pass for one chain (8-rank C4: 129-chain jobs, 3 passes of 64 at
+            # N = 19, beside 127-chain ones); a job's top chains are top values it reads:
+            # past the dense top's K_MAX_NEED the decomposition is rebuilt round-robin
+            cnt = np.bincount(chain_job[chain_job >= 0], minlength=n_lower)
+            heap = [(int(c), j) for j, c in enumerate(cnt)]
+            heapq.heapify(heap)
+            for c in rest:
+                k, j = heapq.heappop(heap)
+                chain_job[c] = j
+                heapq.heappush(heap, (k + 1, j))
+        else:
+            chain_job[rest] = np.arange(rest.size) % n_lower
         n_jobs = n_lower
     else:
         per_job = max(16, int(np.ceil(E / max(1, target_jobs)))) if E else 1
@@ -640,6 +655,10 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         top_lvl_off=np.asarray(top_lvl_off, dtype=np.int32), n_jobs=int(n_jobs),
         n_slots=int(n_slots), tree_exact=n_cycle == 0)
     _dense_top_lists(pc)
+    if balanced and n_lower > 0 and pc.job_need_off.size > 1 and \
+            int(np.diff(pc.job_need_off).max()) > K_MAX_NEED:
+        return build_tree_preconditioner(lp, src, dst, degree, target_jobs, max_top, coarse,
+                                         balanced=False)
     if coarse is not None and coarse.n > 0:
         cid = coarse.cidx
         pc.n_coarse = coarse.n
@@ -653,6 +672,9 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         pc.c_child = coarse.child
         pc.c_lvl_off = coarse.lvl_off
     return pc
+
+
+K_MAX_NEED = 128  # csrc/nxhip.hip kMaxNeed: top values one job of the dense top reads
 
 
 def _dense_top_lists(pc: TreePreconditioner) -> None:
