@@ -1086,7 +1086,8 @@ template <int BS>
 __device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const double* sD,
                                    const double* sJ) {
   // small coarse sets: the buffer is built in LDS and the coarse chains' data loaded in
-  // parallel (thread = chain) before one thread sums them in a fixed order, then copied out
+  // parallel (thread = chain), then every coarse junction sums its chains in chain order
+  // (thread = junction; the additions of one thread walking the chains) and writes out
   // (was: built in global memory, two dependent round trips plus a read-modify-write per
   // chain on thread 0 -- ~14 us on the ranks holding the tree's upper part, 8-rank rehearsal)
   constexpr int kCapCC = 256;
@@ -1114,34 +1115,39 @@ __device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const doub
       sCib[i] = pa.chain_Ib[c];
     }
   __syncthreads();
-  if (threadIdx.x == 0) {  // few chains; serial keeps the sums in a fixed order
-    for (int i = 0; i < ncc; ++i) {
-      int t, b;
-      double g, it, ib;
-      if (lds) {
-        t = sCt[i];
-        b = sCb[i];
-        g = sCg[i];
-        it = sCit[i];
-        ib = sCib[i];
-      } else {
-        const int c = pa.cc_chain[i];
-        t = pa.cc_top[i];
-        b = pa.cc_bot[i];
-        g = 1.0 / pa.chain_T[c];
-        it = pa.chain_It[c];
-        ib = pa.chain_Ib[c];
+  if (lds) {  // thread = coarse junction k: its sums over the chains in chain order (the same
+              // additions in the same order as one thread walking the chains)
+    for (int k = threadIdx.x; k < nC; k += BS) {
+      double D = sBuf[k], J = sBuf[nC + k], Gk = sBuf[2 * nC + k];
+      for (int i = 0; i < ncc; ++i) {
+        const int t = sCt[i], b = sCb[i];
+        if (t == k) {
+          D += sCg[i];
+          J += sCit[i];
+        }
+        if (b == k) {
+          D += sCg[i];
+          J += sCib[i];
+          Gk = sCg[i];
+        }
       }
+      pa.cbuf[k] = D;
+      pa.cbuf[nC + k] = J;
+      pa.cbuf[2 * nC + k] = Gk;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) {  // large coarse sets: one thread, in global memory, same order
+    for (int i = 0; i < ncc; ++i) {
+      const int c = pa.cc_chain[i];
+      const int t = pa.cc_top[i], b = pa.cc_bot[i];
+      const double g = 1.0 / pa.chain_T[c];
       buf[t] += g;
       buf[b] += g;
-      buf[nC + t] += it;
-      buf[nC + b] += ib;
+      buf[nC + t] += pa.chain_It[c];
+      buf[nC + b] += pa.chain_Ib[c];
       buf[2 * nC + b] = g;
     }
-  }
-  if (lds) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < 3 * nC; i += BS) pa.cbuf[i] = sBuf[i];
   }
 }
 
