@@ -1074,6 +1074,10 @@ struct PcArgs {
   const int* slot_wave;
   int topdown;    // one rank, direct: the top part solved in every down sweep workgroup
   int coarsedown;  // several ranks, direct: the coarse step (k_pc_coarse) in every one
+  // small coarse forests (<= 64 junctions, <= kWaveKids children): per junction
+  // [level | nk << 8 | (parent + 1) << 12, children packed 8 bits each] (nx_set_coarse), so
+  // the one-wave coarse solve needs no staging (coarse_wave_solve)
+  const int* c_wave;
   int top_ts0, top_nt, top_dc0, top_ndc;  // the top part's slots and hanging-chain entries
 };
 
@@ -2557,11 +2561,57 @@ __device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* 
   }
 }
 
+// The coarse forest (<= 64 junctions) by one wave from registers: lane = coarse junction,
+// its level, parent and children from pa.c_wave, its all-reduced D, J, G passed in; the
+// same arithmetic in the same order as pc_coarse_lds. Writes z into sZc (lanes < n_coarse).
+__device__ __forceinline__ void coarse_wave_solve(const PcArgs& pa, int w0, int w1, double D,
+                                                  double J, double g0, double* sZc) {
+  if (threadIdx.x >= 64) return;
+  const int nC = pa.n_coarse, nl = pa.n_clvl;
+  const int cj = threadIdx.x;
+  const bool cmine = cj < nC;
+  const int clv = cmine ? (w0 & 0xff) : -1;
+  const int cnk = cmine ? ((w0 >> 8) & 0xf) : 0;
+  const int p = cmine ? ((w0 >> 12) & 0xff) - 1 : -1;
+  int cch[kWaveKids];
+#pragma unroll
+  for (int k = 0; k < kWaveKids; ++k) cch[k] = k < cnk ? (w1 >> (8 * k)) & 0xff : 0;
+  double gk[kWaveKids];
+#pragma unroll
+  for (int k = 0; k < kWaveKids; ++k) gk[k] = __shfl(g0, cch[k]);
+  int kmax = cnk;
+  for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+  for (int lv = nl - 1; lv >= 0; --lv) {
+    double dk[kWaveKids], jk[kWaveKids];
+#pragma unroll
+    for (int k = 0; k < kWaveKids; ++k) {
+      dk[k] = k < kmax ? __shfl(D, cch[k]) : 1.0;
+      jk[k] = k < kmax ? __shfl(J, cch[k]) : 0.0;
+    }
+    if (clv == lv) {
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k) {
+        if (k >= cnk) break;
+        D -= gk[k] * gk[k] / dk[k];
+        J += gk[k] * jk[k] / dk[k];
+      }
+    }
+  }
+  double zc = 0.0;
+  for (int lv = 0; lv < nl; ++lv) {  // root level first
+    const double zp = __shfl(zc, p >= 0 ? p : cj);
+    if (clv == lv) zc = (J + (p >= 0 ? g0 * zp : 0.0)) / D;
+  }
+  if (cmine) sZc[cj] = zc;
+}
+
 // Several ranks, direct solve (pa.coarsedown): k_pc_coarse's work in every down workgroup.
 // This thread's top slot (loaded at the sweep's start, beside its chain prefetch) ...
 struct CoarsePre {
   int k, par, lvo;
   double J, D, T;
+  int cw0, cw1;       // pa.c_wave: this lane's coarse junction (lanes < n_coarse)
+  double cD, cJ, cG;  // its all-reduced D, J and chain conductance to the parent
 };
 
 __device__ __forceinline__ void coarse_top_pre(const PcArgs& pa, CoarsePre& p) {
@@ -2572,6 +2622,19 @@ __device__ __forceinline__ void coarse_top_pre(const PcArgs& pa, CoarsePre& p) {
   p.D = 1.0;
   p.T = 1.0;
   p.lvo = sl <= pa.n_top_lvl ? pa.top_lvl_off[sl] : 0;
+  const int nC = pa.n_coarse;
+  p.cw0 = 0;
+  p.cw1 = 0;
+  p.cD = 1.0;
+  p.cJ = 0.0;
+  p.cG = 0.0;
+  if (pa.c_wave && sl < nC) {
+    p.cw0 = pa.c_wave[2 * sl];
+    p.cw1 = pa.c_wave[2 * sl + 1];
+    p.cD = pa.cbuf[sl];
+    p.cJ = pa.cbuf[nC + sl];
+    p.cG = pa.cbuf[2 * nC + sl];
+  }
   if (sl < nt) {
     const int j = ts0 + sl;
     p.k = pa.slot_cidx[j];
@@ -2593,7 +2656,12 @@ __device__ void coarse_top_block(const PcArgs& pa, const CoarsePre& p, double* c
   const int ntl = pa.n_top_lvl, ts0 = pa.top_ts0, nt = pa.top_nt;
   const int sl = threadIdx.x;
   if (sl <= ntl) tLv[sl] = p.lvo;
-  pc_coarse_lds(pa, cD, cJ, cZ);  // ends with a barrier (tLv is staged too)
+  if (pa.c_wave) {  // small forest: one wave straight from the prefetched registers
+    coarse_wave_solve(pa, p.cw0, p.cw1, p.cD, p.cJ, p.cG, cZ);
+    __syncthreads();
+  } else {
+    pc_coarse_lds(pa, cD, cJ, cZ);  // ends with a barrier (tLv is staged too)
+  }
   int mylv = -1;
   if (sl < nt)
     for (int q = 0; q < ntl; ++q)
@@ -6679,6 +6747,24 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   pa.c_child_off = up(c_child_off, n_coarse + 1);
   pa.c_child = up(ncl ? c_child : nullptr, ncl);
   pa.c_lvl_off = up(c_lvl_off, n_clvl + 1);
+  pa.c_wave = nullptr;
+  if (n_coarse <= 64 && n_clvl <= 255) {  // coarse_wave_solve's packed set-up
+    std::vector<int> cw(2 * std::max(1, (int)n_coarse), 0);
+    bool ok = true;
+    for (int lv = 0; lv < n_clvl && ok; ++lv)
+      for (int j = c_lvl_off[lv]; j < c_lvl_off[lv + 1] && ok; ++j) {
+        const int nk = c_child_off[j + 1] - c_child_off[j];
+        if (nk > kWaveKids) {
+          ok = false;
+          break;
+        }
+        cw[2 * j] = lv | (nk << 8) | ((c_parent[j] + 1) << 12);
+        int kids = 0;
+        for (int k = 0; k < nk; ++k) kids |= c_child[c_child_off[j] + k] << (8 * k);
+        cw[2 * j + 1] = kids;
+      }
+    if (ok) pa.c_wave = up(cw.data(), (int64_t)cw.size());
+  }
   double* cb = nullptr;  // [D | J | G | alpha]
   HIPCALL(hipMalloc((void**)&cb, sizeof(double) * (3 * n_coarse + 1)));
   HIPCALL(hipMemset(cb, 0, sizeof(double) * (3 * n_coarse + 1)));
