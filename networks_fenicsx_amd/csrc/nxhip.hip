@@ -2361,12 +2361,14 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
             z[lam] += zj;
           else
             z[lam] = zj;
+          pa.slot_z[ts0 + rsl] = zj;
         }
-        if (!down || blockIdx.x == 0) pa.slot_z[ts0 + rsl] = zj;
         if (!dir) part += sY[rsl] * zj;
       }
       __syncthreads();
     }
+    // down: workgroup 0's copy after the levels (no global store inside their barriers)
+    if (down && blockIdx.x == 0 && rmine) pa.slot_z[ts0 + rsl] = sJ0[rsl];
   } else
   for (int lv = 0; lv < nl; ++lv) {  // root level first: z_j = (J_j + g_par z_par) / D_j
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
@@ -2381,7 +2383,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
         else
           z[sLam[sl]] = zj;
       }
-      if (!down || blockIdx.x == 0) pa.slot_z[ts0 + sl] = zj;
+      if (!down || blockIdx.x == 0) pa.slot_z[ts0 + sl] = zj;  // (non-register path)
       if (!dir) part += sY[sl] * zj;
     }
     __syncthreads();
@@ -2678,10 +2680,13 @@ __device__ void coarse_top_block(const PcArgs& pa, const CoarsePre& p, double* c
         zj = num / p.D;
       }
       tZ[sl] = zj;
-      if (blockIdx.x == 0) pa.slot_z[ts0 + sl] = zj;
     }
     __syncthreads();
   }
+  // workgroup 0's copy for the reduce kernel, after the levels (no global store inside the
+  // level loop's barriers)
+  if (blockIdx.x == 0)
+    for (int i = sl; i < nt; i += kPcThreads) pa.slot_z[ts0 + i] = tZ[i];
 }
 
 // The fused halo pack (k_pack_beta's work) of the one-graph multi-rank solve: the last
