@@ -206,8 +206,10 @@ def _free_port() -> int:
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults: ~7 ms timed at C3 after ~4 ms of warm-up (the GPU idles through the host
+    # set-up; a few warm-up steps leave the first timed ones slow)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--levels", type=int, default=None,
                     help="tree generations (default: 15 at 1 GPU, 15 + log2(P) at P GPUs)")
     ap.add_argument("--N", type=int, default=None,
