@@ -225,6 +225,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
     ap.add_argument("--solver", choices=("direct", "minres"), default="direct",
                     help="the direct tree solve (reference default preonly + lu) or MINRES")
+    ap.add_argument("--allow-fallback", action="store_true",
+                    help="report a run whose direct solve fell back to MINRES instead of "
+                         "failing (exit status 3)")
     return ap.parse_args(argv)
 
 
@@ -341,6 +344,12 @@ def run(args, world: int) -> int:
     ms_per_step = 1e3 * elapsed / args.steps
     iters = state["it"]
     solver_used = "direct" if h.solver()[1] == 1 else "minres"
+    if direct and solver_used != "direct" and not args.allow_fallback:
+        # the ranks decide together (schedule signature), so every rank stops here
+        print(f"bench.py: rank {rank}: the direct solve was requested but the ranks ran "
+              "MINRES (a rank's decomposition cannot run it exactly); --allow-fallback "
+              "measures the fallback", file=sys.stderr, flush=True)
+        return 3
     # the committed PMC summaries profile the default workload (C3) on one GPU only
     default_workload = world == 1 and (levels, N) == (15, 15) and not args.no_pc
 

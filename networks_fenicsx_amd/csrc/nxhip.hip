@@ -6642,6 +6642,9 @@ NX_API int nx_set_pc_exact(nx_network_t* h, int32_t enable) {
   HIPCALL(hipStreamSynchronize(h->stream));
   CHECK(drop_handle_graphs(h));
   h->pa.exact = enable ? 1 : 0;
+  // direct_local() reads pa.exact: over RCCL the ranks' cached decision (direct_all, taken
+  // in check_schedules) must be taken again
+  h->sched_checked = false;
   return NX_OK;
 }
 

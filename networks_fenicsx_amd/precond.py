@@ -93,14 +93,23 @@ class CoarseStructure:
 
 
 def coarse_structure(src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
-                     owner: np.ndarray, nranks: int) -> CoarseStructure:
-    """Interface junctions + per-rank Steiner closure, as a level-ordered forest."""
+                     owner: np.ndarray, nranks: int,
+                     terminals: np.ndarray | None = None) -> CoarseStructure:
+    """Interface junctions + per-rank Steiner closure, as a level-ordered forest.
+
+    ``terminals``: junctions kept in the coarse set besides the interface ones (their
+    Steiner closure too). A one-rank problem has no interface junctions; forcing some lets
+    the multi-rank direct schedule run on a one-rank RCCL communicator (its GPU test)."""
     src = np.asarray(src, dtype=np.int64)
     dst = np.asarray(dst, dtype=np.int64)
     n_nodes, E = int(np.asarray(degree).size), int(src.size)
     is_bif = np.asarray(degree) > 1
     coarse = np.zeros(n_nodes, dtype=bool)
-    if nranks > 1 and E > 0:
+    forced = np.zeros(n_nodes, dtype=bool)
+    if terminals is not None:
+        forced[np.asarray(terminals, dtype=np.int64)] = True
+        forced &= is_bif
+    if (nranks > 1 or forced.any()) and E > 0:
         owner = np.asarray(owner, dtype=np.int64)
         ends = np.concatenate([src, dst])
         eo = np.concatenate([owner, owner])
@@ -109,7 +118,7 @@ def coarse_structure(src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
         mx = np.full(n_nodes, -1, dtype=np.int64)
         np.minimum.at(mn, ends[m], eo[m])
         np.maximum.at(mx, ends[m], eo[m])
-        terminal = is_bif & (mx > mn)
+        terminal = (is_bif & (mx > mn)) | forced
         coarse |= terminal
         order = np.argsort(owner, kind="stable")
         bounds = np.searchsorted(owner[order], np.arange(nranks + 1))

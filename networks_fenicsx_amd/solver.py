@@ -8,8 +8,10 @@ same constructor signature, ``assemble``, ``solve``, ``A``, ``b``, ``ksp`` and
 
 * ``ksp_type="preonly"`` (the reference default): a direct solve -- the block LU of the
   saddle-point system whose Schur complement the tree preconditioner inverts exactly
-  (``nx_set_solver``), one HIP graph, checked by the true residual. Used where it is exact
-  (one rank, trees); a graph with cycles, or a residual above ``ksp_rtol``, runs MINRES;
+  (``nx_set_solver``), checked by the true residual. Used where it is exact: a tree, on one
+  rank or on several (every rank's decomposition must run the LDS sweeps with the coarse
+  step; the ranks decide together); otherwise, or with a residual above ``ksp_rtol`` after
+  one refinement step, MINRES runs;
 * ``ksp_type="minres"`` (or any other iterative type): preconditioned MINRES -- CSR SpMV,
   fused vector updates and deterministic reductions in HIP graphs.
 

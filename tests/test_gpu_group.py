@@ -251,6 +251,97 @@ def test_rccl_single_rank_communicator(pc):
         asm.close()
 
 
+def _forced_coarse_direct(case: str, terminals, transport: str, then_lumped: bool = False):
+    """One rank whose coarse set is forced (``coarse_structure(terminals=...)``: junctions
+    kept out of the local eliminations exactly as interface junctions are), so the
+    multi-rank direct schedule (``launch_direct_team``) runs on one GPU. ``transport``:
+    ``"rccl"`` (a one-rank RCCL communicator) or ``"group"`` (a one-rank in-process group).
+    ``then_lumped``: after the first solve switch the preconditioner to the lumped mass and
+    solve again (the results are the second solve's).
+    Returns (solution, iterations, relres, solver used, graph mode, true residual)."""
+    from networks_fenicsx_amd import _lib
+    from networks_fenicsx_amd.precond import build_tree_preconditioner, coarse_structure
+
+    make, N, strategy, pbc = CASES[case]
+    mesh = NetworkMesh(make(), N=N, color_strategy=strategy)
+    src, dst = mesh.edges
+    cs = coarse_structure(src, dst, mesh.degrees, np.zeros(src.size, np.int64), 1,
+                          terminals=terminals)
+    assert cs.n >= len(terminals)
+    asm = HydraulicNetworkAssembler(mesh)
+    grp = None
+    try:
+        lp = asm.local_problem
+        h = asm.handle
+        if transport == "rccl":
+            h.comm_init(1, 0, _lib.comm_unique_id(), lp.peers, lp.send_off, lp.send_idx,
+                        lp.recv_off)
+        # no cut bifurcation on one rank: every multiplier row is this rank's own
+        h.set_cut(0, np.full(lp.lm_nodes.size, -1, np.int32), np.zeros(1, np.int32),
+                  np.zeros(0, np.int32), np.zeros(0))
+        asm._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, coarse=cs)
+        assert asm._pc.n_coarse == cs.n
+        asm.set_preconditioner(True)
+        asm.set_direct(True)
+        asm.compute_forms(p_bc_ex=pbc)
+        asm.assemble()
+        if transport == "group":
+            grp = _lib.Group([h])
+        it, rr, conv = (h if grp is None else grp).solve(1e-12, 50000, 4)
+        if then_lumped:
+            assert h.solver()[1] == 1
+            h.set_pc_exact(False)
+            asm.assemble()
+            it, rr, conv = (h if grp is None else grp).solve(1e-12, 50000, 4)
+        assert conv, (it, rr)
+        used = "direct" if h.solver()[1] == 1 else "minres"
+        out = (h.solution(), it, rr, used, h.graph_mode(), h.true_residual())
+        if grp is not None:
+            grp.close()
+            grp = None
+        return out
+    finally:
+        if grp is not None:
+            grp.close()
+        asm.close()
+
+
+@pytest.mark.parametrize("case,n_term", [("depth6_N40", 1), ("depth6_N40", 3),
+                                         ("arterial5_N40", 2)])
+def test_rccl_direct_single_rank_communicator(case, n_term):
+    """The RCCL direct solve -- the bench's default at P > 1 (launch_direct_team over a
+    communicator: the schedule signature's all-reduce with direct_all, the coarse
+    all-reduce, the cut rows' residual all-reduce, captured as one HIP graph) -- on a
+    one-rank communicator with a forced coarse set: solver_used == "direct", the RCCL graph
+    ran, the oracle's direct solution to 1e-10, and bit for bit the in-process group's
+    result (same kernels and decomposition, device-copy transport). Replaces the reference's
+    distributed solve (solver.py:127-132)."""
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    bif = np.asarray(mesh.bifurcation_values)
+    terms = bif[np.linspace(0, bif.size - 1, n_term).astype(np.int64)]
+    x1, it1, rr1, used1, graph1, true1 = _forced_coarse_direct(case, terms, "rccl")
+    assert used1 == "direct" and it1 in (1, 2), (used1, it1)
+    assert graph1, "the RCCL direct solve was not captured as a HIP graph"
+    assert np.linalg.norm(x1 - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    assert rr1 <= 1e-12 and true1 <= 1e-12, (rr1, true1)
+    x2, it2, rr2, used2, _, _ = _forced_coarse_direct(case, terms, "group")
+    assert used2 == "direct" and it2 == it1
+    np.testing.assert_array_equal(x1, x2)
+    assert rr1 == rr2
+
+
+def test_rccl_direct_follows_pc_mass_switch():
+    """ADVICE r02: over RCCL the ranks' direct decision is cached with the schedule check;
+    switching the preconditioner's mass to lumped (nx_set_pc_exact) after a direct solve
+    must invalidate it, so the next solve runs MINRES (the direct solve needs the exact
+    Schur complement)."""
+    G, mesh, Ab, bb, x_ref = _reference("depth6_N40")
+    terms = np.asarray(mesh.bifurcation_values)[:1]
+    x, it, rr, used, _, _ = _forced_coarse_direct("depth6_N40", terms, "rccl", then_lumped=True)
+    assert used == "minres"
+    assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
 def test_group_ranks_with_different_schedules_fail_loudly(monkeypatch):
     """A rank whose preconditioner runs another kernel schedule (here: the global-memory
     kernels on rank 1 only) must make the solve fail, not pair mismatched exchanges."""

@@ -265,3 +265,35 @@ def test_direct_tree_solve_model(case):
         assert err <= 1e-11, err
     else:
         assert err > 1e-6, err
+
+
+@pytest.mark.parametrize("case,n_term", [("depth6_N40", 1), ("depth6_N40", 3),
+                                         ("arterial5_N40", 2)])
+def test_forced_coarse_terminals_one_rank(case, n_term):
+    """coarse_structure(terminals=...) on one rank: the coarse set is the Steiner closure of
+    the forced junctions (one terminal: itself; several: the paths between them), and the
+    decomposition rooted at them keeps P^{-1} exact -- the coarse model (partials, coarse
+    forest solve, back-substitution) equals the single-rank application."""
+    from networks_fenicsx_amd.precond import coarse_structure
+
+    make, N, strategy, _ = CASES[case]
+    m, Ab, lp = _problem(make(), N, strategy)
+    src, dst = m.edges
+    bif = np.asarray(m.bifurcation_values)
+    terms = bif[np.linspace(0, bif.size - 1, n_term).astype(np.int64)]
+    cs = coarse_structure(src, dst, m.degrees, np.zeros(src.size, np.int64), 1, terminals=terms)
+    assert set(terms.tolist()) <= set(cs.node.tolist())
+    if n_term == 1:
+        assert cs.n == 1
+    # the coarse set is connected through coarse junctions only (Steiner closure): its
+    # forest has one root
+    assert int((cs.parent < 0).sum()) == 1
+    pc = build_tree_preconditioner(lp, src, dst, m.degrees, coarse=cs)
+    assert pc.n_coarse == cs.n
+    dq = lumped_mass(Ab, lp)
+    r = np.random.default_rng(5).standard_normal(Ab.shape[0])
+    st = pc_up_model(pc, lp, dq, r)
+    z = pc_finish_model(pc, lp, dq, st, st["partial"])
+    pc1 = build_tree_preconditioner(lp, src, dst, m.degrees)
+    z1 = apply_model(pc1, lp, dq, r)
+    assert np.linalg.norm(z - z1) <= 1e-12 * np.linalg.norm(z1)
