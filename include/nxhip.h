@@ -332,6 +332,12 @@ int nx_get_profile_direct(nx_network_t* h, double* ms4, int64_t* count);
  * kernel k_dir_publish_fr, which also forms the *n_left multiplier rows of the top part from
  * the CSR), 0 when a separate CSR SpMV (k_residual_ck) does. */
 int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left);
+/* What the last direct solve ran: *path = 1 for the fused step k_dir_step (one rank, the
+ * deferred assembly + the whole tree solve + the residual check + the published state in
+ * one launch; under profiling its time is the 1st of nx_get_profile_direct, the others 0),
+ * 0 for the separate launches (assembly, up sweep, down sweep, publish). Replaces nothing
+ * in the reference (PETSc's KSPSolve is one call: solver.py:127). */
+int nx_get_direct_path(nx_network_t* h, int32_t* path);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
 /* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,

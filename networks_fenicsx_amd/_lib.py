@@ -64,6 +64,7 @@ _SIGS = {
     "nx_get_profile": (C.c_int, [_h, _pd, _pi64, _pd, _pi64]),
     "nx_get_profile_direct": (C.c_int, [_h, _pd, _pi64]),
     "nx_get_direct_info": (C.c_int, [_h, _pi32, _pi32]),
+    "nx_get_direct_path": (C.c_int, [_h, _pi32]),
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
     "nx_bench_spmv_cold": (C.c_int, [_h, _i32, _pi32, _pd]),
@@ -359,6 +360,13 @@ class Handle:
         f, n = C.c_int32(0), C.c_int32(0)
         check(lib().nx_get_direct_info(self.ptr, C.byref(f), C.byref(n)))
         return {"fused_residual": bool(f.value), "n_left": int(n.value)}
+
+    def direct_path(self) -> str:
+        """What the last direct solve ran (nx_get_direct_path): ``"fused"`` (k_dir_step, one
+        launch) or ``"launches"`` (assembly, up, down, publish)."""
+        v = C.c_int32(0)
+        check(lib().nx_get_direct_path(self.ptr, C.byref(v)))
+        return "fused" if v.value == 1 else "launches"
 
     def reset_profile(self) -> None:
         check(lib().nx_reset_profile(self.ptr))

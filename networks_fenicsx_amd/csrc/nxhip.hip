@@ -50,6 +50,11 @@ thread_local std::string g_err;
 __device__ unsigned long long g_phase[128];
 __device__ unsigned long long g_wgs[8][512];  // per-workgroup start / end, last launch wins
 __device__ unsigned long long g_wge[8][512];
+__device__ unsigned long long g_dst[6][512];  // k_dir_step: per-workgroup stamps (nx_debug_dstep)
+#define NX_DSTAMP(k)                                                   \
+  do {                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 512) g_dst[(k)][blockIdx.x] = wall_clock64(); \
+  } while (0)
 #define NX_PHASE(slot)                                           \
   do {                                                           \
     if (blockIdx.x == 0) {                                       \
@@ -84,6 +89,9 @@ __device__ unsigned long long g_wge[8][512];
   } while (0)
 #define NX_PHASE_END(base) \
   do {                     \
+  } while (0)
+#define NX_DSTAMP(k) \
+  do {               \
   } while (0)
 #endif
 
@@ -446,6 +454,34 @@ __device__ __forceinline__ double wave_sum(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// Hand-offs between the workgroups of ONE launch (k_dir_step): write-through stores and
+// loads of agent scope (global_store / global_load ... sc1; MI355X_MICROARCH.md,
+// inter-workgroup visibility, "stores all sc1 / loads all sc1" with one agent-scope atomic
+// per storing workgroup after every storing wave's vmcnt(0)). No release fence, so the
+// XCD's L2 -- dirty with CSR values and x -- is not written back on the critical path.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __builtin_bit_cast(
+      double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool WT>
+__device__ __forceinline__ double ldv(const double* p) {
+  if constexpr (WT) return ld_wt(p);
+  return *p;
+}
+template <bool WT>
+__device__ __forceinline__ void stv(double* p, double v) {
+  if constexpr (WT) st_wt(p, v);
+  else *p = v;
+}
+// every wave's outstanding vector-memory operations (its write-through stores) complete
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Block of kBlock threads -> one partial per block.
 __device__ __forceinline__ void block_sum_store(double v, double* out) {
@@ -1195,7 +1231,6 @@ struct ChainLane {
     const int base = e * (2 * N + 1);
     const double* dqe = pa.dq + (int64_t)e * (N + 1);
     mo = active ? dqe[0] / 3.0 : 1.0;
-    double acc = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
       const int k = l * CPL + t;
@@ -1205,12 +1240,22 @@ struct ChainLane {
       dof_c[t] = base + 2 * kp + 1;
       dof_q[t] = base + 2 * qp;
       rho[t] = valid[t] ? dqe[qp] : 0.0;
-      acc += rho[t];
-      D[t] = acc;
     }
     has_last = active && (l == (N - 1) / CPL);
     dof_qN = base + 2 * (flip ? 0 : N);
     rhoN = has_last ? dqe[flip ? 0 : N] : 0.0;
+    finish();
+  }
+
+  // resistance distances and the chain total from rho / rhoN (k_dir_step sets those from
+  // the masses it just assembled: the same bits as setup's loads of dq)
+  __device__ __forceinline__ void finish() {
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      acc += rho[t];
+      D[t] = acc;
+    }
     const double excl = seg_incl_scan<W>(acc) - acc;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) D[t] += excl;
@@ -1684,7 +1729,7 @@ __device__ __forceinline__ void chain_cell_mo(const PcArgs& pa, const ChainLane<
 // multiplier couplings are +-1 (k_pattern's rows, chain order: s = -1 on a flipped chain).
 // Stores r, adds r^2 and vin^2 to rr / bb, and posts the chain's shares of its end junctions'
 // multiplier rows (A[lam_top, q_0] = -s, A[lam_bot, q_N] = +s) to sQt / sQb[lc].
-template <int W, int CPL>
+template <int W, int CPL, bool STORE = true>
 __device__ __forceinline__ void direct_residual(const PcArgs& pa, const ChainLane<W, CPL>& ch,
                                                 bool active, int flip, const double* vc,
                                                 const double* vq, double vqN, const double* xc,
@@ -1720,8 +1765,10 @@ __device__ __forceinline__ void direct_residual(const PcArgs& pa, const ChainLan
       acc = mol * xql + (mdl + md[t]) * xq[t] + mo[t] * qn;
     }
     const double rq = vq[t] - (acc + sg * (xc[t] - xcl));  // flux row: mass + s (p_k - p_{k-1})
-    pa.rres[ch.dof_c[t]] = rc;
-    pa.rres[ch.dof_q[t]] = rq;
+    if (STORE) {  // (a refinement step starts from r; k_dir_step does not keep it)
+      pa.rres[ch.dof_c[t]] = rc;
+      pa.rres[ch.dof_q[t]] = rq;
+    }
     rr += rc * rc + rq * rq;
     bb += vc[t] * vc[t] + vq[t] * vq[t];
   }
@@ -1737,7 +1784,7 @@ __device__ __forceinline__ void direct_residual(const PcArgs& pa, const ChainLan
         xcl = xc[t];
       }
     const double rq = vqN - ((mol * xql + mdl * xq[CPL]) + sg * (zb - xcl));
-    pa.rres[ch.dof_qN] = rq;
+    if (STORE) pa.rres[ch.dof_qN] = rq;
     rr += rq * rq;
     bb += vqN * vqN;
     sQb[lc] = sg * xq[CPL];
@@ -2132,26 +2179,31 @@ __device__ __forceinline__ void top_pre_idx(const PcArgs& pa, TopPre& p) {
   p.off = tid < nt ? pa.slot_dc_off[ts0 + tid] : 0;
 }
 
+// WT: the inputs were handed over inside the launch (k_dir_step): write-through loads; y
+// null: the multiplier rows' rhs is zero (the assembled b, first pass)
+template <bool WT = false>
 __device__ __forceinline__ void top_pre_val(const PcArgs& pa, const double* __restrict__ y,
                                             TopPre& p) {
   const int tid = threadIdx.x;
   const int ts0 = pa.top_ts0, ts1 = pa.top_ts0 + pa.top_nt;
   const bool dc = tid < pa.top_ndc, sl = tid < pa.top_nt;
   const bool low = dc && p.lo >= 0 && !(p.lo >= ts0 && p.lo < ts1);  // a lower job's root
-  p.T = dc ? pa.chain_T[p.c] : 1.0;
-  p.It = dc ? pa.chain_It[p.c] : 0.0;
-  p.Dl = low ? pa.slot_D[p.lo] : 1.0;
-  p.Jl = low ? pa.slot_J[p.lo] : 0.0;
-  p.y = sl ? y[p.lam] : 0.0;
-  p.Tp = sl && p.pcn >= 0 ? pa.chain_T[p.pcn] : 1.0;
-  p.Ib = sl && p.pcn >= 0 ? pa.chain_Ib[p.pcn] : 0.0;
+  p.T = dc ? ldv<WT>(pa.chain_T + p.c) : 1.0;
+  p.It = dc ? ldv<WT>(pa.chain_It + p.c) : 0.0;
+  p.Dl = low ? ldv<WT>(pa.slot_D + p.lo) : 1.0;
+  p.Jl = low ? ldv<WT>(pa.slot_J + p.lo) : 0.0;
+  p.y = sl && y ? y[p.lam] : 0.0;
+  p.Tp = sl && p.pcn >= 0 ? ldv<WT>(pa.chain_T + p.pcn) : 1.0;
+  p.Ib = sl && p.pcn >= 0 ? ldv<WT>(pa.chain_Ib + p.pcn) : 0.0;
 }
 
 // The top part's elimination and back-substitution (one workgroup of kTopThreads). down = 1:
 // run inside a direct down sweep (pa.topdown, one rank): the top values stay in LDS (sJ0)
 // for the workgroup's own chains, workgroup 0 stores them in slot_z (k_dir_publish_fr moves
 // them into x after the sweep), nothing else is written.
-template <bool MULTI>
+// WT (k_dir_step's last workgroup): the inputs come write-through (top_pre_val) and the
+// values go out write-through (slot_z) to the other workgroups of the launch.
+template <bool MULTI, bool WT = false>
 __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ y,
                                          const double* __restrict__ r2, double* __restrict__ z,
                                          const MrState* __restrict__ st,
@@ -2191,16 +2243,16 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     const bool pre = i == tid;
     const int c = pre ? p_c : pa.slot_dc[dc0 + i];
     const int lo = pre ? p_lo : pa.dc_lo[dc0 + i];
-    const double g = 1.0 / (pre ? pre_.T : pa.chain_T[c]);
-    const double it = pre ? pre_.It : pa.chain_It[c];
+    const double g = 1.0 / (pre ? pre_.T : ldv<WT>(pa.chain_T + c));
+    const double it = pre ? pre_.It : ldv<WT>(pa.chain_It + c);
     int child = -1;
     double dD = 0.0, dJ = it;
     if (lo >= ts0 && lo < ts1) {  // child above the cut: solved in the level sweep
       child = lo - ts0;
     } else if (lo >= 0) {
-      const double Dl = pre ? pre_.Dl : pa.slot_D[lo];
+      const double Dl = pre ? pre_.Dl : ldv<WT>(pa.slot_D + lo);
       dD = g * (1.0 - g / Dl);
-      dJ += g * (pre ? pre_.Jl : pa.slot_J[lo]) / Dl;
+      dJ += g * (pre ? pre_.Jl : ldv<WT>(pa.slot_J + lo)) / Dl;
     } else {
       dD = g;
     }
@@ -2214,7 +2266,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     const int j = ts0 + sl;
     const bool pre = sl == tid;
     const int lam = pre ? p_lam : pa.slot_lam[j];
-    double yl = pre ? pre_.y : y[lam];
+    double yl = pre ? pre_.y : (y ? y[lam] : 0.0);
     if (upd) {
       yl -= c2 * r2[lam];
       y[lam] = yl;
@@ -2223,9 +2275,9 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     sLam[sl] = lam;
     sY[sl] = yl;
     const int pcn = pre ? p_pcn : pa.slot_pchain[j];
-    const double gp = pcn >= 0 ? 1.0 / (pre ? pre_.Tp : pa.chain_T[pcn]) : 0.0;
+    const double gp = pcn >= 0 ? 1.0 / (pre ? pre_.Tp : ldv<WT>(pa.chain_T + pcn)) : 0.0;
     sD0[sl] = gp;
-    sJ0[sl] = yl + (pcn >= 0 ? (pre ? pre_.Ib : pa.chain_Ib[pcn]) : 0.0);
+    sJ0[sl] = yl + (pcn >= 0 ? (pre ? pre_.Ib : ldv<WT>(pa.chain_Ib + pcn)) : 0.0);
     const int par = pre ? p_par : pa.slot_parent[j];
     sPar[sl] = par >= 0 ? par - ts0 : -1;
     sGp[sl] = gp;
@@ -2361,7 +2413,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
             z[lam] += zj;
           else
             z[lam] = zj;
-          pa.slot_z[ts0 + rsl] = zj;
+          stv<WT>(pa.slot_z + ts0 + rsl, zj);
         }
         if (!dir) part += sY[rsl] * zj;
       }
@@ -2383,7 +2435,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
         else
           z[sLam[sl]] = zj;
       }
-      if (!down || blockIdx.x == 0) pa.slot_z[ts0 + sl] = zj;  // (non-register path)
+      if (!down || blockIdx.x == 0) stv<WT>(pa.slot_z + ts0 + sl, zj);  // (non-register path)
       if (!dir) part += sY[sl] * zj;
     }
     __syncthreads();
@@ -3102,6 +3154,774 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
     __syncthreads();
     pc_prep_in_block<kPcThreads>(pa, MULTI ? pa.mdense != 0 : pa.dense != 0, sTa, sGz, sGp, sGt,
                                  sGd, sGc);
+  }
+}
+
+// ======================================================================================
+// k_dir_step: the whole direct step of ONE rank in ONE launch (default; DESIGN.md section
+// 3c). It replaces the four launches k_assemble_seg -> k_pc_up_lds (mode 3) ->
+// k_pc_down_lds<.., true> (top part in every workgroup) -> k_dir_publish_fr. One workgroup
+// per job (n_jobs <= the CU count, so all are resident; the host checks):
+//   phase 1  every workgroup assembles its chains' edges -- CSR values, rhs, lumped mass,
+//            k_assemble's arithmetic bit for bit -- and a strided share of the multiplier
+//            rows, then runs the up sweep on the rhs it holds in registers (no reload); the
+//            top part's inputs (chains at top junctions, job roots) go out write-through;
+//   top      the workgroup arriving last (one agent-scope atomic each) solves the top part
+//            ONCE (top_body, write-through in and out) and raises a flag; the others wait
+//            for it (bounded: a workgroup that waits too long counts an error and leaves; the
+//            host then resets the counters and runs the four-launch path);
+//   phase 2  the down sweep from the job's own phase-1 data (same workgroup: no hand-off)
+//            and the top values: x, the fused true residual (not stored: a refinement step
+//            recomputes r), its partial sums and the flux-end shares of the rows no job forms
+//            written through; the last workgroup to arrive sums them in a fixed order and
+//            publishes the state (system-scope write-through, no L2 write-back).
+// b on the multiplier rows is zero (the assembly writes zeros there; assembly.py: L[lambda]
+// = 0), so no workgroup reads rhs rows another one wrote.
+// ======================================================================================
+struct DirStep {
+  const double* edge_x;
+  const double* edge_R;
+  const double* edge_bc;
+  const double* edge_f;  // per-edge source, or null: f everywhere
+  double f;
+  const int* edge_lm;
+  const int* edge_seg;
+  double* val;
+  double* rhs;
+  double* dq;
+  int64_t nnz_lm, B;
+  const double* lm_val;
+  double* val_lm;
+  double* rhs_lm;
+  double* x;
+  // the multiplier rows no job forms (left rows): the flux-end shares the jobs post
+  const int* chain_post;  // 2 per chain: post slot of its top / bottom end, -1
+  const int* left_off;    // n_left + 1: post range of every left row
+  int n_left;
+  double* post;
+  // hand-offs: [0] phase-1 arrivals, [1] phase-2 arrivals, [2] top flag, [3] wait errors
+  unsigned* sync;
+  unsigned epoch;  // launches since the counters were zero
+  // the published state
+  double rtol;
+  int seq_next;
+  int* seq;
+  MrState* mirror;
+  double* bbst;
+};
+
+constexpr int kDirWaitPolls = 1 << 20;  // s_sleep-paced polls before a waiting workgroup gives up
+// LDS of k_dir_step (doubles): the largest of phase 1, the top part and phase 2, then the
+// top values (kept from the hand-off into phase 2)
+constexpr int kDirLdsPhase1 = 3 * kCapC + 5 * kCapS + kCapDC + (kCapDC + kCapS + 1 + kCapLvl + 1 + 1) / 2 + 1;
+constexpr int kDirLdsTop = 6 * kCapT + 3 * kCapTDC + (2 * kCapT + kCapT + 1 + kCapTDC + kMaxTopLvl + 1 + 1) / 2 + 1;
+constexpr int kDirLdsPhase2 = 3 * kCapS + 2 * kCapC + (kCapS + kCapLvl + 1 + 1) / 2 + 1;
+constexpr int kDirLdsMain = kDirLdsTop > kDirLdsPhase1 ? (kDirLdsTop > kDirLdsPhase2 ? kDirLdsTop : kDirLdsPhase2)
+                                                       : (kDirLdsPhase1 > kDirLdsPhase2 ? kDirLdsPhase1 : kDirLdsPhase2);
+constexpr int kDirLds = kDirLdsMain + kCapT;
+
+// One chain's edge assembled in registers by its W lanes (lane = CPL cells, chain order):
+// cell tensors R h / 3, R h / 6 and the rhs as k_assemble computes them, the lumped flux
+// mass in k_assemble's order of additions (so ch.rho has dq's bits), the CSR segment of the
+// edge (unit stride over the lanes; the tensors of the entry's cells fetched by shuffles)
+// and the chain lane state the up sweep needs (ChainLane::setup without the loads).
+template <int W, int CPL>
+__device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& da, int c,
+                                              bool active, ChainLane<W, CPL>& ch,
+                                              double (&vc)[CPL], double (&vq)[CPL], double& vN,
+                                              int& flip) {
+#pragma clang fp contract(off)
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const int e = active ? pa.chain_edge[c] : 0;
+  flip = active ? pa.chain_flip[c] : 0;
+  double x0[3], x1[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    x0[i] = da.edge_x[6 * (int64_t)e + i];
+    x1[i] = da.edge_x[6 * (int64_t)e + 3 + i];
+  }
+  const double R = da.edge_R[e];
+  const double fe = da.edge_f ? da.edge_f[e] : da.f;
+  const double bc0 = da.edge_bc[2 * (int64_t)e], bc1 = da.edge_bc[2 * (int64_t)e + 1];
+  const int s = da.edge_lm[2 * (int64_t)e] >= 0;
+  const int sg0 = da.edge_seg[e], seglen = da.edge_seg[e + 1] - sg0;
+  const int64_t base = (int64_t)e * (2 * N + 1);
+  const int64_t qb = (int64_t)e * (N + 1);
+  const double invN = 1.0 / (double)N;
+  double md[CPL], mo[CPL];
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    const int k = l * CPL + t;
+    ch.valid[t] = active && k < N;
+    const int kp = flip ? N - 1 - k : k;
+    const int qp = flip ? N - k : k;
+    ch.dof_c[t] = (int)(base + 2 * kp + 1);
+    ch.dof_q[t] = (int)(base + 2 * qp);
+    md[t] = 0.0;
+    mo[t] = 0.0;
+    vc[t] = 0.0;
+    if (ch.valid[t]) {
+      double va[3], vb[3];
+      vertex(x0, x1, kp, N, invN, va);
+      vertex(x0, x1, kp + 1, N, invN, vb);
+      const double d0 = vb[0] - va[0], d1 = vb[1] - va[1], d2 = vb[2] - va[2];
+      const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+      md[t] = R * h / 3.0;
+      mo[t] = R * h / 6.0;
+      vc[t] = -(fe * h);  // negated pressure row: -(f h)
+      da.rhs[ch.dof_c[t]] = vc[t];
+    }
+  }
+  // lumped flux mass of chain flux k (between chain cells k - 1 and k), k_assemble's sums:
+  // edge flux q: d = md_q + mo_q, then (mo_{q-1} + md_{q-1}) + d; q = N: mo_{N-1} + md_{N-1}
+  const double mdP = __shfl_up(md[CPL - 1], 1, W), moP = __shfl_up(mo[CPL - 1], 1, W);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    ch.rho[t] = 0.0;
+    vq[t] = 0.0;
+    if (!ch.valid[t]) continue;
+    const int k = l * CPL + t;
+    const double mdq = t > 0 ? md[t - 1] : mdP, moq = t > 0 ? mo[t - 1] : moP;  // cell k - 1
+    double d;
+    if (!flip) {  // edge flux k: cells k - 1 and k
+      d = md[t] + mo[t];
+      if (k > 0) d = (moq + mdq) + d;
+    } else if (k > 0) {  // edge flux N - k: edge cells N - k (chain k - 1) and N - k - 1 (chain k)
+      d = mdq + moq;
+      d = (mo[t] + md[t]) + d;
+    } else {  // edge flux N: edge cell N - 1 (chain cell 0) only
+      d = mo[t] + md[t];
+    }
+    ch.rho[t] = d;
+    const int qp = flip ? N - k : k;
+    da.dq[qb + qp] = d;
+    vq[t] = qp == 0 ? bc0 : (qp == N ? bc1 : 0.0);
+    da.rhs[ch.dof_q[t]] = vq[t];
+  }
+  // chain flux N (the lane holding chain cell N - 1): edge flux N (its last cell) or, flipped,
+  // edge flux 0 (its first cell)
+  ch.has_last = active && (l == (N - 1) / CPL);
+  ch.dof_qN = (int)(base + 2 * (flip ? 0 : N));
+  ch.rhoN = 0.0;
+  vN = 0.0;
+  {
+    const int tl = (N - 1) - l * CPL;
+    double mdl = 0.0, mol = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t)
+      if (t == tl) {
+        mdl = md[t];
+        mol = mo[t];
+      }
+    if (ch.has_last) {
+      const double d = flip ? mdl + mol : mol + mdl;
+      ch.rhoN = d;
+      da.dq[qb + (flip ? 0 : N)] = d;
+      vN = flip ? bc0 : bc1;
+      da.rhs[ch.dof_qN] = vN;
+    }
+  }
+  // ChainLane::setup's mo: the edge's q_0 lumped mass / 3 (chain flux 0, or N when flipped)
+  const double dq0 = flip ? __shfl(ch.rhoN, (N - 1) / CPL, W) : __shfl(ch.rho[0], 0, W);
+  ch.mo = active ? dq0 / 3.0 : 1.0;
+  ch.finish();
+  // the edge's CSR segment: entry i (decode_entry) by lane i mod W; uniform trip count
+  // across the wave (the longest segment: 7N + 3) so every shuffle has all lanes
+  const int smax = 7 * N + 3;
+  for (int ib = 0; ib < smax; ib += W) {
+    const int i = ib + l;
+    const bool in = active && i < seglen;
+    const Entry en = decode_entry(in ? i : 0, N, s);
+    const int ca = en.cell, cb = min(en.cell + 1, N - 1);
+    const int ka = flip ? N - 1 - ca : ca, kb = flip ? N - 1 - cb : cb;
+    double mdA = 0.0, moA = 0.0, mdB = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      const double a = __shfl(md[t], ka / CPL, W), b = __shfl(mo[t], ka / CPL, W);
+      const double m2 = __shfl(md[t], kb / CPL, W);
+      if (ka % CPL == t) {
+        mdA = a;
+        moA = b;
+      }
+      if (kb % CPL == t) mdB = m2;
+    }
+    double v;
+    switch (en.vk) {
+      case V_P1: v = 1.0; break;
+      case V_M1: v = -1.0; break;
+      case V_MD: v = mdA; break;
+      case V_MO: v = moA; break;
+      default: v = mdA + mdB; break;  // interior diagonal: cells g and g+1
+    }
+    if (in) da.val[sg0 + i] = v;
+  }
+}
+
+// Phase 1: assembly + up sweep (k_pc_up_lds's mode-3 arithmetic; b_lambda = 0).
+template <int W, int CPL>
+__device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da,
+                                             double* lds) {
+  double* sT = lds;
+  double* sIt = sT + kCapC;
+  double* sIb = sIt + kCapC;
+  double* sD0 = sIb + kCapC;
+  double* sJ0 = sD0 + kCapS;
+  double* sD = sJ0 + kCapS;
+  double* sJ = sD + kCapS;
+  double* sIv = sJ + kCapS;
+  double* sG = sIv + kCapS;
+  int* sChild = reinterpret_cast<int*>(sG + kCapDC);
+  int* sOff = sChild + kCapDC;
+  int* sLvl = sOff + kCapS + 1;
+  const int job = blockIdx.x;
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  const int ts0 = pa.top_ts0, ts1 = pa.top_ts0 + pa.top_nt;
+  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
+  const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
+  const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
+  // prefetch of this thread's junction slot of phase A (independent of the chains)
+  constexpr int kPre = 4;
+  int p_pcn = -1, p_o0 = 0, p_o1 = 0, p_dc[kPre], p_lo[kPre];
+  if ((int)threadIdx.x < js1 - js0) {
+    const int j = js0 + threadIdx.x;
+    p_pcn = pa.slot_pchain[j];
+    p_o0 = pa.slot_dc_off[j];
+    p_o1 = pa.slot_dc_off[j + 1];
+#pragma unroll
+    for (int q = 0; q < kPre; ++q) {
+      const bool in = p_o0 + q < p_o1;
+      p_dc[q] = in ? pa.slot_dc[p_o0 + q] : 0;
+      p_lo[q] = in ? pa.dc_lo[p_o0 + q] : -1;
+    }
+  }
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    const int cu = active ? pa.chain_up[c] : -1, clo = active ? pa.chain_lo[c] : -1;
+    ChainLane<W, CPL> ch;
+    double vc[CPL], vq[CPL], vN;
+    int flip;
+    dir_chain_asm<W, CPL>(pa, da, c, active, ch, vc, vq, vN, flip);
+    double ytop = 0.0, ybot = 0.0;
+    direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
+    double sr = 0.0, srd = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      if (!ch.valid[t]) continue;
+      sr += vc[t];
+      srd += vc[t] * ch.D[t];
+    }
+    sr = seg_sum<W>(sr);
+    srd = seg_sum<W>(srd);
+    if (active && l == 0) {
+      const double ib = srd / ch.T;
+      const double it = (sr - ib) + ytop, ibe = ib + ybot;  // + the multiplier rows' share
+      sT[c - c0] = ch.T;
+      sIb[c - c0] = ibe;
+      sIt[c - c0] = it;
+      if ((cu >= ts0 && cu < ts1) || (clo >= ts0 && clo < ts1)) {  // the top part reads it
+        st_wt(pa.chain_T + c, ch.T);
+        st_wt(pa.chain_It + c, it);
+        st_wt(pa.chain_Ib + c, ibe);
+      }
+    }
+  }
+  if (lv1 <= lv0) return;
+  const int jwave = pa.job_wave ? pa.job_wave[job] : 0;
+  int wv0 = 0, wv1 = 0, wv2 = 0;
+  if (jwave > 0 && (int)threadIdx.x < js1 - js0) {
+    const int* w = pa.slot_wave + 3 * (int64_t)(js0 + threadIdx.x);
+    wv0 = w[0];
+    wv1 = w[1];
+    wv2 = w[2];
+  }
+  const int ns = js1 - js0;
+  const int dc0 = pa.slot_dc_off[js0];
+  __syncthreads();
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {  // phase A
+    const int j = js0 + sl;
+    const bool pre = sl == (int)threadIdx.x;
+    const int pcn = pre ? p_pcn : pa.slot_pchain[j];
+    double D0 = pcn >= 0 ? 1.0 / sT[pcn - c0] : 0.0;
+    double J0 = pcn >= 0 ? sIb[pcn - c0] : 0.0;  // (- b_lambda = -0 added: no change)
+    const int o0 = pre ? p_o0 : pa.slot_dc_off[j], o1 = pre ? p_o1 : pa.slot_dc_off[j + 1];
+    sOff[sl] = o0 - dc0;
+    for (int i = o0; i < o1; ++i) {
+      const int q = i - o0;
+      const bool pq = pre && q < kPre;
+      int dcq = 0, loq = -1;
+#pragma unroll
+      for (int r = 0; r < kPre; ++r)
+        if (r == q) {
+          dcq = p_dc[r];
+          loq = p_lo[r];
+        }
+      const int cl = (pq ? dcq : pa.slot_dc[i]) - c0;
+      const int lo = pq ? loq : pa.dc_lo[i];
+      const double g = 1.0 / sT[cl];
+      J0 += sIt[cl];
+      if (lo >= 0) {
+        sChild[i - dc0] = lo - js0;
+        sG[i - dc0] = g;
+      } else {
+        sChild[i - dc0] = -1;
+        D0 += g;
+      }
+    }
+    sD0[sl] = D0;
+    sJ0[sl] = J0;
+  }
+  if (threadIdx.x == 0) sOff[ns] = pa.slot_dc_off[js1] - dc0;
+  if ((int)threadIdx.x <= min(lv1 - lv0, kCapLvl)) sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
+  __syncthreads();
+  bool wave_lv = jwave > 0;
+  if (!wave_lv) {
+    int nkids = 0;
+    if ((int)threadIdx.x < ns)
+      for (int i = sOff[threadIdx.x]; i < sOff[threadIdx.x + 1]; ++i) nkids += sChild[i] >= 0;
+    wave_lv = __syncthreads_or(nkids > kWaveKids) == 0 && ns <= 64 && lv1 - lv0 <= kCapLvl;
+  }
+  if (wave_lv) {  // one wave: lane = slot, the children's values by shuffles
+    if (threadIdx.x < 64) {
+      const int sl = threadIdx.x;
+      const bool mine = sl < ns;
+      int mylv = -1;
+      int cl[kWaveKids];
+      double cg[kWaveKids];
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k) {
+        cl[k] = sl;
+        cg[k] = 0.0;
+      }
+      int nk = 0, kmax;
+      if (jwave > 0) {
+        kmax = jwave - 1;
+        if (mine) {
+          mylv = wv0 & 0xff;
+          nk = (wv0 >> 8) & 0xff;
+          const int cw[kWaveKids] = {wv1 & 0xffff, wv1 >> 16, wv2 & 0xffff, wv2 >> 16};
+#pragma unroll
+          for (int k = 0; k < kWaveKids; ++k)
+            if (k < nk) {
+              cl[k] = cw[k] & 63;
+              cg[k] = sG[cw[k] >> 6];
+            }
+        }
+      } else {
+        for (int q = 0; q < lv1 - lv0; ++q)
+          if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
+        if (mine)
+          for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+            const int chd = sChild[i];
+            if (chd < 0) continue;
+#pragma unroll
+            for (int k = 0; k < kWaveKids; ++k)
+              if (k == nk) {
+                cl[k] = chd;
+                cg[k] = sG[i];
+              }
+            ++nk;
+          }
+        kmax = nk;
+        for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+      }
+      double D = mine ? sD0[sl] : 1.0, J = mine ? sJ0[sl] : 0.0, iv = 1.0;
+      for (int q = lv1 - lv0 - 1; q >= 0; --q) {
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          if (k >= kmax) break;
+          const double Jc = __shfl(J, cl[k]);
+          const double Dc = __shfl(iv, cl[k]);
+          if (mylv == q && k < nk) {
+            const double g = cg[k];
+            D += g * (1.0 - g * Dc);
+            J += g * Jc * Dc;
+          }
+        }
+        if (mylv == q) iv = 1.0 / D;
+      }
+      if (mine) {
+        sD[sl] = D;
+        sJ[sl] = J;
+        sIv[sl] = iv;
+      }
+    }
+    __syncthreads();
+  } else {
+    for (int lv = lv1 - 1; lv >= lv0; --lv) {  // deepest level first
+      const int la = lv - lv0 <= kCapLvl ? sLvl[lv - lv0] : pa.lvl_slot_off[lv];
+      const int lb = lv - lv0 < kCapLvl ? sLvl[lv - lv0 + 1] : pa.lvl_slot_off[lv + 1];
+      for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
+        const int sl = j - js0;
+        double D = sD0[sl], J = sJ0[sl];
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int ch = sChild[i];
+          if (ch < 0) continue;
+          const double g = sG[i], iv = sIv[ch];
+          D += g * (1.0 - g * iv);
+          J += g * sJ[ch] * iv;
+        }
+        sIv[sl] = 1.0 / D;
+        sD[sl] = D;
+        sJ[sl] = J;
+      }
+      __syncthreads();
+    }
+  }
+  // back-substitution coefficients (own phase 2 reads them); the job's root level hands its
+  // (D, J) to the top part
+  const int root1 = sLvl[1];
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
+    const int j = js0 + sl;
+    const int pcn = pa.slot_pchain[j];
+    const double J = sJ[sl], iv = sIv[sl];
+    pa.slot_A[j] = J * iv;
+    pa.slot_B[j] = pcn >= 0 ? iv / sT[pcn - c0] : 0.0;
+    if (j < root1) {
+      st_wt(pa.slot_D + j, sD[sl]);
+      st_wt(pa.slot_J + j, J);
+    }
+  }
+}
+
+// Phase 2: the down sweep (k_pc_down_lds's mode-3 arithmetic with the fused residual, r not
+// stored); sTop: the top part's values by top position.
+template <int W, int CPL>
+__device__ __forceinline__ void dir_down_fused(const PcArgs& pa, const DirStep& da, double* lds,
+                                               const double* sTop) {
+  // (contraction as in k_pc_down_lds: the same x bit for bit)
+  double* sZ = lds;
+  double* sA = sZ + kCapS;
+  double* sB = sA + kCapS;
+  double* sQt = sB + kCapS;
+  double* sQb = sQt + kCapC;
+  int* sP = reinterpret_cast<int*>(sQb + kCapC);
+  int* sLvl = sP + kCapS;
+  __shared__ double s_w[2 * (kPcThreads / 64)];
+  const int job = blockIdx.x;
+  const int ts0 = pa.top_ts0;
+  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
+  const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
+  const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
+  const int ns = js1 - js0;
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  double* __restrict__ x = da.x;
+  const double* __restrict__ b = da.rhs;  // this job's own rows (written by this workgroup)
+  ChainLane<W, CPL> ch;
+  double vc[CPL], vq[CPL], vN = 0.0, mo_r[CPL];
+  int ch_up = -1, ch_lo = -1, flip = 0, post_t = -1, post_b = -1;
+  auto load_lane = [&](int c, bool active) {
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      vc[t] = ch.valid[t] ? b[ch.dof_c[t]] : 0.0;
+      vq[t] = ch.valid[t] ? b[ch.dof_q[t]] : 0.0;
+    }
+    vN = ch.has_last ? b[ch.dof_qN] : 0.0;
+    ch_up = active ? pa.chain_up[c] : -1;
+    ch_lo = active ? pa.chain_lo[c] : -1;
+    flip = active ? pa.chain_flip[c] : 0;
+    post_t = active ? da.chain_post[2 * (int64_t)c] : -1;
+    post_b = active ? da.chain_post[2 * (int64_t)c + 1] : -1;
+  };
+  ch.setup(pa, c0 + seg, c0 + seg < c1);
+  load_lane(c0 + seg, c0 + seg < c1);
+  int p_par = -1, p_lam = 0, p_lv = -1;
+  double p_A = 0.0, p_B = 0.0;
+  const bool hwave = pa.job_wave != nullptr && lv1 > lv0 && pa.job_wave[job] > 0;
+  if ((int)threadIdx.x < ns) {
+    const int j = js0 + threadIdx.x;
+    p_par = pa.slot_parent[j];
+    p_A = pa.slot_A[j];
+    p_B = pa.slot_B[j];
+    p_lam = pa.slot_lam[j];
+    if (hwave) p_lv = pa.slot_wave[3 * (int64_t)j] & 0xff;
+  }
+  // phase A: every slot's A, B, parent (local index, or the parent's value: a top slot)
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
+    const int j = js0 + sl;
+    const bool pre = sl == (int)threadIdx.x;
+    const int p = pre ? p_par : pa.slot_parent[j];
+    const bool local = p >= js0 && p < js1;
+    sA[sl] = pre ? p_A : pa.slot_A[j];
+    sB[sl] = pre ? p_B : pa.slot_B[j];
+    sP[sl] = local ? p - js0 : -1;
+    sZ[sl] = (!local && p >= 0) ? sTop[p - ts0] : 0.0;
+  }
+  if (lv1 > lv0 && (int)threadIdx.x <= min(lv1 - lv0, kCapLvl))
+    sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
+  __syncthreads();
+  if (ns <= 64 && lv1 - lv0 <= kCapLvl) {  // one wave: lane = slot, parent by shuffle
+    if (threadIdx.x < 64) {
+      const int sl = threadIdx.x;
+      const bool mine = sl < ns;
+      int mylv = hwave ? p_lv : -1;
+      if (!hwave)
+        for (int q = 0; q < lv1 - lv0; ++q)
+          if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
+      const double A = mine ? sA[sl] : 0.0, Bv = mine ? sB[sl] : 0.0;
+      const int p = mine ? sP[sl] : -1;
+      double zv = mine ? sZ[sl] : 0.0;
+      for (int q = 0; q < lv1 - lv0; ++q) {
+        const double zp = __shfl(zv, p >= 0 ? p : sl);
+        if (mylv == q) zv = A + Bv * zp;
+      }
+      if (mine) sZ[sl] = zv;
+    }
+    __syncthreads();
+  } else {
+    for (int lv = lv0; lv < lv1; ++lv) {  // root level first
+      const int la = lv - lv0 <= kCapLvl ? sLvl[lv - lv0] : pa.lvl_slot_off[lv];
+      const int lb = lv - lv0 < kCapLvl ? sLvl[lv - lv0 + 1] : pa.lvl_slot_off[lv + 1];
+      for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
+        const int sl = j - js0;
+        const int p = sP[sl];
+        sZ[sl] = sA[sl] + sB[sl] * (p >= 0 ? sZ[p] : sZ[sl]);
+      }
+      __syncthreads();
+    }
+  }
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
+    const bool pre = sl == (int)threadIdx.x;
+    x[pre ? p_lam : pa.slot_lam[js0 + sl]] = sZ[sl];
+  }
+  double rr = 0.0, bb = 0.0;
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    if (cb != c0) {  // more chains than one pass: set up and load here
+      ch.setup(pa, c, active);
+      load_lane(c, active);
+    }
+    chain_cell_mo<W, CPL>(pa, ch, c, active, flip, mo_r);
+    const int up = ch_up, lo = ch_lo;
+    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : sTop[up - ts0];
+    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : sTop[lo - ts0];
+    const double T = ch.T, iT = 1.0 / T;
+    double bcv[CPL], a[CPL], bs[CPL], zc[CPL];
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) bcv[t] = vc[t];
+    {
+      double ytop, ybot;
+      direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
+    }
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      a[t] = (T - ch.D[t]) * vc[t];
+      bs[t] = ch.D[t] * vc[t];
+      sa += a[t];
+      sb += bs[t];
+    }
+    const double ia = seg_incl_scan<W>(sa), ibv = seg_incl_scan<W>(sb);
+    const double Atot = seg_sum<W>(sa);
+    double pa_ = ia - sa, pb_ = ibv - sb;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      pa_ += a[t];
+      const double suffix = Atot - pa_ + a[t];
+      const double prefix = pb_;
+      pb_ += bs[t];
+      zc[t] = 0.0;
+      if (!ch.valid[t]) continue;
+      const double Dk = ch.D[t];
+      double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      zk -= ch.mo * vc[t];  // the consistent-mass Schur complement
+      zc[t] = zk;
+      x[ch.dof_c[t]] = zk;
+    }
+    double xv[CPL + 1];
+    direct_flux_cons<W, CPL>(ch, flip, bcv, vq, vN, zt, zb, xv);
+#pragma unroll
+    for (int t = 0; t <= CPL; ++t) {
+      const bool on = t < CPL ? ch.valid[t] : ch.has_last;
+      if (on) x[t < CPL ? ch.dof_q[t] : ch.dof_qN] = xv[t];
+    }
+    direct_residual<W, CPL, false>(pa, ch, active, flip, bcv, vq, vN, zc, xv, zt, zb, mo_r, rr, bb,
+                                   sQt, sQb, c - c0);
+    // the chain's ends at rows no job forms: their flux shares, write-through
+    if (active && l == 0 && post_t >= 0) st_wt(da.post + post_t, sQt[c - c0]);
+    if (ch.has_last && post_b >= 0) st_wt(da.post + post_b, sQb[c - c0]);
+  }
+  __syncthreads();
+  // multiplier rows of the junctions whose chains are all in this job (b_lambda = 0)
+  if ((int)threadIdx.x < ns) {
+    const int j = js0 + threadIdx.x;
+    if (pa.slot_rloc[j]) {
+      const int pc = pa.slot_pchain[j];
+      double acc = pc >= 0 ? sQb[pc - c0] : 0.0;
+      for (int i = pa.slot_dc_off[j]; i < pa.slot_dc_off[j + 1]; ++i) acc += sQt[pa.slot_dc[i] - c0];
+      const double rl = 0.0 - acc;
+      rr += rl * rl;
+    }
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_w[threadIdx.x >> 6] = rr;
+    s_w[kPcThreads / 64 + (threadIdx.x >> 6)] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tr = s_w[0], tb = s_w[kPcThreads / 64];
+    for (int i = 1; i < kPcThreads / 64; ++i) {
+      tr += s_w[i];
+      tb += s_w[kPcThreads / 64 + i];
+    }
+    st_wt(pa.rpart + job, tr);
+    st_wt(pa.rpart + pa.n_jobs + job, tb);
+  }
+}
+
+// The state to the host-coherent mirror with system-scope write-through stores (no release
+// fence: this XCD's L2, dirty with x, is not written back first), the stamp after them.
+__device__ __forceinline__ void publish_wt(const MrState& s, int q, int* seq, MrState* mirror) {
+  *seq = q;  // device count of published states (read by later launches)
+  MrState o = s;
+  o.pad = 0;
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&o);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(mirror);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(MrState) / 8); ++i)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  vm_drain();
+  __hip_atomic_store(&mirror->pad, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The last workgroup of phase 2: the partials and the left rows' shares, fixed order.
+__device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirStep& da) {
+#pragma clang fp contract(off)
+  __shared__ double s_r[kPcThreads / 64], s_b[kPcThreads / 64];
+  const int nj = pa.n_jobs;
+  double rr = 0.0, bb = 0.0;
+  for (int i = threadIdx.x; i < nj; i += kPcThreads) {
+    rr += ld_wt(pa.rpart + i);
+    bb += ld_wt(pa.rpart + nj + i);
+  }
+  for (int i = threadIdx.x; i < da.n_left; i += kPcThreads) {
+    double acc = 0.0;
+    for (int k = da.left_off[i]; k < da.left_off[i + 1]; ++k) acc += ld_wt(da.post + k);
+    const double rv = 0.0 - acc;  // b = 0 on the multiplier rows
+    rr += rv * rv;
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_r[threadIdx.x >> 6] = rr;
+    s_b[threadIdx.x >> 6] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    rr = 0.0;
+    bb = 0.0;
+    for (int w = 0; w < kPcThreads / 64; ++w) {
+      rr += s_r[w];
+      bb += s_b[w];
+    }
+    da.bbst[0] = bb;
+    MrState s{};
+    s.beta1 = sqrt(bb);
+    s.relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
+    s.rtol = da.rtol;
+    s.it = 1;
+    s.done = 1;
+    s.converged = s.relres <= da.rtol ? 1 : 0;
+    publish_wt(s, da.seq_next, da.seq, da.mirror);
+  }
+}
+
+template <int W, int CPL>
+__global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) {
+  __shared__ double smem[kDirLds];
+  __shared__ int sFlag;
+  const int job = blockIdx.x;
+  const int nj = pa.n_jobs;
+  const unsigned last = da.epoch * (unsigned)nj + (unsigned)(nj - 1);
+  NX_DSTAMP(0);
+  // the multiplier rows (+-1 values, zero rhs): a strided share per workgroup
+  const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
+  for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
+    if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
+    if (i < da.B) da.rhs_lm[i] = 0.0;
+  }
+  dir_up_fused<W, CPL>(pa, da, smem);
+  double* sTop = smem + kDirLdsMain;
+  const int nt = pa.top_nt, ts0 = pa.top_ts0;
+  if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
+    vm_drain();
+    __syncthreads();
+    NX_DSTAMP(1);
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(da.sync, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      sFlag = old == last ? 1 : 0;
+    }
+    __syncthreads();
+    if (sFlag) {
+      double* t = smem;
+      TopLds L;
+      L.sD0 = t; t += kCapT;
+      L.sJ0 = t; t += kCapT;
+      L.sD = t; t += kCapT;
+      L.sJ = t; t += kCapT;
+      L.sGp = t; t += kCapT;
+      L.sY = t; t += kCapT;
+      L.sG = t; t += kCapTDC;
+      L.sDD = t; t += kCapTDC;
+      L.sDJ = t; t += kCapTDC;
+      int* u = reinterpret_cast<int*>(t);
+      L.sPar = u; u += kCapT;
+      L.sLam = u; u += kCapT;
+      L.sOff = u; u += kCapT + 1;
+      L.sChild = u; u += kCapTDC;
+      L.sLv = u;
+      TopPre pre;
+      top_pre_idx(pa, pre);
+      top_pre_val<true>(pa, nullptr, pre);
+      top_body<false, true>(pa, nullptr, nullptr, da.x, nullptr, nullptr, 0, nullptr, nullptr,
+                            kModeDirect, L, false, pre);
+      vm_drain();
+      __syncthreads();
+      NX_DSTAMP(5);
+      if (threadIdx.x == 0)
+        __hip_atomic_store(da.sync + 2, da.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (threadIdx.x == 0) {
+      int ok = 0;
+      for (int k = 0; k < kDirWaitPolls; ++k) {
+        if (__hip_atomic_load(da.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            da.epoch + 1u) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sFlag = ok ? 1 : -1;
+    }
+    __syncthreads();
+    if (sFlag < 0) return;  // the top values never came (the host sees no published state)
+    NX_DSTAMP(2);
+    for (int i = threadIdx.x; i < nt; i += kPcThreads) sTop[i] = ld_wt(pa.slot_z + ts0 + i);
+    __syncthreads();
+  }
+  dir_down_fused<W, CPL>(pa, da, smem, sTop);
+  // hand-off 2: the residual partials and shares -> the last workgroup publishes
+  vm_drain();
+  __syncthreads();
+  NX_DSTAMP(3);
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(da.sync + 1, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    sFlag = old == last ? 1 : 0;
+  }
+  __syncthreads();
+  if (sFlag) {
+    dir_publish_fused(pa, da);
+    NX_DSTAMP(4);
   }
 }
 
@@ -4169,6 +4989,18 @@ struct nx_network {
   int* d_left = nullptr;
   int n_left = 0;
   double* dir_bb = nullptr;
+  // the fused direct step (k_dir_step, one rank): per chain the post slots of its ends at
+  // rows no job forms, every left row's post range, the posts, the hand-off counters and
+  // the launches since they were zero (all in pc_bufs; reset with every upload)
+  bool dstep_ok = false;   // the decomposition allows it (nx_set_preconditioner)
+  bool dstep_off = false;  // a launch gave up waiting (workgroups not co-resident)
+  int* d_chain_post = nullptr;
+  int* d_left_off = nullptr;
+  double* d_post = nullptr;
+  unsigned* d_dsync = nullptr;
+  unsigned dstep_epoch = 0;
+  bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
+  int last_dir_path = 0;   // the last direct solve: 0 four launches, 1 k_dir_step
   std::vector<int> left_host;  // the rows of d_left
   // several ranks, direct (nx_set_cut): the multiplier rows of the K cut bifurcations are
   // completed inside the residual's all-reduce (no halo of x): per left row its cut index,
@@ -5104,7 +5936,7 @@ bool defer_ok(const nx_network* h) {
     const char* e = std::getenv("NXHIP_DEFER");
     return e == nullptr || std::atoi(e) != 0;
   }();
-  return env && !h->fe && !h->prof && h->nranks == 1 && h->comm == nullptr && h->group == nullptr;
+  return env && !h->fe && h->nranks == 1 && h->comm == nullptr && h->group == nullptr;
 }
 
 int flush_assembly(nx_network* h) {
@@ -5112,7 +5944,15 @@ int flush_assembly(nx_network* h) {
   const int lhs = h->pend_lhs, rhs = h->pend_rhs;
   h->pend_lhs = h->pend_rhs = 0;
   CHECK(set_device(h));
-  return launch_assembly(h, lhs, rhs);
+  CHECK(launch_assembly(h, lhs, rhs));
+  if (h->prof && (h->E > 0 || h->fe)) {  // profiling: the assembly kernel's own events
+    HIPCALL(hipEventSynchronize(h->ev[1]));
+    float ms = 0.f;
+    HIPCALL(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    h->asm_ms += ms;
+    h->asm_cnt += 1;
+  }
+  return NX_OK;
 }
 
 }  // namespace
@@ -5286,6 +6126,12 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const int cb = grid_of(h->E, G);
   double* yq = h->vb[1];
   double* w = h->vb[0];
+  if (refine && h->need_r) {  // the fused step (k_dir_step) kept no residual: r = b - A x
+    const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
+    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
+    h->need_r = false;
+  }
   // refine: the previous pass's residual check left r = b - A x in tmp
   const double* bin = refine ? h->tmp : h->rhs;
   if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
@@ -5334,6 +6180,47 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
                         h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));  // r kept: refinement
   hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
                      nrb, rtol, h->d_seq, h->d_last);
+}
+
+// The fused direct step (k_dir_step): one rank, the deferred assembly pending, the LDS
+// sweeps with the fused residual, one round of jobs (all resident), direct launches (a graph
+// would freeze the launch count), not disabled by a failed launch or NXHIP_DIR_FUSED=0.
+int dir_graph_flag();
+bool dstep_on(const nx_network* h) {
+  const char* e = std::getenv("NXHIP_DIR_FUSED");  // read per solve: tests switch it
+  const bool env = e == nullptr || std::atoi(e) != 0;
+  return env && h->dstep_ok && !h->dstep_off && h->pc_lds && h->fres_ok && h->pa.exact &&
+         h->pc_jobs > 0 && h->pc_jobs <= h->n_cu && h->comm == nullptr && h->group == nullptr &&
+         h->nranks == 1 && !dir_graph_flag();
+}
+
+template <int W, int CPL>
+void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
+  DirStep da{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
+             h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
+             h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
+             h->d_post, h->d_dsync, h->dstep_epoch, rtol, h->seq + 1, h->d_seq, h->d_last,
+             h->dir_bb};
+  hipExtLaunchKernelGGL((k_dir_step<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0, h->stream,
+                        prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0, h->pa, da);
+}
+
+// Launch k_dir_step and wait for its published state (the host's sequence advances).
+int run_dstep(nx_network* h, double rtol, bool prof) {
+  switch (h->pc_variant) {
+    case 0: launch_dstep_wc<16, 1>(h, rtol, prof); break;
+    case 1: launch_dstep_wc<16, 2>(h, rtol, prof); break;
+    case 2: launch_dstep_wc<16, 4>(h, rtol, prof); break;
+    case 3: launch_dstep_wc<64, 2>(h, rtol, prof); break;
+    case 5: launch_dstep_wc<8, 2>(h, rtol, prof); break;
+    case 8: launch_dstep_wc<64, 8>(h, rtol, prof); break;
+    case 9: launch_dstep_wc<64, 16>(h, rtol, prof); break;
+    default: launch_dstep_wc<64, 4>(h, rtol, prof); break;
+  }
+  HIPCALL(hipGetLastError());
+  h->dstep_epoch += 1;
+  h->seq += 1;
+  return wait_published(h);
 }
 
 int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
@@ -5494,9 +6381,48 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   const bool multi = team_multi(t);
   nx_network* h = t.hs[0];
   LeanGraphs& lg = lean_of(t);
-  if (!multi && h->prof) {  // eager, with events bound to the sweeps' and the residual's dispatches
-    if (!h->dev[0])
-      for (auto& e : h->dev) HIPCALL(hipEventCreate(&e));
+  const bool prof1 = !multi && h->prof;  // events bound to the dispatches (profiling)
+  if (prof1 && !h->dev[0])
+    for (auto& e : h->dev) HIPCALL(hipEventCreate(&e));
+  const bool with_asm = !multi && h->pend_lhs && h->pend_rhs;  // deferred assembly heads it
+  h->last_dir_path = 0;
+  if (with_asm && dstep_on(h)) {  // the fused step: assembly + solve + check in one launch
+    const int rc = run_dstep(h, rtol, prof1);
+    if (rc == NX_OK) {
+      h->pend_lhs = h->pend_rhs = 0;
+      h->last_dir_path = 1;
+      if (prof1) {
+        HIPCALL(hipEventSynchronize(h->dev[1]));
+        float ms = 0.f;
+        HIPCALL(hipEventElapsedTime(&ms, h->dev[0], h->dev[1]));
+        h->dir_ms[0] += ms;
+        h->dir_cnt += 1;
+      }
+      MrState s = *h->h_last;
+      if (!s.converged && s.relres == s.relres) {  // one refinement step (forms r first)
+        h->need_r = true;
+        CHECK(launch_direct(h, rtol, 1));
+        h->seq += 1;
+        CHECK(wait_published(h));
+        s = *h->h_last;
+        s.it = 2;
+      }
+      if (iters) *iters = s.it;
+      if (relres) *relres = s.relres;
+      if (converged) *converged = s.converged;
+      return NX_OK;
+    }
+    if (rc != NX_ERR_STATE) return rc;
+    // a workgroup gave up waiting (they were not all resident): reset the hand-off counters
+    // and take the four-launch path from now on (the assembly is still pending)
+    (void)hipGetLastError();
+    HIPCALL(hipStreamSynchronize(h->stream));
+    HIPCALL(hipMemset(h->d_dsync, 0, 4 * sizeof(unsigned)));
+    h->dstep_epoch = 0;
+    h->dstep_off = true;
+  }
+  if (prof1) {  // eager, with events bound to the sweeps' and the residual's dispatches
+    CHECK(flush_assembly(h));
     CHECK(launch_direct(h, rtol, 0, true));
     h->seq += 1;
     CHECK(wait_published(h));
@@ -5519,7 +6445,6 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     if (converged) *converged = s.converged;
     return NX_OK;
   }
-  const bool with_asm = !multi && h->pend_lhs && h->pend_rhs;  // deferred assembly heads it
   for (int r = 0; r < t.P; ++r)
     if (!with_asm) CHECK(flush_assembly(t.hs[r]));
   // (measured and kept out: forking the CSR values' assembly onto a second graph branch
@@ -6145,6 +7070,12 @@ NX_API int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left) 
   return NX_OK;
 }
 
+NX_API int nx_get_direct_path(nx_network_t* h, int32_t* path) {
+  if (!h || !path) return fail(NX_ERR_ARG, "null argument");
+  *path = h->last_dir_path;
+  return NX_OK;
+}
+
 NX_API int nx_reset_profile(nx_network_t* h) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
   h->spmv_ms = h->asm_ms = 0.0;
@@ -6438,6 +7369,13 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->fres_ok = false;
   h->d_left = nullptr;
   h->n_left = 0;
+  h->dstep_ok = false;  // (the fused step's buffers were in the freed pc_bufs)
+  h->d_chain_post = h->d_left_off = nullptr;
+  h->d_post = nullptr;
+  h->d_dsync = nullptr;
+  h->dstep_epoch = 0;
+  h->dstep_off = false;
+  h->need_r = false;
   if (lds && n_jobs > 0) {  // one rank or several (then only owned rows of lower jobs)
     std::vector<int> job_of_chain(n_chains, -1), job_of_slot(n_slots, -1);
     for (int jb = 0; jb < n_jobs; ++jb) {
@@ -6481,6 +7419,49 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     if (h->n_cut >= 0) {
       const int rc = build_left_cut(h);
       if (rc != NX_OK) return rc;
+    }
+    // the fused direct step (one rank): every slot a job reads outside itself -- its root's
+    // parent, its chains' far ends -- is a top slot (the down sweep takes it from the top
+    // values), and the left rows get their flux-end shares posted (chain order per row)
+    if (h->fres_ok && h->nranks == 1 && h->n_ghost == 0) {
+      const int ts0 = top_lvl_off[0], ts1 = top_lvl_off[n_top_lvl];
+      auto top = [&](int j) { return j >= ts0 && j < ts1; };
+      bool ok = true;
+      for (int64_t c = 0; c < n_chains && ok; ++c)
+        for (int end = 0; end < 2; ++end) {
+          const int j = end ? chain_lo[c] : chain_up[c];
+          if (j >= 0 && job_of_slot[j] != job_of_chain[c] && !top(j)) ok = false;
+        }
+      for (int64_t j = 0; j < n_slots && ok; ++j) {
+        const int p = slot_parent[j];
+        if (job_of_slot[j] >= 0 && p >= 0 && job_of_slot[p] != job_of_slot[j] && !top(p)) ok = false;
+      }
+      std::vector<int> row_of(h->n_own - h->n_edge_dofs, -1);
+      for (size_t i = 0; i < left.size(); ++i) row_of[left[i] - h->n_edge_dofs] = (int)i;
+      std::vector<int> off(left.size() + 1, 0), fill(left.size(), 0);
+      std::vector<int> cpost(2 * std::max<int64_t>(n_chains, 1), -1);
+      auto row_at = [&](int j) { return j < 0 ? -1 : row_of[slot_lam[j] - h->n_edge_dofs]; };
+      for (int64_t c = 0; c < n_chains; ++c)
+        for (int end = 0; end < 2; ++end) {
+          const int r = row_at(end ? chain_lo[c] : chain_up[c]);
+          if (r >= 0) off[r + 1] += 1;
+        }
+      for (size_t i = 0; i < left.size(); ++i) off[i + 1] += off[i];
+      for (int64_t c = 0; c < n_chains; ++c)
+        for (int end = 0; end < 2; ++end) {
+          const int r = row_at(end ? chain_lo[c] : chain_up[c]);
+          if (r >= 0) cpost[2 * c + end] = off[r] + fill[r]++;
+        }
+      h->d_chain_post = const_cast<int*>(up(cpost.data(), (int64_t)cpost.size()));
+      h->d_left_off = const_cast<int*>(up(off.data(), (int64_t)off.size()));
+      h->d_post = scratch(std::max(1, off.back()));
+      unsigned* sy = nullptr;
+      if (hipMalloc((void**)&sy, 4 * sizeof(unsigned)) == hipSuccess) {
+        h->pc_bufs.push_back(sy);
+        if (hipMemset(sy, 0, 4 * sizeof(unsigned)) != hipSuccess) sy = nullptr;
+      }
+      h->d_dsync = sy;
+      h->dstep_ok = ok && h->d_chain_post && h->d_left_off && h->d_post && h->d_dsync;
     }
   }
   pa.top_reg = 1;
@@ -7048,6 +8029,12 @@ NX_API int nx_debug_phases(unsigned long long* out, int32_t n) {
   if (!out || n < 1 || n > 128) return fail(NX_ERR_ARG, "bad argument");
   HIPCALL(hipDeviceSynchronize());
   HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n));
+  return NX_OK;
+}
+
+NX_API int nx_debug_dstep(unsigned long long* out) {  // 6 x 512 stamps of k_dir_step
+  HIPCALL(hipDeviceSynchronize());
+  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(unsigned long long) * 6 * 512));
   return NX_OK;
 }
 

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Per-workgroup phase stamps of the fused direct step k_dir_step (debug build, GPU box).
+
+Loads ``libnxhip_phase.so`` (``python -c 'from networks_fenicsx_amd import build;
+build.build(phase_timing=True)'``), runs the bench workload's direct step a few times and
+prints, for the last launch, the distribution over workgroups (wall_clock64, 100 MHz, in us
+from the earliest workgroup start) of: start, phase-1 arrival, top values received, phase-2
+arrival; and when the last workgroup finished the top part and published.
+
+    python scripts/dstep_phases.py [levels] [N]
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+os.environ.setdefault("NXHIP_LIB", str(REPO / "networks_fenicsx_amd" / "libnxhip_phase.so"))
+sys.path.insert(0, str(REPO))
+
+import numpy as np  # noqa: E402
+
+from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh, _lib  # noqa: E402
+from networks_fenicsx_amd import network_generation as ng  # noqa: E402
+
+
+def main() -> int:
+    levels = int(sys.argv[1]) if len(sys.argv) > 1 else 15
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 15
+    mesh = NetworkMesh(ng.make_tree(levels, levels, levels), N=N, color_strategy="smallest_last")
+    asm = HydraulicNetworkAssembler(mesh)
+    asm.compute_forms(p_bc_ex=lambda x: x[1])
+    asm.set_direct(True)
+    h = asm.handle
+    for _ in range(5):
+        asm.assemble()
+        it, rr, conv = h.solve(1e-12, 100, 4)
+    assert h.direct_path() == "fused", h.direct_path()
+    nj = asm.tree_preconditioner.n_jobs
+    buf = (C.c_ulonglong * (6 * 512))()
+    fn = _lib.lib().nx_debug_dstep
+    fn.argtypes = [C.POINTER(C.c_ulonglong)]
+    _lib.check(fn(buf))
+    g = np.array(buf, dtype=np.float64).reshape(6, 512)[:, :nj]
+    t0 = g[0].min()
+    us = (g - t0) / 100.0  # 100 MHz ticks -> us
+    names = ["start", "phase-1 arrival", "top values in", "phase-2 arrival", "published",
+             "top part solved"]
+    print(f"{nj} workgroups, residual {rr:.2e}; us from the first workgroup start")
+    for k in (0, 1, 2, 3):
+        v = us[k]
+        print(f"  {names[k]:16s} min {v.min():7.2f}  med {np.median(v):7.2f}  max {v.max():7.2f}")
+    last1 = int(np.argmax(g[1]))
+    print(f"  top part solved by wg {last1} at {us[5][last1]:7.2f} (its arrival {us[1][last1]:7.2f})")
+    pub = np.argmax(g[4])
+    print(f"  published by wg {pub} at {us[4][pub]:7.2f}")
+    d1 = us[1] - us[0]
+    d2 = us[3] - us[2]
+    print(f"  phase 1 per wg: min {d1.min():.2f} med {np.median(d1):.2f} max {d1.max():.2f}")
+    print(f"  phase 2 per wg: min {d2.min():.2f} med {np.median(d2):.2f} max {d2.max():.2f}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

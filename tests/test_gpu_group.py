@@ -295,7 +295,9 @@ def _forced_coarse_direct(case: str, terminals, transport: str, then_lumped: boo
             it, rr, conv = (h if grp is None else grp).solve(1e-12, 50000, 4)
         assert conv, (it, rr)
         used = "direct" if h.solver()[1] == 1 else "minres"
-        out = (h.solution(), it, rr, used, h.graph_mode(), h.true_residual())
+        # (a group member's residual needs every rank's solution: RCCL only)
+        out = (h.solution(), it, rr, used, h.graph_mode(),
+               h.true_residual() if grp is None else None)
         if grp is not None:
             grp.close()
             grp = None
