@@ -234,6 +234,19 @@ int nx_get_pc_kernels(nx_network_t* h, int32_t* lds);
  */
 int nx_set_solver(nx_network_t* h, int32_t solver, int32_t tree_exact);
 int nx_get_solver(nx_network_t* h, int32_t* requested, int32_t* last_run);
+/*
+ * Graphs with cycles (one rank): the direct solve stays exact, as MUMPS' LU is on any graph
+ * (solver.py:58-65; the reference's own cyclic graph, tests/test_edge_info.py:8-35). The
+ * decomposition grounds one end of each of the n cycle-closing chains; rows[2i], rows[2i+1]
+ * = the flux end row and the multiplier row whose coupling that drops (precond.py
+ * TreePreconditioner.cyc_rows). The tree solve inverts A without those n symmetric +-1
+ * pairs; nx_solve adds them back with a rank-2n Woodbury correction built once per assembled
+ * matrix (2n tree solves of unit vectors, a (2n)^2 capacitance matrix), then checks the true
+ * residual with the CSR. n <= 128 (else the solve runs MINRES); n = 0 clears it. Set after
+ * every nx_set_preconditioner (which clears it). Replaces nothing one-to-one: MUMPS'
+ * factorisation (solver.py:58-65) covers cycles implicitly.
+ */
+int nx_set_cycles(nx_network_t* h, int32_t n, const int32_t* rows);
 
 /*
  * Process-wide solve mode. 1 (default): with the preconditioner a solve is ONE HIP graph

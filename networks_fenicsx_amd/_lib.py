@@ -86,6 +86,7 @@ _SIGS = {
     "nx_set_pc_exact": (C.c_int, [_h, _i32]),
     "nx_get_pc_exact": (C.c_int, [_h, _pi32]),
     "nx_set_solver": (C.c_int, [_h, _i32, _i32]),
+    "nx_set_cycles": (C.c_int, [_h, _i32, _pi32]),
     "nx_get_solver": (C.c_int, [_h, _pi32, _pi32]),
     "nx_set_lean": (C.c_int, [_i32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
@@ -93,6 +94,7 @@ _SIGS = {
     "nx_group_destroy": (C.c_int, [_h]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
+MAX_CYCLES = 128  # kMaxCyc of csrc/nxhip.hip: cycle-closing chains the direct solve corrects
 
 
 class NxError(RuntimeError):
@@ -438,6 +440,13 @@ class Handle:
                 self.ptr, nC, q["slot_cidx"], int(pc.cc_chain.size), q["cc_chain"], q["cc_top"],
                 q["cc_bot"], q["c_parent"], q["c_child_off"], q["c_child"],
                 int(pc.c_lvl_off.size - 1), q["c_lvl_off"]))
+        cyc = np.ascontiguousarray(getattr(pc, "cyc_rows", np.zeros((0, 2))), dtype=np.int32)
+        multi = getattr(self, "_multi", False) or self.n_cols > self.n_rows
+        if cyc.size and nC == 0 and not multi and cyc.shape[0] <= MAX_CYCLES:
+            # one rank, a graph with cycles: the direct solve corrects for the couplings its
+            # tree solve drops (nx_set_cycles; past MAX_CYCLES the solve runs MINRES)
+            self._pc_keep_y = cyc
+            check(lib().nx_set_cycles(self.ptr, int(cyc.shape[0]), _ptr(cyc, C.c_int32)))
 
     def set_pc_exact(self, enable: bool) -> None:
         """Consistent (exact Schur complement, default) or lumped flux mass in P."""
@@ -460,6 +469,7 @@ class Handle:
 
     def set_halo(self, nranks: int, rank: int, peers, send_off, send_idx, recv_off):
         """Halo plan without a transport (in-process group members)."""
+        self._multi = int(nranks) > 1
         peers = np.ascontiguousarray(peers, dtype=np.int32)
         send_off = np.ascontiguousarray(send_off, dtype=np.int32)
         send_idx = np.ascontiguousarray(send_idx, dtype=np.int32)
@@ -499,6 +509,7 @@ class Handle:
         return int(n.value)
 
     def comm_init(self, nranks: int, rank: int, uid: bytes, peers, send_off, send_idx, recv_off):
+        self._multi = True  # (a communicator, even of one rank: no cycle correction)
         uid_arr = (C.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid)
         peers = np.ascontiguousarray(peers, dtype=np.int32)
         send_off = np.ascontiguousarray(send_off, dtype=np.int32)

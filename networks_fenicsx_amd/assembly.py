@@ -403,9 +403,10 @@ class HydraulicNetworkAssembler:
 
     def set_direct(self, enable: bool) -> None:
         """Ask ``nx_solve`` for the direct tree solve (``nx_set_solver``); the device runs it
-        only where it is exact -- exact preconditioner, no cycle (the decomposition's
-        ``tree_exact``), and with several ranks the LDS sweeps with the coarse step on every
-        rank (the ranks decide together) -- and MINRES otherwise."""
+        only where it is exact -- exact preconditioner; a forest (the decomposition's
+        ``tree_exact``) or, on one rank, up to 128 cycle-closing chains corrected by a
+        Woodbury step (``nx_set_cycles``); with several ranks the LDS sweeps with the coarse
+        step on every rank (the ranks decide together) -- and MINRES otherwise."""
         want = (bool(enable), bool(self._pc is not None and self._pc.tree_exact))
         if getattr(self, "_direct_state", None) != want:
             self._handle.set_solver(*want)

@@ -50,7 +50,7 @@ thread_local std::string g_err;
 __device__ unsigned long long g_phase[128];
 __device__ unsigned long long g_wgs[8][512];  // per-workgroup start / end, last launch wins
 __device__ unsigned long long g_wge[8][512];
-__device__ unsigned long long g_dst[6][512];  // k_dir_step: per-workgroup stamps (nx_debug_dstep)
+__device__ unsigned long long g_dst[12][512];  // k_dir_step: per-workgroup stamps (nx_debug_dstep)
 #define NX_DSTAMP(k)                                                   \
   do {                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 512) g_dst[(k)][blockIdx.x] = wall_clock64(); \
@@ -2408,18 +2408,21 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
         const double num = rJ + (p >= 0 ? gp * sJ0[p] : 0.0);
         const double zj = dir ? num * riv : num / rD;
         sJ0[rsl] = zj;  // reuse: z of top slots
-        if (!down) {
-          if (dir && pa.accum)
-            z[lam] += zj;
-          else
-            z[lam] = zj;
-          stv<WT>(pa.slot_z + ts0 + rsl, zj);
-        }
         if (!dir) part += sY[rsl] * zj;
       }
       __syncthreads();
     }
-    // down: workgroup 0's copy after the levels (no global store inside their barriers)
+    // the stores after the levels, not inside their barriers (a workgroup barrier waits for
+    // the workgroup's outstanding stores: a write-through store per level cost ~1 us each);
+    // down: workgroup 0's copy only
+    if (rmine && !down) {
+      const double zj = sJ0[rsl];
+      if (dir && pa.accum)
+        z[lam] += zj;
+      else
+        z[lam] = zj;
+      stv<WT>(pa.slot_z + ts0 + rsl, zj);
+    }
     if (down && blockIdx.x == 0 && rmine) pa.slot_z[ts0 + rsl] = sJ0[rsl];
   } else
   for (int lv = 0; lv < nl; ++lv) {  // root level first: z_j = (J_j + g_par z_par) / D_j
@@ -2429,17 +2432,21 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
       const double num = sJ[sl] + (p >= 0 ? sGp[sl] * sJ0[p] : 0.0);
       const double zj = dir ? num * sY[sl] : num / sD[sl];
       sJ0[sl] = zj;  // reuse: z of top slots
+      if (!dir) part += sY[sl] * zj;
+    }
+    __syncthreads();
+  }
+  if (!reg)  // (the stores after the levels, as above)
+    for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
+      const double zj = sJ0[sl];
       if (!down) {
         if (dir && pa.accum)
           z[sLam[sl]] += zj;
         else
           z[sLam[sl]] = zj;
       }
-      if (!down || blockIdx.x == 0) stv<WT>(pa.slot_z + ts0 + sl, zj);  // (non-register path)
-      if (!dir) part += sY[sl] * zj;
+      if (!down || blockIdx.x == 0) stv<WT>(pa.slot_z + ts0 + sl, zj);
     }
-    __syncthreads();
-  }
   NX_PHASE(36);
   if (down) {
     __syncthreads();  // the top values (sJ0) for the caller's chains
@@ -3220,36 +3227,33 @@ constexpr int kDirLdsMain = kDirLdsTop > kDirLdsPhase1 ? (kDirLdsTop > kDirLdsPh
                                                        : (kDirLdsPhase1 > kDirLdsPhase2 ? kDirLdsPhase1 : kDirLdsPhase2);
 constexpr int kDirLds = kDirLdsMain + kCapT;
 
-// One chain's edge assembled in registers by its W lanes (lane = CPL cells, chain order):
-// cell tensors R h / 3, R h / 6 and the rhs as k_assemble computes them, the lumped flux
-// mass in k_assemble's order of additions (so ch.rho has dq's bits), the CSR segment of the
-// edge (unit stride over the lanes; the tensors of the entry's cells fetched by shuffles)
-// and the chain lane state the up sweep needs (ChainLane::setup without the loads).
+// One chain's lane as k_dir_step assembles it (phase 1) and keeps it for phase 2 when the
+// job's chains fit one pass: the cell tensors R h / 3, R h / 6 (CSR values and lumped mass;
+// mo is also the residual's cell mass), the assembled b (cells, fluxes, q_N) and where the
+// edge's values go. The chain lane state is rebuilt from it (dir_lane_chain: integer math,
+// sums and scans) rather than kept: kept, it overflows the 128-VGPR budget of 1024 threads.
 template <int W, int CPL>
-__device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& da, int c,
-                                              bool active, ChainLane<W, CPL>& ch,
-                                              double (&vc)[CPL], double (&vq)[CPL], double& vN,
-                                              int& flip) {
+struct DirLane {
+  double bc[CPL], bq[CPL], bN;
+  double md[CPL], mo[CPL];
+  int flip, e, sg0, seglen, s;
+};
+
+// The chain lane state (ChainLane::setup without the loads) from a DirLane: the lumped flux
+// mass of chain flux k (between chain cells k - 1 and k) in k_assemble's order of additions
+// (so ch.rho has dq's bits) -- edge flux q: d = md_q + mo_q, then (mo_{q-1} + md_{q-1}) + d;
+// q = N: mo_{N-1} + md_{N-1}.
+template <int W, int CPL>
+__device__ __forceinline__ void dir_lane_chain(const PcArgs& pa, const DirLane<W, CPL>& L,
+                                               bool active, ChainLane<W, CPL>& ch) {
 #pragma clang fp contract(off)
   const int N = pa.N;
   const int l = threadIdx.x & (W - 1);
-  const int e = active ? pa.chain_edge[c] : 0;
-  flip = active ? pa.chain_flip[c] : 0;
-  double x0[3], x1[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    x0[i] = da.edge_x[6 * (int64_t)e + i];
-    x1[i] = da.edge_x[6 * (int64_t)e + 3 + i];
-  }
-  const double R = da.edge_R[e];
-  const double fe = da.edge_f ? da.edge_f[e] : da.f;
-  const double bc0 = da.edge_bc[2 * (int64_t)e], bc1 = da.edge_bc[2 * (int64_t)e + 1];
-  const int s = da.edge_lm[2 * (int64_t)e] >= 0;
-  const int sg0 = da.edge_seg[e], seglen = da.edge_seg[e + 1] - sg0;
-  const int64_t base = (int64_t)e * (2 * N + 1);
-  const int64_t qb = (int64_t)e * (N + 1);
-  const double invN = 1.0 / (double)N;
-  double md[CPL], mo[CPL];
+  const int flip = L.flip;
+  const int64_t base = (int64_t)L.e * (2 * N + 1);
+  const double* md = L.md;
+  const double* mo = L.mo;
+  const double mdP = __shfl_up(md[CPL - 1], 1, W), moP = __shfl_up(mo[CPL - 1], 1, W);
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
     const int k = l * CPL + t;
@@ -3258,30 +3262,8 @@ __device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& d
     const int qp = flip ? N - k : k;
     ch.dof_c[t] = (int)(base + 2 * kp + 1);
     ch.dof_q[t] = (int)(base + 2 * qp);
-    md[t] = 0.0;
-    mo[t] = 0.0;
-    vc[t] = 0.0;
-    if (ch.valid[t]) {
-      double va[3], vb[3];
-      vertex(x0, x1, kp, N, invN, va);
-      vertex(x0, x1, kp + 1, N, invN, vb);
-      const double d0 = vb[0] - va[0], d1 = vb[1] - va[1], d2 = vb[2] - va[2];
-      const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-      md[t] = R * h / 3.0;
-      mo[t] = R * h / 6.0;
-      vc[t] = -(fe * h);  // negated pressure row: -(f h)
-      da.rhs[ch.dof_c[t]] = vc[t];
-    }
-  }
-  // lumped flux mass of chain flux k (between chain cells k - 1 and k), k_assemble's sums:
-  // edge flux q: d = md_q + mo_q, then (mo_{q-1} + md_{q-1}) + d; q = N: mo_{N-1} + md_{N-1}
-  const double mdP = __shfl_up(md[CPL - 1], 1, W), moP = __shfl_up(mo[CPL - 1], 1, W);
-#pragma unroll
-  for (int t = 0; t < CPL; ++t) {
     ch.rho[t] = 0.0;
-    vq[t] = 0.0;
     if (!ch.valid[t]) continue;
-    const int k = l * CPL + t;
     const double mdq = t > 0 ? md[t - 1] : mdP, moq = t > 0 ? mo[t - 1] : moP;  // cell k - 1
     double d;
     if (!flip) {  // edge flux k: cells k - 1 and k
@@ -3294,17 +3276,12 @@ __device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& d
       d = mo[t] + md[t];
     }
     ch.rho[t] = d;
-    const int qp = flip ? N - k : k;
-    da.dq[qb + qp] = d;
-    vq[t] = qp == 0 ? bc0 : (qp == N ? bc1 : 0.0);
-    da.rhs[ch.dof_q[t]] = vq[t];
   }
   // chain flux N (the lane holding chain cell N - 1): edge flux N (its last cell) or, flipped,
   // edge flux 0 (its first cell)
   ch.has_last = active && (l == (N - 1) / CPL);
   ch.dof_qN = (int)(base + 2 * (flip ? 0 : N));
   ch.rhoN = 0.0;
-  vN = 0.0;
   {
     const int tl = (N - 1) - l * CPL;
     double mdl = 0.0, mol = 0.0;
@@ -3314,54 +3291,143 @@ __device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& d
         mdl = md[t];
         mol = mo[t];
       }
-    if (ch.has_last) {
-      const double d = flip ? mdl + mol : mol + mdl;
-      ch.rhoN = d;
-      da.dq[qb + (flip ? 0 : N)] = d;
-      vN = flip ? bc0 : bc1;
-      da.rhs[ch.dof_qN] = vN;
-    }
+    if (ch.has_last) ch.rhoN = flip ? mdl + mol : mol + mdl;
   }
   // ChainLane::setup's mo: the edge's q_0 lumped mass / 3 (chain flux 0, or N when flipped)
   const double dq0 = flip ? __shfl(ch.rhoN, (N - 1) / CPL, W) : __shfl(ch.rho[0], 0, W);
   ch.mo = active ? dq0 / 3.0 : 1.0;
   ch.finish();
-  // the edge's CSR segment: entry i (decode_entry) by lane i mod W; uniform trip count
-  // across the wave (the longest segment: 7N + 3) so every shuffle has all lanes
-  const int smax = 7 * N + 3;
-  for (int ib = 0; ib < smax; ib += W) {
-    const int i = ib + l;
-    const bool in = active && i < seglen;
-    const Entry en = decode_entry(in ? i : 0, N, s);
-    const int ca = en.cell, cb = min(en.cell + 1, N - 1);
-    const int ka = flip ? N - 1 - ca : ca, kb = flip ? N - 1 - cb : cb;
-    double mdA = 0.0, moA = 0.0, mdB = 0.0;
+}
+
+// One chain's edge assembled in registers by its W lanes (lane = CPL cells, chain order):
+// cell tensors R h / 3, R h / 6 and the rhs as k_assemble computes them. Nothing is stored
+// here (dir_chain_store).
+template <int W, int CPL>
+__device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& da, int c,
+                                              bool active, DirLane<W, CPL>& L) {
+#pragma clang fp contract(off)
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const int e = active ? pa.chain_edge[c] : 0;
+  const int flip = active ? pa.chain_flip[c] : 0;
+  L.e = e;
+  L.flip = flip;
+  double x0[3], x1[3];
 #pragma unroll
-    for (int t = 0; t < CPL; ++t) {
-      const double a = __shfl(md[t], ka / CPL, W), b = __shfl(mo[t], ka / CPL, W);
-      const double m2 = __shfl(md[t], kb / CPL, W);
-      if (ka % CPL == t) {
-        mdA = a;
-        moA = b;
+  for (int i = 0; i < 3; ++i) {
+    x0[i] = da.edge_x[6 * (int64_t)e + i];
+    x1[i] = da.edge_x[6 * (int64_t)e + 3 + i];
+  }
+  const double R = da.edge_R[e];
+  const double fe = da.edge_f ? da.edge_f[e] : da.f;
+  const double bc0 = da.edge_bc[2 * (int64_t)e], bc1 = da.edge_bc[2 * (int64_t)e + 1];
+  L.s = da.edge_lm[2 * (int64_t)e] >= 0;
+  L.sg0 = da.edge_seg[e];
+  L.seglen = da.edge_seg[e + 1] - L.sg0;
+  const double invN = 1.0 / (double)N;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    const int k = l * CPL + t;
+    const bool valid = active && k < N;
+    const int kp = flip ? N - 1 - k : k;
+    const int qp = flip ? N - k : k;
+    L.md[t] = 0.0;
+    L.mo[t] = 0.0;
+    L.bc[t] = 0.0;
+    L.bq[t] = 0.0;
+    if (valid) {
+      double va[3], vb[3];
+      vertex(x0, x1, kp, N, invN, va);
+      vertex(x0, x1, kp + 1, N, invN, vb);
+      const double d0 = vb[0] - va[0], d1 = vb[1] - va[1], d2 = vb[2] - va[2];
+      const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+      L.md[t] = R * h / 3.0;
+      L.mo[t] = R * h / 6.0;
+      L.bc[t] = -(fe * h);  // negated pressure row: -(f h)
+      L.bq[t] = qp == 0 ? bc0 : (qp == N ? bc1 : 0.0);
+    }
+  }
+  L.bN = (active && l == (N - 1) / CPL) ? (flip ? bc0 : bc1) : 0.0;
+}
+
+// The assembly's stores of one chain's edge from its lane state: rhs, lumped mass, and the
+// CSR segment (entry i by lane i mod W, unit stride; the tensors of the entry's cells fetched
+// by shuffles; uniform trip count across the wave -- the longest segment, 7N + 3 -- so every
+// shuffle has all lanes).
+template <int W, int CPL>
+__device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep& da, bool active,
+                                                const DirLane<W, CPL>& L) {
+  ChainLane<W, CPL> ch;
+  dir_lane_chain<W, CPL>(pa, L, active, ch);
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const int flip = L.flip;
+  const int64_t qb = (int64_t)L.e * (N + 1);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    if (!ch.valid[t]) continue;
+    const int k = l * CPL + t;
+    da.rhs[ch.dof_c[t]] = L.bc[t];
+    da.rhs[ch.dof_q[t]] = L.bq[t];
+    da.dq[qb + (flip ? N - k : k)] = ch.rho[t];
+  }
+  if (ch.has_last) {
+    da.rhs[ch.dof_qN] = L.bN;
+    da.dq[qb + (flip ? 0 : N)] = ch.rhoN;
+  }
+  // the CSR segment, each lane its own cells' rows (edge order: cell g owns p_g's 2 entries
+  // and q_{g+1}'s 5 -- q_N's 3 + s_dst for g = N - 1 -- from q0len + 7 g on; cell 0 also the
+  // q_0 row): values as decode_entry lists them, the next edge cell's masses from the
+  // neighbouring lane (chain cell k + 1, or k - 1 on a flipped chain)
+  const int s0 = L.s, q0len = 3 + s0;
+  const int sdst = L.seglen - (7 * N + 1 + s0);
+  const double mdD = __shfl_down(L.md[0], 1, W), moD = __shfl_down(L.mo[0], 1, W);
+  const double mdU = __shfl_up(L.md[CPL - 1], 1, W), moU = __shfl_up(L.mo[CPL - 1], 1, W);
+  double* __restrict__ v = da.val + L.sg0;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    if (!ch.valid[t]) continue;
+    const int k = l * CPL + t;
+    const int g = flip ? N - 1 - k : k;
+    const double md = L.md[t], mo = L.mo[t];
+    double* o = v + q0len + 7 * g;
+    o[0] = 1.0;
+    o[1] = -1.0;
+    o[2] = mo;
+    o[3] = -1.0;
+    if (g < N - 1) {  // the next edge cell: chain cell k + 1 (k - 1 when flipped)
+      double mdn, mon;
+      if (!flip) {
+        mdn = t + 1 < CPL ? L.md[t + 1] : mdD;
+        mon = t + 1 < CPL ? L.mo[t + 1] : moD;
+      } else {
+        mdn = t > 0 ? L.md[t - 1] : mdU;
+        mon = t > 0 ? L.mo[t - 1] : moU;
       }
-      if (kb % CPL == t) mdB = m2;
+      o[4] = md + mdn;
+      o[5] = 1.0;
+      o[6] = mon;
+    } else {
+      o[4] = md;
+      if (sdst) o[5] = 1.0;
     }
-    double v;
-    switch (en.vk) {
-      case V_P1: v = 1.0; break;
-      case V_M1: v = -1.0; break;
-      case V_MD: v = mdA; break;
-      case V_MO: v = moA; break;
-      default: v = mdA + mdB; break;  // interior diagonal: cells g and g+1
+    if (g == 0) {  // row q_0: [q_0, p_0, q_1, (lambda_src)]
+      v[0] = md;
+      v[1] = 1.0;
+      v[2] = mo;
+      if (s0) v[3] = -1.0;
     }
-    if (in) da.val[sg0 + i] = v;
   }
 }
 
 // Phase 1: assembly + up sweep (k_pc_up_lds's mode-3 arithmetic; b_lambda = 0).
+// keep (the job's chains fit one pass): the assembly's stores are left to the caller
+// (dir_chain_store after the hand-off) and the lane state stays in L for phase 2; the slot's
+// back-substitution coefficients (thread = slot) are returned in sA_ / sB_ either way.
 template <int W, int CPL>
 __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da,
-                                             double* lds) {
+                                             double* lds, DirLane<W, CPL>& L, bool keep,
+                                             double& sA_, double& sB_) {
   double* sT = lds;
   double* sIt = sT + kCapC;
   double* sIb = sIt + kCapC;
@@ -3401,12 +3467,15 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
     const int c = cb + seg;
     const bool active = c < c1;
     const int cu = active ? pa.chain_up[c] : -1, clo = active ? pa.chain_lo[c] : -1;
+    dir_chain_asm<W, CPL>(pa, da, c, active, L);
+    if (!keep) dir_chain_store<W, CPL>(pa, da, active, L);
     ChainLane<W, CPL> ch;
-    double vc[CPL], vq[CPL], vN;
-    int flip;
-    dir_chain_asm<W, CPL>(pa, da, c, active, ch, vc, vq, vN, flip);
+    dir_lane_chain<W, CPL>(pa, L, active, ch);
+    double vc[CPL];
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) vc[t] = L.bc[t];
     double ytop = 0.0, ybot = 0.0;
-    direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
+    direct_cell_inputs<W, CPL>(pa, ch, L.flip, L.bq, L.bN, vc, ytop, ybot);
     double sr = 0.0, srd = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
@@ -3574,12 +3643,13 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
   // back-substitution coefficients (own phase 2 reads them); the job's root level hands its
   // (D, J) to the top part
   const int root1 = sLvl[1];
-  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
+  if ((int)threadIdx.x < ns) {  // ns <= kCapS < kPcThreads: thread = slot
+    const int sl = threadIdx.x;
     const int j = js0 + sl;
-    const int pcn = pa.slot_pchain[j];
+    const int pcn = p_pcn;
     const double J = sJ[sl], iv = sIv[sl];
-    pa.slot_A[j] = J * iv;
-    pa.slot_B[j] = pcn >= 0 ? iv / sT[pcn - c0] : 0.0;
+    sA_ = J * iv;
+    sB_ = pcn >= 0 ? iv / sT[pcn - c0] : 0.0;
     if (j < root1) {
       st_wt(pa.slot_D + j, sD[sl]);
       st_wt(pa.slot_J + j, J);
@@ -3589,9 +3659,12 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
 
 // Phase 2: the down sweep (k_pc_down_lds's mode-3 arithmetic with the fused residual, r not
 // stored); sTop: the top part's values by top position.
+// keep: the job's chains in one pass, their lane state (assembled b, cell inputs, cell
+// masses) still in L from phase 1 -- no reloads; sA_ / sB_: this thread's slot coefficients.
 template <int W, int CPL>
 __device__ __forceinline__ void dir_down_fused(const PcArgs& pa, const DirStep& da, double* lds,
-                                               const double* sTop) {
+                                               const double* sTop, const DirLane<W, CPL>& L,
+                                               bool keep, double sA_, double sB_) {
   // (contraction as in k_pc_down_lds: the same x bit for bit)
   double* sZ = lds;
   double* sA = sZ + kCapS;
@@ -3628,16 +3701,32 @@ __device__ __forceinline__ void dir_down_fused(const PcArgs& pa, const DirStep& 
     post_t = active ? da.chain_post[2 * (int64_t)c] : -1;
     post_b = active ? da.chain_post[2 * (int64_t)c + 1] : -1;
   };
-  ch.setup(pa, c0 + seg, c0 + seg < c1);
-  load_lane(c0 + seg, c0 + seg < c1);
+  if (keep) {  // phase 1's lane: only the chain's ends and posts are loaded
+    const int c = c0 + seg;
+    const bool active = c < c1;
+    dir_lane_chain<W, CPL>(pa, L, active, ch);
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      vc[t] = L.bc[t];
+      vq[t] = L.bq[t];
+      mo_r[t] = L.mo[t];
+    }
+    vN = L.bN;
+    ch_up = active ? pa.chain_up[c] : -1;
+    ch_lo = active ? pa.chain_lo[c] : -1;
+    flip = L.flip;
+    post_t = active ? da.chain_post[2 * (int64_t)c] : -1;
+    post_b = active ? da.chain_post[2 * (int64_t)c + 1] : -1;
+  } else {
+    ch.setup(pa, c0 + seg, c0 + seg < c1);
+    load_lane(c0 + seg, c0 + seg < c1);
+  }
   int p_par = -1, p_lam = 0, p_lv = -1;
-  double p_A = 0.0, p_B = 0.0;
+  const double p_A = sA_, p_B = sB_;  // (ns <= kCapS < kPcThreads: thread = slot)
   const bool hwave = pa.job_wave != nullptr && lv1 > lv0 && pa.job_wave[job] > 0;
   if ((int)threadIdx.x < ns) {
     const int j = js0 + threadIdx.x;
     p_par = pa.slot_parent[j];
-    p_A = pa.slot_A[j];
-    p_B = pa.slot_B[j];
     p_lam = pa.slot_lam[j];
     if (hwave) p_lv = pa.slot_wave[3 * (int64_t)j] & 0xff;
   }
@@ -3647,8 +3736,8 @@ __device__ __forceinline__ void dir_down_fused(const PcArgs& pa, const DirStep& 
     const bool pre = sl == (int)threadIdx.x;
     const int p = pre ? p_par : pa.slot_parent[j];
     const bool local = p >= js0 && p < js1;
-    sA[sl] = pre ? p_A : pa.slot_A[j];
-    sB[sl] = pre ? p_B : pa.slot_B[j];
+    sA[sl] = p_A;
+    sB[sl] = p_B;
     sP[sl] = local ? p - js0 : -1;
     sZ[sl] = (!local && p >= 0) ? sTop[p - ts0] : 0.0;
   }
@@ -3697,7 +3786,7 @@ __device__ __forceinline__ void dir_down_fused(const PcArgs& pa, const DirStep& 
       ch.setup(pa, c, active);
       load_lane(c, active);
     }
-    chain_cell_mo<W, CPL>(pa, ch, c, active, flip, mo_r);
+    if (!keep) chain_cell_mo<W, CPL>(pa, ch, c, active, flip, mo_r);
     const int up = ch_up, lo = ch_lo;
     const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : sTop[up - ts0];
     const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : sTop[lo - ts0];
@@ -3842,15 +3931,27 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
   const int nj = pa.n_jobs;
   const unsigned last = da.epoch * (unsigned)nj + (unsigned)(nj - 1);
   NX_DSTAMP(0);
-  // the multiplier rows (+-1 values, zero rhs): a strided share per workgroup
-  const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
-  for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
-    if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
-    if (i < da.B) da.rhs_lm[i] = 0.0;
-  }
-  dir_up_fused<W, CPL>(pa, da, smem);
-  double* sTop = smem + kDirLdsMain;
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  // the job's chains in one pass: the assembly's stores wait until this workgroup has handed
+  // over its top inputs (they fill the wait for the top values instead of delaying it), and
+  // phase 2 runs on phase 1's registers
+  bool keep = c1 - c0 <= kPcThreads / W;
+  DirLane<W, CPL> L;
+  double sA_ = 0.0, sB_ = 0.0;
   const int nt = pa.top_nt, ts0 = pa.top_ts0;
+  dir_up_fused<W, CPL>(pa, da, smem, L, keep, sA_, sB_);
+  // the multiplier rows (+-1 values, zero rhs): a strided share per workgroup; then this
+  // workgroup's edges (keep)
+  auto stores = [&]() {
+    const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
+    for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
+      if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
+      if (i < da.B) da.rhs_lm[i] = 0.0;
+    }
+    if (keep) dir_chain_store<W, CPL>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
+  };
+  double* sTop = smem + kDirLdsMain;
+  bool late = false;  // the workgroup that solved the top part (keep): lanes re-assembled
   if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
     vm_drain();
     __syncthreads();
@@ -3862,53 +3963,66 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
     }
     __syncthreads();
     if (sFlag) {
+      // this workgroup re-assembles its lanes after the top part (kept registers would stay
+      // live through the solve, past the register budget) and stores after its phase 2
+      late = keep;
       double* t = smem;
-      TopLds L;
-      L.sD0 = t; t += kCapT;
-      L.sJ0 = t; t += kCapT;
-      L.sD = t; t += kCapT;
-      L.sJ = t; t += kCapT;
-      L.sGp = t; t += kCapT;
-      L.sY = t; t += kCapT;
-      L.sG = t; t += kCapTDC;
-      L.sDD = t; t += kCapTDC;
-      L.sDJ = t; t += kCapTDC;
+      TopLds T;
+      T.sD0 = t; t += kCapT;
+      T.sJ0 = t; t += kCapT;
+      T.sD = t; t += kCapT;
+      T.sJ = t; t += kCapT;
+      T.sGp = t; t += kCapT;
+      T.sY = t; t += kCapT;
+      T.sG = t; t += kCapTDC;
+      T.sDD = t; t += kCapTDC;
+      T.sDJ = t; t += kCapTDC;
       int* u = reinterpret_cast<int*>(t);
-      L.sPar = u; u += kCapT;
-      L.sLam = u; u += kCapT;
-      L.sOff = u; u += kCapT + 1;
-      L.sChild = u; u += kCapTDC;
-      L.sLv = u;
+      T.sPar = u; u += kCapT;
+      T.sLam = u; u += kCapT;
+      T.sOff = u; u += kCapT + 1;
+      T.sChild = u; u += kCapTDC;
+      T.sLv = u;
       TopPre pre;
       top_pre_idx(pa, pre);
       top_pre_val<true>(pa, nullptr, pre);
+      NX_DSTAMP(6);
       top_body<false, true>(pa, nullptr, nullptr, da.x, nullptr, nullptr, 0, nullptr, nullptr,
-                            kModeDirect, L, false, pre);
+                            kModeDirect, T, false, pre);
+      NX_DSTAMP(7);
       vm_drain();
       __syncthreads();
       NX_DSTAMP(5);
       if (threadIdx.x == 0)
         __hip_atomic_store(da.sync + 2, da.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (threadIdx.x == 0) {
-      int ok = 0;
-      for (int k = 0; k < kDirWaitPolls; ++k) {
-        if (__hip_atomic_load(da.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            da.epoch + 1u) {
-          ok = 1;
-          break;
+    } else {
+      stores();
+      NX_DSTAMP(8);
+      if (threadIdx.x == 0) {
+        int ok = 0;
+        for (int k = 0; k < kDirWaitPolls; ++k) {
+          if (__hip_atomic_load(da.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              da.epoch + 1u) {
+            ok = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_s_sleep(2);
+        if (!ok) __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag = ok ? 1 : -1;
       }
-      if (!ok) __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sFlag = ok ? 1 : -1;
     }
     __syncthreads();
     if (sFlag < 0) return;  // the top values never came (the host sees no published state)
     NX_DSTAMP(2);
     for (int i = threadIdx.x; i < nt; i += kPcThreads) sTop[i] = ld_wt(pa.slot_z + ts0 + i);
     __syncthreads();
+  } else {
+    stores();
   }
-  dir_down_fused<W, CPL>(pa, da, smem, sTop);
+  const bool lane_on = c0 + (int)threadIdx.x / W < c1;
+  if (late) dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, lane_on, L);
+  dir_down_fused<W, CPL>(pa, da, smem, sTop, L, keep, sA_, sB_);
   // hand-off 2: the residual partials and shares -> the last workgroup publishes
   vm_drain();
   __syncthreads();
@@ -3922,6 +4036,10 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
   if (sFlag) {
     dir_publish_fused(pa, da);
     NX_DSTAMP(4);
+  }
+  if (late) {  // (the kernel's end, not the published state, waits for these)
+    dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, lane_on, L);
+    stores();
   }
 }
 
@@ -4707,6 +4825,68 @@ __global__ void k_dir_publish_red(const double* __restrict__ rb, double rtol, in
   mr_publish(s, ini);
 }
 
+// ---- graphs with cycles (one rank, nx_set_cycles). The tree solve inverts A_g = A minus
+// the couplings a = A[q, lam] = A[lam, q] of the m/2 cycle-closing chains' grounded ends
+// (U = the unit columns of those rows, A = A_g + U C U^T, C = blocks [[0, a], [a, 0]]), so
+//   A^{-1} b = x_g - Z Cinv U^T x_g,  x_g = A_g^{-1} b,  Z = A_g^{-1} U,
+//   Cinv = (C^{-1} + U^T Z)^{-1}                                   (Woodbury),
+// with Z (m columns) and Cinv built once per assembled matrix (cyc_build).
+constexpr int kMaxCyc = 128;  // cycle-closing chains (m = 2 kMaxCyc columns)
+
+// The m x m matrix U^T Z and the couplings a (row q of the CSR, column lam).
+__global__ __launch_bounds__(256) void k_cyc_cap(Csr A, const double* __restrict__ Z, int64_t ldz,
+                                                 const int* __restrict__ rows, int m,
+                                                 double* __restrict__ cap, double* __restrict__ acoef) {
+  for (int i = threadIdx.x; i < m * m; i += 256) {
+    const int r = i / m, c = i % m;
+    cap[i] = Z[(int64_t)c * ldz + rows[r]];
+  }
+  for (int k = threadIdx.x; 2 * k < m; k += 256) {
+    const int q = rows[2 * k], lam = rows[2 * k + 1];
+    double a = 0.0;
+    for (int p = A.rowptr[q]; p < A.rowptr[q + 1]; ++p)
+      if (A.col[p] == lam) a = A.val[p];
+    acoef[k] = a;
+  }
+}
+
+// w = Cinv (U^T x - prev) (prev: U^T x before a refinement pass added its correction, or
+// null); save: U^T x is stored there instead (before a refinement pass). One workgroup.
+__global__ __launch_bounds__(256) void k_cyc_w(const double* __restrict__ x, const int* __restrict__ rows,
+                                               int m, const double* __restrict__ cinv,
+                                               const double* __restrict__ prev, double* __restrict__ w,
+                                               double* __restrict__ save) {
+  __shared__ double g[2 * kMaxCyc];
+  for (int i = threadIdx.x; i < m; i += 256) {
+    const double v = x[rows[i]];
+    if (save) save[i] = v;
+    g[i] = prev ? v - prev[i] : v;
+  }
+  if (save) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += 256) {
+    double s = 0.0;
+    for (int j = 0; j < m; ++j) s += cinv[(int64_t)i * m + j] * g[j];
+    w[i] = s;
+  }
+}
+
+// x -= Z w, one row per thread (the m columns in order).
+__global__ __launch_bounds__(kBlock) void k_cyc_fix(double* __restrict__ x, const double* __restrict__ Z,
+                                                    int64_t ldz, const double* __restrict__ w, int m,
+                                                    int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int j = 0; j < m; ++j) s += Z[(int64_t)j * ldz + i] * w[j];
+  x[i] -= s;
+}
+
+// b = e_row: the right-hand side of one column of Z (b zeroed before)
+__global__ void k_cyc_unit(double* __restrict__ b, const int* __restrict__ rows, int j) {
+  b[rows[j]] = 1.0;
+}
+
 // ||b - A x|| / ||b|| from k_residual's partials (fixed order), published like a MINRES
 // state (it = 1, done) to the host-coherent mirror the host spins on.
 __global__ __launch_bounds__(kReduceThreads) void k_dir_publish(const double* __restrict__ p,
@@ -5002,6 +5182,19 @@ struct nx_network {
   bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
   int last_dir_path = 0;   // the last direct solve: 0 four launches, 1 k_dir_step
   std::vector<int> left_host;  // the rows of d_left
+  // graphs with cycles (nx_set_cycles, one rank): the couplings the tree solve drops, as
+  // row pairs (flux end, multiplier), and the Woodbury correction (k_cyc_*): Z (m = 2 n_cyc
+  // columns of n_col), Cinv (m x m), U^T x before a refinement pass, w; rebuilt when the
+  // matrix was assembled again (lhs_version)
+  int n_cyc = 0;
+  int* d_cyc_rows = nullptr;
+  double* cyc_z = nullptr;
+  double* cyc_cinv = nullptr;
+  double* cyc_cap = nullptr;   // m x m, then m / 2 couplings
+  double* cyc_prev = nullptr;  // m
+  double* cyc_w = nullptr;     // m
+  bool cyc_raw = false;        // cyc_build's solves: the tree solve alone
+  int64_t lhs_version = 0, cyc_version = -1;
   // several ranks, direct (nx_set_cut): the multiplier rows of the K cut bifurcations are
   // completed inside the residual's all-reduce (no halo of x): per left row its cut index,
   // per cut index the owned row (or -1) and this rank's flux ends at it (row, +-1)
@@ -5814,7 +6007,8 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->send_idx, h->send_buf, h->gath, h->d_seq,
                   h->fe_kind, h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent,
                   h->fe_bptr, h->fe_bidx, h->fe_bent, h->out_idx,
-                  h->d_left_k, h->d_cut_own, h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf};
+                  h->d_left_k, h->d_cut_own, h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf,
+                  h->d_cyc_rows, h->cyc_z, h->cyc_cinv, h->cyc_cap, h->cyc_prev, h->cyc_w};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -5976,7 +6170,10 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
       h->asm_cnt += 1;
     }
   }
-  if (lhs) h->have_lhs = true;
+  if (lhs) {
+    h->have_lhs = true;
+    h->lhs_version += 1;  // (a graph with cycles rebuilds its Woodbury correction)
+  }
   if (rhs) h->have_rhs = true;
   return NX_OK;
 }
@@ -6134,6 +6331,11 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   }
   // refine: the previous pass's residual check left r = b - A x in tmp
   const double* bin = refine ? h->tmp : h->rhs;
+  const bool cyc = h->n_cyc > 0 && !h->cyc_raw;  // graphs with cycles: Woodbury after the sweeps
+  const int m = 2 * h->n_cyc;
+  if (cyc && refine)  // U^T x before the sweeps add the tree solve's correction
+    hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
+                       h->cyc_cinv, nullptr, h->cyc_w, h->cyc_prev);
   if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
     h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
     h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the residual check
@@ -6174,6 +6376,12 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
                          h->pa, (int)h->E, cb, h->edge_lm, h->n_edge_dofs, h->n_own, bin, h->z, h->x);
   }
   }  // unfused
+  if (cyc) {  // x -= Z Cinv U^T (x - x_before): the couplings the tree solve dropped
+    hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
+                       h->cyc_cinv, refine ? h->cyc_prev : nullptr, h->cyc_w, nullptr);
+    hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
+                       h->x, h->cyc_z, h->n_col, h->cyc_w, m, h->n_own);
+  }
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
   hipExtLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream,
                         prof ? h->dev[6] : nullptr, prof ? h->dev[7] : nullptr, 0, csr_of(h), h->x,
@@ -6240,14 +6448,83 @@ int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
   return NX_OK;
 }
 
+// Graphs with cycles: Z = A_g^{-1} U column by column (the tree solve of a unit right-hand
+// side, accumulated into a zeroed x), then C^{-1} + U^T Z inverted on the host (m <= 256,
+// Gauss-Jordan with partial pivoting). Once per assembled matrix.
+int cyc_build(nx_network* h) {
+  const int m = 2 * h->n_cyc;
+  h->cyc_raw = true;
+  h->need_r = false;
+  for (int j = 0; j < m; ++j) {
+    HIPCALL(hipMemsetAsync(h->tmp, 0, sizeof(double) * h->n_col, h->stream));
+    HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, h->stream));
+    hipLaunchKernelGGL(k_cyc_unit, dim3(1), dim3(1), 0, h->stream, h->tmp, h->d_cyc_rows, j);
+    const int rc = launch_direct(h, 0.0, 1);
+    if (rc != NX_OK) {
+      h->cyc_raw = false;
+      return rc;
+    }
+    h->seq += 1;
+    CHECK(wait_published(h));
+    HIPCALL(hipMemcpyAsync(h->cyc_z + (int64_t)j * h->n_col, h->x, sizeof(double) * h->n_col,
+                           hipMemcpyDeviceToDevice, h->stream));
+  }
+  h->cyc_raw = false;
+  hipLaunchKernelGGL(k_cyc_cap, dim3(1), dim3(256), 0, h->stream, csr_of(h), h->cyc_z, h->n_col,
+                     h->d_cyc_rows, m, h->cyc_cap, h->cyc_cap + (int64_t)m * m);
+  std::vector<double> cap((size_t)m * m + m / 2);
+  HIPCALL(hipMemcpyAsync(cap.data(), h->cyc_cap, sizeof(double) * cap.size(),
+                         hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  // C^{-1} + U^T Z; C^{-1} of [[0, a], [a, 0]] is [[0, 1/a], [1/a, 0]]
+  std::vector<double> a(cap.begin(), cap.begin() + (int64_t)m * m), inv((size_t)m * m, 0.0);
+  for (int k = 0; k < m / 2; ++k) {
+    const double c = cap[(size_t)m * m + k];
+    if (c == 0.0) return fail(NX_ERR_STATE, "cycle chain: no coupling at its grounded end");
+    a[(size_t)(2 * k) * m + 2 * k + 1] += 1.0 / c;
+    a[(size_t)(2 * k + 1) * m + 2 * k] += 1.0 / c;
+  }
+  for (int i = 0; i < m; ++i) inv[(size_t)i * m + i] = 1.0;
+  for (int col = 0; col < m; ++col) {
+    int piv = col;
+    for (int r = col + 1; r < m; ++r)
+      if (std::fabs(a[(size_t)r * m + col]) > std::fabs(a[(size_t)piv * m + col])) piv = r;
+    if (a[(size_t)piv * m + col] == 0.0) return fail(NX_ERR_STATE, "cycle correction is singular");
+    if (piv != col)
+      for (int k = 0; k < m; ++k) {
+        std::swap(a[(size_t)piv * m + k], a[(size_t)col * m + k]);
+        std::swap(inv[(size_t)piv * m + k], inv[(size_t)col * m + k]);
+      }
+    const double d = 1.0 / a[(size_t)col * m + col];
+    for (int k = 0; k < m; ++k) {
+      a[(size_t)col * m + k] *= d;
+      inv[(size_t)col * m + k] *= d;
+    }
+    for (int r = 0; r < m; ++r) {
+      if (r == col) continue;
+      const double f = a[(size_t)r * m + col];
+      if (f == 0.0) continue;
+      for (int k = 0; k < m; ++k) {
+        a[(size_t)r * m + k] -= f * a[(size_t)col * m + k];
+        inv[(size_t)r * m + k] -= f * inv[(size_t)col * m + k];
+      }
+    }
+  }
+  HIPCALL(hipMemcpy(h->cyc_cinv, inv.data(), sizeof(double) * inv.size(), hipMemcpyHostToDevice));
+  h->cyc_version = h->lhs_version;
+  return NX_OK;
+}
+
 // Exact on this handle: one rank (no communicator, no group), the exact Schur-complement
 // preconditioner (consistent mass) on a decomposition without grounded cycle chains.
 // This rank can run the direct solve exactly: the exact Schur-complement preconditioner
 // (consistent mass) on a decomposition without grounded cycle chains; with several ranks
 // also the LDS sweeps (their mode kModeDirect) and the coarse step.
 bool direct_local(const nx_network* h) {
-  if (!(h->solver == 1 && h->pc && h->pa.exact && h->tree_exact && h->E > 0)) return false;
   const bool multi = h->comm != nullptr || h->group != nullptr || h->nranks > 1;
+  // a graph with cycles: one rank, with the Woodbury correction of its cycle chains
+  const bool exact = h->tree_exact || (h->n_cyc > 0 && !multi);
+  if (!(h->solver == 1 && h->pc && h->pa.exact && exact && h->E > 0)) return false;
   return !multi || (h->pc_lds && h->pc_jobs > 0 && h->pa.n_coarse > 0 &&
                     h->pa.n_coarse <= kCapCoarse);
 }
@@ -6384,6 +6661,10 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   const bool prof1 = !multi && h->prof;  // events bound to the dispatches (profiling)
   if (prof1 && !h->dev[0])
     for (auto& e : h->dev) HIPCALL(hipEventCreate(&e));
+  if (!multi && h->n_cyc > 0) {  // cycles: the correction of this matrix first
+    CHECK(flush_assembly(h));
+    if (h->cyc_version != h->lhs_version) CHECK(cyc_build(h));
+  }
   const bool with_asm = !multi && h->pend_lhs && h->pend_rhs;  // deferred assembly heads it
   h->last_dir_path = 0;
   if (with_asm && dstep_on(h)) {  // the fused step: assembly + solve + check in one launch
@@ -7181,6 +7462,10 @@ NX_API int nx_bench_spmv_cold(nx_network_t* h, int32_t reps, int32_t* copies_out
   return NX_OK;
 }
 
+namespace {
+void free_cycles(nx_network* h);
+}  // namespace
+
 NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chains,
                                  const int32_t* chain_edge, const int32_t* chain_flip,
                                  const int32_t* chain_up, const int32_t* chain_lo, int64_t n_slots,
@@ -7197,6 +7482,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
   CHECK(drop_handle_graphs(h));  // captured launches depend on the preconditioner
+  free_cycles(h);  // (nx_set_cycles belongs to this decomposition: set again after it)
   if (!enable) {
     h->pc = false;
     return NX_OK;
@@ -7612,6 +7898,49 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
     return fail(NX_ERR_HIP, "dense top upload failed");
   pa.n_top = nt;
   pa.dense = 1;
+  return NX_OK;
+}
+
+namespace {
+void free_cycles(nx_network* h) {
+  for (void* p : {(void*)h->d_cyc_rows, (void*)h->cyc_z, (void*)h->cyc_cinv, (void*)h->cyc_cap,
+                  (void*)h->cyc_prev, (void*)h->cyc_w})
+    if (p) (void)hipFree(p);
+  h->d_cyc_rows = nullptr;
+  h->cyc_z = h->cyc_cinv = h->cyc_cap = h->cyc_prev = h->cyc_w = nullptr;
+  h->n_cyc = 0;
+  h->cyc_version = -1;
+}
+}  // namespace
+
+NX_API int nx_set_cycles(nx_network_t* h, int32_t n, const int32_t* rows) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (n < 0 || (n > 0 && !rows)) return fail(NX_ERR_ARG, "n >= 0 row pairs");
+  if (n > 0 && !h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
+  if (n > 0 && (h->nranks > 1 || h->comm || h->group || h->n_ghost > 0))
+    return fail(NX_ERR_STATE, "the cycle correction is one rank's");
+  if (n > kMaxCyc) return fail(NX_ERR_ARG, "more cycle chains than kMaxCyc (the solve runs MINRES)");
+  for (int64_t i = 0; i < 2 * (int64_t)n; ++i)
+    if (rows[i] < 0 || rows[i] >= h->n_own) return fail(NX_ERR_ARG, "cycle row out of range");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  CHECK(drop_handle_graphs(h));
+  free_cycles(h);
+  if (n == 0) return NX_OK;
+  const int m = 2 * n;
+  HIPCALL(hipMalloc((void**)&h->d_cyc_rows, sizeof(int) * m));
+  HIPCALL(hipMalloc((void**)&h->cyc_z, sizeof(double) * m * h->n_col));
+  HIPCALL(hipMalloc((void**)&h->cyc_cinv, sizeof(double) * m * m));
+  HIPCALL(hipMalloc((void**)&h->cyc_cap, sizeof(double) * (m * m + n)));
+  HIPCALL(hipMalloc((void**)&h->cyc_prev, sizeof(double) * m));
+  HIPCALL(hipMalloc((void**)&h->cyc_w, sizeof(double) * m));
+  HIPCALL(hipMemcpy(h->d_cyc_rows, rows, sizeof(int) * m, hipMemcpyHostToDevice));
+  h->n_cyc = n;
+  // the residual check of the corrected x is the CSR's (the sweeps' fused one is A_g's), so
+  // neither the fused residual nor the fused step run
+  h->fres_ok = false;
+  h->dstep_ok = false;
   return NX_OK;
 }
 
@@ -8032,9 +8361,9 @@ NX_API int nx_debug_phases(unsigned long long* out, int32_t n) {
   return NX_OK;
 }
 
-NX_API int nx_debug_dstep(unsigned long long* out) {  // 6 x 512 stamps of k_dir_step
+NX_API int nx_debug_dstep(unsigned long long* out) {  // 12 x 512 stamps of k_dir_step
   HIPCALL(hipDeviceSynchronize());
-  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(unsigned long long) * 6 * 512));
+  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(unsigned long long) * 12 * 512));
   return NX_OK;
 }
 

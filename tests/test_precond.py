@@ -297,3 +297,79 @@ def test_forced_coarse_terminals_one_rank(case, n_term):
     pc1 = build_tree_preconditioner(lp, src, dst, m.degrees)
     z1 = apply_model(pc1, lp, dq, r)
     assert np.linalg.norm(z - z1) <= 1e-12 * np.linalg.norm(z1)
+
+
+def lattice_graph(nx_: int, ny: int):
+    """An nx_ x ny grid of pipes (many cycles: (nx_-1)(ny-1) of them), inlet/outlet at two
+    corners through extra boundary edges -- an anastomosed network's worst case."""
+    import networkx as nx
+
+    G = nx.DiGraph()
+    idx = lambda i, j: i * ny + j  # noqa: E731
+    for i in range(nx_):
+        for j in range(ny):
+            G.add_node(idx(i, j), pos=np.array([float(i), float(j) + 0.1 * i, 0.0]))
+    n = nx_ * ny
+    G.add_node(n, pos=np.array([-1.0, 0.0, 0.0]))
+    G.add_node(n + 1, pos=np.array([float(nx_), float(ny - 1) + 0.1 * (nx_ - 1), 0.0]))
+    G.add_edge(n, idx(0, 0))
+    for i in range(nx_):
+        for j in range(ny):
+            if i + 1 < nx_:
+                G.add_edge(idx(i, j), idx(i + 1, j))
+            if j + 1 < ny:
+                G.add_edge(idx(i, j), idx(i, j + 1))
+    G.add_edge(idx(nx_ - 1, ny - 1), n + 1)
+    return G
+
+
+CYCLIC = {"edge_info_N10": (CASES["edge_info_N10"][0], 10),
+          "lattice4x5_N6": (lambda: lattice_graph(4, 5), 6),
+          "lattice6x6_N3": (lambda: lattice_graph(6, 6), 3)}
+
+
+@pytest.mark.parametrize("case", sorted(CYCLIC))
+def test_cycle_rows_and_woodbury(case):
+    """Graphs with cycles (nx_set_cycles): the decomposition lists, per cycle-closing chain,
+    the (flux end, multiplier) pair its grounded end drops -- a +-1 coupling of A. Without
+    those pairs the system A_g is exactly what the tree solve inverts (the direct model equals
+    a sparse solve of A_g), and the rank-2k Woodbury correction the device applies recovers
+    A^{-1} b (the reference's MUMPS LU, solver.py:58-65) to 1e-12."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+
+    make, N = CYCLIC[case]
+    m, Ab, lp = _problem(make(), N)
+    src, dst = m.edges
+    pc = build_tree_preconditioner(lp, src, dst, m.degrees, target_jobs=16)
+    k = m.num_edges - m.num_nodes + 1  # independent cycles (one connected component)
+    assert not pc.tree_exact and pc.cyc_rows.shape == (k, 2)
+    q, lam = pc.cyc_rows[:, 0].astype(np.int64), pc.cyc_rows[:, 1].astype(np.int64)
+    Ad = Ab.toarray()
+    per = 2 * N + 1
+    assert np.all(q < lp.n_edge_dofs) and np.all(q % per % (2 * N) == 0)  # flux end rows
+    assert np.all(lam >= lp.n_edge_dofs)  # multiplier rows
+    a = Ad[q, lam]
+    assert np.all(np.abs(a) == 1.0) and np.array_equal(a, Ad[lam, q])
+    Ag = Ad.copy()
+    Ag[q, lam] = 0.0
+    Ag[lam, q] = 0.0
+    Ags = sp.csr_matrix(Ag)
+    dq = lumped_mass(Ab, lp)
+    b = np.random.default_rng(11).standard_normal(Ab.shape[0])
+    xg = direct_model(pc, lp, dq, Ags, b)
+    xg_ref = spla.spsolve(Ags.tocsc(), b)
+    assert np.linalg.norm(xg - xg_ref) <= 1e-11 * np.linalg.norm(xg_ref)
+    # Woodbury, as k_cyc_*: Z = A_g^{-1} U, Cinv = (C^{-1} + U^T Z)^{-1}
+    rows = pc.cyc_rows.reshape(-1).astype(np.int64)
+    mm = rows.size
+    Z = np.stack([direct_model(pc, lp, dq, Ags, np.eye(Ab.shape[0])[r]) for r in rows], axis=1)
+    cap = Z[rows]
+    for i in range(k):
+        cap[2 * i, 2 * i + 1] += 1.0 / a[i]
+        cap[2 * i + 1, 2 * i] += 1.0 / a[i]
+    w = np.linalg.solve(cap, xg[rows])
+    x = xg - Z @ w
+    x_ref = spla.spsolve(Ab.tocsc(), b)
+    assert np.linalg.norm(x - x_ref) <= 1e-12 * np.linalg.norm(x_ref)
+    assert mm == 2 * k
