@@ -82,8 +82,7 @@ def mr_spmv_bytes(n_rows: int, nnz: int, preconditioned: bool, iterations: int =
 
 def res_chunks(n: int) -> int:
     """256-row chunks per k_residual_ck block: csrc/nxhip.hip res_chunks()."""
-    env = int(os.environ.get("NXHIP_RES_CHUNKS", "0") or 0)
-    return max(1, env) if env > 0 else (4 if n > (4 << 20) else 2)
+    return 4 if n > (4 << 20) else 2
 
 
 def direct_kernel_bytes(n: int, nnz: int, n_e: int, E: int, N: int, B: int, nblk: int,
@@ -117,6 +116,15 @@ def direct_kernel_bytes(n: int, nnz: int, n_e: int, E: int, N: int, B: int, nblk
         # values + rhs written, dq written, edge inputs read (edge_x 48, R, bc 16, lm 8, seg 4)
         "k_assemble_seg": 8 * nnz + 8 * n + dq + 80 * E,
     }
+
+
+def dstep_bytes(n: int, nnz: int, E: int, N: int, B: int, nnz_lm: int) -> int:
+    """Algorithmic bytes of one k_dir_step launch (the whole one-rank direct step, DESIGN.md
+    section 3c): the edge inputs (80 B per edge, as the assembly kernel), the chain statics
+    (edge, flip, up, lo in phase 1; up, lo and two post slots in phase 2: 32 B per chain), the
+    junction slots' statics (~88 B each), the multiplier rows' values read; written: the CSR
+    values, rhs, lumped mass and x (the residual is formed in registers, not stored)."""
+    return 8 * nnz + 16 * n + 8 * E * (N + 1) + 80 * E + 32 * E + 88 * B + 8 * nnz_lm
 
 
 def pmc_traffic(kernel_prefix: str):
@@ -393,9 +401,32 @@ def run(args, world: int) -> int:
             step(h)
         pd = h.profile_direct()
         prof = h.profile()
+        path = h.direct_path()
         h.set_profiling(False)
         cnt = max(pd["count"], 1)
         n, nnz = h.n_rows, h.nnz
+        if path == "fused":  # one launch per step: k_dir_step (its time is pd's first slot)
+            t = pd["up_ms"] / cnt
+            kb = dstep_bytes(n, nnz, E, N, B, (nnz - E * (7 * N + 1)) // 2)
+            ach = kb / (t * 1e-3) / 1e9
+            rocname = "k_dir_step<8, 2>"
+            traffic, tsrc, rocprof_ns = (pmc_traffic(rocname) if default_workload
+                                         else (None, None, None))
+            k = {"avg_launch_ms": t, "algorithmic_bytes_per_launch": kb, "achieved_GBs": ach,
+                 "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                 "traffic_ratio": traffic / kb if traffic else None}
+            return {"bound": "hbm",
+                    "kernel": "k_dir_step<8, 2> (the whole direct step in one launch: assembly, "
+                              "up sweep, top part, down sweep, fused residual check, published "
+                              "state; latency-bound)",
+                    "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                    "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+                    "traffic_source": tsrc,
+                    "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
+                    "algorithmic_bytes_per_launch": kb, "avg_launch_ms": t,
+                    "kernels": {"k_dir_step": k}, "assembly_kernel_ms": None,
+                    "direct_path": path}
         n_e = E * (2 * N + 1)
         nblk = -(-n // (256 * res_chunks(n)))  # k_residual_ck blocks (partials)
         info = h.direct_info()
@@ -418,6 +449,15 @@ def run(args, world: int) -> int:
                     "note": "no per-dispatch events in the captured multi-rank graph"}
         dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
         d = kernels[dom]
+        rocnames = {"k_residual_ck": "k_residual_ck", "k_dir_publish_fr": "k_dir_publish_fr",
+                    "k_pc_up_lds": "k_pc_up_lds<false, 8, 2>",
+                    "k_pc_down_lds": "k_pc_down_lds<false, 8, 2, true>",
+                    "k_pc_top_lds": "k_pc_top_lds<false>",
+                    "k_assemble_seg": "k_assemble_seg<16>"}
+        for k, v in kernels.items():  # every kernel's counter bytes and their ratio
+            tr = pmc_traffic(rocnames.get(k, k))[0] if default_workload else None
+            v["traffic"] = tr
+            v["traffic_ratio"] = tr / v["algorithmic_bytes_per_launch"] if tr else None
         names = {"k_residual_ck": "k_residual_ck (CSR SpMV r = b - A x: the direct solve's "
                                   "true-residual check)",
                  "k_dir_publish_fr": "k_dir_publish_fr (the fused residual check's sums, the top "
@@ -445,7 +485,7 @@ def run(args, world: int) -> int:
                 "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
                 "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
                 "avg_launch_ms": d["avg_launch_ms"], "kernels": kernels,
-                "assembly_kernel_ms": ms["k_assemble_seg"]}
+                "assembly_kernel_ms": ms["k_assemble_seg"], "direct_path": path}
 
     roof = direct_roofline() if solver_used == "direct" else minres_roofline()
     warm_spmv_ms = h.bench_spmv(200)

@@ -288,8 +288,8 @@ class HydraulicNetworkAssembler:
         self._edge_ids = lp.edges
         # MINRES preconditioner (tree Schur complement); topology-only, built once
         if mesh.N <= 1024:
-            jobs = int(os.environ.get("NXHIP_PC_JOBS", "256"))  # swept: 64..1024
-            self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=jobs)
+            # 256 jobs = one workgroup per CU (swept on MI355X: 64..1024)
+            self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=256)
         self.set_preconditioner(True)
         self._make_spaces()
 

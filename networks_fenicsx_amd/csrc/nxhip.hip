@@ -50,7 +50,7 @@ thread_local std::string g_err;
 __device__ unsigned long long g_phase[128];
 __device__ unsigned long long g_wgs[8][512];  // per-workgroup start / end, last launch wins
 __device__ unsigned long long g_wge[8][512];
-__device__ unsigned long long g_dst[12][512];  // k_dir_step: per-workgroup stamps (nx_debug_dstep)
+__device__ unsigned long long g_dst[32][512];  // k_dir_step: per-workgroup stamps (nx_debug_dstep)
 #define NX_DSTAMP(k)                                                   \
   do {                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 512) g_dst[(k)][blockIdx.x] = wall_clock64(); \
@@ -589,14 +589,7 @@ __global__ __launch_bounds__(kBlock) void k_residual(Csr A, const double* __rest
 // The direct solve's check: the same residual, `ck` 256-row chunks per block (fewer partials
 // for the publish step to sum). Swept on MI355X (r02g, profiles/r02g_sweep.log): C3 (1 M rows)
 // 1: 0.0883-0.0896, 2: 0.0855-0.0876, 4: 0.089 ms/step; C4 (10 M rows) 1: 1.136, 4: 1.105.
-// NXHIP_RES_CHUNKS overrides.
-int res_chunks(int64_t n) {
-  static const int c = [] {
-    const char* e = std::getenv("NXHIP_RES_CHUNKS");
-    return e ? std::max(1, std::atoi(e)) : 0;
-  }();
-  return c > 0 ? c : (n > (int64_t(4) << 20) ? 4 : 2);
-}
+int res_chunks(int64_t n) { return n > (int64_t(4) << 20) ? 4 : 2; }
 __global__ __launch_bounds__(kBlock) void k_residual_ck(Csr A, const double* __restrict__ x,
                                                         const double* __restrict__ b,
                                                         double* __restrict__ partials, int nblk,
@@ -641,7 +634,6 @@ __global__ __launch_bounds__(kBlock) void k_residual_ck(Csr A, const double* __r
 // r1/r2 swap roles every iteration and w1/w2 too; the host passes the pointers.
 constexpr int kChunksADefault = 2;   // k_mr_a: chunks of 256 rows per block (swept: 1,2,4)
 constexpr int kBlocksBDefault = 512;  // k_mr_b / start: grid-stride vector kernels
-constexpr int kMaxBlocksB = 4096;
 
 struct MrState {
   double beta1, beta, oldb, alfa, dbar, epsln, phibar, cs, sn, tnorm2, relres, rtol;
@@ -1102,7 +1094,7 @@ struct PcArgs {
   const double* rhs_b;  // the assembled rhs b (a refinement pass checks b - A (x + d))
   double* rres;   // r (kept for a refinement step)
   double* rpart;  // per job: partial ||r||^2, then (n_jobs on) partial ||b||^2
-  int top_reg;    // k_pc_top_lds: register level sweeps allowed (NXHIP_TOP_REG)
+  int top_reg;    // k_pc_top_lds: register level sweeps allowed
   // the up sweep's one-wave junction levels, set up by the host: per job kmax + 1 (0: the
   // job runs the block-wide levels), per lower slot [level | nk << 8, child 0 | child 1 << 16,
   // child 2 | child 3 << 16] with child = local slot | dc offset << 6
@@ -2286,6 +2278,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
   if (threadIdx.x == 0) sOff[nt] = ndc;
   __syncthreads();
   NX_PHASE(33);
+  if constexpr (WT) NX_DSTAMP(9);
   for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {  // phase A3: fold the fixed parts
     double D0 = sD0[sl], J0 = sJ0[sl];
     for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
@@ -2304,7 +2297,8 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
   // each -- every binary tree's): thread = slot, its level, children and their g loaded
   // into registers once, so a level costs one LDS round trip for the children's values
   // (both issued together) and the division, instead of two dependent trips per child.
-  // Same arithmetic in the same order. NXHIP_TOP_REG=0: the loops over LDS below.
+  // Same arithmetic in the same order. Otherwise (a slot with more junction children): the
+  // loops over LDS below.
   const int rsl = threadIdx.x;
   const bool rmine = rsl < nt;
   int rlv = -1, rnk = 0, rch[kWaveKids];
@@ -2360,6 +2354,9 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
         sJ[rsl] = rJ;
       }
       __syncthreads();
+      if constexpr (WT) {
+        if (lv < 16) NX_DSTAMP(12 + lv);
+      }
     }
   } else
   for (int lv = nl - 1; lv >= 0; --lv) {
@@ -2390,6 +2387,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     __syncthreads();
   }
   NX_PHASE(35);
+  if constexpr (WT) NX_DSTAMP(10);
   if (MULTI && pa.n_coarse > 0) {  // back-substitution after the exchange (k_pc_coarse)
     for (int sl = threadIdx.x; sl < nt; sl += kTopThreads) {
       pa.slot_D[ts0 + sl] = sD[sl];
@@ -2412,6 +2410,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
       }
       __syncthreads();
     }
+    if constexpr (WT) NX_DSTAMP(11);
     // the stores after the levels, not inside their barriers (a workgroup barrier waits for
     // the workgroup's outstanding stores: a write-through store per level cost ~1 us each);
     // down: workgroup 0's copy only
@@ -4524,138 +4523,15 @@ __global__ __launch_bounds__(kBlock) void k_gather_out(const double* __restrict_
   if (i < n) out[i] = x[idx[i]];
 }
 
-// ---- Direct solve on a tree (nx_set_solver(h, 1), one rank): block LU of the symmetric
-// system A = [[M, K], [K^T, 0]] (flux rows q; pressure cells and multipliers s), whose Schur
-// complement S = K^T M^{-1} K is exactly what the tree preconditioner inverts (P =
-// blockdiag(M, S); precond.py). Three steps, each a sweep the preconditioner already has:
-//   y   = M^{-1} b_q                      k_dir_pre  (per chain: Thomas scans)
-//   w_s = K^T y - b_s                     k_dir_pre (cells), k_dir_wl (multipliers)
-//   x_s = S^{-1} w_s                      up / top / down sweeps, mode 2 (apply only)
-//   x_q = M^{-1} (b_q - K x_s)            k_dir_post (per chain)
-// then the true residual ||b - A x|| / ||b|| (k_residual + k_dir_publish). This is the
-// reference's default ksp_type=preonly + pc_type=lu (a direct factorisation, solver.py:
-// 58-65) specialised to the network's tree structure; a graph with cycles, where the tree
-// preconditioner grounds a chain and S^{-1} is only approximate, runs MINRES instead.
-template <int W, int CPL>
-__global__ __launch_bounds__(kBlock) void k_dir_pre(PcArgs pa, int n_chains,
-                                                    const double* __restrict__ b,
-                                                    double* __restrict__ yq,
-                                                    double* __restrict__ w) {
-#pragma clang fp contract(off)
-  constexpr int G = kBlock / W;
-  const int c = blockIdx.x * G + (int)threadIdx.x / W;
-  const bool active = c < n_chains;
-  const int l = threadIdx.x & (W - 1);
-  ChainLane<W, CPL> ch;
-  ch.setup(pa, active ? c : 0, active);
-  const int flip = active ? pa.chain_flip[c] : 0;
-  double rq[CPL], bc[CPL];
-#pragma unroll
-  for (int t = 0; t < CPL; ++t) {
-    rq[t] = ch.valid[t] ? b[ch.dof_q[t]] : 0.0;
-    bc[t] = ch.valid[t] ? b[ch.dof_c[t]] : 0.0;
-  }
-  const double rqN = ch.has_last ? b[ch.dof_qN] : 0.0;
-  double yv[CPL + 1];
-  chain_mass_solve<W, CPL>(pa, ch, rq, rqN, yv);
-  // y at the fluxes (the multiplier rows read the edge ends); the cell rows of K^T y - b
-  // from the lane's values and the next lane's first: cell k lies between chain fluxes k
-  // and k + 1 (q_N is the has_last lane's element CPL); row p_g = +q_g - q_{g+1}
-  const double nxt0 = __shfl_down(yv[0], 1, W);
-  const int N = pa.N;
-#pragma unroll
-  for (int t = 0; t < CPL; ++t) {
-    if (!ch.valid[t]) continue;
-    yq[ch.dof_q[t]] = yv[t];
-    const int k = l * CPL + t;
-    const double ynext = (k + 1 == N) ? yv[CPL] : (t + 1 < CPL ? yv[t + 1] : nxt0);
-    const double d = yv[t] - ynext;
-    w[ch.dof_c[t]] = (flip ? -d : d) - bc[t];
-  }
-  if (ch.has_last) yq[ch.dof_qN] = yv[CPL];
-}
+// ---- Direct solve (nx_set_solver(h, 1)): block LU of the symmetric system A = [[M, K],
+// [K^T, 0]] (flux rows q; pressure cells and multipliers s), whose Schur complement
+// S = K^T M^{-1} K is exactly what the tree preconditioner inverts (P = blockdiag(M, S);
+// precond.py): y = M^{-1} b_q, x_s = S^{-1} (K^T y - b_s), x_q = M^{-1} (b_q - K x_s), all
+// inside the LDS sweeps' mode 3 (kModeDirect; one rank: k_dir_step), then the true residual.
+// This is the reference's default ksp_type=preonly + pc_type=lu (a direct factorisation,
+// solver.py:58-65) specialised to the network's tree structure (graphs with cycles: the
+// Woodbury correction of the cycle chains, k_cyc_*).
 
-// Multiplier rows of w = K^T y - b (+-1 at the flux ends of the edges meeting there).
-__global__ __launch_bounds__(kBlock) void k_dir_wl(Csr A, int64_t n_edge_dofs,
-                                                   const double* __restrict__ y,
-                                                   const double* __restrict__ b,
-                                                   double* __restrict__ w) {
-#pragma clang fp contract(off)
-  const int64_t i = n_edge_dofs + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.n_rows) return;
-  double acc = 0.0;
-  for (int k = A.rowptr[i]; k < A.rowptr[i + 1]; ++k) acc += A.val[k] * y[A.col[k]];
-  w[i] = acc - b[i];
-}
-
-// x_q = M^{-1} (b_q - K z_s) per chain (conservatively, direct_flux_cons), x_s = z_s.
-// Blocks past the chains copy the multiplier rows.
-template <int W, int CPL, bool ACC>
-__global__ __launch_bounds__(kBlock) void k_dir_post(PcArgs pa, int n_chains, int chain_blocks,
-                                                     const int* __restrict__ edge_lm,
-                                                     int64_t n_edge_dofs, int64_t n_own,
-                                                     const double* __restrict__ b,
-                                                     const double* __restrict__ z,
-                                                     double* __restrict__ x) {
-#pragma clang fp contract(off)
-  if ((int)blockIdx.x >= chain_blocks) {
-    const int64_t i = n_edge_dofs + (int64_t)(blockIdx.x - chain_blocks) * kBlock + threadIdx.x;
-    if (i < n_own) x[i] = ACC ? x[i] + z[i] : z[i];
-    return;
-  }
-  constexpr int G = kBlock / W;
-  const int c = blockIdx.x * G + (int)threadIdx.x / W;
-  const bool active = c < n_chains;
-  ChainLane<W, CPL> ch;
-  ch.setup(pa, active ? c : 0, active);
-  const int e = active ? pa.chain_edge[c] : 0;
-  const int ls = active ? edge_lm[2 * e] : -1, lt = active ? edge_lm[2 * e + 1] : -1;
-  const double zsrc = ls >= 0 ? z[ls] : 0.0, zdst = lt >= 0 ? z[lt] : 0.0;
-  double bq[CPL], bc[CPL];
-#pragma unroll
-  for (int t = 0; t < CPL; ++t) {
-    bq[t] = ch.valid[t] ? b[ch.dof_q[t]] : 0.0;
-    bc[t] = ch.valid[t] ? b[ch.dof_c[t]] : 0.0;
-    if (ch.valid[t]) x[ch.dof_c[t]] = ACC ? x[ch.dof_c[t]] + z[ch.dof_c[t]] : z[ch.dof_c[t]];
-  }
-  const double bqN = ch.has_last ? b[ch.dof_qN] : 0.0;
-  const int flip = active ? pa.chain_flip[c] : 0;  // chain top = the edge's source unless flipped
-  double xv[CPL + 1];
-  direct_flux_cons<W, CPL>(ch, flip, bc, bq, bqN, flip ? zdst : zsrc, flip ? zsrc : zdst, xv);
-#pragma unroll
-  for (int t = 0; t < CPL; ++t)
-    if (ch.valid[t]) x[ch.dof_q[t]] = ACC ? x[ch.dof_q[t]] + xv[t] : xv[t];
-  if (ch.has_last) x[ch.dof_qN] = ACC ? x[ch.dof_qN] + xv[CPL] : xv[CPL];
-}
-
-// Several ranks: this rank's ||r||^2 and ||b||^2 partial sums -> out[0], out[1] (then
-// all-reduced and published by k_dir_publish_red).
-__global__ __launch_bounds__(kReduceThreads) void k_dir_reduce2(const double* __restrict__ p,
-                                                                int nblk, double* __restrict__ out) {
-  __shared__ double s_r[kReduceThreads / 64], s_b[kReduceThreads / 64];
-  double rr = 0.0, bb = 0.0;
-  for (int i = threadIdx.x; i < nblk; i += kReduceThreads) {
-    rr += p[i];
-    bb += p[nblk + i];
-  }
-  rr = wave_sum(rr);
-  bb = wave_sum(bb);
-  if ((threadIdx.x & 63) == 0) {
-    s_r[threadIdx.x >> 6] = rr;
-    s_b[threadIdx.x >> 6] = bb;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    rr = 0.0;
-    bb = 0.0;
-    for (int w = 0; w < kReduceThreads / 64; ++w) {
-      rr += s_r[w];
-      bb += s_b[w];
-    }
-    out[0] = rr;
-    out[1] = bb;
-  }
-}
 
 // Several ranks, fused check: this rank's ||r||^2, ||b||^2 (the down sweeps' partials in job
 // order, then its owned rows no job could form -- the top part's and the cut junctions'
@@ -5147,7 +5023,7 @@ struct nx_network {
   int* send_idx = nullptr;
   double* send_buf = nullptr;
   // beta^2 partials of all ranks (nranks), gathered point-to-point with the halo so the
-  // iteration needs no separate all-reduce for it (NXHIP_BETA_P2P=0: all-reduce instead)
+  // iteration needs no separate all-reduce for it
   double* gath = nullptr;
   bool beta_p2p = true;
   bool rccl_graph_ok = true;  // capture of the RCCL iteration worked (or was not tried)
@@ -5795,9 +5671,6 @@ NX_API int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* e
   }
   if ((rc = dalloc(&h->x, n_col))) return bail(rc);
   if ((rc = dalloc(&h->tmp, n_col))) return bail(rc);
-  if (const char* e = std::getenv("NXHIP_A_CHUNKS")) h->chunksA = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("NXHIP_B_BLOCKS"))
-    h->nB = std::min(kMaxBlocksB, std::max(1, std::atoi(e)));
   h->nA = std::max(1, grid_of(n_own, kRowsPerBlock * h->chunksA));
   if ((rc = dalloc(&h->partials, 2 * (int64_t)h->nblk))) return bail(rc);
   if ((rc = dalloc(&h->partA, h->nA))) return bail(rc);
@@ -6124,13 +5997,9 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
 // Deferred assembly: on one rank (no group, no communicator, P1/DG0) nx_assemble only
 // records what to assemble, and the next call that uses the device -- every NX_API entry
 // point flushes it first -- launches it; the direct solve captures it as the head of its
-// own graph instead (one launch per step less). NXHIP_DEFER=0 launches at once.
+// own graph instead (one launch per step less).
 bool defer_ok(const nx_network* h) {
-  static const bool env = [] {
-    const char* e = std::getenv("NXHIP_DEFER");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return env && !h->fe && h->nranks == 1 && h->comm == nullptr && h->group == nullptr;
+  return !h->fe && h->nranks == 1 && h->comm == nullptr && h->group == nullptr;
 }
 
 int flush_assembly(nx_network* h) {
@@ -6301,28 +6170,17 @@ LeanGraphs& lean_of(const Team& t) { return t.g ? t.g->lean : t.hs[0]->lean; }
 // refine = 0: x = A^{-1} b; refine = 1: one step of iterative refinement, x += A^{-1} r with
 // r = b - A x as the previous pass's residual check left it in tmp. Both end with the true
 // residual (r kept in tmp again) published.
-int top_down_flag() {
-  static const int f = [] {
-    const char* e = std::getenv("NXHIP_TOP_DOWN");
-    return (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
-  }();
-  return f;
-}
 
 // One rank, direct: the top part in every down workgroup (pa.topdown) -- only when the jobs
 // run in one round (every workgroup repeats the top part; C4 on one GPU, 4 rounds, measured
 // 0.524 vs 0.488 ms/step with the top kernel)
 bool top_down_on(const nx_network* h) {
-  return h->fres_ok && h->top_nt > 0 && top_down_flag() && h->pc_jobs <= h->n_cu;
+  return h->fres_ok && h->top_nt > 0 && h->pc_jobs <= h->n_cu;
 }
 
 template <int W, int CPL>
 void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const hipEvent_t* evs = prof ? h->dev : nullptr;
-  constexpr int G = kBlock / W;
-  const int cb = grid_of(h->E, G);
-  double* yq = h->vb[1];
-  double* w = h->vb[0];
   if (refine && h->need_r) {  // the fused step (k_dir_step) kept no residual: r = b - A x
     const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
     hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
@@ -6336,10 +6194,10 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   if (cyc && refine)  // U^T x before the sweeps add the tree solve's correction
     hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
                        h->cyc_cinv, nullptr, h->cyc_w, h->cyc_prev);
-  if (h->pc_lds) {  // fused: the LDS sweeps in mode kModeDirect do pre and post themselves
+  {  // the LDS sweeps in mode kModeDirect (direct_local: pc_lds)
     h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
     h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the residual check
-    // and every down workgroup the top part (no k_pc_top_lds; NXHIP_TOP_DOWN=0 keeps it)
+    // and every down workgroup the top part (no k_pc_top_lds) when the jobs run in one round
     const bool td = top_down_on(h);
     h->pa.topdown = td ? 1 : 0;
     launch_pc<false>(h, const_cast<double*>(bin), bin, h->st, h->st + 1, kModeDirect, 0, h->x, evs);
@@ -6356,26 +6214,7 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
                             h->pa.slot_lam + h->top_ts0, h->pa.slot_z + h->top_ts0, ntop);
       return;
     }
-  } else {
-  const int64_t n_lm = h->n_own - h->n_edge_dofs;
-  if (cb > 0)
-    hipLaunchKernelGGL((k_dir_pre<W, CPL>), dim3(cb), dim3(kBlock), 0, h->stream, h->pa, (int)h->E,
-                       bin, yq, w);
-  if (n_lm > 0)
-    hipLaunchKernelGGL(k_dir_wl, dim3(grid_of(n_lm, kBlock)), dim3(kBlock), 0, h->stream,
-                       csr_of(h), h->n_edge_dofs, yq, bin, w);
-  launch_pc<false>(h, w, w, h->st, h->st + 1, 2, 0);
-  launch_pc<false>(h, w, w, h->st, h->st + 1, 2, 1);
-  const int lb = grid_of(n_lm, kBlock);
-  if (cb + lb > 0) {
-    if (refine)
-      hipLaunchKernelGGL((k_dir_post<W, CPL, true>), dim3(cb + lb), dim3(kBlock), 0, h->stream,
-                         h->pa, (int)h->E, cb, h->edge_lm, h->n_edge_dofs, h->n_own, bin, h->z, h->x);
-    else
-      hipLaunchKernelGGL((k_dir_post<W, CPL, false>), dim3(cb + lb), dim3(kBlock), 0, h->stream,
-                         h->pa, (int)h->E, cb, h->edge_lm, h->n_edge_dofs, h->n_own, bin, h->z, h->x);
   }
-  }  // unfused
   if (cyc) {  // x -= Z Cinv U^T (x - x_before): the couplings the tree solve dropped
     hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
                        h->cyc_cinv, refine ? h->cyc_prev : nullptr, h->cyc_w, nullptr);
@@ -6393,13 +6232,12 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
 // The fused direct step (k_dir_step): one rank, the deferred assembly pending, the LDS
 // sweeps with the fused residual, one round of jobs (all resident), direct launches (a graph
 // would freeze the launch count), not disabled by a failed launch or NXHIP_DIR_FUSED=0.
-int dir_graph_flag();
 bool dstep_on(const nx_network* h) {
   const char* e = std::getenv("NXHIP_DIR_FUSED");  // read per solve: tests switch it
   const bool env = e == nullptr || std::atoi(e) != 0;
   return env && h->dstep_ok && !h->dstep_off && h->pc_lds && h->fres_ok && h->pa.exact &&
          h->pc_jobs > 0 && h->pc_jobs <= h->n_cu && h->comm == nullptr && h->group == nullptr &&
-         h->nranks == 1 && !dir_graph_flag();
+         h->nranks == 1;
 }
 
 template <int W, int CPL>
@@ -6524,9 +6362,12 @@ bool direct_local(const nx_network* h) {
   const bool multi = h->comm != nullptr || h->group != nullptr || h->nranks > 1;
   // a graph with cycles: one rank, with the Woodbury correction of its cycle chains
   const bool exact = h->tree_exact || (h->n_cyc > 0 && !multi);
-  if (!(h->solver == 1 && h->pc && h->pa.exact && exact && h->E > 0)) return false;
-  return !multi || (h->pc_lds && h->pc_jobs > 0 && h->pa.n_coarse > 0 &&
-                    h->pa.n_coarse <= kCapCoarse);
+  // the LDS sweeps run it (their mode 3); the global-memory fallback (LDS caps exceeded)
+  // leaves the solve to MINRES
+  if (!(h->solver == 1 && h->pc && h->pc_lds && h->pa.exact && exact && h->E > 0)) return false;
+  // several ranks: the coarse step, and the residual formed by the down sweeps
+  return !multi || (h->pc_jobs > 0 && h->pa.n_coarse > 0 && h->pa.n_coarse <= kCapCoarse &&
+                    h->fres_ok);
 }
 
 // The ranks decide together: a group compares its handles here, RCCL ranks agreed in
@@ -6607,19 +6448,11 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
     return NX_OK;
   }
   CHECK(team_halo(t, VS_X, 0));
-  for (int r = 0; r < t.P; ++r) {
-    nx_network* h = t.hs[r];
-    if (h->fres_ok) {  // the down sweeps formed the local rows; the rest need the halo of x
-      hipLaunchKernelGGL(k_dir_reduce2_fr, dim3(1), dim3(kReduceThreads), 0, h->stream,
-                         h->pa.rpart, h->pc_jobs, h->d_left, h->n_left, csr_of(h), h->x, h->rhs,
-                         h->tmp, h->dir_bb, refine, h->red + 2);
-      continue;
-    }
-    const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
-    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));  // r kept: refinement
-    hipLaunchKernelGGL(k_dir_reduce2, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                       nrb, h->red + 2);
+  for (int r = 0; r < t.P; ++r) {  // the down sweeps formed the local rows (direct_local:
+    nx_network* h = t.hs[r];       // fres_ok); the rest need the halo of x
+    hipLaunchKernelGGL(k_dir_reduce2_fr, dim3(1), dim3(kReduceThreads), 0, h->stream,
+                       h->pa.rpart, h->pc_jobs, h->d_left, h->n_left, csr_of(h), h->x, h->rhs,
+                       h->tmp, h->dir_bb, refine, h->red + 2);
   }
   CHECK(team_allreduce(t, 2, 2));
   for (int r = 0; r < t.P; ++r) {
@@ -6641,17 +6474,10 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
 // One rank: the direct solve's five kernels are launched directly by default -- from an
 // idle stream the first starts ~3 us after the call and the host enqueues the rest while
 // it runs, where a graph replay costs ~10 us of fixed host time (C3: 0.0708 vs 0.0739
-// ms/step, r02n A/B). NXHIP_DIR_GRAPH=1 replays a graph instead. Several ranks: graphs.
+// ms/step, r02n A/B). Several ranks: graphs.
 // (Measured and kept out: the down sweep's last workgroup publishing through an atomic
 // ticket instead of k_dir_publish_fr -- 0.079 vs 0.072 ms/step: every workgroup's release
 // fence writes back its XCD's L2, dirty with x, before the ticket.)
-int dir_graph_flag() {
-  static const int f = [] {
-    const char* e = std::getenv("NXHIP_DIR_GRAPH");
-    return (e != nullptr && std::atoi(e) != 0) ? 1 : 0;
-  }();
-  return f;
-}
 
 int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
                  int32_t* converged) {
@@ -6736,8 +6562,8 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     if (asmb) CHECK(launch_assembly(h, 1, 1));
     return launch_direct(h, rtol, refine);
   };
-  // one rank: graph replay or the five launches issued directly (NXHIP_DIR_GRAPH)
-  const bool graphs = (!h->comm || h->rccl_graph_ok) && (multi || dir_graph_flag());
+  // several ranks: graph replay; one rank: the launches issued directly
+  const bool graphs = (!h->comm || h->rccl_graph_ok) && multi;
   auto run = [&](hipGraphExec_t* exec, hipGraph_t* graph, int* len, double* grtol, int key,
                  int refine, bool asmb) -> int {
     if (graphs && (!*exec || *grtol != rtol || *len != key)) {
@@ -6785,13 +6611,10 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   return NX_OK;
 }
 
-// 1: one graph per solve where possible (default; NXHIP_LEAN=0 or nx_set_lean(0): the
+// 1: one graph per solve where possible (default; nx_set_lean(0): the
 // general path with eager prologue and chunked iterations)
-int& lean_flag() {
-  static int f = [] {
-    const char* e = std::getenv("NXHIP_LEAN");
-    return (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
-  }();
+int& lean_flag() {  // nx_set_lean
+  static int f = 1;
   return f;
 }
 bool lean_mode() { return lean_flag() != 0; }
@@ -7054,12 +6877,8 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   const bool prof = h0->prof && t.g == nullptr;
   // RCCL iterations are captured too (host-side enqueue of ~8 operations per iteration
   // would otherwise pace the loop); if the capture fails, that handle stays eager
-  static const bool rccl_graph_env = [] {
-    const char* e = std::getenv("NXHIP_RCCL_GRAPH");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
   const bool rccl = t.hs[0]->comm != nullptr;
-  bool use_graph = !prof && (!rccl || (rccl_graph_env && h0->rccl_graph_ok));
+  bool use_graph = !prof && (!rccl || h0->rccl_graph_ok);
   if (use_graph) {
     const int rc = build_chunk_graph(t, check_every);
     if (rc != NX_OK) {
@@ -7499,11 +7318,6 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   else if (N <= 512) variant = 8;
   else if (N <= 1024) variant = 9;
   else return fail(NX_ERR_ARG, "tree preconditioner supports N <= 1024 cells per edge");
-  if (const char* e = std::getenv("NXHIP_PC_VARIANT")) {  // tuning: (W, CPL) override
-    const int v = std::atoi(e);
-    const int cap[10] = {16, 32, 64, 128, 256, 16, 16, 32, 512, 1024};
-    if (v >= 0 && v < 10 && N <= cap[v]) variant = v;
-  }
   if (n_chains != h->E) return fail(NX_ERR_ARG, "one chain per local edge expected");
   // one slot per owned multiplier, plus (several ranks) the ghost junctions at the ends of
   // local edges, which are coarse (nx_set_coarse)
@@ -7593,8 +7407,6 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   pa.KJ = nullptr;
   pa.dc_kappa = scratch(slot_dc_off[n_slots]);
   pa.slot_invD = scratch(n_slots);
-  if (const char* e = std::getenv("NXHIP_PC_FACTOR"))
-    if (std::atoi(e) == 0) pa.dc_kappa = nullptr;  // keep the per-iteration eliminations
   {  // consistent-mass flux block: pivots of T = tridiag(1, 4, 1), 2 at both ends
     const std::vector<double> ti = mass_lu(N);
     double* d = scratch((int64_t)ti.size());
@@ -7602,9 +7414,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
                             hipSuccess)
       return fail(NX_ERR_HIP, "preconditioner upload failed");
     pa.Tlu = d;
-    pa.exact = 1;
-    if (const char* e = std::getenv("NXHIP_PC_EXACT"))
-      if (std::atoi(e) == 0) pa.exact = 0;  // lumped D: P = blockdiag(D, G^T D^{-1} G)
+    pa.exact = 1;  // (nx_set_pc_exact(h, 0): lumped D, P = blockdiag(D, G^T D^{-1} G))
   }
   for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
                         (const void*)pa.chain_lo, (const void*)pa.slot_lam, (const void*)pa.slot_pchain,
@@ -7618,9 +7428,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     if (p == nullptr) return fail(NX_ERR_HIP, "preconditioner upload failed");
   if (!h->z) CHECK(dalloc(&h->z, std::max<int64_t>(h->n_col, 1)));
   if (!h->vv) CHECK(dalloc(&h->vv, std::max<int64_t>(h->n_own, 1)));
-  {  // stored Lanczos vectors (NXHIP_STORED_V=0: the w recurrence from the first rotation)
-    const char* e = std::getenv("NXHIP_STORED_V");
-    if ((e == nullptr || std::atoi(e) != 0) && !h->vs) {
+  {  // stored Lanczos vectors
+    if (!h->vs) {
       CHECK(dalloc(&h->vs, (int64_t)kMaxV * std::max<int64_t>(h->n_own, 1)));
       CHECK(dalloc(&h->hist, 4 * (int64_t)kMaxV));
     }
@@ -7751,7 +7560,6 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     }
   }
   pa.top_reg = 1;
-  if (const char* e = std::getenv("NXHIP_TOP_REG")) pa.top_reg = std::atoi(e) != 0;
   // the up sweep's one-wave level set-up (k_pc_up_lds): per eligible job (<= 64 slots, <=
   // kCapLvl levels, <= kWaveKids junction children per slot) each slot's level, children
   // (local slot) and their hanging-chain entries (offset from the job's first), packed
@@ -7846,8 +7654,6 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
       return fail(NX_ERR_ARG, "job_root_u / job_root_dc out of range");
   // dense mode: single rank, LDS kernels, a top part that fits
   if (!fits || !h->pc_lds || nt < 1 || nt > kCapT || n_jobs < 1) return NX_OK;
-  if (const char* e = std::getenv("NXHIP_PC_DENSE"))
-    if (std::atoi(e) == 0) return NX_OK;
   auto up = [&](const int32_t* src, int64_t n) -> const int* {
     int* d = nullptr;
     if (n <= 0) n = 1;
@@ -8091,8 +7897,7 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   pa.xalpha = cb + 3 * n_coarse;
   pa.Gc = nullptr;
   if (n_coarse > 0 && n_coarse <= kCapCoarseLds) {
-    const char* e = std::getenv("NXHIP_PC_GC");  // 0: level sweeps in every down workgroup
-    if (!e || std::atoi(e) != 0) {
+    {
       double* gc = nullptr;
       HIPCALL(hipMalloc((void**)&gc, sizeof(double) * n_coarse * n_coarse));
       HIPCALL(hipMemset(gc, 0, sizeof(double) * n_coarse * n_coarse));
@@ -8104,13 +7909,11 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   HIPCALL(hipMalloc((void**)&zc, sizeof(double) * n_coarse));
   h->pc_bufs.push_back(zc);
   pa.zc = zc;
-  // linear form needs the LDS kernels; NXHIP_PC_LIN=0 keeps alpha's own all-reduce
+  // linear form needs the LDS kernels (the global-memory ones keep alpha's own all-reduce)
   pa.lin = h->pc_lds ? 1 : 0;
-  if (const char* e = std::getenv("NXHIP_PC_LIN")) pa.lin = pa.lin && std::atoi(e) != 0;
   // fused one-workgroup steps (k_pc_cpart in the up sweep's last workgroup, the coarse solve
-  // in every down workgroup); NXHIP_PC_FUSE=0 keeps the separate kernels
+  // in every down workgroup); the global-memory kernels keep the separate ones
   pa.fused = (h->pc_lds && h->pc_jobs > 0 && n_coarse <= kCapCoarseLds) ? 1 : 0;
-  if (const char* e = std::getenv("NXHIP_PC_FUSE")) pa.fused = pa.fused && std::atoi(e) != 0;
   pa.fuse_pack = 0;  // set per solve path (solve_lean)
   {
     int* tk = nullptr;
@@ -8244,7 +8047,6 @@ NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_
   CHECK(dalloc(&h->gath, nranks));
   HIPCALL(hipMemsetAsync(h->gath, 0, sizeof(double) * nranks, h->stream));
   h->beta_p2p = true;
-  if (const char* e = std::getenv("NXHIP_BETA_P2P")) h->beta_p2p = std::atoi(e) != 0;
   h->sched_checked = false;  // beta_p2p is part of the schedule signature
   h->nranks = nranks;
   h->rank = rank;
@@ -8363,7 +8165,7 @@ NX_API int nx_debug_phases(unsigned long long* out, int32_t n) {
 
 NX_API int nx_debug_dstep(unsigned long long* out) {  // 12 x 512 stamps of k_dir_step
   HIPCALL(hipDeviceSynchronize());
-  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(unsigned long long) * 12 * 512));
+  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(unsigned long long) * 32 * 512));
   return NX_OK;
 }
 

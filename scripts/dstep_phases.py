@@ -40,11 +40,11 @@ def main() -> int:
         it, rr, conv = h.solve(1e-12, 100, 4)
     assert h.direct_path() == "fused", h.direct_path()
     nj = asm.tree_preconditioner.n_jobs
-    buf = (C.c_ulonglong * (12 * 512))()
+    buf = (C.c_ulonglong * (32 * 512))()
     fn = _lib.lib().nx_debug_dstep
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
     _lib.check(fn(buf))
-    g = np.array(buf, dtype=np.float64).reshape(12, 512)[:, :nj]
+    g = np.array(buf, dtype=np.float64).reshape(32, 512)[:, :nj]
     t0 = g[0].min()
     us = (g - t0) / 100.0  # 100 MHz ticks -> us
     names = ["start", "phase-1 arrival", "top values in", "phase-2 arrival", "published",
@@ -56,6 +56,10 @@ def main() -> int:
     last1 = int(np.argmax(g[5]))  # the workgroup that solved the top part (latest stamp 5)
     print(f"  top part by wg {last1}: arrival {us[1][last1]:7.2f}, inputs loaded "
           f"{us[6][last1]:7.2f}, solved {us[7][last1]:7.2f}, values out {us[5][last1]:7.2f}")
+    print(f"  top part phases: set-up {us[9][last1]:7.2f}, up levels {us[10][last1]:7.2f}, "
+          f"down levels {us[11][last1]:7.2f}")
+    lv = [f"{us[12 + q][last1]:.2f}" for q in range(8)]
+    print(f"  up levels (deepest first) end at: {' '.join(reversed(lv))}")
     v = us[8]
     print(f"  {'stores issued':16s} min {v.min():7.2f}  med {np.median(v):7.2f}  max {v.max():7.2f}")
     pub = np.argmax(g[4])

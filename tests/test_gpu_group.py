@@ -91,18 +91,12 @@ def test_group_solve_matches_direct(case, P, pc):
         grp.close()
 
 
-@pytest.mark.parametrize("env", [{"NXHIP_PC_LIN": "0"}, {"NXHIP_PC_GLOBAL": "1"},
-                                 {"NXHIP_BETA_P2P": "0"}, {"NXHIP_PC_DENSE": "0"},
-                                 {"NXHIP_PC_FACTOR": "0"}, {"NXHIP_PC_FUSE": "0"},
-                                 {"NXHIP_PC_GC": "0"}])
+@pytest.mark.parametrize("env", [{}, {"NXHIP_PC_GLOBAL": "1"}])
 def test_group_alternative_kernel_paths(env, monkeypatch):
-    """Alternative multi-rank paths: alpha with its own all-reduce (NXHIP_PC_LIN=0), the
-    global-memory preconditioner kernels (NXHIP_PC_GLOBAL=1), beta^2 by all-reduce
-    (NXHIP_BETA_P2P=0), the per-iteration top kernel instead of the dense top
-    (NXHIP_PC_DENSE=0), per-iteration eliminations instead of factored ones (NXHIP_PC_FACTOR=0),
-    separate k_pc_cpart / k_pc_coarse / halo-pack kernels instead of the fused ones
-    (NXHIP_PC_FUSE=0), the coarse level sweeps in every down workgroup instead of the dense
-    Gc product (NXHIP_PC_GC=0)."""
+    """The multi-rank MINRES with the LDS sweeps (linear form, fused coarse steps, dense top,
+    beta^2 point-to-point) and with the global-memory preconditioner kernels
+    (NXHIP_PC_GLOBAL=1: the fallback when a job exceeds the LDS caps -- alpha with its own
+    all-reduce, separate k_pc_cpart / k_pc_coarse kernels, the per-iteration top kernel)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     case, P = "depth6_N40", 4
@@ -407,9 +401,11 @@ def test_group_rank_without_dense_top_fails_loudly(monkeypatch):
     try:
         grp.compute_forms(p_bc_ex=pbc)
         grp.assemble()
-        monkeypatch.setenv("NXHIP_PC_DENSE", "0")
-        grp.assemblers[1].set_preconditioner(True)
-        monkeypatch.delenv("NXHIP_PC_DENSE")
+        import dataclasses
+
+        a1 = grp.assemblers[1]  # its decomposition uploaded without the dense top's lists
+        a1.handle.set_preconditioner(dataclasses.replace(
+            a1.tree_preconditioner, job_tslot=np.zeros(0, np.int32)))
         with pytest.raises(NxError, match="different kernel schedules"):
             grp.solve(1e-12, 50000, 4)
         grp._close_group()
