@@ -1113,8 +1113,9 @@ constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve 
 
 // This rank's share of the coarse system: the eliminated (D, J) of its coarse slots (all
 // in the top part, level 0) and the chains joining two coarse junctions. sD/sJ are indexed
-// by top-part position. Ends with the buffer complete (one workgroup).
-template <int BS>
+// by top-part position. Ends with the buffer complete (one workgroup). WT: the chains' data
+// were handed over inside the launch (k_dir_team_up): write-through loads.
+template <int BS, bool WT = false>
 __device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const double* sD,
                                    const double* sJ) {
   // small coarse sets: the buffer is built in LDS and the coarse chains' data loaded in
@@ -1142,9 +1143,9 @@ __device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const doub
       const int c = pa.cc_chain[i];
       sCt[i] = pa.cc_top[i];
       sCb[i] = pa.cc_bot[i];
-      sCg[i] = 1.0 / pa.chain_T[c];
-      sCit[i] = pa.chain_It[c];
-      sCib[i] = pa.chain_Ib[c];
+      sCg[i] = 1.0 / ldv<WT>(pa.chain_T + c);
+      sCit[i] = ldv<WT>(pa.chain_It + c);
+      sCib[i] = ldv<WT>(pa.chain_Ib + c);
     }
   __syncthreads();
   if (lds) {  // thread = coarse junction k: its sums over the chains in chain order (the same
@@ -1173,11 +1174,11 @@ __device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const doub
     for (int i = 0; i < ncc; ++i) {
       const int c = pa.cc_chain[i];
       const int t = pa.cc_top[i], b = pa.cc_bot[i];
-      const double g = 1.0 / pa.chain_T[c];
+      const double g = 1.0 / ldv<WT>(pa.chain_T + c);
       buf[t] += g;
       buf[b] += g;
-      buf[nC + t] += pa.chain_It[c];
-      buf[nC + b] += pa.chain_Ib[c];
+      buf[nC + t] += ldv<WT>(pa.chain_It + c);
+      buf[nC + b] += ldv<WT>(pa.chain_Ib + c);
       buf[2 * nC + b] = g;
     }
   }
@@ -2393,7 +2394,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
       pa.slot_D[ts0 + sl] = sD[sl];
       pa.slot_J[ts0 + sl] = sJ[sl];
     }
-    pc_coarse_partials<kTopThreads>(pa, ts0, nt, sD, sJ);
+    pc_coarse_partials<kTopThreads, WT>(pa, ts0, nt, sD, sJ);
     return;
   }
   double part = 0.0;
@@ -3423,7 +3424,10 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
 // keep (the job's chains fit one pass): the assembly's stores are left to the caller
 // (dir_chain_store after the hand-off) and the lane state stays in L for phase 2; the slot's
 // back-substitution coefficients (thread = slot) are returned in sA_ / sB_ either way.
-template <int W, int CPL>
+// MULTI (k_dir_team_up): every chain's T / It / Ib and every slot's D / J / A / B also go to
+// global memory (the separate down sweep after the coarse all-reduce reads them), as
+// k_pc_up_lds stores them.
+template <int W, int CPL, bool MULTI = false>
 __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da,
                                              double* lds, DirLane<W, CPL>& L, bool keep,
                                              double& sA_, double& sB_) {
@@ -3494,6 +3498,10 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
         st_wt(pa.chain_T + c, ch.T);
         st_wt(pa.chain_It + c, it);
         st_wt(pa.chain_Ib + c, ibe);
+      } else if (MULTI) {
+        pa.chain_T[c] = ch.T;
+        pa.chain_It[c] = it;
+        pa.chain_Ib[c] = ibe;
       }
     }
   }
@@ -3652,6 +3660,13 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
     if (j < root1) {
       st_wt(pa.slot_D + j, sD[sl]);
       st_wt(pa.slot_J + j, J);
+    } else if (MULTI) {
+      pa.slot_D[j] = sD[sl];
+      pa.slot_J[j] = J;
+    }
+    if (MULTI) {
+      pa.slot_A[j] = sA_;
+      pa.slot_B[j] = sB_;
     }
   }
 }
@@ -4040,6 +4055,77 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
     dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, lane_on, L);
     stores();
   }
+}
+
+// k_dir_team_up: the first half of the several-rank direct step (one rank's share, before
+// the coarse all-reduce) in ONE launch: every workgroup assembles its chains' edges in
+// registers and runs the up sweep (dir_up_fused<MULTI>: phase 1 of k_dir_step, with the
+// slots' and chains' data stored for the down sweep), hands the top part's inputs over
+// write-through and leaves after its assembly stores; the workgroup arriving last solves the
+// rank's top part and builds its coarse partials [D | J | G] (top_body<MULTI, WT>: what
+// k_pc_top_lds does), then re-assembles its own lanes and stores them. It replaces
+// k_assemble_seg -> k_pc_up_lds (mode 3) -> k_pc_top_lds. No workgroup waits for another
+// (the last arrival does the work), so any number of jobs may run; the arrival counter is
+// reset by the last workgroup (graph replays launch it with the same arguments).
+template <int W, int CPL>
+__global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep da) {
+  __shared__ double smem[kDirLds];
+  __shared__ int sFlag;
+  const int job = blockIdx.x;
+  const int nj = pa.n_jobs;
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  const bool keep = c1 - c0 <= kPcThreads / W;
+  DirLane<W, CPL> L;
+  double sA_ = 0.0, sB_ = 0.0;
+  dir_up_fused<W, CPL, true>(pa, da, smem, L, keep, sA_, sB_);
+  auto stores = [&]() {
+    const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
+    for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
+      if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
+      if (i < da.B) da.rhs_lm[i] = 0.0;
+    }
+    if (keep) dir_chain_store<W, CPL>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
+  };
+  vm_drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(da.sync, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    sFlag = old == (unsigned)(nj - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!sFlag) {
+    stores();
+    return;
+  }
+  if (pa.top_nt > 0) {
+    double* t = smem;
+    TopLds T;
+    T.sD0 = t; t += kCapT;
+    T.sJ0 = t; t += kCapT;
+    T.sD = t; t += kCapT;
+    T.sJ = t; t += kCapT;
+    T.sGp = t; t += kCapT;
+    T.sY = t; t += kCapT;
+    T.sG = t; t += kCapTDC;
+    T.sDD = t; t += kCapTDC;
+    T.sDJ = t; t += kCapTDC;
+    int* u = reinterpret_cast<int*>(t);
+    T.sPar = u; u += kCapT;
+    T.sLam = u; u += kCapT;
+    T.sOff = u; u += kCapT + 1;
+    T.sChild = u; u += kCapTDC;
+    T.sLv = u;
+    TopPre pre;
+    top_pre_idx(pa, pre);
+    top_pre_val<true>(pa, nullptr, pre);
+    top_body<true, true>(pa, nullptr, nullptr, da.x, nullptr, nullptr, 0, nullptr, nullptr,
+                         kModeDirect, T, false, pre);
+  }
+  if (threadIdx.x == 0)  // (every other workgroup has arrived: nothing counts after this)
+    __hip_atomic_store(da.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (keep) dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, c0 + (int)threadIdx.x / W < c1, L);
+  stores();
 }
 
 // Factored coefficients from this solve's D (after the start application).
@@ -5055,6 +5141,7 @@ struct nx_network {
   double* d_post = nullptr;
   unsigned* d_dsync = nullptr;
   unsigned dstep_epoch = 0;
+  unsigned* d_tsync = nullptr;  // k_dir_team_up's arrival counter (several ranks; pc_bufs)
   bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
   int last_dir_path = 0;   // the last direct solve: 0 four launches, 1 k_dir_step
   std::vector<int> left_host;  // the rows of d_left
@@ -5998,9 +6085,7 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
 // records what to assemble, and the next call that uses the device -- every NX_API entry
 // point flushes it first -- launches it; the direct solve captures it as the head of its
 // own graph instead (one launch per step less).
-bool defer_ok(const nx_network* h) {
-  return !h->fe && h->nranks == 1 && h->comm == nullptr && h->group == nullptr;
-}
+bool defer_ok(const nx_network* h) { return !h->fe; }
 
 int flush_assembly(nx_network* h) {
   if (!h || !(h->pend_lhs || h->pend_rhs)) return NX_OK;
@@ -6251,6 +6336,38 @@ void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
                         prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0, h->pa, da);
 }
 
+// Several ranks: k_dir_team_up, the assembly + up sweep + top part of one rank (half 0 of
+// launch_direct_team's first pass; pa.accum / fres / coarsedown as the caller set them).
+template <int W, int CPL>
+void launch_dteam_wc(nx_network* h) {
+  DirStep da{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
+             h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
+             h->rhs + h->n_edge_dofs, h->x, nullptr, nullptr, 0, nullptr, h->d_tsync, 0,
+             0.0, 0, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL((k_dir_team_up<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0, h->stream,
+                     h->pa, da);
+}
+void launch_dteam(nx_network* h) {
+  switch (h->pc_variant) {
+    case 0: launch_dteam_wc<16, 1>(h); break;
+    case 1: launch_dteam_wc<16, 2>(h); break;
+    case 2: launch_dteam_wc<16, 4>(h); break;
+    case 3: launch_dteam_wc<64, 2>(h); break;
+    case 5: launch_dteam_wc<8, 2>(h); break;
+    case 8: launch_dteam_wc<64, 8>(h); break;
+    case 9: launch_dteam_wc<64, 16>(h); break;
+    default: launch_dteam_wc<64, 4>(h); break;
+  }
+}
+// k_dir_team_up applies: the LDS sweeps with a top part (every rank's coarse junctions are
+// top slots), the fused residual, the counter, one pending assembly of values and rhs.
+bool dteam_on(const nx_network* h) {
+  const char* e = std::getenv("NXHIP_DIR_FUSED");  // read per solve: tests switch it
+  const bool env = e == nullptr || std::atoi(e) != 0;
+  return env && h->pc_lds && h->fres_ok && h->d_tsync && h->pc_jobs > 0 && h->top_nt > 0 &&
+         h->top_nt <= kTopThreads && h->pa.n_top_lvl <= kMaxTopLvl && !h->fe;
+}
+
 // Launch k_dir_step and wait for its published state (the host's sequence advances).
 int run_dstep(nx_network* h, double rtol, bool prof) {
   switch (h->pc_variant) {
@@ -6404,7 +6521,10 @@ bool cut_mode(const nx_network* h) {
   return env && h->n_cut >= 0 && h->fres_ok && h->d_left_k != nullptr && h->cutbuf != nullptr;
 }
 
-int launch_direct_team(const Team& t, double rtol, int refine) {
+// asmb (first pass): every rank's assembly is pending and heads its first half --
+// k_dir_team_up where it applies (assembly + up sweep + top part in one launch), else the
+// assembly kernel then the sweeps.
+int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false) {
   nx_network* h0 = t.hs[0];
   if (refine) {  // the previous pass's check left r = b - A x in tmp; its ghost slots 0
     for (int r = 0; r < t.P; ++r) {
@@ -6421,7 +6541,12 @@ int launch_direct_team(const Team& t, double rtol, int refine) {
       h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
       h->pa.fres = h->fres_ok ? 1 : 0;  // and the down sweep the local rows' residual
       h->pa.coarsedown = coarse_down(h) ? 1 : 0;  // and the coarse step (no k_pc_coarse)
-      launch_pc<true>(h, bin, bin, h->st, h->st + 1, kModeDirect, half, h->x);
+      if (half == 0 && asmb && !refine && dteam_on(h)) {
+        launch_dteam(h);
+      } else {
+        if (half == 0 && asmb && !refine) CHECK(launch_assembly(h, 1, 1));
+        launch_pc<true>(h, bin, bin, h->st, h->st + 1, kModeDirect, half, h->x);
+      }
       h->pa.accum = 0;
       h->pa.fres = 0;
       h->pa.coarsedown = 0;
@@ -6491,7 +6616,9 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     CHECK(flush_assembly(h));
     if (h->cyc_version != h->lhs_version) CHECK(cyc_build(h));
   }
-  const bool with_asm = !multi && h->pend_lhs && h->pend_rhs;  // deferred assembly heads it
+  // the deferred assembly heads the solve (every rank's, several ranks)
+  bool with_asm = true;
+  for (int r = 0; r < t.P; ++r) with_asm = with_asm && t.hs[r]->pend_lhs && t.hs[r]->pend_rhs;
   h->last_dir_path = 0;
   if (with_asm && dstep_on(h)) {  // the fused step: assembly + solve + check in one launch
     const int rc = run_dstep(h, rtol, prof1);
@@ -6558,7 +6685,7 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   // beside the sweeps -- the cross-queue dependencies cost ~13 us at the fork and ~9 us at
   // the join, more than the 17 us assembly they would hide; r02 trace)
   auto body = [&](int refine, bool asmb) -> int {
-    if (multi) return launch_direct_team(t, rtol, refine);
+    if (multi) return launch_direct_team(t, rtol, refine, asmb);
     if (asmb) CHECK(launch_assembly(h, 1, 1));
     return launch_direct(h, rtol, refine);
   };
@@ -6597,7 +6724,7 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   int* len = with_asm ? &lg.direct_asm_len : &lg.direct_len;
   double* grtol = with_asm ? &lg.direct_asm_rtol : &lg.direct_rtol;
   CHECK(run(exec, graph, len, grtol, 1, 0, with_asm));
-  h->pend_lhs = h->pend_rhs = 0;
+  for (int r = 0; r < t.P; ++r) t.hs[r]->pend_lhs = t.hs[r]->pend_rhs = 0;
   MrState s = *h->h_last;
   if (!s.converged && s.relres == s.relres) {  // one refinement step (graph kept in lchunk;
                                                 // MINRES continuation chunks use len > 0)
@@ -7468,6 +7595,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->d_chain_post = h->d_left_off = nullptr;
   h->d_post = nullptr;
   h->d_dsync = nullptr;
+  h->d_tsync = nullptr;
   h->dstep_epoch = 0;
   h->dstep_off = false;
   h->need_r = false;
@@ -7509,6 +7637,14 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     pa.rhs_b = h->rhs;
     h->n_left = (int)left.size();
     h->fres_ok = pa.slot_rloc && h->d_left && pa.rpart && h->dir_bb && h->tmp;
+    {  // k_dir_team_up's arrival counter (zero; its last workgroup resets it)
+      unsigned* ty = nullptr;
+      if (hipMalloc((void**)&ty, sizeof(unsigned)) == hipSuccess) {
+        h->pc_bufs.push_back(ty);
+        if (hipMemset(ty, 0, sizeof(unsigned)) != hipSuccess) ty = nullptr;
+      }
+      h->d_tsync = ty;
+    }
     if (const char* e = std::getenv("NXHIP_DIR_FRES")) h->fres_ok = h->fres_ok && std::atoi(e) != 0;
     h->left_host = left;
     if (h->n_cut >= 0) {
