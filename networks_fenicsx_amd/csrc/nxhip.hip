@@ -3427,9 +3427,11 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
 // MULTI (k_dir_team_up): every chain's T / It / Ib and every slot's D / J / A / B also go to
 // global memory (the separate down sweep after the coarse all-reduce reads them), as
 // k_pc_up_lds stores them.
+// store_now: the assembly's stores in the pass loop (k_dir_team_up with several chain
+// passes); otherwise they come after the hand-off (dir_stores_all).
 template <int W, int CPL, bool MULTI = false>
 __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da,
-                                             double* lds, DirLane<W, CPL>& L, bool keep,
+                                             double* lds, DirLane<W, CPL>& L, bool store_now,
                                              double& sA_, double& sB_) {
   double* sT = lds;
   double* sIt = sT + kCapC;
@@ -3471,7 +3473,7 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
     const bool active = c < c1;
     const int cu = active ? pa.chain_up[c] : -1, clo = active ? pa.chain_lo[c] : -1;
     dir_chain_asm<W, CPL>(pa, da, c, active, L);
-    if (!keep) dir_chain_store<W, CPL>(pa, da, active, L);
+    if (store_now) dir_chain_store<W, CPL>(pa, da, active, L);
     ChainLane<W, CPL> ch;
     dir_lane_chain<W, CPL>(pa, L, active, ch);
     double vc[CPL];
@@ -3937,6 +3939,31 @@ __device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirSte
   }
 }
 
+// The assembly's stores of one workgroup (after its hand-off): a strided share of the
+// multiplier rows (+-1 values, zero rhs), then its chains' edges -- from the kept lanes
+// (keep: one chain pass) or re-assembled pass by pass.
+template <int W, int CPL>
+__device__ __forceinline__ void dir_stores_all(const PcArgs& pa, const DirStep& da, int job,
+                                               bool keep, DirLane<W, CPL>& L) {
+  const int nj = pa.n_jobs;
+  const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
+  for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
+    if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
+    if (i < da.B) da.rhs_lm[i] = 0.0;
+  }
+  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  if (keep) {
+    dir_chain_store<W, CPL>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
+    return;
+  }
+  constexpr int G = kPcThreads / W;
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + (int)threadIdx.x / W;
+    dir_chain_asm<W, CPL>(pa, da, c, c < c1, L);
+    dir_chain_store<W, CPL>(pa, da, c < c1, L);
+  }
+}
+
 template <int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) {
   __shared__ double smem[kDirLds];
@@ -3953,17 +3980,8 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
   DirLane<W, CPL> L;
   double sA_ = 0.0, sB_ = 0.0;
   const int nt = pa.top_nt, ts0 = pa.top_ts0;
-  dir_up_fused<W, CPL>(pa, da, smem, L, keep, sA_, sB_);
-  // the multiplier rows (+-1 values, zero rhs): a strided share per workgroup; then this
-  // workgroup's edges (keep)
-  auto stores = [&]() {
-    const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
-    for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
-      if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
-      if (i < da.B) da.rhs_lm[i] = 0.0;
-    }
-    if (keep) dir_chain_store<W, CPL>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
-  };
+  dir_up_fused<W, CPL>(pa, da, smem, L, false, sA_, sB_);
+  auto stores = [&]() { dir_stores_all<W, CPL>(pa, da, job, keep, L); };
   double* sTop = smem + kDirLdsMain;
   bool late = false;  // the workgroup that solved the top part (keep): lanes re-assembled
   if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
@@ -3978,7 +3996,8 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
     __syncthreads();
     if (sFlag) {
       // this workgroup re-assembles its lanes after the top part (kept registers would stay
-      // live through the solve, past the register budget) and stores after its phase 2
+      // live through the solve, past the register budget) and stores after its phase 2;
+      // with several chain passes its phase 2 reloads b and dq: stored right after the top
       late = keep;
       double* t = smem;
       TopLds T;
@@ -4009,8 +4028,13 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
       NX_DSTAMP(5);
       if (threadIdx.x == 0)
         __hip_atomic_store(da.sync + 2, da.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!keep) {
+        stores();
+        vm_drain();  // (its phase 2 reads them back)
+      }
     } else {
       stores();
+      if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
         int ok = 0;
@@ -4033,7 +4057,9 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
     __syncthreads();
   } else {
     stores();
+    vm_drain();
   }
+  __syncthreads();  // (several passes: phase 2 reads the stored b and dq back)
   const bool lane_on = c0 + (int)threadIdx.x / W < c1;
   if (late) dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, lane_on, L);
   dir_down_fused<W, CPL>(pa, da, smem, sTop, L, keep, sA_, sB_);
@@ -4077,7 +4103,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
   const bool keep = c1 - c0 <= kPcThreads / W;
   DirLane<W, CPL> L;
   double sA_ = 0.0, sB_ = 0.0;
-  dir_up_fused<W, CPL, true>(pa, da, smem, L, keep, sA_, sB_);
+  dir_up_fused<W, CPL, true>(pa, da, smem, L, !keep, sA_, sB_);
   auto stores = [&]() {
     const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
     for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
@@ -6354,6 +6380,7 @@ void launch_dteam(nx_network* h) {
     case 2: launch_dteam_wc<16, 4>(h); break;
     case 3: launch_dteam_wc<64, 2>(h); break;
     case 5: launch_dteam_wc<8, 2>(h); break;
+    case 7: launch_dteam_wc<8, 4>(h); break;
     case 8: launch_dteam_wc<64, 8>(h); break;
     case 9: launch_dteam_wc<64, 16>(h); break;
     default: launch_dteam_wc<64, 4>(h); break;
@@ -6376,6 +6403,7 @@ int run_dstep(nx_network* h, double rtol, bool prof) {
     case 2: launch_dstep_wc<16, 4>(h, rtol, prof); break;
     case 3: launch_dstep_wc<64, 2>(h, rtol, prof); break;
     case 5: launch_dstep_wc<8, 2>(h, rtol, prof); break;
+    case 7: launch_dstep_wc<8, 4>(h, rtol, prof); break;
     case 8: launch_dstep_wc<64, 8>(h, rtol, prof); break;
     case 9: launch_dstep_wc<64, 16>(h, rtol, prof); break;
     default: launch_dstep_wc<64, 4>(h, rtol, prof); break;
@@ -7438,6 +7466,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   const int N = h->N;
   int variant;
   if (N <= 16) variant = 5;  // 8 lanes x 2 cells: one chain round per job (swept: 16x1 +8%)
+  // (N <= 32 by 8 lanes x 4 cells, 128 chains per pass: slower, 8-rank C4 rehearsal r03o --
+  // team up 50 -> 57 us, down 41 -> 66 us per rank; the lanes' serial work dominates)
   else if (N <= 32) variant = 1;
   else if (N <= 64) variant = 2;
   else if (N <= 128) variant = 3;
