@@ -1100,6 +1100,10 @@ struct PcArgs {
   // child 2 | child 3 << 16] with child = local slot | dc offset << 6
   const int* job_wave;
   const int* slot_wave;
+  // the top part's register level sweeps, host-built (top_body): per top slot its level and
+  // junction-children count (lv | nk << 8), then kWaveKids entries child | (dc offset << 12);
+  // null when a slot has more children or the top part exceeds one workgroup
+  const int* top_wave;
   int topdown;    // one rank, direct: the top part solved in every down sweep workgroup
   int coarsedown;  // several ranks, direct: the coarse step (k_pc_coarse) in every one
   // small coarse forests (<= 64 junctions, <= kWaveKids children): per junction
@@ -2159,6 +2163,7 @@ struct TopLds {
 struct TopPre {
   int c, lo, lam, pcn, par, off;
   double T, It, Dl, Jl, y, Tp, Ib;
+  int w[1 + kWaveKids];  // pa.top_wave of slot tid (loaded with the indices)
 };
 
 __device__ __forceinline__ void top_pre_idx(const PcArgs& pa, TopPre& p) {
@@ -2170,6 +2175,9 @@ __device__ __forceinline__ void top_pre_idx(const PcArgs& pa, TopPre& p) {
   p.pcn = tid < nt ? pa.slot_pchain[ts0 + tid] : -1;
   p.par = tid < nt ? pa.slot_parent[ts0 + tid] : -1;
   p.off = tid < nt ? pa.slot_dc_off[ts0 + tid] : 0;
+#pragma unroll
+  for (int k = 0; k <= kWaveKids; ++k)
+    p.w[k] = (pa.top_wave && tid < nt) ? pa.top_wave[(1 + kWaveKids) * (int64_t)tid + k] : 0;
 }
 
 // WT: the inputs were handed over inside the launch (k_dir_step): write-through loads; y
@@ -2309,7 +2317,17 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     rch[k] = 0;
     rg[k] = 0.0;
   }
-  if (rmine) {
+  const bool hw = pa.top_wave != nullptr;  // (uniform) the host's set-up, loaded up front
+  if (rmine && hw) {
+    rlv = pre_.w[0] & 0xff;
+    rnk = (pre_.w[0] >> 8) & 0xff;
+#pragma unroll
+    for (int k = 0; k < kWaveKids; ++k)
+      if (k < rnk) {
+        rch[k] = pre_.w[1 + k] & 0xfff;
+        rg[k] = sG[pre_.w[1 + k] >> 12];
+      }
+  } else if (rmine) {
     for (int q = 0; q < nl; ++q)
       if (ts0 + rsl >= sLv[q] && ts0 + rsl < sLv[q + 1]) rlv = q;
     for (int i = sOff[rsl]; i < sOff[rsl + 1]; ++i) {
@@ -2324,7 +2342,8 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
       ++rnk;
     }
   }
-  const bool reg = pa.top_reg && nt <= kTopThreads && __syncthreads_or(rnk > kWaveKids) == 0;
+  const bool reg = hw || (pa.top_reg && nt <= kTopThreads &&
+                          __syncthreads_or(rnk > kWaveKids) == 0);
   double rD = rmine ? sD0[rsl] : 1.0, rJ = rmine ? sJ0[rsl] : 0.0, riv = 1.0;
   if (reg) {
     for (int lv = nl - 1; lv >= 0; --lv) {
@@ -7768,6 +7787,30 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
       pa.job_wave = up(jw.data(), n_jobs);
       pa.slot_wave = up(sw.data(), (int64_t)sw.size());
     }
+  }
+  // the top part's register set-up (top_body): every slot's level, junction children (top
+  // position) and their hanging-chain entries, when all have <= kWaveKids and fit
+  pa.top_wave = nullptr;
+  if (n_top_lvl > 0 && h->top_nt > 0 && h->top_nt <= kTopThreads) {
+    const int ts0 = top_lvl_off[0], nt = h->top_nt, dc0 = slot_dc_off[ts0];
+    std::vector<int> tw((size_t)(1 + kWaveKids) * nt, 0);
+    bool ok = slot_dc_off[ts0 + nt] - dc0 < (1 << 19);
+    for (int q = 0; q < n_top_lvl && ok; ++q)
+      for (int j = top_lvl_off[q]; j < top_lvl_off[q + 1] && ok; ++j) {
+        int nk = 0;
+        int* w = tw.data() + (size_t)(1 + kWaveKids) * (j - ts0);
+        for (int i = slot_dc_off[j]; i < slot_dc_off[j + 1]; ++i) {
+          const int lo = dc_lo[i];
+          if (!(lo >= ts0 && lo < ts0 + nt)) continue;  // a junction child in the top part
+          if (nk >= kWaveKids || q > 0xff) {
+            ok = false;
+            break;
+          }
+          w[1 + nk++] = (lo - ts0) | ((i - dc0) << 12);
+        }
+        w[0] = q | (nk << 8);
+      }
+    if (ok) pa.top_wave = up(tw.data(), (int64_t)tw.size());
   }
   h->pc_lds = lds;
   h->pa = pa;
