@@ -3917,7 +3917,10 @@ __device__ __forceinline__ void publish_wt(const MrState& s, int q, int* seq, Mr
 }
 
 // The last workgroup of phase 2: the partials and the left rows' shares, fixed order.
-__device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirStep& da) {
+// lo0 / lo1: left row threadIdx.x's post range (loaded by every workgroup before its
+// arrival: static), so only the write-through loads remain after the hand-off.
+__device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirStep& da, int lo0,
+                                                  int lo1) {
 #pragma clang fp contract(off)
   __shared__ double s_r[kPcThreads / 64], s_b[kPcThreads / 64];
   const int nj = pa.n_jobs;
@@ -3928,7 +3931,9 @@ __device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirSte
   }
   for (int i = threadIdx.x; i < da.n_left; i += kPcThreads) {
     double acc = 0.0;
-    for (int k = da.left_off[i]; k < da.left_off[i + 1]; ++k) acc += ld_wt(da.post + k);
+    const bool pre = i == (int)threadIdx.x;
+    const int k0 = pre ? lo0 : da.left_off[i], k1 = pre ? lo1 : da.left_off[i + 1];
+    for (int k = k0; k < k1; ++k) acc += ld_wt(da.post + k);
     const double rv = 0.0 - acc;  // b = 0 on the multiplier rows
     rr += rv * rv;
   }
@@ -4081,6 +4086,11 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
   __syncthreads();  // (several passes: phase 2 reads the stored b and dq back)
   const bool lane_on = c0 + (int)threadIdx.x / W < c1;
   if (late) dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, lane_on, L);
+  int lo0 = 0, lo1 = 0;  // this thread's left row's post range (dir_publish_fused)
+  if ((int)threadIdx.x < da.n_left) {
+    lo0 = da.left_off[threadIdx.x];
+    lo1 = da.left_off[threadIdx.x + 1];
+  }
   dir_down_fused<W, CPL>(pa, da, smem, sTop, L, keep, sA_, sB_);
   // hand-off 2: the residual partials and shares -> the last workgroup publishes
   vm_drain();
@@ -4093,7 +4103,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
   }
   __syncthreads();
   if (sFlag) {
-    dir_publish_fused(pa, da);
+    dir_publish_fused(pa, da, lo0, lo1);
     NX_DSTAMP(4);
   }
   if (late) {  // (the kernel's end, not the published state, waits for these)
@@ -4118,21 +4128,18 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
   __shared__ int sFlag;
   const int job = blockIdx.x;
   const int nj = pa.n_jobs;
+  NX_DSTAMP(0);
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   const bool keep = c1 - c0 <= kPcThreads / W;
   DirLane<W, CPL> L;
   double sA_ = 0.0, sB_ = 0.0;
-  dir_up_fused<W, CPL, true>(pa, da, smem, L, !keep, sA_, sB_);
-  auto stores = [&]() {
-    const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
-    for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
-      if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
-      if (i < da.B) da.rhs_lm[i] = 0.0;
-    }
-    if (keep) dir_chain_store<W, CPL>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
-  };
+  // (the assembly's stores after the hand-off, re-assembled pass by pass with several
+  // passes: the last arrival -- the top part's start -- comes sooner)
+  dir_up_fused<W, CPL, true>(pa, da, smem, L, false, sA_, sB_);
+  auto stores = [&]() { dir_stores_all<W, CPL>(pa, da, job, keep, L); };
   vm_drain();
   __syncthreads();
+  NX_DSTAMP(1);
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(da.sync, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
@@ -4141,6 +4148,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
   __syncthreads();
   if (!sFlag) {
     stores();
+    NX_DSTAMP(8);
     return;
   }
   if (pa.top_nt > 0) {
@@ -4164,9 +4172,11 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
     TopPre pre;
     top_pre_idx(pa, pre);
     top_pre_val<true>(pa, nullptr, pre);
+    NX_DSTAMP(6);
     top_body<true, true>(pa, nullptr, nullptr, da.x, nullptr, nullptr, 0, nullptr, nullptr,
                          kModeDirect, T, false, pre);
   }
+  NX_DSTAMP(7);
   if (threadIdx.x == 0)  // (every other workgroup has arrived: nothing counts after this)
     __hip_atomic_store(da.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (keep) dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, c0 + (int)threadIdx.x / W < c1, L);
