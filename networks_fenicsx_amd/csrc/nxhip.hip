@@ -3373,7 +3373,11 @@ __device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& d
 // CSR segment (entry i by lane i mod W, unit stride; the tensors of the entry's cells fetched
 // by shuffles; uniform trip count across the wave -- the longest segment, 7N + 3 -- so every
 // shuffle has all lanes).
-template <int W, int CPL>
+// UNIT: the CSR segment in k_assemble's order instead (entry i by lane i mod W, unit stride
+// over the lanes: whole cache lines per store; the tensors of the entry's cells fetched by
+// shuffles, ~2x the issue time) -- the workgroups that store while waiting for the top part,
+// where the issue time is hidden and partially written lines would cost HBM traffic.
+template <int W, int CPL, bool UNIT = false>
 __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep& da, bool active,
                                                 const DirLane<W, CPL>& L) {
   ChainLane<W, CPL> ch;
@@ -3398,6 +3402,37 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
   // and q_{g+1}'s 5 -- q_N's 3 + s_dst for g = N - 1 -- from q0len + 7 g on; cell 0 also the
   // q_0 row): values as decode_entry lists them, the next edge cell's masses from the
   // neighbouring lane (chain cell k + 1, or k - 1 on a flipped chain)
+  if constexpr (UNIT) {
+    const int smax = 7 * N + 3;
+    for (int ib = 0; ib < smax; ib += W) {
+      const int i = ib + l;
+      const bool in = active && i < L.seglen;
+      const Entry en = decode_entry(in ? i : 0, N, L.s);
+      const int ca = en.cell, cb = min(en.cell + 1, N - 1);
+      const int ka = flip ? N - 1 - ca : ca, kb = flip ? N - 1 - cb : cb;
+      double mdA = 0.0, moA = 0.0, mdB = 0.0;
+#pragma unroll
+      for (int t = 0; t < CPL; ++t) {
+        const double a = __shfl(L.md[t], ka / CPL, W), b = __shfl(L.mo[t], ka / CPL, W);
+        const double m2 = __shfl(L.md[t], kb / CPL, W);
+        if (ka % CPL == t) {
+          mdA = a;
+          moA = b;
+        }
+        if (kb % CPL == t) mdB = m2;
+      }
+      double v;
+      switch (en.vk) {
+        case V_P1: v = 1.0; break;
+        case V_M1: v = -1.0; break;
+        case V_MD: v = mdA; break;
+        case V_MO: v = moA; break;
+        default: v = mdA + mdB; break;  // interior diagonal: cells g and g+1
+      }
+      if (in) da.val[L.sg0 + i] = v;
+    }
+    return;
+  }
   const int s0 = L.s, q0len = 3 + s0;
   const int sdst = L.seglen - (7 * N + 1 + s0);
   const double mdD = __shfl_down(L.md[0], 1, W), moD = __shfl_down(L.mo[0], 1, W);
@@ -3966,7 +4001,7 @@ __device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirSte
 // The assembly's stores of one workgroup (after its hand-off): a strided share of the
 // multiplier rows (+-1 values, zero rhs), then its chains' edges -- from the kept lanes
 // (keep: one chain pass) or re-assembled pass by pass.
-template <int W, int CPL>
+template <int W, int CPL, bool UNIT = false>
 __device__ __forceinline__ void dir_stores_all(const PcArgs& pa, const DirStep& da, int job,
                                                bool keep, DirLane<W, CPL>& L) {
   const int nj = pa.n_jobs;
@@ -3977,14 +4012,14 @@ __device__ __forceinline__ void dir_stores_all(const PcArgs& pa, const DirStep& 
   }
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   if (keep) {
-    dir_chain_store<W, CPL>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
+    dir_chain_store<W, CPL, UNIT>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
     return;
   }
   constexpr int G = kPcThreads / W;
   for (int cb = c0; cb < c1; cb += G) {
     const int c = cb + (int)threadIdx.x / W;
     dir_chain_asm<W, CPL>(pa, da, c, c < c1, L);
-    dir_chain_store<W, CPL>(pa, da, c < c1, L);
+    dir_chain_store<W, CPL, UNIT>(pa, da, c < c1, L);
   }
 }
 
@@ -4057,7 +4092,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
         vm_drain();  // (its phase 2 reads them back)
       }
     } else {
-      stores();
+      dir_stores_all<W, CPL, true>(pa, da, job, keep, L);  // (hidden in the wait: unit stride)
       if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
@@ -4147,7 +4182,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
   }
   __syncthreads();
   if (!sFlag) {
-    stores();
+    dir_stores_all<W, CPL, true>(pa, da, job, keep, L);  // (unit stride: see dir_chain_store)
     NX_DSTAMP(8);
     return;
   }
