@@ -249,6 +249,33 @@ int nx_get_solver(nx_network_t* h, int32_t* requested, int32_t* last_run);
 int nx_set_cycles(nx_network_t* h, int32_t n, const int32_t* rows);
 
 /*
+ * General flux degree k >= 2 with DG0 pressure (assembly.py:121-146, flux_degree=k), one
+ * rank: the direct solve through the condensed system. The DG0 divergence touches a cell's
+ * two vertex fluxes only, so the k-1 interior fluxes per cell are condensed out per cell;
+ * what remains has the P1/DG0 structure with the cell mass R h [[a, b], [b, a]]
+ * (element.condensed_flux_mass: k = 2: a = 1/8, b = -1/24). An auxiliary P1/DG0 handle of
+ * the same graph (nx_create + its tree preconditioner, nx_set_solver 1) inverts it.
+ *
+ * nx_set_cell_mass(aux, ratio, mo_div): the auxiliary handle's flux mass is the condensed
+ *   one, ratio = a / b (T = tridiag(1, 2 ratio, 1), ratio at both ends; P1: 2) and mo_div =
+ *   (a + b) / b (P1: 3). The handle is internal from then on: its own CSR is no longer the
+ *   system its sweeps invert (it checks no residual; nx_solve on it runs MINRES).
+ * nx_fe_set_direct(h, aux, k, n_lm, ...): attaches aux to the (k, 0) handle h (nx_create_fe):
+ *   slot[e] = aux edge of h's edge e; v_fe / v_aux (E (N+1)) the vertex-flux rows, edge-major;
+ *   i_fe (E N (k-1)) the interior-flux rows, cell-major; p_fe / p_aux (E N) pressure rows;
+ *   l_fe / l_aux (n_lm) multiplier rows; cst = C (2 x (k-1)) | K ((k-1) x 2) | M_ii^{-1}
+ *   ((k-1)^2), row-major; ab = a + b. aux = NULL detaches. With nx_set_solver(h, 1, 1),
+ *   nx_solve condenses, solves on aux, expands, checks h's true residual and refines up to
+ *   twice (iters = passes), MINRES when that still misses rtol. layout_fe.build_fe_aux_maps
+ *   builds the maps. Replaces MUMPS' LU of the (k, 0) system (solver.py:58-65).
+ */
+int nx_set_cell_mass(nx_network_t* aux, double ratio, double mo_div);
+int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64_t n_lm,
+                     const int32_t* slot, const int32_t* v_fe, const int32_t* v_aux,
+                     const int32_t* i_fe, const int32_t* p_fe, const int32_t* p_aux,
+                     const int32_t* l_fe, const int32_t* l_aux, const double* cst, double ab);
+
+/*
  * Process-wide solve mode. 1 (default): with the preconditioner a solve is ONE HIP graph
  * launch -- start application, per-solve coefficients and the first iterations (also with
  * several ranks, RCCL or group, when beta^2 travels point-to-point) -- whose last k_mr_a

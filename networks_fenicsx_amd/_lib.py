@@ -87,6 +87,9 @@ _SIGS = {
     "nx_get_pc_exact": (C.c_int, [_h, _pi32]),
     "nx_set_solver": (C.c_int, [_h, _i32, _i32]),
     "nx_set_cycles": (C.c_int, [_h, _i32, _pi32]),
+    "nx_set_cell_mass": (C.c_int, [_h, _f64, _f64]),
+    "nx_fe_set_direct": (C.c_int, [_h, _h, _i32, _i64, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
+                                   _pi32, _pi32, _pd, _f64]),
     "nx_get_solver": (C.c_int, [_h, _pi32, _pi32]),
     "nx_set_lean": (C.c_int, [_i32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
@@ -456,6 +459,29 @@ class Handle:
         e = C.c_int32(0)
         check(lib().nx_get_pc_exact(self.ptr, C.byref(e)))
         return bool(e.value)
+
+    def set_cell_mass(self, ratio: float, mo_div: float) -> None:
+        """``nx_set_cell_mass``: this (auxiliary) handle's sweeps invert the condensed flux
+        mass ``R h [[a, b], [b, a]]`` (ratio = a / b, mo_div = (a + b) / b)."""
+        check(lib().nx_set_cell_mass(self.ptr, float(ratio), float(mo_div)))
+
+    def fe_set_direct(self, aux: "Handle | None", k: int, slot, maps, cst, ab: float) -> None:
+        """``nx_fe_set_direct``: attach the auxiliary P1/DG0 handle that solves this (k, 0)
+        handle's condensed system (``maps``: :class:`layout_fe.FeAuxMaps`)."""
+        if aux is None:
+            z = _ptr(np.zeros(1, np.int32), C.c_int32)
+            check(lib().nx_fe_set_direct(self.ptr, None, 0, 0, *([z] * 8), None, 0.0))
+            self._fe_aux = None
+            return
+        i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+        arrs = [i32(slot), i32(maps.v_fe), i32(maps.v_aux), i32(maps.i_fe), i32(maps.p_fe),
+                i32(maps.p_aux), i32(maps.l_fe) if maps.l_fe.size else np.zeros(1, np.int32),
+                i32(maps.l_aux) if maps.l_aux.size else np.zeros(1, np.int32)]
+        cst = np.ascontiguousarray(cst, dtype=np.float64)
+        check(lib().nx_fe_set_direct(self.ptr, aux.ptr, int(k), int(maps.l_fe.size),
+                                     *[_ptr(a, C.c_int32) for a in arrs],
+                                     _ptr(cst, C.c_double), float(ab)))
+        self._fe_aux = aux  # the auxiliary handle lives as long as this one uses it
 
     def set_solver(self, direct: bool, tree_exact: bool) -> None:
         """``nx_set_solver``: the direct tree solve (where exact) or MINRES."""

@@ -34,9 +34,9 @@ import numpy as np
 from . import _lib
 from .comm import MIN, GroupRankComm
 from .fem import Constant, Function, FunctionSpace
-from .element import stable_pair
+from .element import condensed_flux_mass, stable_pair
 from .layout import LocalProblem, build_local_problem
-from .layout_fe import FeLayout, build_fe_layout
+from .layout_fe import FeLayout, build_fe_aux_maps, build_fe_layout
 from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
@@ -329,6 +329,44 @@ class HydraulicNetworkAssembler:
         self._p_idx = fe.p_rows
         self._lm_idx = fe.lm_rows
         self._set_output_map()
+        self._fe_aux = None
+        if m == 0 and mesh.N <= 1024:
+            self._init_fe_direct(src, dst)
+
+    def _init_fe_direct(self, src, dst) -> None:
+        """(k, 0): the direct solve through the condensed P1/DG0 system (``nx_fe_set_direct``).
+        An auxiliary P1/DG0 handle of the same graph carries the tree decomposition; its flux
+        mass becomes the condensed ``R h [[a, b], [b, a]]`` (``element.condensed_flux_mass``),
+        whose ratios are integers: ``a / b = (-1)^(k+1) (k+1)``. Forests only (a graph with
+        cycles runs MINRES: the Woodbury correction is built from the P1 CSR)."""
+        mesh, fe = self._network_mesh, self._fe
+        k = self._degrees[0]
+        lp = build_local_problem(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, 0, 1)
+        pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=256)
+        if not pc.tree_exact:
+            return
+        aux = _lib.Handle(_device_for_rank(), mesh.N, lp.edge_x, lp.edge_lm, lp.lm_rowptr,
+                          lp.lm_col, lp.lm_val, lp.n_ghost)
+        aux.set_preconditioner(pc)
+        if not aux.pc_lds():
+            return
+        alpha, beta, C, K, Mii = condensed_flux_mass(k)
+        ratio = round(alpha / beta)
+        assert abs(alpha / beta - ratio) < 1e-12, (alpha, beta)
+        aux.set_cell_mass(float(ratio), float(ratio + 1))
+        slot = np.full(mesh.num_edges, -1, dtype=np.int64)
+        slot[np.asarray(lp.edges)] = np.arange(np.asarray(lp.edges).size)
+        maps = build_fe_aux_maps(fe, lp)
+        cst = np.concatenate([C.ravel(), K.ravel(), Mii.ravel()])
+        self._handle.fe_set_direct(aux, k, slot, maps, cst, alpha + beta)
+        self._fe_aux = aux
+        self._fe_aux_pc = pc
+
+    @property
+    def fe_direct_available(self) -> bool:
+        """A general-degree (k, 0) assembler whose direct solve runs through the condensed
+        P1/DG0 system (forest graphs)."""
+        return getattr(self, "_fe_aux", None) is not None
 
     def _init_comm(self) -> None:
         comm = self._network_mesh.comm
@@ -407,7 +445,8 @@ class HydraulicNetworkAssembler:
         ``tree_exact``) or, on one rank, up to 128 cycle-closing chains corrected by a
         Woodbury step (``nx_set_cycles``); with several ranks the LDS sweeps with the coarse
         step on every rank (the ranks decide together) -- and MINRES otherwise."""
-        want = (bool(enable), bool(self._pc is not None and self._pc.tree_exact))
+        exact = (self._pc is not None and self._pc.tree_exact) or self.fe_direct_available
+        want = (bool(enable), bool(exact))
         if getattr(self, "_direct_state", None) != want:
             self._handle.set_solver(*want)
             self._direct_state = want

@@ -1104,6 +1104,10 @@ struct PcArgs {
   // junction-children count (lv | nk << 8), then kWaveKids entries child | (dc offset << 12);
   // null when a slot has more children or the top part exceeds one workgroup
   const int* top_wave;
+  // the flux mass of one cell is R h [[a, b], [b, a]] (P1: a = 1/3, b = 1/6; a (k, 0) system
+  // condensed to its vertex fluxes: element.condensed_flux_mass): mo = b R h of a chain is
+  // its end flux's lumped mass (a + b) R h / mo_div, mo_div = (a + b) / b (P1: 3)
+  double mo_div;
   int topdown;    // one rank, direct: the top part solved in every down sweep workgroup
   int coarsedown;  // several ranks, direct: the coarse step (k_pc_coarse) in every one
   // small coarse forests (<= 64 junctions, <= kWaveKids children): per junction
@@ -1227,7 +1231,7 @@ struct ChainLane {
     const int flip = active ? pa.chain_flip[c] : 0;
     const int base = e * (2 * N + 1);
     const double* dqe = pa.dq + (int64_t)e * (N + 1);
-    mo = active ? dqe[0] / 3.0 : 1.0;
+    mo = active ? dqe[0] / pa.mo_div : 1.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
       const int k = l * CPL + t;
@@ -5278,6 +5282,18 @@ struct nx_network {
   int* fe_bptr = nullptr;
   int* fe_bidx = nullptr;
   int* fe_bent = nullptr;
+  // (k, 0) solved through the condensed P1/DG0 system (nx_fe_set_direct): its handle (not
+  // owned), the row maps, the cell constants C | K | Mii and a + b
+  nx_network* fe_aux = nullptr;
+  int fe_k = 0, fe_nl = 0;
+  int *fe_slot = nullptr, *fe_vfe = nullptr, *fe_vaux = nullptr, *fe_ife = nullptr;
+  int *fe_pfe = nullptr, *fe_paux = nullptr, *fe_lfe = nullptr, *fe_laux = nullptr;
+  double* fe_cst = nullptr;
+  double fe_ab = 0.0;
+  hipEvent_t fe_ev[2] = {nullptr, nullptr};  // condensed rhs ready / auxiliary solve done
+  // an auxiliary handle: its cell mass is a condensed one (nx_set_cell_mass), so its own CSR
+  // is not the system the sweeps invert -- no residual check of its own
+  bool cond_mass = false;
 };
 
 struct nx_group {
@@ -5731,14 +5747,16 @@ int set_device(nx_network* h) {
 // N+1 with 2 at both ends (assembly.py:253 on equal cells): T = L U with unit lower
 // multipliers l_k = 1 / u_{k-1} (l_0 = 0) and pivots u_0 = 2, u_k = d_k - l_k.
 // Returns [l_0..l_N | 1/u_0..1/u_N].
-std::vector<double> mass_lu(int N) {
+// ratio = a / b of the cell mass (P1: 2): T = M / (b R h) = tridiag(1, 2 ratio, 1) with ratio
+// at both ends
+std::vector<double> mass_lu(int N, double ratio = 2.0) {
   const int n = N + 1;
   std::vector<double> lu(2 * (size_t)n, 0.0);
-  double u = 2.0;
+  double u = ratio;
   lu[n] = 1.0 / u;
   for (int k = 1; k < n; ++k) {
     const double l = 1.0 / u;
-    u = (k == N ? 2.0 : 4.0) - l;
+    u = (k == N ? ratio : 2.0 * ratio) - l;
     lu[k] = l;
     lu[n + k] = 1.0 / u;
   }
@@ -5967,6 +5985,94 @@ __global__ __launch_bounds__(kBlock) void k_assemble_fe(FeArgs a) {
   }
 }
 
+// ---- (k, 0) through the condensed P1/DG0 system (nx_fe_set_direct). The divergence against
+// DG0 touches a cell's two vertex fluxes only, so the interior fluxes sit in the flux rows
+// alone: condensed per cell, the system is P1/DG0's with the cell mass R h [[a, b], [b, a]],
+// which the direct tree solve of an auxiliary P1 handle inverts (nx_set_cell_mass).
+struct FeCond {
+  const double* edge_x;
+  const double* edge_R;
+  int N, km;  // km = k - 1 interior fluxes per cell
+  int64_t E;
+  const int *slot, *vfe, *vaux, *ife, *pfe, *paux, *lfe, *laux;
+  int nl;
+  const double* cst;  // C (2 km) | K (km 2) | Mii (km km)
+  double ab;          // a + b
+};
+
+// The condensed right-hand side b_v - C b_i (vertex rows; pressure and multiplier rows
+// copied) into the auxiliary handle's rhs, and (dq_aux) its lumped mass (a + b) R h per cell
+// end. One thread per vertex flux, pressure cell, multiplier.
+__global__ __launch_bounds__(kBlock) void k_fe_condense(FeCond c, const double* __restrict__ b,
+                                                        double* __restrict__ dq_aux,
+                                                        double* __restrict__ rhs_aux) {
+#pragma clang fp contract(off)
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int N = c.N, km = c.km;
+  const int64_t nv = c.E * (N + 1), np = c.E * N;
+  if (t < nv) {
+    const int64_t e = t / (N + 1);
+    const int g = (int)(t - e * (N + 1));
+    const double R = c.edge_R[e];
+    double bv = b[c.vfe[t]], d = 0.0;
+    if (g > 0) {  // the cell on the left: this vertex is its right one (C row 1)
+      const int64_t cell = e * N + g - 1;
+      d = c.ab * (R * fe_cell_h(c.edge_x, cell, N));
+      for (int i = 0; i < km; ++i) bv -= c.cst[km + i] * b[c.ife[cell * km + i]];
+    }
+    if (g < N) {  // the cell on the right: its left vertex (C row 0)
+      const int64_t cell = e * N + g;
+      d += c.ab * (R * fe_cell_h(c.edge_x, cell, N));
+      for (int i = 0; i < km; ++i) bv -= c.cst[i] * b[c.ife[cell * km + i]];
+    }
+    rhs_aux[c.vaux[t]] = bv;
+    if (dq_aux) dq_aux[(int64_t)c.slot[e] * (N + 1) + g] = d;
+  } else if (t < nv + np) {
+    rhs_aux[c.paux[t - nv]] = b[c.pfe[t - nv]];
+  } else if (t < nv + np + c.nl) {
+    rhs_aux[c.laux[t - nv - np]] = b[c.lfe[t - nv - np]];
+  }
+}
+
+// The (k, 0) solution from the auxiliary one: vertex fluxes, pressure cells, multipliers
+// copied, interior fluxes x_i = Mii b_i / (R h) - K x_v (accum: added, a refinement pass).
+__global__ __launch_bounds__(kBlock) void k_fe_expand(FeCond c, const double* __restrict__ xa,
+                                                      const double* __restrict__ b,
+                                                      double* __restrict__ x, int accum) {
+#pragma clang fp contract(off)
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int N = c.N, km = c.km;
+  const int64_t nv = c.E * (N + 1), np = c.E * N, n0 = nv + np + c.nl;
+  int64_t dst = -1;
+  double v = 0.0;
+  if (t < nv) {
+    dst = c.vfe[t];
+    v = xa[c.vaux[t]];
+  } else if (t < nv + np) {
+    dst = c.pfe[t - nv];
+    v = xa[c.paux[t - nv]];
+  } else if (t < n0) {
+    dst = c.lfe[t - nv - np];
+    v = xa[c.laux[t - nv - np]];
+  } else if (t < n0 + np) {
+    const int64_t cell = t - n0, e = cell / N;
+    const int g = (int)(cell - e * N);
+    const double Rh = c.edge_R[e] * fe_cell_h(c.edge_x, cell, N);
+    const double xl = xa[c.vaux[e * (N + 1) + g]], xr = xa[c.vaux[e * (N + 1) + g + 1]];
+    const double* K = c.cst + 2 * km;
+    const double* Mii = c.cst + 4 * km;
+    for (int j = 0; j < km; ++j) {
+      double s = 0.0;
+      for (int i = 0; i < km; ++i) s += Mii[j * km + i] * b[c.ife[cell * km + i]];
+      const double xi = s / Rh - K[2 * j] * xl - K[2 * j + 1] * xr;
+      const int64_t r = c.ife[cell * km + j];
+      x[r] = accum ? x[r] + xi : xi;
+    }
+    return;
+  }
+  if (dst >= 0) x[dst] = accum ? x[dst] + v : v;
+}
+
 // terms [ptr[i], ptr[i+1]) of every output i must reference the table and the cell / edge
 // arrays in range
 int check_terms(const char* what, int64_t n_out, const int32_t* ptr, const int32_t* idx,
@@ -6058,7 +6164,9 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->fe_kind, h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent,
                   h->fe_bptr, h->fe_bidx, h->fe_bent, h->out_idx,
                   h->d_left_k, h->d_cut_own, h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf,
-                  h->d_cyc_rows, h->cyc_z, h->cyc_cinv, h->cyc_cap, h->cyc_prev, h->cyc_w};
+                  h->d_cyc_rows, h->cyc_z, h->cyc_cinv, h->cyc_cap, h->cyc_prev, h->cyc_w,
+                  h->fe_slot, h->fe_vfe, h->fe_vaux, h->fe_ife, h->fe_pfe, h->fe_paux, h->fe_lfe,
+                  h->fe_laux, h->fe_cst};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -6074,6 +6182,8 @@ NX_API int nx_destroy(nx_network_t* h) {
   for (double* p : h->snap)
     if (p) (void)hipFree(p);
   for (auto& e : h->snap_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : h->fe_ev)
     if (e) (void)hipEventDestroy(e);
   if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -6390,6 +6500,7 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
       return;
     }
   }
+  if (h->cond_mass) return;  // an auxiliary solve: the (k, 0) handle checks its own residual
   if (cyc) {  // x -= Z Cinv U^T (x - x_before): the couplings the tree solve dropped
     hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
                        h->cyc_cinv, refine ? h->cyc_prev : nullptr, h->cyc_w, nullptr);
@@ -6574,6 +6685,7 @@ bool direct_local(const nx_network* h) {
   // the LDS sweeps run it (their mode 3); the global-memory fallback (LDS caps exceeded)
   // leaves the solve to MINRES
   if (!(h->solver == 1 && h->pc && h->pc_lds && h->pa.exact && exact && h->E > 0)) return false;
+  if (h->cond_mass) return false;  // an auxiliary handle (nx_set_cell_mass): not its own CSR
   // several ranks: the coarse step, and the residual formed by the down sweeps
   return !multi || (h->pc_jobs > 0 && h->pa.n_coarse > 0 && h->pa.n_coarse <= kCapCoarse &&
                     h->fres_ok);
@@ -6990,6 +7102,50 @@ int check_schedules(const Team& t) {
   return NX_OK;
 }
 
+// (k, 0) on one rank through the condensed P1/DG0 system (nx_fe_set_direct): condense the
+// right-hand side (and, first pass, the auxiliary lumped mass) on this handle's stream, the
+// auxiliary handle's tree solve on its stream, expand, then this CSR's true residual,
+// published. Up to two refinement passes (x += the same solve of r). *converged = 0 when
+// still above rtol: the caller runs MINRES.
+int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
+                    int32_t* converged) {
+  nx_network* a = h->fe_aux;
+  CHECK(flush_assembly(h));
+  CHECK(flush_assembly(a));
+  const FeCond c{h->edge_x, h->edge_R, h->N, h->fe_k - 1, h->E, h->fe_slot, h->fe_vfe,
+                 h->fe_vaux, h->fe_ife, h->fe_pfe, h->fe_paux, h->fe_lfe, h->fe_laux, h->fe_nl,
+                 h->fe_cst, h->fe_ab};
+  const int64_t nv = h->E * (h->N + 1), np = h->E * (int64_t)h->N, n0 = nv + np + h->fe_nl;
+  const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
+  MrState s{};
+  int pass = 0;
+  for (; pass < 3; ++pass) {
+    const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
+    hipLaunchKernelGGL(k_fe_condense, dim3(grid_of(n0, kBlock)), dim3(kBlock), 0, h->stream, c,
+                       b, pass ? nullptr : a->dq, a->rhs);
+    HIPCALL(hipEventRecord(h->fe_ev[0], h->stream));
+    HIPCALL(hipStreamWaitEvent(a->stream, h->fe_ev[0], 0));
+    CHECK(launch_direct(a, 0.0, 0));
+    HIPCALL(hipEventRecord(h->fe_ev[1], a->stream));
+    HIPCALL(hipStreamWaitEvent(h->stream, h->fe_ev[1], 0));
+    hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
+                       c, a->x, b, h->x, pass);
+    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
+    hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                       nrb, rtol, h->d_seq, h->d_last);
+    HIPCALL(hipGetLastError());
+    h->seq += 1;
+    CHECK(wait_published(h));
+    s = *h->h_last;
+    if (s.converged || s.relres != s.relres) break;
+  }
+  if (iters) *iters = std::min(pass, 2) + 1;
+  if (relres) *relres = s.relres;
+  if (converged) *converged = s.converged;
+  return NX_OK;
+}
+
 int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, int32_t* iters,
                double* relres, int32_t* converged) {
   for (int r = 0; r < t.P; ++r) {
@@ -7003,6 +7159,16 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   if (team_multi(t)) {  // every rank must take the same path (the signature holds it)
     CHECK(set_device(t.hs[0]));
     CHECK(check_schedules(t));
+  }
+  if (t.P == 1 && t.hs[0]->fe && t.hs[0]->fe_aux && t.hs[0]->solver == 1) {
+    CHECK(set_device(t.hs[0]));
+    int32_t conv = 0;
+    CHECK(fe_solve_direct(t.hs[0], rtol, iters, relres, &conv));
+    if (conv) {
+      t.hs[0]->last_solver = 1;
+      if (converged) *converged = 1;
+      return NX_OK;
+    }
   }
   if (direct_applicable(t)) {
     CHECK(set_device(t.hs[0]));
@@ -7635,6 +7801,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
                             hipSuccess)
       return fail(NX_ERR_HIP, "preconditioner upload failed");
     pa.Tlu = d;
+    pa.mo_div = 3.0;  // P1 (nx_set_cell_mass: a condensed (k, 0) system)
+    h->cond_mass = false;
     pa.exact = 1;  // (nx_set_pc_exact(h, 0): lumped D, P = blockdiag(D, G^T D^{-1} G))
   }
   for (const void* p : {(const void*)pa.chain_edge, (const void*)pa.chain_flip, (const void*)pa.chain_up,
@@ -8001,6 +8169,89 @@ NX_API int nx_set_cycles(nx_network_t* h, int32_t n, const int32_t* rows) {
   // neither the fused residual nor the fused step run
   h->fres_ok = false;
   h->dstep_ok = false;
+  return NX_OK;
+}
+
+NX_API int nx_set_cell_mass(nx_network_t* h, double ratio, double mo_div) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->pc || !h->pa.Tlu) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
+  if (h->fe) return fail(NX_ERR_STATE, "a P1/DG0 handle's preconditioner");
+  if (!(std::fabs(ratio) > 1.0) || !std::isfinite(mo_div) || mo_div == 0.0)
+    return fail(NX_ERR_ARG, "|ratio| must exceed 1 (a diagonally dominant T) and mo_div != 0");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  CHECK(drop_handle_graphs(h));
+  const std::vector<double> ti = mass_lu(h->N, ratio);
+  HIPCALL(hipMemcpy(const_cast<double*>(h->pa.Tlu), ti.data(), sizeof(double) * ti.size(),
+                    hipMemcpyHostToDevice));
+  h->pa.mo_div = mo_div;
+  h->cond_mass = !(ratio == 2.0 && mo_div == 3.0);
+  if (h->cond_mass) {  // the fused residual and the fused step regenerate P1's masses
+    h->fres_ok = false;
+    h->dstep_ok = false;
+  }
+  h->sched_checked = false;
+  return NX_OK;
+}
+
+NX_API int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64_t n_lm,
+                            const int32_t* slot, const int32_t* v_fe, const int32_t* v_aux,
+                            const int32_t* i_fe, const int32_t* p_fe, const int32_t* p_aux,
+                            const int32_t* l_fe, const int32_t* l_aux, const double* cst,
+                            double ab) {
+  CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->fe) return fail(NX_ERR_STATE, "a general-degree handle (nx_create_fe)");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  for (int** p : {&h->fe_slot, &h->fe_vfe, &h->fe_vaux, &h->fe_ife, &h->fe_pfe, &h->fe_paux,
+                  &h->fe_lfe, &h->fe_laux}) {
+    if (*p) HIPCALL(hipFree(*p));
+    *p = nullptr;
+  }
+  if (h->fe_cst) HIPCALL(hipFree(h->fe_cst));
+  h->fe_cst = nullptr;
+  h->fe_aux = nullptr;
+  if (aux == nullptr) return NX_OK;
+  if (k < 2 || k > 16) return fail(NX_ERR_ARG, "flux degree k in 2..16");
+  if (!slot || !v_fe || !v_aux || !i_fe || !p_fe || !p_aux || (n_lm > 0 && (!l_fe || !l_aux)) ||
+      !cst)
+    return fail(NX_ERR_ARG, "NULL array");
+  if (aux->fe || !aux->pc || !aux->cond_mass || aux->N != h->N || aux->E != h->E ||
+      aux->n_cyc > 0 || aux->device != h->device || aux->nranks > 1 || aux->comm || aux->group)
+    return fail(NX_ERR_STATE, "the auxiliary handle must be a one-rank P1/DG0 tree handle with "
+                              "the same N and edges and its cell mass set (nx_set_cell_mass)");
+  const int64_t E = h->E, N = h->N, nv = E * (N + 1), np = E * N, km = k - 1;
+  if (h->n_own != E * (k * N + 1 + N) + n_lm || aux->n_own != E * (2 * N + 1) + n_lm)
+    return fail(NX_ERR_ARG, "row counts do not match a (k, 0) layout and its P1/DG0 one");
+  auto in = [](const int32_t* a, int64_t n, int64_t lim) {
+    for (int64_t i = 0; i < n; ++i)
+      if (a[i] < 0 || a[i] >= lim) return false;
+    return true;
+  };
+  if (!in(slot, E, E) || !in(v_fe, nv, h->n_own) || !in(i_fe, np * km, h->n_own) ||
+      !in(p_fe, np, h->n_own) || !in(l_fe, n_lm, h->n_own) || !in(v_aux, nv, aux->n_own) ||
+      !in(p_aux, np, aux->n_own) || !in(l_aux, n_lm, aux->n_own))
+    return fail(NX_ERR_ARG, "row map out of range");
+  int rc = NX_OK;
+  if ((rc = upload(&h->fe_slot, slot, E, h->stream)) ||
+      (rc = upload(&h->fe_vfe, v_fe, nv, h->stream)) ||
+      (rc = upload(&h->fe_vaux, v_aux, nv, h->stream)) ||
+      (rc = upload(&h->fe_ife, i_fe, np * km, h->stream)) ||
+      (rc = upload(&h->fe_pfe, p_fe, np, h->stream)) ||
+      (rc = upload(&h->fe_paux, p_aux, np, h->stream)) ||
+      (rc = upload(&h->fe_lfe, l_fe, n_lm, h->stream)) ||
+      (rc = upload(&h->fe_laux, l_aux, n_lm, h->stream)) ||
+      (rc = upload(&h->fe_cst, cst, 4 * km + km * km, h->stream)))
+    return rc;
+  for (auto& e : h->fe_ev)
+    if (!e) HIPCALL(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  h->fe_aux = aux;
+  h->fe_k = k;
+  h->fe_nl = (int)n_lm;
+  h->fe_ab = ab;
   return NX_OK;
 }
 

@@ -84,3 +84,57 @@ def stable_pair(flux_degree: int, pressure_degree: int) -> bool:
     numbers ~1e16-1e18), and the reference's direct solve would fail on it.
     """
     return pressure_degree == 0 or flux_degree > pressure_degree
+
+
+def condensed_flux_mass(flux_degree: int):
+    """The P_k flux mass of one cell with its interior nodes condensed out, for DG0 pressure
+    (whose divergence touches only the cell's two vertex values, so the interior fluxes
+    appear in the flux rows alone): ``(alpha, beta, C, K, Mii_inv)`` with, for the cell mass
+    ``R h Mref`` and the node order (left vertex, interior 1..k-1, right vertex),
+
+    * ``R h [[alpha, beta], [beta, alpha]] = R h (M_vv - M_vi M_ii^{-1} M_iv)`` -- the
+      vertex-only (Schur) mass, symmetric under the cell's reflection;
+    * ``C = M_vi M_ii^{-1}`` (2 x (k-1)): the interior right-hand side's share moved onto
+      the vertices, ``b_v -= C b_i`` (h and R cancel);
+    * ``K = M_ii^{-1} M_iv`` ((k-1) x 2) and ``Mii_inv = M_ii^{-1}``: the interior values
+      back from the vertex ones, ``x_i = Mii_inv b_i / (R h) - K x_v``.
+
+    Exact rational arithmetic, rounded once (k = 1: alpha = 1/3, beta = 1/6, no interior)."""
+    from fractions import Fraction as F
+
+    k = int(flux_degree)
+    Cq = lagrange_monomials(k)
+    n = k + 1
+    M = [[F(0)] * n for _ in range(n)]
+    for i in range(n):
+        for j in range(n):
+            s = F(0)
+            for p, ap in enumerate(Cq[i]):
+                for q, bq in enumerate(Cq[j]):
+                    s += ap * bq / (p + q + 1)
+            M[i][j] = s
+    vi = [0, k]
+    ii = list(range(1, k))
+    ni = len(ii)
+    # exact inverse of M_ii (Gauss-Jordan over the rationals)
+    A = [[M[r][c] for c in ii] + [F(int(r2 == r)) for r2 in ii] for r in ii]
+    for col in range(ni):
+        piv = next(r for r in range(col, ni) if A[r][col] != 0)
+        A[col], A[piv] = A[piv], A[col]
+        d = A[col][col]
+        A[col] = [v / d for v in A[col]]
+        for r in range(ni):
+            if r != col and A[r][col] != 0:
+                f = A[r][col]
+                A[r] = [a - f * b for a, b in zip(A[r], A[col])]
+    Minv = [row[ni:] for row in A]
+    Mvi = [[M[v][c] for c in ii] for v in vi]
+    C = [[sum(Mvi[a][t] * Minv[t][j] for t in range(ni)) for j in range(ni)] for a in range(2)]
+    Kq = [[sum(Minv[i][t] * M[ii[t]][vi[b]] for t in range(ni)) for b in range(2)]
+          for i in range(ni)]
+    S = [[M[vi[a]][vi[b]] - sum(C[a][t] * M[ii[t]][vi[b]] for t in range(ni))
+          for b in range(2)] for a in range(2)]
+    assert S[0][0] == S[1][1] and S[0][1] == S[1][0]
+    f64 = lambda X: np.array([[float(v) for v in row] for row in X], dtype=np.float64)  # noqa: E731
+    return (float(S[0][0]), float(S[0][1]), f64(C).reshape(2, ni), f64(Kq).reshape(ni, 2),
+            f64(Minv).reshape(ni, ni))

@@ -208,3 +208,46 @@ def evaluate_terms(lay: FeLayout, R_edge: np.ndarray, f, edge_bc: np.ndarray,
             s += term(lay.b_idx[t], lay.b_ent[t])
         rhs[r] = s
     return val, rhs
+
+
+@dataclass
+class FeAuxMaps:
+    """Rows of the P1/DG0-structured system that the flux-degree-k / DG0 system condenses to
+    (``nx_fe_set_direct``): per FE cell-vertex flux, pressure cell and multiplier, the row of
+    the auxiliary P1 handle built from ``layout.build_local_problem`` of the same graph."""
+
+    v_fe: np.ndarray  # (E (N+1),) FE rows of the vertex fluxes, edge-major (graph order)
+    v_aux: np.ndarray  # their rows in the auxiliary system
+    i_fe: np.ndarray  # (E N (k-1),) FE rows of the interior fluxes, cell-major
+    p_fe: np.ndarray  # (E N,) FE pressure rows, edge-major
+    p_aux: np.ndarray
+    l_fe: np.ndarray  # (B,) FE multiplier rows, ascending node
+    l_aux: np.ndarray
+
+
+def build_fe_aux_maps(lay: FeLayout, lp) -> FeAuxMaps:
+    """Row maps between a (k, 0) layout and the one-rank P1 local problem ``lp`` of the same
+    graph (its edge slots ``lp.edges`` in its own order; multipliers by ascending node)."""
+    if lay.m != 0:
+        raise ValueError("the condensed direct solve is DG0's (pressure_degree 0)")
+    E, N, k = lay.E, lay.N, lay.k
+    slot = np.full(E, -1, dtype=np.int64)
+    slot[np.asarray(lp.edges, dtype=np.int64)] = np.arange(np.asarray(lp.edges).size)
+    if (slot < 0).any():
+        raise ValueError("the auxiliary problem must hold every edge (one rank)")
+    per1 = 2 * N + 1
+    g = np.arange(N + 1)
+    v_fe = lay.flux_rows[:, k * g].ravel()
+    v_aux = (slot[:, None] * per1 + 2 * g[None, :]).ravel()
+    c = np.arange(N)
+    i_fe = (lay.flux_rows[:, (k * c)[:, None] + np.arange(1, k)[None, :]]).ravel()
+    p_fe = lay.p_rows.astype(np.int64)
+    p_aux = (slot[:, None] * per1 + 2 * c[None, :] + 1).ravel()
+    lm1 = np.asarray(lp.lm_nodes, dtype=np.int64)
+    pos = np.searchsorted(lm1, lay.lm_nodes)
+    if not np.array_equal(lm1[np.minimum(pos, lm1.size - 1)], lay.lm_nodes):
+        raise ValueError("multiplier nodes differ")
+    l_aux = lp.n_edge_dofs + pos
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+    return FeAuxMaps(i32(v_fe), i32(v_aux), i32(i_fe), i32(p_fe), i32(p_aux),
+                     i32(lay.lm_rows), i32(l_aux))

@@ -172,7 +172,8 @@ class Solver:
             self.assembler.set_preconditioner(self._pc)
         if self.assembler.preconditioned and h.pc_exact() != self._pc_exact:
             h.set_pc_exact(self._pc_exact)
-        self.assembler.set_direct(self._direct and self.assembler.preconditioned)
+        self.assembler.set_direct(self._direct and (self.assembler.preconditioned
+                                                    or self.assembler.fe_direct_available))
         ce = self._check_every or (4 if self.assembler.preconditioned else 32)
         it, relres, conv = h.solve(self._rtol, self._maxit, ce)
         self._ksp.iterations, self._ksp.residual_estimate, self._ksp.converged = it, relres, conv

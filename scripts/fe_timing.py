@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""General element degrees on the GPU: assembly + plain-MINRES timing and parity at a
-mid-size tree (development / DESIGN numbers). Usage: python scripts/fe_timing.py [levels N]"""
+"""General element degrees on the GPU: assembly + plain-MINRES timing (and the direct solve,
+condensed for (k, 0)) at a mid-size tree (development / DESIGN numbers). Usage: python scripts/fe_timing.py [levels N]"""
 
 from __future__ import annotations
 
@@ -43,6 +43,21 @@ def main() -> int:
             x = np.concatenate([fn.x.array for fn in _functions(asm)])
             line += f" err_vs_analytic={np.linalg.norm(x - xa) / np.linalg.norm(xa):.2e}"
         print(line, flush=True)
+        if asm.fe_direct_available or km == (1, 0):  # the direct solve (condensed for k >= 2)
+            if km == (1, 0):
+                asm.set_preconditioner(True)
+            asm.set_direct(True)
+            ts = []
+            for _ in range(6):
+                t0 = time.perf_counter()
+                h.assemble(True, True)
+                it, rr, conv = h.solve(1e-12, 200000, 4)
+                h.sync()
+                ts.append(1e3 * (time.perf_counter() - t0))
+            x = h.solution()
+            print(f"k={km[0]} m={km[1]} direct passes={it} relres={rr:.2e} conv={conv} "
+                  f"used={h.solver()[1]} min {min(ts[1:]):.3f} ms median "
+                  f"{float(np.median(ts[1:])):.3f} ms", flush=True)
         asm.close()
     return 0
 

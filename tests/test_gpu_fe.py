@@ -167,3 +167,52 @@ def test_fe_single_edge(km):
     x_ref = O.solve_reference(*OF.assemble_reference_fe(F, pbc))
     got = np.concatenate([fn.x.array for fn in sol])
     assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "depth6_N40", "arterial5_N40",
+                                  "tree6_2d_N70"])
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_fe_direct_condensed(case, k):
+    """(k, 0) through the condensed P1/DG0 system (nx_fe_set_direct): the direct path runs
+    (no MINRES), within SOL_TOL of the oracle's LU, its reported residual is the true one,
+    <= 1e-12 after at most two refinement passes; a second solve with other coefficients
+    (the auxiliary lumped mass rebuilt) stays exact."""
+    E = len(CASES[case][0]().edges())
+    R = 1.0 + 0.5 * (np.arange(E) % 3)
+    mesh, asm, F, A, b, pbc = _setup(case, (k, 0), f=0.4, R=R)
+    assert asm.fe_direct_available
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.solver_used == "direct" and solver.ksp.converged
+    assert 1 <= solver.ksp.iterations <= 3
+    x_ref = O.solve_reference(A, b)
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    tr = solver.true_residual()
+    assert tr <= 1e-12
+    assert abs(solver.ksp.residual_estimate - tr) <= 1e-6 * tr + 1e-16
+    # other coefficients: the same handles, the condensed masses rebuilt from the new R
+    R2 = 2.0 - 0.25 * (np.arange(E) % 4)
+    asm.compute_forms(p_bc_ex=pbc, f=0.1, R=R2)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.solver_used == "direct" and solver.ksp.converged
+    A2, b2 = OF.assemble_reference_fe(F, pbc, f=0.1, R=R2)
+    x2 = O.solve_reference(A2, b2)
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x2) / np.linalg.norm(x2) <= SOL_TOL
+
+
+def test_fe_direct_cycles_run_minres():
+    """A graph with cycles (the reference's edge-info graph): no condensed direct solve (the
+    Woodbury correction is built from a P1 CSR), MINRES converges to the oracle's answer."""
+    mesh, asm, F, A, b, pbc = _setup("edge_info_N10", (2, 0))
+    assert not asm.fe_direct_available
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.solver_used == "minres" and solver.ksp.converged
+    got = np.concatenate([fn.x.array for fn in sol])
+    x_ref = O.solve_reference(A, b)
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
