@@ -287,7 +287,8 @@ class HydraulicNetworkAssembler:
             self._init_comm()
         self._edge_ids = lp.edges
         # MINRES preconditioner (tree Schur complement); topology-only, built once
-        if mesh.N <= 1024:
+        if mesh.N <= 1024 and np.any(np.asarray(mesh.degrees) > 1):
+            # (no junction anywhere -- one edge, or separate edges: plain MINRES)
             # 256 jobs = one workgroup per CU (swept on MI355X: 64..1024)
             self._pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=256)
         self.set_preconditioner(True)
@@ -330,7 +331,7 @@ class HydraulicNetworkAssembler:
         self._lm_idx = fe.lm_rows
         self._set_output_map()
         self._fe_aux = None
-        if m == 0 and mesh.N <= 1024:
+        if m == 0 and mesh.N <= 1024 and np.any(np.asarray(mesh.degrees) > 1):
             self._init_fe_direct(src, dst)
 
     def _init_fe_direct(self, src, dst) -> None:

@@ -610,8 +610,14 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         lv_len = np.diff(lvl_slot_off)
         job_of_slot[:n_lower_slots] = np.repeat(lvl_job, lv_len)
     chain_job = np.full(E, -1, dtype=np.int64)
-    jlo = np.where(lo != -1, job_of_slot[slot_of[np.maximum(lo, 0)]], -1)
-    jup = np.where(up != -1, job_of_slot[slot_of[np.maximum(up, 0)]], -1)
+    def job_at(nodes):  # the job of a chain end's slot (-1: no junction there)
+        sl = slot_of[np.maximum(nodes, 0)]
+        out = np.full(nodes.shape, -1, dtype=np.int64)
+        ok = (nodes != -1) & (sl >= 0)
+        out[ok] = job_of_slot[sl[ok]]
+        return out
+
+    jlo, jup = job_at(lo), job_at(up)
     c1 = (lo != -1) & (jlo >= 0)
     chain_job[c1] = jlo[c1]
     c2 = (lo == -1) & (up != -1) & (jup >= 0)

@@ -147,7 +147,7 @@ def test_fe_reassemble_idempotent():
     np.testing.assert_array_equal(asm.handle.rhs(), r1)
 
 
-@pytest.mark.parametrize("km", [(2, 0), (3, 2)])
+@pytest.mark.parametrize("km", [(1, 0), (2, 0), (3, 2)])
 def test_fe_single_edge(km):
     """One edge, one cell: no multipliers; the device solve equals the direct solve."""
     import networkx as nx
