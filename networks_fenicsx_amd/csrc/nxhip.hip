@@ -55,10 +55,6 @@ __device__ unsigned long long g_dst[32][512];  // k_dir_step: per-workgroup stam
   do {                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 512) g_dst[(k)][blockIdx.x] = wall_clock64(); \
   } while (0)
-#define NX_DCOUNT(k, v)                                                \
-  do {                                                                 \
-    if (threadIdx.x == 0 && blockIdx.x < 512) g_dst[(k)][blockIdx.x] = (v); \
-  } while (0)
 #define NX_PHASE(slot)                                           \
   do {                                                           \
     if (blockIdx.x == 0) {                                       \
@@ -96,9 +92,6 @@ __device__ unsigned long long g_dst[32][512];  // k_dir_step: per-workgroup stam
   } while (0)
 #define NX_DSTAMP(k) \
   do {               \
-  } while (0)
-#define NX_DCOUNT(k, v) \
-  do {                  \
   } while (0)
 #endif
 
@@ -4012,19 +4005,15 @@ __device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirSte
 // The assembly's stores of one workgroup (after its hand-off): a strided share of the
 // multiplier rows (+-1 values, zero rhs), then its chains' edges -- from the kept lanes
 // (keep: one chain pass) or re-assembled pass by pass.
-__device__ __forceinline__ void dir_lm_share(const PcArgs& pa, const DirStep& da, int job) {
+template <int W, int CPL, bool UNIT = false>
+__device__ __forceinline__ void dir_stores_all(const PcArgs& pa, const DirStep& da, int job,
+                                               bool keep, DirLane<W, CPL>& L) {
   const int nj = pa.n_jobs;
   const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
   for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
     if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
     if (i < da.B) da.rhs_lm[i] = 0.0;
   }
-}
-
-template <int W, int CPL, bool UNIT = false>
-__device__ __forceinline__ void dir_stores_all(const PcArgs& pa, const DirStep& da, int job,
-                                               bool keep, DirLane<W, CPL>& L) {
-  dir_lm_share(pa, da, job);
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   if (keep) {
     dir_chain_store<W, CPL, UNIT>(pa, da, c0 + (int)threadIdx.x / W < c1, L);
@@ -4168,30 +4157,16 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
 // slots' and chains' data stored for the down sweep), hands the top part's inputs over
 // write-through and leaves after its assembly stores; the workgroup arriving last solves the
 // rank's top part and builds its coarse partials [D | J | G] (top_body<MULTI, WT>: what
-// k_pc_top_lds does). Its own chains' stores are shared out (the helpers): it publishes its
-// job before the top part, and the other workgroups, after their own stores, claim its chain
-// passes one at a time (re-assembled, stored unit-stride); it claims what is left after the
-// top part. The claims come from one counter that only grows, each launch from the base the
-// published word carries, so every pass is stored exactly once, whoever is there. A helper
-// waits a bounded time for the word and then leaves (the last arrival stores what nobody
-// claimed): any number of jobs may run. It replaces k_assemble_seg -> k_pc_up_lds (mode 3)
-// -> k_pc_top_lds. The arrival counter is reset by the last workgroup (graph replays launch
-// it with the same arguments). da.sync: [0] arrivals, [2..3] the published word (job | gen
-// << 16 | claim base << 32), [4..5] the claim counter.
-constexpr int kHelpPolls = 1 << 16;
+// k_pc_top_lds does), then re-assembles its own lanes and stores them. It replaces
+// k_assemble_seg -> k_pc_up_lds (mode 3) -> k_pc_top_lds. No workgroup waits for another
+// (the last arrival does the work), so any number of jobs may run; the arrival counter is
+// reset by the last workgroup (graph replays launch it with the same arguments).
 template <int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep da) {
   __shared__ double smem[kDirLds];
   __shared__ int sFlag;
-  __shared__ unsigned long long sWord;
-  __shared__ int sClaim;
   const int job = blockIdx.x;
   const int nj = pa.n_jobs;
-  unsigned long long* hword = reinterpret_cast<unsigned long long*>(da.sync + 2);
-  unsigned long long* hclaim = reinterpret_cast<unsigned long long*>(da.sync + 4);
-  // the word of the previous launch (published after every workgroup's arrival: read here,
-  // before this one's arrival, it is the old one)
-  if (threadIdx.x == 0) sWord = __hip_atomic_load(hword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   NX_DSTAMP(0);
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   const bool keep = c1 - c0 <= kPcThreads / W;
@@ -4200,6 +4175,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
   // (the assembly's stores after the hand-off, re-assembled pass by pass with several
   // passes: the last arrival -- the top part's start -- comes sooner)
   dir_up_fused<W, CPL, true>(pa, da, smem, L, false, sA_, sB_);
+  auto stores = [&]() { dir_stores_all<W, CPL>(pa, da, job, keep, L); };
   vm_drain();
   __syncthreads();
   NX_DSTAMP(1);
@@ -4209,57 +4185,11 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
     sFlag = old == (unsigned)(nj - 1) ? 1 : 0;
   }
   __syncthreads();
-  constexpr int G = kPcThreads / W;
-  // claim passes of job jl's chains until none is left (base: this launch's first claim)
-  auto claim_loop = [&](int jl, unsigned base) {
-    const int a0 = pa.job_chain_off[jl], a1 = pa.job_chain_off[jl + 1];
-    const int np = (a1 - a0 + G - 1) / G;
-    int got = 0;
-    for (;;) {
-      if (threadIdx.x == 0)
-        sClaim = (int)((unsigned)__hip_atomic_fetch_add(hclaim, 1ull, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT) - base);
-      __syncthreads();
-      const int p = sClaim;
-      __syncthreads();
-      if (p < 0 || p >= np) break;
-      ++got;
-      const int c = a0 + p * G + (int)threadIdx.x / W;
-      dir_chain_asm<W, CPL>(pa, da, c, c < a1, L);
-      dir_chain_store<W, CPL, true>(pa, da, c < a1, L);
-    }
-    NX_DCOUNT(31, (unsigned long long)got);
-    NX_DSTAMP(29);  // (stamps 28-31: team_phases.py)
-  };
   if (!sFlag) {
     dir_stores_all<W, CPL, true>(pa, da, job, keep, L);  // (unit stride: see dir_chain_store)
     NX_DSTAMP(8);
-    // a helper (da.epoch != 0: every workgroup resident, so waiting holds no one up): the
-    // last arrival's word, bounded wait
-    if (threadIdx.x == 0) {
-      const unsigned long long g0 = sWord;
-      unsigned long long w = g0;
-      for (int k = 0; da.epoch != 0u && k < kHelpPolls && w == g0; ++k) {
-        w = __hip_atomic_load(hword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w == g0) __builtin_amdgcn_s_sleep(2);
-      }
-      sFlag = w != g0 ? 1 : 0;
-      sWord = w;
-    }
-    __syncthreads();
-    NX_DSTAMP(28);
-    if (sFlag) claim_loop((int)(sWord & 0xffffull), (unsigned)(sWord >> 32));
     return;
   }
-  if (threadIdx.x == 0) {  // publish this job and the claim base
-    const unsigned long long g0 = sWord;
-    const unsigned base = (unsigned)__hip_atomic_load(hclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long gen = ((g0 >> 16) + 1ull) & 0xffffull;
-    const unsigned long long w = ((unsigned long long)base << 32) | (gen << 16) | (unsigned long long)job;
-    __hip_atomic_store(hword, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sWord = w;
-  }
-  __syncthreads();
   if (pa.top_nt > 0) {
     double* t = smem;
     TopLds T;
@@ -4288,8 +4218,8 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_team_up(PcArgs pa, DirStep d
   NX_DSTAMP(7);
   if (threadIdx.x == 0)  // (every other workgroup has arrived: nothing counts after this)
     __hip_atomic_store(da.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  dir_lm_share(pa, da, job);
-  claim_loop(job, (unsigned)(sWord >> 32));  // (the passes no helper took)
+  if (keep) dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, c0 + (int)threadIdx.x / W < c1, L);
+  stores();
 }
 
 // Factored coefficients from this solve's D (after the start application).
@@ -6613,8 +6543,7 @@ template <int W, int CPL>
 void launch_dteam_wc(nx_network* h) {
   DirStep da{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
              h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
-             h->rhs + h->n_edge_dofs, h->x, nullptr, nullptr, 0, nullptr, h->d_tsync,
-             h->pc_jobs <= h->n_cu ? 1u : 0u,  // (k_dir_team_up: helpers wait only then)
+             h->rhs + h->n_edge_dofs, h->x, nullptr, nullptr, 0, nullptr, h->d_tsync, 0,
              0.0, 0, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL((k_dir_team_up<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0, h->stream,
                      h->pa, da);
@@ -7970,12 +7899,11 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     pa.rhs_b = h->rhs;
     h->n_left = (int)left.size();
     h->fres_ok = pa.slot_rloc && h->d_left && pa.rpart && h->dir_bb && h->tmp;
-    {  // k_dir_team_up's arrival counter (zero; its last workgroup resets it), published
-       // word and claim counter (64-bit, 8-byte aligned)
+    {  // k_dir_team_up's arrival counter (zero; its last workgroup resets it)
       unsigned* ty = nullptr;
-      if (hipMalloc((void**)&ty, 8 * sizeof(unsigned)) == hipSuccess) {
+      if (hipMalloc((void**)&ty, sizeof(unsigned)) == hipSuccess) {
         h->pc_bufs.push_back(ty);
-        if (hipMemset(ty, 0, 8 * sizeof(unsigned)) != hipSuccess) ty = nullptr;
+        if (hipMemset(ty, 0, sizeof(unsigned)) != hipSuccess) ty = nullptr;
       }
       h->d_tsync = ty;
     }

@@ -52,12 +52,6 @@ def main() -> int:
         print(f"  stores done (non-last) med {np.median(us[8]):7.2f} max {us[8].max():7.2f}")
         print(f"  last wg {last}: arrival {us[1][last]:.2f}, inputs loaded {us[6][last]:.2f}, "
               f"top part + coarse partials {us[7][last]:.2f}")
-        helper = np.arange(nj) != last
-        print(f"  helpers: word seen med {np.median(us[28][helper]):7.2f} max "
-              f"{us[28][helper].max():7.2f}; claims end med {np.median(us[29][helper]):7.2f} "
-              f"max {us[29][helper].max():7.2f}; passes claimed by helpers "
-              f"{int(g[31][helper].sum())}, by the last wg {int(g[31][last])} "
-              f"(its end {us[29][last]:.2f})")
         print(f"  up levels of the top part (deepest first) end at: "
               f"{' '.join(f'{us[12 + q][last]:.2f}' for q in reversed(range(8)))}")
     finally:
