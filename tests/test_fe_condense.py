@@ -99,3 +99,32 @@ def test_schur_identity_for_condensed_masses(k):
     SL = B @ np.linalg.solve(np.diag(Ms.sum(1)), B.T)
     np.testing.assert_allclose(np.linalg.inv(S), np.linalg.inv(SL) - beta * R * h * np.eye(N),
                                atol=1e-12)
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_flattened_constants_as_the_kernels_index_them(k):
+    """The constants nx_fe_set_direct uploads (assembly.py: C | K | Mii, row-major) read
+    with k_fe_condense's / k_fe_expand's indexing: C row 0 at cst[i], row 1 at cst[km + i],
+    K[j] at cst[2 km + 2 j + {0, 1}], Mii[j][i] at cst[4 km + j km + i]; the exact condensed
+    ratios a / b = (-1)^(k+1) (k+1) and (a + b) / b that nx_set_cell_mass receives."""
+    alpha, beta, C, K, Mii = condensed_flux_mass(k)
+    km = k - 1
+    cst = np.concatenate([C.ravel(), K.ravel(), Mii.ravel()])
+    assert cst.size == 4 * km + km * km
+    for i in range(km):
+        assert cst[i] == C[0, i] and cst[km + i] == C[1, i]
+    for j in range(km):
+        assert cst[2 * km + 2 * j] == K[j, 0] and cst[2 * km + 2 * j + 1] == K[j, 1]
+        for i in range(km):
+            assert cst[4 * km + j * km + i] == Mii[j, i]
+    ratio = (-1) ** (k + 1) * (k + 1)
+    assert abs(alpha / beta - ratio) < 1e-12
+    assert abs((alpha + beta) / beta - (ratio + 1)) < 1e-12
+    # the pivots of T = tridiag(1, 2 ratio, 1) with ratio at both ends stay away from zero
+    N = 9
+    T = np.diag(np.full(N + 1, 2.0 * ratio)) + np.diag(np.ones(N), 1) + np.diag(np.ones(N), -1)
+    T[0, 0] = T[N, N] = ratio
+    Ms = np.zeros((N + 1, N + 1))
+    for c in range(N):
+        Ms[c:c + 2, c:c + 2] += np.array([[alpha, beta], [beta, alpha]])
+    np.testing.assert_allclose(T * beta, Ms, atol=1e-15)
