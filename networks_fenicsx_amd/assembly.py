@@ -654,3 +654,7 @@ class HydraulicNetworkAssembler:
         if pool is not None:
             pool.close()
         self._handle.close()
+        aux = getattr(self, "_fe_aux", None)
+        if aux is not None:  # (after the handle that used it)
+            aux.close()
+            self._fe_aux = None

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """General element degrees on the GPU: assembly + plain-MINRES timing (and the direct solve,
-condensed for (k, 0)) at a mid-size tree (development / DESIGN numbers). Usage: python scripts/fe_timing.py [levels N]"""
+condensed for (k, 0)) at a mid-size tree (development / DESIGN numbers).
+Usage: python scripts/fe_timing.py [levels N ["k,m;k,m..."]]"""
 
 from __future__ import annotations
 
@@ -23,7 +24,10 @@ def main() -> int:
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     mesh = NetworkMesh(ng.make_tree(levels, levels, levels), N=N, color_strategy="smallest_last")
     pbc = lambda x: x[1]  # noqa: E731
-    for km in [(1, 0), (2, 0), (2, 1), (3, 2)]:
+    pairs = [(1, 0), (2, 0), (2, 1), (3, 2)]
+    if len(sys.argv) > 3:  # e.g. "1,0;2,0;3,0"
+        pairs = [tuple(int(v) for v in p.split(",")) for p in sys.argv[3].split(";")]
+    for km in pairs:
         asm = HydraulicNetworkAssembler(mesh, flux_degree=km[0], pressure_degree=km[1])
         asm.compute_forms(p_bc_ex=pbc)
         h = asm.handle
