@@ -378,6 +378,14 @@ int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left);
  * 0 for the separate launches (assembly, up sweep, down sweep, publish). Replaces nothing
  * in the reference (PETSc's KSPSolve is one call: solver.py:127). */
 int nx_get_direct_path(nx_network_t* h, int32_t* path);
+/* (path 2: the (k, 0) condensed route of nx_fe_set_direct.)
+ * Test hook: the number of s_sleep-paced polls a k_dir_step workgroup spends waiting for the
+ * top part's values before it gives up (default 2^20). 0 makes every waiting workgroup give
+ * up at once, which forces the fallback a non-co-resident launch takes: the host resets the
+ * hand-off counters and the device's published-state count and runs the separate launches
+ * on this handle from then on (until the next nx_set_preconditioner). Replaces nothing in
+ * the reference. */
+int nx_debug_set_wait_polls(nx_network_t* h, uint32_t polls);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
 /* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,

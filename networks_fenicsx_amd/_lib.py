@@ -65,6 +65,7 @@ _SIGS = {
     "nx_get_profile_direct": (C.c_int, [_h, _pd, _pi64]),
     "nx_get_direct_info": (C.c_int, [_h, _pi32, _pi32]),
     "nx_get_direct_path": (C.c_int, [_h, _pi32]),
+    "nx_debug_set_wait_polls": (C.c_int, [_h, C.c_uint32]),
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
     "nx_bench_spmv_cold": (C.c_int, [_h, _i32, _pi32, _pd]),
@@ -368,10 +369,16 @@ class Handle:
 
     def direct_path(self) -> str:
         """What the last direct solve ran (nx_get_direct_path): ``"fused"`` (k_dir_step, one
-        launch) or ``"launches"`` (assembly, up, down, publish)."""
+        launch), ``"launches"`` (assembly, up, down, publish) or ``"condensed"`` (the (k, 0)
+        route through the auxiliary P1/DG0 handle)."""
         v = C.c_int32(0)
         check(lib().nx_get_direct_path(self.ptr, C.byref(v)))
-        return "fused" if v.value == 1 else "launches"
+        return {1: "fused", 2: "condensed"}.get(v.value, "launches")
+
+    def set_wait_polls(self, polls: int) -> None:
+        """Test hook (``nx_debug_set_wait_polls``): the fused step's wait bound; 0 forces
+        the give-up fallback to the separate launches."""
+        check(lib().nx_debug_set_wait_polls(self.ptr, int(polls)))
 
     def reset_profile(self) -> None:
         check(lib().nx_reset_profile(self.ptr))

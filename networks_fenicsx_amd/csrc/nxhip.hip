@@ -3232,6 +3232,7 @@ struct DirStep {
   // hand-offs: [0] phase-1 arrivals, [1] phase-2 arrivals, [2] top flag, [3] wait errors
   unsigned* sync;
   unsigned epoch;  // launches since the counters were zero
+  unsigned polls;  // s_sleep-paced polls before a waiting workgroup gives up (kDirWaitPolls)
   // the published state
   double rtol;
   int seq_next;
@@ -4101,7 +4102,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
         int ok = 0;
-        for (int k = 0; k < kDirWaitPolls; ++k) {
+        for (unsigned k = 0; k < da.polls; ++k) {
           if (__hip_atomic_load(da.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
               da.epoch + 1u) {
             ok = 1;
@@ -5235,6 +5236,7 @@ struct nx_network {
   double* d_post = nullptr;
   unsigned* d_dsync = nullptr;
   unsigned dstep_epoch = 0;
+  unsigned dstep_polls = kDirWaitPolls;  // the wait bound (nx_debug_set_wait_polls: tests)
   unsigned* d_tsync = nullptr;  // k_dir_team_up's arrival counter (several ranks; pc_bufs)
   bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
   int last_dir_path = 0;   // the last direct solve: 0 four launches, 1 k_dir_step
@@ -5252,6 +5254,7 @@ struct nx_network {
   double* cyc_w = nullptr;     // m
   bool cyc_raw = false;        // cyc_build's solves: the tree solve alone
   int64_t lhs_version = 0, cyc_version = -1;
+  int64_t coef_version = 0, asm_coef_version = -1;  // nx_set_coefficients calls; at the last lhs
   // several ranks, direct (nx_set_cut): the multiplier rows of the K cut bifurcations are
   // completed inside the residual's all-reduce (no halo of x): per left row its cut index,
   // per cut index the owned row (or -1) and this rank's flux ends at it (row, +-1)
@@ -6220,6 +6223,7 @@ NX_API int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_c
   }
   h->f = f;
   h->have_coeffs = true;
+  h->coef_version += 1;  // (R may have changed: the next lhs assembly is a new matrix)
   HIPCALL(hipStreamSynchronize(h->stream));
   return NX_OK;
 }
@@ -6326,7 +6330,12 @@ NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
   }
   if (lhs) {
     h->have_lhs = true;
-    h->lhs_version += 1;  // (a graph with cycles rebuilds its Woodbury correction)
+    // a graph with cycles rebuilds its Woodbury correction (2 n_cyc tree solves) only when
+    // the matrix values can have changed: new coefficients since the last lhs assembly
+    if (h->asm_coef_version != h->coef_version) {
+      h->lhs_version += 1;
+      h->asm_coef_version = h->coef_version;
+    }
   }
   if (rhs) h->have_rhs = true;
   return NX_OK;
@@ -6531,8 +6540,8 @@ void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
   DirStep da{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
              h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
              h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
-             h->d_post, h->d_dsync, h->dstep_epoch, rtol, h->seq + 1, h->d_seq, h->d_last,
-             h->dir_bb};
+             h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1, h->d_seq,
+             h->d_last, h->dir_bb};
   hipExtLaunchKernelGGL((k_dir_step<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0, h->stream,
                         prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0, h->pa, da);
 }
@@ -6543,7 +6552,7 @@ template <int W, int CPL>
 void launch_dteam_wc(nx_network* h) {
   DirStep da{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
              h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
-             h->rhs + h->n_edge_dofs, h->x, nullptr, nullptr, 0, nullptr, h->d_tsync, 0,
+             h->rhs + h->n_edge_dofs, h->x, nullptr, nullptr, 0, nullptr, h->d_tsync, 0, 0,
              0.0, 0, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL((k_dir_team_up<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0, h->stream,
                      h->pa, da);
@@ -6852,10 +6861,14 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     }
     if (rc != NX_ERR_STATE) return rc;
     // a workgroup gave up waiting (they were not all resident): reset the hand-off counters
-    // and take the four-launch path from now on (the assembly is still pending)
+    // and take the four-launch path from now on (the assembly is still pending). The launch
+    // published nothing, so the device's count of published states (d_seq, which the next
+    // publish increments) is one behind the host's: take the host's back from the device,
+    // or every later wait_published expects a stamp the publish kernels never write.
     (void)hipGetLastError();
     HIPCALL(hipStreamSynchronize(h->stream));
     HIPCALL(hipMemset(h->d_dsync, 0, 4 * sizeof(unsigned)));
+    HIPCALL(hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost));
     h->dstep_epoch = 0;
     h->dstep_off = true;
   }
@@ -7119,6 +7132,7 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
   MrState s{};
   int pass = 0;
+  h->last_dir_path = 2;  // the condensed route (nx_get_direct_path)
   for (; pass < 3; ++pass) {
     const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
     hipLaunchKernelGGL(k_fe_condense, dim3(grid_of(n0, kBlock)), dim3(kBlock), 0, h->stream, c,
@@ -7558,6 +7572,12 @@ NX_API int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left) 
 NX_API int nx_get_direct_path(nx_network_t* h, int32_t* path) {
   if (!h || !path) return fail(NX_ERR_ARG, "null argument");
   *path = h->last_dir_path;
+  return NX_OK;
+}
+
+NX_API int nx_debug_set_wait_polls(nx_network_t* h, uint32_t polls) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  h->dstep_polls = polls;
   return NX_OK;
 }
 

@@ -144,6 +144,44 @@ def test_dstep_repeated_launches_and_new_coefficients():
     asm.close()
 
 
+@pytest.mark.parametrize("case", ["depth6_N40", "arterial5_N40"])
+def test_dstep_give_up_falls_back_to_launches(case, monkeypatch):
+    """The co-residency fallback: when the waiting workgroups give up
+    (forced here with a wait bound of 0 polls), the launch publishes nothing; the host resets
+    the hand-off counters and its published-state count, and the same solve runs the
+    separate launches -- x bit-equal to NXHIP_DIR_FUSED=0 on the same matrix -- and keeps
+    doing so, correctly, for the following steps."""
+    mesh, asm, P, A, b = _setup(case)
+    h = asm.handle
+    Ab, bb, perm, _ = O.to_build_layout(P, A, b)
+    x_ref = O.solve_reference(A, b)[perm]
+    # the separate launches' answer on this matrix (the reference bits of the fallback)
+    monkeypatch.setenv("NXHIP_DIR_FUSED", "0")
+    asm.assemble()
+    it0, rr0, conv0 = h.solve(1e-12, 100, 4)
+    assert h.direct_path() == "launches" and conv0
+    x_launch = h.solution()
+    monkeypatch.delenv("NXHIP_DIR_FUSED")
+    asm.assemble()
+    h.solve(1e-12, 100, 4)
+    assert h.direct_path() == "fused"
+    # every waiting workgroup gives up at once: the step must still return the answer
+    h.set_wait_polls(0)
+    asm.assemble()
+    it, rr, conv = h.solve(1e-12, 100, 4)
+    assert h.direct_path() == "launches" and conv and it == 1 and rr == rr0
+    np.testing.assert_array_equal(h.solution(), x_launch)
+    h.set_wait_polls(1 << 20)
+    for _ in range(10):  # the fallback is sticky and its published states stay in step
+        asm.assemble()
+        it, rr, conv = h.solve(1e-12, 100, 4)
+        assert h.direct_path() == "launches" and conv and it == 1 and rr == rr0
+        np.testing.assert_array_equal(h.solution(), x_launch)
+    assert np.linalg.norm(x_launch - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    np.testing.assert_array_equal(h.csr()[2], Ab.data)
+    asm.close()
+
+
 def test_dstep_c3_analytic():
     """C3 (make_tree(15), N = 15, 1,032,160 DoF, 256 jobs = one per CU): the fused step
     runs, the analytic answer to 1e-10, the CSR has the closed-form nnz and is symmetric."""
@@ -161,6 +199,13 @@ def test_dstep_c3_analytic():
     x = h.solution()
     assert np.linalg.norm(x - xa) / np.linalg.norm(xa) <= SOL_TOL
     assert h.true_residual() <= 1e-12
+    # the hand-offs between the 256 workgroups (write-through stores + one agent-scope
+    # counter, no release fence: DESIGN.md section 3c) give the same bits on every launch
+    for _ in range(30):
+        asm.assemble()
+        it2, rr2, conv2 = h.solve(1e-12, 100, 4)
+        assert h.direct_path() == "fused" and rr2 == rr
+        np.testing.assert_array_equal(h.solution(), x)
     rp, col, val = h.csr()
     E, B = mesh.num_edges, len(mesh.bifurcation_values)
     assert rp[-1] == E * (7 * 15 + 1) + 6 * B
