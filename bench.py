@@ -200,9 +200,18 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
                            "reference forms + scipy SuperLU spsolve (1 thread, the MUMPS "
                            "stand-in)"})
     head = legs[0]
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {"value": head["value"], "unit": "DoF/s", "cores": head["cores"], "kind": "port",
             "ms_per_step": head["ms_per_step"], "sample": head["sample"],
-            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "legs": legs}
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "affinity_cpus": affinity, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "cores_note": ("the OpenMP legs use every thread OpenMP is given: OMP_NUM_THREADS, "
+                           "which the GPU box sets to its CPU share per GPU (16); "
+                           "os.cpu_count() is the whole shared host"),
+            "legs": legs}
 
 
 def _free_port() -> int:

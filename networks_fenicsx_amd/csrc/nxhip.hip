@@ -50,7 +50,7 @@ thread_local std::string g_err;
 __device__ unsigned long long g_phase[128];
 __device__ unsigned long long g_wgs[8][512];  // per-workgroup start / end, last launch wins
 __device__ unsigned long long g_wge[8][512];
-__device__ unsigned long long g_dst[32][512];  // k_dir_step: per-workgroup stamps (nx_debug_dstep)
+__device__ unsigned long long g_dst[48][512];  // k_dir_step: per-workgroup stamps (nx_debug_dstep)
 #define NX_DSTAMP(k)                                                   \
   do {                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 512) g_dst[(k)][blockIdx.x] = wall_clock64(); \
@@ -1114,6 +1114,17 @@ struct PcArgs {
   // [level | nk << 8 | (parent + 1) << 12, children packed 8 bits each] (nx_set_coarse), so
   // the one-wave coarse solve needs no staging (coarse_wave_solve)
   const int* c_wave;
+  // the top part as wave subtrees (round 4, host-built; null: the level sweeps of top_wave):
+  // every maximal subtree of <= 64 slots is swept by one wave with shuffles (lane = slot, no
+  // barriers), the few slots above them ("upper", top_sub_nup levels) by the level sweeps.
+  // top_sub: per top slot (1 + kWaveKids) ints as top_wave for upper slots (word 0 with bit
+  // 31 set), word 0 = 0 for subtree members; top_lane: per thread of the top part's
+  // workgroup [slot or -1, lane | depth << 6 | nk << 14 | parent lane << 18, kWaveKids x
+  // (child lane | dc offset << 12)]; top_sub_dep: per wave its subtree's depth (0: none)
+  const int* top_sub;
+  const int* top_lane;
+  const int* top_sub_dep;
+  int top_sub_nup;
   int top_ts0, top_nt, top_dc0, top_ndc;  // the top part's slots and hanging-chain entries
 };
 
@@ -2167,7 +2178,8 @@ struct TopLds {
 struct TopPre {
   int c, lo, lam, pcn, par, off;
   double T, It, Dl, Jl, y, Tp, Ib;
-  int w[1 + kWaveKids];  // pa.top_wave of slot tid (loaded with the indices)
+  int w[1 + kWaveKids];  // pa.top_wave (or top_sub) of slot tid (loaded with the indices)
+  int ls, lw[1 + kWaveKids], ldep;  // pa.top_lane of thread tid, its wave's subtree depth
 };
 
 __device__ __forceinline__ void top_pre_idx(const PcArgs& pa, TopPre& p) {
@@ -2179,9 +2191,21 @@ __device__ __forceinline__ void top_pre_idx(const PcArgs& pa, TopPre& p) {
   p.pcn = tid < nt ? pa.slot_pchain[ts0 + tid] : -1;
   p.par = tid < nt ? pa.slot_parent[ts0 + tid] : -1;
   p.off = tid < nt ? pa.slot_dc_off[ts0 + tid] : 0;
+  const int* tw = pa.top_sub ? pa.top_sub : pa.top_wave;
 #pragma unroll
   for (int k = 0; k <= kWaveKids; ++k)
-    p.w[k] = (pa.top_wave && tid < nt) ? pa.top_wave[(1 + kWaveKids) * (int64_t)tid + k] : 0;
+    p.w[k] = (tw && tid < nt) ? tw[(1 + kWaveKids) * (int64_t)tid + k] : 0;
+  p.ls = -1;
+  p.ldep = 0;
+#pragma unroll
+  for (int k = 0; k <= kWaveKids; ++k) p.lw[k] = 0;
+  if (pa.top_sub) {
+    const int* lt = pa.top_lane + (2 + kWaveKids) * (int64_t)tid;
+    p.ls = lt[0];
+#pragma unroll
+    for (int k = 0; k <= kWaveKids; ++k) p.lw[k] = lt[1 + k];
+    p.ldep = pa.top_sub_dep[tid >> 6];
+  }
 }
 
 // WT: the inputs were handed over inside the launch (k_dir_step): write-through loads; y
@@ -2321,8 +2345,10 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     rch[k] = 0;
     rg[k] = 0.0;
   }
-  const bool hw = pa.top_wave != nullptr;  // (uniform) the host's set-up, loaded up front
-  if (rmine && hw) {
+  const bool hs = pa.top_sub != nullptr;  // (uniform) wave subtrees + upper levels
+  const bool hw = hs || pa.top_wave != nullptr;  // (uniform) the host's set-up, loaded up front
+  if (rmine && hs && pre_.w[0] >= 0) {  // a subtree member: its wave sweeps it (rlv = -1)
+  } else if (rmine && hw) {
     rlv = pre_.w[0] & 0xff;
     rnk = (pre_.w[0] >> 8) & 0xff;
 #pragma unroll
@@ -2349,8 +2375,52 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
   const bool reg = hw || (pa.top_reg && nt <= kTopThreads &&
                           __syncthreads_or(rnk > kWaveKids) == 0);
   double rD = rmine ? sD0[rsl] : 1.0, rJ = rmine ? sJ0[rsl] : 0.0, riv = 1.0;
+  // wave subtrees (hs): lane = the subtree's slot (BFS order), the children's values by
+  // shuffles, deepest level first -- the same arithmetic in the same order as the level
+  // sweeps below; D, J (and 1 / D) of every member to LDS for the upper levels and the
+  // back-substitution
+  const int lsl = pre_.ls;
+  const int lvl_l = (pre_.lw[0] >> 6) & 0xff, nk_l = (pre_.lw[0] >> 14) & 0xf;
+  if (hs && pre_.ldep > 0) {
+    int cl[kWaveKids];
+    double cg[kWaveKids];
+#pragma unroll
+    for (int k = 0; k < kWaveKids; ++k) {
+      cl[k] = k < nk_l ? pre_.lw[1 + k] & 63 : (int)(threadIdx.x & 63);
+      cg[k] = k < nk_l ? sG[pre_.lw[1 + k] >> 12] : 0.0;
+    }
+    int kmax = nk_l;
+    for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+    double D = lsl >= 0 ? sD0[lsl] : 1.0, J = lsl >= 0 ? sJ0[lsl] : 0.0, iv = 1.0;
+    for (int q = pre_.ldep - 1; q >= 0; --q) {
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k) {
+        if (k >= kmax) break;
+        const double Jc = __shfl(J, cl[k]);
+        const double Vc = __shfl(dir ? iv : D, cl[k]);
+        if (lvl_l == q && k < nk_l) {
+          const double g = cg[k];
+          if (dir) {
+            D += g * (1.0 - g * Vc);
+            J += g * Jc * Vc;
+          } else {
+            D += g * (1.0 - g / Vc);
+            J += g * Jc / Vc;
+          }
+        }
+      }
+      if (dir && lvl_l == q) iv = 1.0 / D;
+    }
+    if (lsl >= 0) {
+      sD[lsl] = D;
+      sJ[lsl] = J;
+      if (dir) sY[lsl] = iv;
+    }
+  }
+  if (hs) __syncthreads();
+  const int nlr = hs ? pa.top_sub_nup : nl;  // the levels swept block-wide
   if (reg) {
-    for (int lv = nl - 1; lv >= 0; --lv) {
+    for (int lv = nlr - 1; lv >= 0; --lv) {
       if (rlv == lv) {
         double cv[kWaveKids], cj[kWaveKids];
 #pragma unroll
@@ -2425,7 +2495,7 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
     const int p = rmine ? sPar[rsl] : -1;
     const double gp = rmine ? sGp[rsl] : 0.0;
     const int lam = rmine ? sLam[rsl] : 0;
-    for (int lv = 0; lv < nl; ++lv) {
+    for (int lv = 0; lv < nlr; ++lv) {
       if (rlv == lv) {
         const double num = rJ + (p >= 0 ? gp * sJ0[p] : 0.0);
         const double zj = dir ? num * riv : num / rD;
@@ -2433,6 +2503,28 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
         if (!dir) part += sY[rsl] * zj;
       }
       __syncthreads();
+    }
+    if (hs && pre_.ldep > 0) {  // the wave subtrees, root first (a subtree root's parent is
+                                // an upper slot, its value in LDS)
+      const int plane = (pre_.lw[0] >> 18) & 63;
+      const int pq = lsl >= 0 ? sPar[lsl] : -1;
+      const double gq = lsl >= 0 ? sGp[lsl] : 0.0;
+      const double Jq = lsl >= 0 ? sJ[lsl] : 0.0;
+      const double Vq = lsl >= 0 ? (dir ? sY[lsl] : sD[lsl]) : 1.0;
+      double zq = 0.0;
+      for (int q = 0; q < pre_.ldep; ++q) {
+        const double zp = __shfl(zq, plane);
+        if (lvl_l == q && lsl >= 0) {
+          const double zpar = q == 0 ? (pq >= 0 ? sJ0[pq] : 0.0) : zp;
+          const double num = Jq + (pq >= 0 ? gq * zpar : 0.0);
+          zq = dir ? num * Vq : num / Vq;
+        }
+      }
+      if (lsl >= 0) sJ0[lsl] = zq;
+    }
+    if (hs) {
+      __syncthreads();
+      if (!dir && rmine && rlv < 0) part += sY[rsl] * sJ0[rsl];  // (members: after their wave)
     }
     if constexpr (WT) NX_DSTAMP(11);
     // the stores after the levels, not inside their barriers (a workgroup barrier waits for
@@ -3229,7 +3321,8 @@ struct DirStep {
   const int* left_off;    // n_left + 1: post range of every left row
   int n_left;
   double* post;
-  // hand-offs: [0] phase-1 arrivals, [1] phase-2 arrivals, [2] top flag, [3] wait errors
+  // hand-offs: [0] phase-1 arrivals, [1] phase-2 arrivals, [2] top flag, [3] wait errors,
+  // [4] the top solver's job (tagged with the launch) for its helpers
   unsigned* sync;
   unsigned epoch;  // launches since the counters were zero
   unsigned polls;  // s_sleep-paced polls before a waiting workgroup gives up (kDirWaitPolls)
@@ -3239,6 +3332,13 @@ struct DirStep {
   int* seq;
   MrState* mirror;
   double* bbst;
+  // k_dir_step (round 4): per job a kJobHdr-int header, per chain its edge's inputs in chain
+  // order (crec: 10 doubles, ci: 4 ints) and the dynamic LDS split after the stash (doubles:
+  // the phases' shared area, the top values)
+  const int* job_hdr;
+  const double* crec;
+  const int* ci;
+  int lds_main, lds_top;
 };
 
 constexpr int kDirWaitPolls = 1 << 20;  // s_sleep-paced polls before a waiting workgroup gives up
@@ -3566,6 +3666,7 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
       }
     }
   }
+  NX_DSTAMP(32);
   if (lv1 <= lv0) return;
   const int jwave = pa.job_wave ? pa.job_wave[job] : 0;
   int wv0 = 0, wv1 = 0, wv2 = 0;
@@ -3614,6 +3715,7 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
   if (threadIdx.x == 0) sOff[ns] = pa.slot_dc_off[js1] - dc0;
   if ((int)threadIdx.x <= min(lv1 - lv0, kCapLvl)) sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
   __syncthreads();
+  NX_DSTAMP(33);
   bool wave_lv = jwave > 0;
   if (!wave_lv) {
     int nkids = 0;
@@ -3708,6 +3810,7 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
       __syncthreads();
     }
   }
+  NX_DSTAMP(34);
   // back-substitution coefficients (own phase 2 reads them); the job's root level hands its
   // (D, J) to the top part
   const int root1 = sLvl[1];
@@ -3729,215 +3832,6 @@ __device__ __forceinline__ void dir_up_fused(const PcArgs& pa, const DirStep& da
       pa.slot_A[j] = sA_;
       pa.slot_B[j] = sB_;
     }
-  }
-}
-
-// Phase 2: the down sweep (k_pc_down_lds's mode-3 arithmetic with the fused residual, r not
-// stored); sTop: the top part's values by top position.
-// keep: the job's chains in one pass, their lane state (assembled b, cell inputs, cell
-// masses) still in L from phase 1 -- no reloads; sA_ / sB_: this thread's slot coefficients.
-template <int W, int CPL>
-__device__ __forceinline__ void dir_down_fused(const PcArgs& pa, const DirStep& da, double* lds,
-                                               const double* sTop, const DirLane<W, CPL>& L,
-                                               bool keep, double sA_, double sB_) {
-  // (contraction as in k_pc_down_lds: the same x bit for bit)
-  double* sZ = lds;
-  double* sA = sZ + kCapS;
-  double* sB = sA + kCapS;
-  double* sQt = sB + kCapS;
-  double* sQb = sQt + kCapC;
-  int* sP = reinterpret_cast<int*>(sQb + kCapC);
-  int* sLvl = sP + kCapS;
-  __shared__ double s_w[2 * (kPcThreads / 64)];
-  const int job = blockIdx.x;
-  const int ts0 = pa.top_ts0;
-  const int lv0 = pa.job_lvl_off[job], lv1 = pa.job_lvl_off[job + 1];
-  const int js0 = lv1 > lv0 ? pa.lvl_slot_off[lv0] : 0;
-  const int js1 = lv1 > lv0 ? pa.lvl_slot_off[lv1] : 0;
-  const int ns = js1 - js0;
-  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
-  constexpr int G = kPcThreads / W;
-  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
-  double* __restrict__ x = da.x;
-  const double* __restrict__ b = da.rhs;  // this job's own rows (written by this workgroup)
-  ChainLane<W, CPL> ch;
-  double vc[CPL], vq[CPL], vN = 0.0, mo_r[CPL];
-  int ch_up = -1, ch_lo = -1, flip = 0, post_t = -1, post_b = -1;
-  auto load_lane = [&](int c, bool active) {
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) {
-      vc[t] = ch.valid[t] ? b[ch.dof_c[t]] : 0.0;
-      vq[t] = ch.valid[t] ? b[ch.dof_q[t]] : 0.0;
-    }
-    vN = ch.has_last ? b[ch.dof_qN] : 0.0;
-    ch_up = active ? pa.chain_up[c] : -1;
-    ch_lo = active ? pa.chain_lo[c] : -1;
-    flip = active ? pa.chain_flip[c] : 0;
-    post_t = active ? da.chain_post[2 * (int64_t)c] : -1;
-    post_b = active ? da.chain_post[2 * (int64_t)c + 1] : -1;
-  };
-  if (keep) {  // phase 1's lane: only the chain's ends and posts are loaded
-    const int c = c0 + seg;
-    const bool active = c < c1;
-    dir_lane_chain<W, CPL>(pa, L, active, ch);
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) {
-      vc[t] = L.bc[t];
-      vq[t] = L.bq[t];
-      mo_r[t] = L.mo[t];
-    }
-    vN = L.bN;
-    ch_up = active ? pa.chain_up[c] : -1;
-    ch_lo = active ? pa.chain_lo[c] : -1;
-    flip = L.flip;
-    post_t = active ? da.chain_post[2 * (int64_t)c] : -1;
-    post_b = active ? da.chain_post[2 * (int64_t)c + 1] : -1;
-  } else {
-    ch.setup(pa, c0 + seg, c0 + seg < c1);
-    load_lane(c0 + seg, c0 + seg < c1);
-  }
-  int p_par = -1, p_lam = 0, p_lv = -1;
-  const double p_A = sA_, p_B = sB_;  // (ns <= kCapS < kPcThreads: thread = slot)
-  const bool hwave = pa.job_wave != nullptr && lv1 > lv0 && pa.job_wave[job] > 0;
-  if ((int)threadIdx.x < ns) {
-    const int j = js0 + threadIdx.x;
-    p_par = pa.slot_parent[j];
-    p_lam = pa.slot_lam[j];
-    if (hwave) p_lv = pa.slot_wave[3 * (int64_t)j] & 0xff;
-  }
-  // phase A: every slot's A, B, parent (local index, or the parent's value: a top slot)
-  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
-    const int j = js0 + sl;
-    const bool pre = sl == (int)threadIdx.x;
-    const int p = pre ? p_par : pa.slot_parent[j];
-    const bool local = p >= js0 && p < js1;
-    sA[sl] = p_A;
-    sB[sl] = p_B;
-    sP[sl] = local ? p - js0 : -1;
-    sZ[sl] = (!local && p >= 0) ? sTop[p - ts0] : 0.0;
-  }
-  if (lv1 > lv0 && (int)threadIdx.x <= min(lv1 - lv0, kCapLvl))
-    sLvl[threadIdx.x] = pa.lvl_slot_off[lv0 + threadIdx.x];
-  __syncthreads();
-  if (ns <= 64 && lv1 - lv0 <= kCapLvl) {  // one wave: lane = slot, parent by shuffle
-    if (threadIdx.x < 64) {
-      const int sl = threadIdx.x;
-      const bool mine = sl < ns;
-      int mylv = hwave ? p_lv : -1;
-      if (!hwave)
-        for (int q = 0; q < lv1 - lv0; ++q)
-          if (mine && js0 + sl >= sLvl[q] && js0 + sl < sLvl[q + 1]) mylv = q;
-      const double A = mine ? sA[sl] : 0.0, Bv = mine ? sB[sl] : 0.0;
-      const int p = mine ? sP[sl] : -1;
-      double zv = mine ? sZ[sl] : 0.0;
-      for (int q = 0; q < lv1 - lv0; ++q) {
-        const double zp = __shfl(zv, p >= 0 ? p : sl);
-        if (mylv == q) zv = A + Bv * zp;
-      }
-      if (mine) sZ[sl] = zv;
-    }
-    __syncthreads();
-  } else {
-    for (int lv = lv0; lv < lv1; ++lv) {  // root level first
-      const int la = lv - lv0 <= kCapLvl ? sLvl[lv - lv0] : pa.lvl_slot_off[lv];
-      const int lb = lv - lv0 < kCapLvl ? sLvl[lv - lv0 + 1] : pa.lvl_slot_off[lv + 1];
-      for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
-        const int sl = j - js0;
-        const int p = sP[sl];
-        sZ[sl] = sA[sl] + sB[sl] * (p >= 0 ? sZ[p] : sZ[sl]);
-      }
-      __syncthreads();
-    }
-  }
-  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {
-    const bool pre = sl == (int)threadIdx.x;
-    x[pre ? p_lam : pa.slot_lam[js0 + sl]] = sZ[sl];
-  }
-  double rr = 0.0, bb = 0.0;
-  for (int cb = c0; cb < c1; cb += G) {
-    const int c = cb + seg;
-    const bool active = c < c1;
-    if (cb != c0) {  // more chains than one pass: set up and load here
-      ch.setup(pa, c, active);
-      load_lane(c, active);
-    }
-    if (!keep) chain_cell_mo<W, CPL>(pa, ch, c, active, flip, mo_r);
-    const int up = ch_up, lo = ch_lo;
-    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : sTop[up - ts0];
-    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : sTop[lo - ts0];
-    const double T = ch.T, iT = 1.0 / T;
-    double bcv[CPL], a[CPL], bs[CPL], zc[CPL];
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) bcv[t] = vc[t];
-    {
-      double ytop, ybot;
-      direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
-    }
-    double sa = 0.0, sb = 0.0;
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) {
-      a[t] = (T - ch.D[t]) * vc[t];
-      bs[t] = ch.D[t] * vc[t];
-      sa += a[t];
-      sb += bs[t];
-    }
-    const double ia = seg_incl_scan<W>(sa), ibv = seg_incl_scan<W>(sb);
-    const double Atot = seg_sum<W>(sa);
-    double pa_ = ia - sa, pb_ = ibv - sb;
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) {
-      pa_ += a[t];
-      const double suffix = Atot - pa_ + a[t];
-      const double prefix = pb_;
-      pb_ += bs[t];
-      zc[t] = 0.0;
-      if (!ch.valid[t]) continue;
-      const double Dk = ch.D[t];
-      double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
-      zk -= ch.mo * vc[t];  // the consistent-mass Schur complement
-      zc[t] = zk;
-      x[ch.dof_c[t]] = zk;
-    }
-    double xv[CPL + 1];
-    direct_flux_cons<W, CPL>(ch, flip, bcv, vq, vN, zt, zb, xv);
-#pragma unroll
-    for (int t = 0; t <= CPL; ++t) {
-      const bool on = t < CPL ? ch.valid[t] : ch.has_last;
-      if (on) x[t < CPL ? ch.dof_q[t] : ch.dof_qN] = xv[t];
-    }
-    direct_residual<W, CPL, false>(pa, ch, active, flip, bcv, vq, vN, zc, xv, zt, zb, mo_r, rr, bb,
-                                   sQt, sQb, c - c0);
-    // the chain's ends at rows no job forms: their flux shares, write-through
-    if (active && l == 0 && post_t >= 0) st_wt(da.post + post_t, sQt[c - c0]);
-    if (ch.has_last && post_b >= 0) st_wt(da.post + post_b, sQb[c - c0]);
-  }
-  __syncthreads();
-  // multiplier rows of the junctions whose chains are all in this job (b_lambda = 0)
-  if ((int)threadIdx.x < ns) {
-    const int j = js0 + threadIdx.x;
-    if (pa.slot_rloc[j]) {
-      const int pc = pa.slot_pchain[j];
-      double acc = pc >= 0 ? sQb[pc - c0] : 0.0;
-      for (int i = pa.slot_dc_off[j]; i < pa.slot_dc_off[j + 1]; ++i) acc += sQt[pa.slot_dc[i] - c0];
-      const double rl = 0.0 - acc;
-      rr += rl * rl;
-    }
-  }
-  rr = wave_sum(rr);
-  bb = wave_sum(bb);
-  if ((threadIdx.x & 63) == 0) {
-    s_w[threadIdx.x >> 6] = rr;
-    s_w[kPcThreads / 64 + (threadIdx.x >> 6)] = bb;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double tr = s_w[0], tb = s_w[kPcThreads / 64];
-    for (int i = 1; i < kPcThreads / 64; ++i) {
-      tr += s_w[i];
-      tb += s_w[kPcThreads / 64 + i];
-    }
-    st_wt(pa.rpart + job, tr);
-    st_wt(pa.rpart + pa.n_jobs + job, tb);
   }
 }
 
@@ -4028,26 +3922,708 @@ __device__ __forceinline__ void dir_stores_all(const PcArgs& pa, const DirStep& 
   }
 }
 
+// ---- k_dir_step's job description (round 4) ------------------------------------------
+// A workgroup of the fused step used to reach its first arithmetic through four dependent
+// rounds of global loads (job offsets -> level offsets -> chains -> their edges) and loaded
+// its static slot / chain data again after each hand-off. Now: per job a kJobHdr-int header
+// (host-built: c0, c1, lv0, lv1, js0, js1, dc0, dc1, jwave, root1), per chain its edge's
+// inputs in chain order (crec: x_u[3], x_v[3], R, f, b(q_0), b(q_N); ci: edge, flip | s << 1,
+// CSR segment start, length; refreshed whenever the coefficients change), and every static
+// array the job's phases read staged in LDS once (the stash) -- two dependent rounds (the
+// header; then the stash and the chain records, issued together) before the workgroup
+// computes, and none after the hand-offs except the handed-over values themselves.
+constexpr int kJobHdr = 16;
+
+struct ChainRec {
+  double x0[3], x1[3], R, fe, bc0, bc1;
+  int e, flip, s, sg0, seglen;
+};
+
+__device__ __forceinline__ void chain_rec_load(const DirStep& da, int c, bool active,
+                                               ChainRec& r) {
+  const int cc = active ? c : 0;
+  const double* p = da.crec + 10 * (int64_t)cc;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    r.x0[i] = p[i];
+    r.x1[i] = p[3 + i];
+  }
+  r.R = p[6];
+  r.fe = p[7];
+  r.bc0 = p[8];
+  r.bc1 = p[9];
+  const int4 q = *reinterpret_cast<const int4*>(da.ci + 4 * (int64_t)cc);
+  r.e = active ? q.x : 0;
+  r.flip = active ? (q.y & 1) : 0;
+  r.s = q.y >> 1;
+  r.sg0 = q.z;
+  r.seglen = q.w;
+}
+
+// dir_chain_asm from a chain record (the same arithmetic, the same bits)
+template <int W, int CPL>
+__device__ __forceinline__ void dir_chain_asm_rec(const PcArgs& pa, const ChainRec& r, bool active,
+                                                  DirLane<W, CPL>& L) {
+#pragma clang fp contract(off)
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const int flip = r.flip;
+  L.e = r.e;
+  L.flip = flip;
+  L.s = r.s;
+  L.sg0 = r.sg0;
+  L.seglen = r.seglen;
+  const double invN = 1.0 / (double)N;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    const int k = l * CPL + t;
+    const bool valid = active && k < N;
+    const int kp = flip ? N - 1 - k : k;
+    const int qp = flip ? N - k : k;
+    L.md[t] = 0.0;
+    L.mo[t] = 0.0;
+    L.bc[t] = 0.0;
+    L.bq[t] = 0.0;
+    if (valid) {
+      double va[3], vb[3];
+      vertex(r.x0, r.x1, kp, N, invN, va);
+      vertex(r.x0, r.x1, kp + 1, N, invN, vb);
+      const double d0 = vb[0] - va[0], d1 = vb[1] - va[1], d2 = vb[2] - va[2];
+      const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+      L.md[t] = r.R * h / 3.0;
+      L.mo[t] = r.R * h / 6.0;
+      L.bc[t] = -(r.fe * h);  // negated pressure row: -(f h)
+      L.bq[t] = qp == 0 ? r.bc0 : (qp == N ? r.bc1 : 0.0);
+    }
+  }
+  L.bN = (active && l == (N - 1) / CPL) ? (flip ? r.bc0 : r.bc1) : 0.0;
+}
+
+// The job's static arrays in LDS at the start of the dynamic LDS (ints, fixed offsets, so
+// the stash costs no registers): level slot offsets (absolute slot ids), per slot its parent
+// chain, parent slot, multiplier row, own-row flag (slot_rloc), one-wave set-up (3) and
+// down-chain offsets (absolute), per down-chain entry its chain and lower slot, per chain of
+// the first pass its end slots and post slots. The host checks the job sizes against the caps.
+constexpr int kStLv = 256, kStNs = kCapS, kStNd = kCapDC, kStNc = 256;
+constexpr int kOffLv = 0, kOffPc = kOffLv + kStLv, kOffPar = kOffPc + kStNs,
+              kOffLam = kOffPar + kStNs, kOffRl = kOffLam + kStNs, kOffW0 = kOffRl + kStNs,
+              kOffW1 = kOffW0 + kStNs, kOffW2 = kOffW1 + kStNs, kOffDco = kOffW2 + kStNs,
+              kOffSdc = kOffDco + kStNs + 8, kOffDlo = kOffSdc + kStNd, kOffCup = kOffDlo + kStNd,
+              kOffClo = kOffCup + kStNc, kOffCpt = kOffClo + kStNc, kOffCpb = kOffCpt + kStNc,
+              kStashInts = kOffCpb + kStNc;
+constexpr int kStashDbl = (kStashInts + 1) / 2;
+
+struct JobStash {
+  int c0, c1, lv0, lv1, js0, js1, dc0, dc1, jwave, root1;
+  int* base;
+  __device__ __forceinline__ int& lv(int i) const { return base[kOffLv + i]; }
+  __device__ __forceinline__ int& pchain(int i) const { return base[kOffPc + i]; }
+  __device__ __forceinline__ int& par(int i) const { return base[kOffPar + i]; }
+  __device__ __forceinline__ int& lam(int i) const { return base[kOffLam + i]; }
+  __device__ __forceinline__ int& rloc(int i) const { return base[kOffRl + i]; }
+  __device__ __forceinline__ int& w0(int i) const { return base[kOffW0 + i]; }
+  __device__ __forceinline__ int& w1(int i) const { return base[kOffW1 + i]; }
+  __device__ __forceinline__ int& w2(int i) const { return base[kOffW2 + i]; }
+  __device__ __forceinline__ int& dcoff(int i) const { return base[kOffDco + i]; }
+  __device__ __forceinline__ int& sdc(int i) const { return base[kOffSdc + i]; }
+  __device__ __forceinline__ int& dlo(int i) const { return base[kOffDlo + i]; }
+  __device__ __forceinline__ int& cup(int i) const { return base[kOffCup + i]; }
+  __device__ __forceinline__ int& clo(int i) const { return base[kOffClo + i]; }
+  __device__ __forceinline__ int& cpt(int i) const { return base[kOffCpt + i]; }
+  __device__ __forceinline__ int& cpb(int i) const { return base[kOffCpb + i]; }
+};
+
+// this thread's share of the stash, loaded (job_stash_load) before the caller issues its
+// chain records, written to LDS after (job_stash_store): the loads fly together
+struct StashRegs {
+  int lv, pc, par, lam, rl, w0, w1, w2, off, sdc, dlo, cu, cl, pt, pb;
+};
+
+template <int W>
+__device__ __forceinline__ void job_stash_load(const PcArgs& pa, const DirStep& da, int job,
+                                               int* base, JobStash& S, StashRegs& R) {
+  const int4* hd = reinterpret_cast<const int4*>(da.job_hdr + kJobHdr * (int64_t)job);
+  const int4 h0 = hd[0], h1 = hd[1], h2 = hd[2];
+  S.c0 = h0.x;
+  S.c1 = h0.y;
+  S.lv0 = h0.z;
+  S.lv1 = h0.w;
+  S.js0 = h1.x;
+  S.js1 = h1.y;
+  S.dc0 = h1.z;
+  S.dc1 = h1.w;
+  S.jwave = h2.x;
+  S.root1 = h2.y;
+  S.base = base;
+  const int t = threadIdx.x;
+  const int nlv = S.lv1 - S.lv0, ns = S.js1 - S.js0, nd = S.dc1 - S.dc0;
+  const int nc = min(S.c1 - S.c0, kPcThreads / W);
+  const int j = S.js0 + t, c = S.c0 + t, i = S.dc0 + t;
+  const bool sl = t < ns, wv = sl && S.jwave > 0;
+  R.lv = t <= nlv ? pa.lvl_slot_off[S.lv0 + t] : 0;
+  R.pc = sl ? pa.slot_pchain[j] : -1;
+  R.par = sl ? pa.slot_parent[j] : -1;
+  R.lam = sl ? pa.slot_lam[j] : 0;
+  R.rl = sl ? pa.slot_rloc[j] : 0;
+  R.w0 = wv ? pa.slot_wave[3 * (int64_t)j] : 0;
+  R.w1 = wv ? pa.slot_wave[3 * (int64_t)j + 1] : 0;
+  R.w2 = wv ? pa.slot_wave[3 * (int64_t)j + 2] : 0;
+  R.off = t <= ns ? pa.slot_dc_off[j] : 0;
+  R.sdc = t < nd ? pa.slot_dc[i] : 0;
+  R.dlo = t < nd ? pa.dc_lo[i] : -1;
+  const bool ch = t < nc;
+  R.cu = ch ? pa.chain_up[c] : -1;
+  R.cl = ch ? pa.chain_lo[c] : -1;
+  R.pt = ch && da.chain_post ? da.chain_post[2 * (int64_t)c] : -1;
+  R.pb = ch && da.chain_post ? da.chain_post[2 * (int64_t)c + 1] : -1;
+}
+
+__device__ __forceinline__ void job_stash_store(const JobStash& S, const StashRegs& R, int nc) {
+  const int t = threadIdx.x;
+  const int nlv = S.lv1 - S.lv0, ns = S.js1 - S.js0, nd = S.dc1 - S.dc0;
+  if (t <= nlv) S.lv(t) = R.lv;
+  if (t < ns) {
+    S.pchain(t) = R.pc;
+    S.par(t) = R.par;
+    S.lam(t) = R.lam;
+    S.rloc(t) = R.rl;
+    S.w0(t) = R.w0;
+    S.w1(t) = R.w1;
+    S.w2(t) = R.w2;
+  }
+  if (t <= ns) S.dcoff(t) = R.off;
+  if (t < nd) {
+    S.sdc(t) = R.sdc;
+    S.dlo(t) = R.dlo;
+  }
+  if (t < nc) {
+    S.cup(t) = R.cu;
+    S.clo(t) = R.cl;
+    S.cpt(t) = R.pt;
+    S.cpb(t) = R.pb;
+  }
+}
+
+// Phase 1 from the stash (dir_up_fused's arithmetic, the same bits): the chains' edges
+// assembled in registers from their records (rec: the first pass's, loaded by the caller),
+// the up sweep, the top part's inputs posted write-through; sA_ / sB_ the slot's
+// back-substitution coefficients (thread = slot). MULTI: every chain's T / It / Ib and
+// every slot's D / J / A / B also to global memory, as k_pc_up_lds stores them.
+template <int W, int CPL, bool MULTI = false>
+__device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, double* lds,
+                                          const JobStash& S, ChainRec& rec, DirLane<W, CPL>& L,
+                                          double& sA_, double& sB_) {
+  double* sT = lds;
+  double* sIt = sT + kCapC;
+  double* sIb = sIt + kCapC;
+  double* sD0 = sIb + kCapC;
+  double* sJ0 = sD0 + kCapS;
+  double* sD = sJ0 + kCapS;
+  double* sJ = sD + kCapS;
+  double* sIv = sJ + kCapS;
+  double* sG = sIv + kCapS;
+  int* sChild = reinterpret_cast<int*>(sG + kCapDC);
+  int* sOff = sChild + kCapDC;
+  const int c0 = S.c0, c1 = S.c1;
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  const int ts0 = pa.top_ts0, ts1 = pa.top_ts0 + pa.top_nt;
+  const int lv0 = S.lv0, lv1 = S.lv1;
+  const int js0 = S.js0, js1 = S.js1;
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    if (cb != c0) chain_rec_load(da, c, active, rec);
+    const int cu = !active ? -1 : (cb == c0 ? S.cup(seg) : pa.chain_up[c]);
+    const int clo = !active ? -1 : (cb == c0 ? S.clo(seg) : pa.chain_lo[c]);
+    dir_chain_asm_rec<W, CPL>(pa, rec, active, L);
+    ChainLane<W, CPL> ch;
+    dir_lane_chain<W, CPL>(pa, L, active, ch);
+    double vc[CPL];
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) vc[t] = L.bc[t];
+    double ytop = 0.0, ybot = 0.0;
+    direct_cell_inputs<W, CPL>(pa, ch, L.flip, L.bq, L.bN, vc, ytop, ybot);
+    double sr = 0.0, srd = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      if (!ch.valid[t]) continue;
+      sr += vc[t];
+      srd += vc[t] * ch.D[t];
+    }
+    sr = seg_sum<W>(sr);
+    srd = seg_sum<W>(srd);
+    if (active && l == 0) {
+      const double ib = srd / ch.T;
+      const double it = (sr - ib) + ytop, ibe = ib + ybot;  // + the multiplier rows' share
+      sT[c - c0] = ch.T;
+      sIb[c - c0] = ibe;
+      sIt[c - c0] = it;
+      if ((cu >= ts0 && cu < ts1) || (clo >= ts0 && clo < ts1)) {  // the top part reads it
+        st_wt(pa.chain_T + c, ch.T);
+        st_wt(pa.chain_It + c, it);
+        st_wt(pa.chain_Ib + c, ibe);
+      } else if (MULTI) {
+        pa.chain_T[c] = ch.T;
+        pa.chain_It[c] = it;
+        pa.chain_Ib[c] = ibe;
+      }
+    }
+  }
+  NX_DSTAMP(32);
+  if (lv1 <= lv0) return;
+  const int jwave = S.jwave;
+  const int ns = js1 - js0;
+  const int dc0 = S.dc0;
+  __syncthreads();
+  NX_DSTAMP(33);
+  for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {  // phase A (ns <= kCapS: one pass)
+    const int pcn = S.pchain(sl);
+    double D0 = pcn >= 0 ? 1.0 / sT[pcn - c0] : 0.0;
+    double J0 = pcn >= 0 ? sIb[pcn - c0] : 0.0;  // (- b_lambda = -0 added: no change)
+    const int o0 = S.dcoff(sl), o1 = S.dcoff(sl + 1);
+    sOff[sl] = o0 - dc0;
+    for (int i = o0; i < o1; ++i) {
+      const int cl = S.sdc(i - dc0) - c0;
+      const int lo = S.dlo(i - dc0);
+      const double g = 1.0 / sT[cl];
+      J0 += sIt[cl];
+      if (lo >= 0) {
+        sChild[i - dc0] = lo - js0;
+        sG[i - dc0] = g;
+      } else {
+        sChild[i - dc0] = -1;
+        D0 += g;
+      }
+    }
+    sD0[sl] = D0;
+    sJ0[sl] = J0;
+  }
+  if (threadIdx.x == 0) sOff[ns] = S.dc1 - dc0;
+  __syncthreads();
+  bool wave_lv = jwave > 0;
+  if (!wave_lv) {
+    int nkids = 0;
+    if ((int)threadIdx.x < ns)
+      for (int i = sOff[threadIdx.x]; i < sOff[threadIdx.x + 1]; ++i) nkids += sChild[i] >= 0;
+    wave_lv = __syncthreads_or(nkids > kWaveKids) == 0 && ns <= 64 && lv1 - lv0 <= kCapLvl;
+  }
+  if (wave_lv) {  // one wave: lane = slot, the children's values by shuffles
+    if (threadIdx.x < 64) {
+      const int sl = threadIdx.x;
+      const bool mine = sl < ns;
+      int mylv = -1;
+      int cl[kWaveKids];
+      double cg[kWaveKids];
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k) {
+        cl[k] = sl;
+        cg[k] = 0.0;
+      }
+      int nk = 0, kmax;
+      if (jwave > 0) {
+        kmax = jwave - 1;
+        if (mine) {
+          const int wv0 = S.w0(sl), wv1 = S.w1(sl), wv2 = S.w2(sl);
+          mylv = wv0 & 0xff;
+          nk = (wv0 >> 8) & 0xff;
+          const int cw[kWaveKids] = {wv1 & 0xffff, wv1 >> 16, wv2 & 0xffff, wv2 >> 16};
+#pragma unroll
+          for (int k = 0; k < kWaveKids; ++k)
+            if (k < nk) {
+              cl[k] = cw[k] & 63;
+              cg[k] = sG[cw[k] >> 6];
+            }
+        }
+      } else {
+        for (int q = 0; q < lv1 - lv0; ++q)
+          if (mine && js0 + sl >= S.lv(q) && js0 + sl < S.lv(q + 1)) mylv = q;
+        if (mine)
+          for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+            const int chd = sChild[i];
+            if (chd < 0) continue;
+#pragma unroll
+            for (int k = 0; k < kWaveKids; ++k)
+              if (k == nk) {
+                cl[k] = chd;
+                cg[k] = sG[i];
+              }
+            ++nk;
+          }
+        kmax = nk;
+        for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+      }
+      double D = mine ? sD0[sl] : 1.0, J = mine ? sJ0[sl] : 0.0, iv = 1.0;
+      for (int q = lv1 - lv0 - 1; q >= 0; --q) {
+#pragma unroll
+        for (int k = 0; k < kWaveKids; ++k) {
+          if (k >= kmax) break;
+          const double Jc = __shfl(J, cl[k]);
+          const double Dc = __shfl(iv, cl[k]);
+          if (mylv == q && k < nk) {
+            const double g = cg[k];
+            D += g * (1.0 - g * Dc);
+            J += g * Jc * Dc;
+          }
+        }
+        if (mylv == q) iv = 1.0 / D;
+      }
+      if (mine) {
+        sD[sl] = D;
+        sJ[sl] = J;
+        sIv[sl] = iv;
+      }
+    }
+    __syncthreads();
+  } else {
+    for (int lv = lv1 - 1; lv >= lv0; --lv) {  // deepest level first
+      const int la = S.lv(lv - lv0), lb = S.lv(lv - lv0 + 1);
+      for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
+        const int sl = j - js0;
+        double D = sD0[sl], J = sJ0[sl];
+        for (int i = sOff[sl]; i < sOff[sl + 1]; ++i) {
+          const int ch = sChild[i];
+          if (ch < 0) continue;
+          const double g = sG[i], iv = sIv[ch];
+          D += g * (1.0 - g * iv);
+          J += g * sJ[ch] * iv;
+        }
+        sIv[sl] = 1.0 / D;
+        sD[sl] = D;
+        sJ[sl] = J;
+      }
+      __syncthreads();
+    }
+  }
+  NX_DSTAMP(34);
+  // back-substitution coefficients (own phase 2 reads them); the job's root level hands its
+  // (D, J) to the top part
+  const int root1 = S.root1;
+  if ((int)threadIdx.x < ns) {  // ns <= kCapS < kPcThreads: thread = slot
+    const int sl = threadIdx.x;
+    const int j = js0 + sl;
+    const int pcn = S.pchain(sl);
+    const double J = sJ[sl], iv = sIv[sl];
+    sA_ = J * iv;
+    sB_ = pcn >= 0 ? iv / sT[pcn - c0] : 0.0;
+    if (j < root1) {
+      st_wt(pa.slot_D + j, sD[sl]);
+      st_wt(pa.slot_J + j, J);
+    } else if (MULTI) {
+      pa.slot_D[j] = sD[sl];
+      pa.slot_J[j] = J;
+    }
+    if (MULTI) {
+      pa.slot_A[j] = sA_;
+      pa.slot_B[j] = sB_;
+    }
+  }
+}
+
+// Phase 2 from the stash (k_pc_down_lds's mode-3 arithmetic with the fused residual, r not
+// stored): sTop the top part's values by top position; keep: the job's chains in one pass,
+// their lane state still in L from phase 1; sA_ / sB_: this thread's slot coefficients.
+template <int W, int CPL>
+__device__ __forceinline__ void dir_down_v2(const PcArgs& pa, const DirStep& da, double* lds,
+                                            const double* sTop, const JobStash& S,
+                                            const DirLane<W, CPL>& L, bool keep, double sA_,
+                                            double sB_) {
+  // (contraction as in k_pc_down_lds: the same x bit for bit)
+  double* sZ = lds;
+  double* sA = sZ + kCapS;
+  double* sB = sA + kCapS;
+  double* sQt = sB + kCapS;
+  double* sQb = sQt + kCapC;
+  int* sP = reinterpret_cast<int*>(sQb + kCapC);
+  __shared__ double s_w[2 * (kPcThreads / 64)];
+  const int job = blockIdx.x;
+  const int ts0 = pa.top_ts0;
+  const int lv0 = S.lv0, lv1 = S.lv1;
+  const int js0 = S.js0, js1 = S.js1;
+  const int ns = js1 - js0;
+  const int c0 = S.c0, c1 = S.c1;
+  constexpr int G = kPcThreads / W;
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  double* __restrict__ x = da.x;
+  const double* __restrict__ b = da.rhs;  // this job's own rows (written by this workgroup)
+  ChainLane<W, CPL> ch;
+  double vc[CPL], vq[CPL], vN = 0.0, mo_r[CPL];
+  int ch_up = -1, ch_lo = -1, flip = 0, post_t = -1, post_b = -1;
+  auto load_lane = [&](int c, bool active) {
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      vc[t] = ch.valid[t] ? b[ch.dof_c[t]] : 0.0;
+      vq[t] = ch.valid[t] ? b[ch.dof_q[t]] : 0.0;
+    }
+    vN = ch.has_last ? b[ch.dof_qN] : 0.0;
+    ch_up = active ? pa.chain_up[c] : -1;
+    ch_lo = active ? pa.chain_lo[c] : -1;
+    flip = active ? pa.chain_flip[c] : 0;
+    post_t = active ? da.chain_post[2 * (int64_t)c] : -1;
+    post_b = active ? da.chain_post[2 * (int64_t)c + 1] : -1;
+  };
+  if (keep) {  // phase 1's lane; the chain's ends and posts from the stash
+    const bool active = c0 + seg < c1;
+    dir_lane_chain<W, CPL>(pa, L, active, ch);
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      vc[t] = L.bc[t];
+      vq[t] = L.bq[t];
+      mo_r[t] = L.mo[t];
+    }
+    vN = L.bN;
+    ch_up = active ? S.cup(seg) : -1;
+    ch_lo = active ? S.clo(seg) : -1;
+    flip = L.flip;
+    post_t = active ? S.cpt(seg) : -1;
+    post_b = active ? S.cpb(seg) : -1;
+  } else {
+    ch.setup(pa, c0 + seg, c0 + seg < c1);
+    load_lane(c0 + seg, c0 + seg < c1);
+  }
+  const bool hwave = S.jwave > 0 && lv1 > lv0;
+  // phase A: every slot's A, B, parent (local index, or the parent's value: a top slot)
+  if ((int)threadIdx.x < ns) {  // (ns <= kCapS < kPcThreads: thread = slot)
+    const int sl = threadIdx.x;
+    const int p = S.par(sl);
+    const bool local = p >= js0 && p < js1;
+    sA[sl] = sA_;
+    sB[sl] = sB_;
+    sP[sl] = local ? p - js0 : -1;
+    sZ[sl] = (!local && p >= 0) ? sTop[p - ts0] : 0.0;
+  }
+  __syncthreads();
+  NX_DSTAMP(36);
+  if (ns <= 64 && lv1 - lv0 <= kCapLvl) {  // one wave: lane = slot, parent by shuffle
+    if (threadIdx.x < 64) {
+      const int sl = threadIdx.x;
+      const bool mine = sl < ns;
+      int mylv = hwave && mine ? S.w0(sl) & 0xff : -1;
+      if (!hwave)
+        for (int q = 0; q < lv1 - lv0; ++q)
+          if (mine && js0 + sl >= S.lv(q) && js0 + sl < S.lv(q + 1)) mylv = q;
+      const double A = mine ? sA[sl] : 0.0, Bv = mine ? sB[sl] : 0.0;
+      const int p = mine ? sP[sl] : -1;
+      double zv = mine ? sZ[sl] : 0.0;
+      for (int q = 0; q < lv1 - lv0; ++q) {
+        const double zp = __shfl(zv, p >= 0 ? p : sl);
+        if (mylv == q) zv = A + Bv * zp;
+      }
+      if (mine) sZ[sl] = zv;
+    }
+    __syncthreads();
+  } else {
+    for (int lv = lv0; lv < lv1; ++lv) {  // root level first
+      const int la = S.lv(lv - lv0), lb = S.lv(lv - lv0 + 1);
+      for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
+        const int sl = j - js0;
+        const int p = sP[sl];
+        sZ[sl] = sA[sl] + sB[sl] * (p >= 0 ? sZ[p] : sZ[sl]);
+      }
+      __syncthreads();
+    }
+  }
+  NX_DSTAMP(37);
+  if ((int)threadIdx.x < ns) x[S.lam(threadIdx.x)] = sZ[threadIdx.x];
+  double rr = 0.0, bb = 0.0;
+  for (int cb = c0; cb < c1; cb += G) {
+    const int c = cb + seg;
+    const bool active = c < c1;
+    if (cb != c0) {  // more chains than one pass: set up and load here
+      ch.setup(pa, c, active);
+      load_lane(c, active);
+    }
+    if (!keep) chain_cell_mo<W, CPL>(pa, ch, c, active, flip, mo_r);
+    const int up = ch_up, lo = ch_lo;
+    const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : sTop[up - ts0];
+    const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : sTop[lo - ts0];
+    const double T = ch.T, iT = 1.0 / T;
+    double bcv[CPL], a[CPL], bs[CPL], zc[CPL];
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) bcv[t] = vc[t];
+    {
+      double ytop, ybot;
+      direct_cell_inputs<W, CPL>(pa, ch, flip, vq, vN, vc, ytop, ybot);
+    }
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      a[t] = (T - ch.D[t]) * vc[t];
+      bs[t] = ch.D[t] * vc[t];
+      sa += a[t];
+      sb += bs[t];
+    }
+    const double ia = seg_incl_scan<W>(sa), ibv = seg_incl_scan<W>(sb);
+    const double Atot = seg_sum<W>(sa);
+    double pa_ = ia - sa, pb_ = ibv - sb;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      pa_ += a[t];
+      const double suffix = Atot - pa_ + a[t];
+      const double prefix = pb_;
+      pb_ += bs[t];
+      zc[t] = 0.0;
+      if (!ch.valid[t]) continue;
+      const double Dk = ch.D[t];
+      double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
+      zk -= ch.mo * vc[t];  // the consistent-mass Schur complement
+      zc[t] = zk;
+      x[ch.dof_c[t]] = zk;
+    }
+    double xv[CPL + 1];
+    direct_flux_cons<W, CPL>(ch, flip, bcv, vq, vN, zt, zb, xv);
+#pragma unroll
+    for (int t = 0; t <= CPL; ++t) {
+      const bool on = t < CPL ? ch.valid[t] : ch.has_last;
+      if (on) x[t < CPL ? ch.dof_q[t] : ch.dof_qN] = xv[t];
+    }
+    direct_residual<W, CPL, false>(pa, ch, active, flip, bcv, vq, vN, zc, xv, zt, zb, mo_r, rr, bb,
+                                   sQt, sQb, c - c0);
+    // the chain's ends at rows no job forms: their flux shares, write-through
+    if (active && l == 0 && post_t >= 0) st_wt(da.post + post_t, sQt[c - c0]);
+    if (ch.has_last && post_b >= 0) st_wt(da.post + post_b, sQb[c - c0]);
+  }
+  __syncthreads();
+  NX_DSTAMP(38);
+  // multiplier rows of the junctions whose chains are all in this job (b_lambda = 0)
+  if ((int)threadIdx.x < ns && S.rloc(threadIdx.x)) {
+    const int sl = threadIdx.x;
+    const int pc = S.pchain(sl);
+    double acc = pc >= 0 ? sQb[pc - c0] : 0.0;
+    for (int i = S.dcoff(sl); i < S.dcoff(sl + 1); ++i) acc += sQt[S.sdc(i - S.dc0) - c0];
+    const double rl = 0.0 - acc;
+    rr += rl * rl;
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_w[threadIdx.x >> 6] = rr;
+    s_w[kPcThreads / 64 + (threadIdx.x >> 6)] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tr = s_w[0], tb = s_w[kPcThreads / 64];
+    for (int i = 1; i < kPcThreads / 64; ++i) {
+      tr += s_w[i];
+      tb += s_w[kPcThreads / 64 + i];
+    }
+    st_wt(pa.rpart + job, tr);
+    st_wt(pa.rpart + pa.n_jobs + job, tb);
+  }
+}
+
+// The assembly's stores of one workgroup: a share of job jb's multiplier rows (+-1 values,
+// zero rhs: indices jb * kPcThreads + k, k < kPcThreads, then every nj * kPcThreads), then jb's
+// chains [cs, ce) -- from the kept lanes (keep: this workgroup's own single pass, chain cs +
+// group) or re-assembled from their records (chain cb + group - g0 per pass). Only the lane
+// groups [g0, g1) store (the others -- whole waves -- stay free of outstanding stores, so their
+// polls and loads are not queued behind them).
+template <int W, int CPL, bool UNIT = false>
+__device__ __forceinline__ void dir_stores_v2(const PcArgs& pa, const DirStep& da, int jb, bool lm,
+                                              int cs, int ce, bool keep, DirLane<W, CPL>& L,
+                                              int g0 = 0, int g1 = kPcThreads / W) {
+  const int nj = pa.n_jobs;
+  const int grp = (int)threadIdx.x / W;
+  const bool mine = grp >= g0 && grp < g1;
+  if (lm && mine) {
+    const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
+    const int nthr = (g1 - g0) * W;
+    for (int k = (int)threadIdx.x - g0 * W; k < kPcThreads; k += nthr)
+      for (int64_t i = (int64_t)jb * kPcThreads + k; i < nlm; i += (int64_t)nj * kPcThreads) {
+        if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
+        if (i < da.B) da.rhs_lm[i] = 0.0;
+      }
+  }
+  if (keep) {
+    if (mine) dir_chain_store<W, CPL, UNIT>(pa, da, cs + grp < ce, L);
+    return;
+  }
+  const int per = g1 - g0;
+  for (int cb = cs; cb < ce; cb += per) {
+    const int c = cb + grp - g0;
+    if (mine) {
+      ChainRec r;
+      chain_rec_load(da, c, c < ce, r);
+      dir_chain_asm_rec<W, CPL>(pa, r, c < ce, L);
+      dir_chain_store<W, CPL, UNIT>(pa, da, c < ce, L);
+    }
+  }
+}
+
+// k_dir_step's waiting workgroups leave the stores of their first kDirFreeWaves waves until
+// after phase 2: those waves poll for the top values and load them without waiting for the
+// drain of the others' stores. The top solver's assembly is stored by the first workgroups to
+// arrive (helpers), one chain per wave on the other waves: kDirHelpChains chains each.
+constexpr int kDirFreeWaves = 4;
+constexpr int kDirHelpChains = kPcThreads / 64 - kDirFreeWaves;
+// dynamic LDS of k_dir_step: at most this (the static __shared__ words -- flags, the partial
+// sums of phase 2 and the publish -- take the rest of the CU's 160 KiB)
+constexpr int kDirLdsMax = 160 * 1024 - 2048;
+
+// The chain records of k_dir_step (crec / ci) from the edge arrays: run when the
+// decomposition or the coefficients (R, f, boundary values) change, not per step.
+__global__ __launch_bounds__(256) void k_chain_rec(const int* __restrict__ chain_edge,
+                                                   const int* __restrict__ chain_flip, int64_t nc,
+                                                   const double* __restrict__ edge_x,
+                                                   const double* __restrict__ edge_R,
+                                                   const double* __restrict__ edge_f, double f,
+                                                   const double* __restrict__ edge_bc,
+                                                   const int* __restrict__ edge_lm,
+                                                   const int* __restrict__ edge_seg,
+                                                   double* __restrict__ crec, int* __restrict__ ci) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const int e = chain_edge[c];
+  double* r = crec + 10 * c;
+  for (int i = 0; i < 6; ++i) r[i] = edge_x[6 * (int64_t)e + i];
+  r[6] = edge_R[e];
+  r[7] = edge_f ? edge_f[e] : f;
+  r[8] = edge_bc[2 * (int64_t)e];
+  r[9] = edge_bc[2 * (int64_t)e + 1];
+  ci[4 * c] = e;
+  ci[4 * c + 1] = (chain_flip[c] & 1) | ((edge_lm[2 * (int64_t)e] >= 0 ? 1 : 0) << 1);
+  ci[4 * c + 2] = edge_seg[e];
+  ci[4 * c + 3] = edge_seg[e + 1] - edge_seg[e];
+}
+
 template <int W, int CPL>
 __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) {
-  __shared__ double smem[kDirLds];
-  __shared__ int sFlag;
+  extern __shared__ double dsm[];
+  __shared__ int sFlag, sTopJob, sIdx;
+  int* stash = reinterpret_cast<int*>(dsm);  // the job's statics (fixed offsets)
+  double* smem = dsm + kStashDbl;            // phase 1 / the top part / phase 2
+  double* sTop = smem + da.lds_main;         // the top part's values (phase 2 reads them)
   const int job = blockIdx.x;
   const int nj = pa.n_jobs;
   const unsigned last = da.epoch * (unsigned)nj + (unsigned)(nj - 1);
+  const unsigned tag = (da.epoch + 1u) << 10;  // the top solver's announcement (job < 1024)
+  constexpr int G = kPcThreads / W;
   NX_DSTAMP(0);
-  const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
+  JobStash S;
+  ChainRec rec;
+  {
+    StashRegs R;
+    job_stash_load<W>(pa, da, job, stash, S, R);
+    chain_rec_load(da, S.c0 + (int)threadIdx.x / W, S.c0 + (int)threadIdx.x / W < S.c1, rec);
+    job_stash_store(S, R, min(S.c1 - S.c0, G));
+  }
+  __syncthreads();
+  const int c0 = S.c0, c1 = S.c1;
   // the job's chains in one pass: the assembly's stores wait until this workgroup has handed
   // over its top inputs (they fill the wait for the top values instead of delaying it), and
   // phase 2 runs on phase 1's registers
-  bool keep = c1 - c0 <= kPcThreads / W;
+  const bool keep = c1 - c0 <= G;
+  // (keep) helpers store the top solver's assembly; the free waves' lane groups [0, gF)
+  const int nh = min(nj - 1, (G + kDirHelpChains - 1) / kDirHelpChains);
+  constexpr int gF = kDirFreeWaves * 64 / W;
   DirLane<W, CPL> L;
   double sA_ = 0.0, sB_ = 0.0;
   const int nt = pa.top_nt, ts0 = pa.top_ts0;
-  dir_up_fused<W, CPL>(pa, da, smem, L, false, sA_, sB_);
-  auto stores = [&]() { dir_stores_all<W, CPL>(pa, da, job, keep, L); };
-  double* sTop = smem + kDirLdsMain;
-  bool late = false;  // the workgroup that solved the top part (keep): lanes re-assembled
+  dir_up_v2<W, CPL>(pa, da, smem, S, rec, L, sA_, sB_);
+  NX_DSTAMP(35);
+  bool late_store = false;  // the top solver stores its own assembly after phase 2 (no helpers)
+  bool defer_free = false;  // a waiting workgroup's free waves store theirs after phase 2
+  const bool lane_on = c0 + (int)threadIdx.x / W < c1;
   if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
     vm_drain();
     __syncthreads();
@@ -4056,29 +4632,35 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
       const unsigned old = __hip_atomic_fetch_add(da.sync, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
       sFlag = old == last ? 1 : 0;
+      sIdx = (int)(old - da.epoch * (unsigned)nj);  // this workgroup's arrival order
+      if (sFlag && keep && nh > 0)  // tell the helpers whose assembly to store
+        __hip_atomic_store(da.sync + 4, tag | (unsigned)job, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (sFlag) {
       // this workgroup re-assembles its lanes after the top part (kept registers would stay
-      // live through the solve, past the register budget) and stores after its phase 2;
-      // with several chain passes its phase 2 reloads b and dq: stored right after the top
-      late = keep;
+      // live through the solve, past the register budget); its assembly is stored by the
+      // helpers (keep) or after its phase 2 (one job) or, with several chain passes (its phase
+      // 2 reloads b and dq), right after the top part
+      late_store = keep && nh == 0;
+      const int ct = nt + 1, cdc = pa.top_ndc > 0 ? pa.top_ndc : 1;  // this top part's sizes
       double* t = smem;
       TopLds T;
-      T.sD0 = t; t += kCapT;
-      T.sJ0 = t; t += kCapT;
-      T.sD = t; t += kCapT;
-      T.sJ = t; t += kCapT;
-      T.sGp = t; t += kCapT;
-      T.sY = t; t += kCapT;
-      T.sG = t; t += kCapTDC;
-      T.sDD = t; t += kCapTDC;
-      T.sDJ = t; t += kCapTDC;
+      T.sD0 = t; t += ct;
+      T.sJ0 = t; t += ct;
+      T.sD = t; t += ct;
+      T.sJ = t; t += ct;
+      T.sGp = t; t += ct;
+      T.sY = t; t += ct;
+      T.sG = t; t += cdc;
+      T.sDD = t; t += cdc;
+      T.sDJ = t; t += cdc;
       int* u = reinterpret_cast<int*>(t);
-      T.sPar = u; u += kCapT;
-      T.sLam = u; u += kCapT;
-      T.sOff = u; u += kCapT + 1;
-      T.sChild = u; u += kCapTDC;
+      T.sPar = u; u += ct;
+      T.sLam = u; u += ct;
+      T.sOff = u; u += ct + 1;
+      T.sChild = u; u += cdc;
       T.sLv = u;
       TopPre pre;
       top_pre_idx(pa, pre);
@@ -4093,11 +4675,46 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
       if (threadIdx.x == 0)
         __hip_atomic_store(da.sync + 2, da.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!keep) {
-        stores();
+        dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
+      } else {  // its lanes again, redefined inside this branch: not kept through the solve
+        chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+        dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
       }
     } else {
-      dir_stores_all<W, CPL, true>(pa, da, job, keep, L);  // (hidden in the wait: unit stride)
+      // the first nh workgroups to arrive store the top solver's assembly first (they have
+      // the most slack; their polls come before any store of theirs, so they see the
+      // announcement at once), then their own
+      if (keep && nh > 0 && sIdx < nh) {
+        if (threadIdx.x == 0) {
+          int who = -1;
+          for (unsigned k = 0; k < da.polls; ++k) {
+            const unsigned v = __hip_atomic_load(da.sync + 4, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 10) == (tag >> 10)) {
+              who = (int)(v & 1023u);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          sTopJob = who;
+        }
+        __syncthreads();
+        const int tj = sTopJob, hh = sIdx;
+        if (tj >= 0) {  // helper hh: its share of the top solver's chains (+ helper 0 its rows)
+          // one chain per wave (64 lanes: a chain's segment in a few whole-line store rounds)
+          constexpr int CH = (W * CPL + 63) / 64;
+          const int4 th = *reinterpret_cast<const int4*>(da.job_hdr + kJobHdr * (int64_t)tj);
+          DirLane<64, CH> Lh;
+          for (int cs = th.x + hh * kDirHelpChains; cs < th.y; cs += nh * kDirHelpChains)
+            dir_stores_v2<64, CH, true>(pa, da, tj, hh == 0 && cs < th.x + kDirHelpChains, cs,
+                                        min(th.y, cs + kDirHelpChains), false, Lh,
+                                        kDirFreeWaves, kPcThreads / 64);
+        }
+      }
+      // own stores (unit stride: hidden in the wait), but not the free waves' (keep)
+      dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
+      defer_free = keep;
       if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
@@ -4120,18 +4737,16 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
     for (int i = threadIdx.x; i < nt; i += kPcThreads) sTop[i] = ld_wt(pa.slot_z + ts0 + i);
     __syncthreads();
   } else {
-    stores();
+    dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, keep, L);
     vm_drain();
+    __syncthreads();  // (several passes: phase 2 reads the stored b and dq back)
   }
-  __syncthreads();  // (several passes: phase 2 reads the stored b and dq back)
-  const bool lane_on = c0 + (int)threadIdx.x / W < c1;
-  if (late) dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, lane_on, L);
   int lo0 = 0, lo1 = 0;  // this thread's left row's post range (dir_publish_fused)
   if ((int)threadIdx.x < da.n_left) {
     lo0 = da.left_off[threadIdx.x];
     lo1 = da.left_off[threadIdx.x + 1];
   }
-  dir_down_fused<W, CPL>(pa, da, smem, sTop, L, keep, sA_, sB_);
+  dir_down_v2<W, CPL>(pa, da, smem, sTop, S, L, keep, sA_, sB_);
   // hand-off 2: the residual partials and shares -> the last workgroup publishes
   vm_drain();
   __syncthreads();
@@ -4146,10 +4761,19 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
     dir_publish_fused(pa, da, lo0, lo1);
     NX_DSTAMP(4);
   }
-  if (late) {  // (the kernel's end, not the published state, waits for these)
-    dir_chain_asm<W, CPL>(pa, da, c0 + (int)threadIdx.x / W, lane_on, L);
-    stores();
+  // (the kernel's end, not the published state, waits for these; re-assembled: L kept
+  // through phase 2 would overflow the register budget there)
+  if (late_store) {  // one job: the top solver's own
+    chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+    dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
+    dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
+  } else if (defer_free && (int)threadIdx.x / W < gF) {  // the free waves' chains
+    chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+    dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
+    dir_chain_store<W, CPL>(pa, da, lane_on, L);
   }
+  vm_drain();
+  NX_DSTAMP(40);
 }
 
 // k_dir_team_up: the first half of the several-rank direct step (one rank's share, before
@@ -5237,6 +5861,13 @@ struct nx_network {
   unsigned* d_dsync = nullptr;
   unsigned dstep_epoch = 0;
   unsigned dstep_polls = kDirWaitPolls;  // the wait bound (nx_debug_set_wait_polls: tests)
+  // k_dir_step's job headers, chain records (crec / ci: refreshed with the coefficients),
+  // stash strides and dynamic LDS split (all in pc_bufs; nx_set_preconditioner)
+  int* d_job_hdr = nullptr;
+  double* d_crec = nullptr;
+  int* d_ci = nullptr;
+  int dstep_main = 0, dstep_top = 0;
+  size_t dstep_lds = 0;  // dynamic LDS bytes per workgroup
   unsigned* d_tsync = nullptr;  // k_dir_team_up's arrival counter (several ranks; pc_bufs)
   bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
   int last_dir_path = 0;   // the last direct solve: 0 four launches, 1 k_dir_step
@@ -6202,6 +6833,10 @@ NX_API int nx_dims(nx_network_t* h, int64_t* n_rows, int64_t* n_cols, int64_t* n
   return NX_OK;
 }
 
+namespace {
+int chain_rec_refresh(nx_network* h);
+}  // namespace
+
 NX_API int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_const, double f,
                                const double* edge_bc) {
   CHECK(flush_assembly(h));  // a deferred nx_assemble goes first
@@ -6225,7 +6860,7 @@ NX_API int nx_set_coefficients(nx_network_t* h, const double* edge_R, double R_c
   h->have_coeffs = true;
   h->coef_version += 1;  // (R may have changed: the next lhs assembly is a new matrix)
   HIPCALL(hipStreamSynchronize(h->stream));
-  return NX_OK;
+  return chain_rec_refresh(h);
 }
 
 NX_API int nx_set_source(nx_network_t* h, const double* edge_f) {
@@ -6235,7 +6870,7 @@ NX_API int nx_set_source(nx_network_t* h, const double* edge_f) {
   if (edge_f == nullptr) {
     if (h->edge_f) HIPCALL(hipFree(h->edge_f));
     h->edge_f = nullptr;
-    return NX_OK;
+    return chain_rec_refresh(h);
   }
   if (h->E > 0) {
     if (!h->edge_f) CHECK(dalloc(&h->edge_f, h->E));
@@ -6243,7 +6878,7 @@ NX_API int nx_set_source(nx_network_t* h, const double* edge_f) {
                            h->stream));
     HIPCALL(hipStreamSynchronize(h->stream));
   }
-  return NX_OK;
+  return chain_rec_refresh(h);
 }
 
 namespace {
@@ -6307,6 +6942,21 @@ int flush_assembly(nx_network* h) {
   return NX_OK;
 }
 
+}  // namespace
+
+namespace {
+// k_dir_step's chain records from the edge arrays (decomposition or coefficients changed)
+int chain_rec_refresh(nx_network* h) {
+  if (!h->d_crec || h->E == 0) return NX_OK;
+  hipLaunchKernelGGL(k_chain_rec, dim3(grid_of(h->E, 256)), dim3(256), 0, h->stream,
+                     h->pa.chain_edge, h->pa.chain_flip, h->E, h->edge_x, h->edge_R, h->edge_f,
+                     h->f, h->edge_bc, h->edge_lm, h->edge_seg, h->d_crec, h->d_ci);
+  HIPCALL(hipGetLastError());
+  HIPCALL(hipStreamSynchronize(h->stream));
+  return NX_OK;
+}
+// the tile width W of a (W, CPL) variant (nx_set_preconditioner's choice)
+int variant_w(int v) { return v == 5 || v == 7 ? 8 : v == 6 ? 4 : v <= 2 ? 16 : 64; }
 }  // namespace
 
 NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
@@ -6541,9 +7191,17 @@ void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
              h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
              h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
              h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1, h->d_seq,
-             h->d_last, h->dir_bb};
-  hipExtLaunchKernelGGL((k_dir_step<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), 0, h->stream,
-                        prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0, h->pa, da);
+             h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci, h->dstep_main,
+             h->dstep_top};
+  static thread_local std::vector<const void*> opted;  // (the dynamic LDS above 64 KiB, once)
+  const void* fn = reinterpret_cast<const void*>(&k_dir_step<W, CPL>);
+  if (std::find(opted.begin(), opted.end(), fn) == opted.end()) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kDirLdsMax);
+    opted.push_back(fn);
+  }
+  hipExtLaunchKernelGGL((k_dir_step<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
+                        h->stream, prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0,
+                        h->pa, da);
 }
 
 // Several ranks: k_dir_team_up, the assembly + up sweep + top part of one rank (half 0 of
@@ -6867,7 +7525,7 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     // or every later wait_published expects a stamp the publish kernels never write.
     (void)hipGetLastError();
     HIPCALL(hipStreamSynchronize(h->stream));
-    HIPCALL(hipMemset(h->d_dsync, 0, 4 * sizeof(unsigned)));
+    HIPCALL(hipMemset(h->d_dsync, 0, 8 * sizeof(unsigned)));
     HIPCALL(hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost));
     h->dstep_epoch = 0;
     h->dstep_off = true;
@@ -7656,10 +8314,10 @@ NX_API int nx_bench_spmv_cold(nx_network_t* h, int32_t reps, int32_t* copies_out
       return fail(NX_ERR_HIP, "cold SpMV buffers: out of device memory");
     }
     for (void* p : {(void*)rp, (void*)cl, (void*)vl, (void*)x, (void*)y}) bufs.push_back(p);
-    hipMemcpyAsync(rp, h->rowptr, sizeof(int) * (h->n_own + 1), hipMemcpyDeviceToDevice, h->stream);
-    hipMemcpyAsync(cl, h->col, sizeof(int) * h->nnz, hipMemcpyDeviceToDevice, h->stream);
-    hipMemcpyAsync(vl, h->val, sizeof(double) * h->nnz, hipMemcpyDeviceToDevice, h->stream);
-    hipMemcpyAsync(x, h->vb[0], sizeof(double) * h->n_col, hipMemcpyDeviceToDevice, h->stream);
+    (void)hipMemcpyAsync(rp, h->rowptr, sizeof(int) * (h->n_own + 1), hipMemcpyDeviceToDevice, h->stream);
+    (void)hipMemcpyAsync(cl, h->col, sizeof(int) * h->nnz, hipMemcpyDeviceToDevice, h->stream);
+    (void)hipMemcpyAsync(vl, h->val, sizeof(double) * h->nnz, hipMemcpyDeviceToDevice, h->stream);
+    (void)hipMemcpyAsync(x, h->vb[0], sizeof(double) * h->n_col, hipMemcpyDeviceToDevice, h->stream);
     mats[i] = Csr{rp, cl, vl, h->n_own};
     xs[i] = x;
     ys[i] = y;
@@ -7969,9 +8627,9 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
       h->d_left_off = const_cast<int*>(up(off.data(), (int64_t)off.size()));
       h->d_post = scratch(std::max(1, off.back()));
       unsigned* sy = nullptr;
-      if (hipMalloc((void**)&sy, 4 * sizeof(unsigned)) == hipSuccess) {
+      if (hipMalloc((void**)&sy, 8 * sizeof(unsigned)) == hipSuccess) {
         h->pc_bufs.push_back(sy);
-        if (hipMemset(sy, 0, 4 * sizeof(unsigned)) != hipSuccess) sy = nullptr;
+        if (hipMemset(sy, 0, 8 * sizeof(unsigned)) != hipSuccess) sy = nullptr;
       }
       h->d_dsync = sy;
       h->dstep_ok = ok && h->d_chain_post && h->d_left_off && h->d_post && h->d_dsync;
@@ -8024,6 +8682,8 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   // the top part's register set-up (top_body): every slot's level, junction children (top
   // position) and their hanging-chain entries, when all have <= kWaveKids and fit
   pa.top_wave = nullptr;
+  pa.top_sub = pa.top_lane = pa.top_sub_dep = nullptr;
+  pa.top_sub_nup = 0;
   if (n_top_lvl > 0 && h->top_nt > 0 && h->top_nt <= kTopThreads) {
     const int ts0 = top_lvl_off[0], nt = h->top_nt, dc0 = slot_dc_off[ts0];
     std::vector<int> tw((size_t)(1 + kWaveKids) * nt, 0);
@@ -8044,11 +8704,124 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
         w[0] = q | (nk << 8);
       }
     if (ok) pa.top_wave = up(tw.data(), (int64_t)tw.size());
+    // the same top part as wave subtrees (top_body): maximal subtrees of <= 64 slots, one per
+    // wave, BFS lanes; the slots above them swept level by level (NXHIP_TOP_SUB=0: all levels)
+    const char* es = std::getenv("NXHIP_TOP_SUB");
+    if (ok && (es == nullptr || std::atoi(es) != 0)) {
+      constexpr int K1 = 1 + kWaveKids, K2 = 2 + kWaveKids, NW = kTopThreads / 64;
+      std::vector<int> lvl(nt, 0), size(nt, 1), par(nt, -1);
+      for (int q = 0; q < n_top_lvl; ++q)
+        for (int j = top_lvl_off[q]; j < top_lvl_off[q + 1]; ++j) lvl[j - ts0] = q;
+      for (int q = n_top_lvl - 1; q >= 0; --q)  // subtree sizes, deepest level first
+        for (int j = top_lvl_off[q]; j < top_lvl_off[q + 1]; ++j) {
+          const int* w = tw.data() + (size_t)K1 * (j - ts0);
+          for (int k = 0; k < ((w[0] >> 8) & 0xff); ++k) {
+            const int c = w[1 + k] & 0xfff;
+            size[j - ts0] += size[c];
+            par[c] = j - ts0;
+          }
+        }
+      std::vector<int> ts(K1 * (size_t)nt, 0), tl(K2 * (size_t)kTopThreads, 0), tdep(NW, 0);
+      for (int t = 0; t < kTopThreads; ++t) tl[(size_t)K2 * t] = -1;
+      int nsub = 0, nup = 0;
+      bool sok = true;
+      for (int j = 0; j < nt && sok; ++j) {
+        if (size[j] > 64) {  // an upper slot: the level sweeps
+          const int* w = tw.data() + (size_t)K1 * j;
+          int* o = ts.data() + (size_t)K1 * j;
+          o[0] = (int)(0x80000000u | (unsigned)w[0]);
+          for (int k = 0; k < kWaveKids; ++k) o[1 + k] = w[1 + k];
+          nup = std::max(nup, lvl[j] + 1);
+          continue;
+        }
+        if (par[j] >= 0 && size[par[j]] <= 64) continue;  // inside another subtree
+        if (nsub >= NW) {
+          sok = false;
+          break;
+        }
+        std::vector<int> bfs{j}, lane_of(nt, -1), dep{0};  // this subtree, BFS order
+        lane_of[j] = 0;
+        for (size_t i = 0; i < bfs.size(); ++i) {
+          const int* w = tw.data() + (size_t)K1 * bfs[i];
+          for (int k = 0; k < ((w[0] >> 8) & 0xff); ++k) {
+            const int c = w[1 + k] & 0xfff;
+            lane_of[c] = (int)bfs.size();
+            bfs.push_back(c);
+            dep.push_back(dep[i] + 1);
+          }
+        }
+        int md = 0;
+        for (size_t i = 0; i < bfs.size(); ++i) {
+          const int m = bfs[i];
+          const int* w = tw.data() + (size_t)K1 * m;
+          const int nk = (w[0] >> 8) & 0xff;
+          int* o = tl.data() + (size_t)K2 * (nsub * 64 + (int)i);
+          o[0] = m;
+          const int pl = dep[i] > 0 ? lane_of[par[m]] : 0;
+          o[1] = (int)i | (dep[i] << 6) | (nk << 14) | (pl << 18);
+          for (int k = 0; k < nk; ++k) o[2 + k] = lane_of[w[1 + k] & 0xfff] | ((w[1 + k] >> 12) << 12);
+          md = std::max(md, dep[i]);
+        }
+        if (md > 0xff) sok = false;
+        tdep[nsub++] = md + 1;
+      }
+      if (sok && nsub > 0) {
+        pa.top_sub = up(ts.data(), (int64_t)ts.size());
+        pa.top_lane = up(tl.data(), (int64_t)tl.size());
+        pa.top_sub_dep = up(tdep.data(), NW);
+        pa.top_sub_nup = nup;
+      }
+    }
+  }
+  // k_dir_step's job headers, stash strides, dynamic LDS and chain records (round 4)
+  h->d_job_hdr = nullptr;
+  h->d_crec = nullptr;
+  h->d_ci = nullptr;
+  if (h->dstep_ok) {
+    std::vector<int> hdr((size_t)kJobHdr * n_jobs, 0);
+    int mlv = 1, mns = 0, mnd = 0;
+    for (int jb = 0; jb < n_jobs; ++jb) {
+      const int lv0 = job_lvl_off[jb], lv1 = job_lvl_off[jb + 1];
+      const int js0 = lv1 > lv0 ? lvl_slot_off[lv0] : 0, js1 = lv1 > lv0 ? lvl_slot_off[lv1] : 0;
+      int* r = hdr.data() + (size_t)kJobHdr * jb;
+      r[0] = job_chain_off[jb];
+      r[1] = job_chain_off[jb + 1];
+      r[2] = lv0;
+      r[3] = lv1;
+      r[4] = js0;
+      r[5] = js1;
+      r[6] = slot_dc_off[js0];
+      r[7] = slot_dc_off[js1];
+      r[8] = 0;
+      r[9] = lv1 > lv0 ? lvl_slot_off[lv0 + 1] : 0;
+      mlv = std::max(mlv, lv1 - lv0 + 1);
+      mns = std::max(mns, js1 - js0);
+      mnd = std::max(mnd, r[7] - r[6]);
+    }
+    if (pa.job_wave) {  // (the one-wave set-up of the up sweep, when the job has it)
+      std::vector<int> jw(n_jobs, 0);
+      HIPCALL(hipMemcpy(jw.data(), pa.job_wave, sizeof(int) * n_jobs, hipMemcpyDeviceToHost));
+      for (int jb = 0; jb < n_jobs; ++jb) hdr[(size_t)kJobHdr * jb + 8] = jw[jb];
+    }
+    const int W = variant_w(variant);
+    const int nt = h->top_nt, cdc = std::max(1, pa.top_ndc), ct = nt + 1;
+    const int top_ints = 3 * ct + 1 + cdc + n_top_lvl + 1;
+    const int top_dbl = 6 * ct + 3 * cdc + (top_ints + 1) / 2 + 2;
+    h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl});
+    h->dstep_top = nt + (nt & 1);
+    h->dstep_lds = 8 * (size_t)(kStashDbl + h->dstep_main + h->dstep_top);
+    const bool fits = mlv <= kStLv && mns <= kStNs && mnd <= kStNd && kPcThreads / W <= kStNc;
+    h->d_job_hdr = const_cast<int*>(up(hdr.data(), (int64_t)hdr.size()));
+    h->d_crec = scratch(10 * std::max<int64_t>(n_chains, 1));
+    h->d_ci = const_cast<int*>(up(nullptr, 4 * std::max<int64_t>(n_chains, 1)));
+    h->dstep_ok = h->d_job_hdr && h->d_crec && h->d_ci && fits &&
+                  h->dstep_lds <= (size_t)kDirLdsMax;
   }
   h->pc_lds = lds;
   h->pa = pa;
   h->pc_jobs = n_jobs;
   h->pc_variant = variant;
+  if (h->d_crec) CHECK(chain_rec_refresh(h));
   h->pc_slots = n_slots;
   h->pc_ndc = n_slots > 0 ? slot_dc_off[n_slots] : 0;
   h->pc = true;
@@ -8688,9 +9461,9 @@ NX_API int nx_debug_phases(unsigned long long* out, int32_t n) {
   return NX_OK;
 }
 
-NX_API int nx_debug_dstep(unsigned long long* out) {  // 12 x 512 stamps of k_dir_step
+NX_API int nx_debug_dstep(unsigned long long* out) {  // 48 x 512 stamps of k_dir_step
   HIPCALL(hipDeviceSynchronize());
-  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(unsigned long long) * 32 * 512));
+  HIPCALL(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dst), sizeof(unsigned long long) * 48 * 512));
   return NX_OK;
 }
 

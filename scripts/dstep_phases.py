@@ -40,11 +40,11 @@ def main() -> int:
         it, rr, conv = h.solve(1e-12, 100, 4)
     assert h.direct_path() == "fused", h.direct_path()
     nj = asm.tree_preconditioner.n_jobs
-    buf = (C.c_ulonglong * (32 * 512))()
+    buf = (C.c_ulonglong * (48 * 512))()
     fn = _lib.lib().nx_debug_dstep
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
     _lib.check(fn(buf))
-    g = np.array(buf, dtype=np.float64).reshape(32, 512)[:, :nj]
+    g = np.array(buf, dtype=np.float64).reshape(48, 512)[:, :nj]
     t0 = g[0].min()
     us = (g - t0) / 100.0  # 100 MHz ticks -> us
     names = ["start", "phase-1 arrival", "top values in", "phase-2 arrival", "published",
@@ -68,6 +68,17 @@ def main() -> int:
     d2 = us[3] - us[2]
     print(f"  phase 1 per wg: min {d1.min():.2f} med {np.median(d1):.2f} max {d1.max():.2f}")
     print(f"  phase 2 per wg: min {d2.min():.2f} med {np.median(d2):.2f} max {d2.max():.2f}")
+    # inside the phases (thread 0 of every workgroup; medians over workgroups)
+    inner = [(32, 0, "phase 1: chains assembled + condensed"), (33, 32, "phase 1: junction set-up"),
+             (34, 33, "phase 1: junction levels"), (35, 34, "phase 1: posts"),
+             (36, 2, "phase 2: set-up"), (37, 36, "phase 2: junction levels"),
+             (38, 37, "phase 2: chains (x, residual)"), (3, 38, "phase 2: rows + partials"),
+             (40, 3, "end of the workgroup after phase 2")]
+    for k, k0, name in inner:
+        d = us[k] - us[k0]
+        print(f"  {name:38s} med {np.median(d):6.2f}  max {d.max():6.2f}")
+    e = us[40]
+    print(f"  {'workgroup end':16s} min {e.min():7.2f}  med {np.median(e):7.2f}  max {e.max():7.2f}")
     return 0
 
 
