@@ -13,9 +13,10 @@ Workload (p_bc = y, f = 0, R = 1, ``color_strategy="smallest_last"
 
 * 1 GPU: ``make_tree(15,15,15)``, N = 15 -- the depth-14 tree, 1,032,160 DoF (configs[3],
   the configuration the metric is quoted on);
-* P = 2^k GPUs: ``make_tree(15+k, 15+k, 15+k)``, N = 19 -- one tree generation per GPU
-  doubling (weak scaling, ~1.28 M rows per GPU); at 8 GPUs this is SURVEY's C4,
-  ``make_tree(18,18,18)``, N = 19, 10,354,648 DoF (configs[4]). Rank 0 also times the SAME
+* P = 2^k GPUs: ``make_tree(15+k, 15+k, 15+k)``, N = 15 -- one tree generation per GPU
+  doubling, the same N as on one GPU, so every GPU carries the one-GPU load (weak scaling,
+  ~1.03 M rows per GPU; 8 GPUs: 8,257,536 DoF). ``--N 19`` gives SURVEY's C4 at 8 GPUs
+  (``make_tree(18,18,18)``, N = 19, 10,354,648 DoF, configs[4]). Rank 0 also times the SAME
   workload on its GPU alone (``strong_scaling``), so T1 / TP is measured in the same run.
 
 One step = device assembly of the CSR matrix and rhs (``nx_assemble``) + the solve
@@ -230,7 +231,7 @@ def parse_args(argv=None):
     ap.add_argument("--levels", type=int, default=None,
                     help="tree generations (default: 15 at 1 GPU, 15 + log2(P) at P GPUs)")
     ap.add_argument("--N", type=int, default=None,
-                    help="cells per edge (default: 15 at 1 GPU, 19 at P > 1 GPUs)")
+                    help="cells per edge (default 15 at every GPU count; 19: C4 at 8 GPUs)")
     ap.add_argument("--rtol", type=float, default=1e-12)
     ap.add_argument("--check-every", type=int, default=4)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -288,7 +289,7 @@ def run(args, world: int) -> int:
     if world > 1 and 2**extra != world:
         raise SystemExit("world size must be a power of two")
     levels = args.levels if args.levels is not None else 15 + extra
-    N = args.N if args.N is not None else (15 if world == 1 else 19)
+    N = args.N if args.N is not None else 15  # (the one-GPU load on every GPU: weak scaling)
     comm = TorchComm() if world > 1 else SerialComm()
 
     def barrier():

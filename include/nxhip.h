@@ -378,7 +378,8 @@ int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left);
  * 0 for the separate launches (assembly, up sweep, down sweep, publish). Replaces nothing
  * in the reference (PETSc's KSPSolve is one call: solver.py:127). */
 int nx_get_direct_path(nx_network_t* h, int32_t* path);
-/* (path 2: the (k, 0) condensed route of nx_fe_set_direct.)
+/* (path 2: the (k, 0) condensed route of nx_fe_set_direct; path 3: several ranks, the
+ * exchange step k_dir_xr / k_dir_xg, one launch per rank.)
  * Test hook: the number of s_sleep-paced polls a k_dir_step workgroup spends waiting for the
  * top part's values before it gives up (default 2^20). 0 makes every waiting workgroup give
  * up at once, which forces the fallback a non-co-resident launch takes: the host resets the
@@ -386,6 +387,12 @@ int nx_get_direct_path(nx_network_t* h, int32_t* path);
  * on this handle from then on (until the next nx_set_preconditioner). Replaces nothing in
  * the reference. */
 int nx_debug_set_wait_polls(nx_network_t* h, uint32_t polls);
+/* Rehearsal hook: the exchange step (k_dir_xr) of group member h ALONE, reps timed launches
+ * (*ms: average kernel time, HIP events on the dispatch), its two exchanges emulated from
+ * the sums the group's previous graph-path direct solve left -- the per-rank time of a
+ * multi-GPU run measured on one GPU (whose ranks cannot all be resident in one launch).
+ * h's solution is then the rank's share of the answer. Replaces nothing in the reference. */
+int nx_debug_xr_rehearse(nx_network_t* h, double rtol, int32_t reps, double* ms);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
 /* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,
@@ -423,6 +430,20 @@ int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned c
  * NXHIP_DIR_CUT=0 keeps the halo path. Part of the ranks' schedule signature. */
 int nx_set_cut(nx_network_t* h, int32_t K, const int32_t* lm_cut, const int32_t* gk_off,
                const int32_t* gk_row, const double* gk_coef);
+
+/* Several ranks, direct solve in ONE launch per rank (k_dir_xr): the ranks exchange the
+ * coarse partials and the residual's partials device-side, through a mailbox in each rank's
+ * device memory that every rank writes into (IPC-mapped over xGMI) -- no RCCL call in the
+ * step. After nx_comm_init: nx_xch_export writes this rank's mailbox handle
+ * (NX_XCH_HANDLE_BYTES); the host control plane all-gathers them in rank order; every
+ * rank passes all P to nx_xch_import. The ranks decide together (the schedule comparison)
+ * whether every one can run the step; otherwise the graph path (RCCL all-reduces) runs.
+ * NXHIP_DIR_XR=0 keeps the graph path. Replaces the MPI reductions of the reference's
+ * distributed MUMPS solve (solver.py:127-132); in-process groups link their mailboxes in
+ * nx_group_create. */
+#define NX_XCH_HANDLE_BYTES 64
+int nx_xch_export(nx_network_t* h, unsigned char* handle_out);
+int nx_xch_import(nx_network_t* h, const unsigned char* handles);
 
 /* Ranks of the handle's RCCL communicator (ncclCommCount); without one, the rank count of
  * its halo plan (1 for a single-GPU handle). bench.py reports it next to the timing. */

@@ -24,6 +24,7 @@ _lib = None
 
 NX_OK, NX_ERR_ARG, NX_ERR_HIP, NX_ERR_RCCL, NX_ERR_STATE, NX_ERR_NOCONV = 0, -1, -2, -3, -4, -5
 UNIQUE_ID_BYTES = 128
+XCH_HANDLE_BYTES = 64  # NX_XCH_HANDLE_BYTES
 
 _i32, _i64, _f64 = C.c_int32, C.c_int64, C.c_double
 _pd = C.POINTER(C.c_double)
@@ -66,6 +67,7 @@ _SIGS = {
     "nx_get_direct_info": (C.c_int, [_h, _pi32, _pi32]),
     "nx_get_direct_path": (C.c_int, [_h, _pi32]),
     "nx_debug_set_wait_polls": (C.c_int, [_h, C.c_uint32]),
+    "nx_debug_xr_rehearse": (C.c_int, [_h, _f64, _i32, _pd]),
     "nx_reset_profile": (C.c_int, [_h]),
     "nx_bench_spmv": (C.c_int, [_h, _i32, _pd]),
     "nx_bench_spmv_cold": (C.c_int, [_h, _i32, _pi32, _pd]),
@@ -78,6 +80,8 @@ _SIGS = {
     "nx_set_coarse": (C.c_int, [_h, _i32, _pi32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                 _i32, _pi32]),
     "nx_comm_count": (C.c_int, [_h, _pi32]),
+    "nx_xch_export": (C.c_int, [_h, _pu8]),
+    "nx_xch_import": (C.c_int, [_h, _pu8]),
     "nx_set_halo": (C.c_int, [_h, _i32, _i32, _i32, _pi32, _pi32, _pi32, _pi32]),
     "nx_set_cut": (C.c_int, [_h, _i32, _pi32, _pi32, _pi32, _pd]),
     "nx_set_pc_kernels": (C.c_int, [_h, _i32]),
@@ -373,7 +377,14 @@ class Handle:
         route through the auxiliary P1/DG0 handle)."""
         v = C.c_int32(0)
         check(lib().nx_get_direct_path(self.ptr, C.byref(v)))
-        return {1: "fused", 2: "condensed"}.get(v.value, "launches")
+        return {1: "fused", 2: "condensed", 3: "exchange"}.get(v.value, "launches")
+
+    def xr_rehearse(self, rtol: float = 1e-12, reps: int = 20) -> float:
+        """Rehearsal hook (``nx_debug_xr_rehearse``): ms per launch of this group member's
+        exchange step alone, its exchanges emulated from the group's last graph-path solve."""
+        ms = C.c_double(0.0)
+        check(lib().nx_debug_xr_rehearse(self.ptr, float(rtol), int(reps), C.byref(ms)))
+        return float(ms.value)
 
     def set_wait_polls(self, polls: int) -> None:
         """Test hook (``nx_debug_set_wait_polls``): the fused step's wait bound; 0 forces
@@ -534,6 +545,18 @@ class Handle:
         check(lib().nx_set_cut(self.ptr, int(n_cut), _ptr(arrs[0], C.c_int32),
                                _ptr(arrs[1], C.c_int32), _ptr(arrs[2], C.c_int32),
                                _ptr(arrs[3], C.c_double)))
+
+    def xch_export(self) -> bytes:
+        """This rank's exchange mailbox handle (``nx_xch_export``, after comm_init)."""
+        buf = (C.c_ubyte * XCH_HANDLE_BYTES)()
+        check(lib().nx_xch_export(self.ptr, buf))
+        return bytes(buf)
+
+    def xch_import(self, handles) -> None:
+        """Every rank's mailbox handle in rank order (``nx_xch_import``)."""
+        raw = b"".join(handles)
+        buf = (C.c_ubyte * len(raw)).from_buffer_copy(raw)
+        check(lib().nx_xch_import(self.ptr, buf))
 
     def comm_count(self) -> int:
         """Ranks of the RCCL communicator (``ncclCommCount``), else the plan's rank count."""

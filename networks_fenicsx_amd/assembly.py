@@ -380,6 +380,15 @@ class HydraulicNetworkAssembler:
             uid = comm.bcast(uid, root=0)
             self._handle.comm_init(self._nranks, self._rank, uid, lp.peers, lp.send_off,
                                    lp.send_idx, lp.recv_off)
+            # the exchange step's mailboxes (nx_xch_*): every rank maps every rank's; a rank
+            # that cannot export one leaves every rank on the graph path (RCCL all-reduces)
+            try:
+                mine = self._handle.xch_export()
+            except _lib.NxError:
+                mine = None
+            handles = comm.allgather(mine)
+            if all(hd is not None for hd in handles):
+                self._handle.xch_import(handles)
         # the direct solve completes the cut multiplier rows in its residual all-reduce
         self._handle.set_cut(lp.n_cut, lp.lm_cut, lp.gk_off, lp.gk_row, lp.gk_coef)
 

@@ -2790,6 +2790,9 @@ struct CoarsePre {
   double cD, cJ, cG;  // its all-reduced D, J and chain conductance to the parent
 };
 
+// WT: the slots' D / J and the chains' T come from this launch (k_dir_xr: written
+// write-through by other workgroups or plain by this one): loads that bypass L1
+template <bool WT = false>
 __device__ __forceinline__ void coarse_top_pre(const PcArgs& pa, CoarsePre& p) {
   const int sl = threadIdx.x, ts0 = pa.top_ts0, nt = pa.top_nt;
   p.k = -1;
@@ -2816,9 +2819,9 @@ __device__ __forceinline__ void coarse_top_pre(const PcArgs& pa, CoarsePre& p) {
     p.k = pa.slot_cidx[j];
     if (p.k < 0) {
       p.par = pa.slot_parent[j];
-      p.J = pa.slot_J[j];
-      p.D = pa.slot_D[j];
-      if (p.par >= 0) p.T = pa.chain_T[pa.slot_pchain[j]];
+      p.J = ldv<WT>(pa.slot_J + j);
+      p.D = ldv<WT>(pa.slot_D + j);
+      if (p.par >= 0) p.T = ldv<WT>(pa.chain_T + pa.slot_pchain[j]);
     }
   }
 }
@@ -3300,6 +3303,18 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
 // b on the multiplier rows is zero (the assembly writes zeros there; assembly.py: L[lambda]
 // = 0), so no workgroup reads rhs rows another one wrote.
 // ======================================================================================
+// One rank's mailbox of the device-side exchange between ranks (k_dir_xr / k_dir_xg): P
+// slots of each exchange's doubles (exchange 1: the coarse partials [D | J | G]; exchange
+// 2: [||r||^2, ||b||^2, the cut rows' shares]) and 2P arrival flags, one per sender. Each
+// rank writes its slot in every rank's mailbox (system-scope write-through stores: peer
+// memory over xGMI, IPC-mapped; the in-process group: the same device), raises its flag
+// there, polls its own P flags and sums the P slots in rank order.
+struct XPeer {
+  double* mb1;
+  double* mb2;
+  unsigned* fl;
+};
+
 struct DirStep {
   const double* edge_x;
   const double* edge_R;
@@ -3339,6 +3354,13 @@ struct DirStep {
   const double* crec;
   const int* ci;
   int lds_main, lds_top;
+  // several ranks (k_dir_xr / k_dir_xg): the ranks' mailboxes (xpeers[q]: where this rank
+  // writes for rank q), this rank's own (xself: where it reads), the exchange's shape, the
+  // launch tag (monotonic, never reset), the cut rows (the last xK post ranges of left_off)
+  const XPeer* xpeers;
+  XPeer xself;
+  int xP, xrank, xld1, xld2, xK;
+  unsigned xtag;
 };
 
 constexpr int kDirWaitPolls = 1 << 20;  // s_sleep-paced polls before a waiting workgroup gives up
@@ -4327,7 +4349,7 @@ template <int W, int CPL>
 __device__ __forceinline__ void dir_down_v2(const PcArgs& pa, const DirStep& da, double* lds,
                                             const double* sTop, const JobStash& S,
                                             const DirLane<W, CPL>& L, bool keep, double sA_,
-                                            double sB_) {
+                                            double sB_, int job) {
   // (contraction as in k_pc_down_lds: the same x bit for bit)
   double* sZ = lds;
   double* sA = sZ + kCapS;
@@ -4336,7 +4358,7 @@ __device__ __forceinline__ void dir_down_v2(const PcArgs& pa, const DirStep& da,
   double* sQb = sQt + kCapC;
   int* sP = reinterpret_cast<int*>(sQb + kCapC);
   __shared__ double s_w[2 * (kPcThreads / 64)];
-  const int job = blockIdx.x;
+  // (job: this rank's job index -- the in-process group's launch holds every rank's jobs)
   const int ts0 = pa.top_ts0;
   const int lv0 = S.lv0, lv1 = S.lv1;
   const int js0 = S.js0, js1 = S.js1;
@@ -4586,14 +4608,165 @@ __global__ __launch_bounds__(256) void k_chain_rec(const int* __restrict__ chain
   ci[4 * c + 3] = edge_seg[e + 1] - edge_seg[e];
 }
 
-template <int W, int CPL>
-__global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) {
+// ---- the device-side exchange between ranks (k_dir_xr / k_dir_xg) ---------------------
+__device__ __forceinline__ void st_sys(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys(const double* p) {
+  return __builtin_bit_cast(
+      double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+// Exchange round `which` (0: coarse partials, 1: residual partials) of one workgroup: this
+// rank's n doubles (src, LDS) into its slot of every rank's mailbox, then -- after every
+// storing wave's vmcnt(0) and a barrier -- its flag at every rank (tagged with the launch);
+// then this rank's P flags polled (bounded) and the P slots summed in rank order (the same
+// additions as k_group_sum: every rank gets the same bits) into dst (LDS). False: a rank's
+// flag never came.
+__device__ bool xr_allsum(const DirStep& da, int which, const double* src, int n, double* dst) {
+  __shared__ int sOk;
+  const int P = da.xP, r = da.xrank, ld = which ? da.xld2 : da.xld1;
+  for (int q = 0; q < P; ++q) {
+    double* mb = (which ? da.xpeers[q].mb2 : da.xpeers[q].mb1) + (int64_t)r * ld;
+    for (int i = threadIdx.x; i < n; i += kPcThreads) st_sys(mb + i, src[i]);
+  }
+  vm_drain();
+  if (threadIdx.x == 0) sOk = 1;
+  __syncthreads();
+  if ((int)threadIdx.x < P)
+    __hip_atomic_store(da.xpeers[threadIdx.x].fl + which * P + r, da.xtag, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((int)threadIdx.x < P) {
+    bool ok = false;
+    for (unsigned k = 0; k < da.polls; ++k) {
+      if (__hip_atomic_load(da.xself.fl + which * P + threadIdx.x, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_SYSTEM) == da.xtag) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) sOk = 0;
+  }
+  __syncthreads();
+  if (!sOk) return false;
+  const double* mine = which ? da.xself.mb2 : da.xself.mb1;
+  for (int i = threadIdx.x; i < n; i += kPcThreads) {
+    double v = 0.0;
+    for (int q = 0; q < P; ++q) v += ld_sys(mine + (int64_t)q * ld + i);
+    dst[i] = v;
+  }
+  __syncthreads();
+  return true;
+}
+
+// The top part's solver after top_body<MULTI>: exchange 1 of the coarse partials (cbuf),
+// the sums back into cbuf, the coarse forest and the top part's back-substitution
+// (coarse_top_pre / coarse_top_block, k_pc_coarse's arithmetic) into LDS, then the top
+// values to slot_z (write-through: the rank's other workgroups read them) and to x.
+__device__ bool xr_coarse(const PcArgs& pa, const DirStep& da, const TopLds& T) {
+  __shared__ double xb[2 * 3 * kCapCoarseLds];
+  const int nC = pa.n_coarse, n1 = 3 * nC;
+  for (int i = threadIdx.x; i < n1; i += kPcThreads) xb[i] = ld_wt(pa.cbuf + i);
+  __syncthreads();
+  if (!xr_allsum(da, 0, xb, n1, xb + n1)) return false;
+  for (int i = threadIdx.x; i < n1; i += kPcThreads) pa.cbuf[i] = xb[n1 + i];
+  vm_drain();
+  __syncthreads();
+  CoarsePre cp;
+  coarse_top_pre<true>(pa, cp);
+  const int ts0 = pa.top_ts0, nt = pa.top_nt;
+  coarse_top_block(pa, cp, T.sD0, T.sJ0, T.sGp, T.sY, T.sOff);
+  for (int i = threadIdx.x; i < nt; i += kPcThreads) {
+    const double zj = T.sY[i];
+    st_wt(pa.slot_z + ts0 + i, zj);
+    da.x[T.sLam[i]] = zj;
+  }
+  return true;
+}
+
+// The publisher of a rank of several (k_dir_xr / k_dir_xg): dir_publish_fused's sums of the
+// rank's own rows, the cut rows' shares of this rank (the last xK post ranges), exchange 2,
+// then every rank the same relres: the rows' ||r||^2 summed in rank order plus the cut
+// rows' r^2 in index order (r = 0 - the ranks' shares: b = 0 on the multiplier rows).
+__device__ bool dir_publish_xr(const PcArgs& pa, const DirStep& da, int lo0, int lo1) {
+#pragma clang fp contract(off)
+  __shared__ double s_r[kPcThreads / 64], s_b[kPcThreads / 64];
+  __shared__ double xs[2 * (2 + kCapCoarseLds)];
+  const int nj = pa.n_jobs, K = da.xK, nl = da.n_left;
+  double rr = 0.0, bb = 0.0;
+  for (int i = threadIdx.x; i < nj; i += kPcThreads) {
+    rr += ld_wt(pa.rpart + i);
+    bb += ld_wt(pa.rpart + nj + i);
+  }
+  for (int i = threadIdx.x; i < nl; i += kPcThreads) {
+    double acc = 0.0;
+    const bool pre = i == (int)threadIdx.x;
+    const int k0 = pre ? lo0 : da.left_off[i], k1 = pre ? lo1 : da.left_off[i + 1];
+    for (int k = k0; k < k1; ++k) acc += ld_wt(da.post + k);
+    const double rv = 0.0 - acc;  // b = 0 on the multiplier rows
+    rr += rv * rv;
+  }
+  for (int k = threadIdx.x; k < K; k += kPcThreads) {  // this rank's shares of the cut rows
+    double acc = 0.0;
+    for (int e = da.left_off[nl + k]; e < da.left_off[nl + k + 1]; ++e) acc += ld_wt(da.post + e);
+    xs[2 + k] = acc;
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_r[threadIdx.x >> 6] = rr;
+    s_b[threadIdx.x >> 6] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    rr = 0.0;
+    bb = 0.0;
+    for (int w = 0; w < kPcThreads / 64; ++w) {
+      rr += s_r[w];
+      bb += s_b[w];
+    }
+    xs[0] = rr;
+    xs[1] = bb;
+  }
+  __syncthreads();
+  double* ys = xs + 2 + K;
+  if (!xr_allsum(da, 1, xs, 2 + K, ys)) return false;
+  if (threadIdx.x == 0) {
+    rr = ys[0];
+    for (int k = 0; k < K; ++k) {
+      const double rk = 0.0 - ys[2 + k];
+      rr += rk * rk;
+    }
+    bb = ys[1];
+    da.bbst[0] = bb;
+    MrState st{};
+    st.beta1 = sqrt(bb);
+    st.relres = bb > 0.0 ? sqrt(rr / bb) : sqrt(rr);
+    st.rtol = da.rtol;
+    st.it = 1;
+    st.done = 1;
+    st.converged = st.relres <= da.rtol ? 1 : 0;
+    publish_wt(st, da.seq_next, da.seq, da.mirror);
+  }
+  return true;
+}
+
+// The fused direct step of one rank (k_dir_step) or, XR, of one rank of several (k_dir_xr:
+// one launch per GPU; k_dir_xg: every rank of an in-process group in one launch): the top
+// part then ends with this rank's coarse partials, the ranks exchange and sum them
+// (xr_allsum), the top part's solver finishes the coarse forest and the top values, and
+// the publisher exchanges the residual's partials and the cut rows' shares the same way.
+template <int W, int CPL, bool XR>
+__device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& da, int job) {
   extern __shared__ double dsm[];
   __shared__ int sFlag, sTopJob, sIdx;
   int* stash = reinterpret_cast<int*>(dsm);  // the job's statics (fixed offsets)
   double* smem = dsm + kStashDbl;            // phase 1 / the top part / phase 2
   double* sTop = smem + da.lds_main;         // the top part's values (phase 2 reads them)
-  const int job = blockIdx.x;
   const int nj = pa.n_jobs;
   const unsigned last = da.epoch * (unsigned)nj + (unsigned)(nj - 1);
   const unsigned tag = (da.epoch + 1u) << 10;  // the top solver's announcement (job < 1024)
@@ -4666,8 +4839,24 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
       top_pre_idx(pa, pre);
       top_pre_val<true>(pa, nullptr, pre);
       NX_DSTAMP(6);
-      top_body<false, true>(pa, nullptr, nullptr, da.x, nullptr, nullptr, 0, nullptr, nullptr,
-                            kModeDirect, T, false, pre);
+      if constexpr (XR) {
+        // the rank's top part up to its coarse partials [D | J | G] (pc_coarse_partials: in
+        // cbuf; the top slots' D / J in slot_D / slot_J), then the exchange, then the coarse
+        // forest and the top part's back-substitution (k_pc_coarse's arithmetic: the same
+        // bits as the separate launches) from the sums
+        top_body<true, true>(pa, nullptr, nullptr, da.x, nullptr, nullptr, 0, nullptr, nullptr,
+                             kModeDirect, T, false, pre);
+        vm_drain();
+        __syncthreads();
+        if (!xr_coarse(pa, da, T)) {
+          if (threadIdx.x == 0)  // (the waiters give up too; the host reports the exchange)
+            __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
+      } else {
+        top_body<false, true>(pa, nullptr, nullptr, da.x, nullptr, nullptr, 0, nullptr, nullptr,
+                              kModeDirect, T, false, pre);
+      }
       NX_DSTAMP(7);
       vm_drain();
       __syncthreads();
@@ -4746,7 +4935,7 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
     lo0 = da.left_off[threadIdx.x];
     lo1 = da.left_off[threadIdx.x + 1];
   }
-  dir_down_v2<W, CPL>(pa, da, smem, sTop, S, L, keep, sA_, sB_);
+  dir_down_v2<W, CPL>(pa, da, smem, sTop, S, L, keep, sA_, sB_, job);
   // hand-off 2: the residual partials and shares -> the last workgroup publishes
   vm_drain();
   __syncthreads();
@@ -4758,7 +4947,12 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
   }
   __syncthreads();
   if (sFlag) {
-    dir_publish_fused(pa, da, lo0, lo1);
+    if constexpr (XR) {
+      if (!dir_publish_xr(pa, da, lo0, lo1) && threadIdx.x == 0)
+        __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      dir_publish_fused(pa, da, lo0, lo1);
+    }
     NX_DSTAMP(4);
   }
   // (the kernel's end, not the published state, waits for these; re-assembled: L kept
@@ -4774,6 +4968,28 @@ __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) 
   }
   vm_drain();
   NX_DSTAMP(40);
+}
+
+template <int W, int CPL>
+__global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) {
+  dir_step_body<W, CPL, false>(pa, da, blockIdx.x);
+}
+
+// one rank of several, one GPU each (RCCL ranks; the exchange over IPC-mapped peer memory)
+template <int W, int CPL>
+__global__ __launch_bounds__(kPcThreads) void k_dir_xr(PcArgs pa, DirStep da) {
+  dir_step_body<W, CPL, true>(pa, da, blockIdx.x);
+}
+
+// every rank of an in-process group in ONE launch (all their workgroups co-resident, so
+// the ranks' exchanges can wait for each other): workgroup -> (rank, job) by goff
+template <int W, int CPL>
+__global__ __launch_bounds__(kPcThreads) void k_dir_xg(const PcArgs* __restrict__ pas,
+                                                       const DirStep* __restrict__ das,
+                                                       const int* __restrict__ goff, int P) {
+  int r = 0;
+  while (r + 1 < P && (int)blockIdx.x >= goff[r + 1]) ++r;
+  dir_step_body<W, CPL, true>(pas[r], das[r], (int)blockIdx.x - goff[r]);
 }
 
 // k_dir_team_up: the first half of the several-rank direct step (one rank's share, before
@@ -5867,6 +6083,20 @@ struct nx_network {
   double* d_crec = nullptr;
   int* d_ci = nullptr;
   int dstep_main = 0, dstep_top = 0;
+  // several ranks (k_dir_xr / k_dir_xg, round 4): the fused step's tables hold (xr_ok); the
+  // publisher's own left rows (xr_nleft: the left rows that are not cut); this
+  // rank's mailbox (fine-grained; one block: mb1 | mb2 | flags), the peers' (device table,
+  // IPC-mapped for RCCL ranks), the launch tag; host copies of the cut lists
+  bool xr_ok = false;
+  int xr_nleft = 0;
+  void* xmb = nullptr;
+  XPeer* d_xpeers = nullptr;
+  std::vector<void*> xr_opened;  // peers' mailboxes opened by IPC (closed on destroy)
+  bool xr_linked = false;        // the peer table is set (group create / nx_xch_import)
+  bool xr_off = false;           // an exchange timed out: the graph path from then on
+  bool xr_all = false;           // RCCL: every rank can run the exchange step (check_schedules)
+  unsigned xtag = 0;
+  std::vector<int> gk_off_host, gk_row_host;
   size_t dstep_lds = 0;  // dynamic LDS bytes per workgroup
   unsigned* d_tsync = nullptr;  // k_dir_team_up's arrival counter (several ranks; pc_bufs)
   bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
@@ -5934,6 +6164,10 @@ struct nx_group {
   int P = 0;
   std::vector<nx_network*> hs;
   hipStream_t stream = nullptr;
+  // k_dir_xg: the ranks' PcArgs / DirStep and workgroup offsets in device memory (pinned
+  // staging: their contents change per launch -- the tags and sequence numbers)
+  void* xg_dev = nullptr;
+  void* xg_host = nullptr;
   hipGraphExec_t chunk_exec = nullptr;
   hipGraph_t chunk_graph = nullptr;
   int chunk_len = 0;
@@ -6778,12 +7012,20 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
   return NX_OK;
 }
 
+namespace {
+void xr_free(nx_network* h);
+int xr_alloc(nx_network* h, int P);
+int xr_link(nx_network* h, const std::vector<XPeer>& peers);
+XPeer xpeer_of(void* base, int P);
+}  // namespace
+
 NX_API int nx_destroy(nx_network_t* h) {
   if (h) h->pend_lhs = h->pend_rhs = 0;  // nothing to assemble for a dying handle
   if (h == nullptr) return NX_OK;
   if (h->group) return fail(NX_ERR_STATE, "destroy the group (nx_group_destroy) first");
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  xr_free(h);
   {
     nx_network* hs[1] = {h};
     (void)drop_graph(graph_slot(Team{hs, 1, nullptr}));
@@ -7197,6 +7439,7 @@ void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
   const void* fn = reinterpret_cast<const void*>(&k_dir_step<W, CPL>);
   if (std::find(opted.begin(), opted.end(), fn) == opted.end()) {
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kDirLdsMax);
+    (void)hipGetLastError();
     opted.push_back(fn);
   }
   hipExtLaunchKernelGGL((k_dir_step<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
@@ -7475,6 +7718,189 @@ int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false
 // ticket instead of k_dir_publish_fr -- 0.079 vs 0.072 ms/step: every workgroup's release
 // fence writes back its XCD's L2, dirty with x, before the ticket.)
 
+// ---- several ranks: the fused step with the device-side exchange (k_dir_xr / k_dir_xg) --
+constexpr int kXld1 = 3 * kCapCoarseLds, kXld2 = 2 + kCapCoarseLds;
+size_t xmb_bytes(int P) {
+  return sizeof(double) * (size_t)P * (kXld1 + kXld2) + sizeof(unsigned) * 2 * (size_t)P;
+}
+XPeer xpeer_of(void* base, int P) {
+  XPeer x;
+  x.mb1 = static_cast<double*>(base);
+  x.mb2 = x.mb1 + (size_t)P * kXld1;
+  x.fl = reinterpret_cast<unsigned*>(x.mb2 + (size_t)P * kXld2);
+  return x;
+}
+// this rank's mailbox: fine-grained (uncached) device memory -- the peers write into it over
+// xGMI and its reads must not hit a stale L2 line -- zeroed (flags start below every tag)
+int xr_alloc(nx_network* h, int P) {
+  if (h->xmb) return NX_OK;
+  HIPCALL(hipExtMallocWithFlags(&h->xmb, xmb_bytes(P), hipDeviceMallocUncached));
+  HIPCALL(hipMemset(h->xmb, 0, xmb_bytes(P)));
+  HIPCALL(hipMalloc((void**)&h->d_xpeers, sizeof(XPeer) * P));
+  return NX_OK;
+}
+void xr_free(nx_network* h) {
+  for (void* q : h->xr_opened) (void)hipIpcCloseMemHandle(q);
+  h->xr_opened.clear();
+  if (h->xmb) (void)hipFree(h->xmb);
+  if (h->d_xpeers) (void)hipFree(h->d_xpeers);
+  h->xmb = nullptr;
+  h->d_xpeers = nullptr;
+  h->xr_linked = false;
+}
+int xr_link(nx_network* h, const std::vector<XPeer>& peers) {
+  HIPCALL(hipMemcpy(h->d_xpeers, peers.data(), sizeof(XPeer) * peers.size(), hipMemcpyHostToDevice));
+  h->xr_linked = true;
+  h->sched_checked = false;  // (the ranks agree on the exchange in check_schedules)
+  return NX_OK;
+}
+bool xr_variant(int v) { return v == 5 || v == 1 || v == 2; }  // <8,2>, <16,2>, <16,4>
+size_t xr_static_lds(int v);  // the exchange kernels' static LDS (below)
+
+// one rank's share of the decision: its tables, its peers linked, the coarse / cut sizes
+// within the exchange's caps, one round of workgroups, the LDS
+bool xr_local(const nx_network* h) {
+  return h->xr_ok && h->xr_linked && h->pc && h->pc_lds && h->fres_ok && h->pa.exact &&
+         h->pc_jobs > 0 && h->pc_jobs <= h->n_cu && h->pa.n_coarse > 0 &&
+         h->pa.n_coarse <= kCapCoarseLds && h->n_cut >= 0 && h->n_cut <= kCapCoarseLds &&
+         h->top_nt > 0 && h->top_nt <= kTopThreads && h->pa.n_top_lvl <= kMaxTopLvl &&
+         xr_variant(h->pc_variant) && h->dstep_lds + xr_static_lds(h->pc_variant) <= 160 * 1024;
+}
+bool xr_env() {
+  const char* e = std::getenv("NXHIP_DIR_XR");  // read per solve: tests switch it
+  return e == nullptr || std::atoi(e) != 0;
+}
+// every rank runs it (group: all handles, co-resident in one launch; RCCL: check_schedules'
+// agreement), the assembly pending everywhere (it heads the launch)
+bool xr_on(const Team& t, bool with_asm) {
+  if (!with_asm || !xr_env() || !team_multi(t)) return false;
+  if (t.g) {
+    int jobs = 0;
+    for (int r = 0; r < t.P; ++r) {
+      if (!xr_local(t.hs[r]) || t.hs[r]->pc_variant != t.hs[0]->pc_variant) return false;
+      jobs += t.hs[r]->pc_jobs;
+    }
+    return jobs <= t.hs[0]->n_cu;
+  }
+  return t.hs[0]->sched_checked && t.hs[0]->xr_all && xr_local(t.hs[0]);
+}
+
+DirStep dir_args(nx_network* h, double rtol) {
+  return DirStep{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
+                 h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
+                 h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
+                 h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1,
+                 h->d_seq, h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci,
+                 h->dstep_main, h->dstep_top, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u};
+}
+
+template <int W, int CPL>
+int launch_xr_wc(const Team& t, double rtol) {
+  const int P = t.P;
+  std::vector<DirStep> das(P);
+  std::vector<int> goff(P + 1, 0);
+  size_t lds = 0;
+  for (int r = 0; r < P; ++r) {
+    nx_network* h = t.hs[r];
+    h->xtag += 1;  // (the same on every rank: they launch together)
+    DirStep da = dir_args(h, rtol);
+    da.n_left = h->xr_nleft;
+    da.xpeers = h->d_xpeers;
+    da.xself = xpeer_of(h->xmb, P);
+    da.xP = P;
+    da.xrank = h->rank;
+    da.xld1 = kXld1;
+    da.xld2 = kXld2;
+    da.xK = h->n_cut;
+    da.xtag = h->xtag;
+    das[r] = da;
+    goff[r + 1] = goff[r] + h->pc_jobs;
+    lds = std::max(lds, h->dstep_lds);
+  }
+  if (t.g) {  // one launch of every rank's workgroups
+    nx_group* g = t.g;
+    const size_t bp = sizeof(PcArgs) * P, bd = sizeof(DirStep) * P, bo = sizeof(int) * (P + 1);
+    if (!g->xg_dev) {
+      HIPCALL(hipMalloc(&g->xg_dev, bp + bd + bo));
+      HIPCALL(hipHostMalloc(&g->xg_host, bp + bd + bo, hipHostMallocDefault));
+    }
+    char* hb = static_cast<char*>(g->xg_host);
+    for (int r = 0; r < P; ++r) std::memcpy(hb + sizeof(PcArgs) * r, &t.hs[r]->pa, sizeof(PcArgs));
+    std::memcpy(hb + bp, das.data(), bd);
+    std::memcpy(hb + bp + bd, goff.data(), bo);
+    HIPCALL(hipMemcpyAsync(g->xg_dev, g->xg_host, bp + bd + bo, hipMemcpyHostToDevice, g->stream));
+    const char* db = static_cast<const char*>(g->xg_dev);
+    const void* fn = reinterpret_cast<const void*>(&k_dir_xg<W, CPL>);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(160 * 1024 - xr_static_lds(t.hs[0]->pc_variant)));
+    (void)hipGetLastError();
+    hipLaunchKernelGGL((k_dir_xg<W, CPL>), dim3(goff[P]), dim3(kPcThreads), lds, g->stream,
+                       reinterpret_cast<const PcArgs*>(db), reinterpret_cast<const DirStep*>(db + bp),
+                       reinterpret_cast<const int*>(db + bp + bd), P);
+    HIPCALL(hipStreamSynchronize(g->stream));  // (the pinned staging is rewritten next launch)
+  } else {
+    nx_network* h = t.hs[0];
+    const void* fn = reinterpret_cast<const void*>(&k_dir_xr<W, CPL>);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(160 * 1024 - xr_static_lds(h->pc_variant)));
+    (void)hipGetLastError();
+    hipLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
+                       h->stream, h->pa, das[0]);
+  }
+  HIPCALL(hipGetLastError());
+  for (int r = 0; r < P; ++r) {
+    t.hs[r]->dstep_epoch += 1;
+    t.hs[r]->seq += 1;
+  }
+  return NX_OK;
+}
+int launch_xr(const Team& t, double rtol) {
+  switch (t.hs[0]->pc_variant) {
+    case 5: return launch_xr_wc<8, 2>(t, rtol);
+    case 1: return launch_xr_wc<16, 2>(t, rtol);
+    default: return launch_xr_wc<16, 4>(t, rtol);
+  }
+}
+size_t xr_static_lds(int v) {
+  static size_t s[3] = {0, 0, 0};
+  const int i = v == 5 ? 0 : v == 1 ? 1 : 2;
+  if (!s[i]) {
+    hipFuncAttributes a{};
+    const void* fn = i == 0 ? reinterpret_cast<const void*>(&k_dir_xr<8, 2>)
+                   : i == 1 ? reinterpret_cast<const void*>(&k_dir_xr<16, 2>)
+                            : reinterpret_cast<const void*>(&k_dir_xr<16, 4>);
+    s[i] = hipFuncGetAttributes(&a, fn) == hipSuccess ? a.sharedSizeBytes : 64 * 1024;
+  }
+  return s[i];
+}
+
+// The exchange step of every rank of the team and its published residual (the same on
+// every rank). NX_ERR_STATE: an exchange never completed (the hand-off counters are reset;
+// the caller takes the graph path for this and every later solve of the team).
+int run_xr(const Team& t, double rtol) {
+  CHECK(launch_xr(t, rtol));
+  int rc = NX_OK;
+  for (int r = 0; r < t.P && rc == NX_OK; ++r) rc = wait_published(t.hs[r]);
+  if (rc == NX_ERR_STATE) {
+    (void)hipGetLastError();
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      HIPCALL(hipStreamSynchronize(h->stream));
+      HIPCALL(hipMemset(h->d_dsync, 0, 8 * sizeof(unsigned)));
+      HIPCALL(hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost));
+      h->dstep_epoch = 0;
+      h->xr_off = true;
+    }
+    return rc;
+  }
+  CHECK(rc);
+  const MrState& s0 = *t.hs[0]->h_last;
+  for (int r = 1; r < t.P; ++r)
+    if (t.hs[r]->h_last->relres != s0.relres && s0.relres == s0.relres)
+      return fail(NX_ERR_STATE, "ranks disagree on the exchange step's residual");
+  return NX_OK;
+}
+
 int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
                  int32_t* converged) {
   const bool multi = team_multi(t);
@@ -7490,7 +7916,26 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   // the deferred assembly heads the solve (every rank's, several ranks)
   bool with_asm = true;
   for (int r = 0; r < t.P; ++r) with_asm = with_asm && t.hs[r]->pend_lhs && t.hs[r]->pend_rhs;
-  h->last_dir_path = 0;
+  for (int r = 0; r < t.P; ++r) t.hs[r]->last_dir_path = 0;
+  if (multi && !h->xr_off && xr_on(t, with_asm)) {  // several ranks: one launch each
+    const int rc = run_xr(t, rtol);
+    if (rc == NX_OK) {
+      for (int r = 0; r < t.P; ++r) {
+        t.hs[r]->pend_lhs = t.hs[r]->pend_rhs = 0;
+        t.hs[r]->last_dir_path = 3;
+      }
+      const MrState s = *h->h_last;
+      if (s.converged || s.relres != s.relres) {
+        if (iters) *iters = 1;
+        if (relres) *relres = s.relres;
+        if (converged) *converged = s.converged;
+        return NX_OK;
+      }
+      with_asm = false;  // (above rtol: the graph path below solves it again and refines)
+    } else if (rc != NX_ERR_STATE) {
+      return rc;
+    }
+  }
   if (with_asm && dstep_on(h)) {  // the fused step: assembly + solve + check in one launch
     const int rc = run_dstep(h, rtol, prof1);
     if (rc == NX_OK) {
@@ -7747,17 +8192,18 @@ int check_schedules(const Team& t) {
   if (!h->comm || h->sched_checked) return NX_OK;
   // max of s and of -s over the ranks: equal iff all ranks agree; the last entry is the
   // max of -direct_local: the direct solve runs only if every rank can run it
-  int v[2 * kSchedSig + 1];
+  int v[2 * kSchedSig + 2];
   for (int i = 0; i < kSchedSig; ++i) {
     v[i] = s0[i];
     v[kSchedSig + i] = -s0[i];
   }
   v[2 * kSchedSig] = direct_local(h) ? -1 : 0;
+  v[2 * kSchedSig + 1] = xr_local(h) ? -1 : 0;  // the exchange step only if every rank can
   int* d = nullptr;
   HIPCALL(hipMalloc((void**)&d, sizeof(v)));
   int rc = NX_OK;
   if (hipMemcpy(d, v, sizeof(v), hipMemcpyHostToDevice) != hipSuccess ||
-      ncclAllReduce(d, d, 2 * kSchedSig + 1, ncclInt32, ncclMax, h->comm, h->stream) != ncclSuccess ||
+      ncclAllReduce(d, d, 2 * kSchedSig + 2, ncclInt32, ncclMax, h->comm, h->stream) != ncclSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess ||
       hipMemcpy(v, d, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(NX_ERR_RCCL, "kernel schedule comparison across ranks failed");
@@ -7769,6 +8215,7 @@ int check_schedules(const Team& t) {
                                     std::to_string(i) + ": preconditioner decomposition "
                                     "outside the LDS caps on some ranks)");
   h->direct_all = v[2 * kSchedSig] == -1;
+  h->xr_all = v[2 * kSchedSig + 1] == -1;
   h->sched_checked = true;
   return NX_OK;
 }
@@ -8591,10 +9038,16 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
       const int rc = build_left_cut(h);
       if (rc != NX_OK) return rc;
     }
-    // the fused direct step (one rank): every slot a job reads outside itself -- its root's
-    // parent, its chains' far ends -- is a top slot (the down sweep takes it from the top
-    // values), and the left rows get their flux-end shares posted (chain order per row)
-    if (h->fres_ok && h->nranks == 1 && h->n_ghost == 0) {
+    // the fused direct step (one rank, or a rank of several with its cut rows set): every
+    // slot a job reads outside itself -- its root's parent, its chains' far ends -- is a top
+    // slot (the down sweep takes it from the top values), and the rows no job forms get
+    // their flux-end shares posted (chain order per row): the left rows and, with several
+    // ranks, every cut bifurcation's row (owned or not: the K entries after the left rows,
+    // which the publisher exchanges) instead of the cut rows among the left ones
+    const bool xr_tables = h->nranks > 1 && h->n_cut >= 0;
+    h->xr_ok = false;
+    h->xr_nleft = 0;
+    if (h->fres_ok && (h->nranks == 1 ? h->n_ghost == 0 : xr_tables)) {
       const int ts0 = top_lvl_off[0], ts1 = top_lvl_off[n_top_lvl];
       auto top = [&](int j) { return j >= ts0 && j < ts1; };
       bool ok = true;
@@ -8607,22 +9060,55 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
         const int p = slot_parent[j];
         if (job_of_slot[j] >= 0 && p >= 0 && job_of_slot[p] != job_of_slot[j] && !top(p)) ok = false;
       }
+      const int K = xr_tables ? h->n_cut : 0;
+      std::vector<int> dleft;  // the fused publisher's own rows: left rows that are not cut
+      for (int r : left)
+        if (!(xr_tables && h->lm_cut[r - h->n_edge_dofs] >= 0)) dleft.push_back(r);
+      const int nl = (int)dleft.size();
       std::vector<int> row_of(h->n_own - h->n_edge_dofs, -1);
-      for (size_t i = 0; i < left.size(); ++i) row_of[left[i] - h->n_edge_dofs] = (int)i;
-      std::vector<int> off(left.size() + 1, 0), fill(left.size(), 0);
+      for (int i = 0; i < nl; ++i) row_of[dleft[i] - h->n_edge_dofs] = i;
+      if (xr_tables)  // owned cut rows: entry nl + k
+        for (int64_t m = 0; m < (int64_t)row_of.size(); ++m)
+          if (h->lm_cut[m] >= 0) row_of[m] = nl + h->lm_cut[m];
+      std::vector<int> cut_of_row;  // a ghost junction's cut index by this rank's flux-end row
+      if (xr_tables) {
+        cut_of_row.assign(h->n_edge_dofs, -1);
+        for (int k = 0; k < K; ++k)
+          for (int e = h->gk_off_host[k]; e < h->gk_off_host[k + 1]; ++e)
+            cut_of_row[h->gk_row_host[e]] = nl + k;
+      }
+      const int N2 = 2 * N + 1;
+      // the post group of chain c's end (0 top, 1 bottom) at slot j, or -1
+      auto row_at = [&](int64_t c, int end, int j) {
+        if (j < 0) return -1;
+        const int lam = slot_lam[j];
+        if (lam < h->n_own) return row_of[lam - h->n_edge_dofs];
+        if (!xr_tables) return -1;
+        const int e = chain_edge[c], fl = chain_flip[c];  // the chain's end flux row
+        const bool q0 = (end == 0) != (fl != 0);
+        return cut_of_row[(int64_t)e * N2 + (q0 ? 0 : 2 * N)];
+      };
+      std::vector<int> off(nl + K + 1, 0), fill(nl + K, 0);
       std::vector<int> cpost(2 * std::max<int64_t>(n_chains, 1), -1);
-      auto row_at = [&](int j) { return j < 0 ? -1 : row_of[slot_lam[j] - h->n_edge_dofs]; };
       for (int64_t c = 0; c < n_chains; ++c)
         for (int end = 0; end < 2; ++end) {
-          const int r = row_at(end ? chain_lo[c] : chain_up[c]);
+          const int r = row_at(c, end, end ? chain_lo[c] : chain_up[c]);
           if (r >= 0) off[r + 1] += 1;
         }
-      for (size_t i = 0; i < left.size(); ++i) off[i + 1] += off[i];
+      for (int i = 0; i < nl + K; ++i) off[i + 1] += off[i];
       for (int64_t c = 0; c < n_chains; ++c)
         for (int end = 0; end < 2; ++end) {
-          const int r = row_at(end ? chain_lo[c] : chain_up[c]);
+          const int r = row_at(c, end, end ? chain_lo[c] : chain_up[c]);
           if (r >= 0) cpost[2 * c + end] = off[r] + fill[r]++;
         }
+      if (xr_tables) {  // every ghost junction end must have found its cut row
+        for (int64_t c = 0; c < n_chains && ok; ++c)
+          for (int end = 0; end < 2; ++end) {
+            const int j = end ? chain_lo[c] : chain_up[c];
+            if (j >= 0 && slot_lam[j] >= h->n_own && cpost[2 * c + end] < 0) ok = false;
+          }
+        h->xr_nleft = nl;
+      }
       h->d_chain_post = const_cast<int*>(up(cpost.data(), (int64_t)cpost.size()));
       h->d_left_off = const_cast<int*>(up(off.data(), (int64_t)off.size()));
       h->d_post = scratch(std::max(1, off.back()));
@@ -8632,7 +9118,11 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
         if (hipMemset(sy, 0, 8 * sizeof(unsigned)) != hipSuccess) sy = nullptr;
       }
       h->d_dsync = sy;
-      h->dstep_ok = ok && h->d_chain_post && h->d_left_off && h->d_post && h->d_dsync;
+      const bool tables = ok && h->d_chain_post && h->d_left_off && h->d_post && h->d_dsync;
+      if (xr_tables)
+        h->xr_ok = tables;  // (the exchange itself is checked per solve: xr_on)
+      else
+        h->dstep_ok = tables;
     }
   }
   pa.top_reg = 1;
@@ -8777,7 +9267,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->d_job_hdr = nullptr;
   h->d_crec = nullptr;
   h->d_ci = nullptr;
-  if (h->dstep_ok) {
+  if (h->dstep_ok || h->xr_ok) {
     std::vector<int> hdr((size_t)kJobHdr * n_jobs, 0);
     int mlv = 1, mns = 0, mnd = 0;
     for (int jb = 0; jb < n_jobs; ++jb) {
@@ -8814,8 +9304,10 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     h->d_job_hdr = const_cast<int*>(up(hdr.data(), (int64_t)hdr.size()));
     h->d_crec = scratch(10 * std::max<int64_t>(n_chains, 1));
     h->d_ci = const_cast<int*>(up(nullptr, 4 * std::max<int64_t>(n_chains, 1)));
-    h->dstep_ok = h->d_job_hdr && h->d_crec && h->d_ci && fits &&
-                  h->dstep_lds <= (size_t)kDirLdsMax;
+    const bool hdr_ok = h->d_job_hdr && h->d_crec && h->d_ci && fits;
+    h->dstep_ok = h->dstep_ok && hdr_ok && h->dstep_lds <= (size_t)kDirLdsMax;
+    // (several ranks: the coarse exchange's static LDS comes on top; checked at launch)
+    h->xr_ok = h->xr_ok && hdr_ok;
   }
   h->pc_lds = lds;
   h->pa = pa;
@@ -9299,6 +9791,8 @@ NX_API int nx_set_cut(nx_network_t* h, int32_t K, const int32_t* lm_cut, const i
   CHECK(upload(&h->d_gk_coef, coef.data(), (int64_t)coef.size(), h->stream));
   CHECK(dalloc(&h->cutbuf, 2 + (int64_t)K));
   h->lm_cut.assign(lm_cut ? lm_cut : nullptr, lm_cut ? lm_cut + n_lm : nullptr);
+  h->gk_off_host = off;
+  h->gk_row_host.assign(gk_row ? gk_row : nullptr, gk_row ? gk_row + ne : nullptr);
   h->n_cut = K;
   h->sched_checked = false;  // the residual's exchange is part of the schedule signature
   if (!h->left_host.empty() || h->d_left) CHECK(build_left_cut(h));
@@ -9378,6 +9872,142 @@ NX_API int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const uns
   return NX_OK;
 }
 
+namespace {
+// The exchange step of ONE rank alone, its exchanges emulated (rehearsal of a multi-GPU run
+// on one GPU, whose ranks cannot all be resident at once): the rank writes its slots into a
+// scratch mailbox, and reads the sums the group's graph path left (cbuf; cutbuf) from slot 0
+// of a mailbox whose other slots are zero and whose flags are set. Same work as the rank's
+// launch in the real run, minus the wait for the others and the xGMI hops.
+template <int W, int CPL>
+int xr_rehearse_wc(nx_network* h, int P, double rtol, int reps, float* ms_out) {
+  const size_t nb = xmb_bytes(P);
+  void *rd = nullptr, *wr = nullptr;
+  XPeer* dpeers = nullptr;
+  int rc = NX_OK;
+  auto cleanup = [&]() {
+    if (rd) (void)hipFree(rd);
+    if (wr) (void)hipFree(wr);
+    if (dpeers) (void)hipFree(dpeers);
+  };
+  const unsigned tag = 0x7f000001u;
+  {
+    std::vector<double> img(nb / sizeof(double) + 1, 0.0);
+    XPeer x = xpeer_of(img.data(), P);
+    const int nC = h->pa.n_coarse, K = h->n_cut;
+    if (hipMemcpy(x.mb1, h->pa.cbuf, sizeof(double) * 3 * nC, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(x.mb2, h->cutbuf, sizeof(double) * (2 + K), hipMemcpyDeviceToHost) != hipSuccess) {
+      cleanup();
+      return fail(NX_ERR_HIP, "rehearsal: reading the graph path's sums failed");
+    }
+    for (int k = 0; k < K; ++k) x.mb2[2 + k] = -x.mb2[2 + k];  // (the publisher forms 0 - sum)
+    for (int i = 0; i < 2 * P; ++i) x.fl[i] = tag;
+    if (hipMalloc(&rd, nb) != hipSuccess || hipMalloc(&wr, nb) != hipSuccess ||
+        hipMalloc((void**)&dpeers, sizeof(XPeer) * P) != hipSuccess ||
+        hipMemcpy(rd, img.data(), nb, hipMemcpyHostToDevice) != hipSuccess) {
+      cleanup();
+      return fail(NX_ERR_HIP, "rehearsal: mailbox allocation failed");
+    }
+    std::vector<XPeer> peers(P, xpeer_of(wr, P));
+    if (hipMemcpy(dpeers, peers.data(), sizeof(XPeer) * P, hipMemcpyHostToDevice) != hipSuccess) {
+      cleanup();
+      return fail(NX_ERR_HIP, "rehearsal: peer table upload failed");
+    }
+  }
+  hipEvent_t e0, e1;
+  HIPCALL(hipEventCreate(&e0));
+  HIPCALL(hipEventCreate(&e1));
+  const void* fn = reinterpret_cast<const void*>(&k_dir_xr<W, CPL>);
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(160 * 1024 - xr_static_lds(h->pc_variant)));
+  (void)hipGetLastError();
+  float total = 0.f;
+  for (int k = 0; k <= reps && rc == NX_OK; ++k) {  // (launch 0: warm-up, not timed)
+    DirStep da = dir_args(h, rtol);
+    da.n_left = h->xr_nleft;
+    da.xpeers = dpeers;
+    da.xself = xpeer_of(rd, P);
+    da.xP = P;
+    da.xrank = h->rank;
+    da.xld1 = kXld1;
+    da.xld2 = kXld2;
+    da.xK = h->n_cut;
+    da.xtag = tag;
+    hipExtLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
+                          h->stream, e0, e1, 0, h->pa, da);
+    if (hipGetLastError() != hipSuccess) rc = fail(NX_ERR_HIP, "rehearsal launch failed");
+    h->dstep_epoch += 1;
+    h->seq += 1;
+    if (rc == NX_OK) rc = wait_published(h);
+    float ms = 0.f;
+    if (rc == NX_OK && hipEventSynchronize(e1) == hipSuccess &&
+        hipEventElapsedTime(&ms, e0, e1) == hipSuccess && k > 0)
+      total += ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamSynchronize(h->stream);
+  cleanup();
+  if (rc == NX_OK) *ms_out = total / (float)std::max(reps, 1);
+  return rc;
+}
+}  // namespace
+
+// Test / rehearsal hook (no reference counterpart): the exchange step of rank h of a group
+// alone, reps timed launches (HIP events bound to the dispatch), its exchanges emulated from
+// the sums of the group's previous graph-path direct solve (scripts/group_rehearsal.py).
+// The solution left in h's x is the rank's share of the real answer.
+NX_API int nx_debug_xr_rehearse(nx_network_t* h, double rtol, int32_t reps, double* ms) {
+  if (!h || !ms) return fail(NX_ERR_ARG, "null argument");
+  if (!h->group) return fail(NX_ERR_STATE, "a group member (its graph path solved first)");
+  if (!h->xr_ok || !xr_variant(h->pc_variant) || h->pa.n_coarse <= 0 || h->n_cut < 0 ||
+      h->pa.n_coarse > kCapCoarseLds || h->n_cut > kCapCoarseLds)
+    return fail(NX_ERR_STATE, "this rank cannot run the exchange step");
+  CHECK(set_device(h));
+  float v = 0.f;
+  int rc;
+  switch (h->pc_variant) {
+    case 5: rc = xr_rehearse_wc<8, 2>(h, h->nranks, rtol, reps, &v); break;
+    case 1: rc = xr_rehearse_wc<16, 2>(h, h->nranks, rtol, reps, &v); break;
+    default: rc = xr_rehearse_wc<16, 4>(h, h->nranks, rtol, reps, &v); break;
+  }
+  *ms = v;
+  return rc;
+}
+
+NX_API int nx_xch_export(nx_network_t* h, unsigned char* handle_out) {
+  if (!h || !handle_out) return fail(NX_ERR_ARG, "null argument");
+  if (!h->comm) return fail(NX_ERR_STATE, "nx_comm_init first");
+  CHECK(set_device(h));
+  CHECK(xr_alloc(h, h->nranks));
+  hipIpcMemHandle_t m;
+  HIPCALL(hipIpcGetMemHandle(&m, h->xmb));
+  static_assert(sizeof(hipIpcMemHandle_t) <= NX_XCH_HANDLE_BYTES, "IPC handle size");
+  std::memset(handle_out, 0, NX_XCH_HANDLE_BYTES);
+  std::memcpy(handle_out, &m, sizeof(m));
+  return NX_OK;
+}
+
+NX_API int nx_xch_import(nx_network_t* h, const unsigned char* handles) {
+  if (!h || !handles) return fail(NX_ERR_ARG, "null argument");
+  if (!h->comm || !h->xmb) return fail(NX_ERR_STATE, "nx_xch_export first");
+  CHECK(set_device(h));
+  const int P = h->nranks;
+  std::vector<XPeer> peers(P);
+  for (int q = 0; q < P; ++q) {
+    if (q == h->rank) {
+      peers[q] = xpeer_of(h->xmb, P);
+      continue;
+    }
+    hipIpcMemHandle_t m;
+    std::memcpy(&m, handles + (size_t)q * NX_XCH_HANDLE_BYTES, sizeof(m));
+    void* ptr = nullptr;
+    HIPCALL(hipIpcOpenMemHandle(&ptr, m, hipIpcMemLazyEnablePeerAccess));
+    h->xr_opened.push_back(ptr);
+    peers[q] = xpeer_of(ptr, P);
+  }
+  return xr_link(h, peers);
+}
+
 NX_API int nx_group_create(int32_t nranks, nx_network_t* const* handles, nx_group_t** out) {
   if (!out || !handles) return fail(NX_ERR_ARG, "null argument");
   *out = nullptr;
@@ -9386,7 +10016,8 @@ NX_API int nx_group_create(int32_t nranks, nx_network_t* const* handles, nx_grou
   for (int r = 0; r < nranks; ++r) {
     nx_network* h = handles[r];
     if (!h) return fail(NX_ERR_ARG, "null handle in group");
-    CHECK(flush_assembly(h));
+    // (a deferred nx_assemble stays pending: the group's first direct solve runs it inside
+    // its own launch, on the group's stream)
     if (h->group || h->comm) return fail(NX_ERR_STATE, "handle already has a transport");
     if (h->device != handles[0]->device) return fail(NX_ERR_ARG, "group members share one device");
     if (nranks > 1 && (!h->have_plan || h->rank != r || h->nranks != nranks))
@@ -9428,6 +10059,16 @@ NX_API int nx_group_create(int32_t nranks, nx_network_t* const* handles, nx_grou
     h->stream = g->stream;
     h->group = g;
   }
+  // the exchange step's mailboxes (k_dir_xg): each rank writes into every rank's own
+  if (nranks > 1) {
+    std::vector<XPeer> peers(nranks);
+    int rc = NX_OK;
+    for (int r = 0; r < nranks && rc == NX_OK; ++r) rc = xr_alloc(g->hs[r], nranks);
+    for (int r = 0; r < nranks && rc == NX_OK; ++r) peers[r] = xpeer_of(g->hs[r]->xmb, nranks);
+    for (int r = 0; r < nranks && rc == NX_OK; ++r) rc = xr_link(g->hs[r], peers);
+    if (rc != NX_OK)  // (no exchange step: the graph path)
+      for (nx_network* h : g->hs) xr_free(h);
+  }
   *out = g;
   return NX_OK;
 }
@@ -9447,7 +10088,10 @@ NX_API int nx_group_destroy(nx_group_t* g) {
     h->stream = h->own_stream;
     h->own_stream = nullptr;
     h->group = nullptr;
+    xr_free(h);  // (the peers were the group's)
   }
+  if (g->xg_dev) (void)hipFree(g->xg_dev);
+  if (g->xg_host) (void)hipHostFree(g->xg_host);
   (void)hipStreamDestroy(g->stream);
   delete g;
   return NX_OK;

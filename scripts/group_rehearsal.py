@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--N", type=int, default=19)
     ap.add_argument("--solver", choices=("direct", "minres"), default="direct")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--exchange", action="store_true",
+                    help="also time every rank's one-launch exchange step alone "
+                         "(nx_debug_xr_rehearse: its exchanges emulated)")
     args = ap.parse_args()
     levels = args.levels + int(round(math.log2(args.ranks)))
     t0 = time.perf_counter()
@@ -76,6 +79,20 @@ def main() -> int:
         print(f"solver {grp.solver_used}", flush=True)
         want = (1, 2) if grp.solver_used == "direct" else (3,)
         ok = conv and it in want and err < 1e-10 and not np.isnan(x).any()
+        if args.exchange and grp.solver_used == "direct":
+            # every rank's exchange step alone (one launch per rank, as on its own GPU), its
+            # exchanges emulated from this graph-path solve's sums; then its answer again
+            ms = [a.handle.xr_rehearse(1e-12, 20) for a in grp.assemblers]
+            x2 = np.full(xa.size, np.nan)
+            for a in grp.assemblers:
+                x2[DM.global_rows(a.local_problem, mesh0.num_edges,
+                                  mesh0.bifurcation_index)] = a.handle.solution()
+            err2 = float(np.linalg.norm(x2 - xa) / np.linalg.norm(xa))
+            print("exchange step per rank (us): " + " ".join(f"{1e3 * m:.1f}" for m in ms),
+                  flush=True)
+            print(f"exchange step: slowest rank {1e3 * max(ms):.1f} us, rel. error vs analytic "
+                  f"{err2:.3e}", flush=True)
+            ok = ok and err2 < 1e-10
         print("REHEARSAL OK" if ok else "REHEARSAL FAILED", flush=True)
         return 0 if ok else 1
     finally:

@@ -172,6 +172,7 @@ def test_group_direct_cut_rows_in_one_allreduce(case, P, monkeypatch):
     (NXHIP_DIR_COARSE_DOWN=0): the same solution bit for bit, the same reported residual to
     its rounding, and a forced refinement pass (which starts from the stored cut rows' r and
     refines the top values in the down sweeps) converges to the true residual."""
+    monkeypatch.setenv("NXHIP_DIR_XR", "0")  # the graph path's modes (the exchange step: below)
     make, N, strategy, pbc = CASES[case]
     G, mesh, Ab, bb, x_ref = _reference(case)
     grp = RankGroup(G, N, P, color_strategy=strategy)
@@ -453,8 +454,8 @@ def test_group_direct_solve(case, P):
     grp = RankGroup(G, N, P, color_strategy=strategy)
     try:
         grp.compute_forms(p_bc_ex=pbc)
-        grp.assemble()
         grp.set_direct(True)
+        grp.assemble()  # (pending: both solves below take the same path -- the exchange step)
         it, relres, conv = grp.solve(1e-12, 50000, 4)
         assert conv, (it, relres)
         is_tree = mesh.num_edges == mesh.num_nodes - 1
@@ -476,5 +477,75 @@ def test_group_direct_solve(case, P):
         for a, xl in zip(grp.assemblers, grp.solutions()):
             x2[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
         np.testing.assert_array_equal(x2, x)
+    finally:
+        grp.close()
+
+
+def _gathered(grp, Ab, mesh):
+    x = np.zeros(Ab.shape[0])
+    for a, xl in zip(grp.assemblers, grp.solutions()):
+        x[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
+    return x
+
+
+@pytest.mark.parametrize("case,P", [("depth6_N40", 2), ("depth6_N40", 4), ("arterial5_N40", 3),
+                                    ("Y_N4", 2), ("linear_alt_N3", 3), ("tree5_N15", 4)])
+def test_group_exchange_step(case, P, monkeypatch):
+    """The direct step of several ranks in ONE launch per rank (k_dir_xg: every rank's
+    workgroups in one launch, exchanging the coarse partials and the residual's partials
+    through device mailboxes instead of the two RCCL all-reduces): the oracle's solution to
+    1e-10, the graph path's (NXHIP_DIR_XR=0) to its rounding, the reported residual the true
+    one, the same bits on every repeated step, and the ranks' published residuals equal."""
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.set_direct(True)
+        grp.assemble()
+        it, rr, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and it == 1 and grp.solver_used == "direct"
+        paths = {a.handle.direct_path() for a in grp.assemblers}
+        assert paths == {"exchange"}, paths
+        x1 = _gathered(grp, Ab, mesh)
+        assert np.linalg.norm(x1 - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+        true1 = np.linalg.norm(bb - Ab @ x1) / np.linalg.norm(bb)
+        assert abs(rr - true1) <= 0.05 * true1 + 5e-16, (rr, true1)
+        for _ in range(20):  # the exchanges' tags move on; the bits do not
+            grp.assemble()
+            it2, rr2, _ = grp.solve(1e-12, 50000, 4)
+            assert rr2 == rr and {a.handle.direct_path() for a in grp.assemblers} == {"exchange"}
+            np.testing.assert_array_equal(_gathered(grp, Ab, mesh), x1)
+        monkeypatch.setenv("NXHIP_DIR_XR", "0")  # the graph path (RCCL-shaped all-reduces)
+        grp.assemble()
+        it0, rr0, conv0 = grp.solve(1e-12, 50000, 4)
+        assert conv0 and {a.handle.direct_path() for a in grp.assemblers} == {"launches"}
+        x0 = _gathered(grp, Ab, mesh)
+        assert np.linalg.norm(x0 - x1) <= 1e-14 * np.linalg.norm(x1)
+        assert abs(rr0 - rr) <= 0.05 * rr0 + 5e-16, (rr0, rr)
+    finally:
+        grp.close()
+
+
+def test_group_exchange_give_up_falls_back():
+    """Every waiting workgroup gives up (a wait bound of 0 polls): no rank publishes, the host
+    resets the hand-off counters and sequence numbers, and the same solve runs the graph
+    path -- correct, and so is every later step."""
+    case, P = "depth6_N40", 3
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.set_direct(True)
+        for a in grp.assemblers:
+            a.handle.set_wait_polls(0)
+        for _ in range(3):
+            grp.assemble()
+            it, rr, conv = grp.solve(1e-12, 50000, 4)
+            assert conv and grp.solver_used == "direct"
+            assert {a.handle.direct_path() for a in grp.assemblers} == {"launches"}
+            x = _gathered(grp, Ab, mesh)
+            assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
     finally:
         grp.close()
