@@ -4626,7 +4626,7 @@ __device__ __forceinline__ double ld_sys(const double* p) {
 // then this rank's P flags polled (bounded) and the P slots summed in rank order (the same
 // additions as k_group_sum: every rank gets the same bits) into dst (LDS). False: a rank's
 // flag never came.
-__device__ bool xr_allsum(const DirStep& da, int which, const double* src, int n, double* dst) {
+__device__ __forceinline__ bool xr_allsum(const DirStep& da, int which, const double* src, int n, double* dst) {
   __shared__ int sOk;
   const int P = da.xP, r = da.xrank, ld = which ? da.xld2 : da.xld1;
   for (int q = 0; q < P; ++q) {
@@ -4663,22 +4663,60 @@ __device__ bool xr_allsum(const DirStep& da, int which, const double* src, int n
   return true;
 }
 
+// The coarse step's static set-up of this thread's top slot (coarse_top_pre's indices),
+// loaded with the top part's own indices, and its parent chain's T with the top part's
+// inputs (posted by phase 1): nothing of the coarse step waits for a load after the exchange.
+struct CoarseIdx {
+  int k, par, pch, lvo, cw0, cw1;
+  double T;
+};
+__device__ __forceinline__ void coarse_idx_load(const PcArgs& pa, CoarseIdx& c) {
+  const int sl = threadIdx.x, ts0 = pa.top_ts0, nt = pa.top_nt;
+  c.lvo = sl <= pa.n_top_lvl ? pa.top_lvl_off[sl] : 0;
+  const bool cw = pa.c_wave && sl < pa.n_coarse;
+  c.cw0 = cw ? pa.c_wave[2 * sl] : 0;
+  c.cw1 = cw ? pa.c_wave[2 * sl + 1] : 0;
+  c.k = sl < nt ? pa.slot_cidx[ts0 + sl] : -1;
+  c.par = sl < nt ? pa.slot_parent[ts0 + sl] : -1;
+  c.pch = sl < nt ? pa.slot_pchain[ts0 + sl] : -1;
+  c.T = 1.0;
+}
+__device__ __forceinline__ void coarse_idx_val(const PcArgs& pa, CoarseIdx& c) {
+  if (c.k < 0 && c.par >= 0 && c.pch >= 0) c.T = ld_wt(pa.chain_T + c.pch);
+}
+
 // The top part's solver after top_body<MULTI>: exchange 1 of the coarse partials (cbuf),
 // the sums back into cbuf, the coarse forest and the top part's back-substitution
-// (coarse_top_pre / coarse_top_block, k_pc_coarse's arithmetic) into LDS, then the top
-// values to slot_z (write-through: the rank's other workgroups read them) and to x.
-__device__ bool xr_coarse(const PcArgs& pa, const DirStep& da, const TopLds& T) {
+// (coarse_top_block, k_pc_coarse's arithmetic: coarse_top_pre's values, from LDS and the
+// prefetched ci) into LDS, then the top values to slot_z (write-through: the rank's other
+// workgroups read them) and to x.
+__device__ __forceinline__ bool xr_coarse(const PcArgs& pa, const DirStep& da, const TopLds& T,
+                                          const CoarseIdx& ci) {
   __shared__ double xb[2 * 3 * kCapCoarseLds];
   const int nC = pa.n_coarse, n1 = 3 * nC;
   for (int i = threadIdx.x; i < n1; i += kPcThreads) xb[i] = ld_wt(pa.cbuf + i);
   __syncthreads();
   if (!xr_allsum(da, 0, xb, n1, xb + n1)) return false;
-  for (int i = threadIdx.x; i < n1; i += kPcThreads) pa.cbuf[i] = xb[n1 + i];
-  vm_drain();
-  __syncthreads();
-  CoarsePre cp;
-  coarse_top_pre<true>(pa, cp);
-  const int ts0 = pa.top_ts0, nt = pa.top_nt;
+  if (!pa.c_wave) {  // (pc_coarse_lds reads the sums from cbuf)
+    for (int i = threadIdx.x; i < n1; i += kPcThreads) pa.cbuf[i] = xb[n1 + i];
+    vm_drain();
+    __syncthreads();
+  }
+  const int ts0 = pa.top_ts0, nt = pa.top_nt, sl = threadIdx.x;
+  CoarsePre cp;  // (coarse_top_pre's values: the top slots' D / J from top_body's LDS)
+  cp.k = ci.k;
+  cp.par = ci.k < 0 ? ci.par : -1;
+  cp.J = ci.k < 0 && sl < nt ? T.sJ[sl] : 0.0;
+  cp.D = ci.k < 0 && sl < nt ? T.sD[sl] : 1.0;
+  cp.T = ci.k < 0 && ci.par >= 0 ? ci.T : 1.0;
+  cp.lvo = ci.lvo;
+  cp.cw0 = ci.cw0;
+  cp.cw1 = ci.cw1;
+  const bool cm = pa.c_wave && sl < nC;
+  cp.cD = cm ? xb[n1 + sl] : 1.0;
+  cp.cJ = cm ? xb[n1 + nC + sl] : 0.0;
+  cp.cG = cm ? xb[n1 + 2 * nC + sl] : 0.0;
+  __syncthreads();  // (coarse_top_block overwrites T.sD0 / sJ0 / sGp / sY)
   coarse_top_block(pa, cp, T.sD0, T.sJ0, T.sGp, T.sY, T.sOff);
   for (int i = threadIdx.x; i < nt; i += kPcThreads) {
     const double zj = T.sY[i];
@@ -4692,7 +4730,7 @@ __device__ bool xr_coarse(const PcArgs& pa, const DirStep& da, const TopLds& T) 
 // rank's own rows, the cut rows' shares of this rank (the last xK post ranges), exchange 2,
 // then every rank the same relres: the rows' ||r||^2 summed in rank order plus the cut
 // rows' r^2 in index order (r = 0 - the ranks' shares: b = 0 on the multiplier rows).
-__device__ bool dir_publish_xr(const PcArgs& pa, const DirStep& da, int lo0, int lo1) {
+__device__ __forceinline__ bool dir_publish_xr(const PcArgs& pa, const DirStep& da, int lo0, int lo1) {
 #pragma clang fp contract(off)
   __shared__ double s_r[kPcThreads / 64], s_b[kPcThreads / 64];
   __shared__ double xs[2 * (2 + kCapCoarseLds)];
@@ -4837,7 +4875,10 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       T.sLv = u;
       TopPre pre;
       top_pre_idx(pa, pre);
+      CoarseIdx ci;
+      if constexpr (XR) coarse_idx_load(pa, ci);
       top_pre_val<true>(pa, nullptr, pre);
+      if constexpr (XR) coarse_idx_val(pa, ci);
       NX_DSTAMP(6);
       if constexpr (XR) {
         // the rank's top part up to its coarse partials [D | J | G] (pc_coarse_partials: in
@@ -4848,7 +4889,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
                              kModeDirect, T, false, pre);
         vm_drain();
         __syncthreads();
-        if (!xr_coarse(pa, da, T)) {
+        if (!xr_coarse(pa, da, T, ci)) {
           if (threadIdx.x == 0)  // (the waiters give up too; the host reports the exchange)
             __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;
@@ -6000,6 +6041,10 @@ struct nx_network {
   bool pc = false;
   bool pc_lds = false;  // every job fits the LDS kernels' caps
   int pc_variant = 0;   // (W, CPL) instantiation
+  // the fused step's (W, CPL) (k_dir_step / k_dir_xr / k_dir_xg): N <= 32 by 8 lanes so a
+  // job's <= 128 chains run in ONE pass (phase 2 on phase 1's registers, no reloads): 2
+  // cells per lane up to N = 16, 3 up to 24 (C4's N = 19), 4 up to 32 (register spills)
+  int dstep_variant = 0;
   int pc_jobs = 0;
   int64_t pc_slots = 0;
   int64_t pc_ndc = 0;
@@ -7198,7 +7243,7 @@ int chain_rec_refresh(nx_network* h) {
   return NX_OK;
 }
 // the tile width W of a (W, CPL) variant (nx_set_preconditioner's choice)
-int variant_w(int v) { return v == 5 || v == 7 ? 8 : v == 6 ? 4 : v <= 2 ? 16 : 64; }
+int variant_w(int v) { return v == 5 || v == 7 || v == 10 ? 8 : v == 6 ? 4 : v <= 2 ? 16 : 64; }
 }  // namespace
 
 NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
@@ -7482,13 +7527,14 @@ bool dteam_on(const nx_network* h) {
 
 // Launch k_dir_step and wait for its published state (the host's sequence advances).
 int run_dstep(nx_network* h, double rtol, bool prof) {
-  switch (h->pc_variant) {
+  switch (h->dstep_variant) {
     case 0: launch_dstep_wc<16, 1>(h, rtol, prof); break;
     case 1: launch_dstep_wc<16, 2>(h, rtol, prof); break;
     case 2: launch_dstep_wc<16, 4>(h, rtol, prof); break;
     case 3: launch_dstep_wc<64, 2>(h, rtol, prof); break;
     case 5: launch_dstep_wc<8, 2>(h, rtol, prof); break;
     case 7: launch_dstep_wc<8, 4>(h, rtol, prof); break;
+    case 10: launch_dstep_wc<8, 3>(h, rtol, prof); break;
     case 8: launch_dstep_wc<64, 8>(h, rtol, prof); break;
     case 9: launch_dstep_wc<64, 16>(h, rtol, prof); break;
     default: launch_dstep_wc<64, 4>(h, rtol, prof); break;
@@ -7754,7 +7800,7 @@ int xr_link(nx_network* h, const std::vector<XPeer>& peers) {
   h->sched_checked = false;  // (the ranks agree on the exchange in check_schedules)
   return NX_OK;
 }
-bool xr_variant(int v) { return v == 5 || v == 1 || v == 2; }  // <8,2>, <16,2>, <16,4>
+bool xr_variant(int v) { return v == 5 || v == 10 || v == 7 || v == 2; }  // <8,2|3|4>, <16,4>
 size_t xr_static_lds(int v);  // the exchange kernels' static LDS (below)
 
 // one rank's share of the decision: its tables, its peers linked, the coarse / cut sizes
@@ -7764,7 +7810,8 @@ bool xr_local(const nx_network* h) {
          h->pc_jobs > 0 && h->pc_jobs <= h->n_cu && h->pa.n_coarse > 0 &&
          h->pa.n_coarse <= kCapCoarseLds && h->n_cut >= 0 && h->n_cut <= kCapCoarseLds &&
          h->top_nt > 0 && h->top_nt <= kTopThreads && h->pa.n_top_lvl <= kMaxTopLvl &&
-         xr_variant(h->pc_variant) && h->dstep_lds + xr_static_lds(h->pc_variant) <= 160 * 1024;
+         xr_variant(h->dstep_variant) &&
+         h->dstep_lds + xr_static_lds(h->dstep_variant) <= 160 * 1024;
 }
 bool xr_env() {
   const char* e = std::getenv("NXHIP_DIR_XR");  // read per solve: tests switch it
@@ -7777,7 +7824,7 @@ bool xr_on(const Team& t, bool with_asm) {
   if (t.g) {
     int jobs = 0;
     for (int r = 0; r < t.P; ++r) {
-      if (!xr_local(t.hs[r]) || t.hs[r]->pc_variant != t.hs[0]->pc_variant) return false;
+      if (!xr_local(t.hs[r]) || t.hs[r]->dstep_variant != t.hs[0]->dstep_variant) return false;
       jobs += t.hs[r]->pc_jobs;
     }
     return jobs <= t.hs[0]->n_cu;
@@ -7832,7 +7879,7 @@ int launch_xr_wc(const Team& t, double rtol) {
     const char* db = static_cast<const char*>(g->xg_dev);
     const void* fn = reinterpret_cast<const void*>(&k_dir_xg<W, CPL>);
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(160 * 1024 - xr_static_lds(t.hs[0]->pc_variant)));
+                              (int)(160 * 1024 - xr_static_lds(t.hs[0]->dstep_variant)));
     (void)hipGetLastError();
     hipLaunchKernelGGL((k_dir_xg<W, CPL>), dim3(goff[P]), dim3(kPcThreads), lds, g->stream,
                        reinterpret_cast<const PcArgs*>(db), reinterpret_cast<const DirStep*>(db + bp),
@@ -7842,7 +7889,7 @@ int launch_xr_wc(const Team& t, double rtol) {
     nx_network* h = t.hs[0];
     const void* fn = reinterpret_cast<const void*>(&k_dir_xr<W, CPL>);
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(160 * 1024 - xr_static_lds(h->pc_variant)));
+                              (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
     (void)hipGetLastError();
     hipLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
                        h->stream, h->pa, das[0]);
@@ -7855,19 +7902,21 @@ int launch_xr_wc(const Team& t, double rtol) {
   return NX_OK;
 }
 int launch_xr(const Team& t, double rtol) {
-  switch (t.hs[0]->pc_variant) {
+  switch (t.hs[0]->dstep_variant) {
     case 5: return launch_xr_wc<8, 2>(t, rtol);
-    case 1: return launch_xr_wc<16, 2>(t, rtol);
+    case 10: return launch_xr_wc<8, 3>(t, rtol);
+    case 7: return launch_xr_wc<8, 4>(t, rtol);
     default: return launch_xr_wc<16, 4>(t, rtol);
   }
 }
 size_t xr_static_lds(int v) {
-  static size_t s[3] = {0, 0, 0};
-  const int i = v == 5 ? 0 : v == 1 ? 1 : 2;
+  static size_t s[4] = {0, 0, 0, 0};
+  const int i = v == 5 ? 0 : v == 7 ? 1 : v == 10 ? 3 : 2;
   if (!s[i]) {
     hipFuncAttributes a{};
     const void* fn = i == 0 ? reinterpret_cast<const void*>(&k_dir_xr<8, 2>)
-                   : i == 1 ? reinterpret_cast<const void*>(&k_dir_xr<16, 2>)
+                   : i == 1 ? reinterpret_cast<const void*>(&k_dir_xr<8, 4>)
+                   : i == 3 ? reinterpret_cast<const void*>(&k_dir_xr<8, 3>)
                             : reinterpret_cast<const void*>(&k_dir_xr<16, 4>);
     s[i] = hipFuncGetAttributes(&a, fn) == hipSuccess ? a.sharedSizeBytes : 64 * 1024;
   }
@@ -9293,7 +9342,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
       HIPCALL(hipMemcpy(jw.data(), pa.job_wave, sizeof(int) * n_jobs, hipMemcpyDeviceToHost));
       for (int jb = 0; jb < n_jobs; ++jb) hdr[(size_t)kJobHdr * jb + 8] = jw[jb];
     }
-    const int W = variant_w(variant);
+    const int W = variant_w(N <= 16 ? 5 : N <= 24 ? 10 : N <= 32 ? 7 : variant);  // (dstep's)
     const int nt = h->top_nt, cdc = std::max(1, pa.top_ndc), ct = nt + 1;
     const int top_ints = 3 * ct + 1 + cdc + n_top_lvl + 1;
     const int top_dbl = 6 * ct + 3 * cdc + (top_ints + 1) / 2 + 2;
@@ -9313,6 +9362,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->pa = pa;
   h->pc_jobs = n_jobs;
   h->pc_variant = variant;
+  h->dstep_variant = N <= 16 ? 5 : N <= 24 ? 10 : N <= 32 ? 7 : variant;
   if (h->d_crec) CHECK(chain_rec_refresh(h));
   h->pc_slots = n_slots;
   h->pc_ndc = n_slots > 0 ? slot_dc_off[n_slots] : 0;
@@ -9918,7 +9968,7 @@ int xr_rehearse_wc(nx_network* h, int P, double rtol, int reps, float* ms_out) {
   HIPCALL(hipEventCreate(&e1));
   const void* fn = reinterpret_cast<const void*>(&k_dir_xr<W, CPL>);
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(160 * 1024 - xr_static_lds(h->pc_variant)));
+                            (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
   (void)hipGetLastError();
   float total = 0.f;
   for (int k = 0; k <= reps && rc == NX_OK; ++k) {  // (launch 0: warm-up, not timed)
@@ -9959,15 +10009,16 @@ int xr_rehearse_wc(nx_network* h, int P, double rtol, int reps, float* ms_out) {
 NX_API int nx_debug_xr_rehearse(nx_network_t* h, double rtol, int32_t reps, double* ms) {
   if (!h || !ms) return fail(NX_ERR_ARG, "null argument");
   if (!h->group) return fail(NX_ERR_STATE, "a group member (its graph path solved first)");
-  if (!h->xr_ok || !xr_variant(h->pc_variant) || h->pa.n_coarse <= 0 || h->n_cut < 0 ||
+  if (!h->xr_ok || !xr_variant(h->dstep_variant) || h->pa.n_coarse <= 0 || h->n_cut < 0 ||
       h->pa.n_coarse > kCapCoarseLds || h->n_cut > kCapCoarseLds)
     return fail(NX_ERR_STATE, "this rank cannot run the exchange step");
   CHECK(set_device(h));
   float v = 0.f;
   int rc;
-  switch (h->pc_variant) {
+  switch (h->dstep_variant) {
     case 5: rc = xr_rehearse_wc<8, 2>(h, h->nranks, rtol, reps, &v); break;
-    case 1: rc = xr_rehearse_wc<16, 2>(h, h->nranks, rtol, reps, &v); break;
+    case 7: rc = xr_rehearse_wc<8, 4>(h, h->nranks, rtol, reps, &v); break;
+    case 10: rc = xr_rehearse_wc<8, 3>(h, h->nranks, rtol, reps, &v); break;
     default: rc = xr_rehearse_wc<16, 4>(h, h->nranks, rtol, reps, &v); break;
   }
   *ms = v;

@@ -40,6 +40,12 @@ def main() -> int:
         it, rr, conv = h.solve(1e-12, 100, 4)
     assert h.direct_path() == "fused", h.direct_path()
     nj = asm.tree_preconditioner.n_jobs
+    report(nj, rr)
+    return 0
+
+
+def report(nj: int, rr: float) -> None:
+    """Print the last launch's per-workgroup stamps (nx_debug_dstep) of nj workgroups."""
     buf = (C.c_ulonglong * (48 * 512))()
     fn = _lib.lib().nx_debug_dstep
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
@@ -79,7 +85,6 @@ def main() -> int:
         print(f"  {name:38s} med {np.median(d):6.2f}  max {d.max():6.2f}")
     e = us[40]
     print(f"  {'workgroup end':16s} min {e.min():7.2f}  med {np.median(e):7.2f}  max {e.max():7.2f}")
-    return 0
 
 
 if __name__ == "__main__":
