@@ -1016,6 +1016,10 @@ struct PcArgs {
   const int* c_child_off;
   const int* c_child;
   const int* c_lvl_off;
+  // per coarse junction k its coarse chains in chain order (ck_off: n_coarse + 1; ck_ent:
+  // i << 1 | (k is the chain's bottom)): pc_coarse_partials' sums without scanning them all
+  const int* ck_off;
+  const int* ck_ent;
   double* cbuf;
   // linear form (several ranks, LDS kernels): the sweeps condense y instead of
   // r' = y - (alpha/beta) r2 and the down sweep forms z = P^{-1}y - (alpha/beta) z_old,
@@ -1135,7 +1139,7 @@ constexpr int kCapCoarseLds = 256;  // coarse forests the down workgroups solve 
 // by top-part position. Ends with the buffer complete (one workgroup). WT: the chains' data
 // were handed over inside the launch (k_dir_team_up): write-through loads.
 template <int BS, bool WT = false>
-__device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const double* sD,
+__device__ __forceinline__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const double* sD,
                                    const double* sJ) {
   // small coarse sets: the buffer is built in LDS and the coarse chains' data loaded in
   // parallel (thread = chain), then every coarse junction sums its chains in chain order
@@ -1171,16 +1175,29 @@ __device__ void pc_coarse_partials(const PcArgs& pa, int ts0, int nt, const doub
               // additions in the same order as one thread walking the chains)
     for (int k = threadIdx.x; k < nC; k += BS) {
       double D = sBuf[k], J = sBuf[nC + k], Gk = sBuf[2 * nC + k];
-      for (int i = 0; i < ncc; ++i) {
-        const int t = sCt[i], b = sCb[i];
-        if (t == k) {
+      if (pa.ck_off) {  // its own chains only (host-listed in chain order)
+        for (int e = pa.ck_off[k]; e < pa.ck_off[k + 1]; ++e) {
+          const int en = pa.ck_ent[e], i = en >> 1;
           D += sCg[i];
-          J += sCit[i];
+          if (en & 1) {
+            J += sCib[i];
+            Gk = sCg[i];
+          } else {
+            J += sCit[i];
+          }
         }
-        if (b == k) {
-          D += sCg[i];
-          J += sCib[i];
-          Gk = sCg[i];
+      } else {
+        for (int i = 0; i < ncc; ++i) {
+          const int t = sCt[i], b = sCb[i];
+          if (t == k) {
+            D += sCg[i];
+            J += sCit[i];
+          }
+          if (b == k) {
+            D += sCg[i];
+            J += sCib[i];
+            Gk = sCg[i];
+          }
         }
       }
       pa.cbuf[k] = D;
@@ -2604,7 +2621,7 @@ __device__ void pc_prep_in_block(const PcArgs& pa, bool gcols, double* sJ, doubl
 
 // The coarse forest solve of k_pc_coarse (same arithmetic, same order) inside one
 // workgroup, into sZc (n_coarse <= kCapCoarseLds); sD / sJ are scratch.
-__device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* sZc) {
+__device__ __forceinline__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* sZc) {
   // the forest's structure is staged in LDS first (two round trips): its level sweeps
   // (13 levels each way for the 8-rank depth-17 tree) then touch no global memory
   __shared__ int sCo[kCapCoarseLds + 1], sCc[kCapCoarseLds], sCp[kCapCoarseLds];
@@ -2737,6 +2754,54 @@ __device__ void pc_coarse_lds(const PcArgs& pa, double* sD, double* sJ, double* 
   }
 }
 
+// The same coarse forest solve with one division per junction (its 1 / D, formed when its
+// level is done; the children's terms and the back-substitution multiply by it) instead of
+// two per child and one per junction on the way down: the exchange step's (k_dir_xr), where
+// the coarse forest's levels (17 each way at 8 ranks) sit on the critical path. Not the
+// graph path's bits (that divides), the same solution to rounding.
+__device__ __forceinline__ void coarse_wave_solve_rcp(const PcArgs& pa, int w0, int w1, double D,
+                                                      double J, double g0, double* sZc) {
+  if (threadIdx.x >= 64) return;
+  const int nC = pa.n_coarse, nl = pa.n_clvl;
+  const int cj = threadIdx.x;
+  const bool cmine = cj < nC;
+  const int clv = cmine ? (w0 & 0xff) : -1;
+  const int cnk = cmine ? ((w0 >> 8) & 0xf) : 0;
+  const int p = cmine ? ((w0 >> 12) & 0xff) - 1 : -1;
+  int cch[kWaveKids];
+#pragma unroll
+  for (int k = 0; k < kWaveKids; ++k) cch[k] = k < cnk ? (w1 >> (8 * k)) & 0xff : 0;
+  double gk[kWaveKids];
+#pragma unroll
+  for (int k = 0; k < kWaveKids; ++k) gk[k] = __shfl(g0, cch[k]);
+  int kmax = cnk;
+  for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
+  double iv = 1.0;
+  for (int lv = nl - 1; lv >= 0; --lv) {
+    double vk[kWaveKids], jk[kWaveKids];
+#pragma unroll
+    for (int k = 0; k < kWaveKids; ++k) {
+      vk[k] = k < kmax ? __shfl(iv, cch[k]) : 0.0;
+      jk[k] = k < kmax ? __shfl(J, cch[k]) : 0.0;
+    }
+    if (clv == lv) {
+#pragma unroll
+      for (int k = 0; k < kWaveKids; ++k) {
+        if (k >= cnk) break;
+        D -= gk[k] * gk[k] * vk[k];
+        J += gk[k] * jk[k] * vk[k];
+      }
+      iv = 1.0 / D;
+    }
+  }
+  double zc = 0.0;
+  for (int lv = 0; lv < nl; ++lv) {  // root level first
+    const double zp = __shfl(zc, p >= 0 ? p : cj);
+    if (clv == lv) zc = (J + (p >= 0 ? g0 * zp : 0.0)) * iv;
+  }
+  if (cmine) sZc[cj] = zc;
+}
+
 // The coarse forest (<= 64 junctions) by one wave from registers: lane = coarse junction,
 // its level, parent and children from pa.c_wave, its all-reduced D, J, G passed in; the
 // same arithmetic in the same order as pc_coarse_lds. Writes z into sZc (lanes < n_coarse).
@@ -2830,7 +2895,7 @@ __device__ __forceinline__ void coarse_top_pre(const PcArgs& pa, CoarsePre& p) {
 // on every rank and workgroup) and the top part's back-substitution (k_pc_coarse's staged
 // arithmetic, thread = slot) into tZ; workgroup 0 stores the values in slot_z (the
 // residual's reduce kernel moves them into x after the sweep).
-__device__ void coarse_top_block(const PcArgs& pa, const CoarsePre& p, double* cD, double* cJ,
+__device__ __forceinline__ void coarse_top_block(const PcArgs& pa, const CoarsePre& p, double* cD, double* cJ,
                                  double* cZ, double* tZ, int* tLv) {
   const int ntl = pa.n_top_lvl, ts0 = pa.top_ts0, nt = pa.top_nt;
   const int sl = threadIdx.x;
@@ -4690,13 +4755,71 @@ __device__ __forceinline__ void coarse_idx_val(const PcArgs& pa, CoarseIdx& c) {
 // (coarse_top_block, k_pc_coarse's arithmetic: coarse_top_pre's values, from LDS and the
 // prefetched ci) into LDS, then the top values to slot_z (write-through: the rank's other
 // workgroups read them) and to x.
+// The top part's back-substitution from the coarse values (coarse_top_block's arithmetic
+// and order per slot: the same bits) on the wave subtrees of pa.top_sub: the upper slots
+// level by level (barriers), then every subtree by its wave, root first, the parent's value
+// by shuffle. Per slot (LDS): D / J (top_body's sD / sJ), its parent (sPar), its parent
+// chain's T and coarse index (ext, kk).
+__device__ __forceinline__ void xr_top_back(const PcArgs& pa, const CoarsePre& cp, const TopLds& T,
+                                            const TopPre& pre, const double* cZ, double* tZ,
+                                            double* ext, int* kk) {
+  const int nt = pa.top_nt, sl = threadIdx.x;
+  if (sl < nt) {
+    ext[sl] = cp.T;
+    kk[sl] = cp.k;
+  }
+  __syncthreads();
+  const bool upper = sl < nt && pre.w[0] < 0;
+  const int ulv = upper ? (pre.w[0] & 0xff) : -1;
+  const int par = sl < nt ? T.sPar[sl] : -1;
+  for (int lv = 0; lv < pa.top_sub_nup; ++lv) {
+    if (ulv == lv) {
+      double zj;
+      if (cp.k >= 0) {
+        zj = cZ[cp.k];
+      } else {
+        double num = cp.J;
+        if (par >= 0) num += tZ[par] / cp.T;
+        zj = num / cp.D;
+      }
+      tZ[sl] = zj;
+    }
+    __syncthreads();
+  }
+  if (pre.ldep > 0) {
+    const int lsl = pre.ls;
+    const int lvl = (pre.lw[0] >> 6) & 0xff, plane = (pre.lw[0] >> 18) & 63;
+    const int k = lsl >= 0 ? kk[lsl] : -1, pq = lsl >= 0 ? T.sPar[lsl] : -1;
+    const double J = lsl >= 0 ? T.sJ[lsl] : 0.0, D = lsl >= 0 ? T.sD[lsl] : 1.0;
+    const double Tq = lsl >= 0 ? ext[lsl] : 1.0;
+    double zq = 0.0;
+    for (int q = 0; q < pre.ldep; ++q) {
+      const double zp = __shfl(zq, plane);
+      if (lvl == q && lsl >= 0) {
+        if (k >= 0) {
+          zq = cZ[k];
+        } else {
+          const double zpar = q == 0 ? (pq >= 0 ? tZ[pq] : 0.0) : zp;
+          double num = J;
+          if (pq >= 0) num += zpar / Tq;
+          zq = num / D;
+        }
+      }
+    }
+    if (lsl >= 0) tZ[lsl] = zq;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ bool xr_coarse(const PcArgs& pa, const DirStep& da, const TopLds& T,
-                                          const CoarseIdx& ci) {
+                                          const CoarseIdx& ci, const TopPre& pre, double* ext) {
   __shared__ double xb[2 * 3 * kCapCoarseLds];
   const int nC = pa.n_coarse, n1 = 3 * nC;
   for (int i = threadIdx.x; i < n1; i += kPcThreads) xb[i] = ld_wt(pa.cbuf + i);
   __syncthreads();
+  NX_DSTAMP(42);
   if (!xr_allsum(da, 0, xb, n1, xb + n1)) return false;
+  NX_DSTAMP(43);
   if (!pa.c_wave) {  // (pc_coarse_lds reads the sums from cbuf)
     for (int i = threadIdx.x; i < n1; i += kPcThreads) pa.cbuf[i] = xb[n1 + i];
     vm_drain();
@@ -4717,7 +4840,19 @@ __device__ __forceinline__ bool xr_coarse(const PcArgs& pa, const DirStep& da, c
   cp.cJ = cm ? xb[n1 + nC + sl] : 0.0;
   cp.cG = cm ? xb[n1 + 2 * nC + sl] : 0.0;
   __syncthreads();  // (coarse_top_block overwrites T.sD0 / sJ0 / sGp / sY)
-  coarse_top_block(pa, cp, T.sD0, T.sJ0, T.sGp, T.sY, T.sOff);
+  if (pa.top_sub) {  // the coarse forest, then the top part by its wave subtrees
+    if (pa.c_wave) {
+      coarse_wave_solve_rcp(pa, cp.cw0, cp.cw1, cp.cD, cp.cJ, cp.cG, T.sGp);
+      __syncthreads();
+    } else {
+      pc_coarse_lds(pa, T.sD0, T.sJ0, T.sGp);
+    }
+    NX_DSTAMP(46);
+    xr_top_back(pa, cp, T, pre, T.sGp, T.sY, ext, reinterpret_cast<int*>(ext + nt + 1));
+    NX_DSTAMP(47);
+  } else {
+    coarse_top_block(pa, cp, T.sD0, T.sJ0, T.sGp, T.sY, T.sOff);
+  }
   for (int i = threadIdx.x; i < nt; i += kPcThreads) {
     const double zj = T.sY[i];
     st_wt(pa.slot_z + ts0 + i, zj);
@@ -4772,7 +4907,9 @@ __device__ __forceinline__ bool dir_publish_xr(const PcArgs& pa, const DirStep& 
   }
   __syncthreads();
   double* ys = xs + 2 + K;
+  NX_DSTAMP(44);
   if (!xr_allsum(da, 1, xs, 2 + K, ys)) return false;
+  NX_DSTAMP(45);
   if (threadIdx.x == 0) {
     rr = ys[0];
     for (int k = 0; k < K; ++k) {
@@ -4889,7 +5026,10 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
                              kModeDirect, T, false, pre);
         vm_drain();
         __syncthreads();
-        if (!xr_coarse(pa, da, T, ci)) {
+        NX_DSTAMP(41);
+        // (xr_top_back's per-slot scratch after the top part's arrays; sLv is the last)
+        double* ext = reinterpret_cast<double*>(T.sLv + ((pa.n_top_lvl + 2) & ~1));
+        if (!xr_coarse(pa, da, T, ci, pre, ext)) {
           if (threadIdx.x == 0)  // (the waiters give up too; the host reports the exchange)
             __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;
@@ -9262,29 +9402,42 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
         }
       std::vector<int> ts(K1 * (size_t)nt, 0), tl(K2 * (size_t)kTopThreads, 0), tdep(NW, 0);
       for (int t = 0; t < kTopThreads; ++t) tl[(size_t)K2 * t] = -1;
-      int nsub = 0, nup = 0;
+      int nup = 0;
       bool sok = true;
-      for (int j = 0; j < nt && sok; ++j) {
+      std::vector<int> roots;  // the maximal subtrees' roots
+      for (int j = 0; j < nt; ++j) {
         if (size[j] > 64) {  // an upper slot: the level sweeps
           const int* w = tw.data() + (size_t)K1 * j;
           int* o = ts.data() + (size_t)K1 * j;
           o[0] = (int)(0x80000000u | (unsigned)w[0]);
           for (int k = 0; k < kWaveKids; ++k) o[1 + k] = w[1 + k];
           nup = std::max(nup, lvl[j] + 1);
-          continue;
+        } else if (par[j] < 0 || size[par[j]] > 64) {
+          roots.push_back(j);
         }
-        if (par[j] >= 0 && size[par[j]] <= 64) continue;  // inside another subtree
-        if (nsub >= NW) {
+      }
+      // packed into the waves first-fit by decreasing size: lanes of different subtrees never
+      // exchange values, so a wave sweeps all of its subtrees at once
+      std::stable_sort(roots.begin(), roots.end(), [&](int a, int b) { return size[a] > size[b]; });
+      std::vector<int> fill(NW, 0);
+      int nsub = 0;
+      for (int j : roots) {
+        int wv = 0;
+        while (wv < NW && fill[wv] + size[j] > 64) ++wv;
+        if (wv == NW) {
           sok = false;
           break;
         }
+        const int base = fill[wv];
+        fill[wv] += size[j];
+        nsub = std::max(nsub, wv + 1);
         std::vector<int> bfs{j}, lane_of(nt, -1), dep{0};  // this subtree, BFS order
-        lane_of[j] = 0;
+        lane_of[j] = base;
         for (size_t i = 0; i < bfs.size(); ++i) {
           const int* w = tw.data() + (size_t)K1 * bfs[i];
           for (int k = 0; k < ((w[0] >> 8) & 0xff); ++k) {
             const int c = w[1 + k] & 0xfff;
-            lane_of[c] = (int)bfs.size();
+            lane_of[c] = base + (int)bfs.size();
             bfs.push_back(c);
             dep.push_back(dep[i] + 1);
           }
@@ -9294,15 +9447,16 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
           const int m = bfs[i];
           const int* w = tw.data() + (size_t)K1 * m;
           const int nk = (w[0] >> 8) & 0xff;
-          int* o = tl.data() + (size_t)K2 * (nsub * 64 + (int)i);
+          const int ln = base + (int)i;
+          int* o = tl.data() + (size_t)K2 * (wv * 64 + ln);
           o[0] = m;
           const int pl = dep[i] > 0 ? lane_of[par[m]] : 0;
-          o[1] = (int)i | (dep[i] << 6) | (nk << 14) | (pl << 18);
+          o[1] = ln | (dep[i] << 6) | (nk << 14) | (pl << 18);
           for (int k = 0; k < nk; ++k) o[2 + k] = lane_of[w[1 + k] & 0xfff] | ((w[1 + k] >> 12) << 12);
           md = std::max(md, dep[i]);
         }
         if (md > 0xff) sok = false;
-        tdep[nsub++] = md + 1;
+        tdep[wv] = std::max(tdep[wv], md + 1);
       }
       if (sok && nsub > 0) {
         pa.top_sub = up(ts.data(), (int64_t)ts.size());
@@ -9346,7 +9500,9 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     const int nt = h->top_nt, cdc = std::max(1, pa.top_ndc), ct = nt + 1;
     const int top_ints = 3 * ct + 1 + cdc + n_top_lvl + 1;
     const int top_dbl = 6 * ct + 3 * cdc + (top_ints + 1) / 2 + 2;
-    h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl});
+    // (several ranks: xr_top_back's per-slot T and coarse index after the top part)
+    const int xr_dbl = h->nranks > 1 ? 2 * (nt + 1) + 4 : 0;
+    h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl + xr_dbl});
     h->dstep_top = nt + (nt & 1);
     h->dstep_lds = 8 * (size_t)(kStashDbl + h->dstep_main + h->dstep_top);
     const bool fits = mlv <= kStLv && mns <= kStNs && mnd <= kStNd && kPcThreads / W <= kStNc;
@@ -9711,6 +9867,22 @@ NX_API int nx_set_coarse(nx_network_t* h, int32_t n_coarse, const int32_t* slot_
   pa.c_child_off = up(c_child_off, n_coarse + 1);
   pa.c_child = up(ncl ? c_child : nullptr, ncl);
   pa.c_lvl_off = up(c_lvl_off, n_clvl + 1);
+  {  // per coarse junction its chains in chain order (pc_coarse_partials)
+    std::vector<int> off(n_coarse + 1, 0), ent;
+    for (int i = 0; i < n_cc; ++i) {
+      off[cc_top[i] + 1] += 1;
+      off[cc_bot[i] + 1] += 1;
+    }
+    for (int k = 0; k < n_coarse; ++k) off[k + 1] += off[k];
+    ent.assign(std::max(1, off[n_coarse]), 0);
+    std::vector<int> fill(off.begin(), off.end() - 1);
+    for (int i = 0; i < n_cc; ++i) {  // (a chain's top and bottom junctions differ)
+      ent[fill[cc_top[i]]++] = i << 1;
+      ent[fill[cc_bot[i]]++] = (i << 1) | 1;
+    }
+    pa.ck_off = up(off.data(), n_coarse + 1);
+    pa.ck_ent = up(ent.data(), (int64_t)ent.size());
+  }
   pa.c_wave = nullptr;
   if (n_coarse <= 64 && n_clvl <= 255) {  // coarse_wave_solve's packed set-up
     std::vector<int> cw(2 * std::max(1, (int)n_coarse), 0);

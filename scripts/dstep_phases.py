@@ -83,6 +83,12 @@ def report(nj: int, rr: float) -> None:
     for k, k0, name in inner:
         d = us[k] - us[k0]
         print(f"  {name:38s} med {np.median(d):6.2f}  max {d.max():6.2f}")
+    if g[41].max() > 0:  # several ranks (k_dir_xr): the top solver's exchange, the publisher's
+        t, pb = last1, pub
+        print(f"  xr: top part up {us[41][t]:.2f}, partials read {us[42][t]:.2f}, exchange 1 done "
+              f"{us[43][t]:.2f}, values out {us[5][t]:.2f}; publish: exchange 2 from "
+              f"{us[44][pb]:.2f} to {us[45][pb]:.2f}, published {us[4][pb]:.2f}")
+        print(f"  xr: coarse forest solved {us[46][t]:.2f}, top part's values {us[47][t]:.2f}")
     e = us[40]
     print(f"  {'workgroup end':16s} min {e.min():7.2f}  med {np.median(e):7.2f}  max {e.max():7.2f}")
 
