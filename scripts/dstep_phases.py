@@ -68,6 +68,10 @@ def report(nj: int, rr: float) -> None:
     print(f"  up levels (deepest first) end at: {' '.join(reversed(lv))}")
     v = us[8]
     print(f"  {'stores issued':16s} min {v.min():7.2f}  med {np.median(v):7.2f}  max {v.max():7.2f}")
+    late = np.argsort(us[2])[-4:][::-1]  # the latest to receive the top values
+    print("  latest top values in: " + ", ".join(
+        f"wg {w} at {us[2][w]:.2f} (arrived {us[1][w]:.2f}, stores issued {us[8][w]:.2f}"
+        f"{', top solver' if w == last1 else ''})" for w in late))
     pub = np.argmax(g[4])
     print(f"  published by wg {pub} at {us[4][pub]:7.2f}")
     d1 = us[1] - us[0]
