@@ -388,7 +388,10 @@ class HydraulicNetworkAssembler:
                 mine = None
             handles = comm.allgather(mine)
             if all(hd is not None for hd in handles):
-                self._handle.xch_import(handles)
+                try:  # (a rank left unlinked turns the step off everywhere: check_schedules)
+                    self._handle.xch_import(handles)
+                except _lib.NxError:
+                    pass
         # the direct solve completes the cut multiplier rows in its residual all-reduce
         self._handle.set_cut(lp.n_cut, lp.lm_cut, lp.gk_off, lp.gk_row, lp.gk_coef)
 

@@ -3426,9 +3426,6 @@ struct DirStep {
   XPeer xself;
   int xP, xrank, xld1, xld2, xK;
   unsigned xtag;
-  // the waiting workgroups hold their assembly's stores until the top part's solver has
-  // loaded its inputs ([5] = epoch + 1; NXHIP_DIR_GATE, measured)
-  int gate;
 };
 
 constexpr int kDirWaitPolls = 1 << 20;  // s_sleep-paced polls before a waiting workgroup gives up
@@ -4050,44 +4047,6 @@ __device__ __forceinline__ void chain_rec_load(const DirStep& da, int c, bool ac
   r.seglen = q.w;
 }
 
-// A chain record parked in LDS (13 doubles per chain: the top part's solver keeps its own
-// records there through the top part instead of reloading them after it)
-constexpr int kRecDbl = 13;
-__device__ __forceinline__ void chain_rec_park(const ChainRec& r, double* d) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    d[i] = r.x0[i];
-    d[3 + i] = r.x1[i];
-  }
-  d[6] = r.R;
-  d[7] = r.fe;
-  d[8] = r.bc0;
-  d[9] = r.bc1;
-  int* q = reinterpret_cast<int*>(d + 10);
-  q[0] = r.e;
-  q[1] = r.flip;
-  q[2] = r.s;
-  q[3] = r.sg0;
-  q[4] = r.seglen;
-}
-__device__ __forceinline__ void chain_rec_unpark(const double* d, ChainRec& r) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    r.x0[i] = d[i];
-    r.x1[i] = d[3 + i];
-  }
-  r.R = d[6];
-  r.fe = d[7];
-  r.bc0 = d[8];
-  r.bc1 = d[9];
-  const int* q = reinterpret_cast<const int*>(d + 10);
-  r.e = q[0];
-  r.flip = q[1];
-  r.s = q[2];
-  r.sg0 = q[3];
-  r.seglen = q[4];
-}
-
 // dir_chain_asm from a chain record (the same arithmetic, the same bits)
 template <int W, int CPL>
 __device__ __forceinline__ void dir_chain_asm_rec(const PcArgs& pa, const ChainRec& r, bool active,
@@ -4684,9 +4643,6 @@ __device__ __forceinline__ void dir_stores_v2(const PcArgs& pa, const DirStep& d
 // arrive (helpers), one chain per wave on the other waves: kDirHelpChains chains each.
 constexpr int kDirFreeWaves = 4;
 constexpr int kDirHelpChains = kPcThreads / 64 - kDirFreeWaves;
-// the helpers leave their own assembly's stores until after their phase 2 (they are the
-// last to issue stores before the wait: their store waves' issue would delay their phase 2)
-constexpr bool kDirHelpDefer = true;
 // dynamic LDS of k_dir_step: at most this (the static __shared__ words -- flags, the partial
 // sums of phase 2 and the publish -- take the rest of the CU's 160 KiB)
 constexpr int kDirLdsMax = 160 * 1024 - 2048;
@@ -4974,17 +4930,6 @@ __device__ __forceinline__ bool dir_publish_xr(const PcArgs& pa, const DirStep& 
   return true;
 }
 
-// (NXHIP_DIR_GATE) a waiting workgroup's thread 0: bounded wait until the top part's solver
-// has its inputs (no give-up report: the wait for the top values reports it)
-__device__ __forceinline__ void dir_wait_gate(const DirStep& da) {
-  for (unsigned k = 0; k < da.polls; ++k) {
-    if (__hip_atomic_load(da.sync + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        da.epoch + 1u)
-      return;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
 // The fused direct step of one rank (k_dir_step) or, XR, of one rank of several (k_dir_xr:
 // one launch per GPU; k_dir_xg: every rank of an in-process group in one launch): the top
 // part then ends with this rank's coarse partials, the ranks exchange and sum them
@@ -5026,7 +4971,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   NX_DSTAMP(35);
   bool late_store = false;  // the top solver stores its own assembly after phase 2 (no helpers)
   bool defer_free = false;  // a waiting workgroup's free waves store theirs after phase 2
-  bool defer_all = false;   // a helper stores all of its own after phase 2
   const bool lane_on = c0 + (int)threadIdx.x / W < c1;
   if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
     vm_drain();
@@ -5066,21 +5010,13 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       T.sOff = u; u += ct + 1;
       T.sChild = u; u += cdc;
       T.sLv = u;
-      // (keep: its own chain records, loaded with the top part's inputs and parked at the
-      // end of the phases' LDS until its lanes are re-assembled after the top part)
-      double* park = smem + da.lds_main - kRecDbl * (int64_t)G;
-      if (keep) chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
       TopPre pre;
       top_pre_idx(pa, pre);
       CoarseIdx ci;
       if constexpr (XR) coarse_idx_load(pa, ci);
       top_pre_val<true>(pa, nullptr, pre);
       if constexpr (XR) coarse_idx_val(pa, ci);
-      if (keep && (threadIdx.x & (W - 1)) == 0)
-        chain_rec_park(rec, park + kRecDbl * (int64_t)(threadIdx.x / W));
       NX_DSTAMP(6);
-      if (da.gate && threadIdx.x == 0)
-        __hip_atomic_store(da.sync + 5, da.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if constexpr (XR) {
         // the rank's top part up to its coarse partials [D | J | G] (pc_coarse_partials: in
         // cbuf; the top slots' D / J in slot_D / slot_J), then the exchange, then the coarse
@@ -5112,15 +5048,13 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
       } else {  // its lanes again, redefined inside this branch: not kept through the solve
-        chain_rec_unpark(park + kRecDbl * (int64_t)(threadIdx.x / W), rec);
-        if (!lane_on) rec.e = rec.flip = 0;  // (chain_rec_load's inactive lanes)
+        chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
         dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
       }
     } else {
       // the first nh workgroups to arrive store the top solver's assembly first (they have
       // the most slack; their polls come before any store of theirs, so they see the
       // announcement at once), then their own
-      bool helper = false;  // (its own assembly is stored after its phase 2)
       if (keep && nh > 0 && sIdx < nh) {
         if (threadIdx.x == 0) {
           int who = -1;
@@ -5134,11 +5068,9 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
             __builtin_amdgcn_s_sleep(1);
           }
           sTopJob = who;
-          if (da.gate) dir_wait_gate(da);
         }
         __syncthreads();
         const int tj = sTopJob, hh = sIdx;
-        helper = tj >= 0 && kDirHelpDefer;
         if (tj >= 0) {  // helper hh: its share of the top solver's chains (+ helper 0 its rows)
           // one chain per wave (64 lanes: a chain's segment in a few whole-line store rounds)
           constexpr int CH = (W * CPL + 63) / 64;
@@ -5150,14 +5082,9 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
                                         kDirFreeWaves, kPcThreads / 64);
         }
       }
-      if (da.gate && !(keep && nh > 0 && sIdx < nh)) {
-        if (threadIdx.x == 0) dir_wait_gate(da);
-        __syncthreads();
-      }
       // own stores (unit stride: hidden in the wait), but not the free waves' (keep)
-      if (!helper) dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
+      dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
       defer_free = keep;
-      defer_all = helper;
       if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
@@ -5212,10 +5139,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   // (the kernel's end, not the published state, waits for these; re-assembled: L kept
   // through phase 2 would overflow the register budget there)
   if (late_store) {  // one job: the top solver's own
-    chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
-    dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
-    dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
-  } else if (defer_all) {  // a helper's own assembly
     chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
     dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
     dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
@@ -7689,6 +7612,7 @@ bool dstep_on(const nx_network* h) {
          h->nranks == 1;
 }
 
+DirStep dir_args(nx_network* h, double rtol);
 template <int W, int CPL>
 void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
   const DirStep da = dir_args(h, rtol);
@@ -8045,14 +7969,12 @@ bool xr_on(const Team& t, bool with_asm) {
 }
 
 DirStep dir_args(nx_network* h, double rtol) {
-  const char* g = std::getenv("NXHIP_DIR_GATE");
   return DirStep{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
                  h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
                  h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
                  h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1,
                  h->d_seq, h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci,
-                 h->dstep_main, h->dstep_top, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u,
-                 g != nullptr && std::atoi(g) != 0 ? 1 : 0};
+                 h->dstep_main, h->dstep_top, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u};
 }
 
 template <int W, int CPL>
@@ -9576,9 +9498,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     const int top_dbl = 6 * ct + 3 * cdc + (top_ints + 1) / 2 + 2;
     // (several ranks: xr_top_back's per-slot T and coarse index after the top part)
     const int xr_dbl = h->nranks > 1 ? 2 * (nt + 1) + 4 : 0;
-    // (+ the top part's solver's parked chain records at the end: kRecDbl per chain of a pass)
-    const int park_dbl = kRecDbl * (kPcThreads / W);
-    h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl + xr_dbl}) + park_dbl;
+    h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl + xr_dbl});
     h->dstep_top = nt + (nt & 1);
     h->dstep_lds = 8 * (size_t)(kStashDbl + h->dstep_main + h->dstep_top);
     const bool fits = mlv <= kStLv && mns <= kStNs && mnd <= kStNd && kPcThreads / W <= kStNc;
