@@ -8,6 +8,7 @@
 # phases       scripts/dstep_phases.py (debug build, k_dir_step stamps)  -> <tag>_phases.log
 # bench        python bench.py [args]                                    -> <tag>_bench.log
 # profile      scripts/profile.sh <tag> [args] (trace + PMC passes)      -> prof_<tag>/
+# wcal         WRITE_SIZE calibration on known write streams   -> <tag>_wcal_*, wcal_<tag>/
 # rehearsal    the 8-rank C4 group rehearsal under rocprof + per-rank kernel times
 # fe_prof      rocprof kernel stats of the (2, 0) condensed solve at C3
 # cmd:<c>      any command (e.g. cmd:"python scripts/direct_timing.py 18")
@@ -49,6 +50,12 @@ for s in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && step fe_prof 300 "$R/gpurun_out/prof_$T/run.log" \
         rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$T" -o trace --output-format csv \
         -- python3 "$R/scripts/fe_timing.py" 15 15 "2,0") || exit $? ;;
+    wcal)  # WRITE_SIZE against known write streams (scripts/micro/write_ceiling.hip)
+      hipcc --offload-arch=gfx950 -O3 -o gpurun_out/write_ceiling scripts/micro/write_ceiling.hip || exit 1
+      step wcal_time 120 "gpurun_out/${T}_wcal_time.log" gpurun_out/write_ceiling || exit $?
+      (cd /tmp && export TMPDIR=/tmp && step wcal_pmc 120 "$R/gpurun_out/${T}_wcal_pmc.log" \
+        rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/wcal_$T" -o pmc --output-format csv \
+        -- "$R/gpurun_out/write_ceiling") || exit $? ;;
     cmd)
       step cmd 600 "gpurun_out/${T}_cmd.log" bash -c "$arg" || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;

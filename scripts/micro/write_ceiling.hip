@@ -4,12 +4,21 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+// WRITE_SIZE calibration (scripts/gpu_run.sh wcal): every kernel writes exactly `bytes`, 55
+// launches each; rocprofv3 --pmc WRITE_SIZE per kernel / bytes = the counter's factor.
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
 
 __global__ void w1(double* p, long n, double v) {  // one double per thread
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
+}
+__global__ void w1sc1(double* p, long n, double v) {  // one double per thread, write-through
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p + i),
+                       __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void w2(double2* p, long n2, double v) {  // 16 B per thread
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -53,6 +62,7 @@ int main(int argc, char** argv) {
   };
   run("w1 256", [&] { w1<<<(n + 255) / 256, 256>>>(p, n, 1.0); });
   run("w1 1024", [&] { w1<<<(n + 1023) / 1024, 1024>>>(p, n, 1.0); });
+  run("w1sc1 1024", [&] { w1sc1<<<(n + 1023) / 1024, 1024>>>(p, n, 1.0); });
   run("w2 256", [&] { w2<<<(n / 2 + 255) / 256, 256>>>((double2*)p, n / 2, 1.0); });
   run("w2nt 256", [&] { w2nt<<<(n / 2 + 255) / 256, 256>>>((double2*)p, n / 2, 1.0); });
   run("wk<4> 256", [&] { wk<4><<<(n + 1023) / 1024, 256>>>(p, n, 1.0); });
