@@ -103,6 +103,19 @@ int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double* edge_
                  const int32_t* a_idx, const int32_t* a_ent, const int32_t* b_ptr,
                  const int32_t* b_idx, const int32_t* b_ent, nx_network_t** out);
 
+/*
+ * The flux degree k when nx_create_fe's tables are exactly a (k, 0) layout's
+ * (layout_fe.build_fe_layout with m = 0: every entry's and every rhs row's term list equals
+ * the closed form k_assemble_fes evaluates without the tables), else 0 -- then the handle
+ * keeps the gather kernel k_assemble_fe. nx_create_fe runs this check itself; exported so
+ * the host (and the CPU tests) can probe it without a device. Replaces nothing in the
+ * reference: its forms are compiled per degree by FFCx (assembly.py:121-146).
+ */
+int nx_fe_struct_degree(int32_t N, int64_t n_edges, int64_t n_rows, const int32_t* rowptr,
+                        const int32_t* col, int32_t n_table, const int32_t* a_ptr,
+                        const int32_t* a_idx, const int32_t* a_ent, const int32_t* b_ptr,
+                        const int32_t* b_idx, const int32_t* b_ent, int32_t* k_out);
+
 /* Release every device buffer, graph and communicator of the handle. */
 int nx_destroy(nx_network_t* h);
 

@@ -42,6 +42,8 @@ _SIGS = {
                             C.POINTER(_h)]),
     "nx_create_fe": (C.c_int, [_i32, _i32, _i64, _pd, _i64, _pi32, _pi32, _i32, _pi32, _pd,
                                _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, C.POINTER(_h)]),
+    "nx_fe_struct_degree": (C.c_int, [_i32, _i64, _i64, _pi32, _pi32, _i32, _pi32, _pi32,
+                                      _pi32, _pi32, _pi32, _pi32, _pi32]),
     "nx_destroy": (C.c_int, [_h]),
     "nx_dims": (C.c_int, [_h, _pi64, _pi64, _pi64]),
     "nx_set_coefficients": (C.c_int, [_h, _pd, _f64, _f64, _pd]),
@@ -170,6 +172,19 @@ def _ptr(a: np.ndarray | None, ctype):
     if a is None:
         return None
     return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def fe_struct_degree(lay) -> int:
+    """k when ``lay`` (a :class:`layout_fe.FeLayout`) is a (k, 0) layout whose terms the
+    structured kernel forms in closed form, else 0 (``nx_fe_struct_degree``; no device)."""
+    a = [np.ascontiguousarray(x, dtype=np.int32) for x in
+         (lay.rowptr, lay.col, lay.a_ptr, lay.a_idx, lay.a_ent, lay.b_ptr, lay.b_idx, lay.b_ent)]
+    k = C.c_int32()
+    check(lib().nx_fe_struct_degree(int(lay.N), int(lay.E), int(lay.n_rows),
+                                    *[_ptr(x, C.c_int32) for x in a[:2]],
+                                    int(lay.table_kind.size),
+                                    *[_ptr(x, C.c_int32) for x in a[2:]], C.byref(k)))
+    return int(k.value)
 
 
 def device_count() -> int:

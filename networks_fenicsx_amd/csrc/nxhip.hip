@@ -6335,6 +6335,7 @@ struct nx_network {
   // owned), the row maps, the cell constants C | K | Mii and a + b
   nx_network* fe_aux = nullptr;
   int fe_k = 0, fe_nl = 0;
+  int fe_sk = 0;  // > 0: a (k, 0) layout whose terms k_assemble_fes forms in closed form
   int *fe_slot = nullptr, *fe_vfe = nullptr, *fe_vaux = nullptr, *fe_ife = nullptr;
   int *fe_pfe = nullptr, *fe_paux = nullptr, *fe_lfe = nullptr, *fe_laux = nullptr;
   double* fe_cst = nullptr;
@@ -6991,6 +6992,7 @@ struct FeArgs {
   double* val;
   double* rhs;
   int lhs, do_rhs;
+  int64_t n_edges;  // (k_assemble_fes)
 };
 
 // length of cell c of edge e, vertices generated like the reference mesh (mesh.py:275-291)
@@ -7035,6 +7037,112 @@ __global__ __launch_bounds__(kBlock) void k_assemble_fe(FeArgs a) {
     double s = 0.0;
     for (int c = a.b_ptr[t]; c < a.b_ptr[t + 1]; ++c) s += fe_term(a, a.b_idx[c], a.b_ent[c]);
     a.rhs[t] = s;
+  }
+}
+
+// (k, 0) layouts (layout_fe.py with m = 0): the terms of entry (row, col) in closed form --
+// the same (index, table entry) list, in the same order, as the host's gather tables, which
+// nx_create_fe checks entry by entry before it lets k_assemble_fes replace k_assemble_fe.
+// Per edge e: kN + 1 flux rows then N cell pressure rows (per = kN + 1 + N); the multiplier
+// rows after all edges. Table: (k+1)^2 mass, k+1 divergence, +1, -1, source, bc.
+struct FeTerm {
+  int idx, ent;
+};
+__host__ __device__ __forceinline__ int fe_s_terms(int64_t row, int64_t col, int k, int N,
+                                                   int64_t E, FeTerm* out) {
+  const int nq = k + 1, nf = k * N + 1, per = nf + N;
+  const int64_t nE = E * (int64_t)per;
+  const int ent_b = nq * nq, ent_plus = nq * nq + nq, ent_minus = ent_plus + 1;
+  if (row >= nE) {  // a multiplier row: +1 at an in-edge's last flux, -1 at an out-edge's first
+    if (col >= nE) return 0;
+    const int cp = (int)(col % per);
+    if (cp == nf - 1) out[0] = FeTerm{0, ent_plus};
+    else if (cp == 0) out[0] = FeTerm{0, ent_minus};
+    else return 0;
+    return 1;
+  }
+  const int64_t e = row / per;
+  const int pos = (int)(row - e * per);
+  if (col >= nE) {  // a flux end's multiplier column
+    if (pos == nf - 1) out[0] = FeTerm{0, ent_plus};
+    else if (pos == 0) out[0] = FeTerm{0, ent_minus};
+    else return 0;
+    return 1;
+  }
+  if (col / per != e) return 0;
+  const int cp = (int)(col - e * per);
+  const int64_t c0 = e * (int64_t)N;
+  if (pos >= nf) {  // a pressure row: divergence of its cell's flux nodes
+    const int c = pos - nf, i = cp - c * k;
+    if (cp >= nf || i < 0 || i > k) return 0;
+    out[0] = FeTerm{(int)(c0 + c), ent_b + i};
+    return 1;
+  }
+  if (cp >= nf) {  // a flux row's gradient entry
+    const int c = cp - nf, i = pos - c * k;
+    if (i < 0 || i > k) return 0;
+    out[0] = FeTerm{(int)(c0 + c), ent_b + i};
+    return 1;
+  }
+  // flux-flux mass: the cells holding both nodes, by reference entry then cell (generation order)
+  int n = 0;
+  FeTerm t[2];
+  int blk[2];
+  for (int side = 0; side < 2; ++side) {
+    const int c = side == 0 ? pos / k : pos / k - 1;  // the cell on the right / left of the node
+    if (c < 0 || c >= N || (side == 1 && pos % k != 0)) continue;
+    const int i = pos - c * k, j = cp - c * k;
+    if (j < 0 || j > k) continue;
+    t[n] = FeTerm{(int)(c0 + c), i * nq + j};
+    blk[n] = i * nq + j;
+    ++n;
+  }
+  if (n == 2 && (blk[1] < blk[0] || (blk[1] == blk[0] && t[1].idx < t[0].idx))) {
+    out[0] = t[1];
+    out[1] = t[0];
+  } else {
+    for (int q = 0; q < n; ++q) out[q] = t[q];
+  }
+  return n;
+}
+__host__ __device__ __forceinline__ int fe_s_rhs_terms(int64_t row, int k, int N, int64_t E,
+                                                       FeTerm* out) {
+  const int nq = k + 1, nf = k * N + 1, per = nf + N;
+  const int ent_src = nq * nq + nq + 2, ent_bc = ent_src + 1;
+  if (row >= E * (int64_t)per) return 0;
+  const int64_t e = row / per;
+  const int pos = (int)(row - e * per);
+  if (pos >= nf) {
+    out[0] = FeTerm{(int)(e * N + pos - nf), ent_src};
+    return 1;
+  }
+  if (pos == 0) out[0] = FeTerm{(int)(2 * e), ent_bc};
+  else if (pos == nf - 1) out[0] = FeTerm{(int)(2 * e + 1), ent_bc};
+  else return 0;
+  return 1;
+}
+
+// (k, 0) assembly without the gather tables: one thread per row, its CSR segment's terms in
+// closed form (fe_s_terms), summed as k_assemble_fe sums them (the same bits).
+__global__ __launch_bounds__(kBlock) void k_assemble_fes(FeArgs a, const int* __restrict__ rowptr,
+                                                          const int* __restrict__ col, int k) {
+#pragma clang fp contract(off)
+  const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (row >= a.n_rows) return;
+  FeTerm t[2];
+  if (a.lhs) {
+    for (int q = rowptr[row]; q < rowptr[row + 1]; ++q) {
+      const int n = fe_s_terms(row, col[q], k, a.N, a.n_edges, t);
+      double s = 0.0;
+      for (int u = 0; u < n; ++u) s += fe_term(a, t[u].idx, t[u].ent);
+      a.val[q] = s;
+    }
+  }
+  if (a.do_rhs) {
+    const int n = fe_s_rhs_terms(row, k, a.N, a.n_edges, t);
+    double s = 0.0;
+    for (int u = 0; u < n; ++u) s += fe_term(a, t[u].idx, t[u].ent);
+    a.rhs[row] = s;
   }
 }
 
@@ -7145,7 +7253,47 @@ int check_terms(const char* what, int64_t n_out, const int32_t* ptr, const int32
   return NX_OK;
 }
 
+// The flux degree k when the tables are exactly a (k, 0) layout's (fe_s_terms generates every
+// entry's and every rhs row's term list, compared entry by entry), else 0 (the gather kernel).
+int fe_struct_degree(int32_t N, int64_t E, int64_t n_rows, const int32_t* rowptr,
+                     const int32_t* col, int32_t n_table, const int32_t* a_ptr,
+                     const int32_t* a_idx, const int32_t* a_ent, const int32_t* b_ptr,
+                     const int32_t* b_idx, const int32_t* b_ent) {
+  int k = 0;
+  for (int kk = 1; kk <= 16 && !k; ++kk)
+    if (n_table == (kk + 1) * (kk + 1) + (kk + 1) + 4 &&
+        n_rows >= E * (int64_t)(kk * N + 1 + N))
+      k = kk;
+  if (!k) return 0;
+  FeTerm t[2];
+  for (int64_t r = 0; r < n_rows; ++r) {
+    for (int q = rowptr[r]; q < rowptr[r + 1]; ++q) {
+      const int n = fe_s_terms(r, col[q], k, N, E, t);
+      if (n == 0 || a_ptr[q + 1] - a_ptr[q] != n) return 0;
+      for (int u = 0; u < n; ++u)
+        if (a_idx[a_ptr[q] + u] != t[u].idx || a_ent[a_ptr[q] + u] != t[u].ent) return 0;
+    }
+    const int n = fe_s_rhs_terms(r, k, N, E, t);
+    if (b_ptr[r + 1] - b_ptr[r] != n) return 0;
+    for (int u = 0; u < n; ++u)
+      if (b_idx[b_ptr[r] + u] != t[u].idx || b_ent[b_ptr[r] + u] != t[u].ent) return 0;
+  }
+  return k;
+}
+
 }  // namespace
+
+NX_API int nx_fe_struct_degree(int32_t N, int64_t n_edges, int64_t n_rows, const int32_t* rowptr,
+                               const int32_t* col, int32_t n_table, const int32_t* a_ptr,
+                               const int32_t* a_idx, const int32_t* a_ent, const int32_t* b_ptr,
+                               const int32_t* b_idx, const int32_t* b_ent, int32_t* k_out) {
+  if (!rowptr || !col || !a_ptr || !a_idx || !a_ent || !b_ptr || !b_idx || !b_ent || !k_out)
+    return fail(NX_ERR_ARG, "NULL array");
+  if (N < 1 || n_edges < 1 || n_rows < 1) return fail(NX_ERR_ARG, "bad sizes");
+  *k_out = fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr, a_idx, a_ent,
+                            b_ptr, b_idx, b_ent);
+  return NX_OK;
+}
 
 NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
                         int64_t n_rows, const int32_t* rowptr, const int32_t* col,
@@ -7193,6 +7341,8 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
     nx_destroy(h);
     return rc ? rc : fail(NX_ERR_HIP, "upload of the element tables failed");
   }
+  h->fe_sk = fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr, a_idx, a_ent,
+                              b_ptr, b_idx, b_ent);
   *out = h;
   return NX_OK;
 }
@@ -7318,10 +7468,15 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
   if (h->fe) {  // general degrees: one thread per nonzero / rhs row
     FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind, h->fe_tval,
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
-             h->nnz, h->n_own, h->val, h->rhs, lhs, rhs};
+             h->nnz, h->n_own, h->val, h->rhs, lhs, rhs, h->E};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
-    hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
-                          dim3(kBlock), 0, s, e0, e1, 0, a);
+    const char* es = std::getenv("NXHIP_FE_STRUCT");  // 0: the gather tables (tests)
+    if (h->fe_sk > 0 && (es == nullptr || std::atoi(es) != 0))
+      hipExtLaunchKernelGGL(k_assemble_fes, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, s,
+                            e0, e1, 0, a, h->rowptr, h->col, h->fe_sk);
+    else
+      hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
+                            dim3(kBlock), 0, s, e0, e1, 0, a);
     HIPCALL(hipGetLastError());
     return NX_OK;
   }
@@ -8414,7 +8569,12 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
                     int32_t* converged) {
   nx_network* a = h->fe_aux;
   CHECK(flush_assembly(h));
+  const bool apend = a->pend_lhs || a->pend_rhs;
   CHECK(flush_assembly(a));
+  if (apend) {  // (the auxiliary handle's own assembly ran on its stream)
+    HIPCALL(hipEventRecord(h->fe_ev[1], a->stream));
+    HIPCALL(hipStreamWaitEvent(h->stream, h->fe_ev[1], 0));
+  }
   const FeCond c{h->edge_x, h->edge_R, h->N, h->fe_k - 1, h->E, h->fe_slot, h->fe_vfe,
                  h->fe_vaux, h->fe_ife, h->fe_pfe, h->fe_paux, h->fe_lfe, h->fe_laux, h->fe_nl,
                  h->fe_cst, h->fe_ab};
@@ -8427,11 +8587,13 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
     const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
     hipLaunchKernelGGL(k_fe_condense, dim3(grid_of(n0, kBlock)), dim3(kBlock), 0, h->stream, c,
                        b, pass ? nullptr : a->dq, a->rhs);
-    HIPCALL(hipEventRecord(h->fe_ev[0], h->stream));
-    HIPCALL(hipStreamWaitEvent(a->stream, h->fe_ev[0], 0));
-    CHECK(launch_direct(a, 0.0, 0));
-    HIPCALL(hipEventRecord(h->fe_ev[1], a->stream));
-    HIPCALL(hipStreamWaitEvent(h->stream, h->fe_ev[1], 0));
+    {  // the auxiliary tree solve on this handle's stream (no cross-queue hand-offs)
+      const hipStream_t as = a->stream;
+      a->stream = h->stream;
+      const int rc = launch_direct(a, 0.0, 0);
+      a->stream = as;
+      CHECK(rc);
+    }
     hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
                        c, a->x, b, h->x, pass);
     hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
