@@ -6336,6 +6336,8 @@ struct nx_network {
   nx_network* fe_aux = nullptr;
   int fe_k = 0, fe_nl = 0;
   int fe_sk = 0;  // > 0: a (k, 0) layout whose terms k_assemble_fes forms in closed form
+  bool fe_fuse = false;  // nx_fe_set_direct: the row maps in closed form (k_fe_expand_res)
+  int64_t fe_edge_nnz = 0;  // the most nonzeros of one edge's rows (fe_sk > 0)
   int *fe_slot = nullptr, *fe_vfe = nullptr, *fe_vaux = nullptr, *fe_ife = nullptr;
   int *fe_pfe = nullptr, *fe_paux = nullptr, *fe_lfe = nullptr, *fe_laux = nullptr;
   double* fe_cst = nullptr;
@@ -7048,52 +7050,42 @@ __global__ __launch_bounds__(kBlock) void k_assemble_fe(FeArgs a) {
 struct FeTerm {
   int idx, ent;
 };
-__host__ __device__ __forceinline__ int fe_s_terms(int64_t row, int64_t col, int k, int N,
-                                                   int64_t E, FeTerm* out) {
-  const int nq = k + 1, nf = k * N + 1, per = nf + N;
-  const int64_t nE = E * (int64_t)per;
+// an edge row's terms: pos its row and lc its column within the edge (0 .. per-1), or lc = -1
+// for a multiplier column, -2 for another edge's; c0 = the edge's first cell
+__host__ __device__ __forceinline__ int fe_s_terms_loc(int pos, int lc, int k, int N, int c0,
+                                                       FeTerm* out) {
+  const int nq = k + 1, nf = k * N + 1;
   const int ent_b = nq * nq, ent_plus = nq * nq + nq, ent_minus = ent_plus + 1;
-  if (row >= nE) {  // a multiplier row: +1 at an in-edge's last flux, -1 at an out-edge's first
-    if (col >= nE) return 0;
-    const int cp = (int)(col % per);
-    if (cp == nf - 1) out[0] = FeTerm{0, ent_plus};
-    else if (cp == 0) out[0] = FeTerm{0, ent_minus};
-    else return 0;
-    return 1;
-  }
-  const int64_t e = row / per;
-  const int pos = (int)(row - e * per);
-  if (col >= nE) {  // a flux end's multiplier column
+  if (lc == -1) {  // a flux end's multiplier column
     if (pos == nf - 1) out[0] = FeTerm{0, ent_plus};
     else if (pos == 0) out[0] = FeTerm{0, ent_minus};
     else return 0;
     return 1;
   }
-  if (col / per != e) return 0;
-  const int cp = (int)(col - e * per);
-  const int64_t c0 = e * (int64_t)N;
+  if (lc < 0) return 0;
   if (pos >= nf) {  // a pressure row: divergence of its cell's flux nodes
-    const int c = pos - nf, i = cp - c * k;
-    if (cp >= nf || i < 0 || i > k) return 0;
-    out[0] = FeTerm{(int)(c0 + c), ent_b + i};
+    const int c = pos - nf, i = lc - c * k;
+    if (lc >= nf || i < 0 || i > k) return 0;
+    out[0] = FeTerm{c0 + c, ent_b + i};
     return 1;
   }
-  if (cp >= nf) {  // a flux row's gradient entry
-    const int c = cp - nf, i = pos - c * k;
+  if (lc >= nf) {  // a flux row's gradient entry
+    const int c = lc - nf, i = pos - c * k;
     if (i < 0 || i > k) return 0;
-    out[0] = FeTerm{(int)(c0 + c), ent_b + i};
+    out[0] = FeTerm{c0 + c, ent_b + i};
     return 1;
   }
   // flux-flux mass: the cells holding both nodes, by reference entry then cell (generation order)
   int n = 0;
   FeTerm t[2];
   int blk[2];
+  const int pk = pos / k;
   for (int side = 0; side < 2; ++side) {
-    const int c = side == 0 ? pos / k : pos / k - 1;  // the cell on the right / left of the node
-    if (c < 0 || c >= N || (side == 1 && pos % k != 0)) continue;
-    const int i = pos - c * k, j = cp - c * k;
+    const int c = side == 0 ? pk : pk - 1;  // the cell on the right / left of the node
+    if (c < 0 || c >= N || (side == 1 && pos - pk * k != 0)) continue;
+    const int i = pos - c * k, j = lc - c * k;
     if (j < 0 || j > k) continue;
-    t[n] = FeTerm{(int)(c0 + c), i * nq + j};
+    t[n] = FeTerm{c0 + c, i * nq + j};
     blk[n] = i * nq + j;
     ++n;
   }
@@ -7104,6 +7096,24 @@ __host__ __device__ __forceinline__ int fe_s_terms(int64_t row, int64_t col, int
     for (int q = 0; q < n; ++q) out[q] = t[q];
   }
   return n;
+}
+__host__ __device__ __forceinline__ int fe_s_terms(int64_t row, int64_t col, int k, int N,
+                                                   int64_t E, FeTerm* out) {
+  const int nq = k + 1, nf = k * N + 1, per = nf + N;
+  const int64_t nE = E * (int64_t)per;
+  const int ent_plus = nq * nq + nq, ent_minus = ent_plus + 1;
+  if (row >= nE) {  // a multiplier row: +1 at an in-edge's last flux, -1 at an out-edge's first
+    if (col >= nE) return 0;
+    const int cp = (int)(col % per);
+    if (cp == nf - 1) out[0] = FeTerm{0, ent_plus};
+    else if (cp == 0) out[0] = FeTerm{0, ent_minus};
+    else return 0;
+    return 1;
+  }
+  const int64_t e = row / per;
+  const int pos = (int)(row - e * per);
+  const int lc = col >= nE ? -1 : col / per != e ? -2 : (int)(col - e * per);
+  return fe_s_terms_loc(pos, lc, k, N, (int)(e * N), out);
 }
 __host__ __device__ __forceinline__ int fe_s_rhs_terms(int64_t row, int k, int N, int64_t E,
                                                        FeTerm* out) {
@@ -7122,28 +7132,112 @@ __host__ __device__ __forceinline__ int fe_s_rhs_terms(int64_t row, int k, int N
   return 1;
 }
 
-// (k, 0) assembly without the gather tables: one thread per row, its CSR segment's terms in
-// closed form (fe_s_terms), summed as k_assemble_fe sums them (the same bits).
-__global__ __launch_bounds__(kBlock) void k_assemble_fes(FeArgs a, const int* __restrict__ rowptr,
-                                                          const int* __restrict__ col, int k) {
+// (k, 0) assembly without the gather tables (k_assemble_fes): one wave per edge. The edge's
+// rows and CSR segments are contiguous, so the wave's lanes stride over its nonzeros
+// (coalesced col reads and value writes), each finding its row by a binary search of the
+// edge's row pointers in LDS; the cell lengths are formed once per edge (fe_cell_h, the same
+// bits) and every entry sums its closed-form terms (fe_s_terms) in the gather tables' order,
+// so the values equal k_assemble_fe's bit for bit. The multiplier rows: one thread each, in
+// the blocks after the edges'.
+constexpr int kFesWaves = 4;    // waves (edges) per block
+constexpr int kFesRows = 512;   // row pointers per edge in LDS: k N + 1 + N + 1 at most
+constexpr int kFesCells = 256;  // cells per edge in LDS
+constexpr int kFesTable = 128;  // term table entries in LDS
+constexpr int kFesNnz = 1024;   // (k_fe_expand_res) nonzeros per edge in LDS
+__device__ __forceinline__ double fe_term_h(const FeArgs& a, int idx, int ent, double hc) {
 #pragma clang fp contract(off)
-  const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (row >= a.n_rows) return;
+  const double v = a.tval[ent];
+  switch (a.kind[ent]) {
+    case kFeMass: return (a.edge_R[idx / a.N] * hc) * v;
+    case kFeSource: return ((a.edge_f ? a.edge_f[idx / a.N] : a.f) * hc) * v;
+    case kFeBc: return a.edge_bc[idx] * v;
+    default: return v;
+  }
+}
+// an edge entry's value from its local terms (fe_term's expressions: the same bits); the
+// table in LDS, the edge's R and cell lengths at hand
+__device__ __forceinline__ double fe_entry_loc(const FeTerm* t, int n, const int* sKind,
+                                               const double* sTv, double Re, const double* hh,
+                                               int c0) {
+#pragma clang fp contract(off)
+  double s = 0.0;
+  for (int u = 0; u < n; ++u) {
+    const double v = sTv[t[u].ent];
+    s += sKind[t[u].ent] == kFeMass ? (Re * hh[t[u].idx - c0]) * v : v;
+  }
+  return s;
+}
+// the edge's row r's position by binary search of its row pointers (rp[0 .. per])
+__device__ __forceinline__ int fe_row_of(const int* rp, int per, int q) {
+  int lo = 0, hi = per - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rp[mid] <= q) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(64 * kFesWaves) void k_assemble_fes(FeArgs a,
+                                                                  const int* __restrict__ rowptr,
+                                                                  const int* __restrict__ col,
+                                                                  int k, int edge_blocks) {
+#pragma clang fp contract(off)
+  __shared__ int sRp[kFesWaves][kFesRows];
+  __shared__ double sH[kFesWaves][kFesCells];
+  __shared__ double sTv[kFesTable];
+  __shared__ int sKind[kFesTable];
+  const int N = a.N, nf = k * N + 1, per = nf + N, nt = (k + 1) * (k + 1) + (k + 1) + 4;
+  const int64_t E = a.n_edges, nE = E * (int64_t)per;
   FeTerm t[2];
-  if (a.lhs) {
-    for (int q = rowptr[row]; q < rowptr[row + 1]; ++q) {
-      const int n = fe_s_terms(row, col[q], k, a.N, a.n_edges, t);
-      double s = 0.0;
-      for (int u = 0; u < n; ++u) s += fe_term(a, t[u].idx, t[u].ent);
-      a.val[q] = s;
+  if ((int)blockIdx.x >= edge_blocks) {  // the multiplier rows
+    const int64_t row = nE + (int64_t)(blockIdx.x - edge_blocks) * blockDim.x + threadIdx.x;
+    if (row >= a.n_rows) return;
+    if (a.lhs)
+      for (int q = rowptr[row]; q < rowptr[row + 1]; ++q) {
+        const int n = fe_s_terms(row, col[q], k, N, E, t);
+        double s = 0.0;
+        for (int u = 0; u < n; ++u) s += fe_term_h(a, t[u].idx, t[u].ent, 0.0);
+        a.val[q] = s;
+      }
+    if (a.do_rhs) a.rhs[row] = 0.0;  // (no terms)
+    return;
+  }
+  for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+    sTv[i] = a.tval[i];
+    sKind[i] = a.kind[i];
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * kFesWaves + w;
+  const int64_t r0 = e * per;
+  int* rp = sRp[w];
+  double* hh = sH[w];
+  if (e < E) {
+    for (int i = lane; i <= per; i += 64) rp[i] = rowptr[r0 + i];
+    for (int c = lane; c < N; c += 64) hh[c] = fe_cell_h(a.edge_x, e * N + c, N);
+  }
+  __syncthreads();
+  if (e >= E) return;
+  const int q0 = rp[0], q1 = rp[per];
+  const int c0 = (int)(e * N);
+  const double Re = a.edge_R[e];
+  if (a.lhs)
+    for (int q = q0 + lane; q < q1; q += 64) {
+      const int pos = fe_row_of(rp, per, q);
+      const int64_t cq = col[q];
+      const int lc = cq >= nE ? -1 : (cq >= r0 && cq < r0 + per) ? (int)(cq - r0) : -2;
+      const int n = fe_s_terms_loc(pos, lc, k, N, c0, t);
+      a.val[q] = fe_entry_loc(t, n, sKind, sTv, Re, hh, c0);
     }
-  }
-  if (a.do_rhs) {
-    const int n = fe_s_rhs_terms(row, k, a.N, a.n_edges, t);
-    double s = 0.0;
-    for (int u = 0; u < n; ++u) s += fe_term(a, t[u].idx, t[u].ent);
-    a.rhs[row] = s;
-  }
+  if (a.do_rhs)
+    for (int r = lane; r < per; r += 64) {
+      const int n = fe_s_rhs_terms(r0 + r, k, N, E, t);
+      double s = 0.0;
+      for (int u = 0; u < n; ++u) {
+        const int ci = t[u].idx - c0;
+        s += fe_term_h(a, t[u].idx, t[u].ent, ci >= 0 && ci < N ? hh[ci] : 0.0);
+      }
+      a.rhs[r0 + r] = s;
+    }
 }
 
 // ---- (k, 0) through the condensed P1/DG0 system (nx_fe_set_direct). The divergence against
@@ -7234,6 +7328,131 @@ __global__ __launch_bounds__(kBlock) void k_fe_expand(FeCond c, const double* __
   if (dst >= 0) x[dst] = accum ? x[dst] + v : v;
 }
 
+// (k, 0), first pass, fused: expand + the true residual in one launch (nx_fe_set_direct found
+// the row maps in closed form and k_assemble_fes forms the matrix). Every x value is a local
+// function of the auxiliary solution xa and b (vertex fluxes, pressures and multipliers are
+// copies, the interior fluxes from their cell), so one wave per edge forms its edge's x in
+// LDS, stores it, and forms its rows' residual r = b - A x with A's entries from the closed
+// form (fe_s_terms: the stored CSR's values bit for bit, the coefficients unchanged since the
+// lhs assembly) and the multiplier columns' x from xa; the multiplier rows (their columns are
+// edge-end fluxes, copies of xa) in the blocks after the edges'. Block partials of ||r||^2 and
+// ||b||^2 for k_dir_publish.
+struct FeFuse {
+  FeArgs a;
+  FeCond c;
+  const int* rowptr;
+  const int* col;
+  int k, edge_blocks;
+  const double* xa;
+  const double* b;
+  double* x;
+  double* rout;
+  double* partials;
+  int nblk;
+};
+__global__ __launch_bounds__(64 * kFesWaves) void k_fe_expand_res(FeFuse F) {
+#pragma clang fp contract(off)
+  __shared__ int sRp[kFesWaves][kFesRows];
+  __shared__ double sH[kFesWaves][kFesCells];
+  __shared__ double sX[kFesWaves][kFesRows];
+  __shared__ double sP[kFesWaves][kFesNnz];
+  __shared__ double sTv[kFesTable];
+  __shared__ int sKind[kFesTable];
+  const FeArgs& a = F.a;
+  const FeCond& c = F.c;
+  const int N = a.N, k = F.k, km = k - 1, nf = k * N + 1, per = nf + N;
+  const int nt = (k + 1) * (k + 1) + (k + 1) + 4;
+  const int64_t E = a.n_edges, nE = E * (int64_t)per;
+  FeTerm t[2];
+  double rr = 0.0, bb = 0.0;
+  if ((int)blockIdx.x >= F.edge_blocks) {  // the multiplier rows
+    const int64_t row = nE + (int64_t)(blockIdx.x - F.edge_blocks) * blockDim.x + threadIdx.x;
+    if (row < a.n_rows) {
+      const int64_t li = row - nE;
+      F.x[row] = F.xa[c.laux[li]];
+      double s = 0.0;
+      for (int q = F.rowptr[row]; q < F.rowptr[row + 1]; ++q) {
+        const int cq = F.col[q];
+        const int n = fe_s_terms(row, cq, k, N, E, t);
+        double v = 0.0;
+        for (int u = 0; u < n; ++u) v += fe_term_h(a, t[u].idx, t[u].ent, 0.0);
+        const int64_t e2 = cq / per;  // an edge-end flux: its vertex's copy of xa
+        const int pos = (int)(cq - e2 * per);
+        s += v * F.xa[c.vaux[e2 * (N + 1) + pos / k]];
+      }
+      const double bv = F.b[row], rv = bv - s;
+      F.rout[row] = rv;
+      rr = rv * rv;
+      bb = bv * bv;
+    }
+  } else {
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+      sTv[i] = a.tval[i];
+      sKind[i] = a.kind[i];
+    }
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* rp = sRp[w];
+    double* hh = sH[w];
+    double* xs = sX[w];
+    double* pr = sP[w];
+    const double* K = c.cst + 2 * km;
+    const double* Mii = c.cst + 4 * km;
+    // (edge rounds: the partials hold nblk blocks; the loop condition is block-uniform)
+    for (int64_t eb0 = (int64_t)blockIdx.x * kFesWaves; eb0 < E;
+         eb0 += (int64_t)F.edge_blocks * kFesWaves) {
+      const int64_t e = eb0 + w;
+      const int64_t r0 = e * per;
+      const int c0 = (int)(e * N);
+      __syncthreads();  // (the previous round's LDS reads)
+      if (e < E) {
+        for (int i = lane; i <= per; i += 64) rp[i] = F.rowptr[r0 + i];
+        for (int g = lane; g < N; g += 64) hh[g] = fe_cell_h(a.edge_x, e * N + g, N);
+        for (int g = lane; g <= N; g += 64) xs[g * k] = F.xa[c.vaux[e * (N + 1) + g]];
+        for (int g = lane; g < N; g += 64) xs[nf + g] = F.xa[c.paux[e * N + g]];
+      }
+      __syncthreads();
+      const double Re = e < E ? a.edge_R[e] : 0.0;
+      if (e < E)
+        for (int q = lane; q < N * km; q += 64) {  // interior flux j of cell g (k_fe_expand's)
+          const int g = q / km, j = q - g * km;
+          const int64_t cell = e * N + g;
+          const double Rh = Re * hh[g];
+          const double xl = xs[g * k], xr = xs[(g + 1) * k];
+          double s = 0.0;
+          for (int i = 0; i < km; ++i) s += Mii[j * km + i] * F.b[c.ife[cell * km + i]];
+          xs[g * k + 1 + j] = s / Rh - K[2 * j] * xl - K[2 * j + 1] * xr;
+        }
+      __syncthreads();
+      if (e < E) {
+        for (int i = lane; i < per; i += 64) F.x[r0 + i] = xs[i];
+        const int q0 = rp[0], q1 = rp[per];
+        for (int q = q0 + lane; q < q1; q += 64) {  // products, coalesced over the nonzeros
+          const int pos = fe_row_of(rp, per, q);
+          const int64_t cq = F.col[q];
+          const int lc = cq >= nE ? -1 : (cq >= r0 && cq < r0 + per) ? (int)(cq - r0) : -2;
+          const int n = fe_s_terms_loc(pos, lc, k, N, c0, t);
+          const double v = fe_entry_loc(t, n, sKind, sTv, Re, hh, c0);
+          pr[q - q0] = v * (lc >= 0 ? xs[lc] : F.xa[c.laux[cq - nE]]);
+        }
+      }
+      __syncthreads();
+      if (e < E)
+        for (int i = lane; i < per; i += 64) {  // row r0 + i's residual, in CSR order
+          const int q0 = rp[0];
+          double s = 0.0;
+          for (int q = rp[i]; q < rp[i + 1]; ++q) s += pr[q - q0];
+          const double bv = F.b[r0 + i], rv = bv - s;
+          F.rout[r0 + i] = rv;
+          rr += rv * rv;
+          bb += bv * bv;
+        }
+    }
+  }
+  block_sum_store(rr, F.partials + blockIdx.x);
+  __syncthreads();
+  block_sum_store(bb, F.partials + F.nblk + blockIdx.x);
+}
+
 // terms [ptr[i], ptr[i+1]) of every output i must reference the table and the cell / edge
 // arrays in range
 int check_terms(const char* what, int64_t n_out, const int32_t* ptr, const int32_t* idx,
@@ -7264,7 +7483,8 @@ int fe_struct_degree(int32_t N, int64_t E, int64_t n_rows, const int32_t* rowptr
     if (n_table == (kk + 1) * (kk + 1) + (kk + 1) + 4 &&
         n_rows >= E * (int64_t)(kk * N + 1 + N))
       k = kk;
-  if (!k) return 0;
+  if (!k || k * N + 1 + N + 1 > kFesRows || N > kFesCells || n_table > kFesTable)
+    return 0;  // (k_assemble_fes' LDS)
   FeTerm t[2];
   for (int64_t r = 0; r < n_rows; ++r) {
     for (int q = rowptr[r]; q < rowptr[r + 1]; ++q) {
@@ -7343,6 +7563,11 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
   }
   h->fe_sk = fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr, a_idx, a_ent,
                               b_ptr, b_idx, b_ent);
+  if (h->fe_sk > 0) {  // (k_fe_expand_res stages an edge's nonzeros in LDS)
+    const int64_t per = h->fe_sk * (int64_t)N + 1 + N;
+    for (int64_t e = 0; e < n_edges; ++e)
+      h->fe_edge_nnz = std::max<int64_t>(h->fe_edge_nnz, rowptr[(e + 1) * per] - rowptr[e * per]);
+  }
   *out = h;
   return NX_OK;
 }
@@ -7470,13 +7695,19 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
              h->nnz, h->n_own, h->val, h->rhs, lhs, rhs, h->E};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
-    const char* es = std::getenv("NXHIP_FE_STRUCT");  // 0: the gather tables (tests)
-    if (h->fe_sk > 0 && (es == nullptr || std::atoi(es) != 0))
-      hipExtLaunchKernelGGL(k_assemble_fes, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, s,
-                            e0, e1, 0, a, h->rowptr, h->col, h->fe_sk);
-    else
+    // NXHIP_FE_STRUCT=1: the closed-form kernel (measured slower than the gather tables at
+    // C3: latency-bound, one wave per edge), else the gather tables
+    const char* es = std::getenv("NXHIP_FE_STRUCT");
+    if (h->fe_sk > 0 && es != nullptr && std::atoi(es) != 0) {
+      const int eb = (int)grid_of(h->E, kFesWaves);
+      const int64_t nE = h->E * (int64_t)(h->fe_sk * h->N + 1 + h->N);
+      const int lb = (int)grid_of(h->n_own - nE, 64 * kFesWaves);
+      hipExtLaunchKernelGGL(k_assemble_fes, dim3(eb + lb), dim3(64 * kFesWaves), 0, s, e0, e1, 0,
+                            a, h->rowptr, h->col, h->fe_sk, eb);
+    } else {
       hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
                             dim3(kBlock), 0, s, e0, e1, 0, a);
+    }
     HIPCALL(hipGetLastError());
     return NX_OK;
   }
@@ -8594,12 +8825,30 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
       a->stream = as;
       CHECK(rc);
     }
-    hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
-                       c, a->x, b, h->x, pass);
-    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
-    hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                       nrb, rtol, h->d_seq, h->d_last);
+    // NXHIP_FE_FUSE=1: expand + residual fused (measured slower at C3)
+    const char* ef = std::getenv("NXHIP_FE_FUSE");
+    const int64_t nE = h->E * (int64_t)(h->fe_k * h->N + 1 + h->N);
+    const int lb = grid_of(h->n_own - nE, 64 * kFesWaves);
+    const int eb = std::max(1, std::min(grid_of(h->E, kFesWaves), h->nblk - lb));
+    if (pass == 0 && h->fe_fuse && h->fe_sk == h->fe_k && h->asm_coef_version == h->coef_version &&
+        eb + lb <= h->nblk && ef != nullptr && std::atoi(ef) != 0) {
+      const int nblk = eb + lb;  // (<= h->nblk: the partials' size)
+      const FeFuse F{FeArgs{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind,
+                            h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr,
+                            h->fe_bidx, h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E},
+                     c, h->rowptr, h->col, h->fe_k, eb, a->x, h->rhs, h->x, h->tmp, h->partials,
+                     nblk};
+      hipLaunchKernelGGL(k_fe_expand_res, dim3(nblk), dim3(64 * kFesWaves), 0, h->stream, F);
+      hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                         nblk, rtol, h->d_seq, h->d_last);
+    } else {
+      hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
+                         c, a->x, b, h->x, pass);
+      hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                         h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
+      hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                         nrb, rtol, h->d_seq, h->d_last);
+    }
     HIPCALL(hipGetLastError());
     h->seq += 1;
     CHECK(wait_published(h));
@@ -9901,6 +10150,20 @@ NX_API int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64
   h->fe_k = k;
   h->fe_nl = (int)n_lm;
   h->fe_ab = ab;
+  {  // the fused expand + residual: the (k, 0) closed form and its row maps
+    const int64_t per = k * N + 1 + N, nE = E * per;
+    bool ok = h->fe_sk == k && h->fe_edge_nnz <= kFesNnz;
+    for (int64_t e = 0; e < E && ok; ++e) {
+      for (int64_t g = 0; g <= N && ok; ++g) ok = v_fe[e * (N + 1) + g] == e * per + g * k;
+      for (int64_t g = 0; g < N && ok; ++g) {
+        ok = p_fe[e * N + g] == e * per + k * N + 1 + g;
+        for (int64_t j = 0; j < km && ok; ++j)
+          ok = i_fe[(e * N + g) * km + j] == e * per + g * k + 1 + j;
+      }
+    }
+    for (int64_t i = 0; i < n_lm && ok; ++i) ok = l_fe[i] == nE + i;
+    h->fe_fuse = ok;
+  }
   return NX_OK;
 }
 
