@@ -6338,6 +6338,7 @@ struct nx_network {
   int fe_sk = 0;  // > 0: a (k, 0) layout whose terms k_assemble_fes forms in closed form
   bool fe_fuse = false;  // nx_fe_set_direct: the row maps in closed form (k_fe_expand_res)
   int64_t fe_edge_nnz = 0;  // the most nonzeros of one edge's rows (fe_sk > 0)
+  double* fe_cellh = nullptr;  // E*N cell lengths (k_fe_cellh at nx_create_fe)
   int *fe_slot = nullptr, *fe_vfe = nullptr, *fe_vaux = nullptr, *fe_ife = nullptr;
   int *fe_pfe = nullptr, *fe_paux = nullptr, *fe_lfe = nullptr, *fe_laux = nullptr;
   double* fe_cst = nullptr;
@@ -6995,6 +6996,7 @@ struct FeArgs {
   double* rhs;
   int lhs, do_rhs;
   int64_t n_edges;  // (k_assemble_fes)
+  const double* cellh;  // E*N cell lengths (fe_cell_h, once per handle), or null: formed here
 };
 
 // length of cell c of edge e, vertices generated like the reference mesh (mesh.py:275-291)
@@ -7019,12 +7021,22 @@ __device__ __forceinline__ double fe_term(const FeArgs& a, int idx, int ent) {
 #pragma clang fp contract(off)
   const double v = a.tval[ent];
   switch (a.kind[ent]) {
-    case kFeMass: return (a.edge_R[idx / a.N] * fe_cell_h(a.edge_x, idx, a.N)) * v;
+    case kFeMass:
+      return (a.edge_R[idx / a.N] * (a.cellh ? a.cellh[idx] : fe_cell_h(a.edge_x, idx, a.N))) * v;
     case kFeSource:
-      return ((a.edge_f ? a.edge_f[idx / a.N] : a.f) * fe_cell_h(a.edge_x, idx, a.N)) * v;
+      return ((a.edge_f ? a.edge_f[idx / a.N] : a.f) *
+              (a.cellh ? a.cellh[idx] : fe_cell_h(a.edge_x, idx, a.N))) * v;
     case kFeBc: return a.edge_bc[idx] * v;
     default: return v;
   }
+}
+
+// every cell's length once per handle (the geometry is fixed at nx_create_fe): the gathered
+// mass and source terms read it instead of forming both vertices per term (the same bits)
+__global__ __launch_bounds__(kBlock) void k_fe_cellh(const double* __restrict__ edge_x, int N,
+                                                     int64_t n_cells, double* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (c < n_cells) out[c] = fe_cell_h(edge_x, c, N);
 }
 
 __global__ __launch_bounds__(kBlock) void k_assemble_fe(FeArgs a) {
@@ -7253,6 +7265,7 @@ struct FeCond {
   int nl;
   const double* cst;  // C (2 km) | K (km 2) | Mii (km km)
   double ab;          // a + b
+  const double* cellh;  // E*N cell lengths (k_fe_cellh)
 };
 
 // The condensed right-hand side b_v - C b_i (vertex rows; pressure and multiplier rows
@@ -7272,12 +7285,12 @@ __global__ __launch_bounds__(kBlock) void k_fe_condense(FeCond c, const double* 
     double bv = b[c.vfe[t]], d = 0.0;
     if (g > 0) {  // the cell on the left: this vertex is its right one (C row 1)
       const int64_t cell = e * N + g - 1;
-      d = c.ab * (R * fe_cell_h(c.edge_x, cell, N));
+      d = c.ab * (R * c.cellh[cell]);
       for (int i = 0; i < km; ++i) bv -= c.cst[km + i] * b[c.ife[cell * km + i]];
     }
     if (g < N) {  // the cell on the right: its left vertex (C row 0)
       const int64_t cell = e * N + g;
-      d += c.ab * (R * fe_cell_h(c.edge_x, cell, N));
+      d += c.ab * (R * c.cellh[cell]);
       for (int i = 0; i < km; ++i) bv -= c.cst[i] * b[c.ife[cell * km + i]];
     }
     rhs_aux[c.vaux[t]] = bv;
@@ -7312,7 +7325,7 @@ __global__ __launch_bounds__(kBlock) void k_fe_expand(FeCond c, const double* __
   } else if (t < n0 + np) {
     const int64_t cell = t - n0, e = cell / N;
     const int g = (int)(cell - e * N);
-    const double Rh = c.edge_R[e] * fe_cell_h(c.edge_x, cell, N);
+    const double Rh = c.edge_R[e] * c.cellh[cell];
     const double xl = xa[c.vaux[e * (N + 1) + g]], xr = xa[c.vaux[e * (N + 1) + g + 1]];
     const double* K = c.cst + 2 * km;
     const double* Mii = c.cst + 4 * km;
@@ -7557,9 +7570,16 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
       (rc = upload(&h->fe_bptr, b_ptr, n_rows + 1, h->stream)) ||
       (rc = upload(&h->fe_bidx, b_idx, (int64_t)b_ptr[n_rows], h->stream)) ||
       (rc = upload(&h->fe_bent, b_ent, (int64_t)b_ptr[n_rows], h->stream)) ||
+      (rc = dalloc(&h->fe_cellh, n_cells)) ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
     nx_destroy(h);
     return rc ? rc : fail(NX_ERR_HIP, "upload of the element tables failed");
+  }
+  hipLaunchKernelGGL(k_fe_cellh, dim3(grid_of(n_cells, kBlock)), dim3(kBlock), 0, h->stream,
+                     h->edge_x, (int)N, n_cells, h->fe_cellh);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess) {
+    nx_destroy(h);
+    return fail(NX_ERR_HIP, "cell lengths failed");
   }
   h->fe_sk = fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr, a_idx, a_ent,
                               b_ptr, b_idx, b_ent);
@@ -7602,7 +7622,7 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->d_left_k, h->d_cut_own, h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf,
                   h->d_cyc_rows, h->cyc_z, h->cyc_cinv, h->cyc_cap, h->cyc_prev, h->cyc_w,
                   h->fe_slot, h->fe_vfe, h->fe_vaux, h->fe_ife, h->fe_pfe, h->fe_paux, h->fe_lfe,
-                  h->fe_laux, h->fe_cst};
+                  h->fe_laux, h->fe_cst, h->fe_cellh};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -7693,7 +7713,7 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
   if (h->fe) {  // general degrees: one thread per nonzero / rhs row
     FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind, h->fe_tval,
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
-             h->nnz, h->n_own, h->val, h->rhs, lhs, rhs, h->E};
+             h->nnz, h->n_own, h->val, h->rhs, lhs, rhs, h->E, h->fe_cellh};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
     // NXHIP_FE_STRUCT=1: the closed-form kernel (measured slower than the gather tables at
     // C3: latency-bound, one wave per edge), else the gather tables
@@ -8808,7 +8828,7 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
   }
   const FeCond c{h->edge_x, h->edge_R, h->N, h->fe_k - 1, h->E, h->fe_slot, h->fe_vfe,
                  h->fe_vaux, h->fe_ife, h->fe_pfe, h->fe_paux, h->fe_lfe, h->fe_laux, h->fe_nl,
-                 h->fe_cst, h->fe_ab};
+                 h->fe_cst, h->fe_ab, h->fe_cellh};
   const int64_t nv = h->E * (h->N + 1), np = h->E * (int64_t)h->N, n0 = nv + np + h->fe_nl;
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
   MrState s{};
@@ -8835,7 +8855,8 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
       const int nblk = eb + lb;  // (<= h->nblk: the partials' size)
       const FeFuse F{FeArgs{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind,
                             h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr,
-                            h->fe_bidx, h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E},
+                            h->fe_bidx, h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E,
+                            h->fe_cellh},
                      c, h->rowptr, h->col, h->fe_k, eb, a->x, h->rhs, h->x, h->tmp, h->partials,
                      nblk};
       hipLaunchKernelGGL(k_fe_expand_res, dim3(nblk), dim3(64 * kFesWaves), 0, h->stream, F);
