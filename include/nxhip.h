@@ -406,6 +406,12 @@ int nx_debug_set_wait_polls(nx_network_t* h, uint32_t polls);
  * multi-GPU run measured on one GPU (whose ranks cannot all be resident in one launch).
  * h's solution is then the rank's share of the answer. Replaces nothing in the reference. */
 int nx_debug_xr_rehearse(nx_network_t* h, double rtol, int32_t reps, double* ms);
+
+/* Debug / tests: the RCCL ranks' shape of the exchange step on one GPU -- every rank of the
+ * group launches its own k_dir_xr on a stream of its own (concurrent launches meeting only
+ * through the mailboxes, the exchange width the handle's rank count), the ranks' assembly
+ * pending. *relres = the published residual (every rank's equal). */
+int nx_debug_xr_separate(nx_group_t* g, double rtol, double* relres);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
 /* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,

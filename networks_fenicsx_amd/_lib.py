@@ -101,6 +101,7 @@ _SIGS = {
     "nx_set_lean": (C.c_int, [_i32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
     "nx_group_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
+    "nx_debug_xr_separate": (C.c_int, [_h, _f64, _pd]),
     "nx_group_destroy": (C.c_int, [_h]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -610,6 +611,13 @@ class Group:
         check(lib().nx_group_solve(self._g, float(rtol), int(maxit), int(check_every),
                                    C.byref(it), C.byref(rr), C.byref(conv)))
         return int(it.value), float(rr.value), bool(conv.value)
+
+    def xr_separate(self, rtol: float = 1e-12) -> float:
+        """Debug / tests: every rank's exchange step as its own launch on its own stream
+        (the RCCL ranks' shape; ``nx_debug_xr_separate``); the published residual."""
+        rr = C.c_double(0.0)
+        check(lib().nx_debug_xr_separate(self._g, float(rtol), C.byref(rr)))
+        return float(rr.value)
 
     def close(self) -> None:
         if getattr(self, "_g", None):

@@ -8385,18 +8385,21 @@ DirStep dir_args(nx_network* h, double rtol) {
 
 template <int W, int CPL>
 int launch_xr_wc(const Team& t, double rtol) {
-  const int P = t.P;
+  // P: the handles launched here (a group's ranks, or this process's one RCCL rank);
+  // X: the ranks exchanging (every rank of the group or of the communicator)
+  const int P = t.P, X = t.g ? t.P : t.hs[0]->nranks;
   std::vector<DirStep> das(P);
   std::vector<int> goff(P + 1, 0);
   size_t lds = 0;
   for (int r = 0; r < P; ++r) {
     nx_network* h = t.hs[r];
+    if (h->nranks != X) return fail(NX_ERR_STATE, "exchange step: rank count mismatch");
     h->xtag += 1;  // (the same on every rank: they launch together)
     DirStep da = dir_args(h, rtol);
     da.n_left = h->xr_nleft;
     da.xpeers = h->d_xpeers;
-    da.xself = xpeer_of(h->xmb, P);
-    da.xP = P;
+    da.xself = xpeer_of(h->xmb, X);
+    da.xP = X;
     da.xrank = h->rank;
     da.xld1 = kXld1;
     da.xld2 = kXld2;
@@ -10637,6 +10640,55 @@ NX_API int nx_debug_xr_rehearse(nx_network_t* h, double rtol, int32_t reps, doub
   }
   *ms = v;
   return rc;
+}
+
+// The RCCL ranks' shape of the exchange step on one GPU: every rank of the group launches its
+// own k_dir_xr (a one-handle team, no group: the exchange width is the handle's nranks) on a
+// stream of its own, so the launches run concurrently and meet only through the mailboxes,
+// as on separate GPUs. The ranks' assembly must be pending (nx_assemble); their jobs must fit
+// the GPU together (co-resident). *relres: rank 0's published residual (every rank's equal).
+NX_API int nx_debug_xr_separate(nx_group_t* g, double rtol, double* relres) {
+  if (!g || !relres) return fail(NX_ERR_ARG, "null argument");
+  const int P = g->P;
+  int jobs = 0;
+  for (nx_network* h : g->hs) {
+    if (!xr_local(h) || !h->pend_lhs || !h->pend_rhs)
+      return fail(NX_ERR_STATE, "every rank able to run the exchange step, its assembly pending");
+    jobs += h->pc_jobs;
+  }
+  if (jobs > g->hs[0]->n_cu) return fail(NX_ERR_STATE, "the ranks' jobs do not fit the GPU together");
+  CHECK(set_device(g->hs[0]));
+  HIPCALL(hipStreamSynchronize(g->stream));
+  std::vector<hipStream_t> ss(P, nullptr);
+  for (int r = 0; r < P; ++r) HIPCALL(hipStreamCreateWithFlags(&ss[r], hipStreamNonBlocking));
+  for (int r = 0; r < P; ++r) g->hs[r]->stream = ss[r];
+  int rc = NX_OK;
+  int launched = 0;
+  for (int r = 0; r < P && rc == NX_OK; ++r, ++launched) rc = launch_xr(Team{&g->hs[r], 1, nullptr}, rtol);
+  for (int r = 0; r < launched; ++r) {
+    const int w = wait_published(g->hs[r]);
+    if (rc == NX_OK) rc = w;
+  }
+  for (int r = 0; r < P; ++r) (void)hipStreamSynchronize(ss[r]);
+  for (int r = 0; r < P; ++r) {
+    nx_network* h = g->hs[r];
+    h->stream = g->stream;
+    (void)hipStreamDestroy(ss[r]);
+    if (rc != NX_OK) {  // (as run_xr: counters and sequence numbers back in step)
+      (void)hipMemset(h->d_dsync, 0, 8 * sizeof(unsigned));
+      (void)hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost);
+      h->dstep_epoch = 0;
+    } else {
+      h->pend_lhs = h->pend_rhs = 0;
+      h->last_dir_path = 3;
+    }
+  }
+  CHECK(rc);
+  for (int r = 1; r < P; ++r)
+    if (g->hs[r]->h_last->relres != g->hs[0]->h_last->relres)
+      return fail(NX_ERR_STATE, "ranks disagree on the exchange step's residual");
+  *relres = g->hs[0]->h_last->relres;
+  return NX_OK;
 }
 
 NX_API int nx_xch_export(nx_network_t* h, unsigned char* handle_out) {

@@ -527,6 +527,37 @@ def test_group_exchange_step(case, P, monkeypatch):
         grp.close()
 
 
+@pytest.mark.parametrize("case,P", [("depth6_N40", 2), ("arterial5_N40", 3), ("tree5_N15", 4)])
+def test_separate_launches_exchange(case, P):
+    """The RCCL ranks' shape of the exchange step: every rank's k_dir_xr as its own launch on
+    its own stream (one-handle teams: the exchange width is the rank count, not the team
+    size), meeting only through the mailboxes -- the same bits as the group's one launch
+    (k_dir_xg), the oracle to 1e-10, on every repeated step."""
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.set_direct(True)
+        grp.assemble()
+        it, rr, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and {a.handle.direct_path() for a in grp.assemblers} == {"exchange"}
+        x1 = _gathered(grp, Ab, mesh)
+        for _ in range(5):
+            grp.assemble()
+            rr2 = grp._group.xr_separate(1e-12)
+            assert {a.handle.direct_path() for a in grp.assemblers} == {"exchange"}
+            np.testing.assert_array_equal(_gathered(grp, Ab, mesh), x1)
+            assert rr2 == rr, (rr2, rr)
+        assert np.linalg.norm(x1 - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+        grp.assemble()  # and the group's launch again after them
+        it, rr3, _ = grp.solve(1e-12, 50000, 4)
+        assert rr3 == rr
+        np.testing.assert_array_equal(_gathered(grp, Ab, mesh), x1)
+    finally:
+        grp.close()
+
+
 def test_group_exchange_give_up_falls_back():
     """Every waiting workgroup gives up (a wait bound of 0 polls): no rank publishes, the host
     resets the hand-off counters and sequence numbers, and the same solve runs the graph
