@@ -24,7 +24,9 @@ One step = device assembly of the CSR matrix and rhs (``nx_assemble``) + the sol
 reference's default options ask for (``ksp_type=preonly`` + ``pc_type=lu``: a direct
 factorisation, solver.py:58-65): on one GPU the direct tree solve (block LU through the
 tree sweeps, true residual checked, rtol 1e-12, one refinement step if it misses; across
-P ranks the same with the coarse all-reduce), with ``--solver minres`` preconditioned
+P ranks one launch per rank, ``k_dir_xr``, exchanging the coarse partials and the residual
+with the other ranks' kernels through peer-mapped mailboxes, the two-all-reduce graph path
+as the fallback), with ``--solver minres`` preconditioned
 MINRES to rtol 1e-12. The other solver is timed on the same workload and reported beside
 (one GPU). Rank 0 prints one JSON line.
 """
@@ -415,27 +417,34 @@ def run(args, world: int) -> int:
         h.set_profiling(False)
         cnt = max(pd["count"], 1)
         n, nnz = h.n_rows, h.nnz
-        if path == "fused":  # one launch per step: k_dir_step (its time is pd's first slot)
+        if path in ("fused", "exchange") and pd["up_ms"] > 0:
+            # one launch per step (per rank): k_dir_step, or k_dir_xr with the ranks'
+            # exchanges inside (its time is pd's first slot)
             t = pd["up_ms"] / cnt
             kb = dstep_bytes(n, nnz, E, N, B, (nnz - E * (7 * N + 1)) // 2)
             ach = kb / (t * 1e-3) / 1e9
-            rocname = "k_dir_step<8, 2>"
+            kname = "k_dir_step" if path == "fused" else "k_dir_xr"
+            rocname = f"{kname}<8, 2>"
             traffic, tsrc, rocprof_ns = (pmc_traffic(rocname) if default_workload
                                          else (None, None, None))
             k = {"avg_launch_ms": t, "algorithmic_bytes_per_launch": kb, "achieved_GBs": ach,
                  "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                  "traffic_ratio": traffic / kb if traffic else None}
+            what = ("the whole direct step in one launch: assembly, up sweep, top part, down "
+                    "sweep, fused residual check, published state; latency-bound"
+                    if path == "fused" else
+                    "one rank's whole direct step in one launch, the coarse partials and the "
+                    "residual exchanged with the other ranks' kernels through peer-mapped "
+                    "mailboxes; latency-bound")
             return {"bound": "hbm",
-                    "kernel": "k_dir_step<8, 2> (the whole direct step in one launch: assembly, "
-                              "up sweep, top part, down sweep, fused residual check, published "
-                              "state; latency-bound)",
+                    "kernel": f"{rocname} ({what})",
                     "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                     "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
                     "traffic_source": tsrc,
                     "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
                     "algorithmic_bytes_per_launch": kb, "avg_launch_ms": t,
-                    "kernels": {"k_dir_step": k}, "assembly_kernel_ms": None,
+                    "kernels": {kname: k}, "assembly_kernel_ms": None,
                     "direct_path": path}
         n_e = E * (2 * N + 1)
         nblk = -(-n // (256 * res_chunks(n)))  # k_residual_ck blocks (partials)

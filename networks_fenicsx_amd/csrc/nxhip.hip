@@ -8436,8 +8436,10 @@ int launch_xr_wc(const Team& t, double rtol) {
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
     (void)hipGetLastError();
-    hipLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
-                       h->stream, h->pa, das[0]);
+    const bool prof = h->prof && h->dev[0];  // (events bound to the dispatch: bench.py)
+    hipExtLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
+                          h->stream, prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0,
+                          h->pa, das[0]);
   }
   HIPCALL(hipGetLastError());
   for (int r = 0; r < P; ++r) {
@@ -8512,11 +8514,20 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   for (int r = 0; r < t.P; ++r) with_asm = with_asm && t.hs[r]->pend_lhs && t.hs[r]->pend_rhs;
   for (int r = 0; r < t.P; ++r) t.hs[r]->last_dir_path = 0;
   if (multi && !h->xr_off && xr_on(t, with_asm)) {  // several ranks: one launch each
+    if (!t.g && h->prof && !h->dev[0])
+      for (auto& e : h->dev) HIPCALL(hipEventCreate(&e));
     const int rc = run_xr(t, rtol);
     if (rc == NX_OK) {
       for (int r = 0; r < t.P; ++r) {
         t.hs[r]->pend_lhs = t.hs[r]->pend_rhs = 0;
         t.hs[r]->last_dir_path = 3;
+      }
+      if (!t.g && h->prof) {  // k_dir_xr's time (bench.py's roofline: one RCCL rank)
+        HIPCALL(hipEventSynchronize(h->dev[1]));
+        float ms = 0.f;
+        HIPCALL(hipEventElapsedTime(&ms, h->dev[0], h->dev[1]));
+        h->dir_ms[0] += ms;
+        h->dir_cnt += 1;
       }
       const MrState s = *h->h_last;
       if (s.converged || s.relres != s.relres) {
