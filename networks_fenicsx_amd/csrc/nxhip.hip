@@ -4641,6 +4641,12 @@ __device__ __forceinline__ void dir_stores_v2(const PcArgs& pa, const DirStep& d
 // after phase 2: those waves poll for the top values and load them without waiting for the
 // drain of the others' stores. The top solver's assembly is stored by the first workgroups to
 // arrive (helpers), one chain per wave on the other waves: kDirHelpChains chains each.
+// k_dir_xr: the top part's solver re-assembles its lanes inside the first exchange's wait
+// (-DNX_XR_MID_ASM=1; measured A/B) instead of after the top part
+#ifndef NX_XR_MID_ASM
+#define NX_XR_MID_ASM 0
+#endif
+constexpr bool kXrMidAsm = NX_XR_MID_ASM != 0;
 constexpr int kDirFreeWaves = 4;
 constexpr int kDirHelpChains = kPcThreads / 64 - kDirFreeWaves;
 // dynamic LDS of k_dir_step: at most this (the static __shared__ words -- flags, the partial
@@ -4691,7 +4697,12 @@ __device__ __forceinline__ double ld_sys(const double* p) {
 // then this rank's P flags polled (bounded) and the P slots summed in rank order (the same
 // additions as k_group_sum: every rank gets the same bits) into dst (LDS). False: a rank's
 // flag never came.
-__device__ __forceinline__ bool xr_allsum(const DirStep& da, int which, const double* src, int n, double* dst) {
+struct XrNoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <class Mid = XrNoMid>
+__device__ __forceinline__ bool xr_allsum(const DirStep& da, int which, const double* src, int n,
+                                          double* dst, const Mid& mid = Mid{}) {
   __shared__ int sOk;
   const int P = da.xP, r = da.xrank, ld = which ? da.xld2 : da.xld1;
   for (int q = 0; q < P; ++q) {
@@ -4704,6 +4715,7 @@ __device__ __forceinline__ bool xr_allsum(const DirStep& da, int which, const do
   if ((int)threadIdx.x < P)
     __hip_atomic_store(da.xpeers[threadIdx.x].fl + which * P + r, da.xtag, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+  mid();  // (work of this workgroup's own while the other ranks' partials travel)
   if ((int)threadIdx.x < P) {
     bool ok = false;
     for (unsigned k = 0; k < da.polls; ++k) {
@@ -4811,14 +4823,16 @@ __device__ __forceinline__ void xr_top_back(const PcArgs& pa, const CoarsePre& c
   __syncthreads();
 }
 
+template <class Mid = XrNoMid>
 __device__ __forceinline__ bool xr_coarse(const PcArgs& pa, const DirStep& da, const TopLds& T,
-                                          const CoarseIdx& ci, const TopPre& pre, double* ext) {
+                                          const CoarseIdx& ci, const TopPre& pre, double* ext,
+                                          const Mid& mid = Mid{}) {
   __shared__ double xb[2 * 3 * kCapCoarseLds];
   const int nC = pa.n_coarse, n1 = 3 * nC;
   for (int i = threadIdx.x; i < n1; i += kPcThreads) xb[i] = ld_wt(pa.cbuf + i);
   __syncthreads();
   NX_DSTAMP(42);
-  if (!xr_allsum(da, 0, xb, n1, xb + n1)) return false;
+  if (!xr_allsum(da, 0, xb, n1, xb + n1, mid)) return false;
   NX_DSTAMP(43);
   if (!pa.c_wave) {  // (pc_coarse_lds reads the sums from cbuf)
     for (int i = threadIdx.x; i < n1; i += kPcThreads) pa.cbuf[i] = xb[n1 + i];
@@ -5029,7 +5043,14 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         NX_DSTAMP(41);
         // (xr_top_back's per-slot scratch after the top part's arrays; sLv is the last)
         double* ext = reinterpret_cast<double*>(T.sLv + ((pa.n_top_lvl + 2) & ~1));
-        if (!xr_coarse(pa, da, T, ci, pre, ext)) {
+        // (keep: its lanes re-assembled while the other ranks' partials travel)
+        auto mid = [&]() {
+          if (keep && kXrMidAsm) {
+            chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+            dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
+          }
+        };
+        if (!xr_coarse(pa, da, T, ci, pre, ext, mid)) {
           if (threadIdx.x == 0)  // (the waiters give up too; the host reports the exchange)
             __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;
@@ -5047,7 +5068,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       if (!keep) {
         dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
-      } else {  // its lanes again, redefined inside this branch: not kept through the solve
+      } else if (!(XR && kXrMidAsm)) {  // its lanes again: not kept through the solve
         chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
         dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
       }
