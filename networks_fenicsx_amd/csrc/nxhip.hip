@@ -3419,6 +3419,7 @@ struct DirStep {
   const double* crec;
   const int* ci;
   int lds_main, lds_top;
+  int lds_park;  // the top part's solver parks its lanes here (doubles from smem), or -1
   // several ranks (k_dir_xr / k_dir_xg): the ranks' mailboxes (xpeers[q]: where this rank
   // writes for rank q), this rank's own (xself: where it reads), the exchange's shape, the
   // launch tag (monotonic, never reset), the cut rows (the last xK post ranges of left_off)
@@ -3449,6 +3450,48 @@ struct DirLane {
   double md[CPL], mo[CPL];
   int flip, e, sg0, seglen, s;
 };
+
+// A DirLane parked in LDS, field-major (conflict-free): 4 CPL + 1 doubles then 5 ints per
+// thread (the top part's solver keeps its phase-1 lanes there through the top part)
+__host__ __device__ constexpr int dir_park_dbl(int cpl) {
+  return (4 * cpl + 1) * kPcThreads + (5 * kPcThreads + 1) / 2;
+}
+template <int W, int CPL>
+__device__ __forceinline__ void dir_lane_park(const DirLane<W, CPL>& L, double* pk) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int f = 0; f < CPL; ++f) {
+    pk[f * kPcThreads + t] = L.bc[f];
+    pk[(CPL + f) * kPcThreads + t] = L.bq[f];
+    pk[(2 * CPL + f) * kPcThreads + t] = L.md[f];
+    pk[(3 * CPL + f) * kPcThreads + t] = L.mo[f];
+  }
+  pk[4 * CPL * kPcThreads + t] = L.bN;
+  int* pi = reinterpret_cast<int*>(pk + (4 * CPL + 1) * kPcThreads);
+  pi[t] = L.flip;
+  pi[kPcThreads + t] = L.e;
+  pi[2 * kPcThreads + t] = L.sg0;
+  pi[3 * kPcThreads + t] = L.seglen;
+  pi[4 * kPcThreads + t] = L.s;
+}
+template <int W, int CPL>
+__device__ __forceinline__ void dir_lane_unpark(DirLane<W, CPL>& L, const double* pk) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int f = 0; f < CPL; ++f) {
+    L.bc[f] = pk[f * kPcThreads + t];
+    L.bq[f] = pk[(CPL + f) * kPcThreads + t];
+    L.md[f] = pk[(2 * CPL + f) * kPcThreads + t];
+    L.mo[f] = pk[(3 * CPL + f) * kPcThreads + t];
+  }
+  L.bN = pk[4 * CPL * kPcThreads + t];
+  const int* pi = reinterpret_cast<const int*>(pk + (4 * CPL + 1) * kPcThreads);
+  L.flip = pi[t];
+  L.e = pi[kPcThreads + t];
+  L.sg0 = pi[2 * kPcThreads + t];
+  L.seglen = pi[3 * kPcThreads + t];
+  L.s = pi[4 * kPcThreads + t];
+}
 
 // The chain lane state (ChainLane::setup without the loads) from a DirLane: the lumped flux
 // mass of chain flux k (between chain cells k - 1 and k) in k_assemble's order of additions
@@ -5024,6 +5067,8 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       T.sOff = u; u += ct + 1;
       T.sChild = u; u += cdc;
       T.sLv = u;
+      const bool park = !XR && keep && da.lds_park >= 0;
+      if (park) dir_lane_park<W, CPL>(L, smem + da.lds_park);
       TopPre pre;
       top_pre_idx(pa, pre);
       CoarseIdx ci;
@@ -5068,6 +5113,8 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       if (!keep) {
         dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
+      } else if (park) {  // its phase-1 lanes back from LDS (the barrier above ordered them)
+        dir_lane_unpark<W, CPL>(L, smem + da.lds_park);
       } else if (!(XR && kXrMidAsm)) {  // its lanes again: not kept through the solve
         chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
         dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
@@ -6289,6 +6336,7 @@ struct nx_network {
   double* d_crec = nullptr;
   int* d_ci = nullptr;
   int dstep_main = 0, dstep_top = 0;
+  int dstep_park = -1;  // k_dir_step's lane park in LDS (one rank, when it fits), or -1
   // several ranks (k_dir_xr / k_dir_xg, round 4): the fused step's tables hold (xr_ok); the
   // publisher's own left rows (xr_nleft: the left rows that are not cut); this
   // rank's mailbox (fine-grained; one block: mb1 | mb2 | flags), the peers' (device table,
@@ -8395,13 +8443,18 @@ bool xr_on(const Team& t, bool with_asm) {
   return t.hs[0]->sched_checked && t.hs[0]->xr_all && xr_local(t.hs[0]);
 }
 
+bool dir_park_env() {  // NXHIP_DIR_PARK=1: the top part's solver parks its lanes in LDS
+  const char* e = std::getenv("NXHIP_DIR_PARK");
+  return e != nullptr && std::atoi(e) != 0;
+}
 DirStep dir_args(nx_network* h, double rtol) {
   return DirStep{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
                  h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
                  h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
                  h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1,
                  h->d_seq, h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci,
-                 h->dstep_main, h->dstep_top, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u};
+                 h->dstep_main, h->dstep_top, h->nranks > 1 || !dir_park_env() ? -1 : h->dstep_park,
+                 nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u};
 }
 
 template <int W, int CPL>
@@ -9967,6 +10020,18 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     const int xr_dbl = h->nranks > 1 ? 2 * (nt + 1) + 4 : 0;
     h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl + xr_dbl});
     h->dstep_top = nt + (nt & 1);
+    // one rank: the top part's solver parks its phase-1 lanes (dir_lane_park) after the top
+    // part's arrays instead of re-assembling them after it, when the LDS has room
+    h->dstep_park = -1;
+    if (h->nranks <= 1) {
+      const int cpl = N <= 16 ? 2 : N <= 24 ? 3 : 4;
+      const int park = dir_park_dbl(cpl);
+      const int main2 = std::max(h->dstep_main, top_dbl + xr_dbl + park);
+      if (8 * (size_t)(kStashDbl + main2 + h->dstep_top) <= (size_t)kDirLdsMax && N <= 32) {
+        h->dstep_park = top_dbl + xr_dbl;
+        h->dstep_main = main2;
+      }
+    }
     h->dstep_lds = 8 * (size_t)(kStashDbl + h->dstep_main + h->dstep_top);
     const bool fits = mlv <= kStLv && mns <= kStNs && mnd <= kStNd && kPcThreads / W <= kStNc;
     h->d_job_hdr = const_cast<int*>(up(hdr.data(), (int64_t)hdr.size()));
