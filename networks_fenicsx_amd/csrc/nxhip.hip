@@ -3420,6 +3420,7 @@ struct DirStep {
   const int* ci;
   int lds_main, lds_top;
   int lds_park;  // the top part's solver parks its lanes here (doubles from smem), or -1
+  int hdefer;    // helpers store their own assembly after their phase 2 (NXHIP_DIR_HDEFER)
   // several ranks (k_dir_xr / k_dir_xg): the ranks' mailboxes (xpeers[q]: where this rank
   // writes for rank q), this rank's own (xself: where it reads), the exchange's shape, the
   // launch tag (monotonic, never reset), the cut rows (the last xK post ranges of left_off)
@@ -5028,6 +5029,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   NX_DSTAMP(35);
   bool late_store = false;  // the top solver stores its own assembly after phase 2 (no helpers)
   bool defer_free = false;  // a waiting workgroup's free waves store theirs after phase 2
+  bool defer_all = false;   // (hdefer) a helper stores all of its own after phase 2
   const bool lane_on = c0 + (int)threadIdx.x / W < c1;
   if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
     vm_drain();
@@ -5123,6 +5125,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       // the first nh workgroups to arrive store the top solver's assembly first (they have
       // the most slack; their polls come before any store of theirs, so they see the
       // announcement at once), then their own
+      bool helper = false;
       if (keep && nh > 0 && sIdx < nh) {
         if (threadIdx.x == 0) {
           int who = -1;
@@ -5139,6 +5142,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         }
         __syncthreads();
         const int tj = sTopJob, hh = sIdx;
+        helper = tj >= 0 && da.hdefer;
         if (tj >= 0) {  // helper hh: its share of the top solver's chains (+ helper 0 its rows)
           // one chain per wave (64 lanes: a chain's segment in a few whole-line store rounds)
           constexpr int CH = (W * CPL + 63) / 64;
@@ -5151,8 +5155,9 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         }
       }
       // own stores (unit stride: hidden in the wait), but not the free waves' (keep)
-      dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
+      if (!helper) dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
       defer_free = keep;
+      defer_all = helper;
       if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
@@ -5207,6 +5212,10 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   // (the kernel's end, not the published state, waits for these; re-assembled: L kept
   // through phase 2 would overflow the register budget there)
   if (late_store) {  // one job: the top solver's own
+    chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+    dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
+    dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
+  } else if (defer_all) {  // (hdefer) a helper's own assembly
     chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
     dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
     dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
@@ -8443,6 +8452,10 @@ bool xr_on(const Team& t, bool with_asm) {
   return t.hs[0]->sched_checked && t.hs[0]->xr_all && xr_local(t.hs[0]);
 }
 
+bool dir_hdefer_env() {  // NXHIP_DIR_HDEFER=1: helpers defer their own stores past phase 2
+  const char* e = std::getenv("NXHIP_DIR_HDEFER");
+  return e != nullptr && std::atoi(e) != 0;
+}
 bool dir_park_env() {  // NXHIP_DIR_PARK=1: the top part's solver parks its lanes in LDS
   const char* e = std::getenv("NXHIP_DIR_PARK");
   return e != nullptr && std::atoi(e) != 0;
@@ -8454,7 +8467,7 @@ DirStep dir_args(nx_network* h, double rtol) {
                  h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1,
                  h->d_seq, h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci,
                  h->dstep_main, h->dstep_top, h->nranks > 1 || !dir_park_env() ? -1 : h->dstep_park,
-                 nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u};
+                 dir_hdefer_env() ? 1 : 0, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u};
 }
 
 template <int W, int CPL>
