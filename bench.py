@@ -126,8 +126,10 @@ def dstep_bytes(n: int, nnz: int, E: int, N: int, B: int, nnz_lm: int) -> int:
     section 3c): the edge inputs (80 B per edge, as the assembly kernel), the chain statics
     (edge, flip, up, lo in phase 1; up, lo and two post slots in phase 2: 32 B per chain), the
     junction slots' statics (~88 B each), the multiplier rows' values read; written: the CSR
-    values, rhs, lumped mass and x (the residual is formed in registers, not stored)."""
-    return 8 * nnz + 16 * n + 8 * E * (N + 1) + 80 * E + 32 * E + 88 * B + 8 * nnz_lm
+    values, rhs and x (the residual is formed in registers, not stored; since round 5 the
+    lumped mass is not written either -- only a later MINRES or refinement pass reads it, and
+    ensure_dq forms it then)."""
+    return 8 * nnz + 16 * n + 80 * E + 32 * E + 88 * B + 8 * nnz_lm
 
 
 def pmc_traffic(kernel_prefix: str):
@@ -160,7 +162,7 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(mesh, asm, dof: int, budget_s: float):
-    """The hot path on the host cores (rank 0, one GPU only), three legs:
+    """The hot path on the host cores (rank 0, one GPU only), in legs:
 
     * ``port-direct`` / ``port``: ``oracle/nx_cpu.c`` -- OpenMP assembly in the device layout
       + the direct tree solve (the GPU default's algorithm) / MINRES with the same exact tree
@@ -168,7 +170,9 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
     * ``superlu``: the oracle's numpy assembly of the reference forms + SuperLU ``spsolve``
       (1 thread; the stand-in for the reference's MUMPS direct solve).
 
-    The headline ``value`` is the all-cores direct port; each leg runs about ``budget_s / 3``."""
+    The direct port runs at the OpenMP default (``OMP_NUM_THREADS``) and at one thread per CPU
+    of the affinity mask (all host cores); the headline ``value`` is the faster of
+    the two. The legs share ``budget_s`` equally."""
     from networks_fenicsx_amd.assembly import edge_boundary_rhs, evaluate_nodal
     from oracle import nx_cpu
     from oracle import nx_oracle as O
@@ -179,19 +183,29 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
     port = nx_cpu.CpuStep(lp, asm.tree_preconditioner, bc)
     port.assemble()
     port.solve()  # first touch of every buffer outside the timing
-    threads = nx_cpu.threads()
-    for direct, leg, what in ((True, "port-direct", "the direct tree solve (as the GPU's default)"),
-                              (False, "port", "MINRES with the exact tree preconditioner")):
-        ms, runs, its = port.time_steps(budget_s / 3, direct=direct)
+    omp = nx_cpu.threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    runs_of = [(True, "port-direct", omp, "the direct tree solve (as the GPU's default)"),
+               (False, "port", omp, "MINRES with the exact tree preconditioner")]
+    if affinity and affinity != omp:  # every core this process may run on
+        runs_of.insert(1, (True, "port-direct-affinity", affinity,
+                           "the direct tree solve, one thread per CPU of the affinity mask"))
+    for direct, leg, threads, what in runs_of:
+        nx_cpu.set_threads(threads)
+        ms, runs, its = port.time_steps(budget_s / (len(runs_of) + 1), direct=direct)
         legs.append({"leg": leg, "ms_per_step": ms, "value": dof / (ms / 1e3), "cores": threads,
                      "iterations": its,
                      "sample": f"{runs} full steps of the same workload ({dof} DoF): OpenMP "
                                f"assembly + {what} (oracle/nx_cpu.c), {threads} threads"})
+    nx_cpu.set_threads(omp)
     del port
     src, dst = mesh.edges
     P = O.build_problem(mesh.node_coordinates, src, dst, mesh.N, mesh.edge_colors)
     runs, t_total = 0, 0.0
-    while runs < 1 or (t_total < budget_s / 3 and runs < 40):
+    while runs < 1 or (t_total < budget_s / (len(runs_of) + 1) and runs < 40):
         t0 = time.perf_counter()
         A, b = O.assemble_reference(P, lambda x: x[1])
         O.solve_reference(A, b)
@@ -202,19 +216,68 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
                  "sample": f"{runs} full run(s) of the same workload: numpy assembly of the "
                            "reference forms + scipy SuperLU spsolve (1 thread, the MUMPS "
                            "stand-in)"})
-    head = legs[0]
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
+    # the headline: the faster of the direct legs (the GPU default's algorithm) on the host
+    head = max((g for g in legs if g["leg"].startswith("port-direct")), key=lambda g: g["value"])
     return {"value": head["value"], "unit": "DoF/s", "cores": head["cores"], "kind": "port",
             "ms_per_step": head["ms_per_step"], "sample": head["sample"],
             "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
             "affinity_cpus": affinity, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-            "cores_note": ("the OpenMP legs use every thread OpenMP is given: OMP_NUM_THREADS, "
-                           "which the GPU box sets to its CPU share per GPU (16); "
-                           "os.cpu_count() is the whole shared host"),
+            "cores_note": (f"direct legs at the OpenMP default ({omp} threads, from "
+                           "OMP_NUM_THREADS) and at every CPU of the affinity mask "
+                           f"({affinity}); the headline is the faster; os.cpu_count() is the "
+                           "whole shared host"),
             "legs": legs}
+
+
+C4_LEVELS, C4_N = 18, 19  # configs[4]: the depth-17 tree, N = 19, 10,354,648 DoF
+
+
+def c4_leg(args, world: int, rank: int, comm, timed_steps, state, allsum):
+    """configs[4] (``make_tree(18,18,18)``, N = 19) on the same GPUs as the headline, timed
+    the same way (assemble + the direct solve, ``args.steps`` steps after ``args.warmup``;
+    at P > 1 the exchange step, one launch per rank), with its error against the analytic
+    answer. A fixed-size workload: over the driver's 1, 2, 4, 8-GPU runs it is the strong
+    scaling of SURVEY's C4 (``north_star``: >= 6x from 1 to 8 GPUs)."""
+    import numpy as np
+
+    from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh
+    from networks_fenicsx_amd import network_generation as ng
+    from oracle import nx_oracle as O
+
+    t0 = time.perf_counter()
+    G = ng.make_tree(C4_LEVELS, C4_LEVELS, C4_LEVELS) if rank == 0 else None
+    mesh = NetworkMesh(G, N=C4_N, color_strategy="smallest_last", comm=comm)
+    del G
+    asm = HydraulicNetworkAssembler(mesh)
+    asm.compute_forms(p_bc_ex=lambda x: x[1])
+    asm.set_direct(True)
+    setup = time.perf_counter() - t0
+    h = asm.handle
+    try:
+        el = timed_steps(h, args.steps, args.warmup, world > 1)
+        ms = 1e3 * el / args.steps
+        E, B = mesh.num_edges, len(mesh.bifurcation_values)
+        dof = E * (2 * C4_N + 1) + B
+        out = {"workload": f"make_tree({C4_LEVELS},{C4_LEVELS},{C4_LEVELS}) depth-{C4_LEVELS - 1} "
+                           f"binary tree, N={C4_N} (configs[4]), assemble + solve",
+               "dofs": dof, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": ms, "value": dof / (ms / 1e3), "unit": "DoF/s",
+               "solver": "direct" if h.solver()[1] == 1 else "minres",
+               "direct_path": h.direct_path(), "relres": state["relres"],
+               "iterations": state["it"], "setup_s": setup}
+        src, dst = mesh.edges
+        P = O.build_problem(mesh.node_coordinates, src, dst, mesh.N)
+        xa = O.resistor_network_solution(P, lambda x: x[1])[O.build_permutation(P)[0]]
+        lp = asm.local_problem
+        per = 2 * C4_N + 1
+        rows = np.concatenate([(lp.edges[:, None] * per + np.arange(per)[None, :]).ravel(),
+                               E * per + mesh.bifurcation_index[lp.lm_nodes]])
+        x = h.solution()
+        d2, r2 = allsum([float(np.sum((x - xa[rows]) ** 2)), float(np.sum(xa[rows] ** 2))])
+        out["relerr_vs_analytic"] = math.sqrt(d2 / r2)
+        return out
+    finally:
+        asm.close()
 
 
 def _free_port() -> int:
@@ -243,6 +306,8 @@ def parse_args(argv=None):
     ap.add_argument("--api-steps", type=int, default=10,
                     help="steps through the public Solver.assemble/solve surface (0: skip)")
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
+    ap.add_argument("--no-c4", dest="c4", action="store_false",
+                    help="skip the configs[4] leg (C4, make_tree(18), N = 19, on these GPUs)")
     ap.add_argument("--solver", choices=("direct", "minres"), default="direct",
                     help="the direct tree solve (reference default preonly + lu) or MINRES")
     ap.add_argument("--allow-fallback", action="store_true",
@@ -608,6 +673,12 @@ def run(args, world: int) -> int:
                       "t1_direct_ms_per_step": t1d, "t1_setup_s": setup1}
         barrier()
 
+    # --- SURVEY's C4 (configs[4]: make_tree(18), N = 19, 10,354,648 DoF) on the same GPUs:
+    # the fixed-size workload, so the driver's N = 1, 2, 4, 8 runs give its strong scaling
+    c4 = None
+    if args.c4 and (levels, N) != (C4_LEVELS, C4_N):
+        c4 = c4_leg(args, world, rank, comm, timed_steps, state, allsum)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mesh, asm, dof_total, args.cpu_budget)
@@ -644,6 +715,7 @@ def run(args, world: int) -> int:
             "api_ms_per_step": api_ms,
             "api_host_ms_per_step": api_host_ms,
             "strong_scaling": strong,
+            "c4": c4,
             "solver": solver_used,
             "roofline": roof,
             "other_solver": other,

@@ -412,6 +412,19 @@ int nx_debug_xr_rehearse(nx_network_t* h, double rtol, int32_t reps, double* ms)
  * through the mailboxes, the exchange width the handle's rank count), the ranks' assembly
  * pending. *relres = the published residual (every rank's equal). */
 int nx_debug_xr_separate(nx_group_t* g, double rtol, double* relres);
+/* A rank that gives up an exchange raises an abort word in every rank's mailbox, so the
+ * other ranks' exchanges fail at once; the ranks then agree, through one max-all-reduce of
+ * four doubles, on who finished which step, so every rank leaves the exchange step at the
+ * same point and no collective of the graph path is ever paired across steps (the rank that
+ * gave up exchange 2 of a step the others finished keeps its final x and takes their
+ * published residual). Test hook: the poll bound of this rank's exchange `which` (0: the
+ * coarse partials, 1: the residual) in its next steps; 0 makes it give up at once, after
+ * its own slots and flags are written. Replaces nothing in the reference. */
+int nx_debug_xr_polls(nx_network_t* h, int32_t which, uint32_t polls);
+/* out[4] = [the exchange step is off for good (agreed), the last launch's give-up reasons
+ * (bits: 1 exchange 1, 2 exchange 2, 4 another rank's abort seen, 8 a slot with another
+ * launch's tag, 16 a local wait), agreements this rank took part in, the last launch's tag]. */
+int nx_get_xr_status(nx_network_t* h, int32_t* out);
 int nx_reset_profile(nx_network_t* h);
 int nx_bench_spmv(nx_network_t* h, int32_t reps, double* ms_per_spmv);
 /* The same SpMV rotating over private copies of the CSR and vectors (> 512 MiB in total,
@@ -437,6 +450,15 @@ int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_peers,
 int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const unsigned char* id,
                  int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
                  const int32_t* send_idx, const int32_t* recv_off);
+/* Tests: nx_comm_init with a host transport in place of RCCL -- several ranks' processes on
+ * ONE GPU (RCCL refuses two ranks on one device), collectives through the POSIX shared
+ * memory `name` ("/..."; the same on every rank, chosen by rank 0 and broadcast), eager
+ * (every collective synchronises the stream; no graph capture). It runs the RCCL ranks' host
+ * logic unchanged: the exchange step over IPC-mapped mailboxes, its agreement, the graph
+ * path. Not a performance path. Replaces nothing in the reference. */
+int nx_comm_init_host(nx_network_t* h, int32_t nranks, int32_t rank, const char* name,
+                      int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
+                      const int32_t* send_idx, const int32_t* recv_off);
 
 /* Several ranks, direct solve: the multiplier rows of the K cut bifurcations (incident
  * edges on several ranks; one global order, the same on every rank) are completed inside

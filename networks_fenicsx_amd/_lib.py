@@ -79,6 +79,8 @@ _SIGS = {
                                         _pi32, _i32, _pi32, _i32, _pi32]),
     "nx_comm_unique_id": (C.c_int, [_pu8]),
     "nx_comm_init": (C.c_int, [_h, _i32, _i32, _pu8, _i32, _pi32, _pi32, _pi32, _pi32]),
+    "nx_comm_init_host": (C.c_int, [_h, _i32, _i32, C.c_char_p, _i32, _pi32, _pi32, _pi32,
+                                    _pi32]),
     "nx_set_coarse": (C.c_int, [_h, _i32, _pi32, _i32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                 _i32, _pi32]),
     "nx_comm_count": (C.c_int, [_h, _pi32]),
@@ -102,6 +104,8 @@ _SIGS = {
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
     "nx_group_solve": (C.c_int, [_h, _f64, _i32, _i32, _pi32, _pd, _pi32]),
     "nx_debug_xr_separate": (C.c_int, [_h, _f64, _pd]),
+    "nx_debug_xr_polls": (C.c_int, [_h, _i32, C.c_uint32]),
+    "nx_get_xr_status": (C.c_int, [_h, _pi32]),
     "nx_group_destroy": (C.c_int, [_h]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -580,18 +584,37 @@ class Handle:
         check(lib().nx_comm_count(self.ptr, C.byref(n)))
         return int(n.value)
 
-    def comm_init(self, nranks: int, rank: int, uid: bytes, peers, send_off, send_idx, recv_off):
+    def comm_init(self, nranks: int, rank: int, uid, peers, send_off, send_idx, recv_off):
+        """Join the ranks' communicator: RCCL (``uid``: the unique id bytes, ``nx_comm_init``)
+        or, with ``uid`` a ``str`` shared-memory name, the host transport of the tests
+        (``nx_comm_init_host``: several ranks' processes on one GPU)."""
         self._multi = True  # (a communicator, even of one rank: no cycle correction)
-        uid_arr = (C.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid)
         peers = np.ascontiguousarray(peers, dtype=np.int32)
         send_off = np.ascontiguousarray(send_off, dtype=np.int32)
         send_idx = np.ascontiguousarray(send_idx, dtype=np.int32)
         recv_off = np.ascontiguousarray(recv_off, dtype=np.int32)
-        check(lib().nx_comm_init(self.ptr, int(nranks), int(rank), uid_arr, int(peers.size),
-                                 _ptr(peers, C.c_int32), _ptr(send_off, C.c_int32),
-                                 _ptr(send_idx if send_idx.size else np.zeros(1, np.int32),
-                                      C.c_int32),
-                                 _ptr(recv_off, C.c_int32)))
+        plan = (int(peers.size), _ptr(peers, C.c_int32), _ptr(send_off, C.c_int32),
+                _ptr(send_idx if send_idx.size else np.zeros(1, np.int32), C.c_int32),
+                _ptr(recv_off, C.c_int32))
+        if isinstance(uid, str):
+            check(lib().nx_comm_init_host(self.ptr, int(nranks), int(rank), uid.encode(), *plan))
+            return
+        uid_arr = (C.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        check(lib().nx_comm_init(self.ptr, int(nranks), int(rank), uid_arr, *plan))
+
+    def xr_polls(self, which: int, polls: int) -> None:
+        """Test hook (``nx_debug_xr_polls``): the poll bound of this rank's exchange
+        ``which`` (0 coarse partials, 1 residual); 0 gives it up at once."""
+        check(lib().nx_debug_xr_polls(self.ptr, int(which), int(polls)))
+
+    def xr_status(self) -> dict:
+        """``nx_get_xr_status``: whether the exchange step is off for good, the last launch's
+        give-up reasons (bits 1 exchange 1, 2 exchange 2, 4 abort seen, 8 tag, 16 local),
+        the agreements taken part in, the last launch's tag."""
+        out = (C.c_int32 * 4)()
+        check(lib().nx_get_xr_status(self.ptr, out))
+        return {"off": bool(out[0]), "why": int(out[1]), "agreed": int(out[2]),
+                "tag": int(out[3]) & 0xFFFFFFFF}
 
 
 class Group:

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import logging
 import os
+import secrets
 import typing
 
 import numpy as np
@@ -376,7 +377,12 @@ class HydraulicNetworkAssembler:
             self._handle.set_halo(self._nranks, self._rank, lp.peers, lp.send_off, lp.send_idx,
                                   lp.recv_off)
         else:
-            uid = _lib.comm_unique_id() if self._rank == 0 else None
+            if os.environ.get("NXHIP_TRANSPORT", "rccl") == "host":
+                # tests: several ranks' processes on ONE GPU (RCCL refuses that) -- the same
+                # host logic with its collectives through shared memory (nx_comm_init_host)
+                uid = f"/nxhip_{os.getpid()}_{secrets.token_hex(6)}" if self._rank == 0 else None
+            else:
+                uid = _lib.comm_unique_id() if self._rank == 0 else None
             uid = comm.bcast(uid, root=0)
             self._handle.comm_init(self._nranks, self._rank, uid, lp.peers, lp.send_off,
                                    lp.send_idx, lp.recv_off)

@@ -19,7 +19,14 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cmath>
 #include <cstdint>
@@ -3370,8 +3377,11 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
 // ======================================================================================
 // One rank's mailbox of the device-side exchange between ranks (k_dir_xr / k_dir_xg): P
 // slots of each exchange's doubles (exchange 1: the coarse partials [D | J | G]; exchange
-// 2: [||r||^2, ||b||^2, the cut rows' shares]) and 2P arrival flags, one per sender. Each
-// rank writes its slot in every rank's mailbox (system-scope write-through stores: peer
+// 2: [||r||^2, ||b||^2, the cut rows' shares]), each slot ending in the launch tag of its
+// writer; 2P arrival flags, one per sender; then P abort words, one per sender (64-bit:
+// the reasons and the tag of the launch that gave up; an exchange fails at once on an abort
+// of its own launch).
+// Each rank writes its slot in every rank's mailbox (system-scope write-through stores: peer
 // memory over xGMI, IPC-mapped; the in-process group: the same device), raises its flag
 // there, polls its own P flags and sums the P slots in rank order.
 struct XPeer {
@@ -3379,6 +3389,13 @@ struct XPeer {
   double* mb2;
   unsigned* fl;
 };
+// why an exchange step gave up (DirStep::sync[5], read by the host after the launch)
+constexpr unsigned kXrFail1 = 1u;       // exchange 1 (the coarse partials) incomplete
+constexpr unsigned kXrFail2 = 2u;       // exchange 2 (the residual) incomplete: x is final
+constexpr unsigned kXrFailAbort = 4u;   // another rank's abort word was seen
+constexpr unsigned kXrFailTag = 8u;     // a slot carried another launch's tag
+constexpr unsigned kXrFailLocal = 16u;  // a workgroup of this rank gave up its local wait
+constexpr unsigned kXrTopFailed = 0xffffffffu;  // sync[2]: the top part's solver gave up
 
 struct DirStep {
   const double* edge_x;
@@ -3419,8 +3436,6 @@ struct DirStep {
   const double* crec;
   const int* ci;
   int lds_main, lds_top;
-  int lds_park;  // the top part's solver parks its lanes here (doubles from smem), or -1
-  int hdefer;    // helpers store their own assembly after their phase 2 (NXHIP_DIR_HDEFER)
   // several ranks (k_dir_xr / k_dir_xg): the ranks' mailboxes (xpeers[q]: where this rank
   // writes for rank q), this rank's own (xself: where it reads), the exchange's shape, the
   // launch tag (monotonic, never reset), the cut rows (the last xK post ranges of left_off)
@@ -3428,6 +3443,7 @@ struct DirStep {
   XPeer xself;
   int xP, xrank, xld1, xld2, xK;
   unsigned xtag;
+  unsigned xpoll[2];  // each exchange's poll bound (kDirWaitPolls; nx_debug_xr_polls: tests)
 };
 
 constexpr int kDirWaitPolls = 1 << 20;  // s_sleep-paced polls before a waiting workgroup gives up
@@ -3451,48 +3467,6 @@ struct DirLane {
   double md[CPL], mo[CPL];
   int flip, e, sg0, seglen, s;
 };
-
-// A DirLane parked in LDS, field-major (conflict-free): 4 CPL + 1 doubles then 5 ints per
-// thread (the top part's solver keeps its phase-1 lanes there through the top part)
-__host__ __device__ constexpr int dir_park_dbl(int cpl) {
-  return (4 * cpl + 1) * kPcThreads + (5 * kPcThreads + 1) / 2;
-}
-template <int W, int CPL>
-__device__ __forceinline__ void dir_lane_park(const DirLane<W, CPL>& L, double* pk) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int f = 0; f < CPL; ++f) {
-    pk[f * kPcThreads + t] = L.bc[f];
-    pk[(CPL + f) * kPcThreads + t] = L.bq[f];
-    pk[(2 * CPL + f) * kPcThreads + t] = L.md[f];
-    pk[(3 * CPL + f) * kPcThreads + t] = L.mo[f];
-  }
-  pk[4 * CPL * kPcThreads + t] = L.bN;
-  int* pi = reinterpret_cast<int*>(pk + (4 * CPL + 1) * kPcThreads);
-  pi[t] = L.flip;
-  pi[kPcThreads + t] = L.e;
-  pi[2 * kPcThreads + t] = L.sg0;
-  pi[3 * kPcThreads + t] = L.seglen;
-  pi[4 * kPcThreads + t] = L.s;
-}
-template <int W, int CPL>
-__device__ __forceinline__ void dir_lane_unpark(DirLane<W, CPL>& L, const double* pk) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int f = 0; f < CPL; ++f) {
-    L.bc[f] = pk[f * kPcThreads + t];
-    L.bq[f] = pk[(CPL + f) * kPcThreads + t];
-    L.md[f] = pk[(2 * CPL + f) * kPcThreads + t];
-    L.mo[f] = pk[(3 * CPL + f) * kPcThreads + t];
-  }
-  L.bN = pk[4 * CPL * kPcThreads + t];
-  const int* pi = reinterpret_cast<const int*>(pk + (4 * CPL + 1) * kPcThreads);
-  L.flip = pi[t];
-  L.e = pi[kPcThreads + t];
-  L.sg0 = pi[2 * kPcThreads + t];
-  L.seglen = pi[3 * kPcThreads + t];
-  L.s = pi[4 * kPcThreads + t];
-}
 
 // The chain lane state (ChainLane::setup without the loads) from a DirLane: the lumped flux
 // mass of chain flux k (between chain cells k - 1 and k) in k_assemble's order of additions
@@ -3628,11 +3602,11 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
     const int k = l * CPL + t;
     da.rhs[ch.dof_c[t]] = L.bc[t];
     da.rhs[ch.dof_q[t]] = L.bq[t];
-    da.dq[qb + (flip ? N - k : k)] = ch.rho[t];
+    if (da.dq) da.dq[qb + (flip ? N - k : k)] = ch.rho[t];
   }
   if (ch.has_last) {
     da.rhs[ch.dof_qN] = L.bN;
-    da.dq[qb + (flip ? 0 : N)] = ch.rhoN;
+    if (da.dq) da.dq[qb + (flip ? 0 : N)] = ch.rhoN;
   }
   // the CSR segment, each lane its own cells' rows (edge order: cell g owns p_g's 2 entries
   // and q_{g+1}'s 5 -- q_N's 3 + s_dst for g = N - 1 -- from q0len + 7 g on; cell 0 also the
@@ -4685,12 +4659,6 @@ __device__ __forceinline__ void dir_stores_v2(const PcArgs& pa, const DirStep& d
 // after phase 2: those waves poll for the top values and load them without waiting for the
 // drain of the others' stores. The top solver's assembly is stored by the first workgroups to
 // arrive (helpers), one chain per wave on the other waves: kDirHelpChains chains each.
-// k_dir_xr: the top part's solver re-assembles its lanes inside the first exchange's wait
-// (-DNX_XR_MID_ASM=1; measured A/B) instead of after the top part
-#ifndef NX_XR_MID_ASM
-#define NX_XR_MID_ASM 0
-#endif
-constexpr bool kXrMidAsm = NX_XR_MID_ASM != 0;
 constexpr int kDirFreeWaves = 4;
 constexpr int kDirHelpChains = kPcThreads / 64 - kDirFreeWaves;
 // dynamic LDS of k_dir_step: at most this (the static __shared__ words -- flags, the partial
@@ -4735,53 +4703,93 @@ __device__ __forceinline__ double ld_sys(const double* p) {
                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 
+// rank q's abort word in this rank's mailbox: (reasons << 32) | the tag of the launch that
+// gave up; 0 while q never gave up
+__device__ __forceinline__ unsigned long long xr_abort_of(const DirStep& da, int q) {
+  return __hip_atomic_load(reinterpret_cast<unsigned long long*>(da.xself.fl + 2 * da.xP) + q,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One lane of a rank that gives up an exchange step: the reasons for the host (sync[5]) and
+// (reasons, this launch's tag) in its abort word in every other rank's mailbox, so their
+// exchanges waiting on it fail at once instead of waiting out their bound, and their hosts
+// know how far it got (xr_host_finish).
+__device__ __forceinline__ void xr_give_up(const DirStep& da, unsigned why) {
+  __hip_atomic_fetch_or(da.sync + 5, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long w = ((unsigned long long)why << 32) | da.xtag;
+  for (int q = 0; q < da.xP; ++q)
+    if (q != da.xrank)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(da.xpeers[q].fl + 2 * da.xP) + da.xrank,
+                         w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Exchange round `which` (0: coarse partials, 1: residual partials) of one workgroup: this
-// rank's n doubles (src, LDS) into its slot of every rank's mailbox, then -- after every
-// storing wave's vmcnt(0) and a barrier -- its flag at every rank (tagged with the launch);
-// then this rank's P flags polled (bounded) and the P slots summed in rank order (the same
-// additions as k_group_sum: every rank gets the same bits) into dst (LDS). False: a rank's
-// flag never came.
-struct XrNoMid {
-  __device__ __forceinline__ void operator()() const {}
-};
-template <class Mid = XrNoMid>
+// rank's n doubles (src, LDS) and its launch tag (the slot's last double) into its slot of
+// every rank's mailbox, then -- after every storing wave's vmcnt(0) and a barrier -- its
+// flag at every rank (tagged with the launch); then this rank's P flags polled (bounded,
+// and failing at once on a raised abort word) and the P slots summed in rank order (the
+// same additions as k_group_sum: every rank gets the same bits) into dst (LDS), each slot's
+// tag checked beside the sums. False: a rank's flag never came, another rank gave up, or a
+// slot held another launch's data; this rank's abort is then raised everywhere.
+//
+// Ordering (the advisor's r04 finding): the slots and the flag are system-scope atomic
+// stores (write-through to the coherence point) and vmcnt(0) retires the slots' stores
+// before any flag store issues -- what a system-scope release does for atomic data (its
+// L2 write-back covers plain stores only, and there are none here). The reader's slot loads
+// are system-scope atomic loads (they bypass the non-coherent caches), issued after the
+// flag load returned (a barrier orders the polling lanes before every loading lane) -- the
+// acquire's ordering for atomic loads (its cache invalidation covers plain loads only). The
+// slot tags check it: a reordered slot cannot carry this launch's tag.
 __device__ __forceinline__ bool xr_allsum(const DirStep& da, int which, const double* src, int n,
-                                          double* dst, const Mid& mid = Mid{}) {
-  __shared__ int sOk;
+                                          double* dst) {
+  __shared__ unsigned sWhy;
   const int P = da.xP, r = da.xrank, ld = which ? da.xld2 : da.xld1;
+  const double tagd = __builtin_bit_cast(double, (unsigned long long)da.xtag);
   for (int q = 0; q < P; ++q) {
     double* mb = (which ? da.xpeers[q].mb2 : da.xpeers[q].mb1) + (int64_t)r * ld;
     for (int i = threadIdx.x; i < n; i += kPcThreads) st_sys(mb + i, src[i]);
+    if (threadIdx.x == kPcThreads - 1) st_sys(mb + ld - 1, tagd);
   }
   vm_drain();
-  if (threadIdx.x == 0) sOk = 1;
+  if (threadIdx.x == 0) sWhy = 0u;
   __syncthreads();
   if ((int)threadIdx.x < P)
     __hip_atomic_store(da.xpeers[threadIdx.x].fl + which * P + r, da.xtag, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-  mid();  // (work of this workgroup's own while the other ranks' partials travel)
   if ((int)threadIdx.x < P) {
-    bool ok = false;
-    for (unsigned k = 0; k < da.polls; ++k) {
+    unsigned why = which ? kXrFail2 : kXrFail1;
+    const unsigned polls = da.xpoll[which];
+    for (unsigned k = 0; k < polls; ++k) {
       if (__hip_atomic_load(da.xself.fl + which * P + threadIdx.x, __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_SYSTEM) == da.xtag) {
-        ok = true;
+        why = 0u;
+        break;
+      }
+      if ((unsigned)xr_abort_of(da, threadIdx.x) == da.xtag) {  // rank q gave up this launch
+        why |= kXrFailAbort;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (!ok) sOk = 0;
+    if (why) atomicOr(&sWhy, why);
   }
   __syncthreads();
-  if (!sOk) return false;
-  const double* mine = which ? da.xself.mb2 : da.xself.mb1;
-  for (int i = threadIdx.x; i < n; i += kPcThreads) {
-    double v = 0.0;
-    for (int q = 0; q < P; ++q) v += ld_sys(mine + (int64_t)q * ld + i);
-    dst[i] = v;
+  if (sWhy == 0u) {
+    const double* mine = which ? da.xself.mb2 : da.xself.mb1;
+    for (int i = threadIdx.x; i < n; i += kPcThreads) {
+      double v = 0.0;
+      for (int q = 0; q < P; ++q) v += ld_sys(mine + (int64_t)q * ld + i);
+      dst[i] = v;
+    }
+    if ((int)threadIdx.x < P &&
+        __builtin_bit_cast(unsigned long long, ld_sys(mine + (int64_t)threadIdx.x * ld + ld - 1)) !=
+            (unsigned long long)da.xtag)
+      atomicOr(&sWhy, (which ? kXrFail2 : kXrFail1) | kXrFailTag);
+    __syncthreads();
   }
-  __syncthreads();
-  return true;
+  const unsigned why = sWhy;
+  if (why != 0u && threadIdx.x == 0) xr_give_up(da, why);
+  return why == 0u;
 }
 
 // The coarse step's static set-up of this thread's top slot (coarse_top_pre's indices),
@@ -4867,16 +4875,14 @@ __device__ __forceinline__ void xr_top_back(const PcArgs& pa, const CoarsePre& c
   __syncthreads();
 }
 
-template <class Mid = XrNoMid>
 __device__ __forceinline__ bool xr_coarse(const PcArgs& pa, const DirStep& da, const TopLds& T,
-                                          const CoarseIdx& ci, const TopPre& pre, double* ext,
-                                          const Mid& mid = Mid{}) {
+                                          const CoarseIdx& ci, const TopPre& pre, double* ext) {
   __shared__ double xb[2 * 3 * kCapCoarseLds];
   const int nC = pa.n_coarse, n1 = 3 * nC;
   for (int i = threadIdx.x; i < n1; i += kPcThreads) xb[i] = ld_wt(pa.cbuf + i);
   __syncthreads();
   NX_DSTAMP(42);
-  if (!xr_allsum(da, 0, xb, n1, xb + n1, mid)) return false;
+  if (!xr_allsum(da, 0, xb, n1, xb + n1)) return false;
   NX_DSTAMP(43);
   if (!pa.c_wave) {  // (pc_coarse_lds reads the sums from cbuf)
     for (int i = threadIdx.x; i < n1; i += kPcThreads) pa.cbuf[i] = xb[n1 + i];
@@ -4968,6 +4974,18 @@ __device__ __forceinline__ bool dir_publish_xr(const PcArgs& pa, const DirStep& 
   NX_DSTAMP(44);
   if (!xr_allsum(da, 1, xs, 2 + K, ys)) return false;
   NX_DSTAMP(45);
+  {  // a rank that gave up this launch after its flag reached this one: publishing nothing
+     // keeps the ranks together (x is final; the host finishes exchange 2, xr_host_finish)
+    __shared__ int sAb;
+    if (threadIdx.x == 0) sAb = 0;
+    __syncthreads();
+    if ((int)threadIdx.x < da.xP && (unsigned)xr_abort_of(da, threadIdx.x) == da.xtag) sAb = 1;
+    __syncthreads();
+    if (sAb) {
+      if (threadIdx.x == 0) xr_give_up(da, kXrFail2 | kXrFailAbort);
+      return false;
+    }
+  }
   if (threadIdx.x == 0) {
     rr = ys[0];
     for (int k = 0; k < K; ++k) {
@@ -5029,7 +5047,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   NX_DSTAMP(35);
   bool late_store = false;  // the top solver stores its own assembly after phase 2 (no helpers)
   bool defer_free = false;  // a waiting workgroup's free waves store theirs after phase 2
-  bool defer_all = false;   // (hdefer) a helper stores all of its own after phase 2
   const bool lane_on = c0 + (int)threadIdx.x / W < c1;
   if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
     vm_drain();
@@ -5069,8 +5086,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       T.sOff = u; u += ct + 1;
       T.sChild = u; u += cdc;
       T.sLv = u;
-      const bool park = !XR && keep && da.lds_park >= 0;
-      if (park) dir_lane_park<W, CPL>(L, smem + da.lds_park);
       TopPre pre;
       top_pre_idx(pa, pre);
       CoarseIdx ci;
@@ -5090,16 +5105,11 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         NX_DSTAMP(41);
         // (xr_top_back's per-slot scratch after the top part's arrays; sLv is the last)
         double* ext = reinterpret_cast<double*>(T.sLv + ((pa.n_top_lvl + 2) & ~1));
-        // (keep: its lanes re-assembled while the other ranks' partials travel)
-        auto mid = [&]() {
-          if (keep && kXrMidAsm) {
-            chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
-            dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
-          }
-        };
-        if (!xr_coarse(pa, da, T, ci, pre, ext, mid)) {
-          if (threadIdx.x == 0)  // (the waiters give up too; the host reports the exchange)
+        if (!xr_coarse(pa, da, T, ci, pre, ext)) {
+          if (threadIdx.x == 0) {  // the waiters leave at once (no top values will come)
             __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(da.sync + 2, kXrTopFailed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
           return;
         }
       } else {
@@ -5115,9 +5125,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       if (!keep) {
         dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
-      } else if (park) {  // its phase-1 lanes back from LDS (the barrier above ordered them)
-        dir_lane_unpark<W, CPL>(L, smem + da.lds_park);
-      } else if (!(XR && kXrMidAsm)) {  // its lanes again: not kept through the solve
+      } else {  // its lanes again: not kept through the solve
         chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
         dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
       }
@@ -5125,7 +5133,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       // the first nh workgroups to arrive store the top solver's assembly first (they have
       // the most slack; their polls come before any store of theirs, so they see the
       // announcement at once), then their own
-      bool helper = false;
       if (keep && nh > 0 && sIdx < nh) {
         if (threadIdx.x == 0) {
           int who = -1;
@@ -5142,7 +5149,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         }
         __syncthreads();
         const int tj = sTopJob, hh = sIdx;
-        helper = tj >= 0 && da.hdefer;
         if (tj >= 0) {  // helper hh: its share of the top solver's chains (+ helper 0 its rows)
           // one chain per wave (64 lanes: a chain's segment in a few whole-line store rounds)
           constexpr int CH = (W * CPL + 63) / 64;
@@ -5155,23 +5161,29 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         }
       }
       // own stores (unit stride: hidden in the wait), but not the free waves' (keep)
-      if (!helper) dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
+      dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
       defer_free = keep;
-      defer_all = helper;
       if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
         int ok = 0;
         for (unsigned k = 0; k < da.polls; ++k) {
-          if (__hip_atomic_load(da.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              da.epoch + 1u) {
+          const unsigned v = __hip_atomic_load(da.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v == da.epoch + 1u) {
             ok = 1;
+            break;
+          }
+          if (XR && v == kXrTopFailed) {  // the solver gave up its exchange
+            ok = -1;
             break;
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        if (!ok) __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sFlag = ok ? 1 : -1;
+        if (ok == 0) {
+          __hip_atomic_fetch_add(da.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if constexpr (XR) xr_give_up(da, kXrFail1 | kXrFailLocal);
+        }
+        sFlag = ok > 0 ? 1 : -1;
       }
     }
     __syncthreads();
@@ -5212,10 +5224,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   // (the kernel's end, not the published state, waits for these; re-assembled: L kept
   // through phase 2 would overflow the register budget there)
   if (late_store) {  // one job: the top solver's own
-    chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
-    dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
-    dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
-  } else if (defer_all) {  // (hdefer) a helper's own assembly
     chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
     dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
     dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
@@ -6218,6 +6226,19 @@ struct LeanGraphs {
   double direct_asm_rtol = 0.0;
 };
 
+// the host transport (tests; its collectives are with the Team's): a shared-memory segment
+// of a header (a barrier's counters) and one slot per rank
+struct HcHdr {
+  std::atomic<uint32_t> count;
+  std::atomic<uint32_t> gen;
+};
+struct HostComm {
+  int P = 0, rank = 0;
+  size_t slot = 0, bytes = 0;
+  unsigned char* base = nullptr;
+  std::string name;
+};
+
 struct nx_network {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -6332,6 +6353,7 @@ struct nx_network {
   // rows no job forms, every left row's post range, the posts, the hand-off counters and
   // the launches since they were zero (all in pc_bufs; reset with every upload)
   bool dstep_ok = false;   // the decomposition allows it (nx_set_preconditioner)
+  bool dq_stale = false;   // the last assembly was a one-launch step's: dq not formed (ensure_dq)
   bool dstep_off = false;  // a launch gave up waiting (workgroups not co-resident)
   int* d_chain_post = nullptr;
   int* d_left_off = nullptr;
@@ -6345,7 +6367,6 @@ struct nx_network {
   double* d_crec = nullptr;
   int* d_ci = nullptr;
   int dstep_main = 0, dstep_top = 0;
-  int dstep_park = -1;  // k_dir_step's lane park in LDS (one rank, when it fits), or -1
   // several ranks (k_dir_xr / k_dir_xg, round 4): the fused step's tables hold (xr_ok); the
   // publisher's own left rows (xr_nleft: the left rows that are not cut); this
   // rank's mailbox (fine-grained; one block: mb1 | mb2 | flags), the peers' (device table,
@@ -6356,9 +6377,16 @@ struct nx_network {
   XPeer* d_xpeers = nullptr;
   std::vector<void*> xr_opened;  // peers' mailboxes opened by IPC (closed on destroy)
   bool xr_linked = false;        // the peer table is set (group create / nx_xch_import)
-  bool xr_off = false;           // an exchange timed out: the graph path from then on
+  bool xr_off = false;           // the ranks agreed to leave it (xr_agree): the graph path
   bool xr_all = false;           // RCCL: every rank can run the exchange step (check_schedules)
   unsigned xtag = 0;
+  unsigned xpoll[2] = {kDirWaitPolls, kDirWaitPolls};  // per exchange (nx_debug_xr_polls)
+  unsigned xr_why = 0;        // the last exchange step's give-up reasons (kXrFail*), 0: none
+  int xr_agreed = 0;          // agreements this handle took part in (nx_get_xr_status)
+  double* d_agree = nullptr;  // RCCL: the agreement's all-reduce buffer
+  // the host transport (tests: several ranks' processes on ONE GPU, nx_comm_init_host) --
+  // the RCCL rank's host logic with its collectives through shared memory, eager only
+  HostComm* hcomm = nullptr;
   std::vector<int> gk_off_host, gk_row_host;
   size_t dstep_lds = 0;  // dynamic LDS bytes per workgroup
   unsigned* d_tsync = nullptr;  // k_dir_team_up's arrival counter (several ranks; pc_bufs)
@@ -6473,7 +6501,135 @@ struct Team {
   nx_group* g;
 };
 
-bool team_multi(const Team& t) { return t.g != nullptr || t.hs[0]->comm != nullptr; }
+// One rank of a job with one process per rank: an RCCL communicator, or the host transport.
+bool proc_rank(const nx_network* h) { return h->comm != nullptr || h->hcomm != nullptr; }
+bool team_multi(const Team& t) { return t.g != nullptr || proc_rank(t.hs[0]); }
+
+// ---- the host transport (tests only) ----------------------------------------------------
+// RCCL refuses two ranks on one device, so the RCCL ranks' host logic -- the exchange step's
+// IPC mailboxes between processes, the agreement after a give-up (xr_agree), the graph
+// path's collectives -- is tested on one GPU with the collectives through POSIX shared
+// memory: a slot per rank, a sense-reversing barrier, sums in rank order (every rank gets
+// the same bits, as k_group_sum). Every collective synchronises the handle's stream and
+// copies through the host, so nothing is captured into graphs. Not a performance path.
+constexpr size_t kHcHdr = 256;
+constexpr size_t kHcSlot = 8u << 20;  // bytes per rank: the largest halo / all-reduce
+constexpr double kHcTimeoutS = 300.0;
+
+unsigned char* hc_slot(const HostComm* c, int r) { return c->base + kHcHdr + c->slot * (size_t)r; }
+
+int hc_open(const std::string& name, int P, int rank, HostComm** out) {
+  static_assert(std::atomic<uint32_t>::is_always_lock_free, "process-shared atomics");
+  auto* c = new HostComm();
+  c->P = P;
+  c->rank = rank;
+  c->slot = kHcSlot;
+  c->bytes = kHcHdr + kHcSlot * (size_t)P;
+  c->name = name;
+  const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+  if (fd < 0) {
+    delete c;
+    return fail(NX_ERR_STATE, "host transport: shm_open(" + name + ") failed");
+  }
+  // (every rank sizes it the same; a fresh segment reads as zeros: the barrier's counters)
+  void* p = ftruncate(fd, (off_t)c->bytes) == 0
+                ? mmap(nullptr, c->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0)
+                : MAP_FAILED;
+  close(fd);
+  if (p == MAP_FAILED) {
+    delete c;
+    return fail(NX_ERR_STATE, "host transport: mapping " + name + " failed");
+  }
+  c->base = static_cast<unsigned char*>(p);
+  *out = c;
+  return NX_OK;
+}
+void hc_close(HostComm* c) {
+  if (!c) return;
+  if (c->base) munmap(c->base, c->bytes);
+  (void)shm_unlink(c->name.c_str());  // (the first rank to close removes the name)
+  delete c;
+}
+int hc_barrier(HostComm* c) {
+  auto* hd = reinterpret_cast<HcHdr*>(c->base);
+  const uint32_t g = hd->gen.load(std::memory_order_acquire);
+  if (hd->count.fetch_add(1u, std::memory_order_acq_rel) + 1u == (uint32_t)c->P) {
+    hd->count.store(0u, std::memory_order_relaxed);
+    hd->gen.store(g + 1u, std::memory_order_release);
+    return NX_OK;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t k = 1; hd->gen.load(std::memory_order_acquire) == g; ++k) {
+    if ((k & 255) == 0) {
+      sched_yield();
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kHcTimeoutS)
+        return fail(NX_ERR_STATE, "host transport: a rank never reached the barrier");
+    }
+  }
+  return NX_OK;
+}
+// all-reduce of n values of T (device memory d) in rank order: op 0 sum, 1 max
+template <class T>
+int hc_allreduce(nx_network* h, T* d, int64_t n, int op) {
+  HostComm* c = h->hcomm;
+  if (sizeof(T) * (size_t)n > c->slot) return fail(NX_ERR_STATE, "host transport: all-reduce too large");
+  HIPCALL(hipStreamSynchronize(h->stream));
+  HIPCALL(hipMemcpy(hc_slot(c, c->rank), d, sizeof(T) * n, hipMemcpyDeviceToHost));
+  CHECK(hc_barrier(c));
+  std::vector<T> acc(reinterpret_cast<const T*>(hc_slot(c, 0)),
+                     reinterpret_cast<const T*>(hc_slot(c, 0)) + n);
+  for (int q = 1; q < c->P; ++q) {
+    const T* s = reinterpret_cast<const T*>(hc_slot(c, q));
+    for (int64_t i = 0; i < n; ++i) acc[i] = op == 0 ? acc[i] + s[i] : std::max(acc[i], s[i]);
+  }
+  CHECK(hc_barrier(c));  // (every rank has read the slots before they are written again)
+  HIPCALL(hipMemcpy(d, acc.data(), sizeof(T) * n, hipMemcpyHostToDevice));
+  return NX_OK;
+}
+// The halo of v (the pack kernels filled send_buf on the stream) and, beta, every rank's
+// beta^2 partial (red[1]) into gath -- what team_halo's grouped send / recv moves. A slot
+// holds [beta, n_peers, (peer, offset, count) per peer, send_buf]; every rank copies its
+// segments out of its peers' slots.
+int hc_halo(nx_network* h, double* v, bool beta) {
+  HostComm* c = h->hcomm;
+  const int np = (int)h->peers.size(), nsend = h->send_off.back();
+  const size_t head = 2 + 3 * (size_t)np;
+  if (sizeof(double) * (head + (size_t)nsend) > c->slot)
+    return fail(NX_ERR_STATE, "host transport: halo too large");
+  HIPCALL(hipStreamSynchronize(h->stream));
+  double* s = reinterpret_cast<double*>(hc_slot(c, c->rank));
+  s[0] = 0.0;
+  if (beta) HIPCALL(hipMemcpy(s, h->red + 1, sizeof(double), hipMemcpyDeviceToHost));
+  s[1] = np;
+  for (int j = 0; j < np; ++j) {
+    s[2 + 3 * j] = h->peers[j];
+    s[3 + 3 * j] = h->send_off[j];
+    s[4 + 3 * j] = h->send_off[j + 1] - h->send_off[j];
+  }
+  if (nsend > 0) HIPCALL(hipMemcpy(s + head, h->send_buf, sizeof(double) * nsend, hipMemcpyDeviceToHost));
+  CHECK(hc_barrier(c));
+  for (int j = 0; j < np; ++j) {
+    const int cnt = h->recv_off[j + 1] - h->recv_off[j];
+    if (cnt == 0) continue;
+    const double* o = reinterpret_cast<const double*>(hc_slot(c, h->peers[j]));
+    const int nq = (int)o[1];
+    int e = 0;
+    while (e < nq && (int)o[2 + 3 * e] != c->rank) ++e;
+    if (e == nq || (int)o[4 + 3 * e] != cnt)
+      return fail(NX_ERR_STATE, "host transport: the halo plans disagree");
+    HIPCALL(hipMemcpy(v + h->n_own + h->recv_off[j], o + 2 + 3 * (size_t)nq + (size_t)o[3 + 3 * e],
+                      sizeof(double) * cnt, hipMemcpyHostToDevice));
+  }
+  if (beta) {
+    std::vector<double> g(c->P);
+    HIPCALL(hipMemcpy(g.data(), h->gath, sizeof(double) * c->P, hipMemcpyDeviceToHost));
+    for (int q = 0; q < c->P; ++q)
+      if (q != c->rank) g[q] = reinterpret_cast<const double*>(hc_slot(c, q))[0];
+    HIPCALL(hipMemcpy(h->gath, g.data(), sizeof(double) * c->P, hipMemcpyHostToDevice));
+  }
+  CHECK(hc_barrier(c));
+  return NX_OK;
+}
 
 enum VecSel { VS_Z, VS_R2, VS_X };
 double* vec_of(nx_network* h, VecSel s, int64_t k) {
@@ -6519,6 +6675,7 @@ int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false, bool pack
     return NX_OK;
   }
   nx_network* h = t.hs[0];
+  if (h->hcomm) return hc_halo(h, vec_of(h, sel, k), beta);
   if (h->peers.empty() && !beta) return NX_OK;
   double* v = vec_of(h, sel, k);
   NCCLCALL(ncclGroupStart());
@@ -6558,6 +6715,7 @@ int team_allreduce(const Team& t, int slot, int n) {
     return NX_OK;
   }
   nx_network* h = t.hs[0];
+  if (h->hcomm) return hc_allreduce(h, xbuf_of(h, slot), n, 0);
   NCCLCALL(ncclAllReduce(xbuf_of(h, slot), xbuf_of(h, slot), n, ncclDouble, ncclSum, h->comm,
                          h->stream));
   return NX_OK;
@@ -7689,6 +7847,9 @@ NX_API int nx_destroy(nx_network_t* h) {
     (void)drop_graph(graph_slot(Team{hs, 1, nullptr}));
   }
   if (h->comm) ncclCommDestroy(h->comm);
+  hc_close(h->hcomm);
+  h->hcomm = nullptr;
+  if (h->d_agree) (void)hipFree(h->d_agree);
   void* bufs[] = {h->edge_x, h->edge_lm, h->edge_seg, h->edge_R, h->edge_bc, h->edge_f, h->lm_val, h->dq,
                   h->z, h->vv, h->vs, h->hist,
                   h->rowptr, h->col,     h->val,      h->rhs,    h->vb[0],   h->vb[1],
@@ -7788,6 +7949,7 @@ namespace {
 int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s = nullptr) {
   if (!s) s = h->stream;
   if (dq < 0) dq = lhs;
+  if (dq) h->dq_stale = false;
   if (h->fe) {  // general degrees: one thread per nonzero / rhs row
     FeArgs a{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind, h->fe_tval,
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
@@ -7836,6 +7998,15 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
 // point flushes it first -- launches it; the direct solve captures it as the head of its
 // own graph instead (one launch per step less).
 bool defer_ok(const nx_network* h) { return !h->fe; }
+
+// The lumped flux mass before a reader of dq (a refinement pass, the separate sweeps, MINRES,
+// the graph path) when the last assembly was a one-launch step's, which does not form it:
+// the assembly kernel's dq-only launch (the same arithmetic and order: the same bits). Eager,
+// outside any captured graph.
+int ensure_dq(nx_network* h) {
+  if (!h->dq_stale) return NX_OK;
+  return launch_assembly(h, 0, 0, 1);
+}
 
 int flush_assembly(nx_network* h) {
   if (!h || !(h->pend_lhs || h->pend_rhs)) return NX_OK;
@@ -8092,7 +8263,7 @@ bool dstep_on(const nx_network* h) {
   const char* e = std::getenv("NXHIP_DIR_FUSED");  // read per solve: tests switch it
   const bool env = e == nullptr || std::atoi(e) != 0;
   return env && h->dstep_ok && !h->dstep_off && h->pc_lds && h->fres_ok && h->pa.exact &&
-         h->pc_jobs > 0 && h->pc_jobs <= h->n_cu && h->comm == nullptr && h->group == nullptr &&
+         h->pc_jobs > 0 && h->pc_jobs <= h->n_cu && !proc_rank(h) && h->group == nullptr &&
          h->nranks == 1;
 }
 
@@ -8187,6 +8358,7 @@ int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
 // Gauss-Jordan with partial pivoting). Once per assembled matrix.
 int cyc_build(nx_network* h) {
   const int m = 2 * h->n_cyc;
+  CHECK(ensure_dq(h));
   h->cyc_raw = true;
   h->need_r = false;
   for (int j = 0; j < m; ++j) {
@@ -8255,7 +8427,7 @@ int cyc_build(nx_network* h) {
 // (consistent mass) on a decomposition without grounded cycle chains; with several ranks
 // also the LDS sweeps (their mode kModeDirect) and the coarse step.
 bool direct_local(const nx_network* h) {
-  const bool multi = h->comm != nullptr || h->group != nullptr || h->nranks > 1;
+  const bool multi = proc_rank(h) || h->group != nullptr || h->nranks > 1;
   // a graph with cycles: one rank, with the Woodbury correction of its cycle chains
   const bool exact = h->tree_exact || (h->n_cyc > 0 && !multi);
   // the LDS sweeps run it (their mode 3); the global-memory fallback (LDS caps exceeded)
@@ -8270,7 +8442,7 @@ bool direct_local(const nx_network* h) {
 // The ranks decide together: a group compares its handles here, RCCL ranks agreed in
 // check_schedules (all-reduced with the schedule signature).
 bool direct_applicable(const Team& t) {
-  if (t.hs[0]->comm) return t.hs[0]->sched_checked && t.hs[0]->direct_all;
+  if (proc_rank(t.hs[0])) return t.hs[0]->sched_checked && t.hs[0]->direct_all;
   for (int r = 0; r < t.P; ++r)
     if (!direct_local(t.hs[r])) return false;
   return true;
@@ -8385,9 +8557,10 @@ int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false
 // fence writes back its XCD's L2, dirty with x, before the ticket.)
 
 // ---- several ranks: the fused step with the device-side exchange (k_dir_xr / k_dir_xg) --
-constexpr int kXld1 = 3 * kCapCoarseLds, kXld2 = 2 + kCapCoarseLds;
-size_t xmb_bytes(int P) {
-  return sizeof(double) * (size_t)P * (kXld1 + kXld2) + sizeof(unsigned) * 2 * (size_t)P;
+// slot strides: the exchange's doubles, then the writer's tag
+constexpr int kXld1 = 3 * kCapCoarseLds + 1, kXld2 = 2 + kCapCoarseLds + 1;
+size_t xmb_bytes(int P) {  // slots, 2P flags, P 64-bit abort words
+  return sizeof(double) * (size_t)P * (kXld1 + kXld2) + sizeof(unsigned) * 4 * (size_t)P;
 }
 XPeer xpeer_of(void* base, int P) {
   XPeer x;
@@ -8452,27 +8625,45 @@ bool xr_on(const Team& t, bool with_asm) {
   return t.hs[0]->sched_checked && t.hs[0]->xr_all && xr_local(t.hs[0]);
 }
 
-bool dir_hdefer_env() {  // NXHIP_DIR_HDEFER=1: helpers defer their own stores past phase 2
-  const char* e = std::getenv("NXHIP_DIR_HDEFER");
-  return e != nullptr && std::atoi(e) != 0;
-}
-bool dir_park_env() {  // NXHIP_DIR_PARK=1: the top part's solver parks its lanes in LDS
-  const char* e = std::getenv("NXHIP_DIR_PARK");
-  return e != nullptr && std::atoi(e) != 0;
-}
+// The one-launch steps (k_dir_step, k_dir_xr, k_dir_xg) do not write the lumped flux mass
+// dq: only the separate sweeps (a refinement pass, MINRES, the graph path) read it, and
+// ensure_dq forms it before them. (4.2 MB of the step's stores at C3.)
 DirStep dir_args(nx_network* h, double rtol) {
+  h->dq_stale = true;
   return DirStep{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
-                 h->val, h->rhs, h->dq, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
+                 h->val, h->rhs, nullptr, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
                  h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
                  h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1,
                  h->d_seq, h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci,
-                 h->dstep_main, h->dstep_top, h->nranks > 1 || !dir_park_env() ? -1 : h->dstep_park,
-                 dir_hdefer_env() ? 1 : 0, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u};
+                 h->dstep_main, h->dstep_top, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u,
+                 {kDirWaitPolls, kDirWaitPolls}};
+}
+// the exchange fields of rank h's launch among X ranks (its own mailbox, the peers' table)
+void xr_fill(nx_network* h, DirStep& da, int X) {
+  da.n_left = h->xr_nleft;
+  da.xpeers = h->d_xpeers;
+  da.xself = xpeer_of(h->xmb, X);
+  da.xP = X;
+  da.xrank = h->rank;
+  da.xld1 = kXld1;
+  da.xld2 = kXld2;
+  da.xK = h->n_cut;
+  da.xtag = h->xtag;
+  da.xpoll[0] = h->xpoll[0];
+  da.xpoll[1] = h->xpoll[1];
+}
+// the dynamic LDS above 64 KiB, opted in once per kernel (not per launch)
+void opt_in_lds(const void* fn, int bytes) {
+  static thread_local std::vector<const void*> opted;
+  if (std::find(opted.begin(), opted.end(), fn) != opted.end()) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  (void)hipGetLastError();
+  opted.push_back(fn);
 }
 
 template <int W, int CPL>
 int launch_xr_wc(const Team& t, double rtol) {
-  // P: the handles launched here (a group's ranks, or this process's one RCCL rank);
+  // P: the handles launched here (a group's ranks, or this process's one rank);
   // X: the ranks exchanging (every rank of the group or of the communicator)
   const int P = t.P, X = t.g ? t.P : t.hs[0]->nranks;
   std::vector<DirStep> das(P);
@@ -8483,15 +8674,7 @@ int launch_xr_wc(const Team& t, double rtol) {
     if (h->nranks != X) return fail(NX_ERR_STATE, "exchange step: rank count mismatch");
     h->xtag += 1;  // (the same on every rank: they launch together)
     DirStep da = dir_args(h, rtol);
-    da.n_left = h->xr_nleft;
-    da.xpeers = h->d_xpeers;
-    da.xself = xpeer_of(h->xmb, X);
-    da.xP = X;
-    da.xrank = h->rank;
-    da.xld1 = kXld1;
-    da.xld2 = kXld2;
-    da.xK = h->n_cut;
-    da.xtag = h->xtag;
+    xr_fill(h, da, X);
     das[r] = da;
     goff[r + 1] = goff[r] + h->pc_jobs;
     lds = std::max(lds, h->dstep_lds);
@@ -8509,20 +8692,16 @@ int launch_xr_wc(const Team& t, double rtol) {
     std::memcpy(hb + bp + bd, goff.data(), bo);
     HIPCALL(hipMemcpyAsync(g->xg_dev, g->xg_host, bp + bd + bo, hipMemcpyHostToDevice, g->stream));
     const char* db = static_cast<const char*>(g->xg_dev);
-    const void* fn = reinterpret_cast<const void*>(&k_dir_xg<W, CPL>);
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(160 * 1024 - xr_static_lds(t.hs[0]->dstep_variant)));
-    (void)hipGetLastError();
+    opt_in_lds(reinterpret_cast<const void*>(&k_dir_xg<W, CPL>),
+               (int)(160 * 1024 - xr_static_lds(t.hs[0]->dstep_variant)));
     hipLaunchKernelGGL((k_dir_xg<W, CPL>), dim3(goff[P]), dim3(kPcThreads), lds, g->stream,
                        reinterpret_cast<const PcArgs*>(db), reinterpret_cast<const DirStep*>(db + bp),
                        reinterpret_cast<const int*>(db + bp + bd), P);
     HIPCALL(hipStreamSynchronize(g->stream));  // (the pinned staging is rewritten next launch)
   } else {
     nx_network* h = t.hs[0];
-    const void* fn = reinterpret_cast<const void*>(&k_dir_xr<W, CPL>);
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
-    (void)hipGetLastError();
+    opt_in_lds(reinterpret_cast<const void*>(&k_dir_xr<W, CPL>),
+               (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
     const bool prof = h->prof && h->dev[0];  // (events bound to the dispatch: bench.py)
     hipExtLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
                           h->stream, prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0,
@@ -8557,31 +8736,160 @@ size_t xr_static_lds(int v) {
   return s[i];
 }
 
-// The exchange step of every rank of the team and its published residual (the same on
-// every rank). NX_ERR_STATE: an exchange never completed (the hand-off counters are reset;
-// the caller takes the graph path for this and every later solve of the team).
-int run_xr(const Team& t, double rtol) {
-  CHECK(launch_xr(t, rtol));
-  int rc = NX_OK;
-  for (int r = 0; r < t.P && rc == NX_OK; ++r) rc = wait_published(t.hs[r]);
-  if (rc == NX_ERR_STATE) {
-    (void)hipGetLastError();
-    for (int r = 0; r < t.P; ++r) {
-      nx_network* h = t.hs[r];
-      HIPCALL(hipStreamSynchronize(h->stream));
-      HIPCALL(hipMemset(h->d_dsync, 0, 8 * sizeof(unsigned)));
-      HIPCALL(hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost));
-      h->dstep_epoch = 0;
-      h->xr_off = true;
-    }
-    return rc;
+// ---- after an exchange step: finished, or the ranks agree what to do ---------------------
+// Whether rank h's launch published (finished), and if not why (sync[5]); then the hand-off
+// counters and the host's count of published states are put back in step with the device.
+int xr_settle(nx_network* h, bool* published) {
+  const int rc = wait_published(h);
+  *published = rc == NX_OK;
+  if (rc == NX_OK) {
+    h->xr_why = 0;
+    return NX_OK;
   }
-  CHECK(rc);
-  const MrState& s0 = *t.hs[0]->h_last;
-  for (int r = 1; r < t.P; ++r)
-    if (t.hs[r]->h_last->relres != s0.relres && s0.relres == s0.relres)
-      return fail(NX_ERR_STATE, "ranks disagree on the exchange step's residual");
+  if (rc != NX_ERR_STATE) return rc;
+  (void)hipGetLastError();
+  HIPCALL(hipStreamSynchronize(h->stream));
+  unsigned sy[8];
+  HIPCALL(hipMemcpy(sy, h->d_dsync, sizeof(sy), hipMemcpyDeviceToHost));
+  h->xr_why = sy[5] ? sy[5] : (kXrFail1 | kXrFailLocal);
+  HIPCALL(hipMemset(h->d_dsync, 0, 8 * sizeof(unsigned)));
+  HIPCALL(hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost));
+  h->dstep_epoch = 0;
   return NX_OK;
+}
+
+bool xr_x_final(const nx_network* h) {
+  return (h->xr_why & kXrFail2) && !(h->xr_why & kXrFail1);
+}
+
+// A rank whose launch gave up exchange 2 after passing exchange 1 holds its final x; only the
+// residual's sum is missing. Whether the step can still finish is fixed by then: if every
+// rank passed exchange 1, every rank wrote its exchange-2 slot and flag into every mailbox
+// before it polled (so they arrive); if one did not, that rank never writes them and its
+// abort word says so (reasons with kXrFail1, this launch's tag). So the host waits on its own
+// mailbox for one or the other, and in the first case forms the sums and the residual
+// exactly as dir_publish_xr does (rank order, no contraction: the same bits every other rank
+// published) and takes the step as finished. Then every rank finishes a step, or none does.
+constexpr double kXrHostWaitS = 60.0;
+#pragma clang fp contract(off)
+int xr_host_finish(nx_network* h, double rtol, bool* done) {
+  const int X = h->nranks;
+  const unsigned t = h->xtag;
+  const XPeer me = xpeer_of(h->xmb, X);
+  std::vector<unsigned> fl(4 * (size_t)X);
+  std::vector<double> mb((size_t)X * kXld2);
+  *done = false;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    HIPCALL(hipMemcpy(fl.data(), me.fl, sizeof(unsigned) * fl.size(), hipMemcpyDeviceToHost));
+    const auto* ab = reinterpret_cast<const unsigned long long*>(fl.data() + 2 * X);
+    bool all = true;
+    for (int q = 0; q < X; ++q) {
+      if ((unsigned)ab[q] == t && ((ab[q] >> 32) & kXrFail1)) return NX_OK;  // q stopped early
+      all = all && fl[X + q] == t;
+    }
+    if (all) break;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kXrHostWaitS)
+      return fail(NX_ERR_STATE, "exchange step: a rank's residual share never arrived");
+    sched_yield();
+  }
+  HIPCALL(hipMemcpy(mb.data(), me.mb2, sizeof(double) * mb.size(), hipMemcpyDeviceToHost));
+  const int K = h->n_cut, n = 2 + K;
+  for (int q = 0; q < X; ++q)
+    if (__builtin_bit_cast(unsigned long long, mb[(size_t)q * kXld2 + kXld2 - 1]) != t)
+      return fail(NX_ERR_STATE, "exchange step: a residual slot holds another launch's data");
+  std::vector<double> ys(n);
+  for (int i = 0; i < n; ++i) {
+    double v = 0.0;
+    for (int q = 0; q < X; ++q) v += mb[(size_t)q * kXld2 + i];
+    ys[i] = v;
+  }
+  double rr = ys[0];
+  for (int k = 0; k < K; ++k) {
+    const double rk = 0.0 - ys[2 + k];
+    rr += rk * rk;
+  }
+  const double bb = ys[1];
+  HIPCALL(hipMemcpy(h->dir_bb, &bb, sizeof(double), hipMemcpyHostToDevice));
+  MrState* st = h->h_last;
+  st->beta1 = std::sqrt(bb);
+  st->relres = bb > 0.0 ? std::sqrt(rr / bb) : std::sqrt(rr);
+  st->rtol = rtol;
+  st->it = 1;
+  st->done = 1;
+  st->converged = st->relres <= rtol ? 1 : 0;
+  *done = true;
+  return NX_OK;
+}
+#pragma clang fp contract(on)
+
+// The ranks of separate processes (RCCL, or the host transport) after a launch that no rank
+// finished: one max-all-reduce of [tag, -tag] checks they are all at the same step -- by
+// the construction above they are -- and every rank leaves the exchange step for good; the
+// graph path solves this step. (A mismatch would pair collectives of different steps: it
+// stops loudly instead.)
+int xr_allmax(nx_network* h, double* v, int n) {
+  if (!h->d_agree) CHECK(dalloc(&h->d_agree, 8));
+  HIPCALL(hipMemcpy(h->d_agree, v, sizeof(double) * n, hipMemcpyHostToDevice));
+  if (h->hcomm) {
+    CHECK(hc_allreduce(h, h->d_agree, n, 1));
+  } else {
+    NCCLCALL(ncclAllReduce(h->d_agree, h->d_agree, n, ncclDouble, ncclMax, h->comm, h->stream));
+    HIPCALL(hipStreamSynchronize(h->stream));
+  }
+  HIPCALL(hipMemcpy(v, h->d_agree, sizeof(double) * n, hipMemcpyDeviceToHost));
+  return NX_OK;
+}
+int xr_agree(nx_network* h) {
+  double v[2] = {(double)h->xtag, -(double)h->xtag};
+  CHECK(xr_allmax(h, v, 2));
+  h->xr_agreed += 1;
+  h->xr_off = true;
+  if (v[0] != -v[1]) return fail(NX_ERR_STATE, "exchange step: the ranks gave up different steps");
+  return NX_OK;
+}
+
+enum XrOutcome { kXrDone = 0, kXrGraph = 1 };
+// The exchange step of every rank of the team, settled: kXrDone (every rank holds its x and
+// the same published residual, converged) or kXrGraph (the caller solves this step on the
+// graph path: above rtol everywhere -- the assembly is done -- or given up everywhere, the
+// exchange step then off for good and the assembly pending again).
+int xr_conclude(nx_network* const* hs, int P, bool local, double rtol, int* outcome) {
+  int fin = 0;
+  for (int r = 0; r < P; ++r) {
+    nx_network* h = hs[r];
+    bool done = false;
+    CHECK(xr_settle(h, &done));
+    if (!done && xr_x_final(h)) CHECK(xr_host_finish(h, rtol, &done));
+    if (done) {
+      h->pend_lhs = h->pend_rhs = 0;  // (x final: the launch's assembly is complete too)
+      h->last_dir_path = 3;
+      fin += 1;
+    }
+  }
+  *outcome = kXrGraph;
+  if (fin == 0) {  // nobody finished: every rank leaves the exchange step here
+    if (local) {
+      for (int r = 0; r < P; ++r) {
+        hs[r]->xr_off = true;
+        hs[r]->xr_agreed += 1;
+      }
+    } else {
+      CHECK(xr_agree(hs[0]));
+    }
+    return NX_OK;
+  }
+  if (fin != P) return fail(NX_ERR_STATE, "exchange step: some ranks finished the step, some not");
+  const MrState s = *hs[0]->h_last;
+  for (int r = 1; r < P; ++r)
+    if (hs[r]->h_last->relres != s.relres && s.relres == s.relres)
+      return fail(NX_ERR_STATE, "ranks disagree on the exchange step's residual");
+  if (s.converged || s.relres != s.relres) *outcome = kXrDone;
+  return NX_OK;
+}
+int run_xr(const Team& t, double rtol, int* outcome) {
+  CHECK(launch_xr(t, rtol));
+  return xr_conclude(t.hs, t.P, t.g != nullptr, rtol, outcome);
 }
 
 int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
@@ -8603,12 +8911,9 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   if (multi && !h->xr_off && xr_on(t, with_asm)) {  // several ranks: one launch each
     if (!t.g && h->prof && !h->dev[0])
       for (auto& e : h->dev) HIPCALL(hipEventCreate(&e));
-    const int rc = run_xr(t, rtol);
-    if (rc == NX_OK) {
-      for (int r = 0; r < t.P; ++r) {
-        t.hs[r]->pend_lhs = t.hs[r]->pend_rhs = 0;
-        t.hs[r]->last_dir_path = 3;
-      }
+    int outcome = kXrGraph;
+    CHECK(run_xr(t, rtol, &outcome));
+    if (outcome == kXrDone) {
       if (!t.g && h->prof) {  // k_dir_xr's time (bench.py's roofline: one RCCL rank)
         HIPCALL(hipEventSynchronize(h->dev[1]));
         float ms = 0.f;
@@ -8617,16 +8922,15 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
         h->dir_cnt += 1;
       }
       const MrState s = *h->h_last;
-      if (s.converged || s.relres != s.relres) {
-        if (iters) *iters = 1;
-        if (relres) *relres = s.relres;
-        if (converged) *converged = s.converged;
-        return NX_OK;
-      }
-      with_asm = false;  // (above rtol: the graph path below solves it again and refines)
-    } else if (rc != NX_ERR_STATE) {
-      return rc;
+      if (iters) *iters = 1;
+      if (relres) *relres = s.relres;
+      if (converged) *converged = s.converged;
+      return NX_OK;
     }
+    // the graph path solves this step again (run_xr cleared the pending assembly of the
+    // ranks that finished it above rtol; a launch that gave up leaves it pending)
+    with_asm = true;
+    for (int r = 0; r < t.P; ++r) with_asm = with_asm && t.hs[r]->pend_lhs && t.hs[r]->pend_rhs;
   }
   if (with_asm && dstep_on(h)) {  // the fused step: assembly + solve + check in one launch
     const int rc = run_dstep(h, rtol, prof1);
@@ -8643,6 +8947,7 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
       MrState s = *h->h_last;
       if (!s.converged && s.relres == s.relres) {  // one refinement step (forms r first)
         h->need_r = true;
+        CHECK(ensure_dq(h));
         CHECK(launch_direct(h, rtol, 1));
         h->seq += 1;
         CHECK(wait_published(h));
@@ -8669,6 +8974,7 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   }
   if (prof1) {  // eager, with events bound to the sweeps' and the residual's dispatches
     CHECK(flush_assembly(h));
+    CHECK(ensure_dq(h));
     CHECK(launch_direct(h, rtol, 0, true));
     h->seq += 1;
     CHECK(wait_published(h));
@@ -8692,7 +8998,10 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     return NX_OK;
   }
   for (int r = 0; r < t.P; ++r)
-    if (!with_asm) CHECK(flush_assembly(t.hs[r]));
+    if (!with_asm) {
+      CHECK(flush_assembly(t.hs[r]));
+      CHECK(ensure_dq(t.hs[r]));  // (the graphs below read it; an assembly heading them writes it)
+    }
   // (measured and kept out: forking the CSR values' assembly onto a second graph branch
   // beside the sweeps -- the cross-queue dependencies cost ~13 us at the fork and ~9 us at
   // the join, more than the 17 us assembly they would hide; r02 trace)
@@ -8702,13 +9011,13 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
     return launch_direct(h, rtol, refine);
   };
   // several ranks: graph replay; one rank: the launches issued directly
-  const bool graphs = (!h->comm || h->rccl_graph_ok) && multi;
+  const bool graphs = (!proc_rank(h) || h->rccl_graph_ok) && multi;
   auto run = [&](hipGraphExec_t* exec, hipGraph_t* graph, int* len, double* grtol, int key,
                  int refine, bool asmb) -> int {
     if (graphs && (!*exec || *grtol != rtol || *len != key)) {
       CHECK(drop_one(exec, graph, len));
       const int rc = capture(h, graph, exec, [&] { return body(refine, asmb); });
-      if (rc != NX_OK && h->comm) {  // RCCL refused the capture: eager from now on
+      if (rc != NX_OK && proc_rank(h)) {  // RCCL refused the capture: eager from now on
         (void)hipGetLastError();
         h->rccl_graph_ok = false;
       } else {
@@ -8780,7 +9089,7 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
   LeanGraphs& lg = lean_of(t);
   auto cap = [&](hipGraph_t* graph, hipGraphExec_t* exec, const std::function<int()>& body) {
     const int rc = capture(h0, graph, exec, body);
-    if (rc != NX_OK && h0->comm) {  // RCCL refused the capture: eager from now on
+    if (rc != NX_OK && proc_rank(h0)) {  // RCCL refused the capture: eager from now on
       (void)hipGetLastError();
       h0->rccl_graph_ok = false;
       return (int)NX_ERR_RCCL;
@@ -8881,7 +9190,7 @@ int check_schedules(const Team& t) {
                                       std::to_string(r) + ", item " + std::to_string(i) + ")");
   }
   nx_network* h = t.hs[0];
-  if (!h->comm || h->sched_checked) return NX_OK;
+  if (!proc_rank(h) || h->sched_checked) return NX_OK;
   // max of s and of -s over the ranks: equal iff all ranks agree; the last entry is the
   // max of -direct_local: the direct solve runs only if every rank can run it
   int v[2 * kSchedSig + 2];
@@ -8895,7 +9204,9 @@ int check_schedules(const Team& t) {
   HIPCALL(hipMalloc((void**)&d, sizeof(v)));
   int rc = NX_OK;
   if (hipMemcpy(d, v, sizeof(v), hipMemcpyHostToDevice) != hipSuccess ||
-      ncclAllReduce(d, d, 2 * kSchedSig + 2, ncclInt32, ncclMax, h->comm, h->stream) != ncclSuccess ||
+      (h->hcomm ? hc_allreduce(h, d, 2 * kSchedSig + 2, 1) != NX_OK
+                : ncclAllReduce(d, d, 2 * kSchedSig + 2, ncclInt32, ncclMax, h->comm, h->stream) !=
+                      ncclSuccess) ||
       hipStreamSynchronize(h->stream) != hipSuccess ||
       hipMemcpy(v, d, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(NX_ERR_RCCL, "kernel schedule comparison across ranks failed");
@@ -9018,7 +9329,10 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
     }
     // residual above rtol after a refinement step: MINRES from scratch
   }
-  for (int r = 0; r < t.P; ++r) CHECK(flush_assembly(t.hs[r]));  // MINRES: no deferred work
+  for (int r = 0; r < t.P; ++r) {  // MINRES: no deferred work, the lumped mass formed
+    CHECK(flush_assembly(t.hs[r]));
+    CHECK(ensure_dq(t.hs[r]));
+  }
   if (check_every & 1) ++check_every;
   CHECK(set_device(t.hs[0]));
   const bool multi = team_multi(t);
@@ -9027,10 +9341,10 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   {  // one graph per solve (profiling and the all-reduce beta^2 variant keep the general path)
     nx_network* h0 = t.hs[0];
     const bool prof = h0->prof && t.g == nullptr;
-    const bool ok_multi = !multi || (h0->beta_p2p && (!h0->comm || h0->rccl_graph_ok));
+    const bool ok_multi = !multi || (h0->beta_p2p && (!proc_rank(h0) || h0->rccl_graph_ok));
     if (h0->pc && !prof && lean_env && ok_multi) {
       const int rc = solve_lean(t, rtol, maxit, check_every, iters, relres, converged);
-      if (rc != NX_ERR_RCCL || !h0->comm) return rc;  // RCCL capture refused: eager below
+      if (rc != NX_ERR_RCCL || !proc_rank(h0)) return rc;  // RCCL capture refused: eager below
     }
   }
   for (int r = 0; r < t.P; ++r) t.hs[r]->pa.fuse_pack = 0;  // the general path packs itself
@@ -9099,7 +9413,7 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
   const bool prof = h0->prof && t.g == nullptr;
   // RCCL iterations are captured too (host-side enqueue of ~8 operations per iteration
   // would otherwise pace the loop); if the capture fails, that handle stays eager
-  const bool rccl = t.hs[0]->comm != nullptr;
+  const bool rccl = proc_rank(t.hs[0]);
   bool use_graph = !prof && (!rccl || h0->rccl_graph_ok);
   if (use_graph) {
     const int rc = build_chunk_graph(t, check_every);
@@ -9345,6 +9659,7 @@ NX_API int nx_true_residual(nx_network_t* h, double* relres) {
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials + h->nblk,
                      h->nblk, d + 1);
   HIPCALL(hipGetLastError());
+  if (h->hcomm) CHECK(hc_allreduce(h, d, 2, 0));
   if (h->comm) NCCLCALL(ncclAllReduce(d, d, 2, ncclDouble, ncclSum, h->comm, h->stream));
   HIPCALL(hipStreamSynchronize(h->stream));
   double hd[2] = {0.0, 0.0};
@@ -10033,18 +10348,6 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     const int xr_dbl = h->nranks > 1 ? 2 * (nt + 1) + 4 : 0;
     h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl + xr_dbl});
     h->dstep_top = nt + (nt & 1);
-    // one rank: the top part's solver parks its phase-1 lanes (dir_lane_park) after the top
-    // part's arrays instead of re-assembling them after it, when the LDS has room
-    h->dstep_park = -1;
-    if (h->nranks <= 1) {
-      const int cpl = N <= 16 ? 2 : N <= 24 ? 3 : 4;
-      const int park = dir_park_dbl(cpl);
-      const int main2 = std::max(h->dstep_main, top_dbl + xr_dbl + park);
-      if (8 * (size_t)(kStashDbl + main2 + h->dstep_top) <= (size_t)kDirLdsMax && N <= 32) {
-        h->dstep_park = top_dbl + xr_dbl;
-        h->dstep_main = main2;
-      }
-    }
     h->dstep_lds = 8 * (size_t)(kStashDbl + h->dstep_main + h->dstep_top);
     const bool fits = mlv <= kStLv && mns <= kStNs && mnd <= kStNd && kPcThreads / W <= kStNc;
     h->d_job_hdr = const_cast<int*>(up(hdr.data(), (int64_t)hdr.size()));
@@ -10178,7 +10481,7 @@ NX_API int nx_set_cycles(nx_network_t* h, int32_t n, const int32_t* rows) {
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (n < 0 || (n > 0 && !rows)) return fail(NX_ERR_ARG, "n >= 0 row pairs");
   if (n > 0 && !h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
-  if (n > 0 && (h->nranks > 1 || h->comm || h->group || h->n_ghost > 0))
+  if (n > 0 && (h->nranks > 1 || proc_rank(h) || h->group || h->n_ghost > 0))
     return fail(NX_ERR_STATE, "the cycle correction is one rank's");
   if (n > kMaxCyc) return fail(NX_ERR_ARG, "more cycle chains than kMaxCyc (the solve runs MINRES)");
   for (int64_t i = 0; i < 2 * (int64_t)n; ++i)
@@ -10251,7 +10554,7 @@ NX_API int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64
       !cst)
     return fail(NX_ERR_ARG, "NULL array");
   if (aux->fe || !aux->pc || !aux->cond_mass || aux->N != h->N || aux->E != h->E ||
-      aux->n_cyc > 0 || aux->device != h->device || aux->nranks > 1 || aux->comm || aux->group)
+      aux->n_cyc > 0 || aux->device != h->device || aux->nranks > 1 || proc_rank(aux) || aux->group)
     return fail(NX_ERR_STATE, "the auxiliary handle must be a one-rank P1/DG0 tree handle with "
                               "the same N and edges and its cell mass set (nx_set_cell_mass)");
   const int64_t E = h->E, N = h->N, nv = E * (N + 1), np = E * N, km = k - 1;
@@ -10649,6 +10952,21 @@ NX_API int nx_comm_init(nx_network_t* h, int32_t nranks, int32_t rank, const uns
   return NX_OK;
 }
 
+// Tests: nx_comm_init with the host transport in place of RCCL (several ranks' processes on
+// one GPU, which RCCL refuses): `name` is a POSIX shared-memory name every rank passes (rank
+// 0 chooses it, the host control plane broadcasts it). Eager collectives, no graphs.
+NX_API int nx_comm_init_host(nx_network_t* h, int32_t nranks, int32_t rank, const char* name,
+                             int32_t n_peers, const int32_t* peer_rank, const int32_t* send_off,
+                             const int32_t* send_idx, const int32_t* recv_off) {
+  CHECK(flush_assembly(h));
+  if (!h || !name || name[0] != '/') return fail(NX_ERR_ARG, "a shared-memory name \"/...\"");
+  if (h->group || proc_rank(h)) return fail(NX_ERR_STATE, "handle already has a transport");
+  CHECK(nx_set_halo(h, nranks, rank, n_peers, peer_rank, send_off, send_idx, recv_off));
+  CHECK(hc_open(name, nranks, rank, &h->hcomm));
+  h->rccl_graph_ok = false;  // (every collective synchronises the stream: nothing is captured)
+  return NX_OK;
+}
+
 namespace {
 // The exchange step of ONE rank alone, its exchanges emulated (rehearsal of a multi-GPU run
 // on one GPU, whose ranks cannot all be resident at once): the rank writes its slots into a
@@ -10678,6 +10996,11 @@ int xr_rehearse_wc(nx_network* h, int P, double rtol, int reps, float* ms_out) {
     }
     for (int k = 0; k < K; ++k) x.mb2[2 + k] = -x.mb2[2 + k];  // (the publisher forms 0 - sum)
     for (int i = 0; i < 2 * P; ++i) x.fl[i] = tag;
+    const double tagd = __builtin_bit_cast(double, (unsigned long long)tag);
+    for (int q = 0; q < P; ++q) {  // every slot carries its writer's tag
+      x.mb1[(size_t)q * kXld1 + kXld1 - 1] = tagd;
+      x.mb2[(size_t)q * kXld2 + kXld2 - 1] = tagd;
+    }
     if (hipMalloc(&rd, nb) != hipSuccess || hipMalloc(&wr, nb) != hipSuccess ||
         hipMalloc((void**)&dpeers, sizeof(XPeer) * P) != hipSuccess ||
         hipMemcpy(rd, img.data(), nb, hipMemcpyHostToDevice) != hipSuccess) {
@@ -10756,13 +11079,14 @@ NX_API int nx_debug_xr_rehearse(nx_network_t* h, double rtol, int32_t reps, doub
 // own k_dir_xr (a one-handle team, no group: the exchange width is the handle's nranks) on a
 // stream of its own, so the launches run concurrently and meet only through the mailboxes,
 // as on separate GPUs. The ranks' assembly must be pending (nx_assemble); their jobs must fit
-// the GPU together (co-resident). *relres: rank 0's published residual (every rank's equal).
+// the GPU together (co-resident). The outcome is settled as the group's one launch settles it
+// (xr_conclude); a step the ranks did not finish is solved again on the group's graph path. *relres: the published residual (every rank's equal).
 NX_API int nx_debug_xr_separate(nx_group_t* g, double rtol, double* relres) {
   if (!g || !relres) return fail(NX_ERR_ARG, "null argument");
   const int P = g->P;
   int jobs = 0;
   for (nx_network* h : g->hs) {
-    if (!xr_local(h) || !h->pend_lhs || !h->pend_rhs)
+    if (!xr_local(h) || !h->pend_lhs || !h->pend_rhs || h->xr_off)
       return fail(NX_ERR_STATE, "every rank able to run the exchange step, its assembly pending");
     jobs += h->pc_jobs;
   }
@@ -10773,37 +11097,48 @@ NX_API int nx_debug_xr_separate(nx_group_t* g, double rtol, double* relres) {
   for (int r = 0; r < P; ++r) HIPCALL(hipStreamCreateWithFlags(&ss[r], hipStreamNonBlocking));
   for (int r = 0; r < P; ++r) g->hs[r]->stream = ss[r];
   int rc = NX_OK;
-  int launched = 0;
-  for (int r = 0; r < P && rc == NX_OK; ++r, ++launched) rc = launch_xr(Team{&g->hs[r], 1, nullptr}, rtol);
-  for (int r = 0; r < launched; ++r) {
-    const int w = wait_published(g->hs[r]);
-    if (rc == NX_OK) rc = w;
-  }
+  for (int r = 0; r < P && rc == NX_OK; ++r) rc = launch_xr(Team{&g->hs[r], 1, nullptr}, rtol);
+  int outcome = kXrGraph;
+  if (rc == NX_OK) rc = xr_conclude(g->hs.data(), P, true, rtol, &outcome);
   for (int r = 0; r < P; ++r) (void)hipStreamSynchronize(ss[r]);
   for (int r = 0; r < P; ++r) {
-    nx_network* h = g->hs[r];
-    h->stream = g->stream;
+    g->hs[r]->stream = g->stream;
     (void)hipStreamDestroy(ss[r]);
-    if (rc != NX_OK) {  // (as run_xr: counters and sequence numbers back in step)
-      (void)hipMemset(h->d_dsync, 0, 8 * sizeof(unsigned));
-      (void)hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost);
-      h->dstep_epoch = 0;
-    } else {
-      h->pend_lhs = h->pend_rhs = 0;
-      h->last_dir_path = 3;
-    }
   }
   CHECK(rc);
-  for (int r = 1; r < P; ++r)
-    if (g->hs[r]->h_last->relres != g->hs[0]->h_last->relres)
-      return fail(NX_ERR_STATE, "ranks disagree on the exchange step's residual");
-  *relres = g->hs[0]->h_last->relres;
+  if (outcome == kXrDone) {
+    for (nx_network* h : g->hs) h->last_solver = 1;
+    *relres = g->hs[0]->h_last->relres;
+    return NX_OK;
+  }
+  int32_t it = 0, conv = 0;  // (given up everywhere, or above rtol: the group's graph path)
+  CHECK(solve_team(Team{g->hs.data(), P, g}, rtol, 1 << 16, 4, &it, relres, &conv));
+  return NX_OK;
+}
+
+// Test hook: the poll bound of this rank's exchange `which` (0: the coarse partials, 1: the
+// residual) in its next exchange steps; 0 makes that exchange give up at once (after this
+// rank's own slots and flags are written, so the others may still finish it).
+NX_API int nx_debug_xr_polls(nx_network_t* h, int32_t which, uint32_t polls) {
+  if (!h || which < 0 || which > 1) return fail(NX_ERR_ARG, "which is 0 or 1");
+  h->xpoll[which] = polls;
+  return NX_OK;
+}
+
+// [xr_off, the last launch's give-up reasons (kXrFail*), agreements taken part in, the last
+// launch's tag]
+NX_API int nx_get_xr_status(nx_network_t* h, int32_t* out) {
+  if (!h || !out) return fail(NX_ERR_ARG, "null argument");
+  out[0] = h->xr_off ? 1 : 0;
+  out[1] = (int32_t)h->xr_why;
+  out[2] = h->xr_agreed;
+  out[3] = (int32_t)h->xtag;
   return NX_OK;
 }
 
 NX_API int nx_xch_export(nx_network_t* h, unsigned char* handle_out) {
   if (!h || !handle_out) return fail(NX_ERR_ARG, "null argument");
-  if (!h->comm) return fail(NX_ERR_STATE, "nx_comm_init first");
+  if (!proc_rank(h)) return fail(NX_ERR_STATE, "nx_comm_init first");
   CHECK(set_device(h));
   CHECK(xr_alloc(h, h->nranks));
   hipIpcMemHandle_t m;
@@ -10816,7 +11151,7 @@ NX_API int nx_xch_export(nx_network_t* h, unsigned char* handle_out) {
 
 NX_API int nx_xch_import(nx_network_t* h, const unsigned char* handles) {
   if (!h || !handles) return fail(NX_ERR_ARG, "null argument");
-  if (!h->comm || !h->xmb) return fail(NX_ERR_STATE, "nx_xch_export first");
+  if (!proc_rank(h) || !h->xmb) return fail(NX_ERR_STATE, "nx_xch_export first");
   CHECK(set_device(h));
   const int P = h->nranks;
   std::vector<XPeer> peers(P);
@@ -10845,7 +11180,7 @@ NX_API int nx_group_create(int32_t nranks, nx_network_t* const* handles, nx_grou
     if (!h) return fail(NX_ERR_ARG, "null handle in group");
     // (a deferred nx_assemble stays pending: the group's first direct solve runs it inside
     // its own launch, on the group's stream)
-    if (h->group || h->comm) return fail(NX_ERR_STATE, "handle already has a transport");
+    if (h->group || proc_rank(h)) return fail(NX_ERR_STATE, "handle already has a transport");
     if (h->device != handles[0]->device) return fail(NX_ERR_ARG, "group members share one device");
     if (nranks > 1 && (!h->have_plan || h->rank != r || h->nranks != nranks))
       return fail(NX_ERR_STATE, "handle " + std::to_string(r) + " needs nx_set_halo(rank " +

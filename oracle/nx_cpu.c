@@ -25,6 +25,7 @@
 #define API __attribute__((visibility("default")))
 
 API int nxc_threads(void) { return omp_get_max_threads(); }
+API void nxc_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
 /* ---- pattern: one edge's rows are one contiguous CSR segment (device layout) ---- */
 API int64_t nxc_nnz(int N, int64_t E, const int* edge_lm, int64_t B, const int* lm_rowptr) {

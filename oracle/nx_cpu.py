@@ -31,6 +31,8 @@ def lib():
             raise FileNotFoundError(f"{LIB} missing: run `make -C oracle`")
         L = C.CDLL(str(LIB))
         L.nxc_threads.restype = C.c_int
+        L.nxc_set_threads.restype = None
+        L.nxc_set_threads.argtypes = [C.c_int]
         L.nxc_nnz.restype = C.c_int64
         L.nxc_nnz.argtypes = [C.c_int, C.c_int64, _pi, C.c_int64, _pi]
         L.nxc_assemble.restype = None
@@ -50,6 +52,11 @@ def lib():
 
 def threads() -> int:
     return int(lib().nxc_threads())
+
+
+def set_threads(n: int) -> None:
+    """The OpenMP thread count of the following calls (``omp_set_num_threads``)."""
+    lib().nxc_set_threads(int(n))
 
 
 def _p(a, t):

@@ -108,3 +108,16 @@ def test_c4_eight_rank_group(c4):
         rows = DM.global_rows(a.local_problem, E, m0.bifurcation_index)
         err_r = np.linalg.norm(xl - xa[rows]) / np.linalg.norm(xa[rows])
         assert err_r <= TOL, (r, err_r)
+    # the exchange step of every rank alone, as on its own GPU (k_dir_xr<8, 3> at N = 19,
+    # nx_debug_xr_rehearse: its two exchanges emulated from this graph-path solve's sums):
+    # the analytic answer per rank, and the graph path's x to its rounding (the coarse
+    # forest's reciprocal form rounds differently)
+    xg = [xl.copy() for xl in grp.solutions()]
+    for r, a in enumerate(grp.assemblers):
+        ms = a.handle.xr_rehearse(1e-12, 3)
+        assert ms > 0.0
+        xl = a.handle.solution()
+        rows = DM.global_rows(a.local_problem, E, m0.bifurcation_index)
+        err_r = np.linalg.norm(xl - xa[rows]) / np.linalg.norm(xa[rows])
+        assert err_r <= TOL, (r, err_r)
+        assert np.linalg.norm(xl - xg[r]) <= 1e-14 * np.linalg.norm(xg[r]), r

@@ -580,3 +580,83 @@ def test_group_exchange_give_up_falls_back():
             assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
     finally:
         grp.close()
+
+
+@pytest.mark.parametrize("separate", [False, True])
+def test_exchange_one_rank_gives_up_exchange2(separate):
+    """One rank's exchange 2 gives up at once (nx_debug_xr_polls(1, 0): after its own slots
+    and flags went out) while the others finish it -- in the group's one launch and as
+    separate concurrent launches (the RCCL ranks' shape). The rank's host finishes exchange
+    2 from its mailbox with the same bits, so every rank ends the step on the exchange path
+    with the oracle's answer and the same residual; 5 further steps stay on it, bit for bit."""
+    case, P = "depth6_N40", 3
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.set_direct(True)
+        grp.assemble()
+        _, rr, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and {a.handle.direct_path() for a in grp.assemblers} == {"exchange"}
+        x1 = _gathered(grp, Ab, mesh)
+        grp.assemblers[1].handle.xr_polls(1, 0)
+        for k in range(6):
+            grp.assemble()
+            if separate:
+                rr2 = grp._group.xr_separate(1e-12)
+            else:
+                _, rr2, _ = grp.solve(1e-12, 50000, 4)
+            st = [a.handle.xr_status() for a in grp.assemblers]
+            assert {a.handle.direct_path() for a in grp.assemblers} == {"exchange"}, (k, st)
+            assert not any(s["off"] for s in st), st
+            if k == 0:  # (the hook: given up, finished on the host)
+                assert st[1]["why"] & 2, st
+            else:
+                assert all(s["why"] == 0 for s in st), (k, st)
+            assert rr2 == rr
+            np.testing.assert_array_equal(_gathered(grp, Ab, mesh), x1)
+            if k == 0:
+                grp.assemblers[1].handle.xr_polls(1, 1 << 20)  # (steps 1..5: no give-up)
+        assert np.linalg.norm(x1 - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    finally:
+        grp.close()
+
+
+@pytest.mark.parametrize("separate", [False, True])
+def test_exchange_one_rank_gives_up_exchange1(separate):
+    """One rank's exchange 1 gives up at once: that step cannot finish anywhere (the rank
+    never sends its residual share), every rank's launch gives up -- the others on its
+    abort word -- and every rank solves it and the 5 steps after it on the graph path: the
+    same path on every rank, the oracle's answer every step."""
+    case, P = "depth6_N40", 3
+    make, N, strategy, pbc = CASES[case]
+    G, mesh, Ab, bb, x_ref = _reference(case)
+    grp = RankGroup(G, N, P, color_strategy=strategy)
+    try:
+        grp.compute_forms(p_bc_ex=pbc)
+        grp.set_direct(True)
+        grp.assemble()
+        grp.solve(1e-12, 50000, 4)
+        assert {a.handle.direct_path() for a in grp.assemblers} == {"exchange"}
+        grp.assemblers[1].handle.xr_polls(0, 0)
+        grp.assemble()
+        if separate:
+            rr = grp._group.xr_separate(1e-12)
+        else:
+            _, rr, conv = grp.solve(1e-12, 50000, 4)
+            assert conv
+        st = [a.handle.xr_status() for a in grp.assemblers]
+        assert all(s["off"] and s["agreed"] == 1 for s in st), st
+        assert st[1]["why"] & 1 and all(s["why"] & 4 for q, s in enumerate(st) if q != 1), st
+        assert rr <= 1e-12
+        for k in range(6):
+            if k:
+                grp.assemble()
+                _, rr, conv = grp.solve(1e-12, 50000, 4)
+                assert conv and rr <= 1e-12
+            assert {a.handle.direct_path() for a in grp.assemblers} == {"launches"}, k
+            x = _gathered(grp, Ab, mesh)
+            assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL, k
+    finally:
+        grp.close()

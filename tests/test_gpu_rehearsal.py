@@ -1,0 +1,59 @@
+"""The bench's 8-GPU workload (``bench.py --gpus 8``: ``make_tree(18,18,18)``, N = 15, one
+C3-sized piece per rank, 8,257,536 DoF) on one GPU: the 8 per-rank handles through the
+in-process group (graph path: coarse all-reduce, cut rows in the residual's sum), then
+every rank's one-launch exchange step alone as on its own GPU (``k_dir_xr<8, 2>``,
+``nx_debug_xr_rehearse``: its exchanges emulated from the graph path's sums).
+
+Checks (size-independent: the oracle's direct solve does not fit a test at this size): every
+rank's rows against the analytic resistor-network answer to 1e-10, and the exchange step's x
+against the graph path's to 1e-14 (the coarse forest's reciprocal form rounds differently).
+SURVEY's C4 (N = 19, ``k_dir_xr<8, 3>``) is checked the same way in test_gpu_c4.py."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import distributed_model as DM
+from networks_fenicsx_amd import network_generation as ng
+from networks_fenicsx_amd.group import RankGroup
+from oracle import nx_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+LEVELS, N, P = 18, 15, 8
+TOL = 1e-10
+
+
+def p_y(x):
+    return x[1]
+
+
+def test_bench_workload_exchange_rehearsal():
+    G = ng.make_tree(LEVELS, LEVELS, LEVELS)
+    grp = RankGroup(G, N, P, color_strategy="smallest_last")
+    del G
+    try:
+        m0 = grp.meshes[0]
+        src, dst = m0.edges
+        prob = O.build_problem(m0.node_coordinates, src, dst, N)
+        xa = O.resistor_network_solution(prob, p_y)[O.build_permutation(prob)[0]]
+        E = m0.num_edges
+        assert xa.size == 8_257_536
+        grp.compute_forms(p_bc_ex=p_y)
+        grp.set_direct(True)
+        grp.assemble()
+        it, relres, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and it in (1, 2) and grp.solver_used == "direct", (it, relres)
+        xg = [xl.copy() for xl in grp.solutions()]
+        for r, a in enumerate(grp.assemblers):
+            rows = DM.global_rows(a.local_problem, E, m0.bifurcation_index)
+            assert np.linalg.norm(xg[r] - xa[rows]) <= TOL * np.linalg.norm(xa[rows]), r
+            ms = a.handle.xr_rehearse(1e-12, 3)
+            assert ms > 0.0
+            xl = a.handle.solution()
+            err_r = np.linalg.norm(xl - xa[rows]) / np.linalg.norm(xa[rows])
+            assert err_r <= TOL, (r, err_r)
+            assert np.linalg.norm(xl - xg[r]) <= 1e-14 * np.linalg.norm(xg[r]), r
+    finally:
+        grp.close()
