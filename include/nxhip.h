@@ -260,6 +260,20 @@ int nx_get_solver(nx_network_t* h, int32_t* requested, int32_t* last_run);
  * factorisation (solver.py:58-65) covers cycles implicitly.
  */
 int nx_set_cycles(nx_network_t* h, int32_t n, const int32_t* rows);
+/* The same correction with several ranks (RCCL ranks or an in-process group): every rank
+ * calls it after nx_set_preconditioner with the cycle chains of ALL ranks in one global
+ * order (K pairs, K <= 128; the host control plane gathers them). own[2K]: per column of U
+ * (pair k's flux end at 2k, its multiplier at 2k + 1) this rank's row, or -1 where another
+ * rank owns it; qloc[K] / lcol[K]: for the pairs whose chain is this rank's, the flux end row
+ * and the multiplier's column in this rank's numbering (a ghost column when another rank
+ * owns the multiplier row), else -1. Z = A_g^{-1} U is built by 2K team tree solves, U^T Z
+ * and the couplings are summed over the ranks (one all-reduce), every rank inverts the same
+ * capacitance matrix; per solve U^T x is summed (one all-reduce of 2K), x -= Z Cinv U^T x on
+ * every rank's rows, and the true residual comes from the CSR after a halo of x. The cycle
+ * count is part of the ranks' schedule signature. K = 0 clears it. Replaces MUMPS'
+ * distributed factorisation of a cyclic graph (solver.py:58-65, mesh.py:341-348). */
+int nx_set_cycles_team(nx_network_t* h, int32_t K, const int32_t* own, const int32_t* qloc,
+                       const int32_t* lcol);
 
 /*
  * General flux degree k >= 2 with DG0 pressure (assembly.py:121-146, flux_degree=k), one

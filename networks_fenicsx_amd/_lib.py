@@ -96,6 +96,7 @@ _SIGS = {
     "nx_get_pc_exact": (C.c_int, [_h, _pi32]),
     "nx_set_solver": (C.c_int, [_h, _i32, _i32]),
     "nx_set_cycles": (C.c_int, [_h, _i32, _pi32]),
+    "nx_set_cycles_team": (C.c_int, [_h, _i32, _pi32, _pi32, _pi32]),
     "nx_set_cell_mass": (C.c_int, [_h, _f64, _f64]),
     "nx_fe_set_direct": (C.c_int, [_h, _h, _i32, _i64, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                    _pi32, _pi32, _pd, _f64]),
@@ -488,6 +489,18 @@ class Handle:
             # tree solve drops (nx_set_cycles; past MAX_CYCLES the solve runs MINRES)
             self._pc_keep_y = cyc
             check(lib().nx_set_cycles(self.ptr, int(cyc.shape[0]), _ptr(cyc, C.c_int32)))
+
+    def set_cycles_team(self, own, qloc, lcol) -> None:
+        """Several ranks, a graph with cycles (``nx_set_cycles_team``): this rank's share of
+        the Woodbury correction of all ranks' K cycle chains (``own``: 2K, ``qloc`` /
+        ``lcol``: K; see include/nxhip.h). Empty arrays clear it."""
+        arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (own, qloc, lcol)]
+        K = int(arrs[1].size)
+        if arrs[0].size != 2 * K or arrs[2].size != K:
+            raise ValueError("own must hold 2K entries, qloc and lcol K")
+        arrs = [a if a.size else np.zeros(1, np.int32) for a in arrs]
+        self._cyc_team_keep = arrs
+        check(lib().nx_set_cycles_team(self.ptr, K, *[_ptr(a, C.c_int32) for a in arrs]))
 
     def set_pc_exact(self, enable: bool) -> None:
         """Consistent (exact Schur complement, default) or lumped flux mass in P."""

@@ -36,7 +36,8 @@ from . import _lib
 from .comm import MIN, GroupRankComm
 from .fem import Constant, Function, FunctionSpace
 from .element import condensed_flux_mass, stable_pair
-from .layout import LocalProblem, build_local_problem
+from .layout import (LocalProblem, build_local_problem, cycle_pairs_global,
+                     team_cycle_tables)
 from .layout_fe import FeLayout, build_fe_aux_maps, build_fe_layout
 from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
@@ -451,8 +452,39 @@ class HydraulicNetworkAssembler:
             if int(comm.allreduce(lds, MIN)) == 0 and lds:
                 self._handle.set_pc_kernels(True)
                 self._handle.set_preconditioner(self._pc)
+            # a graph with cycles: every rank's share of the Woodbury correction of all
+            # ranks' cycle chains (nx_set_cycles_team; the pairs gathered on the host)
+            pairs = [p for ps in comm.allgather(self.cycle_pairs()) for p in ps]
+            self.set_team_cycles(pairs)
         self._pc_on = on
         return on
+
+    def cycle_pairs(self) -> list:
+        """This rank's cycle chains' dropped couplings (flux end, multiplier) as rows of the
+        single-rank layout (several ranks; ``TreePreconditioner.cyc_rows``)."""
+        if self._pc is None or self._local is None:
+            return []
+        mesh = self._network_mesh
+        return cycle_pairs_global(self._local, self._pc.cyc_rows, mesh.num_edges,
+                                  mesh.bifurcation_index)
+
+    def set_team_cycles(self, all_pairs) -> None:
+        """Several ranks: this rank's share of the direct solve's Woodbury correction of every
+        rank's cycle chains (``nx_set_cycles_team``); beyond ``MAX_CYCLES`` chains (or none)
+        it is cleared and a cyclic graph runs MINRES."""
+        if self._nranks < 2 or not self._pc_on_pending():
+            return
+        pairs = list(all_pairs)
+        if not pairs or len(pairs) > _lib.MAX_CYCLES:
+            self._handle.set_cycles_team([], [], [])
+            return
+        mesh = self._network_mesh
+        own, qloc, lcol = team_cycle_tables(self._local, self._pc.cyc_rows, pairs,
+                                            mesh.num_edges, mesh.bifurcation_index)
+        self._handle.set_cycles_team(own, qloc, lcol)
+
+    def _pc_on_pending(self) -> bool:
+        return self._pc is not None and self._handle is not None
 
     @property
     def preconditioned(self) -> bool:

@@ -6045,9 +6045,59 @@ __global__ __launch_bounds__(kBlock) void k_cyc_fix(double* __restrict__ x, cons
   x[i] -= s;
 }
 
-// b = e_row: the right-hand side of one column of Z (b zeroed before)
+// b = e_row: the right-hand side of one column of Z (b zeroed before; several ranks: only
+// the row's owner sets it, rows[j] < 0 elsewhere)
 __global__ void k_cyc_unit(double* __restrict__ b, const int* __restrict__ rows, int j) {
-  b[rows[j]] = 1.0;
+  if (rows[j] >= 0) b[rows[j]] = 1.0;
+}
+
+// ---- graphs with cycles, several ranks (nx_set_cycles_team): the same Woodbury correction
+// with U's m rows spread over the ranks (a cycle chain's flux end lives with the chain, its
+// multiplier row with the bifurcation's owner). own[i]: this rank's row of U's column i,
+// or -1. Per assembled matrix every rank's share of U^T Z and of the couplings is summed over
+// the ranks (one all-reduce); per solve U^T x is (one all-reduce of m).
+
+// u_i = x[own_i] on this rank's rows, 0 elsewhere (summed over the ranks next)
+__global__ __launch_bounds__(256) void k_cyc_gather(const double* __restrict__ x,
+                                                    const int* __restrict__ own, int m,
+                                                    double* __restrict__ u) {
+  for (int i = threadIdx.x; i < m; i += 256) u[i] = own[i] >= 0 ? x[own[i]] : 0.0;
+}
+
+// This rank's share of U^T Z (rows of U it owns) and of the couplings a (the cycle chains it
+// holds: row q, column lam -- maybe a ghost column -- of its CSR).
+__global__ __launch_bounds__(256) void k_cyc_cap_team(Csr A, const double* __restrict__ Z, int64_t ldz,
+                                                      const int* __restrict__ own, int m,
+                                                      const int* __restrict__ qloc,
+                                                      const int* __restrict__ lcol,
+                                                      double* __restrict__ cap,
+                                                      double* __restrict__ acoef) {
+  for (int i = threadIdx.x; i < m * m; i += 256) {
+    const int r = i / m, c = i % m;
+    cap[i] = own[r] >= 0 ? Z[(int64_t)c * ldz + own[r]] : 0.0;
+  }
+  for (int k = threadIdx.x; 2 * k < m; k += 256) {
+    double a = 0.0;
+    if (qloc[k] >= 0)
+      for (int p = A.rowptr[qloc[k]]; p < A.rowptr[qloc[k] + 1]; ++p)
+        if (A.col[p] == lcol[k]) a = A.val[p];
+    acoef[k] = a;
+  }
+}
+
+// w = Cinv (u - prev) from the summed u (prev: U^T x before a refinement pass, or null).
+__global__ __launch_bounds__(256) void k_cyc_w_team(const double* __restrict__ u, int m,
+                                                    const double* __restrict__ cinv,
+                                                    const double* __restrict__ prev,
+                                                    double* __restrict__ w) {
+  __shared__ double g[2 * kMaxCyc];
+  for (int i = threadIdx.x; i < m; i += 256) g[i] = prev ? u[i] - prev[i] : u[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += 256) {
+    double s = 0.0;
+    for (int j = 0; j < m; ++j) s += cinv[(int64_t)i * m + j] * g[j];
+    w[i] = s;
+  }
 }
 
 // ||b - A x|| / ||b|| from k_residual's partials (fixed order), published like a MINRES
@@ -6405,6 +6455,12 @@ struct nx_network {
   double* cyc_prev = nullptr;  // m
   double* cyc_w = nullptr;     // m
   bool cyc_raw = false;        // cyc_build's solves: the tree solve alone
+  // several ranks (nx_set_cycles_team): per U column this rank's row or -1 (d_cyc_rows),
+  // per pair the flux end row and the multiplier's column when the chain is here, else -1
+  bool cyc_team = false;
+  int* d_cyc_qloc = nullptr;
+  int* d_cyc_lcol = nullptr;
+  double* cyc_u = nullptr;  // m: U^T x summed over the ranks
   int64_t lhs_version = 0, cyc_version = -1;
   int64_t coef_version = 0, asm_coef_version = -1;  // nx_set_coefficients calls; at the last lhs
   // several ranks, direct (nx_set_cut): the multiplier rows of the K cut bifurcations are
@@ -6700,9 +6756,11 @@ int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false, bool pack
   return NX_OK;
 }
 
-// sum-all-reduce of n doubles: red + slot (slot 0..3) or the coarse buffer (slot -1)
+// sum-all-reduce of n doubles: red + slot (slot 0..3), the coarse buffer (-1), the cut rows'
+// buffer (-2), the cycle correction's U^T x (-3) or its U^T Z and couplings (-4)
 double* xbuf_of(nx_network* h, int slot) {
-  return slot == -2 ? h->cutbuf : slot < 0 ? h->pa.cbuf : h->red + slot;
+  return slot == -4 ? h->cyc_cap : slot == -3 ? h->cyc_u : slot == -2 ? h->cutbuf
+         : slot < 0 ? h->pa.cbuf : h->red + slot;
 }
 
 int team_allreduce(const Team& t, int slot, int n) {
@@ -8326,8 +8384,6 @@ int run_dstep(nx_network* h, double rtol, bool prof) {
     case 5: launch_dstep_wc<8, 2>(h, rtol, prof); break;
     case 7: launch_dstep_wc<8, 4>(h, rtol, prof); break;
     case 10: launch_dstep_wc<8, 3>(h, rtol, prof); break;
-    case 8: launch_dstep_wc<64, 8>(h, rtol, prof); break;
-    case 9: launch_dstep_wc<64, 16>(h, rtol, prof); break;
     default: launch_dstep_wc<64, 4>(h, rtol, prof); break;
   }
   HIPCALL(hipGetLastError());
@@ -8353,31 +8409,11 @@ int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
   return NX_OK;
 }
 
-// Graphs with cycles: Z = A_g^{-1} U column by column (the tree solve of a unit right-hand
-// side, accumulated into a zeroed x), then C^{-1} + U^T Z inverted on the host (m <= 256,
-// Gauss-Jordan with partial pivoting). Once per assembled matrix.
-int cyc_build(nx_network* h) {
+// Cinv = (C^{-1} + U^T Z)^{-1} on the host from cyc_cap (m x m U^T Z, then the m / 2
+// couplings a: C^{-1} of [[0, a], [a, 0]] is [[0, 1/a], [1/a, 0]]), Gauss-Jordan with
+// partial pivoting; the same on every rank of a team (the same summed inputs).
+int cyc_invert(nx_network* h) {
   const int m = 2 * h->n_cyc;
-  CHECK(ensure_dq(h));
-  h->cyc_raw = true;
-  h->need_r = false;
-  for (int j = 0; j < m; ++j) {
-    HIPCALL(hipMemsetAsync(h->tmp, 0, sizeof(double) * h->n_col, h->stream));
-    HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, h->stream));
-    hipLaunchKernelGGL(k_cyc_unit, dim3(1), dim3(1), 0, h->stream, h->tmp, h->d_cyc_rows, j);
-    const int rc = launch_direct(h, 0.0, 1);
-    if (rc != NX_OK) {
-      h->cyc_raw = false;
-      return rc;
-    }
-    h->seq += 1;
-    CHECK(wait_published(h));
-    HIPCALL(hipMemcpyAsync(h->cyc_z + (int64_t)j * h->n_col, h->x, sizeof(double) * h->n_col,
-                           hipMemcpyDeviceToDevice, h->stream));
-  }
-  h->cyc_raw = false;
-  hipLaunchKernelGGL(k_cyc_cap, dim3(1), dim3(256), 0, h->stream, csr_of(h), h->cyc_z, h->n_col,
-                     h->d_cyc_rows, m, h->cyc_cap, h->cyc_cap + (int64_t)m * m);
   std::vector<double> cap((size_t)m * m + m / 2);
   HIPCALL(hipMemcpyAsync(cap.data(), h->cyc_cap, sizeof(double) * cap.size(),
                          hipMemcpyDeviceToHost, h->stream));
@@ -8417,6 +8453,35 @@ int cyc_build(nx_network* h) {
     }
   }
   HIPCALL(hipMemcpy(h->cyc_cinv, inv.data(), sizeof(double) * inv.size(), hipMemcpyHostToDevice));
+  return NX_OK;
+}
+
+// Graphs with cycles: Z = A_g^{-1} U column by column (the tree solve of a unit right-hand
+// side, accumulated into a zeroed x), then C^{-1} + U^T Z inverted on the host (m <= 256,
+// Gauss-Jordan with partial pivoting). Once per assembled matrix.
+int cyc_build(nx_network* h) {
+  const int m = 2 * h->n_cyc;
+  CHECK(ensure_dq(h));
+  h->cyc_raw = true;
+  h->need_r = false;
+  for (int j = 0; j < m; ++j) {
+    HIPCALL(hipMemsetAsync(h->tmp, 0, sizeof(double) * h->n_col, h->stream));
+    HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, h->stream));
+    hipLaunchKernelGGL(k_cyc_unit, dim3(1), dim3(1), 0, h->stream, h->tmp, h->d_cyc_rows, j);
+    const int rc = launch_direct(h, 0.0, 1);
+    if (rc != NX_OK) {
+      h->cyc_raw = false;
+      return rc;
+    }
+    h->seq += 1;
+    CHECK(wait_published(h));
+    HIPCALL(hipMemcpyAsync(h->cyc_z + (int64_t)j * h->n_col, h->x, sizeof(double) * h->n_col,
+                           hipMemcpyDeviceToDevice, h->stream));
+  }
+  h->cyc_raw = false;
+  hipLaunchKernelGGL(k_cyc_cap, dim3(1), dim3(256), 0, h->stream, csr_of(h), h->cyc_z, h->n_col,
+                     h->d_cyc_rows, m, h->cyc_cap, h->cyc_cap + (int64_t)m * m);
+  CHECK(cyc_invert(h));
   h->cyc_version = h->lhs_version;
   return NX_OK;
 }
@@ -8428,8 +8493,9 @@ int cyc_build(nx_network* h) {
 // also the LDS sweeps (their mode kModeDirect) and the coarse step.
 bool direct_local(const nx_network* h) {
   const bool multi = proc_rank(h) || h->group != nullptr || h->nranks > 1;
-  // a graph with cycles: one rank, with the Woodbury correction of its cycle chains
-  const bool exact = h->tree_exact || (h->n_cyc > 0 && !multi);
+  // a graph with cycles: the Woodbury correction of its cycle chains (one rank, or every
+  // rank's share of it: nx_set_cycles_team)
+  const bool exact = h->tree_exact || (h->n_cyc > 0 && (!multi || h->cyc_team));
   // the LDS sweeps run it (their mode 3); the global-memory fallback (LDS caps exceeded)
   // leaves the solve to MINRES
   if (!(h->solver == 1 && h->pc && h->pc_lds && h->pa.exact && exact && h->E > 0)) return false;
@@ -8476,8 +8542,14 @@ bool cut_mode(const nx_network* h) {
 // asmb (first pass): every rank's assembly is pending and heads its first half --
 // k_dir_team_up where it applies (assembly + up sweep + top part in one launch), else the
 // assembly kernel then the sweeps.
+int cyc_gather_team(const Team& t, bool prev);
+int cyc_fix_team(const Team& t, double rtol, bool refine);
 int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false) {
   nx_network* h0 = t.hs[0];
+  // graphs with cycles (nx_set_cycles_team): after the sweeps (A_g^{-1} b) the Woodbury
+  // correction and the CSR's true residual publish; the sweeps' own residual is A_g's
+  const bool cyc = h0->cyc_team && h0->n_cyc > 0 && !h0->cyc_raw;
+  if (cyc && refine) CHECK(cyc_gather_team(t, true));  // U^T x before the correction's sweeps
   if (refine) {  // the previous pass's check left r = b - A x in tmp; its ghost slots 0
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
@@ -8516,6 +8588,7 @@ int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false
                          h->pa.slot_lam + h->top_ts0, h->pa.slot_z + h->top_ts0, ntop);
     }
     CHECK(team_allreduce(t, -2, 2 + h0->n_cut));
+    if (cyc) return cyc_fix_team(t, rtol, refine);
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
       hipLaunchKernelGGL(k_dir_publish_cut, dim3(1), dim3(64), 0, h->stream, h->cutbuf,
@@ -8524,6 +8597,7 @@ int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false
     HIPCALL(hipGetLastError());
     return NX_OK;
   }
+  if (cyc) return cyc_fix_team(t, rtol, refine);
   CHECK(team_halo(t, VS_X, 0));
   for (int r = 0; r < t.P; ++r) {  // the down sweeps formed the local rows (direct_local:
     nx_network* h = t.hs[r];       // fres_ok); the rest need the halo of x
@@ -8538,6 +8612,106 @@ int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false
                        h->d_seq, h->d_last);
   }
   HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+// ---- graphs with cycles, several ranks: the Woodbury correction across the ranks ---------
+// U^T x over the ranks into cyc_u (prev: kept in cyc_prev, before a refinement pass's sweeps)
+int cyc_gather_team(const Team& t, bool prev) {
+  const int m = 2 * t.hs[0]->n_cyc;
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_cyc_gather, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
+                       h->cyc_u);
+  }
+  HIPCALL(hipGetLastError());
+  CHECK(team_allreduce(t, -3, m));
+  if (prev)
+    for (int r = 0; r < t.P; ++r)
+      HIPCALL(hipMemcpyAsync(t.hs[r]->cyc_prev, t.hs[r]->cyc_u, sizeof(double) * m,
+                             hipMemcpyDeviceToDevice, t.hs[r]->stream));
+  return NX_OK;
+}
+
+// After the sweeps: x -= Z Cinv U^T (x - x_before) on every rank's rows, then the true
+// residual of A (the halo of x, every owned row from the CSR, the two sums over the ranks)
+// published -- r kept in tmp for a refinement pass.
+int cyc_fix_team(const Team& t, double rtol, bool refine) {
+  const int m = 2 * t.hs[0]->n_cyc;
+  CHECK(cyc_gather_team(t, false));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_cyc_w_team, dim3(1), dim3(256), 0, h->stream, h->cyc_u, m, h->cyc_cinv,
+                       refine ? h->cyc_prev : nullptr, h->cyc_w);
+    hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
+                       h->x, h->cyc_z, h->n_col, h->cyc_w, m, h->n_own);
+  }
+  HIPCALL(hipGetLastError());
+  CHECK(team_halo(t, VS_X, 0));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
+    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials, nrb,
+                       h->red + 2);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials + nrb,
+                       nrb, h->red + 3);
+  }
+  HIPCALL(hipGetLastError());
+  CHECK(team_allreduce(t, 2, 2));
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_dir_publish_red, dim3(1), dim3(64), 0, h->stream, h->red + 2, rtol,
+                       h->d_seq, h->d_last);
+  }
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
+
+// Z = A_g^{-1} U over the ranks (2K team tree solves of a unit right-hand side set by the
+// row's owner, accumulated into zeroed x -- a refinement pass's shape), then every rank's
+// share of U^T Z and of the couplings, summed over the ranks, and the same Cinv on every
+// rank. Once per assembled matrix.
+int cyc_build_team(const Team& t) {
+  const int m = 2 * t.hs[0]->n_cyc;
+  for (int r = 0; r < t.P; ++r) {
+    CHECK(ensure_dq(t.hs[r]));
+    t.hs[r]->cyc_raw = true;
+  }
+  int rc = NX_OK;
+  for (int j = 0; j < m && rc == NX_OK; ++j) {
+    for (int r = 0; r < t.P; ++r) {
+      nx_network* h = t.hs[r];
+      HIPCALL(hipMemsetAsync(h->tmp, 0, sizeof(double) * h->n_col, h->stream));
+      HIPCALL(hipMemsetAsync(h->x, 0, sizeof(double) * h->n_col, h->stream));
+      hipLaunchKernelGGL(k_cyc_unit, dim3(1), dim3(1), 0, h->stream, h->tmp, h->d_cyc_rows, j);
+    }
+    rc = launch_direct_team(t, 0.0, 1, false);
+    for (int r = 0; r < t.P && rc == NX_OK; ++r) {
+      nx_network* h = t.hs[r];
+      h->seq += 1;
+      rc = wait_published(h);
+      if (rc == NX_OK && hipMemcpyAsync(h->cyc_z + (int64_t)j * h->n_col, h->x,
+                                        sizeof(double) * h->n_col, hipMemcpyDeviceToDevice,
+                                        h->stream) != hipSuccess)
+        rc = fail(NX_ERR_HIP, "cycle correction: copying a column of Z failed");
+    }
+  }
+  for (int r = 0; r < t.P; ++r) t.hs[r]->cyc_raw = false;
+  CHECK(rc);
+  for (int r = 0; r < t.P; ++r) {
+    nx_network* h = t.hs[r];
+    hipLaunchKernelGGL(k_cyc_cap_team, dim3(1), dim3(256), 0, h->stream, csr_of(h), h->cyc_z,
+                       h->n_col, h->d_cyc_rows, m, h->d_cyc_qloc, h->d_cyc_lcol, h->cyc_cap,
+                       h->cyc_cap + (int64_t)m * m);
+  }
+  HIPCALL(hipGetLastError());
+  CHECK(team_allreduce(t, -4, m * m + m / 2));
+  for (int r = 0; r < t.P; ++r) {
+    CHECK(cyc_invert(t.hs[r]));
+    t.hs[r]->cyc_version = t.hs[r]->lhs_version;
+  }
   return NX_OK;
 }
 
@@ -8600,6 +8774,7 @@ size_t xr_static_lds(int v);  // the exchange kernels' static LDS (below)
 // within the exchange's caps, one round of workgroups, the LDS
 bool xr_local(const nx_network* h) {
   return h->xr_ok && h->xr_linked && h->pc && h->pc_lds && h->fres_ok && h->pa.exact &&
+         h->n_cyc == 0 &&
          h->pc_jobs > 0 && h->pc_jobs <= h->n_cu && h->pa.n_coarse > 0 &&
          h->pa.n_coarse <= kCapCoarseLds && h->n_cut >= 0 && h->n_cut <= kCapCoarseLds &&
          h->top_nt > 0 && h->top_nt <= kTopThreads && h->pa.n_top_lvl <= kMaxTopLvl &&
@@ -8903,6 +9078,13 @@ int solve_direct(const Team& t, double rtol, int32_t* iters, double* relres,
   if (!multi && h->n_cyc > 0) {  // cycles: the correction of this matrix first
     CHECK(flush_assembly(h));
     if (h->cyc_version != h->lhs_version) CHECK(cyc_build(h));
+  } else if (multi && h->cyc_team && h->n_cyc > 0) {  // (several ranks: built together)
+    bool stale = false;
+    for (int r = 0; r < t.P; ++r) {
+      CHECK(flush_assembly(t.hs[r]));
+      stale = stale || t.hs[r]->cyc_version != t.hs[r]->lhs_version;
+    }
+    if (stale) CHECK(cyc_build_team(t));
   }
   // the deferred assembly heads the solve (every rank's, several ranks)
   bool with_asm = true;
@@ -9158,7 +9340,7 @@ int solve_lean(const Team& t, double rtol, int32_t maxit, int L, int32_t* iters,
 // one (a rank on the global-memory preconditioner kernels while another runs the LDS
 // kernels' linear form would pair different collectives). Each rank decides from its own
 // decomposition (LDS caps), so the ranks compare.
-constexpr int kSchedSig = 10;
+constexpr int kSchedSig = 11;
 bool direct_local(const nx_network* h);
 bool cut_mode(const nx_network* h);
 bool coarse_down(const nx_network* h);
@@ -9177,6 +9359,7 @@ void sched_sig(const nx_network* h, int* s) {
   // the direct solve's residual: halo of x + all-reduce of 2, or one all-reduce of 2 + K
   s[8] = cut_mode(h) ? 1 + h->n_cut : 0;
   s[9] = coarse_down(h) ? 1 : 0;  // the coarse step in the down sweeps or k_pc_coarse
+  s[10] = h->n_cyc;  // the cycle correction's all-reduces (nx_set_cycles_team)
 }
 
 int check_schedules(const Team& t) {
@@ -10354,7 +10537,10 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     h->d_crec = scratch(10 * std::max<int64_t>(n_chains, 1));
     h->d_ci = const_cast<int*>(up(nullptr, 4 * std::max<int64_t>(n_chains, 1)));
     const bool hdr_ok = h->d_job_hdr && h->d_crec && h->d_ci && fits;
-    h->dstep_ok = h->dstep_ok && hdr_ok && h->dstep_lds <= (size_t)kDirLdsMax;
+    // (N > 256, variants <64, 8> / <64, 16>: the lane state spills thousands of VGPRs -- the
+    // separate launches run those; no fused instantiation)
+    h->dstep_ok = h->dstep_ok && hdr_ok && h->dstep_lds <= (size_t)kDirLdsMax &&
+                  (N <= 32 || (variant != 8 && variant != 9));
     // (several ranks: the coarse exchange's static LDS comes on top; checked at launch)
     h->xr_ok = h->xr_ok && hdr_ok;
   }
@@ -10467,10 +10653,12 @@ NX_API int nx_set_pc_dense(nx_network_t* h, int32_t enable, int32_t n_jobs,
 namespace {
 void free_cycles(nx_network* h) {
   for (void* p : {(void*)h->d_cyc_rows, (void*)h->cyc_z, (void*)h->cyc_cinv, (void*)h->cyc_cap,
-                  (void*)h->cyc_prev, (void*)h->cyc_w})
+                  (void*)h->cyc_prev, (void*)h->cyc_w, (void*)h->d_cyc_qloc, (void*)h->d_cyc_lcol,
+                  (void*)h->cyc_u})
     if (p) (void)hipFree(p);
-  h->d_cyc_rows = nullptr;
-  h->cyc_z = h->cyc_cinv = h->cyc_cap = h->cyc_prev = h->cyc_w = nullptr;
+  h->d_cyc_rows = h->d_cyc_qloc = h->d_cyc_lcol = nullptr;
+  h->cyc_z = h->cyc_cinv = h->cyc_cap = h->cyc_prev = h->cyc_w = h->cyc_u = nullptr;
+  h->cyc_team = false;
   h->n_cyc = 0;
   h->cyc_version = -1;
 }
@@ -10504,6 +10692,49 @@ NX_API int nx_set_cycles(nx_network_t* h, int32_t n, const int32_t* rows) {
   // neither the fused residual nor the fused step run
   h->fres_ok = false;
   h->dstep_ok = false;
+  return NX_OK;
+}
+
+// Several ranks, a graph with cycles: this rank's share of the Woodbury correction. K: the
+// cycle chains of all ranks (one global order, the same on every rank); own[2K]: per column
+// of U (flux end, multiplier of pair k at 2k, 2k + 1) this rank's row or -1; qloc[K] /
+// lcol[K]: when pair k's chain is this rank's, its flux end row and the multiplier's column
+// in this rank's numbering (a ghost column when another rank owns the row), else -1.
+NX_API int nx_set_cycles_team(nx_network_t* h, int32_t K, const int32_t* own,
+                              const int32_t* qloc, const int32_t* lcol) {
+  CHECK(flush_assembly(h));
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (K < 0 || (K > 0 && (!own || !qloc || !lcol))) return fail(NX_ERR_ARG, "K >= 0 pairs");
+  if (K > 0 && !h->pc) return fail(NX_ERR_STATE, "nx_set_preconditioner(enable=1) must come first");
+  if (K > 0 && h->nranks < 2) return fail(NX_ERR_STATE, "one rank: nx_set_cycles");
+  if (K > kMaxCyc) return fail(NX_ERR_ARG, "more cycle chains than kMaxCyc (the solve runs MINRES)");
+  for (int64_t i = 0; i < 2 * (int64_t)K; ++i)
+    if (own[i] < -1 || own[i] >= h->n_own) return fail(NX_ERR_ARG, "cycle row out of range");
+  for (int k = 0; k < K; ++k)
+    if (qloc[k] < -1 || qloc[k] >= h->n_edge_dofs || lcol[k] < -1 || lcol[k] >= h->n_col ||
+        (qloc[k] >= 0) != (lcol[k] >= 0))
+      return fail(NX_ERR_ARG, "cycle chain row / column out of range");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  CHECK(drop_handle_graphs(h));
+  free_cycles(h);
+  h->sched_checked = false;
+  if (K == 0) return NX_OK;
+  const int m = 2 * K;
+  HIPCALL(hipMalloc((void**)&h->d_cyc_rows, sizeof(int) * m));
+  HIPCALL(hipMalloc((void**)&h->d_cyc_qloc, sizeof(int) * K));
+  HIPCALL(hipMalloc((void**)&h->d_cyc_lcol, sizeof(int) * K));
+  HIPCALL(hipMalloc((void**)&h->cyc_z, sizeof(double) * m * h->n_col));
+  HIPCALL(hipMalloc((void**)&h->cyc_cinv, sizeof(double) * m * m));
+  HIPCALL(hipMalloc((void**)&h->cyc_cap, sizeof(double) * (m * m + K)));
+  HIPCALL(hipMalloc((void**)&h->cyc_prev, sizeof(double) * m));
+  HIPCALL(hipMalloc((void**)&h->cyc_w, sizeof(double) * m));
+  HIPCALL(hipMalloc((void**)&h->cyc_u, sizeof(double) * m));
+  HIPCALL(hipMemcpy(h->d_cyc_rows, own, sizeof(int) * m, hipMemcpyHostToDevice));
+  HIPCALL(hipMemcpy(h->d_cyc_qloc, qloc, sizeof(int) * K, hipMemcpyHostToDevice));
+  HIPCALL(hipMemcpy(h->d_cyc_lcol, lcol, sizeof(int) * K, hipMemcpyHostToDevice));
+  h->n_cyc = K;
+  h->cyc_team = true;
   return NX_OK;
 }
 

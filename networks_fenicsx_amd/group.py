@@ -38,6 +38,7 @@ class RankGroup:
                                    comm=group.comm(r)) for r in range(nranks)]
         self.assemblers = [HydraulicNetworkAssembler(m) for m in self.meshes]
         self._agree_kernels()
+        self._team_cycles()
         self._group: _lib.Group | None = None
         self.iterations = 0
         self.relres = float("nan")
@@ -61,6 +62,7 @@ class RankGroup:
             a.set_preconditioner(enable)
         if enable:
             self._agree_kernels()
+            self._team_cycles()
 
     def _agree_kernels(self) -> None:
         """The ranks' sweep kernels (LDS or global memory, chosen per rank from its
@@ -77,6 +79,17 @@ class RankGroup:
             if on:
                 a.handle.set_pc_kernels(True)
                 a.handle.set_preconditioner(a.tree_preconditioner)
+
+    def _team_cycles(self) -> None:
+        """A graph with cycles: every rank's share of the direct solve's Woodbury correction
+        of all ranks' cycle chains (what HydraulicNetworkAssembler.set_preconditioner does
+        over a real communicator, here from every rank's pairs at once)."""
+        if self.nranks < 2:
+            return
+        pairs = [p for a in self.assemblers for p in a.cycle_pairs()]
+        for a in self.assemblers:
+            if a.preconditioned:
+                a.set_team_cycles(pairs)
 
     def set_direct(self, enable: bool) -> None:
         """The direct tree solve over all ranks (``nx_set_solver`` on every handle; it runs

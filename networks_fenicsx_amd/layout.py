@@ -28,7 +28,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-__all__ = ["LocalProblem", "dfs_edge_order", "partition_edges", "build_local_problem"]
+__all__ = ["LocalProblem", "dfs_edge_order", "partition_edges", "build_local_problem",
+           "global_row_ids", "team_cycle_tables"]
 
 
 def dfs_edge_order(src: np.ndarray, dst: np.ndarray, n_nodes: int) -> np.ndarray:
@@ -297,3 +298,42 @@ def _cut_lists(lp: LocalProblem, v, src, dst, is_bif, inc_node, inc_edge, owner,
     lp.gk_row = rows[o].astype(np.int32)
     lp.gk_coef = coefs[o].astype(np.float64)
     lp.gk_off = np.searchsorted(ks[o], np.arange(cut.size + 1)).astype(np.int32)
+
+
+def global_row_ids(lp: LocalProblem, n_edges_global: int, bif_index: np.ndarray) -> np.ndarray:
+    """The single-rank layout row of every owned row, then of every ghost column."""
+    per = 2 * lp.N + 1
+    rows = (np.asarray(lp.edges, dtype=np.int64)[:, None] * per + np.arange(per)[None, :]).ravel()
+    lam = n_edges_global * per + np.asarray(bif_index)[np.asarray(lp.lm_nodes, dtype=np.int64)]
+    return np.concatenate([rows, lam, np.asarray(lp.ghost_global, dtype=np.int64)])
+
+
+def cycle_pairs_global(lp: LocalProblem, cyc_rows: np.ndarray, n_edges_global: int,
+                       bif_index: np.ndarray) -> list:
+    """This rank's dropped cycle couplings (``TreePreconditioner.cyc_rows``: flux end row,
+    multiplier column) as single-rank layout rows."""
+    ids = global_row_ids(lp, n_edges_global, bif_index)
+    return [(int(ids[q]), int(ids[c])) for q, c in np.asarray(cyc_rows).reshape(-1, 2)]
+
+
+def team_cycle_tables(lp: LocalProblem, cyc_rows: np.ndarray, all_pairs, n_edges_global: int,
+                      bif_index: np.ndarray):
+    """``nx_set_cycles_team``'s arrays for this rank from every rank's cycle pairs (global
+    rows; one global order: sorted): ``(own[2K], qloc[K], lcol[K])`` -- per column of U this
+    rank's row or -1, and for this rank's own chains the flux end row and the multiplier's
+    column (owned or ghost) in its numbering."""
+    pairs = sorted({(int(a), int(b)) for a, b in all_pairs})
+    ids = global_row_ids(lp, n_edges_global, bif_index)
+    n_own = lp.n_own
+    order = np.argsort(ids[:n_own], kind="stable")
+
+    def owned(g: int) -> int:
+        i = np.searchsorted(ids[:n_own], g, sorter=order)
+        return int(order[i]) if i < n_own and ids[order[i]] == g else -1
+
+    mine = {(int(ids[q]), int(ids[c])): (int(q), int(c))
+            for q, c in np.asarray(cyc_rows).reshape(-1, 2)}
+    own = np.array([owned(g) for pr in pairs for g in pr], dtype=np.int32)
+    qloc = np.array([mine[pr][0] if pr in mine else -1 for pr in pairs], dtype=np.int32)
+    lcol = np.array([mine[pr][1] if pr in mine else -1 for pr in pairs], dtype=np.int32)
+    return own, qloc, lcol

@@ -265,9 +265,10 @@ class TreePreconditioner:
     # no chain closes a cycle (grounded at one end): P^{-1} is the exact block inverse, so
     # the direct tree solve (nx_set_solver) is exact
     tree_exact: bool = False
-    # one rank, graphs with cycles: per cycle-closing chain the coupling its grounded end
-    # drops, (flux end row, multiplier row) -- the system the tree solve inverts is A minus
-    # these symmetric +-1 pairs, and the direct solve corrects for them (nx_set_cycles)
+    # graphs with cycles: per cycle-closing chain the coupling its grounded end drops, (flux
+    # end row, multiplier column: a ghost column with several ranks when another rank owns
+    # the row) -- the system the tree solve inverts is A minus these symmetric +-1 pairs,
+    # and the direct solve corrects for them (nx_set_cycles, nx_set_cycles_team)
     cyc_rows: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.int32))
 
     @property
@@ -499,9 +500,11 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
     cyc = r & ja & jb  # closes a cycle: hang from the shallower end, ground the other
     up[cyc] = np.where(depth[es[cyc]] <= depth[ed[cyc]], es[cyc], ed[cyc])
     n_cycle += int(cyc.sum())
-    # the coupling a grounded cycle end drops: (flux end row, multiplier row) per chain; the
-    # tree solve inverts the system without them, the direct solve adds them back (Woodbury)
-    ce = np.flatnonzero(cyc)
+    # the coupling a grounded cycle end drops: (flux end row, multiplier column) per chain --
+    # a chain closing a cycle inside this rank, or a coarse chain closing a cycle of the
+    # coarse graph (several ranks; its multiplier may be a ghost column); the tree solve
+    # inverts the system without them, the direct solve adds them back (Woodbury)
+    ce = np.flatnonzero(cyc | dem)
     gnd = np.where(up[ce] == es[ce], ed[ce], es[ce])  # the grounded end's junction
     cyc_rows = np.stack([ce * (2 * N + 1) + np.where(gnd == es[ce], 0, 2 * N),
                          lam[gnd]], axis=1).astype(np.int32).reshape(-1, 2)
@@ -679,7 +682,7 @@ def build_tree_preconditioner(lp, src: np.ndarray, dst: np.ndarray, degree: np.n
         lvl_slot_off=np.asarray(lvl_slot_off, dtype=np.int32),
         top_lvl_off=np.asarray(top_lvl_off, dtype=np.int32), n_jobs=int(n_jobs),
         n_slots=int(n_slots), tree_exact=n_cycle == 0,
-        cyc_rows=cyc_rows if n_cycle == ce.size else np.zeros((0, 2), np.int32))
+        cyc_rows=cyc_rows)
     _dense_top_lists(pc)
     if balanced and n_lower > 0 and pc.job_need_off.size > 1 and \
             int(np.diff(pc.job_need_off).max()) > K_MAX_NEED:

@@ -49,6 +49,30 @@ def linear_graph(n: int, dim: int = 2, ordered=lambda _: True) -> nx.DiGraph:
     return G
 
 
+def lattice_graph(nx_: int, ny: int):
+    """An nx_ x ny grid of pipes (many cycles: (nx_-1)(ny-1) of them), inlet/outlet at two
+    corners through extra boundary edges -- an anastomosed network's worst case."""
+    import networkx as nx
+
+    G = nx.DiGraph()
+    idx = lambda i, j: i * ny + j  # noqa: E731
+    for i in range(nx_):
+        for j in range(ny):
+            G.add_node(idx(i, j), pos=np.array([float(i), float(j) + 0.1 * i, 0.0]))
+    n = nx_ * ny
+    G.add_node(n, pos=np.array([-1.0, 0.0, 0.0]))
+    G.add_node(n + 1, pos=np.array([float(nx_), float(ny - 1) + 0.1 * (nx_ - 1), 0.0]))
+    G.add_edge(n, idx(0, 0))
+    for i in range(nx_):
+        for j in range(ny):
+            if i + 1 < nx_:
+                G.add_edge(idx(i, j), idx(i + 1, j))
+            if j + 1 < ny:
+                G.add_edge(idx(i, j), idx(i, j + 1))
+    G.add_edge(idx(nx_ - 1, ny - 1), n + 1)
+    return G
+
+
 # name -> (graph factory, N, colour strategy, p_bc)
 CASES = {
     "Y_N4": (lambda: ng.make_tree(2, 1, 3), 4, None, p_y),
@@ -77,3 +101,8 @@ def graph_arrays(G):
     pos = np.asarray([G.nodes[v]["pos"] for v in G.nodes()], dtype=np.float64)
     edges = np.asarray(list(G.edges()), dtype=np.int64).reshape(-1, 2)
     return pos, edges
+
+# graphs with cycles (the direct solve's Woodbury correction), name -> (factory, N)
+CYCLIC = {"edge_info_N10": (edge_info_graph, 10),
+          "lattice4x5_N6": (lambda: lattice_graph(4, 5), 6),
+          "lattice6x6_N3": (lambda: lattice_graph(6, 6), 3)}

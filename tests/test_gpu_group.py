@@ -15,7 +15,7 @@ import pytest
 import scipy.sparse as sp
 
 import distributed_model as DM
-from cases import CASES
+from cases import CASES, CYCLIC, p_y
 from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh
 from networks_fenicsx_amd import network_generation as ng
 from networks_fenicsx_amd.group import RankGroup
@@ -448,7 +448,8 @@ def test_group_rehearsal_four_ranks_depth16():
 def test_group_direct_solve(case, P):
     """The direct tree solve across ranks (mode kModeDirect of the multi-rank sweeps, coarse
     all-reduce between the halves, halo of x, all-reduced true residual): the oracle's
-    direct solution to 1e-10; graphs with a cycle fall back to MINRES on every rank."""
+    direct solution to 1e-10; graphs with a cycle too, through every rank's share of the
+    Woodbury correction (nx_set_cycles_team)."""
     make, N, strategy, pbc = CASES[case]
     G, mesh, Ab, bb, x_ref = _reference(case)
     grp = RankGroup(G, N, P, color_strategy=strategy)
@@ -459,17 +460,17 @@ def test_group_direct_solve(case, P):
         it, relres, conv = grp.solve(1e-12, 50000, 4)
         assert conv, (it, relres)
         is_tree = mesh.num_edges == mesh.num_nodes - 1
-        assert grp.solver_used == ("direct" if is_tree else "minres")
-        if is_tree:
-            assert it in (1, 2) and relres <= 1e-12
+        assert grp.solver_used == "direct"
+        assert it in (1, 2) and relres <= 1e-12
         x = np.zeros(Ab.shape[0])
         for a, xl in zip(grp.assemblers, grp.solutions()):
             x[DM.global_rows(a.local_problem, mesh.num_edges, mesh.bifurcation_index)] = xl
         err = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
         assert err <= SOL_TOL, err
-        if is_tree:  # the reported residual (fused into the down sweeps) is the true one
-            true = np.linalg.norm(bb - Ab @ x) / np.linalg.norm(bb)
-            assert abs(relres - true) <= 0.05 * true + 5e-16, (relres, true)
+        # the reported residual (fused into the down sweeps; with cycles the CSR's after the
+        # correction) is the true one
+        true = np.linalg.norm(bb - Ab @ x) / np.linalg.norm(bb)
+        assert abs(relres - true) <= 0.05 * true + 5e-16, (relres, true, is_tree)
         # again: the captured graphs are reused and the result does not move
         grp.assemble()
         grp.solve(1e-12, 50000, 4)
@@ -658,5 +659,50 @@ def test_exchange_one_rank_gives_up_exchange1(separate):
             assert {a.handle.direct_path() for a in grp.assemblers} == {"launches"}, k
             x = _gathered(grp, Ab, mesh)
             assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL, k
+    finally:
+        grp.close()
+
+
+
+@pytest.mark.parametrize("case,P", [("edge_info_N10", 3), ("lattice4x5_N6", 2),
+                                    ("lattice4x5_N6", 3), ("lattice6x6_N3", 4)])
+def test_group_direct_solve_cycles(case, P):
+    """Graphs with cycles across ranks: cycle chains inside a rank and coarse chains closing a
+    cycle between ranks are grounded by the decomposition; every rank holds its share of Z =
+    A_g^{-1} U (2K team tree solves per assembled matrix) and the same capacitance inverse,
+    and each solve sums U^T x over the ranks and corrects x: the oracle's LU to 1e-10, the
+    reported residual the CSR's true one, the same bits on a second step, a new matrix (R
+    changed) rebuilds the correction."""
+    make, N = CYCLIC[case]
+    G = make()
+    mesh = NetworkMesh(G, N=N)
+    src, dst = mesh.edges
+    Pr = O.build_problem(mesh.node_coordinates, src, dst, N, mesh.edge_colors)
+    A, b = O.assemble_reference(Pr, p_y)
+    Ab, bb, perm, _ = O.to_build_layout(Pr, A, b)
+    x_ref = O.solve_reference(A, b)[perm]
+    grp = RankGroup(G, N, P)
+    try:
+        grp.compute_forms(p_bc_ex=p_y)
+        grp.set_direct(True)
+        grp.assemble()
+        it, rr, conv = grp.solve(1e-12, 50000, 4)
+        assert conv and grp.solver_used == "direct" and it in (1, 2), (it, rr)
+        x = _gathered(grp, Ab, mesh)
+        assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+        true = np.linalg.norm(bb - Ab @ x) / np.linalg.norm(bb)
+        assert abs(rr - true) <= 0.05 * true + 5e-16, (rr, true)
+        grp.assemble()
+        it2, rr2, _ = grp.solve(1e-12, 50000, 4)
+        np.testing.assert_array_equal(_gathered(grp, Ab, mesh), x)
+        # another matrix: R = 2 everywhere (the correction is rebuilt for it)
+        grp.compute_forms(p_bc_ex=p_y, R=2.0)
+        grp.assemble()
+        it3, rr3, conv3 = grp.solve(1e-12, 50000, 4)
+        assert conv3 and grp.solver_used == "direct"
+        A2, b2 = O.assemble_reference(Pr, p_y, R=2.0)
+        x2_ref = O.solve_reference(A2, b2)[perm]
+        x2 = _gathered(grp, Ab, mesh)
+        assert np.linalg.norm(x2 - x2_ref) / np.linalg.norm(x2_ref) <= SOL_TOL
     finally:
         grp.close()

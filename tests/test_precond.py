@@ -5,7 +5,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from cases import CASES
+from cases import CASES, lattice_graph
 from networks_fenicsx_amd import NetworkMesh
 from networks_fenicsx_amd import network_generation as ng
 from networks_fenicsx_amd.layout import build_local_problem
@@ -299,30 +299,6 @@ def test_forced_coarse_terminals_one_rank(case, n_term):
     assert np.linalg.norm(z - z1) <= 1e-12 * np.linalg.norm(z1)
 
 
-def lattice_graph(nx_: int, ny: int):
-    """An nx_ x ny grid of pipes (many cycles: (nx_-1)(ny-1) of them), inlet/outlet at two
-    corners through extra boundary edges -- an anastomosed network's worst case."""
-    import networkx as nx
-
-    G = nx.DiGraph()
-    idx = lambda i, j: i * ny + j  # noqa: E731
-    for i in range(nx_):
-        for j in range(ny):
-            G.add_node(idx(i, j), pos=np.array([float(i), float(j) + 0.1 * i, 0.0]))
-    n = nx_ * ny
-    G.add_node(n, pos=np.array([-1.0, 0.0, 0.0]))
-    G.add_node(n + 1, pos=np.array([float(nx_), float(ny - 1) + 0.1 * (nx_ - 1), 0.0]))
-    G.add_edge(n, idx(0, 0))
-    for i in range(nx_):
-        for j in range(ny):
-            if i + 1 < nx_:
-                G.add_edge(idx(i, j), idx(i + 1, j))
-            if j + 1 < ny:
-                G.add_edge(idx(i, j), idx(i, j + 1))
-    G.add_edge(idx(nx_ - 1, ny - 1), n + 1)
-    return G
-
-
 CYCLIC = {"edge_info_N10": (CASES["edge_info_N10"][0], 10),
           "lattice4x5_N6": (lambda: lattice_graph(4, 5), 6),
           "lattice6x6_N3": (lambda: lattice_graph(6, 6), 3)}
@@ -373,3 +349,117 @@ def test_cycle_rows_and_woodbury(case):
     x_ref = spla.spsolve(Ab.tocsc(), b)
     assert np.linalg.norm(x - x_ref) <= 1e-12 * np.linalg.norm(x_ref)
     assert mm == 2 * k
+
+
+@pytest.mark.parametrize("case,P", [("edge_info_N10", 2), ("edge_info_N10", 3),
+                                    ("lattice4x5_N6", 2), ("lattice4x5_N6", 3),
+                                    ("lattice6x6_N3", 4)])
+def test_multi_rank_cycle_rows_and_woodbury(case, P):
+    """Several ranks, graphs with cycles (nx_set_cycles_team): each rank's decomposition lists
+    the couplings its grounded chain ends drop -- chains closing a cycle inside the rank and
+    coarse chains closing a cycle of the coarse graph (their multiplier can be another rank's
+    row, a ghost column here). Without all ranks' pairs the system A_g is exactly what the
+    multi-rank direct solve inverts (each rank's sweeps, one sum of the coarse partials, the
+    coarse forest), and the rank-2k Woodbury correction recovers A^{-1} b to 1e-12."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+
+    import distributed_model as DM
+    from networks_fenicsx_amd.precond import lumped_mass, pc_finish_model, pc_up_model
+
+    make, N = CYCLIC[case]
+    m, Ab, lp1 = _problem(make(), N)
+    src, dst = m.edges
+    bif = m.bifurcation_index
+    dq_global = lumped_mass(Ab, lp1)
+    lps = [build_local_problem(m.node_coordinates, src, dst, m.degrees, N, r, P)
+           for r in range(P)]
+    pcs = [build_tree_preconditioner(lp, src, dst, m.degrees, target_jobs=16) for lp in lps]
+    rows = [DM.global_rows(lp, m.num_edges, bif) for lp in lps]
+    # every rank's dropped couplings in global numbering
+    pairs = []
+    for lp, pc, rw in zip(lps, pcs, rows):
+        for q, lam in pc.cyc_rows:
+            gl = rw[lam] if lam < lp.n_own else lp.ghost_global[lam - lp.n_own]
+            pairs.append((int(rw[q]), int(gl)))
+    k = m.num_edges - m.num_nodes + 1
+    assert len(pairs) == k, (len(pairs), k)
+    q = np.array([p[0] for p in pairs])
+    lam = np.array([p[1] for p in pairs])
+    Ad = Ab.toarray()
+    a = Ad[q, lam]
+    assert np.all(np.abs(a) == 1.0) and np.array_equal(a, Ad[lam, q])
+    Ag = Ad.copy()
+    Ag[q, lam] = 0.0
+    Ag[lam, q] = 0.0
+    Ags = sp.csr_matrix(Ag)
+
+    def apply_all(r):  # P^{-1} over the ranks: sweeps, the partials summed, coarse forest
+        sts = [pc_up_model(pc, lp, dq_global[lp.edges], r[rw])
+               for lp, pc, rw in zip(lps, pcs, rows)]
+        tot = sum(st["partial"] for st in sts)
+        z = np.zeros_like(r)
+        for lp, pc, rw, st in zip(lps, pcs, rows, sts):
+            z[rw] = pc_finish_model(pc, lp, dq_global[lp.edges], st, tot)
+        return z
+
+    per = 2 * N + 1
+    rid = np.arange(Ab.shape[0])
+    flux = (rid < m.num_edges * per) & (rid % per % 2 == 0)
+
+    def direct_multi(b):
+        y = apply_all(np.where(flux, b, 0.0))
+        w = np.where(flux, 0.0, Ags @ np.where(flux, y, 0.0) - b)
+        xs = apply_all(w)
+        t = np.where(flux, b - Ags @ np.where(flux, 0.0, xs), 0.0)
+        return np.where(flux, apply_all(t), xs)
+
+    b = np.random.default_rng(5).standard_normal(Ab.shape[0])
+    xg = direct_multi(b)
+    xg_ref = spla.spsolve(Ags.tocsc(), b)
+    assert np.linalg.norm(xg - xg_ref) <= 1e-11 * np.linalg.norm(xg_ref)
+    U = np.stack([q, lam], axis=1).reshape(-1)
+    Z = np.stack([direct_multi(np.eye(Ab.shape[0])[r]) for r in U], axis=1)
+    cap = Z[U]
+    for i in range(k):
+        cap[2 * i, 2 * i + 1] += 1.0 / a[i]
+        cap[2 * i + 1, 2 * i] += 1.0 / a[i]
+    x = xg - Z @ np.linalg.solve(cap, xg[U])
+    x_ref = spla.spsolve(Ab.tocsc(), b)
+    assert np.linalg.norm(x - x_ref) <= 1e-12 * np.linalg.norm(x_ref)
+
+
+@pytest.mark.parametrize("case,P", [("edge_info_N10", 2), ("lattice4x5_N6", 3),
+                                    ("lattice6x6_N3", 4)])
+def test_team_cycle_tables(case, P):
+    """nx_set_cycles_team's per-rank arrays (layout.team_cycle_tables): every column of U has
+    exactly one owning rank whose row is that global row; every pair's chain -- its flux end
+    row and multiplier column, in that rank's numbering -- is on exactly one rank."""
+    from networks_fenicsx_amd.layout import cycle_pairs_global, global_row_ids, team_cycle_tables
+
+    make, N = CYCLIC[case]
+    m, Ab, lp1 = _problem(make(), N)
+    src, dst = m.edges
+    bif = m.bifurcation_index
+    lps = [build_local_problem(m.node_coordinates, src, dst, m.degrees, N, r, P)
+           for r in range(P)]
+    pcs = [build_tree_preconditioner(lp, src, dst, m.degrees, target_jobs=16) for lp in lps]
+    pairs = [p for lp, pc in zip(lps, pcs)
+             for p in cycle_pairs_global(lp, pc.cyc_rows, m.num_edges, bif)]
+    K = len(pairs)
+    assert K == m.num_edges - m.num_nodes + 1
+    order = sorted(pairs)
+    tabs = [team_cycle_tables(lp, pc.cyc_rows, pairs, m.num_edges, bif)
+            for lp, pc in zip(lps, pcs)]
+    for i in range(2 * K):
+        g = order[i // 2][i % 2]
+        owners = [r for r, t in enumerate(tabs) if t[0][i] >= 0]
+        assert len(owners) == 1, (i, owners)
+        r = owners[0]
+        assert global_row_ids(lps[r], m.num_edges, bif)[tabs[r][0][i]] == g
+    for k in range(K):
+        holders = [r for r, t in enumerate(tabs) if t[1][k] >= 0]
+        assert len(holders) == 1, (k, holders)
+        r = holders[0]
+        ids = global_row_ids(lps[r], m.num_edges, bif)
+        assert (ids[tabs[r][1][k]], ids[tabs[r][2][k]]) == order[k]
