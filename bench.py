@@ -15,7 +15,7 @@ Workload (p_bc = y, f = 0, R = 1, ``color_strategy="smallest_last"
   the configuration the metric is quoted on);
 * P = 2^k GPUs: ``make_tree(15+k, 15+k, 15+k)``, N = 15 -- one tree generation per GPU
   doubling, the same N as on one GPU, so every GPU carries the one-GPU load (weak scaling,
-  ~1.03 M rows per GPU; 8 GPUs: 8,257,536 DoF). ``--N 19`` gives SURVEY's C4 at 8 GPUs
+  ~1.03 M rows per GPU; 8 GPUs: 8,257,504 DoF). ``--N 19`` gives SURVEY's C4 at 8 GPUs
   (``make_tree(18,18,18)``, N = 19, 10,354,648 DoF, configs[4]). Rank 0 also times the SAME
   workload on its GPU alone (``strong_scaling``), so T1 / TP is measured in the same run.
 

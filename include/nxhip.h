@@ -303,6 +303,32 @@ int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64_t n_lm
                      const int32_t* l_fe, const int32_t* l_aux, const double* cst, double ab);
 
 /*
+ * Continuous pressure (pressure_degree m >= 1, flux_degree k > m; assembly.py:121-146), one
+ * rank, a forest: the direct solve by condensation onto the graph nodes, replacing MUMPS'
+ * LU (solver.py:58-65) for these pairs. Each edge's own unknowns (its kN+1 flux nodes and
+ * mN-1 interior pressure nodes) are eliminated onto its border: the pressure at its two end
+ * nodes (shared with the other edges there) and the multipliers of the bifurcations at its
+ * ends. Per cell the interior nodes condense onto the vertices by exact reference blocks
+ * scaled by s = R h (layout: element.condensed_cell_blocks); per edge the vertices (q, p)
+ * are eliminated along it (one thread per edge); the border system over the graph nodes
+ * (negative definite, 2 unknowns per node) is eliminated leaf to root by one workgroup;
+ * then every edge back-substitutes. The true residual comes from the CSR, with up to two
+ * refinement passes; nx_get_direct_path reports 4.
+ *   nI = (k-1)+(m-1); cst = Kh (16) | Ch (4 nI) | Eh (4 nI) | Fh (nI nI); tI[nI] (+1 flux,
+ *   -1 pressure interior node); n_nodes border nodes, nrow[2n] (pressure row, multiplier row
+ *   or -1); eb[4E] (source node, target node, the q_0 - lam_source and q_N - lam_target
+ *   couplings: 0 or +-1); the node forest: n_lev levels (lev_off, order), every node's
+ *   (edge, end) incidences (inc_off, inc), parent[3n] (parent node, edge, this node's end of
+ *   it; -1 at a root), children (child_off, child), nown[n] (the edge that writes the node's
+ *   rows). k = 0 detaches it. Built by layout_fe.build_cp_tables.
+ */
+int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const double* cst,
+                 const int32_t* tI, int64_t n_nodes, const int32_t* nrow, const int32_t* eb,
+                 int32_t n_lev, const int32_t* lev_off, const int32_t* order,
+                 const int32_t* inc_off, const int32_t* inc, const int32_t* parent,
+                 const int32_t* child_off, const int32_t* child, const int32_t* nown);
+
+/*
  * Process-wide solve mode. 1 (default): with the preconditioner a solve is ONE HIP graph
  * launch -- start application, per-solve coefficients and the first iterations (also with
  * several ranks, RCCL or group, when beta^2 travels point-to-point) -- whose last k_mr_a
@@ -405,7 +431,8 @@ int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left);
  * 0 for the separate launches (assembly, up sweep, down sweep, publish). Replaces nothing
  * in the reference (PETSc's KSPSolve is one call: solver.py:127). */
 int nx_get_direct_path(nx_network_t* h, int32_t* path);
-/* (path 2: the (k, 0) condensed route of nx_fe_set_direct; path 3: several ranks, the
+/* (path 2: the (k, 0) condensed route of nx_fe_set_direct; path 4: the continuous-pressure
+ * node-condensed route of nx_fe_set_cp; path 3: several ranks, the
  * exchange step k_dir_xr / k_dir_xg, one launch per rank.)
  * Test hook: the number of s_sleep-paced polls a k_dir_step workgroup spends waiting for the
  * top part's values before it gives up (default 2^20). 0 makes every waiting workgroup give

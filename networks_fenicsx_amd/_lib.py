@@ -100,6 +100,8 @@ _SIGS = {
     "nx_set_cell_mass": (C.c_int, [_h, _f64, _f64]),
     "nx_fe_set_direct": (C.c_int, [_h, _h, _i32, _i64, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                    _pi32, _pi32, _pd, _f64]),
+    "nx_fe_set_cp": (C.c_int, [_h, _i32, _i32, _i32, _pd, _pi32, _i64, _pi32, _pi32, _i32,
+                               _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32]),
     "nx_get_solver": (C.c_int, [_h, _pi32, _pi32]),
     "nx_set_lean": (C.c_int, [_i32]),
     "nx_group_create": (C.c_int, [_i32, C.POINTER(_h), C.POINTER(_h)]),
@@ -398,7 +400,8 @@ class Handle:
         route through the auxiliary P1/DG0 handle)."""
         v = C.c_int32(0)
         check(lib().nx_get_direct_path(self.ptr, C.byref(v)))
-        return {1: "fused", 2: "condensed", 3: "exchange"}.get(v.value, "launches")
+        return {1: "fused", 2: "condensed", 3: "exchange", 4: "node-condensed"}.get(v.value,
+                                                                                  "launches")
 
     def xr_rehearse(self, rtol: float = 1e-12, reps: int = 20) -> float:
         """Rehearsal hook (``nx_debug_xr_rehearse``): ms per launch of this group member's
@@ -501,6 +504,26 @@ class Handle:
         arrs = [a if a.size else np.zeros(1, np.int32) for a in arrs]
         self._cyc_team_keep = arrs
         check(lib().nx_set_cycles_team(self.ptr, K, *[_ptr(a, C.c_int32) for a in arrs]))
+
+    def fe_set_cp(self, tab) -> None:
+        """``nx_fe_set_cp``: the continuous-pressure direct solve's tables
+        (``layout_fe.build_cp_tables``); ``None`` detaches it."""
+        if tab is None:
+            z = np.zeros(1, np.int32)
+            check(lib().nx_fe_set_cp(self.ptr, 0, 0, 0, None, None, 0, *([_ptr(z, C.c_int32)] * 2),
+                                     0, *([_ptr(z, C.c_int32)] * 8)))
+            return
+        i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+        arrs = [i32(x) if x.size else np.zeros(1, np.int32) for x in (
+            tab.tI, tab.nrow, tab.eb, tab.lev_off, tab.order, tab.inc_off, tab.inc, tab.parent,
+            tab.child_off, tab.child, tab.nown)]
+        cst = np.ascontiguousarray(tab.cst, dtype=np.float64)
+        self._cp_keep = (arrs, cst)
+        p = [_ptr(a, C.c_int32) for a in arrs]
+        check(lib().nx_fe_set_cp(self.ptr, int(tab.k), int(tab.m), int(tab.nI),
+                                 _ptr(cst, C.c_double), p[0], int(tab.n_nodes), p[1], p[2],
+                                 int(tab.lev_off.size - 1), p[3], p[4], p[5], p[6], p[7], p[8],
+                                 p[9], p[10]))
 
     def set_pc_exact(self, enable: bool) -> None:
         """Consistent (exact Schur complement, default) or lumped flux mass in P."""

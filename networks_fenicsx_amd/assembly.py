@@ -38,7 +38,7 @@ from .fem import Constant, Function, FunctionSpace
 from .element import condensed_flux_mass, stable_pair
 from .layout import (LocalProblem, build_local_problem, cycle_pairs_global,
                      team_cycle_tables)
-from .layout_fe import FeLayout, build_fe_aux_maps, build_fe_layout
+from .layout_fe import FeLayout, build_cp_tables, build_fe_aux_maps, build_fe_layout
 from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
@@ -333,8 +333,16 @@ class HydraulicNetworkAssembler:
         self._lm_idx = fe.lm_rows
         self._set_output_map()
         self._fe_aux = None
+        self._fe_cp = None
         if m == 0 and mesh.N <= 1024 and np.any(np.asarray(mesh.degrees) > 1):
             self._init_fe_direct(src, dst)
+        elif m >= 1:
+            # continuous pressure on a forest: the direct solve by condensation onto the graph
+            # nodes (nx_fe_set_cp); a graph with cycles runs MINRES
+            tab = build_cp_tables(fe, src, dst)
+            if tab is not None:
+                self._handle.fe_set_cp(tab)
+                self._fe_cp = tab
 
     def _init_fe_direct(self, src, dst) -> None:
         """(k, 0): the direct solve through the condensed P1/DG0 system (``nx_fe_set_direct``).
@@ -367,9 +375,11 @@ class HydraulicNetworkAssembler:
 
     @property
     def fe_direct_available(self) -> bool:
-        """A general-degree (k, 0) assembler whose direct solve runs through the condensed
-        P1/DG0 system (forest graphs)."""
-        return getattr(self, "_fe_aux", None) is not None
+        """A general-degree assembler with a direct solve: (k, 0) through the condensed P1/DG0
+        system, continuous pressure (k > m >= 1) by condensation onto the graph nodes (forest
+        graphs)."""
+        return (getattr(self, "_fe_aux", None) is not None
+                or getattr(self, "_fe_cp", None) is not None)
 
     def _init_comm(self) -> None:
         comm = self._network_mesh.comm

@@ -6509,6 +6509,16 @@ struct nx_network {
   // an auxiliary handle: its cell mass is a condensed one (nx_set_cell_mass), so its own CSR
   // is not the system the sweeps invert -- no residual check of its own
   bool cond_mass = false;
+  // continuous pressure (k > m >= 1) on a forest: the node-condensed direct solve
+  // (nx_fe_set_cp): reference blocks, per edge its border nodes, per border node its rows,
+  // the node tree (levels, edges, parent, children), scratch (factors, Se | ge, node values)
+  bool fe_cp = false;
+  int cp_k = 0, cp_m = 0, cp_nI = 0, cp_nn = 0, cp_nlev = 0;
+  double *cp_cst = nullptr, *cp_fac = nullptr, *cp_se = nullptr, *cp_xn = nullptr;
+  double *cp_Pinv = nullptr, *cp_hv = nullptr;
+  int *cp_tI = nullptr, *cp_eb = nullptr, *cp_nrow = nullptr, *cp_lev_off = nullptr;
+  int *cp_order = nullptr, *cp_inc_off = nullptr, *cp_inc = nullptr, *cp_parent = nullptr;
+  int *cp_child_off = nullptr, *cp_child = nullptr, *cp_nown = nullptr;
 };
 
 struct nx_group {
@@ -7635,6 +7645,309 @@ __global__ __launch_bounds__(kBlock) void k_fe_expand(FeCond c, const double* __
   if (dst >= 0) x[dst] = accum ? x[dst] + v : v;
 }
 
+// ---- continuous pressure (k > m >= 1) on a forest: the node-condensed direct solve -------
+// (nx_fe_set_cp). Each edge's own unknowns -- its flux nodes and its interior pressure nodes
+// -- are eliminated onto its border (p_u, lam_u, p_v, lam_v: the pressure at its end nodes,
+// shared with the other edges there, and the multipliers of the bifurcations at its ends).
+// Per edge, one thread: every cell's interior nodes condensed onto its two vertices by the
+// exact reference blocks (element.condensed_cell_blocks, scaled by s = R h), then the vertices
+// (q_i, p_i) eliminated in order along the edge (2 x 2 pivots; the leading blocks of this
+// 1-D mixed system are nonsingular) carrying the border columns: the edge's 4 x 4 border
+// block Se and rhs ge. The border system over the graph nodes (2 unknowns each: p and lam, lam
+// an identity dummy where the node has none) is negative definite and tree-structured: one
+// workgroup eliminates it leaf to root by levels and back-substitutes root to leaf. Then each
+// edge back-substitutes its vertices and its cells' interiors.
+struct CpArgs {
+  int N, k, m, nI;
+  int64_t E;
+  const double* edge_R;
+  const double* cellh;
+  const double* cst;  // Kh (16) | Ch (4 nI) | Eh (4 nI) | Fh (nI nI)
+  const int* tI;      // nI: +1 flux, -1 pressure (interior node types)
+  const int* eb;      // per edge: u, v (border node indices), au, av (lam couplings: 0, +-1)
+  const int* nrow;    // per border node: its pressure row, its multiplier row (or -1)
+  double* fac;        // per edge, per vertex (N + 1): Pi 4 | C 4 | W 8 | rho 2
+  double* se;         // per edge: Se 16 | ge 4
+  double* xn;         // per border node: its (p, lam) values
+};
+constexpr int kCpFac = 18;
+
+__device__ __forceinline__ double cp_pow(double s, int ex) {  // s^ex, ex in {-1, 0, 1}
+  return ex > 0 ? s : ex < 0 ? 1.0 / s : 1.0;
+}
+__device__ __forceinline__ void inv2(const double* P, double* Pi) {
+  const double det = P[0] * P[3] - P[1] * P[2];
+  const double id = 1.0 / det;
+  Pi[0] = P[3] * id;
+  Pi[1] = -P[1] * id;
+  Pi[2] = -P[2] * id;
+  Pi[3] = P[0] * id;
+}
+
+// The forward sweep of one edge (one thread): Se, ge and the per-vertex factors.
+__global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restrict__ b) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.E) return;
+  const int N = a.N, k = a.k, m = a.m, nI = a.nI;
+  const int nf = k * N + 1;
+  const int64_t base = e * (int64_t)(nf + m * N - 1);
+  const double* Kh = a.cst;
+  const double* Ch = a.cst + 16;
+  const int au = a.eb[4 * e + 2], av = a.eb[4 * e + 3];
+  const double R = a.edge_R[e];
+  double* fe = a.fac + e * (int64_t)(N + 1) * kCpFac;
+  auto prow = [&](int j) { return base + nf + j - 1; };  // interior pressure position j
+  double P[4] = {0.0, 0.0, 0.0, 1.0}, W[8] = {0.0}, rho[2] = {b[base], 0.0};
+  W[1] = (double)au;  // q_0 <-> lam_u
+  double Sb[16] = {0.0}, gb[4] = {0.0};
+  const int tV[4] = {1, -1, 1, -1};
+  for (int c = 0; c < N; ++c) {
+    const double s = R * a.cellh[e * N + c];
+    double K[16];
+    for (int r = 0; r < 4; ++r)
+      for (int q = 0; q < 4; ++q) K[4 * r + q] = Kh[4 * r + q] * cp_pow(s, (tV[r] + tV[q]) / 2);
+    double rV[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < nI; ++i) {  // the cell's interior rhs condensed onto its vertices
+      const int ti = a.tI[i];
+      const double bi = ti > 0 ? b[base + c * k + 1 + i] : b[prow(c * m + 1 + (i - (k - 1)))];
+      for (int r = 0; r < 4; ++r) rV[r] -= Ch[r * nI + i] * cp_pow(s, (tV[r] - ti) / 2) * bi;
+    }
+    double C[4];  // left vertex rows (q, p) x right vertex columns (q, p)
+    double Pn[4], Wn[8] = {0.0}, rn[2];
+    if (c == 0) {  // the left p is the border p_u
+      P[0] += K[0];
+      W[0] += K[1];
+      Sb[0] += K[5];
+      rho[0] += rV[0];
+      gb[0] += rV[1];
+      C[0] = K[2]; C[1] = K[3]; C[2] = 0.0; C[3] = 0.0;
+      Wn[0] = K[9];   // right q <-> p_u
+      Wn[4] = K[13];  // right p <-> p_u
+    } else {
+      P[0] += K[0]; P[1] += K[1]; P[2] += K[4]; P[3] += K[5];
+      rho[0] += rV[0];
+      rho[1] += rV[1];
+      C[0] = K[2]; C[1] = K[3]; C[2] = K[6]; C[3] = K[7];
+    }
+    if (c + 1 < N) {
+      Pn[0] = K[10]; Pn[1] = K[11]; Pn[2] = K[14]; Pn[3] = K[15];
+      rn[0] = rV[2] + b[base + (int64_t)k * (c + 1)];
+      rn[1] = rV[3] + b[prow(m * (c + 1))];
+    } else {  // the right p is the border p_v
+      Sb[10] += K[15];
+      gb[2] += rV[3];
+      if (c == 0) {  // (N = 1: p_u <-> p_v)
+        Sb[2] += K[7];
+        Sb[8] += K[13];
+      }
+      Wn[2] += K[11];  // right q <-> p_v
+      Wn[3] = (double)av;  // right q <-> lam_v
+      Wn[4] = 0.0;  // (the right p slot is a dummy)
+      W[2] += C[1];  // left rows <-> p_v
+      W[6] += C[3];
+      C[1] = 0.0;
+      C[3] = 0.0;
+      Pn[0] = K[10]; Pn[1] = 0.0; Pn[2] = 0.0; Pn[3] = 1.0;
+      rn[0] = rV[2] + b[base + nf - 1];
+      rn[1] = 0.0;
+    }
+    double Pi[4];
+    inv2(P, Pi);
+    // X = Pi C (2 x 2), Y = Pi W (2 x 4), z = Pi rho
+    double X[4], Y[8], z[2];
+    for (int r = 0; r < 2; ++r) {
+      for (int q = 0; q < 2; ++q) X[2 * r + q] = Pi[2 * r] * C[q] + Pi[2 * r + 1] * C[2 + q];
+      for (int q = 0; q < 4; ++q) Y[4 * r + q] = Pi[2 * r] * W[q] + Pi[2 * r + 1] * W[4 + q];
+      z[r] = Pi[2 * r] * rho[0] + Pi[2 * r + 1] * rho[1];
+    }
+    for (int r = 0; r < 2; ++r) {  // C^T X, C^T Y, C^T z into the right vertex
+      for (int q = 0; q < 2; ++q) Pn[2 * r + q] -= C[r] * X[q] + C[2 + r] * X[2 + q];
+      for (int q = 0; q < 4; ++q) Wn[4 * r + q] -= C[r] * Y[q] + C[2 + r] * Y[4 + q];
+      rn[r] -= C[r] * z[0] + C[2 + r] * z[1];
+    }
+    for (int r = 0; r < 4; ++r) {  // W^T Y, W^T z into the border
+      for (int q = 0; q < 4; ++q) Sb[4 * r + q] -= W[r] * Y[q] + W[4 + r] * Y[4 + q];
+      gb[r] -= W[r] * z[0] + W[4 + r] * z[1];
+    }
+    double* f = fe + (int64_t)c * kCpFac;
+    for (int i = 0; i < 4; ++i) f[i] = Pi[i];
+    for (int i = 0; i < 4; ++i) f[4 + i] = C[i];
+    for (int i = 0; i < 8; ++i) f[8 + i] = W[i];
+    f[16] = rho[0];
+    f[17] = rho[1];
+    for (int i = 0; i < 4; ++i) P[i] = Pn[i];
+    for (int i = 0; i < 8; ++i) W[i] = Wn[i];
+    rho[0] = rn[0];
+    rho[1] = rn[1];
+  }
+  {  // the last vertex
+    double Pi[4];
+    inv2(P, Pi);
+    double Y[8], z[2];
+    for (int r = 0; r < 2; ++r) {
+      for (int q = 0; q < 4; ++q) Y[4 * r + q] = Pi[2 * r] * W[q] + Pi[2 * r + 1] * W[4 + q];
+      z[r] = Pi[2 * r] * rho[0] + Pi[2 * r + 1] * rho[1];
+    }
+    for (int r = 0; r < 4; ++r) {
+      for (int q = 0; q < 4; ++q) Sb[4 * r + q] -= W[r] * Y[q] + W[4 + r] * Y[4 + q];
+      gb[r] -= W[r] * z[0] + W[4 + r] * z[1];
+    }
+    double* f = fe + (int64_t)N * kCpFac;
+    for (int i = 0; i < 4; ++i) f[i] = Pi[i];
+    for (int i = 0; i < 4; ++i) f[4 + i] = 0.0;
+    for (int i = 0; i < 8; ++i) f[8 + i] = W[i];
+    f[16] = rho[0];
+    f[17] = rho[1];
+  }
+  double* o = a.se + e * 20;
+  for (int i = 0; i < 16; ++i) o[i] = Sb[i];
+  for (int i = 0; i < 4; ++i) o[16 + i] = gb[i];
+}
+
+// The border system over the graph nodes by one workgroup: each node's 2 x 2 block D and rhs
+// from its edges (the node's half of their Se / ge) and b at its rows; leaf to root by levels
+// P_n = D_n - sum_children B_c^T P_c^-1 B_c (B_c: the child's block of its parent edge, child
+// rows x parent columns), then root to leaf x_n = P_n^-1 (h_n - B_n x_parent). Every sum in
+// a fixed order (the node's edges / children in list order).
+struct CpTree {
+  int nn, nlev;
+  const int* lev_off;    // nlev + 1: nodes by level, level 0 the roots
+  const int* order;      // nodes in level order
+  const int* inc_off;    // per node its edges: (edge, end) with end 0 = source, 1 = target
+  const int* inc;        // 2 per entry
+  const int* parent;     // per node: parent node, the edge to it and this node's end there
+  const int* child_off;
+  const int* child;
+  double* Pinv;  // 4 per node
+  double* hv;    // 2 per node
+};
+__device__ __forceinline__ void cp_block(const double* se, int e, int ra, int cb, double* B) {
+  const double* S = se + 20 * (int64_t)e;  // rows of end ra, columns of end cb (2 x 2)
+  B[0] = S[4 * (2 * ra) + 2 * cb];
+  B[1] = S[4 * (2 * ra) + 2 * cb + 1];
+  B[2] = S[4 * (2 * ra + 1) + 2 * cb];
+  B[3] = S[4 * (2 * ra + 1) + 2 * cb + 1];
+}
+__global__ __launch_bounds__(1024) void k_cp_nodes(CpArgs a, CpTree t, const double* __restrict__ b) {
+  for (int L = t.nlev - 1; L >= 0; --L) {
+    for (int i = t.lev_off[L] + threadIdx.x; i < t.lev_off[L + 1]; i += 1024) {
+      const int n = t.order[i];
+      double D[4] = {0.0, 0.0, 0.0, 0.0}, g[2];
+      const int pr = a.nrow[2 * n], lr = a.nrow[2 * n + 1];
+      g[0] = b[pr];
+      g[1] = lr >= 0 ? b[lr] : 0.0;
+      for (int j = t.inc_off[n]; j < t.inc_off[n + 1]; ++j) {
+        const int e = t.inc[2 * j], end = t.inc[2 * j + 1];
+        double B[4];
+        cp_block(a.se, e, end, end, B);
+        for (int q = 0; q < 4; ++q) D[q] += B[q];
+        g[0] += a.se[20 * (int64_t)e + 16 + 2 * end];
+        g[1] += a.se[20 * (int64_t)e + 17 + 2 * end];
+      }
+      if (lr < 0) D[3] = 1.0;  // (no multiplier: a decoupled dummy)
+      for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j) {
+        const int c = t.child[j];
+        const int ce = t.parent[3 * c + 1], cend = t.parent[3 * c + 2];
+        double B[4];  // child rows x this node's columns
+        cp_block(a.se, ce, cend, 1 - cend, B);
+        const double* Pc = t.Pinv + 4 * (int64_t)c;
+        const double* hc = t.hv + 2 * (int64_t)c;
+        double X[4], z[2];  // Pc B, Pc h
+        for (int r = 0; r < 2; ++r) {
+          for (int q = 0; q < 2; ++q) X[2 * r + q] = Pc[2 * r] * B[q] + Pc[2 * r + 1] * B[2 + q];
+          z[r] = Pc[2 * r] * hc[0] + Pc[2 * r + 1] * hc[1];
+        }
+        for (int r = 0; r < 2; ++r) {
+          for (int q = 0; q < 2; ++q) D[2 * r + q] -= B[r] * X[q] + B[2 + r] * X[2 + q];
+          g[r] -= B[r] * z[0] + B[2 + r] * z[1];
+        }
+      }
+      inv2(D, t.Pinv + 4 * (int64_t)n);
+      t.hv[2 * n] = g[0];
+      t.hv[2 * n + 1] = g[1];
+    }
+    __syncthreads();
+  }
+  for (int L = 0; L < t.nlev; ++L) {
+    for (int i = t.lev_off[L] + threadIdx.x; i < t.lev_off[L + 1]; i += 1024) {
+      const int n = t.order[i];
+      const int p = t.parent[3 * n];
+      double r[2] = {t.hv[2 * n], t.hv[2 * n + 1]};
+      if (p >= 0) {
+        double B[4];
+        cp_block(a.se, t.parent[3 * n + 1], t.parent[3 * n + 2], 1 - t.parent[3 * n + 2], B);
+        const double* xp = a.xn + 2 * (int64_t)p;
+        r[0] -= B[0] * xp[0] + B[1] * xp[1];
+        r[1] -= B[2] * xp[0] + B[3] * xp[1];
+      }
+      const double* Pn = t.Pinv + 4 * (int64_t)n;
+      a.xn[2 * n] = Pn[0] * r[0] + Pn[1] * r[1];
+      a.xn[2 * n + 1] = Pn[2] * r[0] + Pn[3] * r[1];
+    }
+    __syncthreads();
+  }
+}
+
+// Back-substitution of one edge (one thread): its vertices from the border values, then every
+// cell's interior nodes; x written (accum: added -- a refinement pass), the node rows too by
+// the edges whose source they are (or, for a node no edge leaves, its first edge in).
+__global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restrict__ b,
+                                                 double* __restrict__ x, const int* __restrict__ nown,
+                                                 int accum) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.E) return;
+  const int N = a.N, k = a.k, m = a.m, nI = a.nI;
+  const int nf = k * N + 1;
+  const int64_t base = e * (int64_t)(nf + m * N - 1);
+  const int u = a.eb[4 * e], v = a.eb[4 * e + 1];
+  const double xb[4] = {a.xn[2 * u], a.xn[2 * u + 1], a.xn[2 * v], a.xn[2 * v + 1]};
+  const double* fe = a.fac + e * (int64_t)(N + 1) * kCpFac;
+  const double* Eh = a.cst + 16 + 4 * nI;
+  const double* Fh = Eh + 4 * nI;
+  const double R = a.edge_R[e];
+  auto put = [&](int64_t r, double val) { x[r] = accum ? x[r] + val : val; };
+  auto prow = [&](int j) { return base + nf + j - 1; };
+  double yn[2] = {0.0, 0.0};  // the next vertex's (q, p)
+  const int tV[4] = {1, -1, 1, -1};
+  for (int i = N; i >= 0; --i) {
+    const double* f = fe + (int64_t)i * kCpFac;
+    double r[2] = {f[16], f[17]};
+    for (int q = 0; q < 4; ++q) {
+      r[0] -= f[8 + q] * xb[q];
+      r[1] -= f[12 + q] * xb[q];
+    }
+    r[0] -= f[4] * yn[0] + f[5] * yn[1];
+    r[1] -= f[6] * yn[0] + f[7] * yn[1];
+    const double y0 = f[0] * r[0] + f[1] * r[1], y1 = f[2] * r[0] + f[3] * r[1];
+    put(base + (int64_t)k * i, y0);
+    if (i > 0 && i < N) put(prow(m * i), y1);
+    if (i < N) {  // cell i: its interior nodes from (q_i, p_i, q_{i+1}, p_{i+1})
+      const double s = R * a.cellh[e * N + i];
+      const double xv[4] = {y0, i == 0 ? xb[0] : y1, yn[0], i + 1 == N ? xb[2] : yn[1]};
+      for (int j = 0; j < nI; ++j) {
+        const int tj = a.tI[j];
+        double val = 0.0;
+        for (int l = 0; l < nI; ++l) {
+          const int tl = a.tI[l];
+          const double bl = tl > 0 ? b[base + i * k + 1 + l] : b[prow(i * m + 1 + (l - (k - 1)))];
+          val += Fh[j * nI + l] * cp_pow(s, -(tj + tl) / 2) * bl;
+        }
+        for (int q = 0; q < 4; ++q) val -= Eh[j * 4 + q] * cp_pow(s, (-tj + tV[q]) / 2) * xv[q];
+        put(tj > 0 ? base + i * k + 1 + j : prow(i * m + 1 + (j - (k - 1))), val);
+      }
+    }
+    yn[0] = y0;
+    yn[1] = y1;
+  }
+  // the border rows: node values written once (the node's designated edge, nown)
+  for (int end = 0; end < 2; ++end) {
+    const int n = end ? v : u;
+    if (nown[n] != e) continue;
+    put(a.nrow[2 * n], a.xn[2 * n]);
+    if (a.nrow[2 * n + 1] >= 0) put(a.nrow[2 * n + 1], a.xn[2 * n + 1]);
+  }
+}
+
 // (k, 0), first pass, fused: expand + the true residual in one launch (nx_fe_set_direct found
 // the row maps in closed form and k_assemble_fes forms the matrix). Every x value is a local
 // function of the auxiliary solution xa and b (vertex fluxes, pressures and multipliers are
@@ -7919,7 +8232,10 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->d_left_k, h->d_cut_own, h->d_gk_off, h->d_gk_row, h->d_gk_coef, h->cutbuf,
                   h->d_cyc_rows, h->cyc_z, h->cyc_cinv, h->cyc_cap, h->cyc_prev, h->cyc_w,
                   h->fe_slot, h->fe_vfe, h->fe_vaux, h->fe_ife, h->fe_pfe, h->fe_paux, h->fe_lfe,
-                  h->fe_laux, h->fe_cst, h->fe_cellh};
+                  h->fe_laux, h->fe_cst, h->fe_cellh, h->d_cyc_qloc, h->d_cyc_lcol, h->cyc_u,
+                  h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_tI,
+                  h->cp_eb, h->cp_nrow, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
+                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -9477,6 +9793,44 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
   return NX_OK;
 }
 
+// Continuous pressure (k > m >= 1) on one rank, a forest (nx_fe_set_cp): the node-condensed
+// direct solve -- per edge its forward sweep, the border system by one workgroup, per edge
+// its back-substitution -- then this CSR's true residual, published. Up to two refinement
+// passes (the same solve of r = b - A x, added). *converged = 0 when still above rtol: the
+// caller runs MINRES.
+int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int32_t* converged) {
+  CHECK(flush_assembly(h));
+  const CpArgs a{(int)h->N, h->cp_k, h->cp_m, h->cp_nI, h->E, h->edge_R, h->fe_cellh, h->cp_cst,
+                 h->cp_tI, h->cp_eb, h->cp_nrow, h->cp_fac, h->cp_se, h->cp_xn};
+  const CpTree tr{h->cp_nn, h->cp_nlev, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
+                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_Pinv, h->cp_hv};
+  const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
+  const int eb = grid_of(h->E, 256);
+  MrState s{};
+  int pass = 0;
+  h->last_dir_path = 4;  // the node-condensed route (nx_get_direct_path)
+  for (; pass < 3; ++pass) {
+    const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
+    hipLaunchKernelGGL(k_cp_edge, dim3(eb), dim3(256), 0, h->stream, a, b);
+    hipLaunchKernelGGL(k_cp_nodes, dim3(1), dim3(1024), 0, h->stream, a, tr, b);
+    hipLaunchKernelGGL(k_cp_back, dim3(eb), dim3(256), 0, h->stream, a, b, h->x, h->cp_nown,
+                       pass ? 1 : 0);
+    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
+    hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                       nrb, rtol, h->d_seq, h->d_last);
+    HIPCALL(hipGetLastError());
+    h->seq += 1;
+    CHECK(wait_published(h));
+    s = *h->h_last;
+    if (s.converged || s.relres != s.relres) break;
+  }
+  if (iters) *iters = std::min(pass, 2) + 1;
+  if (relres) *relres = s.relres;
+  if (converged) *converged = s.converged;
+  return NX_OK;
+}
+
 int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, int32_t* iters,
                double* relres, int32_t* converged) {
   for (int r = 0; r < t.P; ++r) {
@@ -9491,10 +9845,11 @@ int solve_team(const Team& t, double rtol, int32_t maxit, int32_t check_every, i
     CHECK(set_device(t.hs[0]));
     CHECK(check_schedules(t));
   }
-  if (t.P == 1 && t.hs[0]->fe && t.hs[0]->fe_aux && t.hs[0]->solver == 1) {
+  if (t.P == 1 && t.hs[0]->fe && (t.hs[0]->fe_aux || t.hs[0]->fe_cp) && t.hs[0]->solver == 1) {
     CHECK(set_device(t.hs[0]));
     int32_t conv = 0;
-    CHECK(fe_solve_direct(t.hs[0], rtol, iters, relres, &conv));
+    CHECK(t.hs[0]->fe_cp ? fe_cp_solve(t.hs[0], rtol, iters, relres, &conv)
+                         : fe_solve_direct(t.hs[0], rtol, iters, relres, &conv));
     if (conv) {
       t.hs[0]->last_solver = 1;
       if (converged) *converged = 1;
@@ -10758,6 +11113,82 @@ NX_API int nx_set_cell_mass(nx_network_t* h, double ratio, double mo_div) {
     h->dstep_ok = false;
   }
   h->sched_checked = false;
+  return NX_OK;
+}
+
+// Continuous pressure (k > m >= 1), one rank, a forest: attach the node-condensed direct
+// solve (see include/nxhip.h); k = 0 detaches it.
+NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const double* cst,
+                        const int32_t* tI, int64_t n_nodes, const int32_t* nrow, const int32_t* eb,
+                        int32_t n_lev, const int32_t* lev_off, const int32_t* order,
+                        const int32_t* inc_off, const int32_t* inc, const int32_t* parent,
+                        const int32_t* child_off, const int32_t* child, const int32_t* nown) {
+  CHECK(flush_assembly(h));
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->fe) return fail(NX_ERR_STATE, "a general-degree handle (nx_create_fe)");
+  CHECK(set_device(h));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  for (double** p : {&h->cp_cst, &h->cp_fac, &h->cp_se, &h->cp_xn, &h->cp_Pinv, &h->cp_hv}) {
+    if (*p) HIPCALL(hipFree(*p));
+    *p = nullptr;
+  }
+  for (int** p : {&h->cp_tI, &h->cp_eb, &h->cp_nrow, &h->cp_lev_off, &h->cp_order, &h->cp_inc_off,
+                  &h->cp_inc, &h->cp_parent, &h->cp_child_off, &h->cp_child, &h->cp_nown}) {
+    if (*p) HIPCALL(hipFree(*p));
+    *p = nullptr;
+  }
+  h->fe_cp = false;
+  if (k == 0) return NX_OK;
+  const int64_t n = n_nodes, E = h->E;
+  if (!(m >= 1 && k > m) || nI != (k - 1) + (m - 1) || n < 1 || n_lev < 1 || !cst || !nrow ||
+      !eb || !lev_off || !order || !inc_off || !inc || !parent || !child_off || !nown ||
+      (nI > 0 && !tI))
+    return fail(NX_ERR_ARG, "bad continuous-pressure tables");
+  if (h->n_own < E * (int64_t)(k * h->N + 1 + m * h->N - 1) + n)
+    return fail(NX_ERR_ARG, "row counts do not match a (k, m) layout");
+  for (int64_t i = 0; i < n; ++i)
+    if (nrow[2 * i] < 0 || nrow[2 * i] >= h->n_own || nrow[2 * i + 1] < -1 || nrow[2 * i + 1] >= h->n_own ||
+        parent[3 * i] < -1 || parent[3 * i] >= n || parent[3 * i + 1] < -1 || parent[3 * i + 1] >= E ||
+        nown[i] < 0 || nown[i] >= E)
+      return fail(NX_ERR_ARG, "continuous pressure: node tables out of range");
+  for (int64_t e = 0; e < E; ++e)
+    if (eb[4 * e] < 0 || eb[4 * e] >= n || eb[4 * e + 1] < 0 || eb[4 * e + 1] >= n ||
+        std::abs(eb[4 * e + 2]) > 1 || std::abs(eb[4 * e + 3]) > 1)
+      return fail(NX_ERR_ARG, "continuous pressure: edge tables out of range");
+  if (lev_off[0] != 0 || lev_off[n_lev] != n || inc_off[0] != 0 || child_off[0] != 0)
+    return fail(NX_ERR_ARG, "continuous pressure: offsets");
+  for (int64_t i = 0; i < n; ++i)
+    if (order[i] < 0 || order[i] >= n) return fail(NX_ERR_ARG, "continuous pressure: order");
+  for (int64_t j = 0; j < inc_off[n]; ++j)
+    if (inc[2 * j] < 0 || inc[2 * j] >= E || inc[2 * j + 1] < 0 || inc[2 * j + 1] > 1)
+      return fail(NX_ERR_ARG, "continuous pressure: incidence");
+  for (int64_t j = 0; j < child_off[n]; ++j)
+    if (child[j] < 0 || child[j] >= n) return fail(NX_ERR_ARG, "continuous pressure: children");
+  const int64_t ncst = 16 + 8 * (int64_t)nI + (int64_t)nI * nI;
+  CHECK(upload(&h->cp_cst, cst, ncst, h->stream));
+  if (nI > 0) CHECK(upload(&h->cp_tI, tI, nI, h->stream));
+  CHECK(upload(&h->cp_nrow, nrow, 2 * n, h->stream));
+  CHECK(upload(&h->cp_eb, eb, 4 * E, h->stream));
+  CHECK(upload(&h->cp_lev_off, lev_off, (int64_t)n_lev + 1, h->stream));
+  CHECK(upload(&h->cp_order, order, n, h->stream));
+  CHECK(upload(&h->cp_inc_off, inc_off, n + 1, h->stream));
+  CHECK(upload(&h->cp_inc, inc, std::max<int64_t>(1, 2 * (int64_t)inc_off[n]), h->stream));
+  CHECK(upload(&h->cp_parent, parent, 3 * n, h->stream));
+  CHECK(upload(&h->cp_child_off, child_off, n + 1, h->stream));
+  if (child_off[n] > 0) CHECK(upload(&h->cp_child, child, child_off[n], h->stream));
+  CHECK(upload(&h->cp_nown, nown, n, h->stream));
+  CHECK(dalloc(&h->cp_fac, E * (h->N + 1) * (int64_t)kCpFac));
+  CHECK(dalloc(&h->cp_se, 20 * E));
+  CHECK(dalloc(&h->cp_xn, 2 * n));
+  CHECK(dalloc(&h->cp_Pinv, 4 * n));
+  CHECK(dalloc(&h->cp_hv, 2 * n));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  h->cp_k = k;
+  h->cp_m = m;
+  h->cp_nI = nI;
+  h->cp_nn = (int)n;
+  h->cp_nlev = n_lev;
+  h->fe_cp = true;
   return NX_OK;
 }
 

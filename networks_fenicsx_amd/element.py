@@ -138,3 +138,86 @@ def condensed_flux_mass(flux_degree: int):
     f64 = lambda X: np.array([[float(v) for v in row] for row in X], dtype=np.float64)  # noqa: E731
     return (float(S[0][0]), float(S[0][1]), f64(C).reshape(2, ni), f64(Kq).reshape(ni, 2),
             f64(Minv).reshape(ni, ni))
+
+
+def _frac_inverse(A):
+    """Exact inverse of a square matrix of Fractions (Gauss-Jordan, first nonzero pivot)."""
+    from fractions import Fraction as F
+
+    n = len(A)
+    W = [list(row) + [F(int(i == j)) for j in range(n)] for i, row in enumerate(A)]
+    for col in range(n):
+        piv = next(r for r in range(col, n) if W[r][col] != 0)
+        W[col], W[piv] = W[piv], W[col]
+        d = W[col][col]
+        W[col] = [v / d for v in W[col]]
+        for r in range(n):
+            if r != col and W[r][col] != 0:
+                f = W[r][col]
+                W[r] = [a - f * b for a, b in zip(W[r], W[col])]
+    return [row[n:] for row in W]
+
+
+def condensed_cell_blocks(flux_degree: int, pressure_degree: int):
+    """One cell of continuous P_m pressure (m >= 1) and P_k flux with its interior nodes
+    condensed out onto the vertex unknowns ``V = (q_L, p_L, q_R, p_R)`` -- the building block
+    of the continuous-pressure direct solve (``nx_fe_set_cp``).
+
+    The cell matrix with the negated pressure rows is ``A(s) = [[s Mref, -Dref^T], [-Dref, 0]]``
+    (``s = R h``; ``element_tensors``), and ``A(s) = T A(1) T`` with ``T = diag(s^1/2`` on the
+    flux nodes, ``s^-1/2`` on the pressure nodes). So with ``I`` the interior nodes (flux
+    ``1..k-1``, then pressure ``1..m-1``) and ``Ah = A(1)``:
+
+    * ``Kh = Ah_VV - Ah_VI Ah_II^-1 Ah_IV`` (4 x 4): the condensed cell matrix is
+      ``s^(t_r + t_c) Kh[r, c]``;
+    * ``Ch = Ah_VI Ah_II^-1`` (4 x nI): the vertices' rhs ``b_V - s^(t_r - t_c) Ch b_I``;
+    * ``Eh = Ah_II^-1 Ah_IV`` (nI x 4), ``Fh = Ah_II^-1``: the interior values
+      ``x_I = s^(-t_r - t_c) Fh b_I - s^(-t_r + t_c) Eh x_V``;
+
+    with ``t = +1/2`` on flux and ``-1/2`` on pressure rows / columns (every exponent is -1,
+    0 or 1). Exact rational arithmetic, rounded once. Returns ``(Kh, Ch, Eh, Fh, tI)``;
+    ``tI``: the interior nodes' types (+1 flux, -1 pressure)."""
+    from fractions import Fraction as F
+
+    k, m = int(flux_degree), int(pressure_degree)
+    if not (m >= 1 and k > m):
+        raise ValueError("continuous pressure needs 1 <= pressure_degree < flux_degree")
+    Cq, Cp = lagrange_monomials(k), lagrange_monomials(m)
+    dCq = [[c * n for n, c in enumerate(row)][1:] for row in Cq]
+
+    def integ(A, B):
+        return [[sum((ap * bq / (p + q + 1) for p, ap in enumerate(a) for q, bq in enumerate(b)),
+                     F(0)) for b in B] for a in A]
+
+    M = integ(Cq, Cq)
+    D = integ(Cp, dCq)  # (m+1) x (k+1)
+    nq, npl = k + 1, m + 1
+    n = nq + npl
+    Ah = [[F(0)] * n for _ in range(n)]
+    for i in range(nq):
+        for j in range(nq):
+            Ah[i][j] = M[i][j]
+    for a in range(npl):
+        for j in range(nq):
+            Ah[nq + a][j] = -D[a][j]
+            Ah[j][nq + a] = -D[a][j]
+    V = [0, nq, k, nq + m]
+    I = list(range(1, k)) + [nq + a for a in range(1, m)]
+    tI = [1] * (k - 1) + [-1] * (m - 1)
+    sub = lambda R, Cc: [[Ah[r][c] for c in Cc] for r in R]  # noqa: E731
+    AVV, AVI, AIV, AII = sub(V, V), sub(V, I), sub(I, V), sub(I, I)
+    nI = len(I)
+    Fi = _frac_inverse(AII) if nI else []
+    mm = lambda A, B: [[sum((A[i][t] * B[t][j] for t in range(len(B))), F(0))  # noqa: E731
+                        for j in range(len(B[0]))] for i in range(len(A))]
+    if nI:
+        Ch = mm(AVI, Fi)
+        Eh = mm(Fi, AIV)
+        VIE = mm(AVI, Eh)
+        Kh = [[AVV[r][c] - VIE[r][c] for c in range(4)] for r in range(4)]
+    else:
+        Ch, Eh, Kh = [[] for _ in range(4)], [], AVV
+    f64 = lambda X, r, c: np.array([[float(v) for v in row] for row in X],  # noqa: E731
+                                   dtype=np.float64).reshape(r, c)
+    return (f64(Kh, 4, 4), f64(Ch, 4, nI), f64(Eh, nI, 4), f64(Fi, nI, nI),
+            np.array(tI, dtype=np.int32))

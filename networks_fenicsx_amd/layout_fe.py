@@ -251,3 +251,222 @@ def build_fe_aux_maps(lay: FeLayout, lp) -> FeAuxMaps:
     i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
     return FeAuxMaps(i32(v_fe), i32(v_aux), i32(i_fe), i32(p_fe), i32(p_aux),
                      i32(lay.lm_rows), i32(l_aux))
+
+
+@dataclass
+class CpTables:
+    """The continuous-pressure direct solve's tables (``nx_fe_set_cp``, include/nxhip.h):
+    reference blocks, border nodes (every graph node with an edge), per edge its end nodes
+    and multiplier couplings, and the node forest in level order."""
+
+    k: int
+    m: int
+    nI: int
+    cst: np.ndarray  # Kh | Ch | Eh | Fh
+    tI: np.ndarray
+    n_nodes: int
+    nrow: np.ndarray  # (n, 2) pressure row, multiplier row or -1
+    eb: np.ndarray  # (E, 4) source node, target node, q_0 - lam_src, q_N - lam_dst couplings
+    lev_off: np.ndarray
+    order: np.ndarray
+    inc_off: np.ndarray
+    inc: np.ndarray  # (n_inc, 2) edge, end (0 source, 1 target)
+    parent: np.ndarray  # (n, 3) parent node, edge, this node's end of it (-1 at a root)
+    child_off: np.ndarray
+    child: np.ndarray
+    nown: np.ndarray  # the edge that writes each node's rows
+
+
+def build_cp_tables(lay: FeLayout, src: np.ndarray, dst: np.ndarray) -> CpTables | None:
+    """Tables of the node-condensed direct solve for continuous pressure (``lay.m >= 1``), or
+    ``None`` when the graph is not a forest (a cycle: MINRES)."""
+    from collections import deque
+
+    from .element import condensed_cell_blocks
+
+    if lay.m < 1:
+        raise ValueError("the node-condensed solve is continuous pressure's (m >= 1)")
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    E = lay.E
+    nodes = np.asarray(lay.p_nodes, dtype=np.int64)
+    n = nodes.size
+    idx = np.full(int(max(src.max(), dst.max())) + 1 if E else 0, -1, dtype=np.int64)
+    idx[nodes] = np.arange(n)
+    u, v = idx[src], idx[dst]
+    per = lay.k * lay.N + 1 + lay.m * lay.N - 1
+    lam = np.full(idx.size, -1, dtype=np.int64)
+    lam[np.asarray(lay.lm_nodes, dtype=np.int64)] = np.asarray(lay.lm_rows, dtype=np.int64)
+    nrow = np.stack([E * per + np.arange(n), lam[nodes]], axis=1)
+    eb = np.stack([u, v, np.where(lam[src] >= 0, -1, 0), np.where(lam[dst] >= 0, 1, 0)], axis=1)
+    # incidence (edge, end), by node then edge
+    ne = np.concatenate([u, v])
+    ee = np.concatenate([np.arange(E), np.arange(E)])
+    en = np.concatenate([np.zeros(E, np.int64), np.ones(E, np.int64)])
+    o = np.lexsort((ee, ne))
+    inc = np.stack([ee[o], en[o]], axis=1)
+    inc_off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(ne, minlength=n), out=inc_off[1:])
+    # BFS forest from the lowest node of every component
+    parent = np.full((n, 3), -1, dtype=np.int64)
+    level = np.full(n, -1, dtype=np.int64)
+    for r in range(n):
+        if level[r] >= 0:
+            continue
+        level[r] = 0
+        dq = deque([r])
+        while dq:
+            a = dq.popleft()
+            for j in range(inc_off[a], inc_off[a + 1]):
+                e, end = inc[j]
+                b = v[e] if end == 0 else u[e]
+                if b == a or (parent[a, 1] == e):
+                    continue
+                if level[b] >= 0:
+                    return None  # a cycle
+                level[b] = level[a] + 1
+                parent[b] = (a, e, 1 - end)
+                dq.append(b)
+    order = np.lexsort((np.arange(n), level))
+    nlev = int(level.max()) + 1 if n else 1
+    lev_off = np.zeros(nlev + 1, dtype=np.int64)
+    np.cumsum(np.bincount(level, minlength=nlev), out=lev_off[1:])
+    has = parent[:, 0] >= 0
+    ch_par = parent[has, 0]
+    ch = np.flatnonzero(has)
+    oc = np.lexsort((ch, ch_par))
+    child = ch[oc]
+    child_off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(ch_par, minlength=n), out=child_off[1:])
+    nown = inc[inc_off[:-1], 0]
+    Kh, Ch, Eh, Fh, tI = condensed_cell_blocks(lay.k, lay.m)
+    cst = np.concatenate([Kh.ravel(), Ch.ravel(), Eh.ravel(), Fh.ravel()])
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32).ravel()  # noqa: E731
+    return CpTables(lay.k, lay.m, int(tI.size), cst, i32(tI), int(n), i32(nrow), i32(eb),
+                    i32(lev_off), i32(order), i32(inc_off), i32(inc), i32(parent),
+                    i32(child_off), i32(child), i32(nown))
+
+
+def cp_model(lay: FeLayout, tab: CpTables, val: np.ndarray, b: np.ndarray, R: np.ndarray,
+             cell_h: np.ndarray) -> np.ndarray:
+    """numpy restatement of the device's node-condensed solve (k_cp_edge, k_cp_nodes,
+    k_cp_back) for tests: ``x`` of the (k, m) system with values ``val`` and rhs ``b``."""
+    import scipy.sparse as sp
+
+    A = sp.csr_matrix((val, lay.col, lay.rowptr), shape=(lay.n_rows, lay.n_rows))
+    N, k, m, nI, E = lay.N, lay.k, lay.m, tab.nI, lay.E
+    nf = k * N + 1
+    per = nf + m * N - 1
+    Kh = tab.cst[:16].reshape(4, 4)
+    Ch = tab.cst[16:16 + 4 * nI].reshape(4, nI)
+    Eh = tab.cst[16 + 4 * nI:16 + 8 * nI].reshape(nI, 4)
+    Fh = tab.cst[16 + 8 * nI:].reshape(nI, nI)
+    tI = tab.tI.astype(np.int64)
+    tV = np.array([1, -1, 1, -1])
+    eb = tab.eb.reshape(-1, 4)
+    nrow = tab.nrow.reshape(-1, 2)
+    h = np.asarray(cell_h).reshape(E, N)
+    x = np.zeros(lay.n_rows)
+    Se, ge, facs = np.zeros((E, 4, 4)), np.zeros((E, 4)), []
+    for e in range(E):
+        base = e * per
+        prow = lambda j: base + nf + j - 1  # noqa: E731
+        irow = lambda c, i: base + c * k + 1 + i if tI[i] > 0 else prow(c * m + 1 + i - (k - 1))  # noqa: E731
+        P = np.array([[0.0, 0.0], [0.0, 1.0]])
+        W = np.zeros((2, 4))
+        W[0, 1] = eb[e, 2]
+        rho = np.array([b[base], 0.0])
+        Sb, gb, fe = np.zeros((4, 4)), np.zeros(4), []
+        for c in range(N):
+            s = R[e] * h[e, c]
+            K = Kh * s ** ((tV[:, None] + tV[None, :]) // 2)
+            bI = np.array([b[irow(c, i)] for i in range(nI)])
+            rV = -(Ch * s ** ((tV[:, None] - tI[None, :]) // 2)) @ bI if nI else np.zeros(4)
+            Wn = np.zeros((2, 4))
+            if c == 0:
+                P[0, 0] += K[0, 0]; W[0, 0] += K[0, 1]; Sb[0, 0] += K[1, 1]  # noqa: E702
+                rho[0] += rV[0]; gb[0] += rV[1]  # noqa: E702
+                C = np.array([[K[0, 2], K[0, 3]], [0.0, 0.0]])
+                Wn[0, 0], Wn[1, 0] = K[2, 1], K[3, 1]
+            else:
+                P += K[:2, :2]; rho += rV[:2]  # noqa: E702
+                C = K[:2, 2:].copy()
+            if c + 1 < N:
+                Pn = K[2:, 2:].copy()
+                rn = rV[2:] + np.array([b[base + k * (c + 1)], b[prow(m * (c + 1))]])
+            else:
+                Sb[2, 2] += K[3, 3]; gb[2] += rV[3]  # noqa: E702
+                if c == 0:
+                    Sb[0, 2] += K[1, 3]; Sb[2, 0] += K[3, 1]  # noqa: E702
+                Wn[0, 2] += K[2, 3]; Wn[0, 3] = eb[e, 3]; Wn[1, 0] = 0.0  # noqa: E702
+                W[:, 2] += C[:, 1]; C[:, 1] = 0.0  # noqa: E702
+                Pn = np.array([[K[2, 2], 0.0], [0.0, 1.0]])
+                rn = np.array([rV[2] + b[base + nf - 1], 0.0])
+            Pi = np.linalg.inv(P)
+            Pn -= C.T @ Pi @ C; Wn -= C.T @ Pi @ W; rn -= C.T @ Pi @ rho  # noqa: E702
+            Sb -= W.T @ Pi @ W; gb -= W.T @ Pi @ rho  # noqa: E702
+            fe.append((Pi, C, W, rho))
+            P, W, rho = Pn, Wn, rn
+        Pi = np.linalg.inv(P)
+        Sb -= W.T @ Pi @ W; gb -= W.T @ Pi @ rho  # noqa: E702
+        fe.append((Pi, np.zeros((2, 2)), W, rho))
+        Se[e], ge[e] = Sb, gb
+        facs.append(fe)
+    n = tab.n_nodes
+    inc = tab.inc.reshape(-1, 2)
+    par = tab.parent.reshape(-1, 3)
+    Pinv, hv, xn = np.zeros((n, 2, 2)), np.zeros((n, 2)), np.zeros((n, 2))
+    blk = lambda e, ra, cb: Se[e][2 * ra:2 * ra + 2, 2 * cb:2 * cb + 2]  # noqa: E731
+    lev = tab.lev_off
+    for L in range(lev.size - 2, -1, -1):
+        for i in range(lev[L], lev[L + 1]):
+            nd = tab.order[i]
+            D = np.zeros((2, 2))
+            g = np.array([b[nrow[nd, 0]], b[nrow[nd, 1]] if nrow[nd, 1] >= 0 else 0.0])
+            for j in range(tab.inc_off[nd], tab.inc_off[nd + 1]):
+                e, end = inc[j]
+                D += blk(e, end, end)
+                g += ge[e][2 * end:2 * end + 2]
+            if nrow[nd, 1] < 0:
+                D[1, 1] = 1.0
+            for j in range(tab.child_off[nd], tab.child_off[nd + 1]):
+                c = tab.child[j]
+                B = blk(par[c, 1], par[c, 2], 1 - par[c, 2])
+                D -= B.T @ Pinv[c] @ B
+                g -= B.T @ Pinv[c] @ hv[c]
+            Pinv[nd], hv[nd] = np.linalg.inv(D), g
+    for L in range(lev.size - 1):
+        for i in range(lev[L], lev[L + 1]):
+            nd = tab.order[i]
+            r = hv[nd].copy()
+            if par[nd, 0] >= 0:
+                r -= blk(par[nd, 1], par[nd, 2], 1 - par[nd, 2]) @ xn[par[nd, 0]]
+            xn[nd] = Pinv[nd] @ r
+    for nd in range(n):
+        x[nrow[nd, 0]] = xn[nd, 0]
+        if nrow[nd, 1] >= 0:
+            x[nrow[nd, 1]] = xn[nd, 1]
+    for e in range(E):
+        base = e * per
+        prow = lambda j: base + nf + j - 1  # noqa: E731
+        xb = np.concatenate([xn[eb[e, 0]], xn[eb[e, 1]]])
+        yn = np.zeros(2)
+        for i in range(N, -1, -1):
+            Pi, C, W, rho = facs[e][i]
+            y = Pi @ (rho - C @ yn - W @ xb)
+            x[base + k * i] = y[0]
+            if 0 < i < N:
+                x[prow(m * i)] = y[1]
+            if i < N:
+                s = R[e] * h[e, i]
+                xv = np.array([y[0], xb[0] if i == 0 else y[1], yn[0], xb[2] if i + 1 == N else yn[1]])
+                bI = np.array([b[base + i * k + 1 + j] if tI[j] > 0
+                               else b[prow(i * m + 1 + j - (k - 1))] for j in range(nI)])
+                xI = (Fh * s ** (-(tI[:, None] + tI[None, :]) // 2)) @ bI \
+                    - (Eh * s ** ((-tI[:, None] + tV[None, :]) // 2)) @ xv if nI else []
+                for j in range(nI):
+                    r = base + i * k + 1 + j if tI[j] > 0 else prow(i * m + 1 + j - (k - 1))
+                    x[r] = xI[j]
+            yn = y
+    del A
+    return x

@@ -220,3 +220,52 @@ def test_fe_direct_cycles_run_minres():
     got = np.concatenate([fn.x.array for fn in sol])
     x_ref = O.solve_reference(A, b)
     assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "depth6_N40", "arterial5_N40",
+                                  "linear_alt_N3"])
+@pytest.mark.parametrize("km", [(2, 1), (3, 2), (3, 1), (4, 3)])
+def test_fe_continuous_pressure_direct(case, km):
+    """Continuous pressure (k > m >= 1) by condensation onto the graph nodes (nx_fe_set_cp:
+    per edge its forward sweep, the node system by one workgroup, per edge its
+    back-substitution): the direct path runs (no MINRES) in at most three passes, within
+    SOL_TOL of the oracle's LU (independently integrated tensors), its reported residual
+    the true one; a second solve with other coefficients stays exact."""
+    E = len(CASES[case][0]().edges())
+    R = 1.0 + 0.5 * (np.arange(E) % 3)
+    mesh, asm, F, A, b, pbc = _setup(case, km, f=0.4, R=R)
+    assert asm.fe_direct_available
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.solver_used == "direct" and solver.ksp.converged
+    assert asm.handle.direct_path() == "node-condensed"
+    assert 1 <= solver.ksp.iterations <= 3
+    x_ref = O.solve_reference(A, b)
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    tr = solver.true_residual()
+    assert tr <= 1e-12
+    assert abs(solver.ksp.residual_estimate - tr) <= 1e-6 * tr + 1e-16
+    R2 = 2.0 - 0.25 * (np.arange(E) % 4)
+    asm.compute_forms(p_bc_ex=pbc, f=0.1, R=R2)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.solver_used == "direct" and solver.ksp.converged
+    A2, b2 = OF.assemble_reference_fe(F, pbc, f=0.1, R=R2)
+    x2 = O.solve_reference(A2, b2)
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x2) / np.linalg.norm(x2) <= SOL_TOL
+
+
+def test_fe_continuous_pressure_cycles_run_minres():
+    """A graph with cycles: no node-condensed tables, MINRES reaches the oracle's answer."""
+    mesh, asm, F, A, b, pbc = _setup("edge_info_N10", (2, 1))
+    assert not asm.fe_direct_available
+    solver = Solver(asm)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.solver_used == "minres" and solver.ksp.converged
+    got = np.concatenate([fn.x.array for fn in sol])
+    x_ref = O.solve_reference(A, b)
+    assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL

@@ -1,5 +1,5 @@
 """The bench's 8-GPU workload (``bench.py --gpus 8``: ``make_tree(18,18,18)``, N = 15, one
-C3-sized piece per rank, 8,257,536 DoF) on one GPU: the 8 per-rank handles through the
+C3-sized piece per rank, 8,257,504 DoF) on one GPU: the 8 per-rank handles through the
 in-process group (graph path: coarse all-reduce, cut rows in the residual's sum), then
 every rank's one-launch exchange step alone as on its own GPU (``k_dir_xr<8, 2>``,
 ``nx_debug_xr_rehearse``: its exchanges emulated from the graph path's sums).
@@ -39,7 +39,7 @@ def test_bench_workload_exchange_rehearsal():
         prob = O.build_problem(m0.node_coordinates, src, dst, N)
         xa = O.resistor_network_solution(prob, p_y)[O.build_permutation(prob)[0]]
         E = m0.num_edges
-        assert xa.size == 8_257_536
+        assert xa.size == 262_143 * 31 + 131_071 == 8_257_504
         grp.compute_forms(p_bc_ex=p_y)
         grp.set_direct(True)
         grp.assemble()
