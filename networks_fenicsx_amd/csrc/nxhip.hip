@@ -6403,6 +6403,7 @@ struct nx_network {
   // rows no job forms, every left row's post range, the posts, the hand-off counters and
   // the launches since they were zero (all in pc_bufs; reset with every upload)
   bool dstep_ok = false;   // the decomposition allows it (nx_set_preconditioner)
+  bool dstep_multi = false;  // some job of the one-launch step needs several chain passes
   bool dq_stale = false;   // the last assembly was a one-launch step's: dq not formed (ensure_dq)
   bool dstep_off = false;  // a launch gave up waiting (workgroups not co-resident)
   int* d_chain_post = nullptr;
@@ -9119,10 +9120,12 @@ bool xr_on(const Team& t, bool with_asm) {
 // The one-launch steps (k_dir_step, k_dir_xr, k_dir_xg) do not write the lumped flux mass
 // dq: only the separate sweeps (a refinement pass, MINRES, the graph path) read it, and
 // ensure_dq forms it before them. (4.2 MB of the step's stores at C3.)
+// A job with more chains than one pass re-reads its chains' b and dq in phase 2: its step
+// writes them (dstep_multi).
 DirStep dir_args(nx_network* h, double rtol) {
-  h->dq_stale = true;
+  h->dq_stale = !h->dstep_multi;
   return DirStep{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
-                 h->val, h->rhs, nullptr, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
+                 h->val, h->rhs, h->dstep_multi ? h->dq : nullptr, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
                  h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
                  h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1,
                  h->d_seq, h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci,
@@ -10854,7 +10857,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   h->d_ci = nullptr;
   if (h->dstep_ok || h->xr_ok) {
     std::vector<int> hdr((size_t)kJobHdr * n_jobs, 0);
-    int mlv = 1, mns = 0, mnd = 0;
+    int mlv = 1, mns = 0, mnd = 0, mch = 0;
     for (int jb = 0; jb < n_jobs; ++jb) {
       const int lv0 = job_lvl_off[jb], lv1 = job_lvl_off[jb + 1];
       const int js0 = lv1 > lv0 ? lvl_slot_off[lv0] : 0, js1 = lv1 > lv0 ? lvl_slot_off[lv1] : 0;
@@ -10872,6 +10875,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
       mlv = std::max(mlv, lv1 - lv0 + 1);
       mns = std::max(mns, js1 - js0);
       mnd = std::max(mnd, r[7] - r[6]);
+      mch = std::max(mch, r[1] - r[0]);
     }
     if (pa.job_wave) {  // (the one-wave set-up of the up sweep, when the job has it)
       std::vector<int> jw(n_jobs, 0);
@@ -10879,6 +10883,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
       for (int jb = 0; jb < n_jobs; ++jb) hdr[(size_t)kJobHdr * jb + 8] = jw[jb];
     }
     const int W = variant_w(N <= 16 ? 5 : N <= 24 ? 10 : N <= 32 ? 7 : variant);  // (dstep's)
+    h->dstep_multi = mch > kPcThreads / W;
     const int nt = h->top_nt, cdc = std::max(1, pa.top_ndc), ct = nt + 1;
     const int top_ints = 3 * ct + 1 + cdc + n_top_lvl + 1;
     const int top_dbl = 6 * ct + 3 * cdc + (top_ints + 1) / 2 + 2;

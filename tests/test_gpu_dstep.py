@@ -213,3 +213,29 @@ def test_dstep_c3_analytic():
     Ad = sp.csr_matrix((val, col, rp), shape=(h.n_rows, h.n_rows))
     assert abs(Ad - Ad.T).max() == 0.0
     asm.close()
+
+
+def test_dstep_several_chain_passes_fresh_handle():
+    """make_tree(16), N = 4: 65,535 edges over <= 256 jobs, so a job holds ~256 chains, more
+    than one pass of its workgroup (1024 / 8 lanes = 128): phase 2 re-reads the chains' b and
+    lumped mass, which the step then writes itself (dstep_multi) -- on a fresh handle no
+    earlier assembly has left a lumped mass behind. The analytic answer to 1e-10."""
+    mesh = NetworkMesh(ng.make_tree(16, 15, 15), N=4, color_strategy="smallest_last")
+    asm = HydraulicNetworkAssembler(mesh)
+    asm.compute_forms(p_bc_ex=lambda x: x[1])
+    asm.set_direct(True)
+    h = asm.handle
+    assert int(np.diff(asm._pc.job_chain_off).max()) > 128
+    asm.assemble()
+    it, rr, conv = h.solve(1e-12, 100, 4)
+    assert h.direct_path() == "fused" and conv and it == 1 and rr <= 1e-12
+    src, dst = mesh.edges
+    P = O.build_problem(mesh.node_coordinates, src, dst, 4)
+    xa = O.resistor_network_solution(P, lambda x: x[1])[O.build_permutation(P)[0]]
+    assert np.linalg.norm(h.solution() - xa) / np.linalg.norm(xa) <= SOL_TOL
+    assert abs(rr - h.true_residual()) <= 0.05 * rr + 5e-16
+    # MINRES on the same system after the step: the lumped mass is the assembly kernel's
+    asm.set_direct(False)
+    it2, rr2, conv2 = h.solve(1e-10, 200, 4)
+    assert conv2 and np.linalg.norm(h.solution() - xa) / np.linalg.norm(xa) <= 1e-8
+    asm.close()
