@@ -62,6 +62,10 @@ __device__ unsigned long long g_dst[48][512];  // k_dir_step: per-workgroup stam
   do {                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 512) g_dst[(k)][blockIdx.x] = wall_clock64(); \
   } while (0)
+// store-site ledger of the one-launch step (scripts/store_ledger.py, NXHIP_LEDGER): a set bit
+// drops one class of its global stores (1 CSR values, 2 rhs, 4 x, 16 multiplier rows'
+// values) so that WRITE_SIZE differences attribute the written bytes -- debug build only
+#define NX_LEDGER(da, bit) (((da).ledger & (bit)) != 0)
 #define NX_PHASE(slot)                                           \
   do {                                                           \
     if (blockIdx.x == 0) {                                       \
@@ -100,6 +104,7 @@ __device__ unsigned long long g_dst[48][512];  // k_dir_step: per-workgroup stam
 #define NX_DSTAMP(k) \
   do {               \
   } while (0)
+#define NX_LEDGER(da, bit) false
 #endif
 
 int fail(int code, const std::string& msg) {
@@ -3444,6 +3449,7 @@ struct DirStep {
   int xP, xrank, xld1, xld2, xK;
   unsigned xtag;
   unsigned xpoll[2];  // each exchange's poll bound (kDirWaitPolls; nx_debug_xr_polls: tests)
+  int ledger;         // debug build: store classes the step drops (NX_LEDGER)
 };
 
 constexpr int kDirWaitPolls = 1 << 20;  // s_sleep-paced polls before a waiting workgroup gives up
@@ -3600,14 +3606,17 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
   for (int t = 0; t < CPL; ++t) {
     if (!ch.valid[t]) continue;
     const int k = l * CPL + t;
-    da.rhs[ch.dof_c[t]] = L.bc[t];
-    da.rhs[ch.dof_q[t]] = L.bq[t];
+    if (!NX_LEDGER(da, 2)) {
+      da.rhs[ch.dof_c[t]] = L.bc[t];
+      da.rhs[ch.dof_q[t]] = L.bq[t];
+    }
     if (da.dq) da.dq[qb + (flip ? N - k : k)] = ch.rho[t];
   }
   if (ch.has_last) {
-    da.rhs[ch.dof_qN] = L.bN;
+    if (!NX_LEDGER(da, 2)) da.rhs[ch.dof_qN] = L.bN;
     if (da.dq) da.dq[qb + (flip ? 0 : N)] = ch.rhoN;
   }
+  if (NX_LEDGER(da, 1)) return;
   // the CSR segment, each lane its own cells' rows (edge order: cell g owns p_g's 2 entries
   // and q_{g+1}'s 5 -- q_N's 3 + s_dst for g = N - 1 -- from q0len + 7 g on; cell 0 also the
   // q_0 row): values as decode_entry lists them, the next edge cell's masses from the
@@ -4011,8 +4020,8 @@ __device__ __forceinline__ void dir_stores_all(const PcArgs& pa, const DirStep& 
   const int nj = pa.n_jobs;
   const int64_t nlm = da.nnz_lm > da.B ? da.nnz_lm : da.B;
   for (int64_t i = (int64_t)job * kPcThreads + threadIdx.x; i < nlm; i += (int64_t)nj * kPcThreads) {
-    if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
-    if (i < da.B) da.rhs_lm[i] = 0.0;
+    if (i < da.nnz_lm && !NX_LEDGER(da, 16)) da.val_lm[i] = da.lm_val[i];
+    if (i < da.B && !NX_LEDGER(da, 16)) da.rhs_lm[i] = 0.0;
   }
   const int c0 = pa.job_chain_off[job], c1 = pa.job_chain_off[job + 1];
   if (keep) {
@@ -4529,7 +4538,7 @@ __device__ __forceinline__ void dir_down_v2(const PcArgs& pa, const DirStep& da,
     }
   }
   NX_DSTAMP(37);
-  if ((int)threadIdx.x < ns) x[S.lam(threadIdx.x)] = sZ[threadIdx.x];
+  if ((int)threadIdx.x < ns && !NX_LEDGER(da, 4)) x[S.lam(threadIdx.x)] = sZ[threadIdx.x];
   double rr = 0.0, bb = 0.0;
   for (int cb = c0; cb < c1; cb += G) {
     const int c = cb + seg;
@@ -4573,14 +4582,14 @@ __device__ __forceinline__ void dir_down_v2(const PcArgs& pa, const DirStep& da,
       double zk = zt * (T - Dk) * iT + zb * Dk * iT + Dk * iT * suffix + (T - Dk) * iT * prefix;
       zk -= ch.mo * vc[t];  // the consistent-mass Schur complement
       zc[t] = zk;
-      x[ch.dof_c[t]] = zk;
+      if (!NX_LEDGER(da, 4)) x[ch.dof_c[t]] = zk;
     }
     double xv[CPL + 1];
     direct_flux_cons<W, CPL>(ch, flip, bcv, vq, vN, zt, zb, xv);
 #pragma unroll
     for (int t = 0; t <= CPL; ++t) {
       const bool on = t < CPL ? ch.valid[t] : ch.has_last;
-      if (on) x[t < CPL ? ch.dof_q[t] : ch.dof_qN] = xv[t];
+      if (on && !NX_LEDGER(da, 4)) x[t < CPL ? ch.dof_q[t] : ch.dof_qN] = xv[t];
     }
     direct_residual<W, CPL, false>(pa, ch, active, flip, bcv, vq, vN, zc, xv, zt, zb, mo_r, rr, bb,
                                    sQt, sQb, c - c0);
@@ -4635,8 +4644,8 @@ __device__ __forceinline__ void dir_stores_v2(const PcArgs& pa, const DirStep& d
     const int nthr = (g1 - g0) * W;
     for (int k = (int)threadIdx.x - g0 * W; k < kPcThreads; k += nthr)
       for (int64_t i = (int64_t)jb * kPcThreads + k; i < nlm; i += (int64_t)nj * kPcThreads) {
-        if (i < da.nnz_lm) da.val_lm[i] = da.lm_val[i];
-        if (i < da.B) da.rhs_lm[i] = 0.0;
+        if (i < da.nnz_lm && !NX_LEDGER(da, 16)) da.val_lm[i] = da.lm_val[i];
+        if (i < da.B && !NX_LEDGER(da, 16)) da.rhs_lm[i] = 0.0;
       }
   }
   if (keep) {
@@ -4920,7 +4929,7 @@ __device__ __forceinline__ bool xr_coarse(const PcArgs& pa, const DirStep& da, c
   for (int i = threadIdx.x; i < nt; i += kPcThreads) {
     const double zj = T.sY[i];
     st_wt(pa.slot_z + ts0 + i, zj);
-    da.x[T.sLam[i]] = zj;
+    if (!NX_LEDGER(da, 4)) da.x[T.sLam[i]] = zj;
   }
   return true;
 }
@@ -6498,9 +6507,12 @@ struct nx_network {
   // owned), the row maps, the cell constants C | K | Mii and a + b
   nx_network* fe_aux = nullptr;
   int fe_k = 0, fe_nl = 0;
-  int fe_sk = 0;  // > 0: a (k, 0) layout whose terms k_assemble_fes forms in closed form
-  bool fe_fuse = false;  // nx_fe_set_direct: the row maps in closed form (k_fe_expand_res)
-  int64_t fe_edge_nnz = 0;  // the most nonzeros of one edge's rows (fe_sk > 0)
+  int fe_sk = 0;  // > 0: a (k, 0) layout whose terms fe_s_terms forms in closed form
+  // (k, 0) edge templates (fe_build_tpl; k_fe_tasm / k_fe_tres): entries, shape offsets,
+  // shape row starts, the edges' shapes and multiplier columns
+  bool fe_tpl = false;
+  void* fe_tpl_buf = nullptr;
+  int *fe_tpl_off = nullptr, *fe_tpl_rs = nullptr, *fe_tpl_shape = nullptr, *fe_tpl_lam = nullptr;
   double* fe_cellh = nullptr;  // E*N cell lengths (k_fe_cellh at nx_create_fe)
   int *fe_slot = nullptr, *fe_vfe = nullptr, *fe_vaux = nullptr, *fe_ife = nullptr;
   int *fe_pfe = nullptr, *fe_paux = nullptr, *fe_lfe = nullptr, *fe_laux = nullptr;
@@ -7300,7 +7312,7 @@ struct FeArgs {
   double* val;
   double* rhs;
   int lhs, do_rhs;
-  int64_t n_edges;  // (k_assemble_fes)
+  int64_t n_edges;  // (k_fe_tasm)
   const double* cellh;  // E*N cell lengths (fe_cell_h, once per handle), or null: formed here
 };
 
@@ -7361,7 +7373,7 @@ __global__ __launch_bounds__(kBlock) void k_assemble_fe(FeArgs a) {
 
 // (k, 0) layouts (layout_fe.py with m = 0): the terms of entry (row, col) in closed form --
 // the same (index, table entry) list, in the same order, as the host's gather tables, which
-// nx_create_fe checks entry by entry before it lets k_assemble_fes replace k_assemble_fe.
+// nx_create_fe checks entry by entry before it builds the edge templates (fe_build_tpl).
 // Per edge e: kN + 1 flux rows then N cell pressure rows (per = kN + 1 + N); the multiplier
 // rows after all edges. Table: (k+1)^2 mass, k+1 divergence, +1, -1, source, bc.
 struct FeTerm {
@@ -7449,112 +7461,165 @@ __host__ __device__ __forceinline__ int fe_s_rhs_terms(int64_t row, int k, int N
   return 1;
 }
 
-// (k, 0) assembly without the gather tables (k_assemble_fes): one wave per edge. The edge's
-// rows and CSR segments are contiguous, so the wave's lanes stride over its nonzeros
-// (coalesced col reads and value writes), each finding its row by a binary search of the
-// edge's row pointers in LDS; the cell lengths are formed once per edge (fe_cell_h, the same
-// bits) and every entry sums its closed-form terms (fe_s_terms) in the gather tables' order,
-// so the values equal k_assemble_fe's bit for bit. The multiplier rows: one thread each, in
-// the blocks after the edges'.
-constexpr int kFesWaves = 4;    // waves (edges) per block
-constexpr int kFesRows = 512;   // row pointers per edge in LDS: k N + 1 + N + 1 at most
-constexpr int kFesCells = 256;  // cells per edge in LDS
+constexpr int kFesWaves = 4;    // k_fe_tasm / k_fe_tres: waves (edges) per block
+constexpr int kFesRows = 512;   // (nx_fe_struct_degree) rows per edge: k N + 1 + N + 1 at most
+constexpr int kFesCells = 256;  // cells per edge
 constexpr int kFesTable = 128;  // term table entries in LDS
-constexpr int kFesNnz = 1024;   // (k_fe_expand_res) nonzeros per edge in LDS
-__device__ __forceinline__ double fe_term_h(const FeArgs& a, int idx, int ent, double hc) {
+// ---- (k, 0) edge templates (k_fe_tasm / k_fe_tres). Every edge's rows have one of four
+// shapes: a multiplier column at its first flux row or not, at its last or not (the
+// multiplier columns sort after the edge's own). Per shape, nx_create_fe lists the entries in
+// CSR order with their terms (fe_s_terms_loc, cells relative to the edge's first) and local
+// column (-1: the multiplier), checks every edge's rows against its shape, and the kernels
+// then form an edge's values from its R and cell lengths alone: no gather tables, no column
+// reads, no decoding per entry. Same terms in the same order as k_assemble_fe: bit-exact.
+struct FeTplE {
+  short pos, lc;  // row within the edge; local column, -1 = the row's multiplier column
+  short n;        // terms (0..2)
+  short c0, c1;   // their cells relative to the edge's first
+  short e0, e1;   // their table entries
+  short pad;
+};
+struct FeTpl {
+  const FeTplE* tpl;
+  const int* off;      // 5: each shape's first entry
+  const int* rs;       // 4 x (per + 1): each shape's row starts (entry index)
+  const int* shape;    // E: the edge's shape (bit 0: multiplier at row 0, bit 1: at row nf - 1)
+  const int* lam;      // 2 E: the multiplier column of the edge's first / last flux row, -1
+  const int* rowptr;
+  int k, nf, per, edge_blocks;
+};
+
+__global__ __launch_bounds__(64 * kFesWaves) void k_fe_tasm(FeArgs a, FeTpl T) {
 #pragma clang fp contract(off)
-  const double v = a.tval[ent];
-  switch (a.kind[ent]) {
-    case kFeMass: return (a.edge_R[idx / a.N] * hc) * v;
-    case kFeSource: return ((a.edge_f ? a.edge_f[idx / a.N] : a.f) * hc) * v;
-    case kFeBc: return a.edge_bc[idx] * v;
-    default: return v;
-  }
-}
-// an edge entry's value from its local terms (fe_term's expressions: the same bits); the
-// table in LDS, the edge's R and cell lengths at hand
-__device__ __forceinline__ double fe_entry_loc(const FeTerm* t, int n, const int* sKind,
-                                               const double* sTv, double Re, const double* hh,
-                                               int c0) {
-#pragma clang fp contract(off)
-  double s = 0.0;
-  for (int u = 0; u < n; ++u) {
-    const double v = sTv[t[u].ent];
-    s += sKind[t[u].ent] == kFeMass ? (Re * hh[t[u].idx - c0]) * v : v;
-  }
-  return s;
-}
-// the edge's row r's position by binary search of its row pointers (rp[0 .. per])
-__device__ __forceinline__ int fe_row_of(const int* rp, int per, int q) {
-  int lo = 0, hi = per - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (rp[mid] <= q) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-__global__ __launch_bounds__(64 * kFesWaves) void k_assemble_fes(FeArgs a,
-                                                                  const int* __restrict__ rowptr,
-                                                                  const int* __restrict__ col,
-                                                                  int k, int edge_blocks) {
-#pragma clang fp contract(off)
-  __shared__ int sRp[kFesWaves][kFesRows];
-  __shared__ double sH[kFesWaves][kFesCells];
   __shared__ double sTv[kFesTable];
   __shared__ int sKind[kFesTable];
-  const int N = a.N, nf = k * N + 1, per = nf + N, nt = (k + 1) * (k + 1) + (k + 1) + 4;
+  const int N = a.N, nf = T.nf, per = T.per, nq = T.k + 1;
   const int64_t E = a.n_edges, nE = E * (int64_t)per;
-  FeTerm t[2];
-  if ((int)blockIdx.x >= edge_blocks) {  // the multiplier rows
-    const int64_t row = nE + (int64_t)(blockIdx.x - edge_blocks) * blockDim.x + threadIdx.x;
+  if ((int)blockIdx.x >= T.edge_blocks) {  // the multiplier rows: +-1 (one term each)
+    const int64_t row = nE + (int64_t)(blockIdx.x - T.edge_blocks) * blockDim.x + threadIdx.x;
     if (row >= a.n_rows) return;
     if (a.lhs)
-      for (int q = rowptr[row]; q < rowptr[row + 1]; ++q) {
-        const int n = fe_s_terms(row, col[q], k, N, E, t);
+      for (int q = T.rowptr[row]; q < T.rowptr[row + 1]; ++q) {
         double s = 0.0;
-        for (int u = 0; u < n; ++u) s += fe_term_h(a, t[u].idx, t[u].ent, 0.0);
+        for (int c = a.a_ptr[q]; c < a.a_ptr[q + 1]; ++c) s += fe_term(a, a.a_idx[c], a.a_ent[c]);
         a.val[q] = s;
       }
     if (a.do_rhs) a.rhs[row] = 0.0;  // (no terms)
     return;
   }
+  const int nt = nq * nq + nq + 4;
   for (int i = threadIdx.x; i < nt; i += blockDim.x) {
     sTv[i] = a.tval[i];
     sKind[i] = a.kind[i];
   }
+  __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * kFesWaves + w;
-  const int64_t r0 = e * per;
-  int* rp = sRp[w];
-  double* hh = sH[w];
-  if (e < E) {
-    for (int i = lane; i <= per; i += 64) rp[i] = rowptr[r0 + i];
-    for (int c = lane; c < N; c += 64) hh[c] = fe_cell_h(a.edge_x, e * N + c, N);
-  }
-  __syncthreads();
   if (e >= E) return;
-  const int q0 = rp[0], q1 = rp[per];
-  const int c0 = (int)(e * N);
-  const double Re = a.edge_R[e];
-  if (a.lhs)
-    for (int q = q0 + lane; q < q1; q += 64) {
-      const int pos = fe_row_of(rp, per, q);
-      const int64_t cq = col[q];
-      const int lc = cq >= nE ? -1 : (cq >= r0 && cq < r0 + per) ? (int)(cq - r0) : -2;
-      const int n = fe_s_terms_loc(pos, lc, k, N, c0, t);
-      a.val[q] = fe_entry_loc(t, n, sKind, sTv, Re, hh, c0);
-    }
-  if (a.do_rhs)
-    for (int r = lane; r < per; r += 64) {
-      const int n = fe_s_rhs_terms(r0 + r, k, N, E, t);
+  const int64_t c0 = e * N;
+  const double* __restrict__ hh = a.cellh + c0;
+  if (a.lhs) {
+    const int sh = T.shape[e];
+    const FeTplE* __restrict__ tp = T.tpl + T.off[sh];
+    const int L = T.off[sh + 1] - T.off[sh];
+    const int64_t q0 = T.rowptr[e * per];
+    const double Re = a.edge_R[e];
+    for (int i = lane; i < L; i += 64) {
+      const FeTplE t = tp[i];
       double s = 0.0;
-      for (int u = 0; u < n; ++u) {
-        const int ci = t[u].idx - c0;
-        s += fe_term_h(a, t[u].idx, t[u].ent, ci >= 0 && ci < N ? hh[ci] : 0.0);
+      if (t.n > 0) {
+        const double v = sTv[t.e0];
+        s += sKind[t.e0] == kFeMass ? (Re * hh[t.c0]) * v : v;
       }
-      a.rhs[r0 + r] = s;
+      if (t.n > 1) {
+        const double v = sTv[t.e1];
+        s += sKind[t.e1] == kFeMass ? (Re * hh[t.c1]) * v : v;
+      }
+      a.val[q0 + i] = s;
     }
+  }
+  if (a.do_rhs) {  // fe_s_rhs_terms: the source on the pressure rows, the end data
+    const int ent_src = nq * nq + nq + 2, ent_bc = ent_src + 1;
+    const double fe = a.edge_f ? a.edge_f[e] : a.f;
+    for (int r = lane; r < per; r += 64) {
+      double s = 0.0;
+      if (r >= nf) s += (fe * hh[r - nf]) * sTv[ent_src];
+      else if (r == 0) s += a.edge_bc[2 * e] * sTv[ent_bc];
+      else if (r == nf - 1) s += a.edge_bc[2 * e + 1] * sTv[ent_bc];
+      a.rhs[e * per + r] = s;
+    }
+  }
+}
+
+// The true residual r = b - A x of a (k, 0) system with A's entries formed again from the
+// templates (the CSR's values bit for bit while the coefficients are the assembled ones):
+// one wave per edge, a lane per row summing the row's products in CSR order; the multiplier
+// rows from the CSR in the blocks after the edges'. r into rout (a refinement pass starts
+// from it); block partials of ||r||^2, ||b||^2 for k_dir_publish.
+__global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, Csr A,
+                                                             const double* __restrict__ x,
+                                                             const double* __restrict__ b,
+                                                             double* __restrict__ rout,
+                                                             double* __restrict__ partials,
+                                                             int nblk) {
+#pragma clang fp contract(off)
+  __shared__ double sTv[kFesTable];
+  __shared__ int sKind[kFesTable];
+  const int N = a.N, per = T.per, nq = T.k + 1;
+  const int64_t E = a.n_edges, nE = E * (int64_t)per;
+  double rr = 0.0, bb = 0.0;
+  if ((int)blockIdx.x >= T.edge_blocks) {
+    const int64_t row = nE + (int64_t)(blockIdx.x - T.edge_blocks) * blockDim.x + threadIdx.x;
+    if (row < a.n_rows) {
+      double s = 0.0;
+      for (int q = A.rowptr[row]; q < A.rowptr[row + 1]; ++q) s += A.val[q] * x[A.col[q]];
+      const double bv = b[row], rv = bv - s;
+      rout[row] = rv;
+      rr = rv * rv;
+      bb = bv * bv;
+    }
+  } else {
+    const int nt = nq * nq + nq + 4;
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+      sTv[i] = a.tval[i];
+      sKind[i] = a.kind[i];
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t e = (int64_t)blockIdx.x * kFesWaves + w; e < E;
+         e += (int64_t)T.edge_blocks * kFesWaves) {
+      const int sh = T.shape[e];
+      const FeTplE* __restrict__ tp = T.tpl + T.off[sh];
+      const int* __restrict__ rs = T.rs + sh * (per + 1);
+      const double* __restrict__ hh = a.cellh + e * N;
+      const double* __restrict__ xe = x + e * per;
+      const double Re = a.edge_R[e];
+      const int l0 = T.lam[2 * e], l1 = T.lam[2 * e + 1];
+      for (int r = lane; r < per; r += 64) {
+        double s = 0.0;
+        for (int i = rs[r]; i < rs[r + 1]; ++i) {
+          const FeTplE t = tp[i];
+          double v = 0.0;
+          if (t.n > 0) {
+            const double tv = sTv[t.e0];
+            v += sKind[t.e0] == kFeMass ? (Re * hh[t.c0]) * tv : tv;
+          }
+          if (t.n > 1) {
+            const double tv = sTv[t.e1];
+            v += sKind[t.e1] == kFeMass ? (Re * hh[t.c1]) * tv : tv;
+          }
+          s += v * (t.lc >= 0 ? xe[t.lc] : x[r == 0 ? l0 : l1]);
+        }
+        const double bv = b[e * per + r], rv = bv - s;
+        rout[e * per + r] = rv;
+        rr += rv * rv;
+        bb += bv * bv;
+      }
+    }
+  }
+  block_sum_store(rr, partials + blockIdx.x);
+  __syncthreads();
+  block_sum_store(bb, partials + nblk + blockIdx.x);
 }
 
 // ---- (k, 0) through the condensed P1/DG0 system (nx_fe_set_direct). The divergence against
@@ -7949,129 +8014,107 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
   }
 }
 
-// (k, 0), first pass, fused: expand + the true residual in one launch (nx_fe_set_direct found
-// the row maps in closed form and k_assemble_fes forms the matrix). Every x value is a local
-// function of the auxiliary solution xa and b (vertex fluxes, pressures and multipliers are
-// copies, the interior fluxes from their cell), so one wave per edge forms its edge's x in
-// LDS, stores it, and forms its rows' residual r = b - A x with A's entries from the closed
-// form (fe_s_terms: the stored CSR's values bit for bit, the coefficients unchanged since the
-// lhs assembly) and the multiplier columns' x from xa; the multiplier rows (their columns are
-// edge-end fluxes, copies of xa) in the blocks after the edges'. Block partials of ||r||^2 and
-// ||b||^2 for k_dir_publish.
-struct FeFuse {
-  FeArgs a;
-  FeCond c;
-  const int* rowptr;
-  const int* col;
-  int k, edge_blocks;
-  const double* xa;
-  const double* b;
-  double* x;
-  double* rout;
-  double* partials;
-  int nblk;
-};
-__global__ __launch_bounds__(64 * kFesWaves) void k_fe_expand_res(FeFuse F) {
-#pragma clang fp contract(off)
-  __shared__ int sRp[kFesWaves][kFesRows];
-  __shared__ double sH[kFesWaves][kFesCells];
-  __shared__ double sX[kFesWaves][kFesRows];
-  __shared__ double sP[kFesWaves][kFesNnz];
-  __shared__ double sTv[kFesTable];
-  __shared__ int sKind[kFesTable];
-  const FeArgs& a = F.a;
-  const FeCond& c = F.c;
-  const int N = a.N, k = F.k, km = k - 1, nf = k * N + 1, per = nf + N;
-  const int nt = (k + 1) * (k + 1) + (k + 1) + 4;
-  const int64_t E = a.n_edges, nE = E * (int64_t)per;
+// The (k, 0) edge templates (FeTpl): each edge shape's entries from its first edge, every
+// other edge's rows checked against its shape (row lengths and local columns); false (the
+// gather kernels stay) on any difference or a template beyond the int16 fields.
+bool fe_build_tpl(nx_network* h, int k, int32_t N, int64_t E, const int32_t* rowptr,
+                  const int32_t* col) {
+  const int nf = k * N + 1, per = nf + N;
+  const int64_t nE = E * (int64_t)per;
+  if (per >= 32767 || N >= 32767) return false;
+  std::vector<FeTplE> shape_t[4];
+  std::vector<int> shape_rs[4];
+  bool have[4] = {false, false, false, false};
+  std::vector<int> shape((size_t)E), lam((size_t)2 * E);
   FeTerm t[2];
-  double rr = 0.0, bb = 0.0;
-  if ((int)blockIdx.x >= F.edge_blocks) {  // the multiplier rows
-    const int64_t row = nE + (int64_t)(blockIdx.x - F.edge_blocks) * blockDim.x + threadIdx.x;
-    if (row < a.n_rows) {
-      const int64_t li = row - nE;
-      F.x[row] = F.xa[c.laux[li]];
-      double s = 0.0;
-      for (int q = F.rowptr[row]; q < F.rowptr[row + 1]; ++q) {
-        const int cq = F.col[q];
-        const int n = fe_s_terms(row, cq, k, N, E, t);
-        double v = 0.0;
-        for (int u = 0; u < n; ++u) v += fe_term_h(a, t[u].idx, t[u].ent, 0.0);
-        const int64_t e2 = cq / per;  // an edge-end flux: its vertex's copy of xa
-        const int pos = (int)(cq - e2 * per);
-        s += v * F.xa[c.vaux[e2 * (N + 1) + pos / k]];
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t r0 = e * per;
+    int l0 = -1, l1 = -1;
+    for (int q = rowptr[r0]; q < rowptr[r0 + 1]; ++q)
+      if (col[q] >= nE) l0 = col[q];
+    for (int q = rowptr[r0 + nf - 1]; q < rowptr[r0 + nf]; ++q)
+      if (col[q] >= nE) l1 = col[q];
+    const int sh = (l0 >= 0 ? 1 : 0) | (l1 >= 0 ? 2 : 0);
+    shape[e] = sh;
+    lam[2 * e] = l0;
+    lam[2 * e + 1] = l1;
+    std::vector<FeTplE>& tp = shape_t[sh];
+    std::vector<int>& rs = shape_rs[sh];
+    if (!have[sh]) {
+      have[sh] = true;
+      rs.assign(per + 1, 0);
+      for (int pos = 0; pos < per; ++pos) {
+        rs[pos] = (int)tp.size();
+        for (int q = rowptr[r0 + pos]; q < rowptr[r0 + pos + 1]; ++q) {
+          const int64_t cq = col[q];
+          int lc;
+          if (cq >= nE) {
+            if (pos != 0 && pos != nf - 1) return false;
+            lc = -1;
+          } else if (cq >= r0 && cq < r0 + per) {
+            lc = (int)(cq - r0);
+          } else {
+            return false;  // another edge's column: not a (k, 0) edge
+          }
+          const int n = fe_s_terms_loc(pos, lc, k, N, 0, t);
+          if (n < 1 || n > 2) return false;
+          FeTplE x{};
+          x.pos = (short)pos;
+          x.lc = (short)lc;
+          x.n = (short)n;
+          x.c0 = (short)t[0].idx;
+          x.e0 = (short)t[0].ent;
+          x.c1 = (short)(n > 1 ? t[1].idx : 0);
+          x.e1 = (short)(n > 1 ? t[1].ent : 0);
+          tp.push_back(x);
+        }
       }
-      const double bv = F.b[row], rv = bv - s;
-      F.rout[row] = rv;
-      rr = rv * rv;
-      bb = bv * bv;
+      rs[per] = (int)tp.size();
+      if (tp.size() > 30000) return false;
+      continue;
     }
-  } else {
-    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
-      sTv[i] = a.tval[i];
-      sKind[i] = a.kind[i];
-    }
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int* rp = sRp[w];
-    double* hh = sH[w];
-    double* xs = sX[w];
-    double* pr = sP[w];
-    const double* K = c.cst + 2 * km;
-    const double* Mii = c.cst + 4 * km;
-    // (edge rounds: the partials hold nblk blocks; the loop condition is block-uniform)
-    for (int64_t eb0 = (int64_t)blockIdx.x * kFesWaves; eb0 < E;
-         eb0 += (int64_t)F.edge_blocks * kFesWaves) {
-      const int64_t e = eb0 + w;
-      const int64_t r0 = e * per;
-      const int c0 = (int)(e * N);
-      __syncthreads();  // (the previous round's LDS reads)
-      if (e < E) {
-        for (int i = lane; i <= per; i += 64) rp[i] = F.rowptr[r0 + i];
-        for (int g = lane; g < N; g += 64) hh[g] = fe_cell_h(a.edge_x, e * N + g, N);
-        for (int g = lane; g <= N; g += 64) xs[g * k] = F.xa[c.vaux[e * (N + 1) + g]];
-        for (int g = lane; g < N; g += 64) xs[nf + g] = F.xa[c.paux[e * N + g]];
+    if (rowptr[r0 + per] - rowptr[r0] != rs[per]) return false;
+    for (int pos = 0; pos < per; ++pos) {
+      if (rowptr[r0 + pos + 1] - rowptr[r0 + pos] != rs[pos + 1] - rs[pos]) return false;
+      for (int q = rowptr[r0 + pos], i = rs[pos]; q < rowptr[r0 + pos + 1]; ++q, ++i) {
+        const int64_t cq = col[q];
+        const int lc = cq >= nE ? -1 : (cq >= r0 && cq < r0 + per) ? (int)(cq - r0) : -2;
+        if (lc != tp[i].lc) return false;
       }
-      __syncthreads();
-      const double Re = e < E ? a.edge_R[e] : 0.0;
-      if (e < E)
-        for (int q = lane; q < N * km; q += 64) {  // interior flux j of cell g (k_fe_expand's)
-          const int g = q / km, j = q - g * km;
-          const int64_t cell = e * N + g;
-          const double Rh = Re * hh[g];
-          const double xl = xs[g * k], xr = xs[(g + 1) * k];
-          double s = 0.0;
-          for (int i = 0; i < km; ++i) s += Mii[j * km + i] * F.b[c.ife[cell * km + i]];
-          xs[g * k + 1 + j] = s / Rh - K[2 * j] * xl - K[2 * j + 1] * xr;
-        }
-      __syncthreads();
-      if (e < E) {
-        for (int i = lane; i < per; i += 64) F.x[r0 + i] = xs[i];
-        const int q0 = rp[0], q1 = rp[per];
-        for (int q = q0 + lane; q < q1; q += 64) {  // products, coalesced over the nonzeros
-          const int pos = fe_row_of(rp, per, q);
-          const int64_t cq = F.col[q];
-          const int lc = cq >= nE ? -1 : (cq >= r0 && cq < r0 + per) ? (int)(cq - r0) : -2;
-          const int n = fe_s_terms_loc(pos, lc, k, N, c0, t);
-          const double v = fe_entry_loc(t, n, sKind, sTv, Re, hh, c0);
-          pr[q - q0] = v * (lc >= 0 ? xs[lc] : F.xa[c.laux[cq - nE]]);
-        }
-      }
-      __syncthreads();
-      if (e < E)
-        for (int i = lane; i < per; i += 64) {  // row r0 + i's residual, in CSR order
-          const int q0 = rp[0];
-          double s = 0.0;
-          for (int q = rp[i]; q < rp[i + 1]; ++q) s += pr[q - q0];
-          const double bv = F.b[r0 + i], rv = bv - s;
-          F.rout[r0 + i] = rv;
-          rr += rv * rv;
-          bb += bv * bv;
-        }
     }
   }
-  block_sum_store(rr, F.partials + blockIdx.x);
-  __syncthreads();
-  block_sum_store(bb, F.partials + F.nblk + blockIdx.x);
+  std::vector<FeTplE> all;
+  std::vector<int> off(5, 0), rs_all((size_t)4 * (per + 1), 0);
+  for (int sh = 0; sh < 4; ++sh) {
+    off[sh] = (int)all.size();
+    all.insert(all.end(), shape_t[sh].begin(), shape_t[sh].end());
+    if (have[sh])
+      std::copy(shape_rs[sh].begin(), shape_rs[sh].end(), rs_all.begin() + (size_t)sh * (per + 1));
+  }
+  off[4] = (int)all.size();
+  if (all.empty()) return false;
+  FeTplE* d_t = nullptr;
+  if (hipMalloc(&d_t, sizeof(FeTplE) * all.size()) != hipSuccess) return false;
+  h->fe_tpl_buf = d_t;
+  if (hipMemcpy(d_t, all.data(), sizeof(FeTplE) * all.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return false;
+  if (upload(&h->fe_tpl_off, off.data(), 5, h->stream) ||
+      upload(&h->fe_tpl_rs, rs_all.data(), (int64_t)rs_all.size(), h->stream) ||
+      upload(&h->fe_tpl_shape, shape.data(), E, h->stream) ||
+      upload(&h->fe_tpl_lam, lam.data(), 2 * E, h->stream) ||
+      hipStreamSynchronize(h->stream) != hipSuccess)
+    return false;
+  return true;
+}
+int fe_per(const nx_network* h) { return h->fe_sk * (int)h->N + 1 + (int)h->N; }
+bool fe_tpl_on(const nx_network* h) {
+  const char* e = std::getenv("NXHIP_FE_STRUCT");  // read per launch: tests switch it
+  return h->fe_tpl && (e == nullptr || std::atoi(e) != 0);
+}
+FeTpl fe_tpl_args(const nx_network* h, int edge_blocks) {
+  return FeTpl{static_cast<const FeTplE*>(h->fe_tpl_buf), h->fe_tpl_off, h->fe_tpl_rs,
+               h->fe_tpl_shape, h->fe_tpl_lam, h->rowptr, h->fe_sk, h->fe_sk * (int)h->N + 1,
+               fe_per(h), edge_blocks};
 }
 
 // terms [ptr[i], ptr[i+1]) of every output i must reference the table and the cell / edge
@@ -8105,7 +8148,7 @@ int fe_struct_degree(int32_t N, int64_t E, int64_t n_rows, const int32_t* rowptr
         n_rows >= E * (int64_t)(kk * N + 1 + N))
       k = kk;
   if (!k || k * N + 1 + N + 1 > kFesRows || N > kFesCells || n_table > kFesTable)
-    return 0;  // (k_assemble_fes' LDS)
+    return 0;  // (the template sizes)
   FeTerm t[2];
   for (int64_t r = 0; r < n_rows; ++r) {
     for (int q = rowptr[r]; q < rowptr[r + 1]; ++q) {
@@ -8191,11 +8234,7 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
   }
   h->fe_sk = fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr, a_idx, a_ent,
                               b_ptr, b_idx, b_ent);
-  if (h->fe_sk > 0) {  // (k_fe_expand_res stages an edge's nonzeros in LDS)
-    const int64_t per = h->fe_sk * (int64_t)N + 1 + N;
-    for (int64_t e = 0; e < n_edges; ++e)
-      h->fe_edge_nnz = std::max<int64_t>(h->fe_edge_nnz, rowptr[(e + 1) * per] - rowptr[e * per]);
-  }
+  if (h->fe_sk > 0) h->fe_tpl = fe_build_tpl(h, h->fe_sk, N, n_edges, rowptr, col);
   *out = h;
   return NX_OK;
 }
@@ -8236,7 +8275,8 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->fe_laux, h->fe_cst, h->fe_cellh, h->d_cyc_qloc, h->d_cyc_lcol, h->cyc_u,
                   h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_tI,
                   h->cp_eb, h->cp_nrow, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
-                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown};
+                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown, h->fe_tpl_buf,
+                  h->fe_tpl_off, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -8330,15 +8370,12 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
              h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx, h->fe_bent,
              h->nnz, h->n_own, h->val, h->rhs, lhs, rhs, h->E, h->fe_cellh};
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
-    // NXHIP_FE_STRUCT=1: the closed-form kernel (measured slower than the gather tables at
-    // C3: latency-bound, one wave per edge), else the gather tables
-    const char* es = std::getenv("NXHIP_FE_STRUCT");
-    if (h->fe_sk > 0 && es != nullptr && std::atoi(es) != 0) {
+    // (k, 0): the edge templates (NXHIP_FE_STRUCT=0: the gather tables), else the tables
+    if (fe_tpl_on(h)) {
       const int eb = (int)grid_of(h->E, kFesWaves);
-      const int64_t nE = h->E * (int64_t)(h->fe_sk * h->N + 1 + h->N);
-      const int lb = (int)grid_of(h->n_own - nE, 64 * kFesWaves);
-      hipExtLaunchKernelGGL(k_assemble_fes, dim3(eb + lb), dim3(64 * kFesWaves), 0, s, e0, e1, 0,
-                            a, h->rowptr, h->col, h->fe_sk, eb);
+      const int lb = (int)grid_of(h->n_own - h->E * (int64_t)fe_per(h), 64 * kFesWaves);
+      hipExtLaunchKernelGGL(k_fe_tasm, dim3(eb + lb), dim3(64 * kFesWaves), 0, s, e0, e1, 0, a,
+                            fe_tpl_args(h, eb));
     } else {
       hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
                             dim3(kBlock), 0, s, e0, e1, 0, a);
@@ -9124,13 +9161,17 @@ bool xr_on(const Team& t, bool with_asm) {
 // writes them (dstep_multi).
 DirStep dir_args(nx_network* h, double rtol) {
   h->dq_stale = !h->dstep_multi;
-  return DirStep{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
+  DirStep d{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
                  h->val, h->rhs, h->dstep_multi ? h->dq : nullptr, h->nnz_lm, h->B, h->lm_val, h->val + h->nnz_edges,
                  h->rhs + h->n_edge_dofs, h->x, h->d_chain_post, h->d_left_off, h->n_left,
                  h->d_post, h->d_dsync, h->dstep_epoch, h->dstep_polls, rtol, h->seq + 1,
                  h->d_seq, h->d_last, h->dir_bb, h->d_job_hdr, h->d_crec, h->d_ci,
                  h->dstep_main, h->dstep_top, nullptr, XPeer{}, 0, 0, 0, 0, 0, 0u,
-                 {kDirWaitPolls, kDirWaitPolls}};
+                 {kDirWaitPolls, kDirWaitPolls}, 0};
+#ifdef NX_PHASE_TIMING
+  if (const char* e = std::getenv("NXHIP_LEDGER")) d.ledger = std::atoi(e);
+#endif
+  return d;
 }
 // the exchange fields of rank h's launch among X ranks (its own mailbox, the peers' table)
 void xr_fill(nx_network* h, DirStep& da, int X) {
@@ -9759,26 +9800,21 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
       a->stream = as;
       CHECK(rc);
     }
-    // NXHIP_FE_FUSE=1: expand + residual fused (measured slower at C3)
-    const char* ef = std::getenv("NXHIP_FE_FUSE");
-    const int64_t nE = h->E * (int64_t)(h->fe_k * h->N + 1 + h->N);
-    const int lb = grid_of(h->n_own - nE, 64 * kFesWaves);
-    const int eb = std::max(1, std::min(grid_of(h->E, kFesWaves), h->nblk - lb));
-    if (pass == 0 && h->fe_fuse && h->fe_sk == h->fe_k && h->asm_coef_version == h->coef_version &&
-        eb + lb <= h->nblk && ef != nullptr && std::atoi(ef) != 0) {
-      const int nblk = eb + lb;  // (<= h->nblk: the partials' size)
-      const FeFuse F{FeArgs{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind,
-                            h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr,
-                            h->fe_bidx, h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E,
-                            h->fe_cellh},
-                     c, h->rowptr, h->col, h->fe_k, eb, a->x, h->rhs, h->x, h->tmp, h->partials,
-                     nblk};
-      hipLaunchKernelGGL(k_fe_expand_res, dim3(nblk), dim3(64 * kFesWaves), 0, h->stream, F);
+    hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
+                       c, a->x, b, h->x, pass);
+    if (fe_tpl_on(h) && h->asm_coef_version == h->coef_version) {
+      // the true residual from the templates (A's entries formed again: no CSR reads)
+      const int lb = grid_of(h->n_own - h->E * (int64_t)fe_per(h), 64 * kFesWaves);
+      const int eb = std::max(1, std::min(grid_of(h->E, kFesWaves), h->nblk - lb));
+      const FeArgs fa{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind,
+                      h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx,
+                      h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E, h->fe_cellh};
+      hipLaunchKernelGGL(k_fe_tres, dim3(eb + lb), dim3(64 * kFesWaves), 0, h->stream, fa,
+                         fe_tpl_args(h, eb), csr_of(h), h->x, h->rhs, h->tmp, h->partials,
+                         eb + lb);
       hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                         nblk, rtol, h->d_seq, h->d_last);
+                         eb + lb, rtol, h->d_seq, h->d_last);
     } else {
-      hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
-                         c, a->x, b, h->x, pass);
       hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
                          h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
       hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
@@ -11254,20 +11290,6 @@ NX_API int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64
   h->fe_k = k;
   h->fe_nl = (int)n_lm;
   h->fe_ab = ab;
-  {  // the fused expand + residual: the (k, 0) closed form and its row maps
-    const int64_t per = k * N + 1 + N, nE = E * per;
-    bool ok = h->fe_sk == k && h->fe_edge_nnz <= kFesNnz;
-    for (int64_t e = 0; e < E && ok; ++e) {
-      for (int64_t g = 0; g <= N && ok; ++g) ok = v_fe[e * (N + 1) + g] == e * per + g * k;
-      for (int64_t g = 0; g < N && ok; ++g) {
-        ok = p_fe[e * N + g] == e * per + k * N + 1 + g;
-        for (int64_t j = 0; j < km && ok; ++j)
-          ok = i_fe[(e * N + g) * km + j] == e * per + g * k + 1 + j;
-      }
-    }
-    for (int64_t i = 0; i < n_lm && ok; ++i) ok = l_fe[i] == nE + i;
-    h->fe_fuse = ok;
-  }
   return NX_OK;
 }
 

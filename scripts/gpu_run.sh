@@ -11,6 +11,7 @@
 # wcal         WRITE_SIZE calibration on known write streams   -> <tag>_wcal_*, wcal_<tag>/
 # rehearsal    the 8-rank C4 group rehearsal under rocprof + per-rank kernel times
 # fe_prof      rocprof kernel stats of the (2, 0) condensed solve at C3
+# ledger       k_dir_step store ledger (debug build, WRITE_SIZE per class) -> <tag>_ledger.json
 # cmd:<c>      any command (e.g. cmd:"python scripts/direct_timing.py 18")
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(pwd)
@@ -56,6 +57,18 @@ for s in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && step wcal_pmc 120 "$R/gpurun_out/${T}_wcal_pmc.log" \
         rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/wcal_$T" -o pmc --output-format csv \
         -- "$R/gpurun_out/write_ceiling") || exit $? ;;
+    ledger)  # k_dir_step's store ledger: one WRITE_SIZE pass per dropped store class
+      for m in 0 1 2 4 16; do
+        mkdir -p "gpurun_out/ledger_$T/m$m"
+        (cd /tmp && export TMPDIR=/tmp NXHIP_LIB="$R/networks_fenicsx_amd/libnxhip_phase.so" \
+          NXHIP_LEDGER=$m && step "ledger_m$m" 120 "$R/gpurun_out/ledger_$T/m$m/run.log" \
+          rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/ledger_$T/m$m" -o pmc --output-format csv \
+          -- python3 "$R/scripts/store_ledger.py" run 6) || exit $?
+        f=$(find "gpurun_out/ledger_$T/m$m" -name 'pmc_counter_collection.csv' | head -n 1)
+        [ -n "$f" ] && cp "$f" "gpurun_out/ledger_$T/m$m/pmc_counter_collection.csv" 2>/dev/null
+      done
+      python scripts/store_ledger.py summarize "gpurun_out/ledger_$T" > "gpurun_out/${T}_ledger.json" 2>&1
+      cat "gpurun_out/${T}_ledger.json" ;;
     cmd)
       step cmd 600 "gpurun_out/${T}_cmd.log" bash -c "$arg" || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -1,10 +1,11 @@
 """The (k, 0) structured assembly's closed form (CPU; nx_fe_struct_degree, no device).
 
-k_assemble_fes forms every CSR entry and rhs row of a (k, 0) layout from (row, col) alone.
-nx_create_fe switches to it only after nx_fe_struct_degree has found every entry's term list
--- (index, table entry), in summation order -- equal to the gather tables layout_fe builds,
-so the structured kernel adds the same terms in the same order as k_assemble_fe (the CSR
-stays bit-exact against layout_fe.evaluate_terms, tests/test_gpu_fe.py). Here: the check
+fe_s_terms gives every CSR entry and rhs row of a (k, 0) layout from (row, col) alone.
+nx_create_fe builds its edge templates (k_fe_tasm, k_fe_tres) only after
+nx_fe_struct_degree has found every entry's term list -- (index, table entry), in summation
+order -- equal to the gather tables layout_fe builds, so the template kernels add the same
+terms in the same order as k_assemble_fe (the CSR stays bit-exact against
+layout_fe.evaluate_terms, tests/test_gpu_fe.py). Here: the check
 accepts every (k, 0) layout of the test graphs, rejects continuous pressure and any table
 that differs in one term."""
 

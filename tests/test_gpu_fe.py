@@ -54,7 +54,7 @@ def _edge_bc(F, pbc):
 
 @pytest.mark.parametrize("case", ["Y_N4", "edge_info_N10", "depth6_N40"])
 @pytest.mark.parametrize("km", PAIRS)
-@pytest.mark.parametrize("struct", ["1", "0"])  # (k, 0): k_assemble_fes (opt-in) / the gather tables
+@pytest.mark.parametrize("struct", ["1", "0"])  # (k, 0): the edge templates (default) / the gather tables
 def test_fe_csr_and_rhs(case, km, struct, monkeypatch):
     monkeypatch.setenv("NXHIP_FE_STRUCT", struct)
     R = 1.0 + np.arange(len(CASES[case][0]().edges())) % 3
@@ -174,15 +174,16 @@ def test_fe_single_edge(km):
 @pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "depth6_N40", "arterial5_N40",
                                   "tree6_2d_N70"])
 @pytest.mark.parametrize("k", [2, 3, 4])
-@pytest.mark.parametrize("fuse", ["1", "0"])  # expand + residual fused (k_fe_expand_res, opt-in) or not
-def test_fe_direct_condensed(case, k, fuse, monkeypatch):
+@pytest.mark.parametrize("struct", ["1", "0"])  # residual from the edge templates (default) / the CSR
+def test_fe_direct_condensed(case, k, struct, monkeypatch):
     """(k, 0) through the condensed P1/DG0 system (nx_fe_set_direct): the direct path runs
     (no MINRES), within SOL_TOL of the oracle's LU, its reported residual is the true one,
     <= 1e-12 after at most two refinement passes; a second solve with other coefficients
-    (the auxiliary lumped mass rebuilt) stays exact."""
+    (the auxiliary lumped mass rebuilt) stays exact. Both residual kernels (k_fe_tres from the
+    edge templates, k_residual_ck from the CSR) report it."""
     E = len(CASES[case][0]().edges())
     R = 1.0 + 0.5 * (np.arange(E) % 3)
-    monkeypatch.setenv("NXHIP_FE_FUSE", fuse)
+    monkeypatch.setenv("NXHIP_FE_STRUCT", struct)
     mesh, asm, F, A, b, pbc = _setup(case, (k, 0), f=0.4, R=R)
     assert asm.fe_direct_available
     solver = Solver(asm)
