@@ -988,6 +988,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_slot(const double* __restrict
 // A chain is processed by a W-lane segment, CPL cells per lane (N <= W*CPL).
 struct PcArgs {
   int N;
+  // 1 / N, formed once on the host (correctly rounded: the device's 1.0 / (double)N, bit for
+  // bit) -- a uniform the fused kernels would otherwise form in VGPRs and spill
+  double invN;
   const int* chain_edge;
   const int* chain_flip;
   const int* chain_up;
@@ -1232,6 +1235,16 @@ __device__ __forceinline__ void pc_coarse_partials(const PcArgs& pa, int ts0, in
   }
 }
 
+// The lane's position in its chain, formed afresh where a helper needs it: the values
+// derived from it (cell indices) then live only inside the helper instead of through phase 2
+// (k_dir_step spilled two of them to scratch at its 128-VGPR budget)
+template <int W>
+__device__ __forceinline__ int lane_of() {
+  int l = threadIdx.x & (W - 1);
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
 template <int W>
 __device__ __forceinline__ double seg_incl_scan(double v) {
   const int l = threadIdx.x & (W - 1);
@@ -1322,7 +1335,7 @@ __device__ __forceinline__ void chain_mass_solve(const PcArgs& pa, const ChainLa
                                                  double (&out)[CPL + 1]) {
   constexpr int NE = CPL + 1;
   const int N = pa.N;
-  const int l = threadIdx.x & (W - 1);
+  const int l = lane_of<W>();
   const double* __restrict__ lu = pa.Tlu;
   bool on[NE];
   double v[NE], lk[NE], iu[NE];
@@ -1666,7 +1679,7 @@ __device__ __forceinline__ void direct_cell_inputs(const PcArgs& pa, const Chain
   double yv[CPL + 1];
   chain_mass_solve<W, CPL>(pa, ch, bq, bqN, yv);
   const int N = pa.N;
-  const int l = threadIdx.x & (W - 1);
+  const int l = lane_of<W>();
   const double nxt0 = __shfl_down(yv[0], 1, W);
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
@@ -1697,7 +1710,7 @@ __device__ __forceinline__ void direct_flux_cons(const ChainLane<W, CPL>& ch, in
                                                  const double* bc, const double* bq, double bqN,
                                                  double zt, double zb, double (&out)[CPL + 1]) {
 #pragma clang fp contract(off)
-  const int l = threadIdx.x & (W - 1);
+  const int l = lane_of<W>();
   double loc = 0.0;
 #pragma unroll
   for (int t = 0; t < CPL; ++t)
@@ -1746,7 +1759,7 @@ __device__ __forceinline__ void chain_cell_mo(const PcArgs& pa, const ChainLane<
     x1[i] = pa.edge_x[6 * (int64_t)e + 3 + i];
   }
   const double R = pa.edge_R[e];
-  const double invN = 1.0 / (double)N;
+  const double invN = pa.invN;
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
     mo[t] = 0.0;
@@ -1779,7 +1792,7 @@ __device__ __forceinline__ void direct_residual(const PcArgs& pa, const ChainLan
                                                 double* sQt, double* sQb, int lc) {
 #pragma clang fp contract(off)
   const int N = pa.N;
-  const int l = threadIdx.x & (W - 1);
+  const int l = lane_of<W>();
   const double sg = flip ? -1.0 : 1.0;
   // md = R h / 3 = 2 mo exactly (mo = R h / 6: halving is exact in binary)
   double md[CPL];
@@ -3483,7 +3496,7 @@ __device__ __forceinline__ void dir_lane_chain(const PcArgs& pa, const DirLane<W
                                                bool active, ChainLane<W, CPL>& ch) {
 #pragma clang fp contract(off)
   const int N = pa.N;
-  const int l = threadIdx.x & (W - 1);
+  const int l = lane_of<W>();
   const int flip = L.flip;
   const int64_t base = (int64_t)L.e * (2 * N + 1);
   const double* md = L.md;
@@ -3559,7 +3572,7 @@ __device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& d
   L.s = da.edge_lm[2 * (int64_t)e] >= 0;
   L.sg0 = da.edge_seg[e];
   L.seglen = da.edge_seg[e + 1] - L.sg0;
-  const double invN = 1.0 / (double)N;
+  const double invN = pa.invN;
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
     const int k = l * CPL + t;
@@ -4053,6 +4066,16 @@ struct ChainRec {
   int e, flip, s, sg0, seglen;
 };
 
+// The lane's chain c0 + threadIdx.x / W, formed afresh: a re-assembly late in the step then
+// forms its record addresses again instead of keeping the first load's (a 64-bit address
+// live through the whole step -- spilled to scratch at the 128-VGPR budget)
+template <int W>
+__device__ __forceinline__ int fresh_chain(int c0) {
+  int c = c0 + (int)threadIdx.x / W;
+  asm volatile("" : "+v"(c));
+  return c;
+}
+
 __device__ __forceinline__ void chain_rec_load(const DirStep& da, int c, bool active,
                                                ChainRec& r) {
   const int cc = active ? c : 0;
@@ -4087,7 +4110,7 @@ __device__ __forceinline__ void dir_chain_asm_rec(const PcArgs& pa, const ChainR
   L.s = r.s;
   L.sg0 = r.sg0;
   L.seglen = r.seglen;
-  const double invN = 1.0 / (double)N;
+  const double invN = pa.invN;
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
     const int k = l * CPL + t;
@@ -5135,7 +5158,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
       } else {  // its lanes again: not kept through the solve
-        chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+        chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
         dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
       }
     } else {
@@ -5233,11 +5256,11 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   // (the kernel's end, not the published state, waits for these; re-assembled: L kept
   // through phase 2 would overflow the register budget there)
   if (late_store) {  // one job: the top solver's own
-    chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+    chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
     dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
     dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
   } else if (defer_free && (int)threadIdx.x / W < gF) {  // the free waves' chains
-    chain_rec_load(da, c0 + (int)threadIdx.x / W, lane_on, rec);
+    chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
     dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
     dir_chain_store<W, CPL>(pa, da, lane_on, L);
   }
@@ -10488,6 +10511,7 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
   };
   PcArgs pa{};
   pa.N = N;
+  pa.invN = 1.0 / (double)N;
   pa.chain_edge = up(chain_edge, n_chains);
   pa.chain_flip = up(chain_flip, n_chains);
   pa.chain_up = up(chain_up, n_chains);
