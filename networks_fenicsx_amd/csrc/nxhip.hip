@@ -6534,8 +6534,9 @@ struct nx_network {
   // (k, 0) edge templates (fe_build_tpl; k_fe_tasm / k_fe_tres): entries, shape offsets,
   // shape row starts, the edges' shapes and multiplier columns
   bool fe_tpl = false;
-  void* fe_tpl_buf = nullptr;
-  int *fe_tpl_off = nullptr, *fe_tpl_rs = nullptr, *fe_tpl_shape = nullptr, *fe_tpl_lam = nullptr;
+  int2* fe_tpl_buf = nullptr;  // packed entries (fe_tpl_pack)
+  int fe_tpl_off[5] = {0, 0, 0, 0, 0};
+  int *fe_tpl_rs = nullptr, *fe_tpl_shape = nullptr, *fe_tpl_lam = nullptr;
   double* fe_cellh = nullptr;  // E*N cell lengths (k_fe_cellh at nx_create_fe)
   int *fe_slot = nullptr, *fe_vfe = nullptr, *fe_vaux = nullptr, *fe_ife = nullptr;
   int *fe_pfe = nullptr, *fe_paux = nullptr, *fe_lfe = nullptr, *fe_laux = nullptr;
@@ -7502,18 +7503,60 @@ struct FeTplE {
   short e0, e1;   // their table entries
   short pad;
 };
+// An entry packed for LDS: x = c0 | c1 << 16, y = e0 | e1 << 7 | n << 14 | (lc + 1) << 16
+__host__ __device__ __forceinline__ int2 fe_tpl_pack(const FeTplE& t) {
+  return int2{(int)((unsigned)(unsigned short)t.c0 | ((unsigned)(unsigned short)t.c1 << 16)),
+              (int)((unsigned)t.e0 | ((unsigned)t.e1 << 7) | ((unsigned)t.n << 14) |
+                    ((unsigned)(t.lc + 1) << 16))};
+}
 struct FeTpl {
-  const FeTplE* tpl;
-  const int* off;      // 5: each shape's first entry
+  const int2* tpl;     // packed entries, the four shapes one after another
   const int* rs;       // 4 x (per + 1): each shape's row starts (entry index)
   const int* shape;    // E: the edge's shape (bit 0: multiplier at row 0, bit 1: at row nf - 1)
   const int* lam;      // 2 E: the multiplier column of the edge's first / last flux row, -1
   const int* rowptr;
+  int off[5];          // each shape's first entry; off[4] = all
   int k, nf, per, edge_blocks;
 };
+constexpr int kFeTplMax = 4096;  // packed entries (LDS: 32 KiB)
 
+// one packed entry's value: its terms in order, s = 0 + t0 (+ t1), as fe_term forms them
+__device__ __forceinline__ double fe_tpl_val(int2 t, const double* sTv, const int* sKind, double Re,
+                                             const double* hh) {
+#pragma clang fp contract(off)
+  const int n = (t.y >> 14) & 3, e0 = t.y & 127, e1 = (t.y >> 7) & 127;
+  double s = 0.0;
+  if (n > 0) {
+    const double v = sTv[e0];
+    s += sKind[e0] == kFeMass ? (Re * hh[t.x & 0xffff]) * v : v;
+  }
+  if (n > 1) {
+    const double v = sTv[e1];
+    s += sKind[e1] == kFeMass ? (Re * hh[(unsigned)t.x >> 16]) * v : v;
+  }
+  return s;
+}
+
+// Dynamic LDS of k_fe_tasm / k_fe_tres (doubles): the packed templates, the row starts, then
+// per wave its edge's cell lengths (and for the residual its x)
+size_t fe_tpl_lds(int n_tpl, int per, int N, bool res) {
+  return 8 * ((size_t)n_tpl + (4 * (size_t)(per + 1) + 1) / 2 +
+              (size_t)kFesWaves * (N + (res ? per : 0)));
+}
+
+// The templates (and row starts) into LDS, once per workgroup
+__device__ __forceinline__ void fe_tpl_stage(const FeTpl& T, int2* sT, int* sRs) {
+  for (int i = threadIdx.x; i < T.off[4]; i += blockDim.x) sT[i] = T.tpl[i];
+  for (int i = threadIdx.x; i < 4 * (T.per + 1); i += blockDim.x) sRs[i] = T.rs[i];
+}
+
+// Assembly: one wave per edge, the edges in workgroup rounds (the LDS staging amortised); the
+// edge's cell lengths loaded once (coalesced), every entry then from LDS alone; values and
+// rhs stored coalesced over the edge's contiguous segment and rows. The multiplier rows
+// (+-1) from the tables, in the blocks after the edges'.
 __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tasm(FeArgs a, FeTpl T) {
 #pragma clang fp contract(off)
+  extern __shared__ double fe_lds[];
   __shared__ double sTv[kFesTable];
   __shared__ int sKind[kFesTable];
   const int N = a.N, nf = T.nf, per = T.per, nq = T.k + 1;
@@ -7530,55 +7573,55 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tasm(FeArgs a, FeTpl T) {
     if (a.do_rhs) a.rhs[row] = 0.0;  // (no terms)
     return;
   }
+  int2* sT = reinterpret_cast<int2*>(fe_lds);
+  int* sRs = reinterpret_cast<int*>(fe_lds + T.off[4]);
+  double* sH = fe_lds + T.off[4] + (4 * (per + 1) + 1) / 2;
   const int nt = nq * nq + nq + 4;
   for (int i = threadIdx.x; i < nt; i += blockDim.x) {
     sTv[i] = a.tval[i];
     sKind[i] = a.kind[i];
   }
-  __syncthreads();
+  fe_tpl_stage(T, sT, sRs);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t e = (int64_t)blockIdx.x * kFesWaves + w;
-  if (e >= E) return;
-  const int64_t c0 = e * N;
-  const double* __restrict__ hh = a.cellh + c0;
-  if (a.lhs) {
-    const int sh = T.shape[e];
-    const FeTplE* __restrict__ tp = T.tpl + T.off[sh];
-    const int L = T.off[sh + 1] - T.off[sh];
-    const int64_t q0 = T.rowptr[e * per];
-    const double Re = a.edge_R[e];
-    for (int i = lane; i < L; i += 64) {
-      const FeTplE t = tp[i];
-      double s = 0.0;
-      if (t.n > 0) {
-        const double v = sTv[t.e0];
-        s += sKind[t.e0] == kFeMass ? (Re * hh[t.c0]) * v : v;
-      }
-      if (t.n > 1) {
-        const double v = sTv[t.e1];
-        s += sKind[t.e1] == kFeMass ? (Re * hh[t.c1]) * v : v;
-      }
-      a.val[q0 + i] = s;
+  double* __restrict__ hh = sH + w * N;
+  double* __restrict__ val = a.val;
+  double* __restrict__ rhs = a.rhs;
+  const int ent_src = nq * nq + nq + 2, ent_bc = ent_src + 1;
+  for (int64_t eb = (int64_t)blockIdx.x * kFesWaves; eb < E; eb += (int64_t)T.edge_blocks * kFesWaves) {
+    const int64_t e = eb + w;
+    const bool on = e < E;
+    __syncthreads();  // (the staging / the previous round's reads of sH)
+    if (on)
+      for (int c = lane; c < N; c += 64) hh[c] = a.cellh[e * N + c];
+    __syncthreads();
+    if (!on) continue;
+    if (a.lhs) {
+      const int sh = T.shape[e];
+      const int i0 = T.off[sh], L = T.off[sh + 1] - i0;
+      const int64_t q0 = T.rowptr[e * per];
+      const double Re = a.edge_R[e];
+      for (int i = lane; i < L; i += 64) val[q0 + i] = fe_tpl_val(sT[i0 + i], sTv, sKind, Re, hh);
     }
-  }
-  if (a.do_rhs) {  // fe_s_rhs_terms: the source on the pressure rows, the end data
-    const int ent_src = nq * nq + nq + 2, ent_bc = ent_src + 1;
-    const double fe = a.edge_f ? a.edge_f[e] : a.f;
-    for (int r = lane; r < per; r += 64) {
-      double s = 0.0;
-      if (r >= nf) s += (fe * hh[r - nf]) * sTv[ent_src];
-      else if (r == 0) s += a.edge_bc[2 * e] * sTv[ent_bc];
-      else if (r == nf - 1) s += a.edge_bc[2 * e + 1] * sTv[ent_bc];
-      a.rhs[e * per + r] = s;
+    if (a.do_rhs) {  // fe_s_rhs_terms: the source on the pressure rows, the end data
+      const double fe = a.edge_f ? a.edge_f[e] : a.f;
+      const double b0 = a.edge_bc[2 * e], b1 = a.edge_bc[2 * e + 1];
+      for (int r = lane; r < per; r += 64) {
+        double s = 0.0;
+        if (r >= nf) s += (fe * hh[r - nf]) * sTv[ent_src];
+        else if (r == 0) s += b0 * sTv[ent_bc];
+        else if (r == nf - 1) s += b1 * sTv[ent_bc];
+        rhs[e * per + r] = s;
+      }
     }
   }
 }
 
 // The true residual r = b - A x of a (k, 0) system with A's entries formed again from the
 // templates (the CSR's values bit for bit while the coefficients are the assembled ones):
-// one wave per edge, a lane per row summing the row's products in CSR order; the multiplier
-// rows from the CSR in the blocks after the edges'. r into rout (a refinement pass starts
-// from it); block partials of ||r||^2, ||b||^2 for k_dir_publish.
+// one wave per edge, its x and cell lengths staged in LDS (coalesced loads), a lane per row
+// summing the row's products in CSR order from LDS; the multiplier rows from the CSR in the
+// blocks after the edges'. r into rout (a refinement pass starts from it); block partials of
+// ||r||^2, ||b||^2 for k_dir_publish.
 __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, Csr A,
                                                              const double* __restrict__ x,
                                                              const double* __restrict__ b,
@@ -7586,6 +7629,7 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, C
                                                              double* __restrict__ partials,
                                                              int nblk) {
 #pragma clang fp contract(off)
+  extern __shared__ double fe_lds[];
   __shared__ double sTv[kFesTable];
   __shared__ int sKind[kFesTable];
   const int N = a.N, per = T.per, nq = T.k + 1;
@@ -7602,36 +7646,42 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, C
       bb = bv * bv;
     }
   } else {
+    int2* sT = reinterpret_cast<int2*>(fe_lds);
+    int* sRs = reinterpret_cast<int*>(fe_lds + T.off[4]);
+    double* sH = fe_lds + T.off[4] + (4 * (per + 1) + 1) / 2;
+    double* sX = sH + kFesWaves * N;
     const int nt = nq * nq + nq + 4;
     for (int i = threadIdx.x; i < nt; i += blockDim.x) {
       sTv[i] = a.tval[i];
       sKind[i] = a.kind[i];
     }
-    __syncthreads();
+    fe_tpl_stage(T, sT, sRs);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int64_t e = (int64_t)blockIdx.x * kFesWaves + w; e < E;
-         e += (int64_t)T.edge_blocks * kFesWaves) {
+    double* hh = sH + w * N;
+    double* xs = sX + w * per;
+    for (int64_t eb = (int64_t)blockIdx.x * kFesWaves; eb < E;
+         eb += (int64_t)T.edge_blocks * kFesWaves) {
+      const int64_t e = eb + w;
+      const bool on = e < E;
+      __syncthreads();
+      if (on) {
+        for (int c = lane; c < N; c += 64) hh[c] = a.cellh[e * N + c];
+        for (int i = lane; i < per; i += 64) xs[i] = x[e * per + i];
+      }
+      __syncthreads();
+      if (!on) continue;
       const int sh = T.shape[e];
-      const FeTplE* __restrict__ tp = T.tpl + T.off[sh];
-      const int* __restrict__ rs = T.rs + sh * (per + 1);
-      const double* __restrict__ hh = a.cellh + e * N;
-      const double* __restrict__ xe = x + e * per;
+      const int i0 = T.off[sh];
+      const int* rs = sRs + sh * (per + 1);
       const double Re = a.edge_R[e];
       const int l0 = T.lam[2 * e], l1 = T.lam[2 * e + 1];
+      const double x0 = l0 >= 0 ? x[l0] : 0.0, x1 = l1 >= 0 ? x[l1] : 0.0;
       for (int r = lane; r < per; r += 64) {
         double s = 0.0;
         for (int i = rs[r]; i < rs[r + 1]; ++i) {
-          const FeTplE t = tp[i];
-          double v = 0.0;
-          if (t.n > 0) {
-            const double tv = sTv[t.e0];
-            v += sKind[t.e0] == kFeMass ? (Re * hh[t.c0]) * tv : tv;
-          }
-          if (t.n > 1) {
-            const double tv = sTv[t.e1];
-            v += sKind[t.e1] == kFeMass ? (Re * hh[t.c1]) * tv : tv;
-          }
-          s += v * (t.lc >= 0 ? xe[t.lc] : x[r == 0 ? l0 : l1]);
+          const int2 t = sT[i0 + i];
+          const int lc = (int)((unsigned)t.y >> 16) - 1;
+          s += fe_tpl_val(t, sTv, sKind, Re, hh) * (lc >= 0 ? xs[lc] : (r == 0 ? x0 : x1));
         }
         const double bv = b[e * per + r], rv = bv - s;
         rout[e * per + r] = rv;
@@ -8115,13 +8165,13 @@ bool fe_build_tpl(nx_network* h, int k, int32_t N, int64_t E, const int32_t* row
       std::copy(shape_rs[sh].begin(), shape_rs[sh].end(), rs_all.begin() + (size_t)sh * (per + 1));
   }
   off[4] = (int)all.size();
-  if (all.empty()) return false;
-  FeTplE* d_t = nullptr;
-  if (hipMalloc(&d_t, sizeof(FeTplE) * all.size()) != hipSuccess) return false;
-  h->fe_tpl_buf = d_t;
-  if (hipMemcpy(d_t, all.data(), sizeof(FeTplE) * all.size(), hipMemcpyHostToDevice) != hipSuccess)
-    return false;
-  if (upload(&h->fe_tpl_off, off.data(), 5, h->stream) ||
+  if (all.empty() || off[4] > kFeTplMax) return false;
+  for (const FeTplE& t : all)  // (the packed fields' ranges)
+    if (t.e0 < 0 || t.e0 > 127 || t.e1 < 0 || t.e1 > 127 || t.c0 < 0 || t.c1 < 0) return false;
+  std::vector<int2> packed(all.size());
+  for (size_t i = 0; i < all.size(); ++i) packed[i] = fe_tpl_pack(all[i]);
+  std::copy(off.begin(), off.end(), h->fe_tpl_off);
+  if (upload(&h->fe_tpl_buf, packed.data(), (int64_t)packed.size(), h->stream) ||
       upload(&h->fe_tpl_rs, rs_all.data(), (int64_t)rs_all.size(), h->stream) ||
       upload(&h->fe_tpl_shape, shape.data(), E, h->stream) ||
       upload(&h->fe_tpl_lam, lam.data(), 2 * E, h->stream) ||
@@ -8135,9 +8185,14 @@ bool fe_tpl_on(const nx_network* h) {
   return h->fe_tpl && (e == nullptr || std::atoi(e) != 0);
 }
 FeTpl fe_tpl_args(const nx_network* h, int edge_blocks) {
-  return FeTpl{static_cast<const FeTplE*>(h->fe_tpl_buf), h->fe_tpl_off, h->fe_tpl_rs,
-               h->fe_tpl_shape, h->fe_tpl_lam, h->rowptr, h->fe_sk, h->fe_sk * (int)h->N + 1,
-               fe_per(h), edge_blocks};
+  FeTpl t{h->fe_tpl_buf, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam, h->rowptr, {},
+          h->fe_sk, h->fe_sk * (int)h->N + 1, fe_per(h), edge_blocks};
+  for (int i = 0; i < 5; ++i) t.off[i] = h->fe_tpl_off[i];
+  return t;
+}
+// edge workgroups of the template kernels: rounds of kFesWaves edges, a few per CU
+int fe_tpl_blocks(const nx_network* h) {
+  return std::max(1, std::min(grid_of(h->E, kFesWaves), 8 * h->n_cu));
 }
 
 // terms [ptr[i], ptr[i+1]) of every output i must reference the table and the cell / edge
@@ -8299,7 +8354,7 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_tI,
                   h->cp_eb, h->cp_nrow, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
                   h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown, h->fe_tpl_buf,
-                  h->fe_tpl_off, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
+                  h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -8395,10 +8450,11 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
     hipEvent_t e0 = h->prof ? h->ev[0] : nullptr, e1 = h->prof ? h->ev[1] : nullptr;
     // (k, 0): the edge templates (NXHIP_FE_STRUCT=0: the gather tables), else the tables
     if (fe_tpl_on(h)) {
-      const int eb = (int)grid_of(h->E, kFesWaves);
+      const int eb = fe_tpl_blocks(h);
       const int lb = (int)grid_of(h->n_own - h->E * (int64_t)fe_per(h), 64 * kFesWaves);
-      hipExtLaunchKernelGGL(k_fe_tasm, dim3(eb + lb), dim3(64 * kFesWaves), 0, s, e0, e1, 0, a,
-                            fe_tpl_args(h, eb));
+      hipExtLaunchKernelGGL(k_fe_tasm, dim3(eb + lb), dim3(64 * kFesWaves),
+                            fe_tpl_lds(h->fe_tpl_off[4], fe_per(h), (int)h->N, false), s, e0, e1,
+                            0, a, fe_tpl_args(h, eb));
     } else {
       hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
                             dim3(kBlock), 0, s, e0, e1, 0, a);
@@ -9828,11 +9884,12 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
     if (fe_tpl_on(h) && h->asm_coef_version == h->coef_version) {
       // the true residual from the templates (A's entries formed again: no CSR reads)
       const int lb = grid_of(h->n_own - h->E * (int64_t)fe_per(h), 64 * kFesWaves);
-      const int eb = std::max(1, std::min(grid_of(h->E, kFesWaves), h->nblk - lb));
+      const int eb = std::max(1, std::min(fe_tpl_blocks(h), h->nblk - lb));
       const FeArgs fa{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind,
                       h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx,
                       h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E, h->fe_cellh};
-      hipLaunchKernelGGL(k_fe_tres, dim3(eb + lb), dim3(64 * kFesWaves), 0, h->stream, fa,
+      hipLaunchKernelGGL(k_fe_tres, dim3(eb + lb), dim3(64 * kFesWaves),
+                         fe_tpl_lds(h->fe_tpl_off[4], fe_per(h), (int)h->N, true), h->stream, fa,
                          fe_tpl_args(h, eb), csr_of(h), h->x, h->rhs, h->tmp, h->partials,
                          eb + lb);
       hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
