@@ -10,7 +10,7 @@
 # profile      scripts/profile.sh <tag> [args] (trace + PMC passes)      -> prof_<tag>/
 # wcal         WRITE_SIZE calibration on known write streams   -> <tag>_wcal_*, wcal_<tag>/
 # rehearsal    the 8-rank C4 group rehearsal under rocprof + per-rank kernel times
-# fe_prof      rocprof kernel stats of the (2, 0) condensed solve at C3
+# fe_prof[:k,m] rocprof kernel stats of a general-degree solve at C3 (default (2, 0))
 # ledger       k_dir_step store ledger (debug build, WRITE_SIZE per class) -> <tag>_ledger.json
 # cmd:<c>      any command (e.g. cmd:"python scripts/direct_timing.py 18")
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -50,7 +50,7 @@ for s in "$@"; do
       mkdir -p "gpurun_out/prof_$T"
       (cd /tmp && export TMPDIR=/tmp && step fe_prof 300 "$R/gpurun_out/prof_$T/run.log" \
         rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$T" -o trace --output-format csv \
-        -- python3 "$R/scripts/fe_timing.py" 15 15 "2,0") || exit $? ;;
+        -- python3 "$R/scripts/fe_timing.py" 15 15 "${arg:-2,0}") || exit $? ;;
     wcal)  # WRITE_SIZE against known write streams (scripts/micro/write_ceiling.hip)
       hipcc --offload-arch=gfx950 -O3 -o gpurun_out/write_ceiling scripts/micro/write_ceiling.hip || exit 1
       step wcal_time 120 "gpurun_out/${T}_wcal_time.log" gpurun_out/write_ceiling || exit $?
