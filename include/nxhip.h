@@ -106,15 +106,22 @@ int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double* edge_
 /*
  * The flux degree k when nx_create_fe's tables are exactly a (k, 0) layout's
  * (layout_fe.build_fe_layout with m = 0: every entry's and every rhs row's term list equals
- * the closed form k_assemble_fes evaluates without the tables), else 0 -- then the handle
- * keeps the gather kernel k_assemble_fe. nx_create_fe runs this check itself; exported so
- * the host (and the CPU tests) can probe it without a device. Replaces nothing in the
+ * the closed form fe_s_terms gives without the tables), else 0. Exported so the host (and
+ * the CPU tests) can probe the closed form without a device. Replaces nothing in the
  * reference: its forms are compiled per degree by FFCx (assembly.py:121-146).
  */
 int nx_fe_struct_degree(int32_t N, int64_t n_edges, int64_t n_rows, const int32_t* rowptr,
                         const int32_t* col, int32_t n_table, const int32_t* a_ptr,
                         const int32_t* a_idx, const int32_t* a_ent, const int32_t* b_ptr,
                         const int32_t* b_idx, const int32_t* b_ent, int32_t* k_out);
+
+/*
+ * The edge templates of a general-degree handle (nx_create_fe builds them when every edge's
+ * rows match one of a few shapes): *n_shapes = their number, 0 when the handle kept the
+ * gather tables; *rows_per_edge = the rows of one edge. The assembly (k_fe_tasm) and the
+ * direct solves' true residual (k_fe_tres) then read no gather tables and no CSR.
+ */
+int nx_fe_templates(nx_network_t* h, int32_t* n_shapes, int32_t* rows_per_edge);
 
 /* Release every device buffer, graph and communicator of the handle. */
 int nx_destroy(nx_network_t* h);

@@ -44,6 +44,7 @@ _SIGS = {
                                _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, C.POINTER(_h)]),
     "nx_fe_struct_degree": (C.c_int, [_i32, _i64, _i64, _pi32, _pi32, _i32, _pi32, _pi32,
                                       _pi32, _pi32, _pi32, _pi32, _pi32]),
+    "nx_fe_templates": (C.c_int, [_h, _pi32, _pi32]),
     "nx_destroy": (C.c_int, [_h]),
     "nx_dims": (C.c_int, [_h, _pi64, _pi64, _pi64]),
     "nx_set_coefficients": (C.c_int, [_h, _pd, _f64, _f64, _pd]),
@@ -393,6 +394,13 @@ class Handle:
         f, n = C.c_int32(0), C.c_int32(0)
         check(lib().nx_get_direct_info(self.ptr, C.byref(f), C.byref(n)))
         return {"fused_residual": bool(f.value), "n_left": int(n.value)}
+
+    def fe_templates(self) -> tuple[int, int]:
+        """(shapes, rows per edge) of a general-degree handle's edge templates
+        (nx_fe_templates); (0, 0) when it kept the gather tables."""
+        n, per = C.c_int32(0), C.c_int32(0)
+        check(lib().nx_fe_templates(self.ptr, C.byref(n), C.byref(per)))
+        return int(n.value), int(per.value)
 
     def direct_path(self) -> str:
         """What the last direct solve ran (nx_get_direct_path): ``"fused"`` (k_dir_step, one

@@ -68,6 +68,11 @@ def test_fe_csr_and_rhs(case, km, struct, monkeypatch):
     hv, hr = evaluate_terms(lay, R, 0.7, _edge_bc(F, pbc), h)
     np.testing.assert_array_equal(val, hv)  # bit-exact: same terms, same order
     np.testing.assert_array_equal(asm.handle.rhs(), hr)
+    # the edge templates are built for every pair on these graphs (so "1" ran them)
+    k, m = km
+    N = CASES[case][1]
+    assert asm.handle.fe_templates()[1] == k * N + 1 + (N if m == 0 else m * N - 1)
+    assert 1 <= asm.handle.fe_templates()[0] <= 8
 
 
 @pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "edge_info_N10", "depth6_N40",
