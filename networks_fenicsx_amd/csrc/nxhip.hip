@@ -2580,7 +2580,13 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
         z[lam] = zj;
       stv<WT>(pa.slot_z + ts0 + rsl, zj);
     }
-    if (down && blockIdx.x == 0 && rmine) pa.slot_z[ts0 + rsl] = sJ0[rsl];
+    if (down && blockIdx.x == 0 && rmine) {
+      pa.slot_z[ts0 + rsl] = sJ0[rsl];
+      if (!pa.fres) {  // (an auxiliary solve: no publish step writes x's top values)
+        if (dir && pa.accum) z[lam] += sJ0[rsl];
+        else z[lam] = sJ0[rsl];
+      }
+    }
   } else
   for (int lv = 0; lv < nl; ++lv) {  // root level first: z_j = (J_j + g_par z_par) / D_j
     for (int j = sLv[lv] + threadIdx.x; j < sLv[lv + 1]; j += kTopThreads) {
@@ -2603,6 +2609,10 @@ __device__ __forceinline__ void top_body(const PcArgs& pa, double* __restrict__ 
           z[sLam[sl]] = zj;
       }
       if (!down || blockIdx.x == 0) stv<WT>(pa.slot_z + ts0 + sl, zj);
+      if (down && blockIdx.x == 0 && !pa.fres) {  // (as above)
+        if (dir && pa.accum) z[sLam[sl]] += zj;
+        else z[sLam[sl]] = zj;
+      }
     }
   NX_PHASE(36);
   if (down) {
@@ -6534,8 +6544,10 @@ struct nx_network {
   // (k, 0) edge templates (fe_build_tpl; k_fe_tasm / k_fe_tres): entries, shape offsets,
   // shape row starts, the edges' shapes and multiplier columns
   bool fe_tpl = false;
-  int2* fe_tpl_buf = nullptr;  // packed entries (fe_tpl_pack)
-  int fe_tpl_off[5] = {0, 0, 0, 0, 0};
+  int2* fe_tpl_buf = nullptr;   // packed entries (fe_tpl_pack)
+  int2* fe_tpl_rbuf = nullptr;  // packed rhs terms
+  int fe_tpl_off[9] = {};       // per shape (kFeShapes + 1)
+  int fe_tpl_nsh = 0, fe_tpl_per = 0;
   int *fe_tpl_rs = nullptr, *fe_tpl_shape = nullptr, *fe_tpl_lam = nullptr;
   double* fe_cellh = nullptr;  // E*N cell lengths (k_fe_cellh at nx_create_fe)
   int *fe_slot = nullptr, *fe_vfe = nullptr, *fe_vaux = nullptr, *fe_ife = nullptr;
@@ -6554,6 +6566,7 @@ struct nx_network {
   double *cp_cst = nullptr, *cp_fac = nullptr, *cp_se = nullptr, *cp_xn = nullptr;
   double *cp_Pinv = nullptr, *cp_hv = nullptr;
   int *cp_tI = nullptr, *cp_eb = nullptr, *cp_nrow = nullptr, *cp_lev_off = nullptr;
+  std::vector<int> cp_lev_host;  // the level offsets on the host (cp_nodes_launch)
   int *cp_order = nullptr, *cp_inc_off = nullptr, *cp_inc = nullptr, *cp_parent = nullptr;
   int *cp_child_off = nullptr, *cp_child = nullptr, *cp_nown = nullptr;
 };
@@ -7489,79 +7502,91 @@ constexpr int kFesWaves = 4;    // k_fe_tasm / k_fe_tres: waves (edges) per bloc
 constexpr int kFesRows = 512;   // (nx_fe_struct_degree) rows per edge: k N + 1 + N + 1 at most
 constexpr int kFesCells = 256;  // cells per edge
 constexpr int kFesTable = 128;  // term table entries in LDS
-// ---- (k, 0) edge templates (k_fe_tasm / k_fe_tres). Every edge's rows have one of four
-// shapes: a multiplier column at its first flux row or not, at its last or not (the
-// multiplier columns sort after the edge's own). Per shape, nx_create_fe lists the entries in
-// CSR order with their terms (fe_s_terms_loc, cells relative to the edge's first) and local
-// column (-1: the multiplier), checks every edge's rows against its shape, and the kernels
-// then form an edge's values from its R and cell lengths alone: no gather tables, no column
-// reads, no decoding per entry. Same terms in the same order as k_assemble_fe: bit-exact.
+// ---- Edge templates (k_fe_tasm / k_fe_tres), any (k, m). An edge's rows (the `per` rows
+// from e * per: its flux nodes, then its pressure cells or interior pressure nodes) have the
+// same entries on every edge up to a few shapes -- which end has a multiplier column, the
+// order of its end nodes' shared rows. nx_create_fe reads each shape's entries from its first
+// edge's gather-table terms (cells relative to the edge's first; columns local to the edge,
+// or the edge's j-th outside column), checks every other edge's against its shape, and packs
+// an entry into 8 bytes; the kernels then form an edge's values and rhs from its R, f, end
+// data and cell lengths alone. Same terms in the same order as k_assemble_fe: bit-exact. The
+// rows after the edges' (shared node pressures, multipliers) keep the gather tables.
 struct FeTplE {
-  short pos, lc;  // row within the edge; local column, -1 = the row's multiplier column
+  short lc;       // local column; -(1 + j): the edge's j-th outside column (j < kFeExt)
   short n;        // terms (0..2)
-  short c0, c1;   // their cells relative to the edge's first
+  short c0, c1;   // their cells relative to the edge's first (bc terms: the end, 0 / 1)
   short e0, e1;   // their table entries
-  short pad;
 };
-// An entry packed for LDS: x = c0 | c1 << 16, y = e0 | e1 << 7 | n << 14 | (lc + 1) << 16
+constexpr int kFeExt = 4;     // outside columns of an edge (multipliers, shared node rows)
+constexpr int kFeShapes = 8;  // edge shapes
+// An entry packed: x = c0 | c1 << 16, y = e0 | e1 << 7 | n << 14 | (lc + kFeExt) << 16
 __host__ __device__ __forceinline__ int2 fe_tpl_pack(const FeTplE& t) {
   return int2{(int)((unsigned)(unsigned short)t.c0 | ((unsigned)(unsigned short)t.c1 << 16)),
               (int)((unsigned)t.e0 | ((unsigned)t.e1 << 7) | ((unsigned)t.n << 14) |
-                    ((unsigned)(t.lc + 1) << 16))};
+                    ((unsigned)(t.lc + kFeExt) << 16))};
 }
 struct FeTpl {
-  const int2* tpl;     // packed entries, the four shapes one after another
-  const int* rs;       // 4 x (per + 1): each shape's row starts (entry index)
-  const int* shape;    // E: the edge's shape (bit 0: multiplier at row 0, bit 1: at row nf - 1)
-  const int* lam;      // 2 E: the multiplier column of the edge's first / last flux row, -1
+  const int2* tpl;     // packed matrix entries, the shapes one after another
+  const int2* rtpl;    // packed rhs terms: per shape `per` rows
+  const int* rs;       // kFeShapes x (per + 1): each shape's row starts (entry index)
+  const int* shape;    // E: the edge's shape
+  const int* ext;      // kFeExt E: the edge's outside columns, -1
   const int* rowptr;
-  int off[5];          // each shape's first entry; off[4] = all
-  int k, nf, per, edge_blocks;
+  int off[kFeShapes + 1];  // each shape's first entry; off[nsh] = all
+  int nsh, per, edge_blocks;
 };
-constexpr int kFeTplMax = 4096;  // packed entries (LDS: 32 KiB)
+constexpr int kFeTplMax = 16384;  // packed entries (LDS: up to 128 KiB)
 
-// one packed entry's value: its terms in order, s = 0 + t0 (+ t1), as fe_term forms them
+// one packed term list's value, s = 0 + t0 (+ t1), as fe_term forms them (R: the edge's
+// resistance, fe its source, bc its end data, hh its cell lengths)
 __device__ __forceinline__ double fe_tpl_val(int2 t, const double* sTv, const int* sKind, double Re,
-                                             const double* hh) {
+                                             double fe, const double* bc, const double* hh) {
 #pragma clang fp contract(off)
-  const int n = (t.y >> 14) & 3, e0 = t.y & 127, e1 = (t.y >> 7) & 127;
+  const int n = (t.y >> 14) & 3;
   double s = 0.0;
-  if (n > 0) {
-    const double v = sTv[e0];
-    s += sKind[e0] == kFeMass ? (Re * hh[t.x & 0xffff]) * v : v;
-  }
-  if (n > 1) {
-    const double v = sTv[e1];
-    s += sKind[e1] == kFeMass ? (Re * hh[(unsigned)t.x >> 16]) * v : v;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u >= n) break;
+    const int e = u ? (t.y >> 7) & 127 : t.y & 127;
+    const int c = u ? (int)((unsigned)t.x >> 16) : t.x & 0xffff;
+    const double v = sTv[e];
+    const int kd = sKind[e];
+    s += kd == kFeMass ? (Re * hh[c]) * v
+         : kd == kFeSource ? (fe * hh[c]) * v
+         : kd == kFeBc ? bc[c] * v
+         : v;
   }
   return s;
 }
 
-// Dynamic LDS of k_fe_tasm / k_fe_tres (doubles): the packed templates, the row starts, then
-// per wave its edge's cell lengths (and for the residual its x)
-size_t fe_tpl_lds(int n_tpl, int per, int N, bool res) {
-  return 8 * ((size_t)n_tpl + (4 * (size_t)(per + 1) + 1) / 2 +
+// Dynamic LDS of k_fe_tasm / k_fe_tres (doubles): the packed entries, the rhs terms, the
+// row starts, then per wave its edge's cell lengths (and for the residual its x)
+size_t fe_tpl_lds(int n_tpl, int nsh, int per, int N, bool res) {
+  return 8 * ((size_t)n_tpl + (size_t)nsh * per + ((size_t)kFeShapes * (per + 1) + 1) / 2 +
               (size_t)kFesWaves * (N + (res ? per : 0)));
 }
 
-// The templates (and row starts) into LDS, once per workgroup
-__device__ __forceinline__ void fe_tpl_stage(const FeTpl& T, int2* sT, int* sRs) {
-  for (int i = threadIdx.x; i < T.off[4]; i += blockDim.x) sT[i] = T.tpl[i];
-  for (int i = threadIdx.x; i < 4 * (T.per + 1); i += blockDim.x) sRs[i] = T.rs[i];
+// The templates into LDS, once per workgroup
+__device__ __forceinline__ void fe_tpl_stage(const FeTpl& T, int2* sT, int2* sR, int* sRs,
+                                             bool rhs) {
+  for (int i = threadIdx.x; i < T.off[T.nsh]; i += blockDim.x) sT[i] = T.tpl[i];
+  if (rhs)
+    for (int i = threadIdx.x; i < T.nsh * T.per; i += blockDim.x) sR[i] = T.rtpl[i];
+  for (int i = threadIdx.x; i < kFeShapes * (T.per + 1); i += blockDim.x) sRs[i] = T.rs[i];
 }
 
 // Assembly: one wave per edge, the edges in workgroup rounds (the LDS staging amortised); the
 // edge's cell lengths loaded once (coalesced), every entry then from LDS alone; values and
-// rhs stored coalesced over the edge's contiguous segment and rows. The multiplier rows
-// (+-1) from the tables, in the blocks after the edges'.
+// rhs stored coalesced over the edge's contiguous segment and rows. The rows after the
+// edges' (shared node pressures, multipliers) from the gather tables, in the blocks after.
 __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tasm(FeArgs a, FeTpl T) {
 #pragma clang fp contract(off)
   extern __shared__ double fe_lds[];
   __shared__ double sTv[kFesTable];
   __shared__ int sKind[kFesTable];
-  const int N = a.N, nf = T.nf, per = T.per, nq = T.k + 1;
+  const int N = a.N, per = T.per;
   const int64_t E = a.n_edges, nE = E * (int64_t)per;
-  if ((int)blockIdx.x >= T.edge_blocks) {  // the multiplier rows: +-1 (one term each)
+  if ((int)blockIdx.x >= T.edge_blocks) {
     const int64_t row = nE + (int64_t)(blockIdx.x - T.edge_blocks) * blockDim.x + threadIdx.x;
     if (row >= a.n_rows) return;
     if (a.lhs)
@@ -7570,23 +7595,26 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tasm(FeArgs a, FeTpl T) {
         for (int c = a.a_ptr[q]; c < a.a_ptr[q + 1]; ++c) s += fe_term(a, a.a_idx[c], a.a_ent[c]);
         a.val[q] = s;
       }
-    if (a.do_rhs) a.rhs[row] = 0.0;  // (no terms)
+    if (a.do_rhs) {
+      double s = 0.0;
+      for (int c = a.b_ptr[row]; c < a.b_ptr[row + 1]; ++c) s += fe_term(a, a.b_idx[c], a.b_ent[c]);
+      a.rhs[row] = s;
+    }
     return;
   }
   int2* sT = reinterpret_cast<int2*>(fe_lds);
-  int* sRs = reinterpret_cast<int*>(fe_lds + T.off[4]);
-  double* sH = fe_lds + T.off[4] + (4 * (per + 1) + 1) / 2;
-  const int nt = nq * nq + nq + 4;
-  for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+  int2* sR = sT + T.off[T.nsh];
+  int* sRs = reinterpret_cast<int*>(sR + T.nsh * per);
+  double* sH = reinterpret_cast<double*>(sRs) + (kFeShapes * (per + 1) + 1) / 2;
+  for (int i = threadIdx.x; i < kFesTable; i += blockDim.x) {
     sTv[i] = a.tval[i];
     sKind[i] = a.kind[i];
   }
-  fe_tpl_stage(T, sT, sRs);
+  fe_tpl_stage(T, sT, sR, sRs, a.do_rhs != 0);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double* __restrict__ hh = sH + w * N;
   double* __restrict__ val = a.val;
   double* __restrict__ rhs = a.rhs;
-  const int ent_src = nq * nq + nq + 2, ent_bc = ent_src + 1;
   for (int64_t eb = (int64_t)blockIdx.x * kFesWaves; eb < E; eb += (int64_t)T.edge_blocks * kFesWaves) {
     const int64_t e = eb + w;
     const bool on = e < E;
@@ -7595,33 +7623,30 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tasm(FeArgs a, FeTpl T) {
       for (int c = lane; c < N; c += 64) hh[c] = a.cellh[e * N + c];
     __syncthreads();
     if (!on) continue;
+    const int sh = T.shape[e];
+    const double Re = a.edge_R[e];
+    const double fe = a.edge_f ? a.edge_f[e] : a.f;
+    const double bc[2] = {a.edge_bc[2 * e], a.edge_bc[2 * e + 1]};
     if (a.lhs) {
-      const int sh = T.shape[e];
       const int i0 = T.off[sh], L = T.off[sh + 1] - i0;
       const int64_t q0 = T.rowptr[e * per];
-      const double Re = a.edge_R[e];
-      for (int i = lane; i < L; i += 64) val[q0 + i] = fe_tpl_val(sT[i0 + i], sTv, sKind, Re, hh);
+      for (int i = lane; i < L; i += 64)
+        val[q0 + i] = fe_tpl_val(sT[i0 + i], sTv, sKind, Re, fe, bc, hh);
     }
-    if (a.do_rhs) {  // fe_s_rhs_terms: the source on the pressure rows, the end data
-      const double fe = a.edge_f ? a.edge_f[e] : a.f;
-      const double b0 = a.edge_bc[2 * e], b1 = a.edge_bc[2 * e + 1];
-      for (int r = lane; r < per; r += 64) {
-        double s = 0.0;
-        if (r >= nf) s += (fe * hh[r - nf]) * sTv[ent_src];
-        else if (r == 0) s += b0 * sTv[ent_bc];
-        else if (r == nf - 1) s += b1 * sTv[ent_bc];
-        rhs[e * per + r] = s;
-      }
+    if (a.do_rhs) {
+      const int2* rt = sR + sh * per;
+      for (int r = lane; r < per; r += 64)
+        rhs[e * per + r] = fe_tpl_val(rt[r], sTv, sKind, Re, fe, bc, hh);
     }
   }
 }
 
-// The true residual r = b - A x of a (k, 0) system with A's entries formed again from the
-// templates (the CSR's values bit for bit while the coefficients are the assembled ones):
-// one wave per edge, its x and cell lengths staged in LDS (coalesced loads), a lane per row
-// summing the row's products in CSR order from LDS; the multiplier rows from the CSR in the
-// blocks after the edges'. r into rout (a refinement pass starts from it); block partials of
-// ||r||^2, ||b||^2 for k_dir_publish.
+// The true residual r = b - A x with A's edge entries formed again from the templates (the
+// CSR's values bit for bit while the coefficients are the assembled ones): one wave per
+// edge, its x and cell lengths staged in LDS (coalesced loads), a lane per row summing the
+// row's products in CSR order from LDS (its outside columns' x loaded once per edge); the
+// rows after the edges' from the CSR in the blocks after. r into rout (a refinement pass
+// starts from it); block partials of ||r||^2, ||b||^2 for k_dir_publish.
 __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, Csr A,
                                                              const double* __restrict__ x,
                                                              const double* __restrict__ b,
@@ -7632,7 +7657,7 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, C
   extern __shared__ double fe_lds[];
   __shared__ double sTv[kFesTable];
   __shared__ int sKind[kFesTable];
-  const int N = a.N, per = T.per, nq = T.k + 1;
+  const int N = a.N, per = T.per;
   const int64_t E = a.n_edges, nE = E * (int64_t)per;
   double rr = 0.0, bb = 0.0;
   if ((int)blockIdx.x >= T.edge_blocks) {
@@ -7647,15 +7672,14 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, C
     }
   } else {
     int2* sT = reinterpret_cast<int2*>(fe_lds);
-    int* sRs = reinterpret_cast<int*>(fe_lds + T.off[4]);
-    double* sH = fe_lds + T.off[4] + (4 * (per + 1) + 1) / 2;
+    int* sRs = reinterpret_cast<int*>(sT + T.off[T.nsh]);
+    double* sH = reinterpret_cast<double*>(sRs) + (kFeShapes * (per + 1) + 1) / 2;
     double* sX = sH + kFesWaves * N;
-    const int nt = nq * nq + nq + 4;
-    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+    for (int i = threadIdx.x; i < kFesTable; i += blockDim.x) {
       sTv[i] = a.tval[i];
       sKind[i] = a.kind[i];
     }
-    fe_tpl_stage(T, sT, sRs);
+    fe_tpl_stage(T, sT, nullptr, sRs, false);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double* hh = sH + w * N;
     double* xs = sX + w * per;
@@ -7674,14 +7698,28 @@ __global__ __launch_bounds__(64 * kFesWaves) void k_fe_tres(FeArgs a, FeTpl T, C
       const int i0 = T.off[sh];
       const int* rs = sRs + sh * (per + 1);
       const double Re = a.edge_R[e];
-      const int l0 = T.lam[2 * e], l1 = T.lam[2 * e + 1];
-      const double x0 = l0 >= 0 ? x[l0] : 0.0, x1 = l1 >= 0 ? x[l1] : 0.0;
+      const double fe = a.edge_f ? a.edge_f[e] : a.f;
+      const double bc[2] = {a.edge_bc[2 * e], a.edge_bc[2 * e + 1]};
+      double xo[kFeExt];
+#pragma unroll
+      for (int j = 0; j < kFeExt; ++j) {
+        const int c = T.ext[kFeExt * e + j];
+        xo[j] = c >= 0 ? x[c] : 0.0;
+      }
       for (int r = lane; r < per; r += 64) {
         double s = 0.0;
         for (int i = rs[r]; i < rs[r + 1]; ++i) {
           const int2 t = sT[i0 + i];
-          const int lc = (int)((unsigned)t.y >> 16) - 1;
-          s += fe_tpl_val(t, sTv, sKind, Re, hh) * (lc >= 0 ? xs[lc] : (r == 0 ? x0 : x1));
+          const int lc = (int)((unsigned)t.y >> 16) - kFeExt;
+          double xv = 0.0;
+          if (lc >= 0) {
+            xv = xs[lc];
+          } else {
+#pragma unroll
+            for (int j = 0; j < kFeExt; ++j)
+              if (lc == -1 - j) xv = xo[j];
+          }
+          s += fe_tpl_val(t, sTv, sKind, Re, fe, bc, hh) * xv;
         }
         const double bv = b[e * per + r], rv = bv - s;
         rout[e * per + r] = rv;
@@ -7825,7 +7863,7 @@ __device__ __forceinline__ void inv2(const double* P, double* Pi) {
 
 // The forward sweep of one edge (one thread): Se, ge and the per-vertex factors.
 __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restrict__ b) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.E) return;
   const int N = a.N, k = a.k, m = a.m, nI = a.nI;
   const int nf = k * N + 1;
@@ -7967,64 +8005,84 @@ __device__ __forceinline__ void cp_block(const double* se, int e, int ra, int cb
   B[2] = S[4 * (2 * ra + 1) + 2 * cb];
   B[3] = S[4 * (2 * ra + 1) + 2 * cb + 1];
 }
-__global__ __launch_bounds__(1024) void k_cp_nodes(CpArgs a, CpTree t, const double* __restrict__ b) {
-  for (int L = t.nlev - 1; L >= 0; --L) {
+// The node forest's elimination, one node (level order index i): its 2 x 2 pivot block from
+// its edges' border blocks minus its children's Schur terms; the pivot's inverse and the
+// condensed rhs stored for the back-substitution.
+__device__ __forceinline__ void cp_node_up(const CpArgs& a, const CpTree& t,
+                                           const double* __restrict__ b, int i) {
+  const int n = t.order[i];
+  double D[4] = {0.0, 0.0, 0.0, 0.0}, g[2];
+  const int pr = a.nrow[2 * n], lr = a.nrow[2 * n + 1];
+  g[0] = b[pr];
+  g[1] = lr >= 0 ? b[lr] : 0.0;
+  for (int j = t.inc_off[n]; j < t.inc_off[n + 1]; ++j) {
+    const int e = t.inc[2 * j], end = t.inc[2 * j + 1];
+    double B[4];
+    cp_block(a.se, e, end, end, B);
+    for (int q = 0; q < 4; ++q) D[q] += B[q];
+    g[0] += a.se[20 * (int64_t)e + 16 + 2 * end];
+    g[1] += a.se[20 * (int64_t)e + 17 + 2 * end];
+  }
+  if (lr < 0) D[3] = 1.0;  // (no multiplier: a decoupled dummy)
+  for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j) {
+    const int c = t.child[j];
+    const int ce = t.parent[3 * c + 1], cend = t.parent[3 * c + 2];
+    double B[4];  // child rows x this node's columns
+    cp_block(a.se, ce, cend, 1 - cend, B);
+    const double* Pc = t.Pinv + 4 * (int64_t)c;
+    const double* hc = t.hv + 2 * (int64_t)c;
+    double X[4], z[2];  // Pc B, Pc h
+    for (int r = 0; r < 2; ++r) {
+      for (int q = 0; q < 2; ++q) X[2 * r + q] = Pc[2 * r] * B[q] + Pc[2 * r + 1] * B[2 + q];
+      z[r] = Pc[2 * r] * hc[0] + Pc[2 * r + 1] * hc[1];
+    }
+    for (int r = 0; r < 2; ++r) {
+      for (int q = 0; q < 2; ++q) D[2 * r + q] -= B[r] * X[q] + B[2 + r] * X[2 + q];
+      g[r] -= B[r] * z[0] + B[2 + r] * z[1];
+    }
+  }
+  inv2(D, t.Pinv + 4 * (int64_t)n);
+  t.hv[2 * n] = g[0];
+  t.hv[2 * n + 1] = g[1];
+}
+// ... and its back-substitution: the node's values from its parent's
+__device__ __forceinline__ void cp_node_down(const CpArgs& a, const CpTree& t, int i) {
+  const int n = t.order[i];
+  const int p = t.parent[3 * n];
+  double r[2] = {t.hv[2 * n], t.hv[2 * n + 1]};
+  if (p >= 0) {
+    double B[4];
+    cp_block(a.se, t.parent[3 * n + 1], t.parent[3 * n + 2], 1 - t.parent[3 * n + 2], B);
+    const double* xp = a.xn + 2 * (int64_t)p;
+    r[0] -= B[0] * xp[0] + B[1] * xp[1];
+    r[1] -= B[2] * xp[0] + B[3] * xp[1];
+  }
+  const double* Pn = t.Pinv + 4 * (int64_t)n;
+  a.xn[2 * n] = Pn[0] * r[0] + Pn[1] * r[1];
+  a.xn[2 * n + 1] = Pn[2] * r[0] + Pn[3] * r[1];
+}
+
+// Levels [L0, L1) of the node forest (level 0 the roots) in one workgroup, a barrier per
+// level: up = deepest first (the eliminations), else root first (the back-substitution).
+// The levels with many nodes run as k_cp_level launches instead (cp_nodes_launch).
+__global__ __launch_bounds__(1024) void k_cp_nodes(CpArgs a, CpTree t, const double* __restrict__ b,
+                                                   int L0, int L1, int up) {
+  for (int k = 0; k < L1 - L0; ++k) {
+    const int L = up ? L1 - 1 - k : L0 + k;
     for (int i = t.lev_off[L] + threadIdx.x; i < t.lev_off[L + 1]; i += 1024) {
-      const int n = t.order[i];
-      double D[4] = {0.0, 0.0, 0.0, 0.0}, g[2];
-      const int pr = a.nrow[2 * n], lr = a.nrow[2 * n + 1];
-      g[0] = b[pr];
-      g[1] = lr >= 0 ? b[lr] : 0.0;
-      for (int j = t.inc_off[n]; j < t.inc_off[n + 1]; ++j) {
-        const int e = t.inc[2 * j], end = t.inc[2 * j + 1];
-        double B[4];
-        cp_block(a.se, e, end, end, B);
-        for (int q = 0; q < 4; ++q) D[q] += B[q];
-        g[0] += a.se[20 * (int64_t)e + 16 + 2 * end];
-        g[1] += a.se[20 * (int64_t)e + 17 + 2 * end];
-      }
-      if (lr < 0) D[3] = 1.0;  // (no multiplier: a decoupled dummy)
-      for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j) {
-        const int c = t.child[j];
-        const int ce = t.parent[3 * c + 1], cend = t.parent[3 * c + 2];
-        double B[4];  // child rows x this node's columns
-        cp_block(a.se, ce, cend, 1 - cend, B);
-        const double* Pc = t.Pinv + 4 * (int64_t)c;
-        const double* hc = t.hv + 2 * (int64_t)c;
-        double X[4], z[2];  // Pc B, Pc h
-        for (int r = 0; r < 2; ++r) {
-          for (int q = 0; q < 2; ++q) X[2 * r + q] = Pc[2 * r] * B[q] + Pc[2 * r + 1] * B[2 + q];
-          z[r] = Pc[2 * r] * hc[0] + Pc[2 * r + 1] * hc[1];
-        }
-        for (int r = 0; r < 2; ++r) {
-          for (int q = 0; q < 2; ++q) D[2 * r + q] -= B[r] * X[q] + B[2 + r] * X[2 + q];
-          g[r] -= B[r] * z[0] + B[2 + r] * z[1];
-        }
-      }
-      inv2(D, t.Pinv + 4 * (int64_t)n);
-      t.hv[2 * n] = g[0];
-      t.hv[2 * n + 1] = g[1];
+      if (up) cp_node_up(a, t, b, i);
+      else cp_node_down(a, t, i);
     }
     __syncthreads();
   }
-  for (int L = 0; L < t.nlev; ++L) {
-    for (int i = t.lev_off[L] + threadIdx.x; i < t.lev_off[L + 1]; i += 1024) {
-      const int n = t.order[i];
-      const int p = t.parent[3 * n];
-      double r[2] = {t.hv[2 * n], t.hv[2 * n + 1]};
-      if (p >= 0) {
-        double B[4];
-        cp_block(a.se, t.parent[3 * n + 1], t.parent[3 * n + 2], 1 - t.parent[3 * n + 2], B);
-        const double* xp = a.xn + 2 * (int64_t)p;
-        r[0] -= B[0] * xp[0] + B[1] * xp[1];
-        r[1] -= B[2] * xp[0] + B[3] * xp[1];
-      }
-      const double* Pn = t.Pinv + 4 * (int64_t)n;
-      a.xn[2 * n] = Pn[0] * r[0] + Pn[1] * r[1];
-      a.xn[2 * n + 1] = Pn[2] * r[0] + Pn[3] * r[1];
-    }
-    __syncthreads();
-  }
+}
+// One level [i0, i1) of level-order nodes, a thread per node across the grid
+__global__ __launch_bounds__(256) void k_cp_level(CpArgs a, CpTree t, const double* __restrict__ b,
+                                                  int i0, int i1, int up) {
+  const int i = i0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= i1) return;
+  if (up) cp_node_up(a, t, b, i);
+  else cp_node_down(a, t, i);
 }
 
 // Back-substitution of one edge (one thread): its vertices from the border values, then every
@@ -8033,7 +8091,7 @@ __global__ __launch_bounds__(1024) void k_cp_nodes(CpArgs a, CpTree t, const dou
 __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restrict__ b,
                                                  double* __restrict__ x, const int* __restrict__ nown,
                                                  int accum) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.E) return;
   const int N = a.N, k = a.k, m = a.m, nI = a.nI;
   const int nf = k * N + 1;
@@ -8087,108 +8145,174 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
   }
 }
 
-// The (k, 0) edge templates (FeTpl): each edge shape's entries from its first edge, every
-// other edge's rows checked against its shape (row lengths and local columns); false (the
-// gather kernels stay) on any difference or a template beyond the int16 fields.
-bool fe_build_tpl(nx_network* h, int k, int32_t N, int64_t E, const int32_t* rowptr,
-                  const int32_t* col) {
-  const int nf = k * N + 1, per = nf + N;
+// The edge templates (FeTpl) of a layout with `per` rows per edge: each shape's entries and
+// rhs terms from its first edge's gather-table terms, every other edge's checked against its
+// shape (row lengths, local / outside columns, terms); false (the gather kernels stay) on any
+// difference, more than kFeShapes shapes or kFeExt outside columns, or fields out of range.
+struct FeTplBuild {
+  std::vector<int> ent, rent;  // per edge entry: packed lc / terms (for the comparison)
+  std::vector<FeTplE> t, r;
+  std::vector<int> rs;
+};
+bool fe_term_rel(const int32_t* kind, int ent, int idx, int64_t e, int N, short& c) {
+  const int kd = kind[ent];
+  if (kd == kFeMass || kd == kFeSource) {
+    const int64_t rel = idx - e * N;
+    if (rel < 0 || rel >= N) return false;
+    c = (short)rel;
+  } else if (kd == kFeBc) {
+    const int64_t rel = idx - 2 * e;
+    if (rel < 0 || rel > 1) return false;
+    c = (short)rel;
+  } else {
+    c = 0;
+  }
+  return ent >= 0 && ent < 128;
+}
+bool fe_build_tpl(nx_network* h, int per, int32_t N, int64_t E, int64_t n_rows,
+                  const int32_t* rowptr, const int32_t* col, const int32_t* kind,
+                  const int32_t* a_ptr, const int32_t* a_idx, const int32_t* a_ent,
+                  const int32_t* b_ptr, const int32_t* b_idx, const int32_t* b_ent) {
   const int64_t nE = E * (int64_t)per;
-  if (per >= 32767 || N >= 32767) return false;
-  std::vector<FeTplE> shape_t[4];
-  std::vector<int> shape_rs[4];
-  bool have[4] = {false, false, false, false};
-  std::vector<int> shape((size_t)E), lam((size_t)2 * E);
-  FeTerm t[2];
+  if (per < 1 || per >= 32767 || N >= 32767 || nE > n_rows || N > kFesCells) return false;
+  std::vector<FeTplE> shp_t[kFeShapes], shp_r[kFeShapes];
+  std::vector<int> shp_rs[kFeShapes];
+  int nsh = 0;
+  std::vector<int> shape((size_t)E), ext((size_t)kFeExt * E, -1);
+  std::vector<FeTplE> et, er;
+  std::vector<int> ers(per + 1);
+  auto same = [](const FeTplE& x, const FeTplE& y) {
+    return x.lc == y.lc && x.n == y.n && x.c0 == y.c0 && x.c1 == y.c1 && x.e0 == y.e0 &&
+           x.e1 == y.e1;
+  };
   for (int64_t e = 0; e < E; ++e) {
     const int64_t r0 = e * per;
-    int l0 = -1, l1 = -1;
-    for (int q = rowptr[r0]; q < rowptr[r0 + 1]; ++q)
-      if (col[q] >= nE) l0 = col[q];
-    for (int q = rowptr[r0 + nf - 1]; q < rowptr[r0 + nf]; ++q)
-      if (col[q] >= nE) l1 = col[q];
-    const int sh = (l0 >= 0 ? 1 : 0) | (l1 >= 0 ? 2 : 0);
-    shape[e] = sh;
-    lam[2 * e] = l0;
-    lam[2 * e + 1] = l1;
-    std::vector<FeTplE>& tp = shape_t[sh];
-    std::vector<int>& rs = shape_rs[sh];
-    if (!have[sh]) {
-      have[sh] = true;
-      rs.assign(per + 1, 0);
-      for (int pos = 0; pos < per; ++pos) {
-        rs[pos] = (int)tp.size();
-        for (int q = rowptr[r0 + pos]; q < rowptr[r0 + pos + 1]; ++q) {
-          const int64_t cq = col[q];
-          int lc;
-          if (cq >= nE) {
-            if (pos != 0 && pos != nf - 1) return false;
-            lc = -1;
-          } else if (cq >= r0 && cq < r0 + per) {
-            lc = (int)(cq - r0);
-          } else {
-            return false;  // another edge's column: not a (k, 0) edge
-          }
-          const int n = fe_s_terms_loc(pos, lc, k, N, 0, t);
-          if (n < 1 || n > 2) return false;
-          FeTplE x{};
-          x.pos = (short)pos;
-          x.lc = (short)lc;
-          x.n = (short)n;
-          x.c0 = (short)t[0].idx;
-          x.e0 = (short)t[0].ent;
-          x.c1 = (short)(n > 1 ? t[1].idx : 0);
-          x.e1 = (short)(n > 1 ? t[1].ent : 0);
-          tp.push_back(x);
-        }
-      }
-      rs[per] = (int)tp.size();
-      if (tp.size() > 30000) return false;
-      continue;
-    }
-    if (rowptr[r0 + per] - rowptr[r0] != rs[per]) return false;
+    et.clear();
+    er.clear();
+    int ne = 0;
+    int* xe = ext.data() + (size_t)kFeExt * e;
     for (int pos = 0; pos < per; ++pos) {
-      if (rowptr[r0 + pos + 1] - rowptr[r0 + pos] != rs[pos + 1] - rs[pos]) return false;
-      for (int q = rowptr[r0 + pos], i = rs[pos]; q < rowptr[r0 + pos + 1]; ++q, ++i) {
+      ers[pos] = (int)et.size();
+      for (int q = rowptr[r0 + pos]; q < rowptr[r0 + pos + 1]; ++q) {
         const int64_t cq = col[q];
-        const int lc = cq >= nE ? -1 : (cq >= r0 && cq < r0 + per) ? (int)(cq - r0) : -2;
-        if (lc != tp[i].lc) return false;
+        FeTplE x{};
+        if (cq >= r0 && cq < r0 + per) {
+          x.lc = (short)(cq - r0);
+        } else {
+          int j = 0;
+          while (j < ne && xe[j] != cq) ++j;
+          if (j == ne) {
+            if (ne == kFeExt) return false;
+            xe[ne++] = (int)cq;
+          }
+          x.lc = (short)(-1 - j);
+        }
+        const int n = a_ptr[q + 1] - a_ptr[q];
+        if (n < 1 || n > 2) return false;
+        x.n = (short)n;
+        if (!fe_term_rel(kind, a_ent[a_ptr[q]], a_idx[a_ptr[q]], e, N, x.c0)) return false;
+        x.e0 = (short)a_ent[a_ptr[q]];
+        if (n > 1) {
+          if (!fe_term_rel(kind, a_ent[a_ptr[q] + 1], a_idx[a_ptr[q] + 1], e, N, x.c1)) return false;
+          x.e1 = (short)a_ent[a_ptr[q] + 1];
+        }
+        et.push_back(x);
       }
+      const int nr = b_ptr[r0 + pos + 1] - b_ptr[r0 + pos];
+      if (nr > 2) return false;
+      FeTplE y{};
+      y.n = (short)nr;
+      if (nr > 0) {
+        if (!fe_term_rel(kind, b_ent[b_ptr[r0 + pos]], b_idx[b_ptr[r0 + pos]], e, N, y.c0)) return false;
+        y.e0 = (short)b_ent[b_ptr[r0 + pos]];
+      }
+      if (nr > 1) {
+        if (!fe_term_rel(kind, b_ent[b_ptr[r0 + pos] + 1], b_idx[b_ptr[r0 + pos] + 1], e, N, y.c1))
+          return false;
+        y.e1 = (short)b_ent[b_ptr[r0 + pos] + 1];
+      }
+      er.push_back(y);
     }
+    ers[per] = (int)et.size();
+    int sh = 0;
+    for (; sh < nsh; ++sh) {
+      if (shp_t[sh].size() != et.size() || shp_rs[sh] != ers) continue;
+      bool eq = true;
+      for (size_t i = 0; i < et.size() && eq; ++i) eq = same(shp_t[sh][i], et[i]);
+      for (int i = 0; i < per && eq; ++i) eq = same(shp_r[sh][i], er[i]);
+      if (eq) break;
+    }
+    if (sh == nsh) {
+      if (nsh == kFeShapes) return false;
+      shp_t[nsh] = et;
+      shp_r[nsh] = er;
+      shp_rs[nsh] = ers;
+      ++nsh;
+    }
+    shape[e] = sh;
   }
-  std::vector<FeTplE> all;
-  std::vector<int> off(5, 0), rs_all((size_t)4 * (per + 1), 0);
-  for (int sh = 0; sh < 4; ++sh) {
-    off[sh] = (int)all.size();
-    all.insert(all.end(), shape_t[sh].begin(), shape_t[sh].end());
-    if (have[sh])
-      std::copy(shape_rs[sh].begin(), shape_rs[sh].end(), rs_all.begin() + (size_t)sh * (per + 1));
+  std::vector<int2> packed, rpacked;
+  std::vector<int> rs_all((size_t)kFeShapes * (per + 1), 0);
+  int off[kFeShapes + 1] = {};
+  for (int sh = 0; sh < nsh; ++sh) {
+    off[sh] = (int)packed.size();
+    for (const FeTplE& x : shp_t[sh]) packed.push_back(fe_tpl_pack(x));
+    for (const FeTplE& y : shp_r[sh]) rpacked.push_back(fe_tpl_pack(y));
+    std::copy(shp_rs[sh].begin(), shp_rs[sh].end(), rs_all.begin() + (size_t)sh * (per + 1));
   }
-  off[4] = (int)all.size();
-  if (all.empty() || off[4] > kFeTplMax) return false;
-  for (const FeTplE& t : all)  // (the packed fields' ranges)
-    if (t.e0 < 0 || t.e0 > 127 || t.e1 < 0 || t.e1 > 127 || t.c0 < 0 || t.c1 < 0) return false;
-  std::vector<int2> packed(all.size());
-  for (size_t i = 0; i < all.size(); ++i) packed[i] = fe_tpl_pack(all[i]);
-  std::copy(off.begin(), off.end(), h->fe_tpl_off);
+  off[nsh] = (int)packed.size();
+  if (packed.empty() || off[nsh] > kFeTplMax) return false;
+  if (fe_tpl_lds(off[nsh], nsh, per, N, true) > 150 * 1024) return false;  // (+ static LDS)
+  for (int i = 0; i <= nsh; ++i) h->fe_tpl_off[i] = off[i];
+  h->fe_tpl_nsh = nsh;
+  h->fe_tpl_per = per;
   if (upload(&h->fe_tpl_buf, packed.data(), (int64_t)packed.size(), h->stream) ||
+      upload(&h->fe_tpl_rbuf, rpacked.data(), (int64_t)rpacked.size(), h->stream) ||
       upload(&h->fe_tpl_rs, rs_all.data(), (int64_t)rs_all.size(), h->stream) ||
       upload(&h->fe_tpl_shape, shape.data(), E, h->stream) ||
-      upload(&h->fe_tpl_lam, lam.data(), 2 * E, h->stream) ||
+      upload(&h->fe_tpl_lam, ext.data(), (int64_t)ext.size(), h->stream) ||
       hipStreamSynchronize(h->stream) != hipSuccess)
     return false;
   return true;
 }
-int fe_per(const nx_network* h) { return h->fe_sk * (int)h->N + 1 + (int)h->N; }
+// rows per edge of the layouts nx_create_fe may be given: flux degree k, pressure degree m
+// (DG0 for m = 0), by the size of the term table; the first whose templates check out
+bool fe_try_tpl(nx_network* h, int32_t N, int64_t E, int64_t n_rows, int32_t n_table,
+                const int32_t* rowptr, const int32_t* col, const int32_t* kind,
+                const int32_t* a_ptr, const int32_t* a_idx, const int32_t* a_ent,
+                const int32_t* b_ptr, const int32_t* b_idx, const int32_t* b_ent) {
+  for (int k = 1; k <= 16; ++k)
+    for (int m = 0; m < k || (m == 0 && k == 1); ++m) {
+      const int npl = m == 0 ? 1 : m + 1;
+      if (n_table != (k + 1) * (k + 1) + npl * (k + 1) + 2 + npl + 1) continue;
+      const int per = k * N + 1 + (m == 0 ? N : m * N - 1);
+      if (E * (int64_t)per > n_rows) continue;
+      if (fe_build_tpl(h, per, N, E, n_rows, rowptr, col, kind, a_ptr, a_idx, a_ent, b_ptr,
+                       b_idx, b_ent))
+        return true;
+    }
+  return false;
+}
+int fe_per(const nx_network* h) { return h->fe_tpl_per; }
 bool fe_tpl_on(const nx_network* h) {
   const char* e = std::getenv("NXHIP_FE_STRUCT");  // read per launch: tests switch it
   return h->fe_tpl && (e == nullptr || std::atoi(e) != 0);
 }
 FeTpl fe_tpl_args(const nx_network* h, int edge_blocks) {
-  FeTpl t{h->fe_tpl_buf, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam, h->rowptr, {},
-          h->fe_sk, h->fe_sk * (int)h->N + 1, fe_per(h), edge_blocks};
-  for (int i = 0; i < 5; ++i) t.off[i] = h->fe_tpl_off[i];
+  FeTpl t{h->fe_tpl_buf, h->fe_tpl_rbuf, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam, h->rowptr,
+          {}, h->fe_tpl_nsh, h->fe_tpl_per, edge_blocks};
+  for (int i = 0; i <= kFeShapes; ++i) t.off[i] = h->fe_tpl_off[i];
   return t;
+}
+void opt_in_lds(const void* fn, int bytes);
+// the dynamic LDS of the template kernels (opted in past 64 KiB: high degrees, long edges)
+size_t fe_tpl_lds_of(const nx_network* h, bool res) {
+  const size_t b = fe_tpl_lds(h->fe_tpl_off[h->fe_tpl_nsh], h->fe_tpl_nsh, h->fe_tpl_per,
+                              (int)h->N, res);
+  if (b > 64 * 1024)
+    opt_in_lds(res ? reinterpret_cast<const void*>(&k_fe_tres)
+                   : reinterpret_cast<const void*>(&k_fe_tasm), 150 * 1024);
+  return b;
 }
 // edge workgroups of the template kernels: rounds of kFesWaves edges, a few per CU
 int fe_tpl_blocks(const nx_network* h) {
@@ -8312,7 +8436,8 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
   }
   h->fe_sk = fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr, a_idx, a_ent,
                               b_ptr, b_idx, b_ent);
-  if (h->fe_sk > 0) h->fe_tpl = fe_build_tpl(h, h->fe_sk, N, n_edges, rowptr, col);
+  h->fe_tpl = fe_try_tpl(h, N, n_edges, n_rows, n_table, rowptr, col, table_kind, a_ptr, a_idx,
+                         a_ent, b_ptr, b_idx, b_ent);
   *out = h;
   return NX_OK;
 }
@@ -8323,6 +8448,13 @@ int xr_alloc(nx_network* h, int P);
 int xr_link(nx_network* h, const std::vector<XPeer>& peers);
 XPeer xpeer_of(void* base, int P);
 }  // namespace
+
+NX_API int nx_fe_templates(nx_network_t* h, int32_t* n_shapes, int32_t* rows_per_edge) {
+  if (!h || !n_shapes || !rows_per_edge) return fail(NX_ERR_ARG, "null argument");
+  *n_shapes = h->fe_tpl ? h->fe_tpl_nsh : 0;
+  *rows_per_edge = h->fe_tpl ? h->fe_tpl_per : 0;
+  return NX_OK;
+}
 
 NX_API int nx_destroy(nx_network_t* h) {
   if (h) h->pend_lhs = h->pend_rhs = 0;  // nothing to assemble for a dying handle
@@ -8354,7 +8486,7 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_tI,
                   h->cp_eb, h->cp_nrow, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
                   h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown, h->fe_tpl_buf,
-                  h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
+                  h->fe_tpl_rbuf, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (void* p : h->pc_bufs)
@@ -8453,8 +8585,7 @@ int launch_assembly(nx_network* h, int lhs, int rhs, int dq = -1, hipStream_t s 
       const int eb = fe_tpl_blocks(h);
       const int lb = (int)grid_of(h->n_own - h->E * (int64_t)fe_per(h), 64 * kFesWaves);
       hipExtLaunchKernelGGL(k_fe_tasm, dim3(eb + lb), dim3(64 * kFesWaves),
-                            fe_tpl_lds(h->fe_tpl_off[4], fe_per(h), (int)h->N, false), s, e0, e1,
-                            0, a, fe_tpl_args(h, eb));
+                            fe_tpl_lds_of(h, false), s, e0, e1, 0, a, fe_tpl_args(h, eb));
     } else {
       hipExtLaunchKernelGGL(k_assemble_fe, dim3(grid_of(std::max(h->nnz, h->n_own), kBlock)),
                             dim3(kBlock), 0, s, e0, e1, 0, a);
@@ -8691,8 +8822,10 @@ LeanGraphs& lean_of(const Team& t) { return t.g ? t.g->lean : t.hs[0]->lean; }
 // One rank, direct: the top part in every down workgroup (pa.topdown) -- only when the jobs
 // run in one round (every workgroup repeats the top part; C4 on one GPU, 4 rounds, measured
 // 0.524 vs 0.488 ms/step with the top kernel)
+// (an auxiliary solve of the (k, 0) route too: no residual check, workgroup 0 writes x's top
+// values itself)
 bool top_down_on(const nx_network* h) {
-  return h->fres_ok && h->top_nt > 0 && h->pc_jobs <= h->n_cu;
+  return (h->fres_ok || h->cond_mass) && h->top_nt > 0 && h->pc_jobs <= h->n_cu;
 }
 
 template <int W, int CPL>
@@ -9850,6 +9983,7 @@ int check_schedules(const Team& t) {
 // auxiliary handle's tree solve on its stream, expand, then this CSR's true residual,
 // published. Up to two refinement passes (x += the same solve of r). *converged = 0 when
 // still above rtol: the caller runs MINRES.
+void fe_true_residual(nx_network* h, double rtol, int nrb);
 int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
                     int32_t* converged) {
   nx_network* a = h->fe_aux;
@@ -9881,25 +10015,7 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
     }
     hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
                        c, a->x, b, h->x, pass);
-    if (fe_tpl_on(h) && h->asm_coef_version == h->coef_version) {
-      // the true residual from the templates (A's entries formed again: no CSR reads)
-      const int lb = grid_of(h->n_own - h->E * (int64_t)fe_per(h), 64 * kFesWaves);
-      const int eb = std::max(1, std::min(fe_tpl_blocks(h), h->nblk - lb));
-      const FeArgs fa{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind,
-                      h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx,
-                      h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E, h->fe_cellh};
-      hipLaunchKernelGGL(k_fe_tres, dim3(eb + lb), dim3(64 * kFesWaves),
-                         fe_tpl_lds(h->fe_tpl_off[4], fe_per(h), (int)h->N, true), h->stream, fa,
-                         fe_tpl_args(h, eb), csr_of(h), h->x, h->rhs, h->tmp, h->partials,
-                         eb + lb);
-      hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                         eb + lb, rtol, h->d_seq, h->d_last);
-    } else {
-      hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                         h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
-      hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                         nrb, rtol, h->d_seq, h->d_last);
-    }
+    fe_true_residual(h, rtol, nrb);
     HIPCALL(hipGetLastError());
     h->seq += 1;
     CHECK(wait_published(h));
@@ -9913,10 +10029,61 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
 }
 
 // Continuous pressure (k > m >= 1) on one rank, a forest (nx_fe_set_cp): the node-condensed
-// direct solve -- per edge its forward sweep, the border system by one workgroup, per edge
+// direct solve -- per edge its forward sweep, the node forest level by level, per edge
 // its back-substitution -- then this CSR's true residual, published. Up to two refinement
 // passes (the same solve of r = b - A x, added). *converged = 0 when still above rtol: the
 // caller runs MINRES.
+// A general-degree handle's true residual r = b - A x (kept in tmp for a refinement pass) and
+// its published relres: from the edge templates while the CSR holds the assembled
+// coefficients (no CSR reads for the edges' rows), else from the CSR
+void fe_true_residual(nx_network* h, double rtol, int nrb) {
+  if (fe_tpl_on(h) && h->asm_coef_version == h->coef_version) {
+    const int lb = grid_of(h->n_own - h->E * (int64_t)fe_per(h), 64 * kFesWaves);
+    const int eb = std::max(1, std::min(fe_tpl_blocks(h), h->nblk - lb));
+    const FeArgs fa{h->edge_x, h->edge_R, h->edge_bc, h->f, h->edge_f, h->N, h->fe_kind,
+                    h->fe_tval, h->fe_aptr, h->fe_aidx, h->fe_aent, h->fe_bptr, h->fe_bidx,
+                    h->fe_bent, h->nnz, h->n_own, h->val, h->rhs, 1, 0, h->E, h->fe_cellh};
+    hipLaunchKernelGGL(k_fe_tres, dim3(eb + lb), dim3(64 * kFesWaves), fe_tpl_lds_of(h, true),
+                       h->stream, fa, fe_tpl_args(h, eb), csr_of(h), h->x, h->rhs, h->tmp,
+                       h->partials, eb + lb);
+    hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                       eb + lb, rtol, h->d_seq, h->d_last);
+    return;
+  }
+  hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                     h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
+  hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
+                     nrb, rtol, h->d_seq, h->d_last);
+}
+
+// The node forest's solve: levels of more than kCpWide nodes as grid launches (a thread per
+// node), the runs of narrower levels in one workgroup each; up deepest first, then down.
+constexpr int kCpWide = 2048;
+void cp_nodes_launch(nx_network* h, const CpArgs& a, const CpTree& tr, const double* b) {
+  const std::vector<int>& lo = h->cp_lev_host;
+  const int nl = h->cp_nlev;
+  auto wide = [&](int L) { return lo[L + 1] - lo[L] > kCpWide; };
+  for (int up = 1; up >= 0; --up) {
+    // runs of levels in the pass's order: a wide level alone, consecutive narrow ones together
+    int k = 0;
+    while (k < nl) {
+      const int L = up ? nl - 1 - k : k;
+      if (wide(L)) {
+        const int n = lo[L + 1] - lo[L];
+        hipLaunchKernelGGL(k_cp_level, dim3(grid_of(n, 256)), dim3(256), 0, h->stream, a, tr, b,
+                           lo[L], lo[L + 1], up);
+        ++k;
+        continue;
+      }
+      int k1 = k;
+      while (k1 < nl && !wide(up ? nl - 1 - k1 : k1)) ++k1;
+      const int La = up ? nl - k1 : k, Lb = up ? nl - k : k1;  // levels [La, Lb)
+      hipLaunchKernelGGL(k_cp_nodes, dim3(1), dim3(1024), 0, h->stream, a, tr, b, La, Lb, up);
+      k = k1;
+    }
+  }
+}
+
 int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int32_t* converged) {
   CHECK(flush_assembly(h));
   const CpArgs a{(int)h->N, h->cp_k, h->cp_m, h->cp_nI, h->E, h->edge_R, h->fe_cellh, h->cp_cst,
@@ -9924,20 +10091,18 @@ int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int3
   const CpTree tr{h->cp_nn, h->cp_nlev, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
                   h->cp_parent, h->cp_child_off, h->cp_child, h->cp_Pinv, h->cp_hv};
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
-  const int eb = grid_of(h->E, 256);
+  // (one thread per edge: 64-thread workgroups spread the edges over every CU)
+  const int eb = grid_of(h->E, 64);
   MrState s{};
   int pass = 0;
   h->last_dir_path = 4;  // the node-condensed route (nx_get_direct_path)
   for (; pass < 3; ++pass) {
     const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
-    hipLaunchKernelGGL(k_cp_edge, dim3(eb), dim3(256), 0, h->stream, a, b);
-    hipLaunchKernelGGL(k_cp_nodes, dim3(1), dim3(1024), 0, h->stream, a, tr, b);
-    hipLaunchKernelGGL(k_cp_back, dim3(eb), dim3(256), 0, h->stream, a, b, h->x, h->cp_nown,
+    hipLaunchKernelGGL(k_cp_edge, dim3(eb), dim3(64), 0, h->stream, a, b);
+    cp_nodes_launch(h, a, tr, b);
+    hipLaunchKernelGGL(k_cp_back, dim3(eb), dim3(64), 0, h->stream, a, b, h->x, h->cp_nown,
                        pass ? 1 : 0);
-    hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
-                       h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
-    hipLaunchKernelGGL(k_dir_publish, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials,
-                       nrb, rtol, h->d_seq, h->d_last);
+    fe_true_residual(h, rtol, nrb);
     HIPCALL(hipGetLastError());
     h->seq += 1;
     CHECK(wait_published(h));
@@ -11310,6 +11475,7 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   h->cp_nI = nI;
   h->cp_nn = (int)n;
   h->cp_nlev = n_lev;
+  h->cp_lev_host.assign(lev_off, lev_off + n_lev + 1);
   h->fe_cp = true;
   return NX_OK;
 }

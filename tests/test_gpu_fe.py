@@ -275,3 +275,25 @@ def test_fe_continuous_pressure_cycles_run_minres():
     got = np.concatenate([fn.x.array for fn in sol])
     x_ref = O.solve_reference(A, b)
     assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+
+
+@pytest.mark.parametrize("case", ["depth6_N40", "arterial5_N40"])
+@pytest.mark.parametrize("k", [2, 3])
+def test_fe_condensed_template_residual_bits(case, k, monkeypatch):
+    """The condensed route with the edge templates (assembly k_fe_tasm, residual k_fe_tres)
+    gives x bit for bit as with the gather tables and the CSR residual (the same matrix and
+    rhs bits, the same solve); the reported residuals agree to rounding."""
+    E = len(CASES[case][0]().edges())
+    R = 1.0 + 0.5 * (np.arange(E) % 3)
+    mesh, asm, F, A, b, pbc = _setup(case, (k, 0), f=0.4, R=R)
+    assert asm.handle.fe_templates()[0] > 0
+    solver = Solver(asm)
+    out = []
+    for struct in ("1", "0"):
+        monkeypatch.setenv("NXHIP_FE_STRUCT", struct)
+        solver.assemble()
+        solver.solve()
+        assert solver.ksp.solver_used == "direct" and solver.ksp.iterations == 1
+        out.append((asm.handle.solution(), solver.ksp.residual_estimate))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert abs(out[0][1] - out[1][1]) <= 1e-3 * out[1][1] + 1e-16
