@@ -346,7 +346,9 @@ def run(args, world: int) -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local_rank)
+    # (ranks beyond the visible GPUs share them: a one-GPU rehearsal of the multi-rank path
+    # with NXHIP_TRANSPORT=host; the driver's runs give every rank its own GPU)
+    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
 
     from networks_fenicsx_amd import HydraulicNetworkAssembler, NetworkMesh, Solver
     from networks_fenicsx_amd import network_generation as ng
