@@ -81,7 +81,7 @@ int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
 /*
  * General element degrees: HydraulicNetworkAssembler(mesh, flux_degree=k,
  * pressure_degree=m) (assembly.py:121-146) -- P_k equispaced flux per edge, DG0 (m = 0)
- * or continuous P_m pressure. One rank; no tree preconditioner (plain MINRES). The host
+ * or continuous P_m pressure. No tree preconditioner (plain MINRES). The host
  * (networks_fenicsx_amd/layout_fe.py) numbers the DoFs, gives the sorted CSR pattern and
  * lists, for every nonzero and every rhs row, its terms in summation order; the device
  * evaluates them on every nx_assemble (k_assemble_fe: one thread per nonzero / row):
@@ -92,14 +92,17 @@ int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
  *   h_c is the cell length from edge_x, computed like the reference mesh generator.
  *
  *   n_rows, rowptr (n_rows+1), col   the symmetric system's CSR pattern (sorted rows)
+ *   n_ghost                          several ranks, (k, 0): columns n_rows.. are ghosts
+ *                                    (layout_fe.build_fe_rank_layout; nx_comm_init then
+ *                                    gives the halo plan, as for nx_create); 0 on one rank
  *   n_table, table_kind, table_val   the term table (reference element tensors, signs)
  *   a_ptr (nnz+1), a_idx, a_ent      the terms of every nonzero
  *   b_ptr (n_rows+1), b_idx, b_ent   the terms of every rhs row
  * nx_set_coefficients, nx_assemble, nx_solve and the getters work as for nx_create.
  */
 int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
-                 int64_t n_rows, const int32_t* rowptr, const int32_t* col, int32_t n_table,
-                 const int32_t* table_kind, const double* table_val, const int32_t* a_ptr,
+                 int64_t n_rows, const int32_t* rowptr, const int32_t* col, int64_t n_ghost,
+                 int32_t n_table, const int32_t* table_kind, const double* table_val, const int32_t* a_ptr,
                  const int32_t* a_idx, const int32_t* a_ent, const int32_t* b_ptr,
                  const int32_t* b_idx, const int32_t* b_ent, nx_network_t** out);
 
@@ -302,6 +305,9 @@ int nx_set_cycles_team(nx_network_t* h, int32_t K, const int32_t* own, const int
  *   nx_solve condenses, solves on aux, expands, checks h's true residual and refines up to
  *   twice (iters = passes), MINRES when that still misses rtol. layout_fe.build_fe_aux_maps
  *   builds the maps. Replaces MUMPS' LU of the (k, 0) system (solver.py:58-65).
+ *   Several ranks: h (n_ghost > 0) and aux (the rank's P1/DG0 handle with its halo, cut rows
+ *   and preconditioner) each joined to the ranks' communicator; the aux solve is the ranks'
+ *   direct tree solve, h's residual takes the halo of x and one all-reduce.
  */
 int nx_set_cell_mass(nx_network_t* aux, double ratio, double mo_div);
 int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64_t n_lm,

@@ -40,7 +40,7 @@ _SIGS = {
     "nx_device_count": (C.c_int, [_pi32]),
     "nx_create": (C.c_int, [_i32, _i32, _i64, _pd, _pi32, _i64, _pi32, _pi32, _pd, _i64,
                             C.POINTER(_h)]),
-    "nx_create_fe": (C.c_int, [_i32, _i32, _i64, _pd, _i64, _pi32, _pi32, _i32, _pi32, _pd,
+    "nx_create_fe": (C.c_int, [_i32, _i32, _i64, _pd, _i64, _pi32, _pi32, _i64, _i32, _pi32, _pd,
                                _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, C.POINTER(_h)]),
     "nx_fe_struct_degree": (C.c_int, [_i32, _i64, _i64, _pi32, _pi32, _i32, _pi32, _pi32,
                                       _pi32, _pi32, _pi32, _pi32, _pi32]),
@@ -235,7 +235,8 @@ class Handle:
     @classmethod
     def create_fe(cls, device: int, lay) -> "Handle":
         """Handle for general element degrees from a :class:`layout_fe.FeLayout`
-        (``nx_create_fe``: one rank, CSR pattern and term tables from the host)."""
+        (``nx_create_fe``: CSR pattern and term tables from the host; a rank layout's ghost
+        columns follow its owned rows)."""
         L = lib()
         self = cls.__new__(cls)
         self._keep = []
@@ -248,7 +249,7 @@ class Handle:
         tval = np.ascontiguousarray(lay.table_val, dtype=np.float64)
         check(L.nx_create_fe(int(device), int(lay.N), int(lay.E), _ptr(edge_x, C.c_double),
                              int(lay.n_rows), _ptr(rp, C.c_int32), _ptr(col, C.c_int32),
-                             int(kind.size), _ptr(kind, C.c_int32), _ptr(tval, C.c_double),
+                             int(getattr(lay, "n_ghost", 0)), int(kind.size), _ptr(kind, C.c_int32), _ptr(tval, C.c_double),
                              _ptr(ap, C.c_int32), _ptr(ai, C.c_int32), _ptr(ae, C.c_int32),
                              _ptr(bp, C.c_int32), _ptr(bi, C.c_int32), _ptr(be, C.c_int32),
                              C.byref(h)))

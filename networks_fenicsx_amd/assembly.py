@@ -38,7 +38,8 @@ from .fem import Constant, Function, FunctionSpace
 from .element import condensed_flux_mass, stable_pair
 from .layout import (LocalProblem, build_local_problem, cycle_pairs_global,
                      team_cycle_tables)
-from .layout_fe import FeLayout, build_cp_tables, build_fe_aux_maps, build_fe_layout
+from .layout_fe import (FeLayout, build_cp_tables, build_fe_aux_maps, build_fe_layout,
+                        build_fe_rank_layout, fe_aux_slots)
 from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
@@ -263,7 +264,8 @@ class HydraulicNetworkAssembler:
         mesh: the :class:`NetworkMesh`
         flux_degree: degree k of the equispaced Lagrange flux on every edge (default 1)
         pressure_degree: 0 for DG0 pressure (default), m >= 1 for continuous P_m (needs
-            k > m); anything but (1, 0) runs on one rank without the tree preconditioner
+            k > m); other pairs than (1, 0) run without the tree preconditioner, (k, 0) on
+            one or several ranks, continuous pressure on one
     """
 
     @timed("nxfx:HydraulicNetworkAssembler:__init__")
@@ -297,31 +299,48 @@ class HydraulicNetworkAssembler:
         self._make_spaces()
 
     def _init_general_degrees(self) -> None:
-        """Flux P_k / pressure DG0 or continuous P_m (``layout_fe.py``): one rank, gather
-        assembly (``nx_create_fe``), plain MINRES -- the tree preconditioner is P1/DG0's."""
+        """Flux P_k / pressure DG0 or continuous P_m (``layout_fe.py``): gather assembly
+        (``nx_create_fe``), the condensed direct solves, plain MINRES otherwise -- the tree
+        preconditioner is P1/DG0's. Several ranks: (k, 0), one process per rank, each rank
+        the edges of its P1/DG0 rank layout (``layout_fe.build_fe_rank_layout``)."""
         mesh = self._network_mesh
         k, m = self._degrees
         if not stable_pair(k, m):
             raise ValueError(
                 f"flux_degree={k}, pressure_degree={m}: with continuous pressure the flux degree "
                 "must exceed the pressure degree (otherwise the system is singular)")
-        if self._nranks > 1:
-            raise NotImplementedError("flux_degree / pressure_degree other than (1, 0) run on "
-                                      "one rank; the partitioned path is P1/DG0")
+        ranks = self._nranks > 1
+        if ranks and m != 0:
+            raise NotImplementedError("continuous pressure (pressure_degree >= 1) runs on one "
+                                      "rank; several ranks run (k, 0)")
+        if ranks and isinstance(mesh.comm, GroupRankComm):
+            raise NotImplementedError("general degrees on several ranks run one process per "
+                                      "rank (RCCL), not an in-process group")
         src, dst = mesh.edges
         self._local = None
-        self._fe = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, k, m)
+        self._fe_lp = None
+        if ranks:
+            self._fe_lp = build_local_problem(mesh.node_coordinates, src, dst, mesh.degrees,
+                                              mesh.N, self._rank, self._nranks)
+            self._fe = build_fe_rank_layout(mesh.node_coordinates, src, dst, mesh.N, k,
+                                            self._fe_lp)
+            self._edge_ids = np.asarray(self._fe_lp.edges)
+        else:
+            self._fe = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, k, m)
+            self._edge_ids = np.arange(mesh.num_edges)
         self._handle = _lib.Handle.create_fe(_device_for_rank(), self._fe)
-        self._edge_ids = np.arange(mesh.num_edges)
-        self._pc_on = False
         fe = self._fe
-        colors = mesh.edge_colors
+        if ranks:
+            self._join_comm(self._handle, fe.peers, fe.send_off, fe.send_idx, fe.recv_off)
+        self._pc_on = False
+        colors = mesh.edge_colors[self._edge_ids]
         self._flux_spaces, self._flux_idx = [], []
         for c in range(mesh.num_edge_colors):
-            edges = np.flatnonzero(colors == c)  # graph.edges() order inside a colour
+            slots = np.flatnonzero(colors == c)  # graph.edges() order inside a colour
+            edges = self._edge_ids[slots]
             self._flux_spaces.append(
                 FunctionSpace(mesh, "flux", "P", k, False, edges.size * (k * mesh.N + 1), edges, c))
-            self._flux_idx.append(fe.flux_rows[edges].ravel())
+            self._flux_idx.append(fe.flux_rows[slots].ravel())
         if m == 0:
             self._pressure_space = FunctionSpace(mesh, "pressure", "DG", 0, True,
                                                  fe.p_rows.size, self._edge_ids)
@@ -346,30 +365,52 @@ class HydraulicNetworkAssembler:
 
     def _init_fe_direct(self, src, dst) -> None:
         """(k, 0): the direct solve through the condensed P1/DG0 system (``nx_fe_set_direct``).
-        An auxiliary P1/DG0 handle of the same graph carries the tree decomposition; its flux
+        An auxiliary P1/DG0 handle of the same edges carries the tree decomposition; its flux
         mass becomes the condensed ``R h [[a, b], [b, a]]`` (``element.condensed_flux_mass``),
         whose ratios are integers: ``a / b = (-1)^(k+1) (k+1)``. Forests only (a graph with
-        cycles runs MINRES: the Woodbury correction is built from the P1 CSR)."""
+        cycles runs MINRES: the Woodbury correction is built from the P1 CSR). Several ranks:
+        the auxiliary handle is the rank's P1/DG0 handle (its halo, cut rows, coarse step),
+        and the ranks attach it only if every rank can run its direct tree solve."""
         mesh, fe = self._network_mesh, self._fe
         k = self._degrees[0]
-        lp = build_local_problem(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, 0, 1)
+        ranks = self._nranks > 1
+        lp = self._fe_lp if ranks else build_local_problem(mesh.node_coordinates, src, dst,
+                                                           mesh.degrees, mesh.N, 0, 1)
         pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=256)
-        if not pc.tree_exact:
+        aux = None
+        ok = bool(pc.tree_exact)
+        if ranks:  # (every rank makes the same collective calls below: decide together)
+            ok = int(self._network_mesh.comm.allreduce(int(ok), MIN)) == 1
+        if ok:
+            aux = _lib.Handle(_device_for_rank(), mesh.N, lp.edge_x, lp.edge_lm, lp.lm_rowptr,
+                              lp.lm_col, lp.lm_val, lp.n_ghost)
+            if ranks:
+                self._join_comm(aux, lp.peers, lp.send_off, lp.send_idx, lp.recv_off)
+                aux.set_cut(lp.n_cut, lp.lm_cut, lp.gk_off, lp.gk_row, lp.gk_coef)
+            aux.set_preconditioner(pc)
+            ok = aux.pc_lds()
+        if ok:
+            alpha, beta, C, K, Mii = condensed_flux_mass(k)
+            ratio = round(alpha / beta)
+            assert abs(alpha / beta - ratio) < 1e-12, (alpha, beta)
+            aux.set_cell_mass(float(ratio), float(ratio + 1))
+            aux.set_solver(True, True)  # (its sweeps invert an exact forest decomposition)
+            maps = build_fe_aux_maps(fe, lp)
+            cst = np.concatenate([C.ravel(), K.ravel(), Mii.ravel()])
+            try:
+                self._handle.fe_set_direct(aux, k, fe_aux_slots(fe, lp), maps, cst, alpha + beta)
+            except _lib.NxError:
+                if not ranks:
+                    raise
+                ok = False
+        if ranks and int(self._network_mesh.comm.allreduce(int(ok), MIN)) == 0:
+            if ok:  # another rank cannot: every rank runs MINRES
+                self._handle.fe_set_direct(None, k, None, None, None, 0.0)
+            ok = False
+        if not ok:
+            if aux is not None:
+                aux.close()
             return
-        aux = _lib.Handle(_device_for_rank(), mesh.N, lp.edge_x, lp.edge_lm, lp.lm_rowptr,
-                          lp.lm_col, lp.lm_val, lp.n_ghost)
-        aux.set_preconditioner(pc)
-        if not aux.pc_lds():
-            return
-        alpha, beta, C, K, Mii = condensed_flux_mass(k)
-        ratio = round(alpha / beta)
-        assert abs(alpha / beta - ratio) < 1e-12, (alpha, beta)
-        aux.set_cell_mass(float(ratio), float(ratio + 1))
-        slot = np.full(mesh.num_edges, -1, dtype=np.int64)
-        slot[np.asarray(lp.edges)] = np.arange(np.asarray(lp.edges).size)
-        maps = build_fe_aux_maps(fe, lp)
-        cst = np.concatenate([C.ravel(), K.ravel(), Mii.ravel()])
-        self._handle.fe_set_direct(aux, k, slot, maps, cst, alpha + beta)
         self._fe_aux = aux
         self._fe_aux_pc = pc
 
@@ -381,6 +422,19 @@ class HydraulicNetworkAssembler:
         return (getattr(self, "_fe_aux", None) is not None
                 or getattr(self, "_fe_cp", None) is not None)
 
+    def _join_comm(self, handle: _lib.Handle, peers, send_off, send_idx, recv_off) -> None:
+        """``handle`` joins the ranks' communicator with this halo plan (rank 0 makes the id,
+        the mesh's communicator broadcasts it; every rank calls this in the same order)."""
+        comm = self._network_mesh.comm
+        if os.environ.get("NXHIP_TRANSPORT", "rccl") == "host":
+            # tests: several ranks' processes on ONE GPU (RCCL refuses that) -- the same
+            # host logic with its collectives through shared memory (nx_comm_init_host)
+            uid = f"/nxhip_{os.getpid()}_{secrets.token_hex(6)}" if self._rank == 0 else None
+        else:
+            uid = _lib.comm_unique_id() if self._rank == 0 else None
+        uid = comm.bcast(uid, root=0)
+        handle.comm_init(self._nranks, self._rank, uid, peers, send_off, send_idx, recv_off)
+
     def _init_comm(self) -> None:
         comm = self._network_mesh.comm
         lp = self._local
@@ -388,15 +442,7 @@ class HydraulicNetworkAssembler:
             self._handle.set_halo(self._nranks, self._rank, lp.peers, lp.send_off, lp.send_idx,
                                   lp.recv_off)
         else:
-            if os.environ.get("NXHIP_TRANSPORT", "rccl") == "host":
-                # tests: several ranks' processes on ONE GPU (RCCL refuses that) -- the same
-                # host logic with its collectives through shared memory (nx_comm_init_host)
-                uid = f"/nxhip_{os.getpid()}_{secrets.token_hex(6)}" if self._rank == 0 else None
-            else:
-                uid = _lib.comm_unique_id() if self._rank == 0 else None
-            uid = comm.bcast(uid, root=0)
-            self._handle.comm_init(self._nranks, self._rank, uid, lp.peers, lp.send_off,
-                                   lp.send_idx, lp.recv_off)
+            self._join_comm(self._handle, lp.peers, lp.send_off, lp.send_idx, lp.recv_off)
             # the exchange step's mailboxes (nx_xch_*): every rank maps every rank's; a rank
             # that cannot export one leaves every rank on the graph path (RCCL all-reduces)
             try:

@@ -8383,14 +8383,15 @@ NX_API int nx_fe_struct_degree(int32_t N, int64_t n_edges, int64_t n_rows, const
 
 NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
                         int64_t n_rows, const int32_t* rowptr, const int32_t* col,
-                        int32_t n_table, const int32_t* table_kind, const double* table_val,
+                        int64_t n_ghost, int32_t n_table, const int32_t* table_kind,
+                        const double* table_val,
                         const int32_t* a_ptr, const int32_t* a_idx, const int32_t* a_ent,
                         const int32_t* b_ptr, const int32_t* b_idx, const int32_t* b_ent,
                         nx_network_t** out) {
   if (out == nullptr) return fail(NX_ERR_ARG, "out is NULL");
   *out = nullptr;
-  if (N < 1 || n_edges < 1 || n_rows < 1 || n_table < 1)
-    return fail(NX_ERR_ARG, "N, n_edges, n_rows and n_table must be >= 1");
+  if (N < 1 || n_edges < 1 || n_rows < 1 || n_table < 1 || n_ghost < 0)
+    return fail(NX_ERR_ARG, "N, n_edges, n_rows and n_table must be >= 1, n_ghost >= 0");
   if (!edge_x || !rowptr || !col || !table_kind || !table_val || !a_ptr || !a_idx || !a_ent ||
       !b_ptr || !b_idx || !b_ent)
     return fail(NX_ERR_ARG, "NULL array");
@@ -8409,7 +8410,8 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
   // the pattern and allocates the solver; the edge data and term tables are added here
   std::vector<double> zeros((size_t)std::max<int64_t>(nnz, 1), 0.0);
   nx_network_t* h = nullptr;
-  CHECK(nx_create(device, N, 0, nullptr, nullptr, n_rows, rowptr, col, zeros.data(), 0, &h));
+  CHECK(nx_create(device, N, 0, nullptr, nullptr, n_rows, rowptr, col, zeros.data(), n_ghost,
+                  &h));
   h->fe = true;
   h->E = n_edges;
   int rc = NX_OK;
@@ -8434,10 +8436,11 @@ NX_API int nx_create_fe(int32_t device, int32_t N, int64_t n_edges, const double
     nx_destroy(h);
     return fail(NX_ERR_HIP, "cell lengths failed");
   }
-  h->fe_sk = fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr, a_idx, a_ent,
-                              b_ptr, b_idx, b_ent);
-  h->fe_tpl = fe_try_tpl(h, N, n_edges, n_rows, n_table, rowptr, col, table_kind, a_ptr, a_idx,
-                         a_ent, b_ptr, b_idx, b_ent);
+  // (a rank layout's ghost columns are outside both analyses: the gather tables run it)
+  h->fe_sk = n_ghost ? 0 : fe_struct_degree(N, n_edges, n_rows, rowptr, col, n_table, a_ptr,
+                                            a_idx, a_ent, b_ptr, b_idx, b_ent);
+  h->fe_tpl = n_ghost ? false : fe_try_tpl(h, N, n_edges, n_rows, n_table, rowptr, col,
+                                           table_kind, a_ptr, a_idx, a_ent, b_ptr, b_idx, b_ent);
   *out = h;
   return NX_OK;
 }
@@ -9107,10 +9110,12 @@ bool cut_mode(const nx_network* h) {
 
 // asmb (first pass): every rank's assembly is pending and heads its first half --
 // k_dir_team_up where it applies (assembly + up sweep + top part in one launch), else the
-// assembly kernel then the sweeps.
+// assembly kernel then the sweeps. check = false: the sweeps only (x = A^{-1} b, no residual
+// and no publish -- the (k, 0) route's auxiliary solve, whose CSR is not its system).
 int cyc_gather_team(const Team& t, bool prev);
 int cyc_fix_team(const Team& t, double rtol, bool refine);
-int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false) {
+int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false,
+                       bool check = true) {
   nx_network* h0 = t.hs[0];
   // graphs with cycles (nx_set_cycles_team): after the sweeps (A_g^{-1} b) the Woodbury
   // correction and the CSR's true residual publish; the sweeps' own residual is A_g's
@@ -9143,6 +9148,7 @@ int launch_direct_team(const Team& t, double rtol, int refine, bool asmb = false
     }
     if (half == 0) CHECK(team_allreduce(t, -1, 3 * h0->pa.n_coarse));
   }
+  if (!check) return NX_OK;
   if (cut_mode(h0)) {  // the cut rows ride in the residual's all-reduce: no halo of x
     for (int r = 0; r < t.P; ++r) {
       nx_network* h = t.hs[r];
@@ -9978,15 +9984,36 @@ int check_schedules(const Team& t) {
   return NX_OK;
 }
 
-// (k, 0) on one rank through the condensed P1/DG0 system (nx_fe_set_direct): condense the
-// right-hand side (and, first pass, the auxiliary lumped mass) on this handle's stream, the
-// auxiliary handle's tree solve on its stream, expand, then this CSR's true residual,
-// published. Up to two refinement passes (x += the same solve of r). *converged = 0 when
-// still above rtol: the caller runs MINRES.
+// (k, 0) through the condensed P1/DG0 system (nx_fe_set_direct): condense the right-hand
+// side (and, first pass, the auxiliary lumped mass) on this handle's stream, the auxiliary
+// handle's tree solve on its stream, expand, then this CSR's true residual, published. Up
+// to two refinement passes (x += the same solve of r). *converged = 0 when still above
+// rtol: the caller runs MINRES. Several ranks (process ranks: RCCL or the host transport):
+// the auxiliary solve is the ranks' direct tree solve (launch_direct_team: the coarse step's
+// all-reduce, the cut rows), condense and expand stay per edge, and the true residual takes
+// the halo of x and one all-reduce of two sums.
 void fe_true_residual(nx_network* h, double rtol, int nrb);
+int fe_true_residual_team(nx_network* h, double rtol, int nrb) {
+  nx_network* hs[1] = {h};
+  const Team t{hs, 1, nullptr};
+  CHECK(team_halo(t, VS_X, 0));
+  hipLaunchKernelGGL(k_residual_ck, dim3(nrb), dim3(kBlock), 0, h->stream, csr_of(h), h->x,
+                     h->rhs, h->partials, nrb, h->tmp, res_chunks(h->n_own));
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials, nrb,
+                     h->red + 2);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, h->stream, h->partials + nrb,
+                     nrb, h->red + 3);
+  HIPCALL(hipGetLastError());
+  CHECK(team_allreduce(t, 2, 2));
+  hipLaunchKernelGGL(k_dir_publish_red, dim3(1), dim3(64), 0, h->stream, h->red + 2, rtol,
+                     h->d_seq, h->d_last);
+  HIPCALL(hipGetLastError());
+  return NX_OK;
+}
 int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
                     int32_t* converged) {
   nx_network* a = h->fe_aux;
+  const bool ranks = proc_rank(h);
   CHECK(flush_assembly(h));
   const bool apend = a->pend_lhs || a->pend_rhs;
   CHECK(flush_assembly(a));
@@ -10009,13 +10036,18 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
     {  // the auxiliary tree solve on this handle's stream (no cross-queue hand-offs)
       const hipStream_t as = a->stream;
       a->stream = h->stream;
-      const int rc = launch_direct(a, 0.0, 0);
+      nx_network* ah[1] = {a};
+      const int rc = ranks ? launch_direct_team(Team{ah, 1, nullptr}, 0.0, 0, false, false)
+                           : launch_direct(a, 0.0, 0);
       a->stream = as;
       CHECK(rc);
     }
     hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
                        c, a->x, b, h->x, pass);
-    fe_true_residual(h, rtol, nrb);
+    if (ranks)
+      CHECK(fe_true_residual_team(h, rtol, nrb));
+    else
+      fe_true_residual(h, rtol, nrb);
     HIPCALL(hipGetLastError());
     h->seq += 1;
     CHECK(wait_published(h));
@@ -11413,6 +11445,8 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   CHECK(flush_assembly(h));
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->fe) return fail(NX_ERR_STATE, "a general-degree handle (nx_create_fe)");
+  if (k != 0 && (h->nranks > 1 || h->n_ghost > 0))
+    return fail(NX_ERR_STATE, "continuous pressure runs on one rank");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
   for (double** p : {&h->cp_cst, &h->cp_fac, &h->cp_se, &h->cp_xn, &h->cp_Pinv, &h->cp_hv}) {
@@ -11504,9 +11538,16 @@ NX_API int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64
       !cst)
     return fail(NX_ERR_ARG, "NULL array");
   if (aux->fe || !aux->pc || !aux->cond_mass || aux->N != h->N || aux->E != h->E ||
-      aux->n_cyc > 0 || aux->device != h->device || aux->nranks > 1 || proc_rank(aux) || aux->group)
-    return fail(NX_ERR_STATE, "the auxiliary handle must be a one-rank P1/DG0 tree handle with "
-                              "the same N and edges and its cell mass set (nx_set_cell_mass)");
+      aux->n_cyc > 0 || aux->device != h->device || aux->nranks != h->nranks ||
+      aux->rank != h->rank || proc_rank(aux) != proc_rank(h) || aux->group || h->group)
+    return fail(NX_ERR_STATE, "the auxiliary handle must be a P1/DG0 tree handle of the same "
+                              "ranks with the same N and edges and its cell mass set "
+                              "(nx_set_cell_mass)");
+  if (proc_rank(aux) &&
+      !(aux->pc_lds && aux->pa.exact && aux->tree_exact && aux->pc_jobs > 0 &&
+        aux->pa.n_coarse > 0 && aux->pa.n_coarse <= kCapCoarse))
+    return fail(NX_ERR_STATE, "the auxiliary handle's ranks cannot run the direct tree solve "
+                              "(LDS sweeps, exact forest, the coarse step)");
   const int64_t E = h->E, N = h->N, nv = E * (N + 1), np = E * N, km = k - 1;
   if (h->n_own != E * (k * N + 1 + N) + n_lm || aux->n_own != E * (2 * N + 1) + n_lm)
     return fail(NX_ERR_ARG, "row counts do not match a (k, 0) layout and its P1/DG0 one");
@@ -11823,7 +11864,8 @@ NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_
   if (!h) return fail(NX_ERR_ARG, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(NX_ERR_ARG, "bad rank/nranks");
   if (nranks > 1 && h->pc) return fail(NX_ERR_STATE, "set the halo plan before the preconditioner");
-  if (nranks > 1 && h->fe) return fail(NX_ERR_STATE, "general element degrees run on one rank");
+  if (nranks > 1 && h->fe && h->fe_cp)
+    return fail(NX_ERR_STATE, "continuous pressure runs on one rank");
   if (n_peers < 0 || (n_peers > 0 && (!peer_rank || !send_off || !recv_off)))
     return fail(NX_ERR_ARG, "bad halo plan");
   CHECK(set_device(h));

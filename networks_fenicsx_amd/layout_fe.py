@@ -1,4 +1,4 @@
-"""DoF layout and gather-assembly tables for general element degrees (one rank).
+"""DoF layout and gather-assembly tables for general element degrees.
 
 ``HydraulicNetworkAssembler(mesh, flux_degree=k, pressure_degree=m)`` (reference
 ``assembly.py:121-146``) with ``(k, m) != (1, 0)``. The P1/DG0 default keeps its own layout
@@ -16,6 +16,12 @@ Device layout (``n_rows`` owned rows, no ghosts):
 
 Pressure rows and their rhs are negated, as in the P1 path, so the matrix is symmetric.
 
+Several ranks (DG0 pressure, ``build_fe_rank_layout``): a rank holds the edges, owned
+multipliers and ghost columns of its P1/DG0 rank layout (``layout.build_local_problem``) --
+its local edges' rows, then its owned multipliers, then the ghost columns in the P1 layout's
+order (the multipliers of cut bifurcations owned elsewhere and the remote flux ends its
+multiplier rows read). The halo plan is the P1 rank layout's, renumbered.
+
 Assembly tables: every nonzero and every rhs entry is a short sum of terms
 ``table_val[ent] x factor`` (factor ``R_e h_c``, ``f h_c``, ``edge_bc`` or 1; see
 ``include/nxhip.h`` ``nx_create_fe``). The terms are generated cell by cell from the
@@ -31,7 +37,8 @@ import numpy as np
 
 from .element import element_tensors, stable_pair
 
-__all__ = ["FeLayout", "build_fe_layout", "KIND_CONST", "KIND_MASS", "KIND_SOURCE", "KIND_BC"]
+__all__ = ["FeLayout", "build_fe_layout", "build_fe_rank_layout", "fe_global_rows", "KIND_CONST",
+           "KIND_MASS", "KIND_SOURCE", "KIND_BC"]
 
 KIND_CONST, KIND_MASS, KIND_SOURCE, KIND_BC = 0, 1, 2, 3
 
@@ -59,10 +66,80 @@ class FeLayout:
     lm_nodes: np.ndarray  # bifurcations, ascending
     lm_rows: np.ndarray
     edge_x: np.ndarray  # (E, 6) source xyz, target xyz
+    # several ranks (build_fe_rank_layout): the ghost columns after the owned rows, the
+    # global edge id of every local edge, and the halo plan (nx_set_halo's arrays)
+    n_ghost: int = 0
+    edges: np.ndarray | None = None
+    n_edges_global: int = 0
+    peers: np.ndarray | None = None
+    send_off: np.ndarray | None = None
+    send_idx: np.ndarray | None = None
+    recv_off: np.ndarray | None = None
 
     @property
     def nnz(self) -> int:
         return int(self.col.size)
+
+
+def _tables(k: int, m: int):
+    """The term table (kinds, values) and its entry indices for the pair (k, m)."""
+    Mref, Dref, wref = element_tensors(k, m)
+    nq, npl = k + 1, wref.size
+    ent = {"mass": np.arange(nq * nq).reshape(nq, nq),
+           "b": nq * nq + np.arange(npl * nq).reshape(npl, nq)}
+    ent["plus"] = nq * nq + npl * nq
+    ent["minus"] = ent["plus"] + 1
+    ent["src"] = ent["minus"] + 1 + np.arange(npl)
+    ent["bc"] = int(ent["src"][-1]) + 1
+    table_kind = np.concatenate([np.full(nq * nq, KIND_MASS), np.full(npl * nq, KIND_CONST),
+                                 [KIND_CONST, KIND_CONST], np.full(npl, KIND_SOURCE),
+                                 [KIND_BC]]).astype(np.int32)
+    # negated pressure rows: divergence -Dref (row p, col q); gradient -Dref^T (row q, col p)
+    table_val = np.concatenate([Mref.ravel(), -Dref.ravel(), [1.0, -1.0], -wref, [1.0]])
+    return table_kind, table_val, ent, nq, npl
+
+
+def _cell_terms(qrow, prow, cell, ent, nq, npl, E, N):
+    """Every cell's mass and divergence / gradient terms, in generation order."""
+    rows, cols, idx, ents = [], [], [], []
+    for i in range(nq):
+        for j in range(nq):
+            rows.append(qrow[:, :, i]); cols.append(qrow[:, :, j])  # noqa: E702
+            idx.append(cell); ents.append(np.full((E, N), ent["mass"][i, j]))  # noqa: E702
+    for a in range(npl):
+        for j in range(nq):
+            rows.append(prow[:, :, a]); cols.append(qrow[:, :, j])  # noqa: E702
+            idx.append(cell); ents.append(np.full((E, N), ent["b"][a, j]))  # noqa: E702
+            rows.append(qrow[:, :, j]); cols.append(prow[:, :, a])  # noqa: E702
+            idx.append(cell); ents.append(np.full((E, N), ent["b"][a, j]))  # noqa: E702
+    return rows, cols, idx, ents
+
+
+def _csr_and_rhs(rows, cols, idx, ents, br, bi, be, n_rows):
+    """Terms grouped per (row, column) in generation order -> CSR pattern and term lists;
+    rhs terms grouped per row."""
+    R = np.concatenate([np.ravel(x) for x in rows])
+    C = np.concatenate([np.ravel(x) for x in cols])
+    Ix = np.concatenate([np.ravel(x) for x in idx])
+    T = np.concatenate([np.ravel(x) for x in ents])
+    order = np.lexsort((np.arange(R.size), C, R))  # by row, column, then generation order
+    R, C, Ix, T = R[order], C[order], Ix[order], T[order]
+    new = np.ones(R.size, dtype=bool)
+    new[1:] = (R[1:] != R[:-1]) | (C[1:] != C[:-1])
+    starts = np.flatnonzero(new)
+    a_ptr = np.append(starts, R.size)
+    col = C[starts]
+    rowptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(np.bincount(R[starts], minlength=n_rows), out=rowptr[1:])
+    BR = np.concatenate([np.ravel(x) for x in br])
+    BI = np.concatenate([np.ravel(x) for x in bi])
+    BE = np.concatenate([np.ravel(x) for x in be])
+    border = np.argsort(BR, kind="stable")
+    b_ptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(np.bincount(BR, minlength=n_rows), out=b_ptr[1:])
+    if max(a_ptr[-1], rowptr[-1], n_rows) >= np.iinfo(np.int32).max:
+        raise ValueError("problem too large for 32-bit CSR indices")
+    return rowptr, col, a_ptr, Ix, T, b_ptr, BI[border], BE[border]
 
 
 def build_fe_layout(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degree: np.ndarray,
@@ -99,65 +176,24 @@ def build_fe_layout(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degree: n
         prow = np.where(ppos[None] == 0, node_row[src][:, None, None], prow)
         prow = np.where(ppos[None] == m * N, node_row[dst][:, None, None], prow)
 
-    Mref, Dref, wref = element_tensors(k, m)
-    nq, npl = k + 1, wref.size
-    ent_mass = np.arange(nq * nq).reshape(nq, nq)
-    ent_b = nq * nq + np.arange(npl * nq).reshape(npl, nq)
-    ent_plus = nq * nq + npl * nq
-    ent_minus = ent_plus + 1
-    ent_src = ent_minus + 1 + np.arange(npl)
-    ent_bc = int(ent_src[-1]) + 1
-    table_kind = np.concatenate([np.full(nq * nq, KIND_MASS), np.full(npl * nq, KIND_CONST),
-                                 [KIND_CONST, KIND_CONST], np.full(npl, KIND_SOURCE),
-                                 [KIND_BC]]).astype(np.int32)
-    # negated pressure rows: divergence -Dref (row p, col q); gradient -Dref^T (row q, col p)
-    table_val = np.concatenate([Mref.ravel(), -Dref.ravel(), [1.0, -1.0], -wref, [1.0]])
-
+    table_kind, table_val, ent, nq, npl = _tables(k, m)
     cell = np.arange(E, dtype=np.int64)[:, None] * N + c[None, :]  # (E, N)
-    rows, cols, idx, ent = [], [], [], []
-    for i in range(nq):
-        for j in range(nq):
-            rows.append(qrow[:, :, i]); cols.append(qrow[:, :, j])
-            idx.append(cell); ent.append(np.full((E, N), ent_mass[i, j]))
-    for a in range(npl):
-        for j in range(nq):
-            rows.append(prow[:, :, a]); cols.append(qrow[:, :, j])
-            idx.append(cell); ent.append(np.full((E, N), ent_b[a, j]))
-            rows.append(qrow[:, :, j]); cols.append(prow[:, :, a])
-            idx.append(cell); ent.append(np.full((E, N), ent_b[a, j]))
+    rows, cols, idx, ents = _cell_terms(qrow, prow, cell, ent, nq, npl, E, N)
     # junctions (assembly.py:268-277): +1 at in-edge ends, -1 at out-edge starts, both blocks
     e_in = np.flatnonzero(lm_row[dst] >= 0)
     e_out = np.flatnonzero(lm_row[src] >= 0)
-    for e_set, lam, qr, en in ((e_in, lm_row[dst[e_in]], flux_rows[e_in, -1], ent_plus),
-                               (e_out, lm_row[src[e_out]], flux_rows[e_out, 0], ent_minus)):
+    for e_set, lam, qr, en in ((e_in, lm_row[dst[e_in]], flux_rows[e_in, -1], ent["plus"]),
+                               (e_out, lm_row[src[e_out]], flux_rows[e_out, 0], ent["minus"])):
         z = np.zeros(e_set.size, dtype=np.int64)
-        rows += [lam, qr]; cols += [qr, lam]
-        idx += [z, z]; ent += [np.full(e_set.size, en), np.full(e_set.size, en)]
-    R = np.concatenate([np.ravel(x) for x in rows])
-    C = np.concatenate([np.ravel(x) for x in cols])
-    Ix = np.concatenate([np.ravel(x) for x in idx])
-    T = np.concatenate([np.ravel(x) for x in ent])
-    order = np.lexsort((np.arange(R.size), C, R))  # by row, column, then generation order
-    R, C, Ix, T = R[order], C[order], Ix[order], T[order]
-    new = np.ones(R.size, dtype=bool)
-    new[1:] = (R[1:] != R[:-1]) | (C[1:] != C[:-1])
-    starts = np.flatnonzero(new)
-    a_ptr = np.append(starts, R.size)
-    col = C[starts]
-    rowptr = np.zeros(n_rows + 1, dtype=np.int64)
-    np.cumsum(np.bincount(R[starts], minlength=n_rows), out=rowptr[1:])
-
+        rows += [lam, qr]; cols += [qr, lam]  # noqa: E702
+        idx += [z, z]; ents += [np.full(e_set.size, en), np.full(e_set.size, en)]  # noqa: E702
     # rhs: source on pressure rows, boundary data at both flux ends of every edge
     e_ids = np.arange(E, dtype=np.int64)
     br = [prow[:, :, a] for a in range(npl)] + [flux_rows[:, 0], flux_rows[:, -1]]
     bi = [cell for _ in range(npl)] + [2 * e_ids, 2 * e_ids + 1]
-    be = [np.full((E, N), ent_src[a]) for a in range(npl)] + [np.full(E, ent_bc)] * 2
-    BR = np.concatenate([np.ravel(x) for x in br])
-    BI = np.concatenate([np.ravel(x) for x in bi])
-    BE = np.concatenate([np.ravel(x) for x in be])
-    border = np.argsort(BR, kind="stable")
-    b_ptr = np.zeros(n_rows + 1, dtype=np.int64)
-    np.cumsum(np.bincount(BR, minlength=n_rows), out=b_ptr[1:])
+    be = [np.full((E, N), ent["src"][a]) for a in range(npl)] + [np.full(E, ent["bc"])] * 2
+    rowptr, col, a_ptr, Ix, T, b_ptr, BI, BE = _csr_and_rhs(rows, cols, idx, ents, br, bi, be,
+                                                            n_rows)
 
     if m == 0:
         p_rows = (base[:, None] + nf + c[None, :]).ravel()
@@ -167,13 +203,98 @@ def build_fe_layout(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, degree: n
     pos3 = np.zeros((n_nodes, 3))
     pos3[:, : pos.shape[1]] = pos
     edge_x = np.concatenate([pos3[src], pos3[dst]], axis=1)
-    if max(a_ptr[-1], rowptr[-1], n_rows) >= np.iinfo(np.int32).max:
-        raise ValueError("problem too large for 32-bit CSR indices")
     i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
     return FeLayout(N, k, m, E, int(n_rows), i32(rowptr), i32(col), table_kind,
                     np.ascontiguousarray(table_val), i32(a_ptr), i32(Ix), i32(T), i32(b_ptr),
-                    i32(BI[border]), i32(BE[border]), flux_rows, p_rows, p_nodes, lm_nodes,
-                    lm_row[lm_nodes], edge_x)
+                    i32(BI), i32(BE), flux_rows, p_rows, p_nodes, lm_nodes,
+                    lm_row[lm_nodes], edge_x, n_edges_global=E)
+
+
+def build_fe_rank_layout(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, N: int, k: int,
+                         lp) -> FeLayout:
+    """One rank's (k, 0) layout over the edges, owned multipliers and ghost columns of its
+    P1/DG0 rank layout ``lp`` (``layout.build_local_problem``, several ranks). Its rows are
+    the one-rank layout's rows of those edges and multipliers (``fe_global_rows``): the same
+    terms, the remote flux ends of an owned multiplier row as ghost columns."""
+    m = 0
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    edges = np.asarray(lp.edges, dtype=np.int64)
+    E = edges.size
+    nf, npe = k * N + 1, N
+    per = nf + npe
+    per1 = 2 * N + 1
+    n_lm = int(np.asarray(lp.lm_nodes).size)
+    n_own = E * per + n_lm
+    n_own1 = int(lp.n_own)
+    n_edge1 = E * per1
+    base = np.arange(E, dtype=np.int64) * per
+    flux_rows = base[:, None] + np.arange(nf)[None, :]
+
+    def col_of(c1):  # P1 rank column -> this layout's column
+        c1 = np.asarray(c1, dtype=np.int64)
+        s, j = np.divmod(np.minimum(c1, n_edge1 - 1) if E else c1 * 0, per1)
+        edge_col = s * per + np.where(j == 0, 0, nf - 1)
+        return np.where(c1 >= n_own1, n_own + (c1 - n_own1),
+                        np.where(c1 >= n_edge1, E * per + (c1 - n_edge1), edge_col))
+
+    c = np.arange(N)
+    qrow = base[:, None, None] + (c[:, None] * k + np.arange(k + 1)[None, :])[None]
+    prow = (base[:, None] + nf + c[None, :])[:, :, None]
+    table_kind, table_val, ent, nq, npl = _tables(k, m)
+    cell = np.arange(E, dtype=np.int64)[:, None] * N + c[None, :]
+    rows, cols, idx, ents = _cell_terms(qrow, prow, cell, ent, nq, npl, E, N)
+    # flux end rows -> their multiplier (owned row or ghost column): lp.edge_lm
+    elm = np.asarray(lp.edge_lm, dtype=np.int64).reshape(E, 2)
+    for end, en in ((0, ent["minus"]), (1, ent["plus"])):
+        on = np.flatnonzero(elm[:, end] >= 0)
+        rows.append(flux_rows[on, 0 if end == 0 else -1])
+        cols.append(col_of(elm[on, end]))
+        idx.append(np.zeros(on.size, dtype=np.int64))
+        ents.append(np.full(on.size, en))
+    # owned multiplier rows -> every incident flux end (local or ghost): lp's rows
+    lrp = np.asarray(lp.lm_rowptr, dtype=np.int64)
+    lcol = np.asarray(lp.lm_col, dtype=np.int64)
+    lval = np.asarray(lp.lm_val, dtype=np.float64)
+    lrow = np.repeat(np.arange(n_lm), np.diff(lrp))
+    rows.append(E * per + lrow)
+    cols.append(col_of(lcol))
+    idx.append(np.zeros(lcol.size, dtype=np.int64))
+    ents.append(np.where(lval > 0, ent["plus"], ent["minus"]))
+    e_ids = np.arange(E, dtype=np.int64)
+    br = [prow[:, :, 0], flux_rows[:, 0], flux_rows[:, -1]]
+    bi = [cell, 2 * e_ids, 2 * e_ids + 1]
+    be = [np.full((E, N), ent["src"][0]), np.full(E, ent["bc"]), np.full(E, ent["bc"])]
+    rowptr, col, a_ptr, Ix, T, b_ptr, BI, BE = _csr_and_rhs(rows, cols, idx, ents, br, bi, be,
+                                                            n_own)
+    n_nodes = pos.shape[0]
+    pos3 = np.zeros((n_nodes, 3))
+    pos3[:, : pos.shape[1]] = pos
+    edge_x = np.concatenate([pos3[src[edges]], pos3[dst[edges]]], axis=1)
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+    lay = FeLayout(N, k, m, E, int(n_own), i32(rowptr), i32(col), table_kind,
+                   np.ascontiguousarray(table_val), i32(a_ptr), i32(Ix), i32(T), i32(b_ptr),
+                   i32(BI), i32(BE), flux_rows, (base[:, None] + nf + c[None, :]).ravel(),
+                   np.zeros(0, dtype=np.int64), np.asarray(lp.lm_nodes, dtype=np.int64),
+                   E * per + np.arange(n_lm, dtype=np.int64), edge_x)
+    lay.n_ghost = int(lp.n_ghost)
+    lay.edges = edges
+    lay.n_edges_global = int(src.size)
+    lay.peers = i32(lp.peers)
+    lay.send_off = i32(lp.send_off)
+    lay.send_idx = i32(col_of(np.asarray(lp.send_idx, dtype=np.int64)))
+    lay.recv_off = i32(lp.recv_off)
+    return lay
+
+
+def fe_global_rows(lay: FeLayout, degree: np.ndarray) -> np.ndarray:
+    """The one-rank layout row (``build_fe_layout`` of the whole graph) of every owned row of
+    a rank layout: edge rows by global edge, multipliers by bifurcation rank (DG0)."""
+    per = lay.k * lay.N + 1 + lay.N
+    edges = np.arange(lay.E) if lay.edges is None else np.asarray(lay.edges, dtype=np.int64)
+    bif = np.flatnonzero(np.asarray(degree) > 1)
+    lam = lay.n_edges_global * per + np.searchsorted(bif, np.asarray(lay.lm_nodes, np.int64))
+    return np.concatenate([(edges[:, None] * per + np.arange(per)[None, :]).ravel(), lam])
 
 
 def evaluate_terms(lay: FeLayout, R_edge: np.ndarray, f, edge_bc: np.ndarray,
@@ -225,16 +346,25 @@ class FeAuxMaps:
     l_aux: np.ndarray
 
 
+def fe_aux_slots(lay: FeLayout, lp) -> np.ndarray:
+    """The auxiliary P1 handle's slot of every edge of the layout (its local order)."""
+    ge = np.arange(lay.E) if lay.edges is None else np.asarray(lay.edges, dtype=np.int64)
+    full = np.full(max(lay.n_edges_global, lay.E), -1, dtype=np.int64)
+    full[np.asarray(lp.edges, dtype=np.int64)] = np.arange(np.asarray(lp.edges).size)
+    slot = full[ge]
+    if (slot < 0).any() or np.asarray(lp.edges).size != lay.E:
+        raise ValueError("the auxiliary problem must hold the layout's edges")
+    return slot
+
+
 def build_fe_aux_maps(lay: FeLayout, lp) -> FeAuxMaps:
-    """Row maps between a (k, 0) layout and the one-rank P1 local problem ``lp`` of the same
-    graph (its edge slots ``lp.edges`` in its own order; multipliers by ascending node)."""
+    """Row maps between a (k, 0) layout and the P1 local problem ``lp`` of the same edges
+    (one rank: the whole graph; several: the rank's P1 layout that ``build_fe_rank_layout``
+    followed) -- its edge slots ``lp.edges`` in its own order, multipliers by ascending node."""
     if lay.m != 0:
         raise ValueError("the condensed direct solve is DG0's (pressure_degree 0)")
     E, N, k = lay.E, lay.N, lay.k
-    slot = np.full(E, -1, dtype=np.int64)
-    slot[np.asarray(lp.edges, dtype=np.int64)] = np.arange(np.asarray(lp.edges).size)
-    if (slot < 0).any():
-        raise ValueError("the auxiliary problem must hold every edge (one rank)")
+    slot = fe_aux_slots(lay, lp)
     per1 = 2 * N + 1
     g = np.arange(N + 1)
     v_fe = lay.flux_rows[:, k * g].ravel()

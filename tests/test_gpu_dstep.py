@@ -239,3 +239,44 @@ def test_dstep_several_chain_passes_fresh_handle():
     it2, rr2, conv2 = h.solve(1e-10, 200, 4)
     assert conv2 and np.linalg.norm(h.solution() - xa) / np.linalg.norm(xa) <= 1e-8
     asm.close()
+
+
+def _edge_case_graphs():
+    import networkx as nx
+
+    one = nx.DiGraph()
+    one.add_node(0, pos=np.array([0.0, 0.0, 0.0]))
+    one.add_node(1, pos=np.array([0.3, 1.1, 0.0]))
+    one.add_edge(0, 1)
+    two = nx.DiGraph()  # a forest of two components, one of them a Y
+    for i, p in enumerate([[0, 0, 0], [0, 1, 0], [2, 0, 0], [2, 1, 0], [1.5, 2, 0], [2.5, 2, 0]]):
+        two.add_node(i, pos=np.array(p, dtype=float))
+    two.add_edges_from([(0, 1), (2, 3), (3, 4), (3, 5)])
+    return {"one_edge": one, "forest2": two}
+
+
+@pytest.mark.parametrize("name", ["one_edge", "forest2"])
+@pytest.mark.parametrize("N", [1, 7])
+@pytest.mark.parametrize("direct", [True, False])
+def test_small_graph_edge_cases(name, N, direct):
+    """Edge cases of the job decomposition: a single edge (one job, no junction, no top
+    part) and a forest of two components, N = 1 and 7, through the fused direct step and
+    MINRES: the oracle's direct solve to 1e-10, the CSR bit-exact."""
+    G = _edge_case_graphs()[name]
+    mesh = NetworkMesh(G, N=N)
+    asm = HydraulicNetworkAssembler(mesh)
+    pbc = lambda x: x[1]  # noqa: E731
+    asm.compute_forms(p_bc_ex=pbc)
+    asm.set_direct(direct)
+    h = asm.handle
+    asm.assemble()
+    it, rr, conv = h.solve(1e-12, 1000, 4)
+    assert conv
+    src, dst = mesh.edges
+    P = O.build_problem(mesh.node_coordinates, src, dst, N, mesh.edge_colors)
+    A, b = O.assemble_reference(P, pbc)
+    Ab, bb, perm, _ = O.to_build_layout(P, A, b)
+    np.testing.assert_array_equal(h.csr()[2], Ab.data)
+    x_ref = O.solve_reference(A, b)[perm]
+    assert np.linalg.norm(h.solution() - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    asm.close()

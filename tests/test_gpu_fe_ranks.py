@@ -1,0 +1,116 @@
+"""General degrees (k, 0) on several ranks, one process per rank (several processes on one
+GPU through the host transport, as in test_gpu_xr_procs.py; the RCCL ranks' host logic).
+
+Checked: every rank takes the condensed direct solve (the ranks' direct tree solve of the
+auxiliary P1/DG0 system) and converges in one pass; the gathered solution equals the
+oracle's one-rank direct solve of the (k, 0) system (``oracle/nx_oracle_fe.py``) to 1e-10;
+every rank publishes the same residual bits; plain MINRES across the ranks reaches the same
+solution (1e-8, its rtol 1e-12 on a condition number ~1e4)."""
+
+from __future__ import annotations
+
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from cases import CASES
+from networks_fenicsx_amd import NetworkMesh
+from networks_fenicsx_amd.layout_fe import build_fe_layout
+from oracle import nx_oracle as O
+from oracle import nx_oracle_fe as OF
+
+pytestmark = pytest.mark.gpu
+
+HERE = Path(__file__).resolve().parent
+SOL_TOL = 1e-10
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def _run(tmp_path, case, P, k, steps=3, minres=0, timeout=240):
+    port = _free_port()
+    procs = []
+    for r in range(P):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NXHIP_TRANSPORT="host")
+        cmd = [sys.executable, "-u", str(HERE / "fe_procs_worker.py"), "--case", case,
+               "--k", str(k), "--steps", str(steps), "--minres", str(minres),
+               "--out", str(tmp_path)]
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, start_new_session=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{out[-4000:]}"
+    ranks = [json.loads((tmp_path / f"rank{r}.json").read_text())["steps"] for r in range(P)]
+    data = [np.load(tmp_path / f"rank{r}.npz") for r in range(P)]
+    return ranks, data
+
+
+def _reference(case, k):
+    """The oracle's one-rank solve, in the one-rank (k, 0) layout's row order."""
+    make, N, strategy, pbc = CASES[case]
+    mesh = NetworkMesh(make(), N=N, color_strategy=strategy)
+    src, dst = mesh.edges
+    E = mesh.num_edges
+    F = OF.build_problem_fe(mesh.node_coordinates, src, dst, N, k, 0, mesh.edge_colors)
+    A, b = OF.assemble_reference_fe(F, pbc, f=0.3, R=1.0 + 0.5 * (np.arange(E) % 3))
+    x_ref = O.solve_reference(A, b)
+    lay = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, N, k, 0)
+    colors = mesh.edge_colors
+    blocks = [lay.flux_rows[np.flatnonzero(colors == c)].ravel()
+              for c in range(mesh.num_edge_colors)] + [lay.p_rows, lay.lm_rows]
+    x = np.empty(lay.n_rows)
+    x[np.concatenate(blocks)] = x_ref
+    return x
+
+
+def _gather(data, j, n):
+    x = np.full(n, np.nan)
+    for d in data:
+        x[d["rows"]] = d["x"][j]
+    assert not np.isnan(x).any(), "every row owned by some rank"
+    return x
+
+
+@pytest.mark.parametrize("case,P,k", [("depth6_N40", 2, 2), ("depth6_N40", 3, 3),
+                                      ("arterial5_N40", 2, 2), ("double_Y_N5", 2, 3)])
+def test_fe_ranks_direct(tmp_path, case, P, k):
+    ranks, data = _run(tmp_path, case, P, k)
+    x_ref = _reference(case, k)
+    for s in range(len(ranks[0])):
+        for r in range(P):
+            st = ranks[r][s]
+            assert st["direct_available"] and st["solver"] == "direct", (r, st)
+            assert st["path"] == "condensed" and st["converged"] and st["iterations"] == 1, (r, st)
+            assert st["relres"] == ranks[0][s]["relres"]  # one all-reduce: the same bits
+        x = _gather(data, s, x_ref.size)
+        assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL, s
+
+
+def test_fe_ranks_minres(tmp_path):
+    ranks, data = _run(tmp_path, "double_Y_N5", 2, 2, steps=1, minres=1)
+    x_ref = _reference("double_Y_N5", 2)
+    for r in range(2):
+        assert ranks[r][-1]["solver"] == "minres" and ranks[r][-1]["converged"]
+    x = _gather(data, 1, x_ref.size)
+    assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= 1e-8
