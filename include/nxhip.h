@@ -92,9 +92,11 @@ int nx_create(int32_t device, int32_t N, int64_t n_edges, const double* edge_x,
  *   h_c is the cell length from edge_x, computed like the reference mesh generator.
  *
  *   n_rows, rowptr (n_rows+1), col   the symmetric system's CSR pattern (sorted rows)
- *   n_ghost                          several ranks, (k, 0): columns n_rows.. are ghosts
- *                                    (layout_fe.build_fe_rank_layout; nx_comm_init then
- *                                    gives the halo plan, as for nx_create); 0 on one rank
+ *   n_ghost                          several ranks: columns n_rows.. are ghosts
+ *                                    (layout_fe.build_fe_rank_layout / build_fe_partition;
+ *                                    nx_comm_init then gives the halo plan, as for
+ *                                    nx_create); 0 on one rank. n_edges may then count
+ *                                    ghost edges too (coefficients, no rows)
  *   n_table, table_kind, table_val   the term table (reference element tensors, signs)
  *   a_ptr (nnz+1), a_idx, a_ent      the terms of every nonzero
  *   b_ptr (n_rows+1), b_idx, b_ent   the terms of every rhs row

@@ -36,10 +36,10 @@ from . import _lib
 from .comm import MIN, GroupRankComm
 from .fem import Constant, Function, FunctionSpace
 from .element import condensed_flux_mass, stable_pair
-from .layout import (LocalProblem, build_local_problem, cycle_pairs_global,
+from .layout import (LocalProblem, build_local_problem, cycle_pairs_global, partition_edges,
                      team_cycle_tables)
 from .layout_fe import (FeLayout, build_cp_tables, build_fe_aux_maps, build_fe_layout,
-                        build_fe_rank_layout, fe_aux_slots)
+                        build_fe_partition, build_fe_rank_layout, fe_aux_slots)
 from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
@@ -264,8 +264,8 @@ class HydraulicNetworkAssembler:
         mesh: the :class:`NetworkMesh`
         flux_degree: degree k of the equispaced Lagrange flux on every edge (default 1)
         pressure_degree: 0 for DG0 pressure (default), m >= 1 for continuous P_m (needs
-            k > m); other pairs than (1, 0) run without the tree preconditioner, (k, 0) on
-            one or several ranks, continuous pressure on one
+            k > m); other pairs than (1, 0) run without the tree preconditioner, on one or
+            several ranks (several: (k, 0) solves directly, continuous pressure by MINRES)
     """
 
     @timed("nxfx:HydraulicNetworkAssembler:__init__")
@@ -301,8 +301,11 @@ class HydraulicNetworkAssembler:
     def _init_general_degrees(self) -> None:
         """Flux P_k / pressure DG0 or continuous P_m (``layout_fe.py``): gather assembly
         (``nx_create_fe``), the condensed direct solves, plain MINRES otherwise -- the tree
-        preconditioner is P1/DG0's. Several ranks: (k, 0), one process per rank, each rank
-        the edges of its P1/DG0 rank layout (``layout_fe.build_fe_rank_layout``)."""
+        preconditioner is P1/DG0's. Several ranks, one process per rank: (k, 0) on the edges
+        of the P1/DG0 rank layout (``layout_fe.build_fe_rank_layout``) with the condensed
+        direct solve across the ranks; continuous pressure by row ownership
+        (``layout_fe.build_fe_partition``: a node's shared pressure row with one rank, the
+        remote edges at the node as ghost edges) with plain MINRES over the halo."""
         mesh = self._network_mesh
         k, m = self._degrees
         if not stable_pair(k, m):
@@ -310,21 +313,25 @@ class HydraulicNetworkAssembler:
                 f"flux_degree={k}, pressure_degree={m}: with continuous pressure the flux degree "
                 "must exceed the pressure degree (otherwise the system is singular)")
         ranks = self._nranks > 1
-        if ranks and m != 0:
-            raise NotImplementedError("continuous pressure (pressure_degree >= 1) runs on one "
-                                      "rank; several ranks run (k, 0)")
         if ranks and isinstance(mesh.comm, GroupRankComm):
             raise NotImplementedError("general degrees on several ranks run one process per "
                                       "rank (RCCL), not an in-process group")
         src, dst = mesh.edges
         self._local = None
         self._fe_lp = None
-        if ranks:
+        n_rows_edges = None  # edges whose rows this rank owns (the rest: ghost edges)
+        if ranks and m == 0:
             self._fe_lp = build_local_problem(mesh.node_coordinates, src, dst, mesh.degrees,
                                               mesh.N, self._rank, self._nranks)
             self._fe = build_fe_rank_layout(mesh.node_coordinates, src, dst, mesh.N, k,
                                             self._fe_lp)
             self._edge_ids = np.asarray(self._fe_lp.edges)
+        elif ranks:
+            full = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, k, m)
+            owner = partition_edges(src, dst, mesh.node_coordinates.shape[0], self._nranks)
+            self._fe = build_fe_partition(full, src, dst, owner, self._rank, self._nranks)
+            self._edge_ids = np.asarray(self._fe.edges)  # coefficients: own + ghost edges
+            n_rows_edges = self._fe.n_own_edges
         else:
             self._fe = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, k, m)
             self._edge_ids = np.arange(mesh.num_edges)
@@ -333,20 +340,21 @@ class HydraulicNetworkAssembler:
         if ranks:
             self._join_comm(self._handle, fe.peers, fe.send_off, fe.send_idx, fe.recv_off)
         self._pc_on = False
-        colors = mesh.edge_colors[self._edge_ids]
+        own_ids = self._edge_ids[:n_rows_edges]
+        colors = mesh.edge_colors[own_ids]
         self._flux_spaces, self._flux_idx = [], []
         for c in range(mesh.num_edge_colors):
             slots = np.flatnonzero(colors == c)  # graph.edges() order inside a colour
-            edges = self._edge_ids[slots]
+            edges = own_ids[slots]
             self._flux_spaces.append(
                 FunctionSpace(mesh, "flux", "P", k, False, edges.size * (k * mesh.N + 1), edges, c))
             self._flux_idx.append(fe.flux_rows[slots].ravel())
         if m == 0:
             self._pressure_space = FunctionSpace(mesh, "pressure", "DG", 0, True,
-                                                 fe.p_rows.size, self._edge_ids)
+                                                 fe.p_rows.size, own_ids)
         else:
             self._pressure_space = FunctionSpace(mesh, "pressure", "P", m, False,
-                                                 fe.p_rows.size, self._edge_ids)
+                                                 fe.p_rows.size, own_ids)
         self._lm_space = FunctionSpace(mesh, "multiplier", "DG", 0, True, fe.lm_nodes.size)
         self._p_idx = fe.p_rows
         self._lm_idx = fe.lm_rows
@@ -355,9 +363,9 @@ class HydraulicNetworkAssembler:
         self._fe_cp = None
         if m == 0 and mesh.N <= 1024 and np.any(np.asarray(mesh.degrees) > 1):
             self._init_fe_direct(src, dst)
-        elif m >= 1:
+        elif m >= 1 and not ranks:
             # continuous pressure on a forest: the direct solve by condensation onto the graph
-            # nodes (nx_fe_set_cp); a graph with cycles runs MINRES
+            # nodes (nx_fe_set_cp); a graph with cycles (or several ranks) runs MINRES
             tab = build_cp_tables(fe, src, dst)
             if tab is not None:
                 self._handle.fe_set_cp(tab)

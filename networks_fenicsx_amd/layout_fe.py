@@ -37,8 +37,8 @@ import numpy as np
 
 from .element import element_tensors, stable_pair
 
-__all__ = ["FeLayout", "build_fe_layout", "build_fe_rank_layout", "fe_global_rows", "KIND_CONST",
-           "KIND_MASS", "KIND_SOURCE", "KIND_BC"]
+__all__ = ["FeLayout", "build_fe_layout", "build_fe_rank_layout", "build_fe_partition",
+           "fe_global_rows", "fe_row_owner", "KIND_CONST", "KIND_MASS", "KIND_SOURCE", "KIND_BC"]
 
 KIND_CONST, KIND_MASS, KIND_SOURCE, KIND_BC = 0, 1, 2, 3
 
@@ -75,6 +75,9 @@ class FeLayout:
     send_off: np.ndarray | None = None
     send_idx: np.ndarray | None = None
     recv_off: np.ndarray | None = None
+    n_own_edges: int = -1  # build_fe_partition: edges [0, n_own_edges) own rows, the rest
+    global_rows: np.ndarray | None = None  # are ghost edges (coefficients only)
+    ghost_rows: np.ndarray | None = None
 
     @property
     def nnz(self) -> int:
@@ -287,9 +290,158 @@ def build_fe_rank_layout(pos: np.ndarray, src: np.ndarray, dst: np.ndarray, N: i
     return lay
 
 
+def fe_row_owner(lay: FeLayout, src: np.ndarray, dst: np.ndarray, edge_owner: np.ndarray,
+                 n_nodes: int) -> np.ndarray:
+    """Owning rank of every row of a one-rank layout: an edge's rows go with the edge, a
+    node's shared pressure row and a bifurcation's multiplier row with the node's first
+    in-edge, else its first out-edge (``layout.build_local_problem``'s rule)."""
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    E = src.size
+    per = lay.k * lay.N + 1 + (lay.N if lay.m == 0 else lay.m * lay.N - 1)
+    first_in = np.full(n_nodes, E, dtype=np.int64)
+    np.minimum.at(first_in, dst, np.arange(E))
+    first_out = np.full(n_nodes, E, dtype=np.int64)
+    np.minimum.at(first_out, src, np.arange(E))
+    anchor = np.where(first_in < E, first_in, first_out)
+    own = np.empty(lay.n_rows, dtype=np.int32)
+    own[: E * per] = np.repeat(np.asarray(edge_owner, dtype=np.int32), per)
+    pn = np.asarray(lay.p_nodes, dtype=np.int64)
+    own[E * per: E * per + pn.size] = edge_owner[anchor[pn]]
+    own[np.asarray(lay.lm_rows, dtype=np.int64)] = edge_owner[anchor[np.asarray(lay.lm_nodes)]]
+    return own
+
+
+def build_fe_partition(full: FeLayout, src: np.ndarray, dst: np.ndarray,
+                       edge_owner: np.ndarray, rank: int, nranks: int) -> FeLayout:
+    """One rank's part of a one-rank layout ``full`` by row ownership (``fe_row_owner``),
+    for any pair -- continuous pressure's shared node rows included. The rank's rows are
+    its owned rows in the one-rank order (its edges' rows, its node pressure rows, its
+    multipliers); every other column it reads is a ghost, ordered by owner, then by the
+    owner's local index, so the owner's send list and the ghost slots line up. Its edges
+    are its own (ascending) then the ghost edges whose cells its rows' terms read (a shared
+    node row sums the element terms of every edge at the node): coefficients and cell
+    lengths cover both, rows only the owned."""
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    E, N = src.size, full.N
+    per = full.k * N + 1 + (N if full.m == 0 else full.m * N - 1)
+    owner_e = np.asarray(edge_owner, dtype=np.int32)
+    n_nodes = int(max(src.max(), dst.max())) + 1 if E else 0
+    n_nodes = max(n_nodes, int(np.max(full.p_nodes, initial=-1)) + 1,
+                  int(np.max(full.lm_nodes, initial=-1)) + 1)
+    row_own = fe_row_owner(full, src, dst, owner_e, n_nodes)
+    rows_of = [np.flatnonzero(row_own == q) for q in range(nranks)]
+    loc = np.empty(full.n_rows, dtype=np.int64)  # local index on the owning rank
+    for q in range(nranks):
+        loc[rows_of[q]] = np.arange(rows_of[q].size)
+    mine = rows_of[rank]
+    n_own = mine.size
+    rp = np.asarray(full.rowptr, dtype=np.int64)
+    starts, ends = rp[mine], rp[mine + 1]
+    cnt = ends - starts
+    ent_idx = (np.repeat(starts - np.cumsum(np.concatenate([[0], cnt[:-1]])), cnt)
+               + np.arange(int(cnt.sum())))  # the owned rows' entries, in order
+    gcol = np.asarray(full.col, dtype=np.int64)[ent_idx]
+
+    def ghosts_of(q):
+        rq = rows_of[q]
+        s_, e_ = rp[rq], rp[rq + 1]
+        c_ = e_ - s_
+        ix = np.repeat(s_ - np.cumsum(np.concatenate([[0], c_[:-1]])), c_) + np.arange(int(c_.sum()))
+        cq = np.unique(np.asarray(full.col, dtype=np.int64)[ix])
+        cq = cq[row_own[cq] != q]
+        return cq[np.lexsort((loc[cq], row_own[cq]))]
+
+    gh = ghosts_of(rank)
+    col_local = np.empty(full.n_rows, dtype=np.int64)
+    col_local[mine] = np.arange(n_own)
+    col_local[gh] = n_own + np.arange(gh.size)
+    col = col_local[gcol]
+    o = np.lexsort((col, np.repeat(np.arange(n_own), cnt)))  # rows keep sorted local columns
+    ent_idx, col = ent_idx[o], col[o]
+    # terms of the owned entries and rhs rows; the cells / edges they read
+    kind = np.asarray(full.table_kind)
+    ap = np.asarray(full.a_ptr, dtype=np.int64)
+    t0, t1 = ap[ent_idx], ap[ent_idx + 1]
+    tcnt = t1 - t0
+    tix = np.repeat(t0 - np.cumsum(np.concatenate([[0], tcnt[:-1]])), tcnt) + np.arange(int(tcnt.sum()))
+    a_idx = np.asarray(full.a_idx, dtype=np.int64)[tix]
+    a_ent = np.asarray(full.a_ent, dtype=np.int64)[tix]
+    bp = np.asarray(full.b_ptr, dtype=np.int64)
+    b0, b1 = bp[mine], bp[mine + 1]
+    bcnt = b1 - b0
+    bix = np.repeat(b0 - np.cumsum(np.concatenate([[0], bcnt[:-1]])), bcnt) + np.arange(int(bcnt.sum()))
+    b_idx = np.asarray(full.b_idx, dtype=np.int64)[bix]
+    b_ent = np.asarray(full.b_ent, dtype=np.int64)[bix]
+    # a term's idx is a cell for the mass / source kinds and for the divergence entries (the
+    # constants before the junctions' +-1, kept as their cell: _cell_terms), else 0 / 2e+end
+    ent_junction = (full.k + 1) ** 2 + (1 if full.m == 0 else full.m + 1) * (full.k + 1)
+    a_cell = np.isin(kind[a_ent], [KIND_MASS, KIND_SOURCE]) | (
+        (kind[a_ent] == KIND_CONST) & (a_ent < ent_junction))
+    b_cell = np.isin(kind[b_ent], [KIND_MASS, KIND_SOURCE])
+    b_bc = kind[b_ent] == KIND_BC
+    own_e = np.flatnonzero(owner_e == rank)
+    read_e = np.unique(np.concatenate([a_idx[a_cell] // N, b_idx[b_cell] // N, b_idx[b_bc] // 2]))
+    ghost_e = np.setdiff1d(read_e, own_e)
+    edges = np.concatenate([own_e, ghost_e])
+    e_loc = np.full(E, -1, dtype=np.int64)
+    e_loc[edges] = np.arange(edges.size)
+    a_idx[a_cell] = e_loc[a_idx[a_cell] // N] * N + a_idx[a_cell] % N
+    b_new = b_idx.copy()
+    b_new[b_cell] = e_loc[b_idx[b_cell] // N] * N + b_idx[b_cell] % N
+    b_new[b_bc] = 2 * e_loc[b_idx[b_bc] // 2] + b_idx[b_bc] % 2
+    b_idx = b_new
+    rowptr = np.concatenate([[0], np.cumsum(cnt)])
+    a_ptr = np.concatenate([[0], np.cumsum(tcnt)])
+    b_ptr = np.concatenate([[0], np.cumsum(bcnt)])
+    # the function rows: owned edges' flux rows, pressure in the function's order, multipliers
+    flux_rows = col_local[np.asarray(full.flux_rows)[own_e]]
+    p_sel = np.asarray(full.p_rows, dtype=np.int64)
+    p_rows = col_local[p_sel[row_own[p_sel] == rank]]
+    pn = np.asarray(full.p_nodes, dtype=np.int64)
+    pn_rows = E * per + np.arange(pn.size)
+    lmr = np.asarray(full.lm_rows, dtype=np.int64)
+    lm_mine = row_own[lmr] == rank
+    # halo plan: what each peer reads of mine, in its ghost order
+    peers, send_off, send_idx, recv_off = [], [0], [], [0]
+    g_owner = row_own[gh]
+    for q in range(nranks):
+        if q == rank:
+            continue
+        theirs = ghosts_of(q)
+        snd = loc[theirs[row_own[theirs] == rank]]
+        rcv = int(np.count_nonzero(g_owner == q))
+        if snd.size == 0 and rcv == 0:
+            continue
+        peers.append(q)
+        send_idx.extend(snd.tolist())
+        send_off.append(len(send_idx))
+        recv_off.append(recv_off[-1] + rcv)
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+    lay = FeLayout(N, full.k, full.m, int(edges.size), int(n_own), i32(rowptr), i32(col),
+                   full.table_kind, full.table_val, i32(a_ptr), i32(a_idx), i32(a_ent),
+                   i32(b_ptr), i32(b_idx), i32(b_ent), flux_rows, p_rows,
+                   pn[row_own[pn_rows] == rank], np.asarray(full.lm_nodes)[lm_mine],
+                   col_local[lmr[lm_mine]], np.asarray(full.edge_x)[edges])
+    lay.n_ghost = int(gh.size)
+    lay.edges = edges
+    lay.n_edges_global = E
+    lay.n_own_edges = int(own_e.size)
+    lay.global_rows = mine
+    lay.ghost_rows = gh
+    lay.peers = i32(peers)
+    lay.send_off = i32(send_off)
+    lay.send_idx = i32(send_idx)
+    lay.recv_off = i32(recv_off)
+    return lay
+
+
 def fe_global_rows(lay: FeLayout, degree: np.ndarray) -> np.ndarray:
     """The one-rank layout row (``build_fe_layout`` of the whole graph) of every owned row of
     a rank layout: edge rows by global edge, multipliers by bifurcation rank (DG0)."""
+    if getattr(lay, "global_rows", None) is not None:  # build_fe_partition keeps them
+        return np.asarray(lay.global_rows, dtype=np.int64)
     per = lay.k * lay.N + 1 + lay.N
     edges = np.arange(lay.E) if lay.edges is None else np.asarray(lay.edges, dtype=np.int64)
     bif = np.flatnonzero(np.asarray(degree) > 1)

@@ -1,10 +1,11 @@
-"""One rank of tests/test_gpu_fe_ranks.py: a (k, 0) problem partitioned over processes, several
+"""One rank of tests/test_gpu_fe_ranks.py: a (k, m) problem partitioned over processes, several
 on ONE GPU, through the library's host transport (``NXHIP_TRANSPORT=host``: the RCCL ranks'
 host logic with the collectives through shared memory; host control over gloo).
 
-Each step: assemble + solve (the condensed direct solve: condense per edge, the ranks'
-direct tree solve of the auxiliary P1/DG0 system, expand, the residual over the ranks), a
-gloo barrier; then one plain-MINRES solve (``--minres``). Writes ``rank<r>.json`` and
+Each step: assemble + solve ((k, 0): the condensed direct solve -- condense per edge, the
+ranks' direct tree solve of the auxiliary P1/DG0 system, expand, the residual over the
+ranks; continuous pressure: plain MINRES over the halo), a gloo barrier; then one
+plain-MINRES solve (``--minres``). Writes ``rank<r>.json`` and
 ``rank<r>.npz`` (one-rank layout rows of the owned rows, x per solve) into ``--out``.
 """
 
@@ -25,6 +26,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="depth6_N40")
     ap.add_argument("--k", type=int, default=2)
+    ap.add_argument("--m", type=int, default=0)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--minres", type=int, default=0)
     ap.add_argument("--out", required=True)
@@ -45,7 +47,7 @@ def main() -> int:
     make, N, strategy, pbc = CASES[args.case]
     G = make() if rank == 0 else None
     mesh = NetworkMesh(G, N=N, color_strategy=strategy, comm=TorchComm())
-    asm = HydraulicNetworkAssembler(mesh, flux_degree=args.k, pressure_degree=0)
+    asm = HydraulicNetworkAssembler(mesh, flux_degree=args.k, pressure_degree=args.m)
     E = mesh.num_edges
     asm.compute_forms(p_bc_ex=pbc, f=0.3, R=1.0 + 0.5 * (np.arange(E) % 3))
     asm.set_direct(True)

@@ -100,3 +100,72 @@ def test_rank_layouts_cover_the_layout(case, P, k):
             jq = lq.peers.tolist().index(r)
             recv = gids[q][lq.n_rows + np.arange(lq.recv_off[jq], lq.recv_off[jq + 1])]
             np.testing.assert_array_equal(sent, recv)
+
+
+def _partition(mesh, k, m, P):
+    from networks_fenicsx_amd.layout import partition_edges
+    from networks_fenicsx_amd.layout_fe import build_fe_partition
+
+    src, dst = mesh.edges
+    full = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, k, m)
+    owner = partition_edges(src, dst, mesh.node_coordinates.shape[0], P)
+    return full, [build_fe_partition(full, src, dst, owner, r, P) for r in range(P)]
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "edge_info_N10", "double_Y_N5", "depth6_N40",
+                                  "arterial5_N40"])
+@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("km", [(2, 1), (3, 1), (3, 2), (2, 0)])
+def test_partitions_cover_the_layout(case, P, km):
+    """Any pair, continuous pressure's shared node rows included (``build_fe_partition``):
+    every owned row is the one-rank row (columns, values and rhs bit for bit), the ghost
+    edges give the remote cells' terms, every row is owned once, the halo plans line up."""
+    mesh = _mesh(case)
+    E = mesh.num_edges
+    full, lays = _partition(mesh, *km, P)
+    R = 1.0 + 0.25 * (np.arange(E) % 5)
+    f = 0.1 + 0.05 * (np.arange(E) % 3)
+    fv, fr = _terms(full, mesh, R, f)
+    owned = np.zeros(full.n_rows, dtype=np.int64)
+    gids = []
+    for r, lay in enumerate(lays):
+        rows = fe_global_rows(lay, mesh.degrees)
+        cols = np.concatenate([rows, lay.ghost_rows])
+        owned[rows] += 1
+        v, b = _terms(lay, mesh, R, f)
+        for i in range(lay.n_rows):
+            g = rows[i]
+            s0, s1 = lay.rowptr[i], lay.rowptr[i + 1]
+            t0, t1 = full.rowptr[g], full.rowptr[g + 1]
+            assert (np.diff(lay.col[s0:s1]) > 0).all()  # sorted local columns
+            got = sorted(zip(cols[lay.col[s0:s1]].tolist(), v[s0:s1].tolist()))
+            want = sorted(zip(full.col[t0:t1].tolist(), fv[t0:t1].tolist()))
+            assert got == want, (r, i, g)
+            assert b[i] == fr[g]
+        gids.append(cols)
+    np.testing.assert_array_equal(owned, 1)
+    for r, (lay, cols) in enumerate(zip(lays, gids)):
+        for j, q in enumerate(lay.peers.tolist()):
+            sent = cols[lay.send_idx[lay.send_off[j]:lay.send_off[j + 1]]]
+            lq = lays[q]
+            jq = lq.peers.tolist().index(r)
+            recv = gids[q][lq.n_rows + np.arange(lq.recv_off[jq], lq.recv_off[jq + 1])]
+            np.testing.assert_array_equal(sent, recv)
+
+
+@pytest.mark.parametrize("case", ["edge_info_N10", "depth6_N40"])
+@pytest.mark.parametrize("P", [2, 3])
+def test_partition_is_the_rank_layout_for_dg0(case, P):
+    """(k, 0): the generic partition and the P1-derived rank layout are the same tables (no
+    ghost edges: DG0's multiplier rows read no cells)."""
+    mesh = _mesh(case)
+    src, dst = mesh.edges
+    full, lays = _partition(mesh, 2, 0, P)
+    for r, part in enumerate(lays):
+        lp = build_local_problem(mesh.node_coordinates, src, dst, mesh.degrees, mesh.N, r, P)
+        lay = build_fe_rank_layout(mesh.node_coordinates, src, dst, mesh.N, 2, lp)
+        assert part.n_own_edges == part.E == lay.E and part.n_ghost == lay.n_ghost
+        for name in ("rowptr", "col", "a_ptr", "a_idx", "a_ent", "b_ptr", "b_idx", "b_ent",
+                     "flux_rows", "p_rows", "lm_rows", "edge_x", "peers", "send_off",
+                     "send_idx", "recv_off"):
+            np.testing.assert_array_equal(getattr(part, name), getattr(lay, name), err_msg=name)

@@ -1,11 +1,12 @@
-"""General degrees (k, 0) on several ranks, one process per rank (several processes on one
+"""General degrees on several ranks, one process per rank (several processes on one
 GPU through the host transport, as in test_gpu_xr_procs.py; the RCCL ranks' host logic).
 
 Checked: every rank takes the condensed direct solve (the ranks' direct tree solve of the
 auxiliary P1/DG0 system) and converges in one pass; the gathered solution equals the
 oracle's one-rank direct solve of the (k, 0) system (``oracle/nx_oracle_fe.py``) to 1e-10;
 every rank publishes the same residual bits; plain MINRES across the ranks reaches the same
-solution (1e-8, its rtol 1e-12 on a condition number ~1e4)."""
+solution (1e-8, its rtol 1e-12 on a condition number ~1e4), for (k, 0) and for continuous
+pressure (whose shared node rows are partitioned by ownership)."""
 
 from __future__ import annotations
 
@@ -38,14 +39,14 @@ def _free_port() -> int:
         return int(s.getsockname()[1])
 
 
-def _run(tmp_path, case, P, k, steps=3, minres=0, timeout=240):
+def _run(tmp_path, case, P, k, steps=3, minres=0, timeout=240, m=0):
     port = _free_port()
     procs = []
     for r in range(P):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NXHIP_TRANSPORT="host")
         cmd = [sys.executable, "-u", str(HERE / "fe_procs_worker.py"), "--case", case,
-               "--k", str(k), "--steps", str(steps), "--minres", str(minres),
+               "--k", str(k), "--m", str(m), "--steps", str(steps), "--minres", str(minres),
                "--out", str(tmp_path)]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, start_new_session=True))
@@ -66,16 +67,16 @@ def _run(tmp_path, case, P, k, steps=3, minres=0, timeout=240):
     return ranks, data
 
 
-def _reference(case, k):
-    """The oracle's one-rank solve, in the one-rank (k, 0) layout's row order."""
+def _reference(case, k, m=0):
+    """The oracle's one-rank solve, in the one-rank (k, m) layout's row order."""
     make, N, strategy, pbc = CASES[case]
     mesh = NetworkMesh(make(), N=N, color_strategy=strategy)
     src, dst = mesh.edges
     E = mesh.num_edges
-    F = OF.build_problem_fe(mesh.node_coordinates, src, dst, N, k, 0, mesh.edge_colors)
+    F = OF.build_problem_fe(mesh.node_coordinates, src, dst, N, k, m, mesh.edge_colors)
     A, b = OF.assemble_reference_fe(F, pbc, f=0.3, R=1.0 + 0.5 * (np.arange(E) % 3))
     x_ref = O.solve_reference(A, b)
-    lay = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, N, k, 0)
+    lay = build_fe_layout(mesh.node_coordinates, src, dst, mesh.degrees, N, k, m)
     colors = mesh.edge_colors
     blocks = [lay.flux_rows[np.flatnonzero(colors == c)].ravel()
               for c in range(mesh.num_edge_colors)] + [lay.p_rows, lay.lm_rows]
@@ -113,4 +114,18 @@ def test_fe_ranks_minres(tmp_path):
     for r in range(2):
         assert ranks[r][-1]["solver"] == "minres" and ranks[r][-1]["converged"]
     x = _gather(data, 1, x_ref.size)
+    assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= 1e-8
+
+
+@pytest.mark.parametrize("case,P,km", [("double_Y_N5", 2, (2, 1)), ("edge_info_N10", 3, (3, 2)),
+                                       ("Y_N4", 2, (3, 1))])
+def test_fe_ranks_continuous_pressure(tmp_path, case, P, km):
+    """Continuous pressure over the ranks (``build_fe_partition``: shared node rows owned
+    once, ghost edges for their remote terms): plain MINRES, the one-rank answer."""
+    ranks, data = _run(tmp_path, case, P, km[0], steps=1, m=km[1])
+    x_ref = _reference(case, *km)
+    for r in range(P):
+        assert ranks[r][0]["solver"] == "minres" and ranks[r][0]["converged"], ranks[r][0]
+        assert ranks[r][0]["iterations"] == ranks[0][0]["iterations"]
+    x = _gather(data, 0, x_ref.size)
     assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= 1e-8
