@@ -344,6 +344,19 @@ int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const double
                  const int32_t* child_off, const int32_t* child, const int32_t* nown);
 
 /*
+ * Several ranks, continuous pressure (called before nx_fe_set_cp; layout_fe.
+ * build_cp_rank_tables): this rank runs the edge kernels on its n_own_edges edges (gid: each
+ * one's global edge), every rank's border blocks and the node rows' rhs are summed over the
+ * ranks (one all-reduce per pass), every rank solves the node forest, and each writes the
+ * node rows it owns (nrowx, 2 per node: local rows or -1). nx_fe_set_cp's eb / nown then
+ * list this rank's edges (nown: -1 where another rank writes the node), its nrow the node
+ * rhs slots (2n, 2n + 1 or -1), its incidence and parents global edges. Replaces the
+ * distributed MUMPS LU (solver.py:58-65) for these pairs.
+ */
+int nx_fe_cp_ranks(nx_network_t* h, int64_t n_own_edges, int64_t n_edges_global,
+                   const int32_t* gid, int64_t n_nodes, const int32_t* nrowx);
+
+/*
  * Process-wide solve mode. 1 (default): with the preconditioner a solve is ONE HIP graph
  * launch -- start application, per-solve coefficients and the first iterations (also with
  * several ranks, RCCL or group, when beta^2 travels point-to-point) -- whose last k_mr_a

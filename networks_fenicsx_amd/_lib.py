@@ -101,6 +101,7 @@ _SIGS = {
     "nx_set_cell_mass": (C.c_int, [_h, _f64, _f64]),
     "nx_fe_set_direct": (C.c_int, [_h, _h, _i32, _i64, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32,
                                    _pi32, _pi32, _pd, _f64]),
+    "nx_fe_cp_ranks": (C.c_int, [_h, _i64, _i64, _pi32, _i64, _pi32]),
     "nx_fe_set_cp": (C.c_int, [_h, _i32, _i32, _i32, _pd, _pi32, _i64, _pi32, _pi32, _i32,
                                _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32, _pi32]),
     "nx_get_solver": (C.c_int, [_h, _pi32, _pi32]),
@@ -533,6 +534,16 @@ class Handle:
                                  _ptr(cst, C.c_double), p[0], int(tab.n_nodes), p[1], p[2],
                                  int(tab.lev_off.size - 1), p[3], p[4], p[5], p[6], p[7], p[8],
                                  p[9], p[10]))
+
+    def fe_cp_ranks(self, n_own_edges: int, n_edges_global: int, gid, nrowx) -> None:
+        """``nx_fe_cp_ranks`` (several ranks, before :meth:`fe_set_cp`): this rank's edges'
+        global ids and the local rows of the node rows it owns (2 per node, -1 elsewhere)."""
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        nrowx = np.ascontiguousarray(nrowx, dtype=np.int32).ravel()
+        self._cp_rank_keep = (gid, nrowx)
+        check(lib().nx_fe_cp_ranks(self.ptr, int(n_own_edges), int(n_edges_global),
+                                   _ptr(gid if gid.size else np.zeros(1, np.int32), C.c_int32),
+                                   int(nrowx.size // 2), _ptr(nrowx, C.c_int32)))
 
     def set_pc_exact(self, enable: bool) -> None:
         """Consistent (exact Schur complement, default) or lumped flux mass in P."""

@@ -38,8 +38,8 @@ from .fem import Constant, Function, FunctionSpace
 from .element import condensed_flux_mass, stable_pair
 from .layout import (LocalProblem, build_local_problem, cycle_pairs_global, partition_edges,
                      team_cycle_tables)
-from .layout_fe import (FeLayout, build_cp_tables, build_fe_aux_maps, build_fe_layout,
-                        build_fe_partition, build_fe_rank_layout, fe_aux_slots)
+from .layout_fe import (FeLayout, build_cp_rank_tables, build_cp_tables, build_fe_aux_maps,
+                        build_fe_layout, build_fe_partition, build_fe_rank_layout, fe_aux_slots)
 from .mesh import NetworkMesh
 from .precond import TreePreconditioner, build_tree_preconditioner
 from .timing import timed
@@ -265,7 +265,7 @@ class HydraulicNetworkAssembler:
         flux_degree: degree k of the equispaced Lagrange flux on every edge (default 1)
         pressure_degree: 0 for DG0 pressure (default), m >= 1 for continuous P_m (needs
             k > m); other pairs than (1, 0) run without the tree preconditioner, on one or
-            several ranks (several: (k, 0) solves directly, continuous pressure by MINRES)
+            several ranks, with their direct solves on forests
     """
 
     @timed("nxfx:HydraulicNetworkAssembler:__init__")
@@ -305,7 +305,8 @@ class HydraulicNetworkAssembler:
         of the P1/DG0 rank layout (``layout_fe.build_fe_rank_layout``) with the condensed
         direct solve across the ranks; continuous pressure by row ownership
         (``layout_fe.build_fe_partition``: a node's shared pressure row with one rank, the
-        remote edges at the node as ghost edges) with plain MINRES over the halo."""
+        remote edges at the node as ghost edges) with the node-condensed direct solve across
+        the ranks (``layout_fe.build_cp_rank_tables``); MINRES over the halo otherwise."""
         mesh = self._network_mesh
         k, m = self._degrees
         if not stable_pair(k, m):
@@ -320,6 +321,7 @@ class HydraulicNetworkAssembler:
         self._local = None
         self._fe_lp = None
         n_rows_edges = None  # edges whose rows this rank owns (the rest: ghost edges)
+        full = None
         if ranks and m == 0:
             self._fe_lp = build_local_problem(mesh.node_coordinates, src, dst, mesh.degrees,
                                               mesh.N, self._rank, self._nranks)
@@ -363,10 +365,14 @@ class HydraulicNetworkAssembler:
         self._fe_cp = None
         if m == 0 and mesh.N <= 1024 and np.any(np.asarray(mesh.degrees) > 1):
             self._init_fe_direct(src, dst)
-        elif m >= 1 and not ranks:
+        elif m >= 1:
             # continuous pressure on a forest: the direct solve by condensation onto the graph
-            # nodes (nx_fe_set_cp); a graph with cycles (or several ranks) runs MINRES
-            tab = build_cp_tables(fe, src, dst)
+            # nodes (nx_fe_set_cp; several ranks: every rank's border blocks summed, the node
+            # forest solved on every rank, nx_fe_cp_ranks); a graph with cycles runs MINRES
+            tab = build_cp_tables(full if ranks else fe, src, dst)
+            if tab is not None and ranks:
+                tab, gid, nrowx = build_cp_rank_tables(tab, fe)
+                self._handle.fe_cp_ranks(fe.n_own_edges, mesh.num_edges, gid, nrowx)
             if tab is not None:
                 self._handle.fe_set_cp(tab)
                 self._fe_cp = tab

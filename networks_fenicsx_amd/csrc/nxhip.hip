@@ -6569,6 +6569,13 @@ struct nx_network {
   std::vector<int> cp_lev_host;  // the level offsets on the host (cp_nodes_launch)
   int *cp_order = nullptr, *cp_inc_off = nullptr, *cp_inc = nullptr, *cp_parent = nullptr;
   int *cp_child_off = nullptr, *cp_child = nullptr, *cp_nown = nullptr;
+  // several ranks (nx_fe_cp_ranks): this rank's edges run the edge kernels (cp_Eown), every
+  // rank's Se | ge (cp_Eg edges, by global edge: cp_gid) and node rhs (2 per node, after
+  // them in cp_se) are summed over the ranks, the node forest is solved on every rank, and
+  // each rank writes the node rows it owns (cp_nrowx: local rows, -1 elsewhere)
+  int64_t cp_Eown = 0, cp_Eg = 0;
+  int *cp_gid = nullptr, *cp_nrowx = nullptr;
+  std::vector<int> cp_gid_host, cp_nrowx_host;
 };
 
 struct nx_group {
@@ -6817,10 +6824,11 @@ int team_halo(const Team& t, VecSel sel, int64_t k, bool beta = false, bool pack
 }
 
 // sum-all-reduce of n doubles: red + slot (slot 0..3), the coarse buffer (-1), the cut rows'
-// buffer (-2), the cycle correction's U^T x (-3) or its U^T Z and couplings (-4)
+// buffer (-2), the cycle correction's U^T x (-3) or its U^T Z and couplings (-4), the
+// continuous-pressure border blocks and node rhs (-5)
 double* xbuf_of(nx_network* h, int slot) {
-  return slot == -4 ? h->cyc_cap : slot == -3 ? h->cyc_u : slot == -2 ? h->cutbuf
-         : slot < 0 ? h->pa.cbuf : h->red + slot;
+  return slot == -5 ? h->cp_se : slot == -4 ? h->cyc_cap : slot == -3 ? h->cyc_u
+         : slot == -2 ? h->cutbuf : slot < 0 ? h->pa.cbuf : h->red + slot;
 }
 
 int team_allreduce(const Team& t, int slot, int n) {
@@ -7846,6 +7854,7 @@ struct CpArgs {
   double* fac;        // per edge, per vertex (N + 1): Pi 4 | C 4 | W 8 | rho 2
   double* se;         // per edge: Se 16 | ge 4
   double* xn;         // per border node: its (p, lam) values
+  const int* gid;     // several ranks: the global edge of each local edge (its se slot)
 };
 constexpr int kCpFac = 18;
 
@@ -7976,7 +7985,7 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
     f[16] = rho[0];
     f[17] = rho[1];
   }
-  double* o = a.se + e * 20;
+  double* o = a.se + 20 * (a.gid ? (int64_t)a.gid[e] : e);
   for (int i = 0; i < 16; ++i) o[i] = Sb[i];
   for (int i = 0; i < 4; ++i) o[16 + i] = gb[i];
 }
@@ -8143,6 +8152,16 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
     put(a.nrow[2 * n], a.xn[2 * n]);
     if (a.nrow[2 * n + 1] >= 0) put(a.nrow[2 * n + 1], a.xn[2 * n + 1]);
   }
+}
+
+// Several ranks: the node rows' rhs this rank owns into the summed node rhs (2 per node)
+__global__ __launch_bounds__(256) void k_cp_nb(const int* __restrict__ nrowx, int nn,
+                                               const double* __restrict__ b,
+                                               double* __restrict__ nb) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= 2 * nn) return;
+  const int r = nrowx[i];
+  if (r >= 0) nb[i] = b[r];
 }
 
 // The edge templates (FeTpl) of a layout with `per` rows per edge: each shape's entries and
@@ -8488,7 +8507,8 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->fe_laux, h->fe_cst, h->fe_cellh, h->d_cyc_qloc, h->d_cyc_lcol, h->cyc_u,
                   h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_tI,
                   h->cp_eb, h->cp_nrow, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
-                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown, h->fe_tpl_buf,
+                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown, h->cp_gid,
+                  h->cp_nrowx, h->fe_tpl_buf,
                   h->fe_tpl_rbuf, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -10118,23 +10138,43 @@ void cp_nodes_launch(nx_network* h, const CpArgs& a, const CpTree& tr, const dou
 
 int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int32_t* converged) {
   CHECK(flush_assembly(h));
-  const CpArgs a{(int)h->N, h->cp_k, h->cp_m, h->cp_nI, h->E, h->edge_R, h->fe_cellh, h->cp_cst,
-                 h->cp_tI, h->cp_eb, h->cp_nrow, h->cp_fac, h->cp_se, h->cp_xn};
+  // several ranks: the edge kernels over this rank's edges (se by global edge), the node
+  // kernels over the summed blocks and node rhs (an: nrow indexes nb), the rows it owns
+  const bool ranks = h->cp_Eg > 0;
+  const int64_t Ee = ranks ? h->cp_Eown : h->E;
+  const CpArgs a{(int)h->N, h->cp_k, h->cp_m, h->cp_nI, Ee, h->edge_R, h->fe_cellh, h->cp_cst,
+                 h->cp_tI, h->cp_eb, ranks ? h->cp_nrowx : h->cp_nrow, h->cp_fac, h->cp_se,
+                 h->cp_xn, ranks ? h->cp_gid : nullptr};
+  CpArgs an = a;
+  an.nrow = h->cp_nrow;
+  double* nb = h->cp_se + 20 * h->cp_Eg;
+  const int64_t nsum = 20 * h->cp_Eg + 2 * (int64_t)h->cp_nn;
+  nx_network* hs[1] = {h};
+  const Team t{hs, 1, nullptr};
   const CpTree tr{h->cp_nn, h->cp_nlev, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
                   h->cp_parent, h->cp_child_off, h->cp_child, h->cp_Pinv, h->cp_hv};
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
   // (one thread per edge: 64-thread workgroups spread the edges over every CU)
-  const int eb = grid_of(h->E, 64);
+  const int eb = std::max(1, grid_of(Ee, 64));
   MrState s{};
   int pass = 0;
   h->last_dir_path = 4;  // the node-condensed route (nx_get_direct_path)
   for (; pass < 3; ++pass) {
     const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
+    if (ranks) HIPCALL(hipMemsetAsync(h->cp_se, 0, sizeof(double) * nsum, h->stream));
     hipLaunchKernelGGL(k_cp_edge, dim3(eb), dim3(64), 0, h->stream, a, b);
-    cp_nodes_launch(h, a, tr, b);
+    if (ranks) {
+      hipLaunchKernelGGL(k_cp_nb, dim3(grid_of(2 * (int64_t)h->cp_nn, 256)), dim3(256), 0,
+                         h->stream, h->cp_nrowx, h->cp_nn, b, nb);
+      CHECK(team_allreduce(t, -5, (int)nsum));
+    }
+    cp_nodes_launch(h, ranks ? an : a, tr, ranks ? nb : b);
     hipLaunchKernelGGL(k_cp_back, dim3(eb), dim3(64), 0, h->stream, a, b, h->x, h->cp_nown,
                        pass ? 1 : 0);
-    fe_true_residual(h, rtol, nrb);
+    if (ranks)
+      CHECK(fe_true_residual_team(h, rtol, nrb));
+    else
+      fe_true_residual(h, rtol, nrb);
     HIPCALL(hipGetLastError());
     h->seq += 1;
     CHECK(wait_published(h));
@@ -11435,8 +11475,30 @@ NX_API int nx_set_cell_mass(nx_network_t* h, double ratio, double mo_div) {
   return NX_OK;
 }
 
-// Continuous pressure (k > m >= 1), one rank, a forest: attach the node-condensed direct
-// solve (see include/nxhip.h); k = 0 detaches it.
+// Several ranks, continuous pressure: this rank's part of the node-condensed direct solve,
+// given before nx_fe_set_cp (whose eb / nown then list this rank's n_own_edges edges and whose
+// node tables name global edges). gid: the global edge of each of them; nrowx (2 per node):
+// the local rows of the node rows this rank owns, -1 elsewhere.
+NX_API int nx_fe_cp_ranks(nx_network_t* h, int64_t n_own_edges, int64_t n_edges_global,
+                          const int32_t* gid, int64_t n_nodes, const int32_t* nrowx) {
+  if (!h) return fail(NX_ERR_ARG, "null handle");
+  if (!h->fe) return fail(NX_ERR_STATE, "a general-degree handle (nx_create_fe)");
+  if (n_own_edges < 0 || n_own_edges > h->E || n_edges_global < n_own_edges || n_nodes < 1 ||
+      (n_own_edges > 0 && !gid) || !nrowx)
+    return fail(NX_ERR_ARG, "bad rank tables");
+  for (int64_t e = 0; e < n_own_edges; ++e)
+    if (gid[e] < 0 || gid[e] >= n_edges_global) return fail(NX_ERR_ARG, "gid out of range");
+  for (int64_t i = 0; i < 2 * n_nodes; ++i)
+    if (nrowx[i] < -1 || nrowx[i] >= h->n_own) return fail(NX_ERR_ARG, "nrowx out of range");
+  h->cp_Eown = n_own_edges;
+  h->cp_Eg = n_edges_global;
+  h->cp_gid_host.assign(gid ? gid : nullptr, gid ? gid + n_own_edges : nullptr);
+  h->cp_nrowx_host.assign(nrowx, nrowx + 2 * n_nodes);
+  return NX_OK;
+}
+
+// Continuous pressure (k > m >= 1), a forest: attach the node-condensed direct solve (see
+// include/nxhip.h); k = 0 detaches it.
 NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const double* cst,
                         const int32_t* tI, int64_t n_nodes, const int32_t* nrow, const int32_t* eb,
                         int32_t n_lev, const int32_t* lev_off, const int32_t* order,
@@ -11445,8 +11507,10 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   CHECK(flush_assembly(h));
   if (!h) return fail(NX_ERR_ARG, "null handle");
   if (!h->fe) return fail(NX_ERR_STATE, "a general-degree handle (nx_create_fe)");
-  if (k != 0 && (h->nranks > 1 || h->n_ghost > 0))
-    return fail(NX_ERR_STATE, "continuous pressure runs on one rank");
+  // several ranks: nx_fe_cp_ranks first (this rank's edges and the global edge count)
+  const bool ranks = !h->cp_gid_host.empty() || h->cp_Eg > 0;
+  if (k != 0 && (h->nranks > 1 || h->n_ghost > 0) && !ranks)
+    return fail(NX_ERR_STATE, "several ranks: nx_fe_cp_ranks before nx_fe_set_cp");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
   for (double** p : {&h->cp_cst, &h->cp_fac, &h->cp_se, &h->cp_xn, &h->cp_Pinv, &h->cp_hv}) {
@@ -11454,23 +11518,35 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
     *p = nullptr;
   }
   for (int** p : {&h->cp_tI, &h->cp_eb, &h->cp_nrow, &h->cp_lev_off, &h->cp_order, &h->cp_inc_off,
-                  &h->cp_inc, &h->cp_parent, &h->cp_child_off, &h->cp_child, &h->cp_nown}) {
+                  &h->cp_inc, &h->cp_parent, &h->cp_child_off, &h->cp_child, &h->cp_nown,
+                  &h->cp_gid, &h->cp_nrowx}) {
     if (*p) HIPCALL(hipFree(*p));
     *p = nullptr;
   }
   h->fe_cp = false;
-  if (k == 0) return NX_OK;
-  const int64_t n = n_nodes, E = h->E;
+  if (k == 0) {
+    h->cp_Eown = h->cp_Eg = 0;
+    h->cp_gid_host.clear();
+    h->cp_nrowx_host.clear();
+    return NX_OK;
+  }
+  // E: the edges the edge kernels run (eb rows, nown); Es: the edges the node tables name
+  const int64_t n = n_nodes, E = ranks ? h->cp_Eown : h->E, Es = ranks ? h->cp_Eg : h->E;
   if (!(m >= 1 && k > m) || nI != (k - 1) + (m - 1) || n < 1 || n_lev < 1 || !cst || !nrow ||
       !eb || !lev_off || !order || !inc_off || !inc || !parent || !child_off || !nown ||
       (nI > 0 && !tI))
     return fail(NX_ERR_ARG, "bad continuous-pressure tables");
-  if (h->n_own < E * (int64_t)(k * h->N + 1 + m * h->N - 1) + n)
+  if (!ranks && h->n_own < E * (int64_t)(k * h->N + 1 + m * h->N - 1) + n)
     return fail(NX_ERR_ARG, "row counts do not match a (k, m) layout");
+  if (ranks && (h->n_own < E * (int64_t)(k * h->N + 1 + m * h->N - 1) ||
+                (int64_t)h->cp_nrowx_host.size() != 2 * n))
+    return fail(NX_ERR_ARG, "several ranks: rows / node rows do not match the tables");
+  // one rank: nrow are rows; several: indices of the summed node rhs (2 per node)
+  const int64_t nlim = ranks ? 2 * n : h->n_own;
   for (int64_t i = 0; i < n; ++i)
-    if (nrow[2 * i] < 0 || nrow[2 * i] >= h->n_own || nrow[2 * i + 1] < -1 || nrow[2 * i + 1] >= h->n_own ||
-        parent[3 * i] < -1 || parent[3 * i] >= n || parent[3 * i + 1] < -1 || parent[3 * i + 1] >= E ||
-        nown[i] < 0 || nown[i] >= E)
+    if (nrow[2 * i] < 0 || nrow[2 * i] >= nlim || nrow[2 * i + 1] < -1 || nrow[2 * i + 1] >= nlim ||
+        parent[3 * i] < -1 || parent[3 * i] >= n || parent[3 * i + 1] < -1 || parent[3 * i + 1] >= Es ||
+        nown[i] < (ranks ? -1 : 0) || nown[i] >= E)
       return fail(NX_ERR_ARG, "continuous pressure: node tables out of range");
   for (int64_t e = 0; e < E; ++e)
     if (eb[4 * e] < 0 || eb[4 * e] >= n || eb[4 * e + 1] < 0 || eb[4 * e + 1] >= n ||
@@ -11481,7 +11557,7 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   for (int64_t i = 0; i < n; ++i)
     if (order[i] < 0 || order[i] >= n) return fail(NX_ERR_ARG, "continuous pressure: order");
   for (int64_t j = 0; j < inc_off[n]; ++j)
-    if (inc[2 * j] < 0 || inc[2 * j] >= E || inc[2 * j + 1] < 0 || inc[2 * j + 1] > 1)
+    if (inc[2 * j] < 0 || inc[2 * j] >= Es || inc[2 * j + 1] < 0 || inc[2 * j + 1] > 1)
       return fail(NX_ERR_ARG, "continuous pressure: incidence");
   for (int64_t j = 0; j < child_off[n]; ++j)
     if (child[j] < 0 || child[j] >= n) return fail(NX_ERR_ARG, "continuous pressure: children");
@@ -11498,8 +11574,13 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   CHECK(upload(&h->cp_child_off, child_off, n + 1, h->stream));
   if (child_off[n] > 0) CHECK(upload(&h->cp_child, child, child_off[n], h->stream));
   CHECK(upload(&h->cp_nown, nown, n, h->stream));
-  CHECK(dalloc(&h->cp_fac, E * (h->N + 1) * (int64_t)kCpFac));
-  CHECK(dalloc(&h->cp_se, 20 * E));
+  CHECK(dalloc(&h->cp_fac, std::max<int64_t>(1, E) * (h->N + 1) * (int64_t)kCpFac));
+  // (several ranks: every rank's blocks by global edge, then the node rhs, summed)
+  CHECK(dalloc(&h->cp_se, 20 * Es + (ranks ? 2 * n : 0)));
+  if (ranks) {
+    CHECK(upload(&h->cp_gid, h->cp_gid_host.data(), std::max<int64_t>(1, E), h->stream));
+    CHECK(upload(&h->cp_nrowx, h->cp_nrowx_host.data(), 2 * n, h->stream));
+  }
   CHECK(dalloc(&h->cp_xn, 2 * n));
   CHECK(dalloc(&h->cp_Pinv, 4 * n));
   CHECK(dalloc(&h->cp_hv, 2 * n));
@@ -11864,8 +11945,8 @@ NX_API int nx_set_halo(nx_network_t* h, int32_t nranks, int32_t rank, int32_t n_
   if (!h) return fail(NX_ERR_ARG, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(NX_ERR_ARG, "bad rank/nranks");
   if (nranks > 1 && h->pc) return fail(NX_ERR_STATE, "set the halo plan before the preconditioner");
-  if (nranks > 1 && h->fe && h->fe_cp)
-    return fail(NX_ERR_STATE, "continuous pressure runs on one rank");
+  if (nranks > 1 && h->fe && h->fe_cp && h->cp_Eg == 0)
+    return fail(NX_ERR_STATE, "the halo plan before the continuous-pressure tables");
   if (n_peers < 0 || (n_peers > 0 && (!peer_rank || !send_off || !recv_off)))
     return fail(NX_ERR_ARG, "bad halo plan");
   CHECK(set_device(h));

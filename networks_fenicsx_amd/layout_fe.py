@@ -38,7 +38,7 @@ import numpy as np
 from .element import element_tensors, stable_pair
 
 __all__ = ["FeLayout", "build_fe_layout", "build_fe_rank_layout", "build_fe_partition",
-           "fe_global_rows", "fe_row_owner", "KIND_CONST", "KIND_MASS", "KIND_SOURCE", "KIND_BC"]
+           "fe_global_rows", "fe_row_owner", "build_cp_rank_tables", "KIND_CONST", "KIND_MASS", "KIND_SOURCE", "KIND_BC"]
 
 KIND_CONST, KIND_MASS, KIND_SOURCE, KIND_BC = 0, 1, 2, 3
 
@@ -627,6 +627,49 @@ def build_cp_tables(lay: FeLayout, src: np.ndarray, dst: np.ndarray) -> CpTables
     return CpTables(lay.k, lay.m, int(tI.size), cst, i32(tI), int(n), i32(nrow), i32(eb),
                     i32(lev_off), i32(order), i32(inc_off), i32(inc), i32(parent),
                     i32(child_off), i32(child), i32(nown))
+
+
+def build_cp_rank_tables(tab: CpTables, part: FeLayout):
+    """One rank's share of the node-condensed solve (``nx_fe_cp_ranks`` + ``nx_fe_set_cp``)
+    from the one-rank tables ``tab`` and the rank's partition ``part``
+    (``build_fe_partition``): ``(tab_rank, gid, nrowx)``. The rank's edges run the edge
+    kernels (``eb`` of its own edges; ``gid`` their global ids); the node tables keep global
+    nodes and edges, every rank solving the whole node forest over the summed blocks; ``nrow``
+    names the summed node rhs (2n, 2n + 1 or -1); ``nrowx`` the local rows of the node rows
+    this rank owns, and ``nown`` the local edge that writes them (-1 elsewhere)."""
+    from dataclasses import replace
+
+    own_e = np.asarray(part.edges, dtype=np.int64)[: part.n_own_edges]
+    n = tab.n_nodes
+    nrow_g = np.asarray(tab.nrow, dtype=np.int64).reshape(n, 2)
+    grows = np.asarray(part.global_rows, dtype=np.int64)
+
+    def local(rows):
+        i = np.searchsorted(grows, rows)
+        i = np.minimum(i, max(grows.size - 1, 0))
+        hit = (rows >= 0) & (grows.size > 0) & (grows[i] == rows)
+        return np.where(hit, i, -1)
+
+    nrowx = np.stack([local(nrow_g[:, 0]), local(nrow_g[:, 1])], axis=1)
+    nrow_nb = np.stack([2 * np.arange(n), np.where(nrow_g[:, 1] >= 0, 2 * np.arange(n) + 1, -1)],
+                       axis=1)
+    # the node rows' writer: the node's anchor edge when this rank owns the rows (the anchor
+    # is then one of its own edges)
+    e_loc = np.full(part.n_edges_global, -1, dtype=np.int64)
+    e_loc[own_e] = np.arange(own_e.size)
+    src_e = np.asarray(tab.eb, dtype=np.int64).reshape(-1, 4)
+    # one-rank writer (nown) is any incident edge; take the owned one: the first incident
+    # edge of the node that is local
+    inc = np.asarray(tab.inc, dtype=np.int64).reshape(-1, 2)
+    off = np.asarray(tab.inc_off, dtype=np.int64)
+    nown = np.full(n, -1, dtype=np.int64)
+    for nd in np.flatnonzero(nrowx[:, 0] >= 0):
+        loc_edges = e_loc[inc[off[nd]:off[nd + 1], 0]]
+        loc_edges = loc_edges[loc_edges >= 0]
+        nown[nd] = loc_edges[0]
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32).ravel()  # noqa: E731
+    tab_r = replace(tab, nrow=i32(nrow_nb), eb=i32(src_e[own_e]), nown=i32(nown))
+    return tab_r, i32(own_e), i32(nrowx)
 
 
 def cp_model(lay: FeLayout, tab: CpTables, val: np.ndarray, b: np.ndarray, R: np.ndarray,

@@ -169,3 +169,45 @@ def test_partition_is_the_rank_layout_for_dg0(case, P):
                      "flux_rows", "p_rows", "lm_rows", "edge_x", "peers", "send_off",
                      "send_idx", "recv_off"):
             np.testing.assert_array_equal(getattr(part, name), getattr(lay, name), err_msg=name)
+
+
+@pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "depth6_N40", "arterial5_N40"])
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("km", [(2, 1), (3, 2)])
+def test_cp_rank_tables(case, P, km):
+    """The node-condensed solve's rank tables (``build_cp_rank_tables``): every node row is
+    written by exactly one rank, from one of its own edges incident to the node; the edge
+    kernels cover every edge once; the node rhs slots are 2n / 2n + 1."""
+    from networks_fenicsx_amd.layout_fe import build_cp_rank_tables, build_cp_tables
+
+    mesh = _mesh(case)
+    src, dst = mesh.edges
+    full, lays = _partition(mesh, *km, P)
+    tab = build_cp_tables(full, src, dst)
+    n = tab.n_nodes
+    written = np.zeros(full.n_rows, dtype=np.int64)
+    edges_run = np.zeros(mesh.num_edges, dtype=np.int64)
+    for lay in lays:
+        tr, gid, nrowx = build_cp_rank_tables(tab, lay)
+        nrowx = nrowx.reshape(n, 2)
+        edges_run[gid] += 1
+        np.testing.assert_array_equal(tr.eb.reshape(-1, 4), tab.eb.reshape(-1, 4)[gid])
+        nb = tr.nrow.reshape(n, 2)
+        np.testing.assert_array_equal(nb[:, 0], 2 * np.arange(n))
+        for nd in range(n):
+            if nrowx[nd, 0] < 0:
+                assert tr.nown[nd] == -1
+                continue
+            g = lay.global_rows[nrowx[nd]]
+            assert g[0] == tab.nrow[2 * nd]
+            written[g[0]] += 1
+            if tab.nrow[2 * nd + 1] >= 0:
+                assert g[1] == tab.nrow[2 * nd + 1]
+                written[g[1]] += 1
+            e = gid[tr.nown[nd]]
+            assert nd in (tab.eb[4 * e], tab.eb[4 * e + 1])
+    np.testing.assert_array_equal(edges_run, 1)
+    node_rows = tab.nrow.reshape(n, 2)
+    np.testing.assert_array_equal(written[node_rows[:, 0]], 1)
+    lam = node_rows[node_rows[:, 1] >= 0, 1]
+    np.testing.assert_array_equal(written[lam], 1)

@@ -117,15 +117,34 @@ def test_fe_ranks_minres(tmp_path):
     assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= 1e-8
 
 
-@pytest.mark.parametrize("case,P,km", [("double_Y_N5", 2, (2, 1)), ("edge_info_N10", 3, (3, 2)),
-                                       ("Y_N4", 2, (3, 1))])
+@pytest.mark.parametrize("case,P,km", [("double_Y_N5", 2, (2, 1)), ("depth6_N40", 3, (3, 2)),
+                                       ("arterial5_N40", 2, (2, 1)), ("Y_N4", 2, (3, 1))])
 def test_fe_ranks_continuous_pressure(tmp_path, case, P, km):
     """Continuous pressure over the ranks (``build_fe_partition``: shared node rows owned
-    once, ghost edges for their remote terms): plain MINRES, the one-rank answer."""
-    ranks, data = _run(tmp_path, case, P, km[0], steps=1, m=km[1])
+    once, ghost edges for their remote terms) on a forest: the node-condensed direct solve
+    (every rank's border blocks and node rhs summed, the node forest on every rank) to the
+    one-rank LU's answer, then plain MINRES to the same."""
+    ranks, data = _run(tmp_path, case, P, km[0], steps=2, minres=1, m=km[1])
     x_ref = _reference(case, *km)
+    for s in range(2):
+        for r in range(P):
+            st = ranks[r][s]
+            assert st["direct_available"] and st["solver"] == "direct", (r, st)
+            assert st["path"] == "node-condensed" and st["converged"], (r, st)
+            assert st["relres"] == ranks[0][s]["relres"]
+        x = _gather(data, s, x_ref.size)
+        assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL, s
     for r in range(P):
+        assert ranks[r][2]["solver"] == "minres" and ranks[r][2]["converged"], ranks[r][2]
+    x = _gather(data, 2, x_ref.size)
+    assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= 1e-8
+
+
+def test_fe_ranks_continuous_pressure_cycles(tmp_path):
+    """A graph with cycles (the reference's edge_info graph): plain MINRES over the ranks."""
+    ranks, data = _run(tmp_path, "edge_info_N10", 3, 3, steps=1, m=2)
+    x_ref = _reference("edge_info_N10", 3, 2)
+    for r in range(3):
         assert ranks[r][0]["solver"] == "minres" and ranks[r][0]["converged"], ranks[r][0]
-        assert ranks[r][0]["iterations"] == ranks[0][0]["iterations"]
     x = _gather(data, 0, x_ref.size)
     assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= 1e-8
