@@ -357,7 +357,9 @@ class HydraulicNetworkAssembler:
         else:
             self._pressure_space = FunctionSpace(mesh, "pressure", "P", m, False,
                                                  fe.p_rows.size, own_ids)
+            self._pressure_space.nodes = np.asarray(fe.p_nodes)  # the shared node values first
         self._lm_space = FunctionSpace(mesh, "multiplier", "DG", 0, True, fe.lm_nodes.size)
+        self._lm_space.nodes = np.asarray(fe.lm_nodes)
         self._p_idx = fe.p_rows
         self._lm_idx = fe.lm_rows
         self._set_output_map()
@@ -485,6 +487,7 @@ class HydraulicNetworkAssembler:
         self._pressure_space = FunctionSpace(mesh, "pressure", "DG", 0, True,
                                              lp.edges.size * N, lp.edges)
         self._lm_space = FunctionSpace(mesh, "multiplier", "DG", 0, True, lp.lm_nodes.size)
+        self._lm_space.nodes = np.asarray(lp.lm_nodes)
         # gather maps: device vector -> function arrays
         per = 2 * N + 1
         slot = np.full(mesh.num_edges, -1, dtype=np.int64)

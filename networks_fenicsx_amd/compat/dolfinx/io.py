@@ -1,8 +1,9 @@
 """``dolfinx.io.VTXWriter`` stand-in (``demos/demo_tree.py:57-62`` and the other demos).
 
-ADIOS2 is not available, so the writer creates the ``.bp`` path as a directory and writes
-one ``step_<k>.npz`` per ``write(t)`` with every function's values, its graph edges and the
-vertex coordinates of its cells (enough to rebuild the field in any post-processor).
+ADIOS2 is not available, so the writer creates the ``.bp`` path as a directory and writes,
+per ``write(t)``, one VTK XML file per function (``step_<k>_<name>.vtu``, what ParaView
+would have shown from the ``.bp``; ``post_processing.write_vtu``) and one ``step_<k>.npz``
+with every function's values, its graph edges and the vertex coordinates of its cells.
 """
 
 from __future__ import annotations
@@ -44,6 +45,11 @@ class VTXWriter:
                     arrays[f"{f.name}/cell_x"] = net.mesh.geometry.x[net.mesh.cells[cells]]
         suffix = f"_r{rank}" if getattr(self.comm, "size", 1) > 1 else ""
         np.savez(self.path / f"step_{self._step:04d}{suffix}.npz", **arrays)
+        from networks_fenicsx_amd.post_processing import _export_vtu
+
+        for f in self.functions:
+            if hasattr(getattr(f.function_space, "mesh", None), "N"):
+                _export_vtu(f, self.path / f"step_{self._step:04d}{suffix}_{f.name}.vtu")
         self._step += 1
 
     def close(self) -> None:

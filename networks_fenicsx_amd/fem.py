@@ -64,6 +64,7 @@ class FunctionSpace:
         self.kind = kind
         self.color = color
         self.edges = edges
+        self.nodes = None  # graph nodes of a multiplier space / of P_m's shared node values
         self.element = _Element(family, degree, discontinuous)
         self.dofmap = _DofMap(n_dofs)
         self._n = n_dofs

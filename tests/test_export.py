@@ -1,0 +1,110 @@
+"""Export of the solution functions (``post_processing.export_functions`` /
+``export_submeshes``; reference ``post_processing.py:55-97``): VTK XML ``.vtu`` per function in
+place of ADIOS2's ``.bp``, XDMF with inline data per submesh (CPU).
+
+Checked on fields whose value is a known function of position (the x coordinate), so the
+written points and values must agree node by node: P1 and P_k flux (Lagrange-curve node
+order), DG0 pressure as cell data, continuous P_m pressure (shared node values first),
+multipliers as vertices; the XDMF topology and geometry against the mesh."""
+
+from __future__ import annotations
+
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+
+from cases import CASES
+from networks_fenicsx_amd import NetworkMesh
+from networks_fenicsx_amd.fem import Function, FunctionSpace
+from networks_fenicsx_amd.post_processing import export_functions, export_submeshes
+
+
+def _mesh():
+    make, N, strategy, _ = CASES["double_Y_N5"]
+    return NetworkMesh(make(), N=N, color_strategy=strategy)
+
+
+def _read(path):
+    root = ET.parse(path).getroot()
+    piece = root.find("UnstructuredGrid/Piece")
+    arrays = {a.get("Name"): np.array(a.text.split(), dtype=float) for a in root.iter("DataArray")}
+    return piece, arrays
+
+
+def _pos(mesh, edge, t):
+    pos = mesh.node_coordinates
+    s, d = mesh.edges[0][edge], mesh.edges[1][edge]
+    return pos[s] + (pos[d] - pos[s]) * t
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_export_vtu_fields(tmp_path, k):
+    mesh = _mesh()
+    N, E = mesh.N, mesh.num_edges
+    src, dst = mesh.edges
+    flux = []
+    for c in range(mesh.num_edge_colors):
+        edges = np.flatnonzero(mesh.edge_colors == c)
+        V = FunctionSpace(mesh, "flux", "P", k, False, edges.size * (k * N + 1), edges, c)
+        t = np.arange(k * N + 1) / (k * N)
+        vals = np.concatenate([_pos(mesh, e, t[:, None])[:, 0] for e in edges])
+        flux.append(Function(V, name=f"flux_{c}", array=vals))
+    all_e = np.arange(E)
+    Vp = FunctionSpace(mesh, "pressure", "DG", 0, True, E * N, all_e)
+    pmid = np.concatenate([_pos(mesh, e, ((np.arange(N) + 0.5) / N)[:, None])[:, 0] for e in all_e])
+    p = Function(Vp, name="pressure", array=pmid)
+    lm_nodes = np.asarray(mesh.bifurcation_values)
+    Vl = FunctionSpace(mesh, "multiplier", "DG", 0, True, lm_nodes.size)
+    Vl.nodes = lm_nodes
+    lm = Function(Vl, name="lm", array=mesh.node_coordinates[lm_nodes, 0].copy())
+    export_functions([*flux, p, lm], tmp_path)
+    for c, f in enumerate(flux):
+        piece, a = _read(tmp_path / f"flux_{c}.vtu")
+        ne = f.function_space.edges.size
+        assert int(piece.get("NumberOfCells")) == ne * N
+        assert int(piece.get("NumberOfPoints")) == ne * N * (k + 1)
+        xyz = a["Points"].reshape(-1, 3)
+        np.testing.assert_allclose(a[f"flux_{c}"], xyz[:, 0], atol=1e-12)
+        assert set(a["types"].tolist()) == {3.0 if k == 1 else 68.0}
+    piece, a = _read(tmp_path / "pressure.vtu")
+    xyz = a["Points"].reshape(-1, 2, 3)
+    np.testing.assert_allclose(a["pressure"], xyz.mean(axis=1)[:, 0], atol=1e-12)
+    piece, a = _read(tmp_path / "lm.vtu")
+    np.testing.assert_allclose(a["lm"], a["Points"].reshape(-1, 3)[:, 0], atol=1e-12)
+    assert (tmp_path / "flux_0.npz").exists() and (tmp_path / "pressure.npz").exists()
+
+
+@pytest.mark.parametrize("m", [1, 2])
+def test_export_vtu_continuous_pressure(tmp_path, m):
+    mesh = _mesh()
+    N, E = mesh.N, mesh.num_edges
+    nodes = np.flatnonzero(np.asarray(mesh.degrees) > 0)
+    t = np.arange(1, m * N) / (m * N)
+    inner = np.concatenate([_pos(mesh, e, t[:, None])[:, 0] for e in range(E)])
+    vals = np.concatenate([mesh.node_coordinates[nodes, 0], inner])
+    V = FunctionSpace(mesh, "pressure", "P", m, False, vals.size, np.arange(E))
+    V.nodes = nodes
+    Vq = FunctionSpace(mesh, "flux", "P", 1, False, 0, np.zeros(0, dtype=np.int64), 0)
+    Vl = FunctionSpace(mesh, "multiplier", "DG", 0, True, 0)
+    Vl.nodes = np.zeros(0, dtype=np.int64)
+    export_functions([Function(Vq, array=np.zeros(0)), Function(V, name="pressure", array=vals),
+                      Function(Vl, name="lm", array=np.zeros(0))], tmp_path)
+    piece, a = _read(tmp_path / "pressure.vtu")
+    assert int(piece.get("NumberOfPoints")) == E * N * (m + 1)
+    np.testing.assert_allclose(a["pressure"], a["Points"].reshape(-1, 3)[:, 0], atol=1e-12)
+
+
+def test_export_submeshes_xdmf(tmp_path):
+    mesh = _mesh()
+    export_submeshes(mesh, tmp_path)
+    N = mesh.N
+    for c, edges in enumerate(mesh.submeshes):
+        root = ET.parse(tmp_path / f"submesh_{c}.xdmf").getroot()
+        items = list(root.iter("DataItem"))
+        topo = np.array(items[0].text.split(), dtype=np.int64).reshape(-1, 2)
+        geo = np.array(items[1].text.split(), dtype=float).reshape(-1, 3)
+        cells = mesh.mesh.cells[(edges[:, None] * N + np.arange(N)[None, :]).ravel()]
+        np.testing.assert_array_equal(topo, cells)
+        gx = mesh.mesh.geometry.x
+        np.testing.assert_allclose(geo[:, : gx.shape[1]], gx)
