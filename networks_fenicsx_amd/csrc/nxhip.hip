@@ -6575,6 +6575,7 @@ struct nx_network {
   // each rank writes the node rows it owns (cp_nrowx: local rows, -1 elsewhere)
   int64_t cp_Eown = 0, cp_Eg = 0;
   int *cp_gid = nullptr, *cp_nrowx = nullptr;
+  int* cp_rec = nullptr;  // the node records (CpTree::rec)
   std::vector<int> cp_gid_host, cp_nrowx_host;
 };
 
@@ -8006,7 +8007,19 @@ struct CpTree {
   const int* child;
   double* Pinv;  // 4 per node
   double* hv;    // 2 per node
+  // per level-order index, the node's record (kCpRec ints, cp_records): every index the
+  // node's elimination / back-substitution reads, in one place -- one dependent load instead
+  // of the chain order -> offsets -> lists -> entries; nullptr: the lists
+  const int* rec;
 };
+// node record (ints): [0] n, [1] pressure row, [2] multiplier row, [3] #edges (-1: more
+// than kCpRecInc, read the lists), [4..11] (edge, end) x kCpRecInc, [12] #children (-1: more
+// than kCpRecCh), [13..21] (child, its parent edge, its end there) x kCpRecCh, [22] parent,
+// [23] parent edge, [24] this node's end of it
+constexpr int kCpRecInc = 4, kCpRecCh = 3;
+constexpr int kCpRecC = 4 + 2 * kCpRecInc;          // 12: #children
+constexpr int kCpRecP = kCpRecC + 1 + 3 * kCpRecCh;  // 22: parent, its edge, this node's end
+constexpr int kCpRecPad = 28;                        // (7 x 16 B)
 __device__ __forceinline__ void cp_block(const double* se, int e, int ra, int cb, double* B) {
   const double* S = se + 20 * (int64_t)e;  // rows of end ra, columns of end cb (2 x 2)
   B[0] = S[4 * (2 * ra) + 2 * cb];
@@ -8017,37 +8030,84 @@ __device__ __forceinline__ void cp_block(const double* se, int e, int ra, int cb
 // The node forest's elimination, one node (level order index i): its 2 x 2 pivot block from
 // its edges' border blocks minus its children's Schur terms; the pivot's inverse and the
 // condensed rhs stored for the back-substitution.
+// one incident edge's border block into the node's pivot and rhs
+__device__ __forceinline__ void cp_up_edge(const CpArgs& a, int e, int end, double* D, double* g) {
+  double B[4];
+  cp_block(a.se, e, end, end, B);
+  for (int q = 0; q < 4; ++q) D[q] += B[q];
+  g[0] += a.se[20 * (int64_t)e + 16 + 2 * end];
+  g[1] += a.se[20 * (int64_t)e + 17 + 2 * end];
+}
+// one child's Schur term, its pivot inverse Pc and rhs hc given
+__device__ __forceinline__ void cp_up_child_v(const CpArgs& a, int ce, int cend,
+                                              const double* Pc, const double* hc, double* D,
+                                              double* g) {
+  double B[4];  // child rows x this node's columns
+  cp_block(a.se, ce, cend, 1 - cend, B);
+  double X[4], z[2];  // Pc B, Pc h
+  for (int r = 0; r < 2; ++r) {
+    for (int q = 0; q < 2; ++q) X[2 * r + q] = Pc[2 * r] * B[q] + Pc[2 * r + 1] * B[2 + q];
+    z[r] = Pc[2 * r] * hc[0] + Pc[2 * r + 1] * hc[1];
+  }
+  for (int r = 0; r < 2; ++r) {
+    for (int q = 0; q < 2; ++q) D[2 * r + q] -= B[r] * X[q] + B[2 + r] * X[2 + q];
+    g[r] -= B[r] * z[0] + B[2 + r] * z[1];
+  }
+}
+__device__ __forceinline__ void cp_up_child(const CpArgs& a, const CpTree& t, int c, int ce,
+                                            int cend, double* D, double* g) {
+  cp_up_child_v(a, ce, cend, t.Pinv + 4 * (int64_t)c, t.hv + 2 * (int64_t)c, D, g);
+}
 __device__ __forceinline__ void cp_node_up(const CpArgs& a, const CpTree& t,
                                            const double* __restrict__ b, int i) {
-  const int n = t.order[i];
   double D[4] = {0.0, 0.0, 0.0, 0.0}, g[2];
-  const int pr = a.nrow[2 * n], lr = a.nrow[2 * n + 1];
-  g[0] = b[pr];
-  g[1] = lr >= 0 ? b[lr] : 0.0;
-  for (int j = t.inc_off[n]; j < t.inc_off[n + 1]; ++j) {
-    const int e = t.inc[2 * j], end = t.inc[2 * j + 1];
-    double B[4];
-    cp_block(a.se, e, end, end, B);
-    for (int q = 0; q < 4; ++q) D[q] += B[q];
-    g[0] += a.se[20 * (int64_t)e + 16 + 2 * end];
-    g[1] += a.se[20 * (int64_t)e + 17 + 2 * end];
-  }
-  if (lr < 0) D[3] = 1.0;  // (no multiplier: a decoupled dummy)
-  for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j) {
-    const int c = t.child[j];
-    const int ce = t.parent[3 * c + 1], cend = t.parent[3 * c + 2];
-    double B[4];  // child rows x this node's columns
-    cp_block(a.se, ce, cend, 1 - cend, B);
-    const double* Pc = t.Pinv + 4 * (int64_t)c;
-    const double* hc = t.hv + 2 * (int64_t)c;
-    double X[4], z[2];  // Pc B, Pc h
-    for (int r = 0; r < 2; ++r) {
-      for (int q = 0; q < 2; ++q) X[2 * r + q] = Pc[2 * r] * B[q] + Pc[2 * r + 1] * B[2 + q];
-      z[r] = Pc[2 * r] * hc[0] + Pc[2 * r + 1] * hc[1];
+  int n;
+  if (t.rec != nullptr) {  // the record in 7 independent 16-B loads, every index static
+    int r[kCpRecPad];
+    const int4* q4 = reinterpret_cast<const int4*>(t.rec + (int64_t)kCpRecPad * i);
+#pragma unroll
+    for (int w = 0; w < kCpRecPad / 4; ++w) {
+      const int4 v = q4[w];
+      r[4 * w] = v.x;
+      r[4 * w + 1] = v.y;
+      r[4 * w + 2] = v.z;
+      r[4 * w + 3] = v.w;
     }
-    for (int r = 0; r < 2; ++r) {
-      for (int q = 0; q < 2; ++q) D[2 * r + q] -= B[r] * X[q] + B[2 + r] * X[2 + q];
-      g[r] -= B[r] * z[0] + B[2 + r] * z[1];
+    n = r[0];
+    const int lr = r[2];
+    g[0] = b[r[1]];
+    g[1] = lr >= 0 ? b[lr] : 0.0;
+    if (r[3] >= 0) {
+#pragma unroll
+      for (int j = 0; j < kCpRecInc; ++j)
+        if (j < r[3]) cp_up_edge(a, r[4 + 2 * j], r[5 + 2 * j], D, g);
+    } else {
+      for (int j = t.inc_off[n]; j < t.inc_off[n + 1]; ++j)
+        cp_up_edge(a, t.inc[2 * j], t.inc[2 * j + 1], D, g);
+    }
+    if (lr < 0) D[3] = 1.0;  // (no multiplier: a decoupled dummy)
+    constexpr int kc = kCpRecC;  // the children's part of the record
+    if (r[kc] >= 0) {
+#pragma unroll
+      for (int j = 0; j < kCpRecCh; ++j)
+        if (j < r[kc]) cp_up_child(a, t, r[kc + 1 + 3 * j], r[kc + 2 + 3 * j], r[kc + 3 + 3 * j], D, g);
+    } else {
+      for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j) {
+        const int c = t.child[j];
+        cp_up_child(a, t, c, t.parent[3 * c + 1], t.parent[3 * c + 2], D, g);
+      }
+    }
+  } else {
+    n = t.order[i];
+    const int pr = a.nrow[2 * n], lr = a.nrow[2 * n + 1];
+    g[0] = b[pr];
+    g[1] = lr >= 0 ? b[lr] : 0.0;
+    for (int j = t.inc_off[n]; j < t.inc_off[n + 1]; ++j)
+      cp_up_edge(a, t.inc[2 * j], t.inc[2 * j + 1], D, g);
+    if (lr < 0) D[3] = 1.0;  // (no multiplier: a decoupled dummy)
+    for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j) {
+      const int c = t.child[j];
+      cp_up_child(a, t, c, t.parent[3 * c + 1], t.parent[3 * c + 2], D, g);
     }
   }
   inv2(D, t.Pinv + 4 * (int64_t)n);
@@ -8056,12 +8116,26 @@ __device__ __forceinline__ void cp_node_up(const CpArgs& a, const CpTree& t,
 }
 // ... and its back-substitution: the node's values from its parent's
 __device__ __forceinline__ void cp_node_down(const CpArgs& a, const CpTree& t, int i) {
-  const int n = t.order[i];
-  const int p = t.parent[3 * n];
+  int n, p, pe, pend;
+  if (t.rec != nullptr) {  // node and parent from the record (one 16-B load each)
+    const int* q = t.rec + (int64_t)kCpRecPad * i;
+    const int4 h = *reinterpret_cast<const int4*>(q);
+    const int4 v = *reinterpret_cast<const int4*>(q + 20);  // [22] parent, [23] its edge
+    const int4 w = *reinterpret_cast<const int4*>(q + 24);  // [24] this node's end of it
+    n = h.x;
+    p = v.z;
+    pe = v.w;
+    pend = w.x;
+  } else {
+    n = t.order[i];
+    p = t.parent[3 * n];
+    pe = t.parent[3 * n + 1];
+    pend = t.parent[3 * n + 2];
+  }
   double r[2] = {t.hv[2 * n], t.hv[2 * n + 1]};
   if (p >= 0) {
     double B[4];
-    cp_block(a.se, t.parent[3 * n + 1], t.parent[3 * n + 2], 1 - t.parent[3 * n + 2], B);
+    cp_block(a.se, pe, pend, 1 - pend, B);
     const double* xp = a.xn + 2 * (int64_t)p;
     r[0] -= B[0] * xp[0] + B[1] * xp[1];
     r[1] -= B[2] * xp[0] + B[3] * xp[1];
@@ -8085,6 +8159,8 @@ __global__ __launch_bounds__(1024) void k_cp_nodes(CpArgs a, CpTree t, const dou
     __syncthreads();
   }
 }
+constexpr int kCpWide = 2048;  // wider levels: grid launches (cp_nodes_launch)
+
 // One level [i0, i1) of level-order nodes, a thread per node across the grid
 __global__ __launch_bounds__(256) void k_cp_level(CpArgs a, CpTree t, const double* __restrict__ b,
                                                   int i0, int i1, int up) {
@@ -8508,7 +8584,7 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_tI,
                   h->cp_eb, h->cp_nrow, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
                   h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown, h->cp_gid,
-                  h->cp_nrowx, h->fe_tpl_buf,
+                  h->cp_nrowx, h->cp_rec, h->fe_tpl_buf,
                   h->fe_tpl_rbuf, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -10110,7 +10186,6 @@ void fe_true_residual(nx_network* h, double rtol, int nrb) {
 
 // The node forest's solve: levels of more than kCpWide nodes as grid launches (a thread per
 // node), the runs of narrower levels in one workgroup each; up deepest first, then down.
-constexpr int kCpWide = 2048;
 void cp_nodes_launch(nx_network* h, const CpArgs& a, const CpTree& tr, const double* b) {
   const std::vector<int>& lo = h->cp_lev_host;
   const int nl = h->cp_nlev;
@@ -10152,7 +10227,7 @@ int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int3
   nx_network* hs[1] = {h};
   const Team t{hs, 1, nullptr};
   const CpTree tr{h->cp_nn, h->cp_nlev, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
-                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_Pinv, h->cp_hv};
+                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_Pinv, h->cp_hv, h->cp_rec};
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
   // (one thread per edge: 64-thread workgroups spread the edges over every CU)
   const int eb = std::max(1, grid_of(Ee, 64));
@@ -11519,7 +11594,7 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   }
   for (int** p : {&h->cp_tI, &h->cp_eb, &h->cp_nrow, &h->cp_lev_off, &h->cp_order, &h->cp_inc_off,
                   &h->cp_inc, &h->cp_parent, &h->cp_child_off, &h->cp_child, &h->cp_nown,
-                  &h->cp_gid, &h->cp_nrowx}) {
+                  &h->cp_gid, &h->cp_nrowx, &h->cp_rec}) {
     if (*p) HIPCALL(hipFree(*p));
     *p = nullptr;
   }
@@ -11574,6 +11649,36 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   CHECK(upload(&h->cp_child_off, child_off, n + 1, h->stream));
   if (child_off[n] > 0) CHECK(upload(&h->cp_child, child, child_off[n], h->stream));
   CHECK(upload(&h->cp_nown, nown, n, h->stream));
+  {  // the node records in level order (CpTree::rec; the same sums in the same order)
+    std::vector<int> rec((size_t)n * kCpRecPad, 0);
+    for (int64_t i = 0; i < n; ++i) {
+      int* r = rec.data() + i * kCpRecPad;
+      const int nd = order[i];
+      r[0] = nd;
+      r[1] = nrow[2 * nd];
+      r[2] = nrow[2 * nd + 1];
+      const int ni = inc_off[nd + 1] - inc_off[nd], nc = child_off[nd + 1] - child_off[nd];
+      r[3] = ni <= kCpRecInc ? ni : -1;
+      for (int j = 0; j < ni && ni <= kCpRecInc; ++j) {
+        r[4 + 2 * j] = inc[2 * (inc_off[nd] + j)];
+        r[5 + 2 * j] = inc[2 * (inc_off[nd] + j) + 1];
+      }
+      constexpr int kc = kCpRecC;
+      r[kc] = nc <= kCpRecCh ? nc : -1;
+      for (int j = 0; j < nc && nc <= kCpRecCh; ++j) {
+        const int c = child[child_off[nd] + j];
+        r[kc + 1 + 3 * j] = c;
+        r[kc + 2 + 3 * j] = parent[3 * c + 1];
+        r[kc + 3 + 3 * j] = parent[3 * c + 2];
+      }
+      r[kCpRecP] = parent[3 * nd];
+      r[kCpRecP + 1] = parent[3 * nd + 1];
+      r[kCpRecP + 2] = parent[3 * nd + 2];
+    }
+    static_assert(kCpRecP == 22 && kCpRecP + 3 <= kCpRecPad, "the record's parent at [22..24]");
+
+    if (!std::getenv("NXHIP_CP_NOREC")) CHECK(upload(&h->cp_rec, rec.data(), n * kCpRecPad, h->stream));
+  }
   CHECK(dalloc(&h->cp_fac, std::max<int64_t>(1, E) * (h->N + 1) * (int64_t)kCpFac));
   // (several ranks: every rank's blocks by global edge, then the node rhs, summed)
   CHECK(dalloc(&h->cp_se, 20 * Es + (ranks ? 2 * n : 0)));

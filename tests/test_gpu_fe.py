@@ -228,6 +228,28 @@ def test_fe_direct_cycles_run_minres():
     assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
 
 
+@pytest.mark.parametrize("case,km", [("depth6_N40", (2, 1)), ("arterial5_N40", (3, 2)),
+                                     ("tree6_2d_N70", (2, 1))])
+def test_fe_cp_node_records_bits(case, km, monkeypatch):
+    """The node kernels read each node's packed record (``CpTree::rec``) instead of its
+    lists: the same sums in the same order, so x is bit-identical to the lists' path
+    (``NXHIP_CP_NOREC=1``, read when the tables are attached)."""
+    xs = []
+    for norec in ("0", "1"):
+        if norec == "1":
+            monkeypatch.setenv("NXHIP_CP_NOREC", "1")
+        else:
+            monkeypatch.delenv("NXHIP_CP_NOREC", raising=False)
+        mesh, asm, F, A, b, pbc = _setup(case, km, f=0.3)
+        asm.set_direct(True)
+        asm.assemble()
+        it, rr, conv = asm.handle.solve(1e-12, 100, 4)
+        assert conv and asm.handle.direct_path() == "node-condensed"
+        xs.append(asm.handle.solution())
+        asm.close()
+    np.testing.assert_array_equal(xs[0], xs[1])
+
+
 @pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "depth6_N40", "arterial5_N40",
                                   "linear_alt_N3"])
 @pytest.mark.parametrize("km", [(2, 1), (3, 2), (3, 1), (4, 3)])
