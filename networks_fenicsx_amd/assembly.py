@@ -318,6 +318,12 @@ class HydraulicNetworkAssembler:
             raise NotImplementedError("general degrees on several ranks run one process per "
                                       "rank (RCCL), not an in-process group")
         src, dst = mesh.edges
+        if ranks:  # (every rank decides the same from the same partition: no rank is left
+            # waiting in a collective for one that raised)
+            owner = partition_edges(src, dst, mesh.node_coordinates.shape[0], self._nranks)
+            if (np.bincount(owner, minlength=self._nranks) == 0).any():
+                raise ValueError(f"general element degrees on {self._nranks} ranks need at least "
+                                 f"one edge per rank ({mesh.num_edges} edges)")
         self._local = None
         self._fe_lp = None
         n_rows_edges = None  # edges whose rows this rank owns (the rest: ghost edges)
