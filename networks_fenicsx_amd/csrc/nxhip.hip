@@ -11683,7 +11683,10 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   // (several ranks: every rank's blocks by global edge, then the node rhs, summed)
   CHECK(dalloc(&h->cp_se, 20 * Es + (ranks ? 2 * n : 0)));
   if (ranks) {
-    CHECK(upload(&h->cp_gid, h->cp_gid_host.data(), std::max<int64_t>(1, E), h->stream));
+    if (E > 0)
+      CHECK(upload(&h->cp_gid, h->cp_gid_host.data(), E, h->stream));
+    else
+      CHECK(dalloc(&h->cp_gid, 1));
     CHECK(upload(&h->cp_nrowx, h->cp_nrowx_host.data(), 2 * n, h->stream));
   }
   CHECK(dalloc(&h->cp_xn, 2 * n));
