@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--N", type=int, default=19)
     ap.add_argument("--solver", choices=("direct", "minres"), default="direct")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--reverse", action="store_true",
+                    help="with --exchange: time the ranks again in reverse order (is a rank's "
+                         "time its own or its place in the sequence?)")
     ap.add_argument("--exchange", action="store_true",
                     help="also time every rank's one-launch exchange step alone "
                          "(nx_debug_xr_rehearse: its exchanges emulated)")
@@ -83,6 +86,14 @@ def main() -> int:
             # every rank's exchange step alone (one launch per rank, as on its own GPU), its
             # exchanges emulated from this graph-path solve's sums; then its answer again
             ms = [a.handle.xr_rehearse(1e-12, 20) for a in grp.assemblers]
+            if args.reverse:
+                # (a rehearsal overwrites the graph path's summed partials it emulates its
+                # exchanges from: solve on the graph path again first)
+                grp.assemble()
+                grp.solve(1e-12, 50000, 4)
+                rev = [a.handle.xr_rehearse(1e-12, 20) for a in grp.assemblers[::-1]][::-1]
+                print("exchange step per rank, timed in reverse order (us): "
+                      + " ".join(f"{1e3 * m:.1f}" for m in rev), flush=True)
             x2 = np.full(xa.size, np.nan)
             for a in grp.assemblers:
                 x2[DM.global_rows(a.local_problem, mesh0.num_edges,
