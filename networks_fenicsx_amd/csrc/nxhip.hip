@@ -8850,7 +8850,9 @@ int wait_published(nx_network* h) {
   const int want = h->seq;
   for (uint64_t spin = 1;; ++spin) {
     if (__atomic_load_n(&h->h_last->pad, __ATOMIC_ACQUIRE) == want) return NX_OK;
-    if ((spin & 1023) == 0) {
+    // (a stream query now and then -- about every millisecond -- catches a launch that ended
+    // without publishing; more often, one could land on the publish and delay seeing it)
+    if ((spin & 16383) == 0) {
       const hipError_t e = hipStreamQuery(h->stream);
       if (e == hipSuccess) {  // stream idle: the stamp must be there now
         if (__atomic_load_n(&h->h_last->pad, __ATOMIC_ACQUIRE) == want) return NX_OK;
