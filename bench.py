@@ -280,6 +280,45 @@ def c4_leg(args, world: int, rank: int, comm, timed_steps, state, allsum):
         asm.close()
 
 
+def fe_leg(mesh, steps: int = 20, warmup: int = 5) -> dict:
+    """General element degrees on the headline tree (one GPU, reported beside the headline):
+    (2, 0) through the condensed direct solve and (2, 1) through the node-condensed one,
+    assemble + solve timed like the headline (``nx_assemble`` + ``nx_solve`` per step)."""
+    from networks_fenicsx_amd import HydraulicNetworkAssembler
+
+    out = {}
+    for k, m in ((2, 0), (2, 1)):
+        key = f"k{k}_m{m}"
+        try:
+            t0 = time.perf_counter()
+            asm = HydraulicNetworkAssembler(mesh, flux_degree=k, pressure_degree=m)
+            asm.compute_forms(p_bc_ex=lambda x: x[1])
+            asm.set_direct(True)
+            setup = time.perf_counter() - t0
+            h = asm.handle
+            try:
+                res = None
+                for _ in range(warmup):
+                    asm.assemble()
+                    res = h.solve(1e-12, 50000, 32)
+                h.sync()
+                ts = time.perf_counter()
+                for _ in range(steps):
+                    asm.assemble()
+                    res = h.solve(1e-12, 50000, 32)
+                h.sync()
+                ms = 1e3 * (time.perf_counter() - ts) / steps
+                out[key] = {"rows": h.n_rows, "ms_per_step": ms, "steps": steps,
+                            "solver": "direct" if h.solver()[1] == 1 else "minres",
+                            "direct_path": h.direct_path(), "passes": res[0],
+                            "relres": res[1], "converged": res[2], "setup_s": setup}
+            finally:
+                asm.close()
+        except Exception as e:  # (reported, never fatal to the headline)
+            out[key] = {"error": f"{type(e).__name__}: {e}"}
+    return out
+
+
 def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -306,6 +345,8 @@ def parse_args(argv=None):
     ap.add_argument("--api-steps", type=int, default=10,
                     help="steps through the public Solver.assemble/solve surface (0: skip)")
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
+    ap.add_argument("--no-fe", dest="fe", action="store_false",
+                    help="skip the general-degree leg ((2, 0) and (2, 1) on the headline tree)")
     ap.add_argument("--no-c4", dest="c4", action="store_false",
                     help="skip the configs[4] leg (C4, make_tree(18), N = 19, on these GPUs)")
     ap.add_argument("--solver", choices=("direct", "minres"), default="direct",
@@ -681,6 +722,10 @@ def run(args, world: int) -> int:
     if args.c4 and (levels, N) != (C4_LEVELS, C4_N):
         c4 = c4_leg(args, world, rank, comm, timed_steps, state, allsum)
 
+    fe = None
+    if args.fe and world == 1 and (levels, N) == (15, 15):
+        fe = fe_leg(mesh)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mesh, asm, dof_total, args.cpu_budget)
@@ -718,6 +763,7 @@ def run(args, world: int) -> int:
             "api_host_ms_per_step": api_host_ms,
             "strong_scaling": strong,
             "c4": c4,
+            "general_degrees": fe,
             "solver": solver_used,
             "roofline": roof,
             "other_solver": other,
