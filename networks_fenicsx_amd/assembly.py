@@ -379,9 +379,23 @@ class HydraulicNetworkAssembler:
             # forest solved on every rank, nx_fe_cp_ranks); a graph with cycles runs MINRES
             tab = build_cp_tables(full if ranks else fe, src, dst)
             if tab is not None and ranks:
-                tab, gid, nrowx = build_cp_rank_tables(tab, fe)
-                self._handle.fe_cp_ranks(fe.n_own_edges, mesh.num_edges, gid, nrowx)
-            if tab is not None:
+                # the ranks attach it together or not at all: a rank whose tables or
+                # allocation fail would otherwise leave the others in fe_cp_solve's
+                # all-reduce alone (RCCL has no timeout) -- the (k, 0) path's rule
+                ok = 1
+                try:
+                    tab, gid, nrowx = build_cp_rank_tables(tab, fe)
+                    self._handle.fe_cp_ranks(fe.n_own_edges, mesh.num_edges, gid, nrowx)
+                    self._handle.fe_set_cp(tab)
+                except (_lib.NxError, ValueError, AssertionError, IndexError) as err:
+                    logging.error("rank %d: the continuous-pressure direct solve could not be "
+                                  "attached (%s); every rank runs MINRES", self._rank, err)
+                    ok = 0
+                if int(mesh.comm.allreduce(ok, MIN)) != 1:
+                    self._handle.fe_set_cp(None)
+                    tab = None
+                self._fe_cp = tab
+            elif tab is not None:
                 self._handle.fe_set_cp(tab)
                 self._fe_cp = tab
 

@@ -494,6 +494,14 @@ __device__ __forceinline__ void stv(double* p, double v) {
 }
 // every wave's outstanding vector-memory operations (its write-through stores) complete
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// One wave's LDS writes visible to its own later LDS reads (other lanes): the LDS serves a
+// wave's requests in order; this keeps the compiler from moving them across (no workgroup
+// barrier: the other waves may be elsewhere)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Block of kBlock threads -> one partial per block.
 __device__ __forceinline__ void block_sum_store(double v, double* out) {
@@ -3473,6 +3481,9 @@ struct DirStep {
   unsigned xtag;
   unsigned xpoll[2];  // each exchange's poll bound (kDirWaitPolls; nx_debug_xr_polls: tests)
   int ledger;         // debug build: store classes the step drops (NX_LEDGER)
+  // phase 2 by superposition (dir_sup_*; NXHIP_DIR_SUP, default 1): bit 0 on, bit 1 the
+  // waiting workgroups' u-independent part after their stores instead of before
+  int sup;
 };
 
 constexpr int kDirWaitPolls = 1 << 20;  // s_sleep-paced polls before a waiting workgroup gives up
@@ -3493,8 +3504,9 @@ constexpr int kDirLds = kDirLdsMain + kCapT;
 template <int W, int CPL>
 struct DirLane {
   double bc[CPL], bq[CPL], bN;
-  double md[CPL], mo[CPL];
+  double mo[CPL];  // R h / 6; R h / 3 = 2 mo exactly (md: halving is exact in binary)
   int flip, e, sg0, seglen, s;
+  __device__ __forceinline__ double md(int t) const { return 2.0 * mo[t]; }
 };
 
 // The chain lane state (ChainLane::setup without the loads) from a DirLane: the lumped flux
@@ -3509,7 +3521,9 @@ __device__ __forceinline__ void dir_lane_chain(const PcArgs& pa, const DirLane<W
   const int l = lane_of<W>();
   const int flip = L.flip;
   const int64_t base = (int64_t)L.e * (2 * N + 1);
-  const double* md = L.md;
+  double md[CPL];
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) md[t] = L.md(t);
   const double* mo = L.mo;
   const double mdP = __shfl_up(md[CPL - 1], 1, W), moP = __shfl_up(mo[CPL - 1], 1, W);
 #pragma unroll
@@ -3589,7 +3603,6 @@ __device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& d
     const bool valid = active && k < N;
     const int kp = flip ? N - 1 - k : k;
     const int qp = flip ? N - k : k;
-    L.md[t] = 0.0;
     L.mo[t] = 0.0;
     L.bc[t] = 0.0;
     L.bq[t] = 0.0;
@@ -3599,8 +3612,7 @@ __device__ __forceinline__ void dir_chain_asm(const PcArgs& pa, const DirStep& d
       vertex(x0, x1, kp + 1, N, invN, vb);
       const double d0 = vb[0] - va[0], d1 = vb[1] - va[1], d2 = vb[2] - va[2];
       const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-      L.md[t] = R * h / 3.0;
-      L.mo[t] = R * h / 6.0;
+      L.mo[t] = R * h / 6.0;  // (R h / 3 = 2 L.mo[t], bit for bit)
       L.bc[t] = -(fe * h);  // negated pressure row: -(f h)
       L.bq[t] = qp == 0 ? bc0 : (qp == N ? bc1 : 0.0);
     }
@@ -3655,8 +3667,8 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
       double mdA = 0.0, moA = 0.0, mdB = 0.0;
 #pragma unroll
       for (int t = 0; t < CPL; ++t) {
-        const double a = __shfl(L.md[t], ka / CPL, W), b = __shfl(L.mo[t], ka / CPL, W);
-        const double m2 = __shfl(L.md[t], kb / CPL, W);
+        const double b = __shfl(L.mo[t], ka / CPL, W), a = 2.0 * b;
+        const double m2 = 2.0 * __shfl(L.mo[t], kb / CPL, W);
         if (ka % CPL == t) {
           mdA = a;
           moA = b;
@@ -3677,15 +3689,15 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
   }
   const int s0 = L.s, q0len = 3 + s0;
   const int sdst = L.seglen - (7 * N + 1 + s0);
-  const double mdD = __shfl_down(L.md[0], 1, W), moD = __shfl_down(L.mo[0], 1, W);
-  const double mdU = __shfl_up(L.md[CPL - 1], 1, W), moU = __shfl_up(L.mo[CPL - 1], 1, W);
+  const double moD = __shfl_down(L.mo[0], 1, W), mdD = 2.0 * moD;
+  const double moU = __shfl_up(L.mo[CPL - 1], 1, W), mdU = 2.0 * moU;
   double* __restrict__ v = da.val + L.sg0;
 #pragma unroll
   for (int t = 0; t < CPL; ++t) {
     if (!ch.valid[t]) continue;
     const int k = l * CPL + t;
     const int g = flip ? N - 1 - k : k;
-    const double md = L.md[t], mo = L.mo[t];
+    const double md = L.md(t), mo = L.mo[t];
     double* o = v + q0len + 7 * g;
     o[0] = 1.0;
     o[1] = -1.0;
@@ -3694,10 +3706,10 @@ __device__ __forceinline__ void dir_chain_store(const PcArgs& pa, const DirStep&
     if (g < N - 1) {  // the next edge cell: chain cell k + 1 (k - 1 when flipped)
       double mdn, mon;
       if (!flip) {
-        mdn = t + 1 < CPL ? L.md[t + 1] : mdD;
+        mdn = t + 1 < CPL ? L.md(t + 1) : mdD;
         mon = t + 1 < CPL ? L.mo[t + 1] : moD;
       } else {
-        mdn = t > 0 ? L.md[t - 1] : mdU;
+        mdn = t > 0 ? L.md(t - 1) : mdU;
         mon = t > 0 ? L.mo[t - 1] : moU;
       }
       o[4] = md + mdn;
@@ -4010,6 +4022,7 @@ __device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirSte
   }
   rr = wave_sum(rr);
   bb = wave_sum(bb);
+  NX_DSTAMP(23);
   if ((threadIdx.x & 63) == 0) {
     s_r[threadIdx.x >> 6] = rr;
     s_b[threadIdx.x >> 6] = bb;
@@ -4022,6 +4035,7 @@ __device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirSte
       rr += s_r[w];
       bb += s_b[w];
     }
+    NX_DSTAMP(24);
     da.bbst[0] = bb;
     MrState s{};
     s.beta1 = sqrt(bb);
@@ -4107,6 +4121,48 @@ __device__ __forceinline__ void chain_rec_load(const DirStep& da, int c, bool ac
   r.seglen = q.w;
 }
 
+// A chain record in LDS (12 doubles per lane group, field i by lane i % W of the group): the
+// top solver's copy of its job's records (DirStep::sup & 4)
+constexpr int kRecLds = 12;
+template <int W>
+__device__ __forceinline__ void rec_to_lds(double* base, bool active, const ChainRec& r) {
+  if (!active) return;
+  const int l = threadIdx.x & (W - 1);
+  double* o = base + kRecLds * (int)(threadIdx.x / W);
+  const double ints0 = __builtin_bit_cast(double, (long long)(unsigned)r.e |
+                                                      ((long long)(r.flip | (r.s << 1)) << 32));
+  const double ints1 = __builtin_bit_cast(double, (long long)(unsigned)r.sg0 |
+                                                      ((long long)r.seglen << 32));
+#pragma unroll
+  for (int i = 0; i < kRecLds; ++i)
+    if (i % W == l) {
+      const double v = i < 3 ? r.x0[i] : i < 6 ? r.x1[i - 3] : i == 6 ? r.R : i == 7 ? r.fe
+                       : i == 8 ? r.bc0 : i == 9 ? r.bc1 : i == 10 ? ints0 : ints1;
+      o[i] = v;
+    }
+}
+template <int W>
+__device__ __forceinline__ void rec_from_lds(const double* base, bool active, ChainRec& r) {
+  const double* o = base + kRecLds * (int)(threadIdx.x / W);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    r.x0[i] = active ? o[i] : 0.0;
+    r.x1[i] = active ? o[3 + i] : 0.0;
+  }
+  r.R = active ? o[6] : 0.0;
+  r.fe = active ? o[7] : 0.0;
+  r.bc0 = active ? o[8] : 0.0;
+  r.bc1 = active ? o[9] : 0.0;
+  const long long a = active ? __builtin_bit_cast(long long, o[10]) : 0;
+  const long long b = active ? __builtin_bit_cast(long long, o[11]) : 0;
+  r.e = (int)(a & 0xffffffffll);
+  const int fs = (int)(a >> 32);
+  r.flip = fs & 1;
+  r.s = fs >> 1;
+  r.sg0 = (int)(b & 0xffffffffll);
+  r.seglen = (int)(b >> 32);
+}
+
 // dir_chain_asm from a chain record (the same arithmetic, the same bits)
 template <int W, int CPL>
 __device__ __forceinline__ void dir_chain_asm_rec(const PcArgs& pa, const ChainRec& r, bool active,
@@ -4127,7 +4183,6 @@ __device__ __forceinline__ void dir_chain_asm_rec(const PcArgs& pa, const ChainR
     const bool valid = active && k < N;
     const int kp = flip ? N - 1 - k : k;
     const int qp = flip ? N - k : k;
-    L.md[t] = 0.0;
     L.mo[t] = 0.0;
     L.bc[t] = 0.0;
     L.bq[t] = 0.0;
@@ -4137,8 +4192,7 @@ __device__ __forceinline__ void dir_chain_asm_rec(const PcArgs& pa, const ChainR
       vertex(r.x0, r.x1, kp + 1, N, invN, vb);
       const double d0 = vb[0] - va[0], d1 = vb[1] - va[1], d2 = vb[2] - va[2];
       const double h = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-      L.md[t] = r.R * h / 3.0;
-      L.mo[t] = r.R * h / 6.0;
+      L.mo[t] = r.R * h / 6.0;  // (R h / 3 = 2 L.mo[t], bit for bit)
       L.bc[t] = -(r.fe * h);  // negated pressure row: -(f h)
       L.bq[t] = qp == 0 ? r.bc0 : (qp == N ? r.bc1 : 0.0);
     }
@@ -4256,10 +4310,15 @@ __device__ __forceinline__ void job_stash_store(const JobStash& S, const StashRe
 // the up sweep, the top part's inputs posted write-through; sA_ / sB_ the slot's
 // back-substitution coefficients (thread = slot). MULTI: every chain's T / It / Ib and
 // every slot's D / J / A / B also to global memory, as k_pc_up_lds stores them.
+template <int W, int CPL>
+__device__ __forceinline__ void dir_sup_chain_core(const ChainLane<W, CPL>& ch,
+                                                   const DirLane<W, CPL>& L, const double* vc,
+                                                   double* park);
+
 template <int W, int CPL, bool MULTI = false>
 __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, double* lds,
                                           const JobStash& S, ChainRec& rec, DirLane<W, CPL>& L,
-                                          double& sA_, double& sB_) {
+                                          double& sA_, double& sB_, double* park = nullptr) {
   double* sT = lds;
   double* sIt = sT + kCapC;
   double* sIb = sIt + kCapC;
@@ -4277,6 +4336,12 @@ __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, d
   const int ts0 = pa.top_ts0, ts1 = pa.top_ts0 + pa.top_nt;
   const int lv0 = S.lv0, lv1 = S.lv1;
   const int js0 = S.js0, js1 = S.js1;
+  // superposition (park, one chain pass) with the job's slots in one wave (the host-built
+  // one-wave set-up): wave 0 alone runs the junction phases, with no workgroup barrier after
+  // the chains' one, and the other waves run their chains' u-independent part meanwhile
+  // (wave 0 runs its own before that barrier, where it would wait for the other waves)
+  const bool wslots = park && S.jwave > 0 && js1 - js0 <= 64 && lv1 > lv0;
+  const bool core_now = park && (!wslots || threadIdx.x < 64);
   for (int cb = c0; cb < c1; cb += G) {
     const int c = cb + seg;
     const bool active = c < c1;
@@ -4291,6 +4356,14 @@ __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, d
     for (int t = 0; t < CPL; ++t) vc[t] = L.bc[t];
     double ytop = 0.0, ybot = 0.0;
     direct_cell_inputs<W, CPL>(pa, ch, L.flip, L.bq, L.bN, vc, ytop, ybot);
+    // phase 2's u-independent part of the chain (superposition, one pass), here while its
+    // lane state is at hand -- or kept for after the barrier (wslots)
+    if (core_now) {
+      dir_sup_chain_core<W, CPL>(ch, L, vc, park);
+    } else if (park) {  // (the cell inputs wait in the park's cell slots, not in registers)
+#pragma unroll
+      for (int t = 0; t < CPL; ++t) park[t * kPcThreads + threadIdx.x] = vc[t];
+    }
     double sr = 0.0, srd = 0.0;
 #pragma unroll
     for (int t = 0; t < CPL; ++t) {
@@ -4324,6 +4397,15 @@ __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, d
   const int dc0 = S.dc0;
   __syncthreads();
   NX_DSTAMP(33);
+  if (wslots && threadIdx.x >= 64) {  // the other waves: their chains' part, then leave
+    ChainLane<W, CPL> ch;
+    dir_lane_chain<W, CPL>(pa, L, c0 + seg < c1, ch);
+    double vc[CPL];
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) vc[t] = park[t * kPcThreads + threadIdx.x];
+    dir_sup_chain_core<W, CPL>(ch, L, vc, park);
+    return;
+  }
   for (int sl = threadIdx.x; sl < ns; sl += kPcThreads) {  // phase A (ns <= kCapS: one pass)
     const int pcn = S.pchain(sl);
     double D0 = pcn >= 0 ? 1.0 / sT[pcn - c0] : 0.0;
@@ -4347,7 +4429,11 @@ __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, d
     sJ0[sl] = J0;
   }
   if (threadIdx.x == 0) sOff[ns] = S.dc1 - dc0;
-  __syncthreads();
+  if (wslots) {
+    wave_lds_sync();
+  } else {
+    __syncthreads();
+  }
   bool wave_lv = jwave > 0;
   if (!wave_lv) {
     int nkids = 0;
@@ -4421,7 +4507,11 @@ __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, d
         sIv[sl] = iv;
       }
     }
-    __syncthreads();
+    if (wslots) {
+      wave_lds_sync();
+    } else {
+      __syncthreads();
+    }
   } else {
     for (int lv = lv1 - 1; lv >= lv0; --lv) {  // deepest level first
       const int la = S.lv(lv - lv0), lb = S.lv(lv - lv0 + 1);
@@ -4657,6 +4747,261 @@ __device__ __forceinline__ void dir_down_v2(const PcArgs& pa, const DirStep& da,
     st_wt(pa.rpart + job, tr);
     st_wt(pa.rpart + pa.n_jobs + job, tb);
   }
+}
+
+// ---- phase 2 by superposition (round 6; DirStep::sup) --------------------------------------
+// A job's down sweep is affine in the few top values it reads: a root slot's value is
+// A + B u (u = its parent's top value), a lower slot's A + B z_parent, and a chain's cells
+// and fluxes are affine in its end values (zt, zb): the cells
+//   z_k = zt (T - D_k) / T + zb D_k / T + [D_k suffix_k + (T - D_k) prefix_k] / T - mo w_k,
+// the fluxes x_q[k] = q_0 - s P_k with T q_0 = s1 + s s2 - s (zb - zt) (direct_flux_cons).
+// So everything that does not depend on u -- the chain lane state, the Thomas scans of
+// M^{-1} b_q, the prefix sums, every slot's particular value z_p (u = 0) and its response
+// H = dz / du with the top value it hangs from (rho) -- runs BEFORE the top values arrive:
+// the chains' part in phase 1 on its lane state (dir_sup_chain_core; the Thomas scans are
+// phase 1's own), the slots' part in the wait (dir_sup_slots). After them only
+// z = z_p + H u per slot, z_k += zt (T - D_k) / T + zb D_k / T, x_q += s (zt - zb) / T, the
+// fused true residual from those final values (registers and shuffles; no loads) and the
+// partial sums remain (dir_sup_finish). x itself is stored after the phase-2 hand-off
+// (dir_sup_store_x): nothing of this launch reads it, and its drain then stays off the
+// hand-off. Same solution in exact arithmetic; the additions are ordered differently, so x
+// differs from the launches' x by rounding (tests: 1e-14), and the residual reported is
+// that of the stored x, bit for bit.
+// LDS: the slots' arrays in their own region after the top values (sup: sA, sB, sZp, sH,
+// kCapS doubles each; ints sRho, sP) -- the top part's solver fills them during its own
+// wait, so they must survive the top part -- then the lanes' park; sQt, sQb [kCapC] in the
+// phases' shared area (smem).
+constexpr int kDirLdsSupSlots = 5 * kCapS;
+
+__device__ __forceinline__ bool sup_one_wave(const JobStash& S) {
+  return S.js1 - S.js0 <= 64 && S.lv1 - S.lv0 <= kCapLvl;
+}
+
+// Every slot's particular value z_p, its response H and the top position rho it hangs from
+// (-1: none), in the slots' region sup (A, B: phase 1's coefficients, kCapS each, then z_p,
+// H, rho).
+// One wave when the job's slots fit (no block barrier: the caller's next barrier publishes
+// them), else level sweeps in LDS (every thread must call).
+template <int W, int CPL>
+__device__ __forceinline__ void dir_sup_slots(const PcArgs& pa, double* sup, const JobStash& S) {
+  const bool slt = (int)threadIdx.x < kCapS;
+  double* sA = sup;
+  double* sB = sA + kCapS;
+  double* sZp = sB + kCapS;
+  double* sH = sZp + kCapS;
+  int* sRho = reinterpret_cast<int*>(sH + kCapS);
+  int* sP = sRho + kCapS;
+  const double sA_ = slt ? sA[threadIdx.x] : 0.0, sB_ = slt ? sB[threadIdx.x] : 0.0;
+  const int ts0 = pa.top_ts0;
+  const int lv0 = S.lv0, lv1 = S.lv1, js0 = S.js0, js1 = S.js1;
+  const int ns = js1 - js0;
+  if (sup_one_wave(S)) {
+    if (threadIdx.x < 64) {  // lane = slot, the parent's (z_p, H, rho) by shuffles
+      const int sl = threadIdx.x;
+      const bool mine = sl < ns;
+      const bool hwave = S.jwave > 0 && lv1 > lv0;
+      int mylv = hwave && mine ? S.w0(sl) & 0xff : -1;
+      if (!hwave)
+        for (int q = 0; q < lv1 - lv0; ++q)
+          if (mine && js0 + sl >= S.lv(q) && js0 + sl < S.lv(q + 1)) mylv = q;
+      const int p = mine ? S.par(sl) : -1;
+      const bool local = p >= js0 && p < js1;
+      const int pl = local ? p - js0 : sl;
+      double zv = sA_, hv = (mine && !local && p >= 0) ? sB_ : 0.0;
+      int rho = (mine && !local && p >= 0) ? p - ts0 : -1;
+      for (int q = 1; q < lv1 - lv0; ++q) {  // (level 0: the roots, set above)
+        const double zp = __shfl(zv, pl), hp = __shfl(hv, pl);
+        const int rp = __shfl(rho, pl);
+        if (mylv == q && local) {
+          zv = sA_ + sB_ * zp;
+          hv = sB_ * hp;
+          rho = rp;
+        }
+      }
+      if (mine) {
+        sZp[sl] = zv;
+        sH[sl] = hv;
+        sRho[sl] = rho;
+      }
+    }
+    return;
+  }
+  if ((int)threadIdx.x < ns) {
+    const int sl = threadIdx.x;
+    const int p = S.par(sl);
+    const bool local = p >= js0 && p < js1;
+    sP[sl] = local ? p - js0 : -1;
+    sZp[sl] = sA_;
+    sH[sl] = (!local && p >= 0) ? sB_ : 0.0;
+    sRho[sl] = (!local && p >= 0) ? p - ts0 : -1;
+  }
+  __syncthreads();
+  for (int lv = lv0; lv < lv1; ++lv) {  // root level first
+    const int la = S.lv(lv - lv0), lb = S.lv(lv - lv0 + 1);
+    for (int j = la + threadIdx.x; j < lb; j += kPcThreads) {
+      const int sl = j - js0;
+      const int p = sP[sl];
+      if (p >= 0) {
+        sZp[sl] = sA[sl] + sB[sl] * sZp[p];
+        sH[sl] = sB[sl] * sH[p];
+        sRho[sl] = sRho[p];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// The u-independent part of one chain (lane state L, one pass): its cells' values and
+// fluxes with zt = zb = 0.
+// park: 2 CPL + 1 doubles per thread in LDS (kept there through the stores and the wait,
+// not in registers: phase 2's registers are at the 128-VGPR budget of 1024 threads). Run by
+// phase 1 (dir_up_v2) on its chain lane state: ch, L and vc = the cell inputs w_c
+// (direct_cell_inputs), so the Thomas scans of M^{-1} b_q are not repeated.
+template <int W, int CPL>
+__device__ __forceinline__ void dir_sup_chain_core(const ChainLane<W, CPL>& ch,
+                                                   const DirLane<W, CPL>& L, const double* vc,
+                                                   double* park) {
+  double zc[CPL], xq[CPL + 1];
+  const double T = ch.T, iT = 1.0 / T;
+  double a[CPL], bs[CPL], sa = 0.0, sb = 0.0;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    a[t] = (T - ch.D[t]) * vc[t];
+    bs[t] = ch.D[t] * vc[t];
+    sa += a[t];
+    sb += bs[t];
+  }
+  const double ia = seg_incl_scan<W>(sa), ibv = seg_incl_scan<W>(sb);
+  const double Atot = seg_sum<W>(sa);
+  double pa_ = ia - sa, pb_ = ibv - sb;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    pa_ += a[t];
+    const double suffix = Atot - pa_ + a[t];
+    const double prefix = pb_;
+    pb_ += bs[t];
+    const double Dk = ch.D[t];
+    zc[t] = ch.valid[t] ? (Dk * iT * suffix + (T - Dk) * iT * prefix) - ch.mo * vc[t] : 0.0;
+  }
+  direct_flux_cons<W, CPL>(ch, L.flip, L.bc, L.bq, L.bN, 0.0, 0.0, xq);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) park[t * kPcThreads + threadIdx.x] = zc[t];
+#pragma unroll
+  for (int t = 0; t <= CPL; ++t) park[(CPL + t) * kPcThreads + threadIdx.x] = xq[t];
+}
+
+// After the top values (sTop by top position): every slot's value (sZ over sZp), then the
+// chains' values from their end values, the fused true residual of those final values, the
+// chains' posts and the job's partial sums (rpart). park: dir_sup_chain_core's values on entry,
+// the final ones on return (stored by dir_sup_store_x after the hand-off).
+template <int W, int CPL>
+__device__ __forceinline__ void dir_sup_finish(const PcArgs& pa, const DirStep& da, double* lds,
+                                               const double* sTop, const JobStash& S,
+                                               const DirLane<W, CPL>& L, double* sup,
+                                               double* park, int job) {
+  double* sZ = sup + 2 * kCapS;  // (over sZp)
+  const double* sH = sZ + kCapS;
+  const int* sRho = reinterpret_cast<const int*>(sH + kCapS);
+  double* sQt = lds;
+  double* sQb = sQt + kCapC;
+  __shared__ double s_w[2 * (kPcThreads / 64)];
+  const int ts0 = pa.top_ts0;
+  const int js0 = S.js0, js1 = S.js1, ns = js1 - js0;
+  const int c0 = S.c0, c1 = S.c1;
+  const int seg = threadIdx.x / W, l = threadIdx.x & (W - 1);
+  const bool active = c0 + seg < c1;
+  if ((int)threadIdx.x < ns) {
+    const int sl = threadIdx.x;
+    const int rho = sRho[sl];
+    const double z = rho >= 0 ? sZ[sl] + sH[sl] * sTop[rho] : sZ[sl];
+    sZ[sl] = z;
+    if (!NX_LEDGER(da, 4)) da.x[S.lam(sl)] = z;
+  }
+  __syncthreads();
+  NX_DSTAMP(21);
+  const int up = active ? S.cup(seg) : -1, lo = active ? S.clo(seg) : -1;
+  const double zt = up < 0 ? 0.0 : (up >= js0 && up < js1) ? sZ[up - js0] : sTop[up - ts0];
+  const double zb = lo < 0 ? 0.0 : (lo >= js0 && lo < js1) ? sZ[lo - js0] : sTop[lo - ts0];
+  ChainLane<W, CPL> ch;
+  dir_lane_chain<W, CPL>(pa, L, active, ch);
+  double zc[CPL], xq[CPL + 1];
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) zc[t] = park[t * kPcThreads + threadIdx.x];
+#pragma unroll
+  for (int t = 0; t <= CPL; ++t) xq[t] = park[(CPL + t) * kPcThreads + threadIdx.x];
+  {
+    const double T = ch.T, iT = 1.0 / T;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      const double Dk = ch.D[t];
+      if (ch.valid[t]) zc[t] = zc[t] + (zt * (T - Dk) * iT + zb * Dk * iT);
+    }
+    const double sg = L.flip ? -1.0 : 1.0;
+    const double dq0 = (sg * (zt - zb)) / T;
+#pragma unroll
+    for (int t = 0; t < CPL; ++t)
+      if (ch.valid[t]) xq[t] = xq[t] + dq0;
+    if (ch.has_last) xq[CPL] = xq[CPL] + dq0;
+  }
+  double rr = 0.0, bb = 0.0;
+  direct_residual<W, CPL, false>(pa, ch, active, L.flip, L.bc, L.bq, L.bN, zc, xq, zt, zb, L.mo,
+                                 rr, bb, sQt, sQb, seg);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) park[t * kPcThreads + threadIdx.x] = zc[t];
+#pragma unroll
+  for (int t = 0; t <= CPL; ++t) park[(CPL + t) * kPcThreads + threadIdx.x] = xq[t];
+  const int post_t = active ? S.cpt(seg) : -1, post_b = active ? S.cpb(seg) : -1;
+  if (active && l == 0 && post_t >= 0) st_wt(da.post + post_t, sQt[seg]);
+  if (ch.has_last && post_b >= 0) st_wt(da.post + post_b, sQb[seg]);
+  __syncthreads();
+  NX_DSTAMP(22);
+  // multiplier rows of the junctions whose chains are all in this job (b_lambda = 0)
+  if ((int)threadIdx.x < ns && S.rloc(threadIdx.x)) {
+    const int sl = threadIdx.x;
+    const int pc = S.pchain(sl);
+    double acc = pc >= 0 ? sQb[pc - c0] : 0.0;
+    for (int i = S.dcoff(sl); i < S.dcoff(sl + 1); ++i) acc += sQt[S.sdc(i - S.dc0) - c0];
+    const double rl = 0.0 - acc;
+    rr += rl * rl;
+  }
+  rr = wave_sum(rr);
+  bb = wave_sum(bb);
+  if ((threadIdx.x & 63) == 0) {
+    s_w[threadIdx.x >> 6] = rr;
+    s_w[kPcThreads / 64 + (threadIdx.x >> 6)] = bb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tr = s_w[0], tb = s_w[kPcThreads / 64];
+    for (int i = 1; i < kPcThreads / 64; ++i) {
+      tr += s_w[i];
+      tb += s_w[kPcThreads / 64 + i];
+    }
+    st_wt(pa.rpart + job, tr);
+    st_wt(pa.rpart + pa.n_jobs + job, tb);
+  }
+}
+
+// The chain lane's final values into x (after the phase-2 hand-off): cells, fluxes, q_N.
+template <int W, int CPL>
+__device__ __forceinline__ void dir_sup_store_x(const PcArgs& pa, const DirStep& da,
+                                                const DirLane<W, CPL>& L, bool active,
+                                                const double* park) {
+  if (!active || NX_LEDGER(da, 4)) return;
+  const double* zc = park + threadIdx.x;
+  const double* xq = park + CPL * kPcThreads + threadIdx.x;
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const int flip = L.flip;
+  double* __restrict__ x = da.x + (int64_t)L.e * (2 * N + 1);
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    const int k = l * CPL + t;
+    if (k >= N) continue;
+    x[2 * (flip ? N - 1 - k : k) + 1] = zc[t * kPcThreads];
+    x[2 * (flip ? N - k : k)] = xq[t * kPcThreads];
+  }
+  if (l == (N - 1) / CPL) x[flip ? 0 : 2 * N] = xq[CPL * kPcThreads];
 }
 
 // The assembly's stores of one workgroup: a share of job jb's multiplier rows (+-1 values,
@@ -5079,13 +5424,36 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   // over its top inputs (they fill the wait for the top values instead of delaying it), and
   // phase 2 runs on phase 1's registers
   const bool keep = c1 - c0 <= G;
-  // (keep) helpers store the top solver's assembly; the free waves' lane groups [0, gF)
-  const int nh = min(nj - 1, (G + kDirHelpChains - 1) / kDirHelpChains);
-  constexpr int gF = kDirFreeWaves * 64 / W;
+  // phase 2 by superposition (dir_sup_*: one chain pass; the top solver then stores its own
+  // assembly after its phase 2, no helpers)
+  const bool sup = keep && (da.sup & 1) != 0;
+  bool sup_s = false;  // this workgroup formed its slots' z_p / H (dir_sup_slots)
+  // the slots' back-substitution coefficients (phase 1's sA_ / sB_, thread = slot) wait in LDS
+  // (sup: the slots' region, kDirLdsSupSlots), not in registers (the top solver's would stay
+  // live through the top part); the chains' u-independent values in the park after it
+  double* sup_lds = sTop + da.lds_top;
+  double* park = sup_lds + kDirLdsSupSlots;
+  // sup & 4: the chain records in LDS too (the top solver re-assembles its lanes from them
+  // after the top part instead of reloading them under the store stream)
+  double* rec_lds = sup && (da.sup & 4) ? park + (2 * CPL + 1) * kPcThreads : nullptr;
+  // (keep) helpers store the top solver's assembly; the free waves' lane groups [0, gF).
+  // Superposition: only wave 0 (the poll) stays free of stores -- the waiting workgroups'
+  // values come after their stores have long drained, so waves 1-3 store in the wait too
+  // Superposition also spreads the top solver's chains thinner: one chain per helper, stored
+  // by the helper's wave 1 after its own stores (no barrier: the helper's other waves do not
+  // wait for the announcement)
+  const int fw = sup ? 1 : kDirFreeWaves, hc = sup ? 1 : kPcThreads / 64 - fw;
+  const int nh = min(nj - 1, (G + hc - 1) / hc);
+  const int gF = fw * 64 / W;
   DirLane<W, CPL> L;
   double sA_ = 0.0, sB_ = 0.0;
   const int nt = pa.top_nt, ts0 = pa.top_ts0;
-  dir_up_v2<W, CPL>(pa, da, smem, S, rec, L, sA_, sB_);
+  if (rec_lds) rec_to_lds<W>(rec_lds, c0 + (int)threadIdx.x / W < c1, rec);
+  dir_up_v2<W, CPL>(pa, da, smem, S, rec, L, sA_, sB_, sup ? park : nullptr);
+  if ((int)threadIdx.x < kCapS) {
+    sup_lds[threadIdx.x] = sA_;
+    sup_lds[kCapS + threadIdx.x] = sB_;
+  }
   NX_DSTAMP(35);
   bool late_store = false;  // the top solver stores its own assembly after phase 2 (no helpers)
   bool defer_free = false;  // a waiting workgroup's free waves store theirs after phase 2
@@ -5134,6 +5502,10 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       if constexpr (XR) coarse_idx_load(pa, ci);
       top_pre_val<true>(pa, nullptr, pre);
       if constexpr (XR) coarse_idx_val(pa, ci);
+      if (sup) {  // its slots' z_p / H while the inputs come (they queue behind the stores)
+        dir_sup_slots<W, CPL>(pa, sup_lds, S);
+        sup_s = true;
+      }
       NX_DSTAMP(6);
       if constexpr (XR) {
         // the rank's top part up to its coarse partials [D | J | G] (pc_coarse_partials: in
@@ -5168,14 +5540,18 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
       } else {  // its lanes again: not kept through the solve
-        chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
+        if (rec_lds) {
+          rec_from_lds<W>(rec_lds, lane_on, rec);
+        } else {
+          chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
+        }
         dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
       }
     } else {
       // the first nh workgroups to arrive store the top solver's assembly first (they have
       // the most slack; their polls come before any store of theirs, so they see the
       // announcement at once), then their own
-      if (keep && nh > 0 && sIdx < nh) {
+      if (!sup && keep && nh > 0 && sIdx < nh) {
         if (threadIdx.x == 0) {
           int who = -1;
           for (unsigned k = 0; k < da.polls; ++k) {
@@ -5196,16 +5572,48 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
           constexpr int CH = (W * CPL + 63) / 64;
           const int4 th = *reinterpret_cast<const int4*>(da.job_hdr + kJobHdr * (int64_t)tj);
           DirLane<64, CH> Lh;
-          for (int cs = th.x + hh * kDirHelpChains; cs < th.y; cs += nh * kDirHelpChains)
-            dir_stores_v2<64, CH, true>(pa, da, tj, hh == 0 && cs < th.x + kDirHelpChains, cs,
-                                        min(th.y, cs + kDirHelpChains), false, Lh,
-                                        kDirFreeWaves, kPcThreads / 64);
+          for (int cs = th.x + hh * hc; cs < th.y; cs += nh * hc)
+            dir_stores_v2<64, CH, true>(pa, da, tj, hh == 0 && cs < th.x + hc, cs,
+                                        min(th.y, cs + hc), false, Lh, fw, kPcThreads / 64);
         }
+      }
+      // superposition: the slots' z_p / H (one wave, a free one, when they fit) before the
+      // stores, or (sup & 2) after them
+      if (sup && !(da.sup & 2)) {
+        dir_sup_slots<W, CPL>(pa, sup_lds, S);
+        sup_s = true;
+        NX_DSTAMP(20);
       }
       // own stores (unit stride: hidden in the wait), but not the free waves' (keep)
       dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
       defer_free = keep;
+      if (sup && nh > 0 && sIdx < nh && threadIdx.x / 64 == 1) {  // helper: wave 1, one chain
+        int who = -1;
+        if ((threadIdx.x & 63) == 0)
+          for (unsigned k = 0; k < da.polls; ++k) {
+            const unsigned v = __hip_atomic_load(da.sync + 4, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 10) == (tag >> 10)) {
+              who = (int)(v & 1023u);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        const int tj = __shfl(who, 0);
+        if (tj >= 0) {
+          constexpr int CH = (W * CPL + 63) / 64;
+          const int4 th = *reinterpret_cast<const int4*>(da.job_hdr + kJobHdr * (int64_t)tj);
+          DirLane<64, CH> Lh;
+          for (int cs = th.x + sIdx; cs < th.y; cs += nh)
+            dir_stores_v2<64, CH, true>(pa, da, tj, cs == th.x, cs, cs + 1, false, Lh, 1, 2);
+        }
+      }
       if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
+      if (sup && !sup_s) {
+        dir_sup_slots<W, CPL>(pa, sup_lds, S);
+        sup_s = true;
+        NX_DSTAMP(20);
+      }
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
         int ok = 0;
@@ -5243,8 +5651,19 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
     lo0 = da.left_off[threadIdx.x];
     lo1 = da.left_off[threadIdx.x + 1];
   }
-  dir_down_v2<W, CPL>(pa, da, smem, sTop, S, L, keep, sA_, sB_, job);
+  if (sup) {
+    if (!sup_s) {  // no top part: the slots now
+      dir_sup_slots<W, CPL>(pa, sup_lds, S);
+      __syncthreads();
+    }
+    dir_sup_finish<W, CPL>(pa, da, smem, sTop, S, L, sup_lds, park, job);
+  } else {
+    const bool sl = (int)threadIdx.x < kCapS;
+    dir_down_v2<W, CPL>(pa, da, smem, sTop, S, L, keep, sl ? sup_lds[threadIdx.x] : 0.0,
+                        sl ? sup_lds[kCapS + threadIdx.x] : 0.0, job);
+  }
   // hand-off 2: the residual partials and shares -> the last workgroup publishes
+  NX_DSTAMP(25);
   vm_drain();
   __syncthreads();
   NX_DSTAMP(3);
@@ -5263,16 +5682,22 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
     }
     NX_DSTAMP(4);
   }
+  if (sup) dir_sup_store_x<W, CPL>(pa, da, L, lane_on, park);
   // (the kernel's end, not the published state, waits for these; re-assembled: L kept
   // through phase 2 would overflow the register budget there)
-  if (late_store) {  // one job: the top solver's own
-    chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
+  // (rec_lds: from the records' LDS copy)
+  if (late_store || (defer_free && (int)threadIdx.x / W < gF)) {
+    if (rec_lds) {
+      rec_from_lds<W>(rec_lds, lane_on, rec);
+    } else {
+      chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
+    }
     dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
-    dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
-  } else if (defer_free && (int)threadIdx.x / W < gF) {  // the free waves' chains
-    chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
-    dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
-    dir_chain_store<W, CPL>(pa, da, lane_on, L);
+    if (late_store) {  // one job: the top solver's own
+      dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
+    } else {  // the free waves' chains
+      dir_chain_store<W, CPL>(pa, da, lane_on, L);
+    }
   }
   vm_drain();
   NX_DSTAMP(40);
@@ -6482,6 +6907,8 @@ struct nx_network {
   HostComm* hcomm = nullptr;
   std::vector<int> gk_off_host, gk_row_host;
   size_t dstep_lds = 0;  // dynamic LDS bytes per workgroup
+  bool dstep_park = false;  // dstep_lds holds the superposition's park (DirStep::sup)
+  bool dstep_rec = false;   // and the chain records' copy (sup & 4)
   unsigned* d_tsync = nullptr;  // k_dir_team_up's arrival counter (several ranks; pc_bufs)
   bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
   int last_dir_path = 0;   // the last direct solve: 0 four launches, 1 k_dir_step
@@ -8760,6 +9187,9 @@ int chain_rec_refresh(nx_network* h) {
 }
 // the tile width W of a (W, CPL) variant (nx_set_preconditioner's choice)
 int variant_w(int v) { return v == 5 || v == 7 || v == 10 ? 8 : v == 6 ? 4 : v <= 2 ? 16 : 64; }
+int variant_cpl(int v) {
+  return v == 0 ? 1 : (v == 1 || v == 3 || v == 5) ? 2 : v == 10 ? 3 : v == 8 ? 8 : v == 9 ? 16 : 4;
+}
 }  // namespace
 
 NX_API int nx_assemble(nx_network_t* h, int32_t lhs, int32_t rhs) {
@@ -9475,6 +9905,13 @@ bool xr_on(const Team& t, bool with_asm) {
 // ensure_dq forms it before them. (4.2 MB of the step's stores at C3.)
 // A job with more chains than one pass re-reads its chains' b and dq in phase 2: its step
 // writes them (dstep_multi).
+// NXHIP_DIR_SUP (read per launch: tests switch it): 0 off (phase 2 after the top values, as
+// before round 6), 1 on (default), 3 on with the waiting workgroups' part after their stores
+int dir_sup_mode() {
+  const char* e = std::getenv("NXHIP_DIR_SUP");
+  return e ? std::atoi(e) : 1;
+}
+
 DirStep dir_args(nx_network* h, double rtol) {
   h->dq_stale = !h->dstep_multi;
   DirStep d{h->edge_x, h->edge_R, h->edge_bc, h->edge_f, h->f, h->edge_lm, h->edge_seg,
@@ -9487,6 +9924,8 @@ DirStep dir_args(nx_network* h, double rtol) {
 #ifdef NX_PHASE_TIMING
   if (const char* e = std::getenv("NXHIP_LEDGER")) d.ledger = std::atoi(e);
 #endif
+  d.sup = h->dstep_park ? dir_sup_mode() : 0;
+  if (d.sup && h->dstep_rec && !(d.sup & 8)) d.sup |= 4;  // (8: tests keep the global reload)
   return d;
 }
 // the exchange fields of rank h's launch among X ranks (its own mailbox, the peers' table)
@@ -11322,7 +11761,19 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
     const int xr_dbl = h->nranks > 1 ? 2 * (nt + 1) + 4 : 0;
     h->dstep_main = std::max({kDirLdsPhase1, kDirLdsPhase2, top_dbl + xr_dbl});
     h->dstep_top = nt + (nt & 1);
-    h->dstep_lds = 8 * (size_t)(kStashDbl + h->dstep_main + h->dstep_top);
+    h->dstep_lds = 8 * (size_t)(kStashDbl + h->dstep_main + h->dstep_top + kDirLdsSupSlots);
+    {  // phase 2 by superposition: its park (2 CPL + 1 doubles per thread), when it fits (with
+       // the exchange kernels' static LDS on several ranks)
+      const int dv = N <= 16 ? 5 : N <= 24 ? 10 : N <= 32 ? 7 : variant;
+      const size_t park = 8 * (size_t)(2 * variant_cpl(dv) + 1) * kPcThreads;
+      // (the exchange kernels' budget on one rank too: the rank count may come later)
+      const size_t cap = std::min((size_t)kDirLdsMax, 160 * 1024 - xr_static_lds(dv));
+      h->dstep_park = h->dstep_lds + park <= cap;
+      if (h->dstep_park) h->dstep_lds += park;
+      const size_t recs = 8 * (size_t)kRecLds * (kPcThreads / variant_w(dv));
+      h->dstep_rec = h->dstep_park && h->dstep_lds + recs <= cap;
+      if (h->dstep_rec) h->dstep_lds += recs;
+    }
     const bool fits = mlv <= kStLv && mns <= kStNs && mnd <= kStNd && kPcThreads / W <= kStNc;
     h->d_job_hdr = const_cast<int*>(up(hdr.data(), (int64_t)hdr.size()));
     h->d_crec = scratch(10 * std::max<int64_t>(n_chains, 1));

@@ -74,6 +74,9 @@ def report(nj: int, rr: float) -> None:
         f"{', top solver' if w == last1 else ''})" for w in late))
     pub = np.argmax(g[4])
     print(f"  published by wg {pub} at {us[4][pub]:7.2f}")
+    print(f"  publisher: phase-2 arrival {us[3][pub]:.2f}, loads summed {us[23][pub]:.2f}, "
+          f"state formed {us[24][pub]:.2f}, published {us[4][pub]:.2f}; last phase-2 arrival "
+          f"{us[3].max():.2f}")
     d1 = us[1] - us[0]
     d2 = us[3] - us[2]
     print(f"  phase 1 per wg: min {d1.min():.2f} med {np.median(d1):.2f} max {d1.max():.2f}")
@@ -84,6 +87,12 @@ def report(nj: int, rr: float) -> None:
              (36, 2, "phase 2: set-up"), (37, 36, "phase 2: junction levels"),
              (38, 37, "phase 2: chains (x, residual)"), (3, 38, "phase 2: rows + partials"),
              (40, 3, "end of the workgroup after phase 2")]
+    if os.environ.get("NXHIP_DIR_SUP", "1") != "0":  # phase 2 by superposition (round 6)
+        inner = inner[:4] + [
+            (20, 1, "sup: u-independent part (waiting wgs)"), (8, 1, "stores issued"),
+            (21, 2, "sup: slot values"), (22, 21, "sup: chains (x, residual)"),
+            (25, 22, "sup: rows + partials"), (3, 25, "hand-off 2 drain + barrier"),
+            (40, 3, "end of the workgroup after phase 2")]
     for k, k0, name in inner:
         d = us[k] - us[k0]
         print(f"  {name:38s} med {np.median(d):6.2f}  max {d.max():6.2f}")

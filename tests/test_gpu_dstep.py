@@ -68,6 +68,43 @@ def test_dstep_matches_oracle_and_launches(case, monkeypatch):
     asm.close()
 
 
+@pytest.mark.parametrize("case", ["Y_N4", "depth6_N40", "arterial5_N40", "tree6_2d_N70",
+                                  "tree5_3d_N31", "linear_alt_N3"])
+def test_dstep_superposition_modes(case, monkeypatch):
+    """Phase 2 by superposition (NXHIP_DIR_SUP): the waiting
+    workgroups form every slot's particular value and response and their chains' u-independent
+    part before the top values arrive, in either order against their stores (1, 3), or not at
+    all (0: phase 2 after the values). The three agree to rounding (the same solution, other
+    orders of addition: |x_p| + |H u| ~ |x| on these graphs, so 1e-14 relative), each matches
+    the oracle's direct solve, reports the residual of the x it stored, and repeats bit for
+    bit."""
+    mesh, asm, P, A, b = _setup(case)
+    h = asm.handle
+    Ab, bb, perm, _ = O.to_build_layout(P, A, b)
+    x_ref = O.solve_reference(A, b)[perm]
+    xs = {}
+    for mode in ("0", "1", "3"):
+        monkeypatch.setenv("NXHIP_DIR_SUP", mode)
+        asm.assemble()
+        it, rr, conv = h.solve(1e-12, 100, 4)
+        assert h.direct_path() == "fused" and conv and it == 1, (mode, it, rr)
+        x = h.solution()
+        assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+        true = h.true_residual()
+        assert abs(rr - true) <= 0.05 * true + 5e-16, (mode, rr, true)
+        for _ in range(3):
+            asm.assemble()
+            it2, rr2, _ = h.solve(1e-12, 100, 4)
+            assert rr2 == rr
+            np.testing.assert_array_equal(h.solution(), x)
+        np.testing.assert_array_equal(h.csr()[2], Ab.data)
+        np.testing.assert_array_equal(h.rhs(), bb)
+        xs[mode] = x
+    for mode in ("1", "3"):
+        assert np.linalg.norm(xs[mode] - xs["0"]) <= 1e-14 * np.linalg.norm(xs["0"]), mode
+    asm.close()
+
+
 def test_dstep_lumped_mass_feeds_minres():
     """The lumped flux mass the fused kernel writes (the preconditioner's D block) is the
     assembly kernel's bit for bit: MINRES after a fused step and after the assembly kernel
