@@ -161,6 +161,24 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def cgroup_cpus() -> int | None:
+    """The CPUs this process's cgroup may use: ``cpu.max`` (v2) or ``cpu.cfs_quota_us`` /
+    ``cpu.cfs_period_us`` (v1), rounded down (at least 1); None when unlimited or unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) // int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return max(1, q // p) if q > 0 and p > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(mesh, asm, dof: int, budget_s: float):
     """The hot path on the host cores (rank 0, one GPU only), in legs:
 
@@ -170,9 +188,11 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
     * ``superlu``: the oracle's numpy assembly of the reference forms + SuperLU ``spsolve``
       (1 thread; the stand-in for the reference's MUMPS direct solve).
 
-    The direct port runs at the OpenMP default (``OMP_NUM_THREADS``) and at one thread per CPU
-    of the affinity mask (all host cores); the headline ``value`` is the faster of
-    the two. The legs share ``budget_s`` equally."""
+    The direct port runs at the OpenMP default (``OMP_NUM_THREADS``) and, when it differs, at
+    the CPU share the process's cgroup grants (``cpu.max`` quota / period: SURVEY 8d's "all
+    host cores" this process may actually use -- the affinity mask names the whole shared
+    host, 256 CPUs, and oversubscribing a 16-CPU share measured 1.3 s per step, noise); the
+    headline ``value`` is the faster. The legs share ``budget_s`` equally."""
     from networks_fenicsx_amd.assembly import edge_boundary_rhs, evaluate_nodal
     from oracle import nx_cpu
     from oracle import nx_oracle as O
@@ -188,11 +208,14 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = None
+    quota = cgroup_cpus()
+    share = min(x for x in (quota, affinity) if x) if (quota or affinity) else None
     runs_of = [(True, "port-direct", omp, "the direct tree solve (as the GPU's default)"),
                (False, "port", omp, "MINRES with the exact tree preconditioner")]
-    if affinity and affinity != omp:  # every core this process may run on
-        runs_of.insert(1, (True, "port-direct-affinity", affinity,
-                           "the direct tree solve, one thread per CPU of the affinity mask"))
+    if share and share != omp:  # every CPU this process may use
+        runs_of.insert(1, (True, "port-direct-share", share,
+                           "the direct tree solve, one thread per CPU of the process's "
+                           "cgroup CPU share"))
     for direct, leg, threads, what in runs_of:
         nx_cpu.set_threads(threads)
         ms, runs, its = port.time_steps(budget_s / (len(runs_of) + 1), direct=direct)
@@ -221,11 +244,12 @@ def cpu_baseline(mesh, asm, dof: int, budget_s: float):
     return {"value": head["value"], "unit": "DoF/s", "cores": head["cores"], "kind": "port",
             "ms_per_step": head["ms_per_step"], "sample": head["sample"],
             "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
-            "affinity_cpus": affinity, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "affinity_cpus": affinity, "cgroup_cpus": quota,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
             "cores_note": (f"direct legs at the OpenMP default ({omp} threads, from "
-                           "OMP_NUM_THREADS) and at every CPU of the affinity mask "
-                           f"({affinity}); the headline is the faster; os.cpu_count() is the "
-                           "whole shared host"),
+                           "OMP_NUM_THREADS) and, if different, at the cgroup CPU share "
+                           f"({quota}; cpu.max quota / period); the headline is the faster; "
+                           "os.cpu_count() and the affinity mask are the whole shared host"),
             "legs": legs}
 
 

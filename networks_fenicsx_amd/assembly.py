@@ -403,8 +403,9 @@ class HydraulicNetworkAssembler:
         """(k, 0): the direct solve through the condensed P1/DG0 system (``nx_fe_set_direct``).
         An auxiliary P1/DG0 handle of the same edges carries the tree decomposition; its flux
         mass becomes the condensed ``R h [[a, b], [b, a]]`` (``element.condensed_flux_mass``),
-        whose ratios are integers: ``a / b = (-1)^(k+1) (k+1)``. Forests only (a graph with
-        cycles runs MINRES: the Woodbury correction is built from the P1 CSR). Several ranks:
+        whose ratios are integers: ``a / b = (-1)^(k+1) (k+1)``. A graph with cycles (one
+        rank, up to ``MAX_CYCLES`` cycle chains): the auxiliary tree solve is corrected by the
+        Woodbury step of its dropped couplings (``fe_cyc_build``). Several ranks:
         the auxiliary handle is the rank's P1/DG0 handle (its halo, cut rows, coarse step),
         and the ranks attach it only if every rank can run its direct tree solve."""
         mesh, fe = self._network_mesh, self._fe
@@ -414,7 +415,10 @@ class HydraulicNetworkAssembler:
                                                            mesh.degrees, mesh.N, 0, 1)
         pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=256)
         aux = None
-        ok = bool(pc.tree_exact)
+        # a graph with cycles on one rank: the auxiliary handle's Woodbury correction of its
+        # cycle chains (nx_set_cycles, set with its decomposition), as P1/DG0's direct solve
+        ncyc = int(np.asarray(pc.cyc_rows).reshape(-1, 2).shape[0])
+        ok = bool(pc.tree_exact) or (not ranks and 0 < ncyc <= _lib.MAX_CYCLES)
         if ranks:  # (every rank makes the same collective calls below: decide together)
             ok = int(self._network_mesh.comm.allreduce(int(ok), MIN)) == 1
         if ok:

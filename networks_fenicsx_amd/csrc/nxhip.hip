@@ -3481,8 +3481,8 @@ struct DirStep {
   unsigned xtag;
   unsigned xpoll[2];  // each exchange's poll bound (kDirWaitPolls; nx_debug_xr_polls: tests)
   int ledger;         // debug build: store classes the step drops (NX_LEDGER)
-  // phase 2 by superposition (dir_sup_*; NXHIP_DIR_SUP, default 1): bit 0 on, bit 1 the
-  // waiting workgroups' u-independent part after their stores instead of before
+  // phase 2 by superposition (dir_sup_*; NXHIP_DIR_SUP, default 1): bit 0 on, bit 2 the
+  // chain records' and lane masses' LDS copies (when they fit)
   int sup;
 };
 
@@ -3999,6 +3999,21 @@ __device__ __forceinline__ void publish_wt(const MrState& s, int q, int* seq, Mr
   __hip_atomic_store(&mirror->pad, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// sum_{k0 <= k < k1} post[k] in order, write-through loads: the first four issued together
+// (a left row has one post per incident chain: three on a binary tree), not one round trip
+// each
+__device__ __forceinline__ double post_sum(const double* post, int k0, int k1) {
+  double v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = k0 + j < k1 ? ld_wt(post + k0 + j) : 0.0;
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (k0 + j < k1) acc += v[j];
+  for (int k = k0 + 4; k < k1; ++k) acc += ld_wt(post + k);
+  return acc;
+}
+
 // The last workgroup of phase 2: the partials and the left rows' shares, fixed order.
 // lo0 / lo1: left row threadIdx.x's post range (loaded by every workgroup before its
 // arrival: static), so only the write-through loads remain after the hand-off.
@@ -4013,11 +4028,9 @@ __device__ __forceinline__ void dir_publish_fused(const PcArgs& pa, const DirSte
     bb += ld_wt(pa.rpart + nj + i);
   }
   for (int i = threadIdx.x; i < da.n_left; i += kPcThreads) {
-    double acc = 0.0;
     const bool pre = i == (int)threadIdx.x;
     const int k0 = pre ? lo0 : da.left_off[i], k1 = pre ? lo1 : da.left_off[i + 1];
-    for (int k = k0; k < k1; ++k) acc += ld_wt(da.post + k);
-    const double rv = 0.0 - acc;  // b = 0 on the multiplier rows
+    const double rv = 0.0 - post_sum(da.post, k0, k1);  // b = 0 on the multiplier rows
     rr += rv * rv;
   }
   rr = wave_sum(rr);
@@ -4161,6 +4174,35 @@ __device__ __forceinline__ void rec_from_lds(const double* base, bool active, Ch
   r.s = fs >> 1;
   r.sg0 = (int)(b & 0xffffffffll);
   r.seglen = (int)(b >> 32);
+}
+
+// A lane state (DirLane) from the LDS copies: the cell masses and cell rhs as phase 1
+// assembled them (lpark: 2 CPL per thread), the flux rhs and the indices from the chain's
+// record -- dir_chain_asm_rec's values, bit for bit, without its arithmetic
+template <int W, int CPL>
+__device__ __forceinline__ void lane_from_lds(const PcArgs& pa, const double* rec_lds,
+                                              const double* lpark, bool active,
+                                              DirLane<W, CPL>& L) {
+  ChainRec r;
+  rec_from_lds<W>(rec_lds, active, r);
+  const int N = pa.N;
+  const int l = threadIdx.x & (W - 1);
+  const int flip = r.flip;
+  L.e = r.e;
+  L.flip = flip;
+  L.s = r.s;
+  L.sg0 = r.sg0;
+  L.seglen = r.seglen;
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) {
+    const int k = l * CPL + t;
+    const bool valid = active && k < N;
+    const int qp = flip ? N - k : k;
+    L.mo[t] = lpark[t * kPcThreads + threadIdx.x];
+    L.bc[t] = lpark[(CPL + t) * kPcThreads + threadIdx.x];
+    L.bq[t] = valid ? (qp == 0 ? r.bc0 : (qp == N ? r.bc1 : 0.0)) : 0.0;
+  }
+  L.bN = (active && l == (N - 1) / CPL) ? (flip ? r.bc0 : r.bc1) : 0.0;
 }
 
 // dir_chain_asm from a chain record (the same arithmetic, the same bits)
@@ -4314,6 +4356,12 @@ template <int W, int CPL>
 __device__ __forceinline__ void dir_sup_chain_core(const ChainLane<W, CPL>& ch,
                                                    const DirLane<W, CPL>& L, const double* vc,
                                                    double* park);
+// the job's slots in one wave with the host-built set-up: phase 1's junction phases then run
+// in wave 0 alone (no workgroup barriers), and the superposition's chain part is split
+// around them (dir_up_v2, dir_sup_core_wave0)
+__device__ __forceinline__ bool sup_wslots(const JobStash& S) {
+  return S.jwave > 0 && S.js1 - S.js0 <= 64 && S.lv1 > S.lv0;
+}
 
 template <int W, int CPL, bool MULTI = false>
 __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, double* lds,
@@ -4338,10 +4386,10 @@ __device__ __forceinline__ void dir_up_v2(const PcArgs& pa, const DirStep& da, d
   const int js0 = S.js0, js1 = S.js1;
   // superposition (park, one chain pass) with the job's slots in one wave (the host-built
   // one-wave set-up): wave 0 alone runs the junction phases, with no workgroup barrier after
-  // the chains' one, and the other waves run their chains' u-independent part meanwhile
-  // (wave 0 runs its own before that barrier, where it would wait for the other waves)
-  const bool wslots = park && S.jwave > 0 && js1 - js0 <= 64 && lv1 > lv0;
-  const bool core_now = park && (!wslots || threadIdx.x < 64);
+  // the chains' one, and the other waves run their chains' u-independent part meanwhile;
+  // wave 0 runs its own after the hand-off (dir_sup_core_wave0), in the wait
+  const bool wslots = park && sup_wslots(S);
+  const bool core_now = park && !wslots;
   for (int cb = c0; cb < c1; cb += G) {
     const int c = cb + seg;
     const bool active = c < c1;
@@ -4890,6 +4938,20 @@ __device__ __forceinline__ void dir_sup_chain_core(const ChainLane<W, CPL>& ch,
   for (int t = 0; t <= CPL; ++t) park[(CPL + t) * kPcThreads + threadIdx.x] = xq[t];
 }
 
+// Wave 0's chains' u-independent part (sup_wslots: deferred from phase 1 into the wait; the
+// cell inputs wait in the park's cell slots)
+template <int W, int CPL>
+__device__ __forceinline__ void dir_sup_core_wave0(const PcArgs& pa, const DirLane<W, CPL>& L,
+                                                   bool active, double* park) {
+  if (threadIdx.x >= 64) return;
+  ChainLane<W, CPL> ch;
+  dir_lane_chain<W, CPL>(pa, L, active, ch);
+  double vc[CPL];
+#pragma unroll
+  for (int t = 0; t < CPL; ++t) vc[t] = park[t * kPcThreads + threadIdx.x];
+  dir_sup_chain_core<W, CPL>(ch, L, vc, park);
+}
+
 // After the top values (sTop by top position): every slot's value (sZ over sZp), then the
 // chains' values from their end values, the fused true residual of those final values, the
 // chains' posts and the job's partial sums (rpart). park: dir_sup_chain_core's values on entry,
@@ -5327,18 +5389,13 @@ __device__ __forceinline__ bool dir_publish_xr(const PcArgs& pa, const DirStep& 
     bb += ld_wt(pa.rpart + nj + i);
   }
   for (int i = threadIdx.x; i < nl; i += kPcThreads) {
-    double acc = 0.0;
     const bool pre = i == (int)threadIdx.x;
     const int k0 = pre ? lo0 : da.left_off[i], k1 = pre ? lo1 : da.left_off[i + 1];
-    for (int k = k0; k < k1; ++k) acc += ld_wt(da.post + k);
-    const double rv = 0.0 - acc;  // b = 0 on the multiplier rows
+    const double rv = 0.0 - post_sum(da.post, k0, k1);  // b = 0 on the multiplier rows
     rr += rv * rv;
   }
-  for (int k = threadIdx.x; k < K; k += kPcThreads) {  // this rank's shares of the cut rows
-    double acc = 0.0;
-    for (int e = da.left_off[nl + k]; e < da.left_off[nl + k + 1]; ++e) acc += ld_wt(da.post + e);
-    xs[2 + k] = acc;
-  }
+  for (int k = threadIdx.x; k < K; k += kPcThreads)  // this rank's shares of the cut rows
+    xs[2 + k] = post_sum(da.post, da.left_off[nl + k], da.left_off[nl + k + 1]);
   rr = wave_sum(rr);
   bb = wave_sum(bb);
   if ((threadIdx.x & 63) == 0) {
@@ -5428,20 +5485,23 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   // assembly after its phase 2, no helpers)
   const bool sup = keep && (da.sup & 1) != 0;
   bool sup_s = false;  // this workgroup formed its slots' z_p / H (dir_sup_slots)
+
   // the slots' back-substitution coefficients (phase 1's sA_ / sB_, thread = slot) wait in LDS
   // (sup: the slots' region, kDirLdsSupSlots), not in registers (the top solver's would stay
   // live through the top part); the chains' u-independent values in the park after it
   double* sup_lds = sTop + da.lds_top;
   double* park = sup_lds + kDirLdsSupSlots;
-  // sup & 4: the chain records in LDS too (the top solver re-assembles its lanes from them
-  // after the top part instead of reloading them under the store stream)
+  // sup & 4: the chain records and every lane's cell masses and cell rhs in LDS too (the top
+  // solver rebuilds its lanes from them after the top part -- no loads under the store
+  // stream, no second assembly -- and so do the stores left for the kernel's tail)
   double* rec_lds = sup && (da.sup & 4) ? park + (2 * CPL + 1) * kPcThreads : nullptr;
+  double* lpark = rec_lds ? rec_lds + kRecLds * G : nullptr;
   // (keep) helpers store the top solver's assembly; the free waves' lane groups [0, gF).
   // Superposition: only wave 0 (the poll) stays free of stores -- the waiting workgroups'
   // values come after their stores have long drained, so waves 1-3 store in the wait too
   // Superposition also spreads the top solver's chains thinner: one chain per helper, stored
-  // by the helper's wave 1 after its own stores (no barrier: the helper's other waves do not
-  // wait for the announcement)
+  // by the helper's wave 0 in the kernel's tail (after x: its stores would hold up the poll
+  // for the top values and their loads behind them; no barrier either)
   const int fw = sup ? 1 : kDirFreeWaves, hc = sup ? 1 : kPcThreads / 64 - fw;
   const int nh = min(nj - 1, (G + hc - 1) / hc);
   const int gF = fw * 64 / W;
@@ -5450,12 +5510,20 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   const int nt = pa.top_nt, ts0 = pa.top_ts0;
   if (rec_lds) rec_to_lds<W>(rec_lds, c0 + (int)threadIdx.x / W < c1, rec);
   dir_up_v2<W, CPL>(pa, da, smem, S, rec, L, sA_, sB_, sup ? park : nullptr);
+  if (lpark) {
+#pragma unroll
+    for (int t = 0; t < CPL; ++t) {
+      lpark[t * kPcThreads + threadIdx.x] = L.mo[t];
+      lpark[(CPL + t) * kPcThreads + threadIdx.x] = L.bc[t];
+    }
+  }
   if ((int)threadIdx.x < kCapS) {
     sup_lds[threadIdx.x] = sA_;
     sup_lds[kCapS + threadIdx.x] = sB_;
   }
   NX_DSTAMP(35);
   bool late_store = false;  // the top solver stores its own assembly after phase 2 (no helpers)
+  bool helper = false;      // (superposition) a helper storing its top solver chain in the tail
   bool defer_free = false;  // a waiting workgroup's free waves store theirs after phase 2
   const bool lane_on = c0 + (int)threadIdx.x / W < c1;
   if (nt > 0) {  // hand-off 1: the top part's inputs -> the last workgroup -> its values
@@ -5504,6 +5572,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       if constexpr (XR) coarse_idx_val(pa, ci);
       if (sup) {  // its slots' z_p / H while the inputs come (they queue behind the stores)
         dir_sup_slots<W, CPL>(pa, sup_lds, S);
+        if (sup_wslots(S)) dir_sup_core_wave0<W, CPL>(pa, L, lane_on, park);
         sup_s = true;
       }
       NX_DSTAMP(6);
@@ -5540,12 +5609,12 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, false, L);
         vm_drain();  // (its phase 2 reads them back)
       } else {  // its lanes again: not kept through the solve
-        if (rec_lds) {
-          rec_from_lds<W>(rec_lds, lane_on, rec);
+        if (lpark) {
+          lane_from_lds<W, CPL>(pa, rec_lds, lpark, lane_on, L);
         } else {
           chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
+          dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
         }
-        dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
       }
     } else {
       // the first nh workgroups to arrive store the top solver's assembly first (they have
@@ -5577,43 +5646,19 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
                                         min(th.y, cs + hc), false, Lh, fw, kPcThreads / 64);
         }
       }
-      // superposition: the slots' z_p / H (one wave, a free one, when they fit) before the
-      // stores, or (sup & 2) after them
-      if (sup && !(da.sup & 2)) {
+      // superposition: the slots' z_p / H and wave 0's chains' part (one wave, the free one,
+      // when they fit) in the wait
+      if (sup) {
         dir_sup_slots<W, CPL>(pa, sup_lds, S);
+        if (sup_wslots(S)) dir_sup_core_wave0<W, CPL>(pa, L, lane_on, park);
         sup_s = true;
         NX_DSTAMP(20);
       }
+      helper = sup && nh > 0 && sIdx < nh;
       // own stores (unit stride: hidden in the wait), but not the free waves' (keep)
       dir_stores_v2<W, CPL, true>(pa, da, job, true, c0, c1, keep, L, keep ? gF : 0);
       defer_free = keep;
-      if (sup && nh > 0 && sIdx < nh && threadIdx.x / 64 == 1) {  // helper: wave 1, one chain
-        int who = -1;
-        if ((threadIdx.x & 63) == 0)
-          for (unsigned k = 0; k < da.polls; ++k) {
-            const unsigned v = __hip_atomic_load(da.sync + 4, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            if ((v >> 10) == (tag >> 10)) {
-              who = (int)(v & 1023u);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        const int tj = __shfl(who, 0);
-        if (tj >= 0) {
-          constexpr int CH = (W * CPL + 63) / 64;
-          const int4 th = *reinterpret_cast<const int4*>(da.job_hdr + kJobHdr * (int64_t)tj);
-          DirLane<64, CH> Lh;
-          for (int cs = th.x + sIdx; cs < th.y; cs += nh)
-            dir_stores_v2<64, CH, true>(pa, da, tj, cs == th.x, cs, cs + 1, false, Lh, 1, 2);
-        }
-      }
       if (!keep) vm_drain();  // (several passes: its phase 2 reads them back)
-      if (sup && !sup_s) {
-        dir_sup_slots<W, CPL>(pa, sup_lds, S);
-        sup_s = true;
-        NX_DSTAMP(20);
-      }
       NX_DSTAMP(8);
       if (threadIdx.x == 0) {
         int ok = 0;
@@ -5654,6 +5699,7 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   if (sup) {
     if (!sup_s) {  // no top part: the slots now
       dir_sup_slots<W, CPL>(pa, sup_lds, S);
+      if (sup_wslots(S)) dir_sup_core_wave0<W, CPL>(pa, L, lane_on, park);
       __syncthreads();
     }
     dir_sup_finish<W, CPL>(pa, da, smem, sTop, S, L, sup_lds, park, job);
@@ -5683,16 +5729,37 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
     NX_DSTAMP(4);
   }
   if (sup) dir_sup_store_x<W, CPL>(pa, da, L, lane_on, park);
+  if (helper && threadIdx.x < 64) {  // helper: wave 0, one chain
+    int who = -1;
+    if ((threadIdx.x & 63) == 0)
+      for (unsigned k = 0; k < da.polls; ++k) {
+        const unsigned v = __hip_atomic_load(da.sync + 4, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 10) == (tag >> 10)) {
+          who = (int)(v & 1023u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    const int tj = __shfl(who, 0);
+    if (tj >= 0) {
+      constexpr int CH = (W * CPL + 63) / 64;
+      const int4 th = *reinterpret_cast<const int4*>(da.job_hdr + kJobHdr * (int64_t)tj);
+      DirLane<64, CH> Lh;
+      for (int cs = th.x + sIdx; cs < th.y; cs += nh)
+        dir_stores_v2<64, CH, true>(pa, da, tj, cs == th.x, cs, cs + 1, false, Lh, 0, 1);
+    }
+  }
   // (the kernel's end, not the published state, waits for these; re-assembled: L kept
   // through phase 2 would overflow the register budget there)
-  // (rec_lds: from the records' LDS copy)
+  // (lpark: from the LDS copies)
   if (late_store || (defer_free && (int)threadIdx.x / W < gF)) {
-    if (rec_lds) {
-      rec_from_lds<W>(rec_lds, lane_on, rec);
+    if (lpark) {
+      lane_from_lds<W, CPL>(pa, rec_lds, lpark, lane_on, L);
     } else {
       chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
+      dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
     }
-    dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
     if (late_store) {  // one job: the top solver's own
       dir_stores_v2<W, CPL>(pa, da, job, true, c0, c1, true, L);
     } else {  // the free waves' chains
@@ -9925,7 +9992,9 @@ DirStep dir_args(nx_network* h, double rtol) {
   if (const char* e = std::getenv("NXHIP_LEDGER")) d.ledger = std::atoi(e);
 #endif
   d.sup = h->dstep_park ? dir_sup_mode() : 0;
-  if (d.sup && h->dstep_rec && !(d.sup & 8)) d.sup |= 4;  // (8: tests keep the global reload)
+  // (bit 2, the LDS copies: only asked for, and only when they fit -- measured neutral at
+  // C3, r06l-r06o: the top solver is not the last workgroup of phase 2 any more)
+  if (!h->dstep_rec) d.sup &= ~4;
   return d;
 }
 // the exchange fields of rank h's launch among X ranks (its own mailbox, the peers' table)
@@ -10547,6 +10616,59 @@ int fe_true_residual_team(nx_network* h, double rtol, int nrb) {
   HIPCALL(hipGetLastError());
   return NX_OK;
 }
+// The couplings a = A[q, lam] of the cycle chains' grounded ends from the P1 layout's rows
+// (the auxiliary handle holds no assembled CSR): a flux end q is its edge's q_0 (-1 at the
+// source multiplier) or q_N (+1 at the target's) -- k_pattern's entries; then U^T Z as
+// k_cyc_cap forms it.
+__global__ __launch_bounds__(256) void k_cyc_cap_p1(const double* __restrict__ Z, int64_t ldz,
+                                                    const int* __restrict__ rows, int m, int N,
+                                                    double* __restrict__ cap,
+                                                    double* __restrict__ acoef) {
+  for (int i = threadIdx.x; i < m * m; i += 256) {
+    const int r = i / m, c = i % m;
+    cap[i] = Z[(int64_t)c * ldz + rows[r]];
+  }
+  for (int k = threadIdx.x; 2 * k < m; k += 256) {
+    const int loc = rows[2 * k] % (2 * N + 1);
+    acoef[k] = loc == 0 ? -1.0 : (loc == 2 * N ? 1.0 : 0.0);  // (0: cyc_invert refuses it)
+  }
+}
+
+// (k, 0) on a graph with cycles (one rank): the auxiliary handle's Woodbury correction for
+// the condensed system (nx_set_cycles on the auxiliary handle): Z = A_g^{-1} U by its tree
+// solves of unit right-hand sides (the condensed lumped mass just written by k_fe_condense),
+// U^T Z and the couplings, Cinv on the host. On this handle's stream; once per assembled
+// matrix of h (its coefficients: the condensed mass is R h [[a, b], [b, a]]).
+int fe_cyc_build(nx_network* h, nx_network* a) {
+  const int m = 2 * a->n_cyc;
+  const hipStream_t as = a->stream;
+  a->stream = h->stream;
+  a->need_r = false;
+  int rc = NX_OK;
+  for (int j = 0; j < m && rc == NX_OK; ++j) {
+    if (hipMemsetAsync(a->tmp, 0, sizeof(double) * a->n_col, a->stream) != hipSuccess ||
+        hipMemsetAsync(a->x, 0, sizeof(double) * a->n_col, a->stream) != hipSuccess) {
+      rc = fail(NX_ERR_HIP, "fe_cyc_build: memset");
+      break;
+    }
+    hipLaunchKernelGGL(k_cyc_unit, dim3(1), dim3(1), 0, a->stream, a->tmp, a->d_cyc_rows, j);
+    rc = launch_direct(a, 0.0, 1);  // (refinement form: x += A_g^{-1} tmp; sweeps only)
+    if (rc == NX_OK &&
+        hipMemcpyAsync(a->cyc_z + (int64_t)j * a->n_col, a->x, sizeof(double) * a->n_col,
+                       hipMemcpyDeviceToDevice, a->stream) != hipSuccess)
+      rc = fail(NX_ERR_HIP, "fe_cyc_build: copy");
+  }
+  if (rc == NX_OK) {
+    hipLaunchKernelGGL(k_cyc_cap_p1, dim3(1), dim3(256), 0, a->stream, a->cyc_z, a->n_col,
+                       a->d_cyc_rows, m, (int)a->N, a->cyc_cap, a->cyc_cap + (int64_t)m * m);
+    rc = cyc_invert(a);
+  }
+  a->stream = as;
+  CHECK(rc);
+  a->cyc_version = h->lhs_version;
+  return NX_OK;
+}
+
 int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
                     int32_t* converged) {
   nx_network* a = h->fe_aux;
@@ -10570,6 +10692,8 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
     const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
     hipLaunchKernelGGL(k_fe_condense, dim3(grid_of(n0, kBlock)), dim3(kBlock), 0, h->stream, c,
                        b, pass ? nullptr : a->dq, a->rhs);
+    const int mcyc = ranks ? 0 : 2 * a->n_cyc;  // a graph with cycles (one rank): Woodbury
+    if (mcyc && pass == 0 && a->cyc_version != h->lhs_version) CHECK(fe_cyc_build(h, a));
     {  // the auxiliary tree solve on this handle's stream (no cross-queue hand-offs)
       const hipStream_t as = a->stream;
       a->stream = h->stream;
@@ -10578,6 +10702,12 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
                            : launch_direct(a, 0.0, 0);
       a->stream = as;
       CHECK(rc);
+    }
+    if (mcyc) {  // x_aux -= Z Cinv U^T x_aux: the couplings the tree solve dropped
+      hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, a->x, a->d_cyc_rows, mcyc,
+                         a->cyc_cinv, nullptr, a->cyc_w, nullptr);
+      hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(a->n_own, kBlock)), dim3(kBlock), 0, h->stream,
+                         a->x, a->cyc_z, a->n_col, a->cyc_w, mcyc, a->n_own);
     }
     hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
                        c, a->x, b, h->x, pass);
@@ -11766,11 +11896,14 @@ NX_API int nx_set_preconditioner(nx_network_t* h, int32_t enable, int64_t n_chai
        // the exchange kernels' static LDS on several ranks)
       const int dv = N <= 16 ? 5 : N <= 24 ? 10 : N <= 32 ? 7 : variant;
       const size_t park = 8 * (size_t)(2 * variant_cpl(dv) + 1) * kPcThreads;
-      // (the exchange kernels' budget on one rank too: the rank count may come later)
-      const size_t cap = std::min((size_t)kDirLdsMax, 160 * 1024 - xr_static_lds(dv));
+      // (several ranks: the exchange kernels' static LDS comes on top; the rank count is set
+      // before the preconditioner -- nx_set_halo refuses to run after it)
+      const size_t cap = h->nranks > 1 ? std::min((size_t)kDirLdsMax, 160 * 1024 - xr_static_lds(dv))
+                                       : (size_t)kDirLdsMax;
       h->dstep_park = h->dstep_lds + park <= cap;
       if (h->dstep_park) h->dstep_lds += park;
-      const size_t recs = 8 * (size_t)kRecLds * (kPcThreads / variant_w(dv));
+      const size_t recs = 8 * ((size_t)kRecLds * (kPcThreads / variant_w(dv)) +
+                               2 * (size_t)variant_cpl(dv) * kPcThreads);
       h->dstep_rec = h->dstep_park && h->dstep_lds + recs <= cap;
       if (h->dstep_rec) h->dstep_lds += recs;
     }
@@ -12180,11 +12313,13 @@ NX_API int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64
       !cst)
     return fail(NX_ERR_ARG, "NULL array");
   if (aux->fe || !aux->pc || !aux->cond_mass || aux->N != h->N || aux->E != h->E ||
-      aux->n_cyc > 0 || aux->device != h->device || aux->nranks != h->nranks ||
+      (aux->n_cyc > 0 && (proc_rank(aux) || aux->nranks > 1)) || aux->device != h->device ||
+      aux->nranks != h->nranks ||
       aux->rank != h->rank || proc_rank(aux) != proc_rank(h) || aux->group || h->group)
-    return fail(NX_ERR_STATE, "the auxiliary handle must be a P1/DG0 tree handle of the same "
+    return fail(NX_ERR_STATE, "the auxiliary handle must be a P1/DG0 handle of the same "
                               "ranks with the same N and edges and its cell mass set "
-                              "(nx_set_cell_mass)");
+                              "(nx_set_cell_mass); a graph with cycles (its Woodbury "
+                              "correction, nx_set_cycles) on one rank");
   if (proc_rank(aux) &&
       !(aux->pc_lds && aux->pa.exact && aux->tree_exact && aux->pc_jobs > 0 &&
         aux->pa.n_coarse > 0 && aux->pa.n_coarse <= kCapCoarse))

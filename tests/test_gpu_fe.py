@@ -214,18 +214,54 @@ def test_fe_direct_condensed(case, k, struct, monkeypatch):
     assert np.linalg.norm(got - x2) / np.linalg.norm(x2) <= SOL_TOL
 
 
-def test_fe_direct_cycles_run_minres():
-    """A graph with cycles (the reference's edge-info graph): no condensed direct solve (the
-    Woodbury correction is built from a P1 CSR), MINRES converges to the oracle's answer."""
-    mesh, asm, F, A, b, pbc = _setup("edge_info_N10", (2, 0))
-    assert not asm.fe_direct_available
+def _setup_cyclic(case, km, f=None, R=None):
+    from cases import CYCLIC, p_y
+
+    make, N = CYCLIC[case]
+    mesh = NetworkMesh(make(), N=N)
+    asm = HydraulicNetworkAssembler(mesh, flux_degree=km[0], pressure_degree=km[1])
+    asm.compute_forms(p_bc_ex=p_y, f=f, R=R)
+    src, dst = mesh.edges
+    F = OF.build_problem_fe(mesh.node_coordinates, src, dst, N, *km, mesh.edge_colors)
+    A, b = OF.assemble_reference_fe(F, p_y, f=0.0 if f is None else f,
+                                    R=1.0 if R is None else R)
+    return mesh, asm, F, A, b, p_y
+
+
+@pytest.mark.parametrize("case", ["edge_info_N10", "lattice4x5_N6", "lattice6x6_N3"])
+@pytest.mark.parametrize("k", [2, 3])
+def test_fe_direct_cycles(case, k):
+    """A graph with cycles (the reference's edge-info graph, two lattices with 12 / 25
+    cycles): the (k, 0) direct solve through the condensed system runs -- the auxiliary tree
+    solve corrected by the Woodbury step of the cycle chains' dropped couplings, built from
+    the condensed mass (fe_cyc_build) -- within SOL_TOL of the oracle's LU, its reported
+    residual the true one; new coefficients rebuild the correction."""
+    from cases import CYCLIC
+
+    E = len(CYCLIC[case][0]().edges())
+    R = 1.0 + 0.5 * (np.arange(E) % 3)
+    mesh, asm, F, A, b, pbc = _setup_cyclic(case, (k, 0), f=0.2, R=R)
+    assert asm.fe_direct_available
     solver = Solver(asm)
     solver.assemble()
     sol = solver.solve()
-    assert solver.ksp.solver_used == "minres" and solver.ksp.converged
+    assert solver.ksp.solver_used == "direct" and solver.ksp.converged
+    assert asm.handle.direct_path() == "condensed"
     got = np.concatenate([fn.x.array for fn in sol])
     x_ref = O.solve_reference(A, b)
     assert np.linalg.norm(got - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+    tr = solver.true_residual()
+    assert tr <= 1e-12
+    assert abs(solver.ksp.residual_estimate - tr) <= 1e-6 * tr + 1e-16
+    R2 = 2.0 - 0.25 * (np.arange(E) % 4)
+    asm.compute_forms(p_bc_ex=pbc, f=0.1, R=R2)
+    solver.assemble()
+    sol = solver.solve()
+    assert solver.ksp.solver_used == "direct" and solver.ksp.converged
+    A2, b2 = OF.assemble_reference_fe(F, pbc, f=0.1, R=R2)
+    x2 = O.solve_reference(A2, b2)
+    got = np.concatenate([fn.x.array for fn in sol])
+    assert np.linalg.norm(got - x2) / np.linalg.norm(x2) <= SOL_TOL
 
 
 @pytest.mark.parametrize("case,km", [("depth6_N40", (2, 1)), ("arterial5_N40", (3, 2)),
