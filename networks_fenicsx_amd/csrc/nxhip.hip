@@ -5455,7 +5455,7 @@ __device__ __forceinline__ bool dir_publish_xr(const PcArgs& pa, const DirStep& 
 // part then ends with this rank's coarse partials, the ranks exchange and sum them
 // (xr_allsum), the top part's solver finishes the coarse forest and the top values, and
 // the publisher exchanges the residual's partials and the cut rows' shares the same way.
-template <int W, int CPL, bool XR>
+template <int W, int CPL, bool XR, bool SUP>
 __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& da, int job) {
   extern __shared__ double dsm[];
   __shared__ int sFlag, sTopJob, sIdx;
@@ -5480,10 +5480,14 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   // the job's chains in one pass: the assembly's stores wait until this workgroup has handed
   // over its top inputs (they fill the wait for the top values instead of delaying it), and
   // phase 2 runs on phase 1's registers
-  const bool keep = c1 - c0 <= G;
+  // (SUP: launched only when every job fits one pass, dstep_multi false -- its instantiation
+  // carries no several-pass code)
+  const bool keep = SUP || c1 - c0 <= G;
   // phase 2 by superposition (dir_sup_*: one chain pass; the top solver then stores its own
   // assembly after its phase 2, no helpers)
-  const bool sup = keep && (da.sup & 1) != 0;
+  // (compiled in only where it is launched, CPL <= 2: its code kept beside the plain phase 2
+  // costs the other instantiations registers they do not have)
+  const bool sup = SUP;
   bool sup_s = false;  // this workgroup formed its slots' z_p / H (dir_sup_slots)
 
   // the slots' back-substitution coefficients (phase 1's sA_ / sB_, thread = slot) wait in LDS
@@ -5770,26 +5774,27 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
   NX_DSTAMP(40);
 }
 
-template <int W, int CPL>
+// SUP: phase 2 by superposition (DirStep::sup; instantiated for CPL <= 2, sup_launch)
+template <int W, int CPL, bool SUP = false>
 __global__ __launch_bounds__(kPcThreads) void k_dir_step(PcArgs pa, DirStep da) {
-  dir_step_body<W, CPL, false>(pa, da, blockIdx.x);
+  dir_step_body<W, CPL, false, SUP>(pa, da, blockIdx.x);
 }
 
 // one rank of several, one GPU each (RCCL ranks; the exchange over IPC-mapped peer memory)
-template <int W, int CPL>
+template <int W, int CPL, bool SUP = false>
 __global__ __launch_bounds__(kPcThreads) void k_dir_xr(PcArgs pa, DirStep da) {
-  dir_step_body<W, CPL, true>(pa, da, blockIdx.x);
+  dir_step_body<W, CPL, true, SUP>(pa, da, blockIdx.x);
 }
 
 // every rank of an in-process group in ONE launch (all their workgroups co-resident, so
 // the ranks' exchanges can wait for each other): workgroup -> (rank, job) by goff
-template <int W, int CPL>
+template <int W, int CPL, bool SUP = false>
 __global__ __launch_bounds__(kPcThreads) void k_dir_xg(const PcArgs* __restrict__ pas,
                                                        const DirStep* __restrict__ das,
                                                        const int* __restrict__ goff, int P) {
   int r = 0;
   while (r + 1 < P && (int)blockIdx.x >= goff[r + 1]) ++r;
-  dir_step_body<W, CPL, true>(pas[r], das[r], (int)blockIdx.x - goff[r]);
+  dir_step_body<W, CPL, true, SUP>(pas[r], das[r], (int)blockIdx.x - goff[r]);
 }
 
 // k_dir_team_up: the first half of the several-rank direct step (one rank's share, before
@@ -9490,19 +9495,28 @@ bool dstep_on(const nx_network* h) {
 }
 
 DirStep dir_args(nx_network* h, double rtol);
+template <int CPL>
+bool sup_launch(const DirStep& da);
 template <int W, int CPL>
 void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
   const DirStep da = dir_args(h, rtol);
   static thread_local std::vector<const void*> opted;  // (the dynamic LDS above 64 KiB, once)
-  const void* fn = reinterpret_cast<const void*>(&k_dir_step<W, CPL>);
+  const bool sup = sup_launch<CPL>(da);
+  const void* fn = sup ? reinterpret_cast<const void*>(&k_dir_step<W, CPL, CPL <= 2>)
+                       : reinterpret_cast<const void*>(&k_dir_step<W, CPL>);
   if (std::find(opted.begin(), opted.end(), fn) == opted.end()) {
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kDirLdsMax);
     (void)hipGetLastError();
     opted.push_back(fn);
   }
-  hipExtLaunchKernelGGL((k_dir_step<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
-                        h->stream, prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0,
-                        h->pa, da);
+  if (sup)
+    hipExtLaunchKernelGGL((k_dir_step<W, CPL, CPL <= 2>), dim3(h->pc_jobs), dim3(kPcThreads),
+                          h->dstep_lds, h->stream, prof ? h->dev[0] : nullptr,
+                          prof ? h->dev[1] : nullptr, 0, h->pa, da);
+  else
+    hipExtLaunchKernelGGL((k_dir_step<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
+                          h->stream, prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0,
+                          h->pa, da);
 }
 
 // Several ranks: k_dir_team_up, the assembly + up sweep + top part of one rank (half 0 of
@@ -9978,6 +9992,12 @@ int dir_sup_mode() {
   const char* e = std::getenv("NXHIP_DIR_SUP");
   return e ? std::atoi(e) : 1;
 }
+// the superposition's instantiation runs this launch: asked for (and the park fits) and
+// compiled for this lane shape
+template <int CPL>
+bool sup_launch(const DirStep& da) {
+  return CPL <= 2 && (da.sup & 1) != 0;
+}
 
 DirStep dir_args(nx_network* h, double rtol) {
   h->dq_stale = !h->dstep_multi;
@@ -9991,7 +10011,7 @@ DirStep dir_args(nx_network* h, double rtol) {
 #ifdef NX_PHASE_TIMING
   if (const char* e = std::getenv("NXHIP_LEDGER")) d.ledger = std::atoi(e);
 #endif
-  d.sup = h->dstep_park ? dir_sup_mode() : 0;
+  d.sup = h->dstep_park && !h->dstep_multi ? dir_sup_mode() : 0;
   // (bit 2, the LDS copies: only asked for, and only when they fit -- measured neutral at
   // C3, r06l-r06o: the top solver is not the last workgroup of phase 2 any more)
   if (!h->dstep_rec) d.sup &= ~4;
@@ -10051,20 +10071,36 @@ int launch_xr_wc(const Team& t, double rtol) {
     std::memcpy(hb + bp + bd, goff.data(), bo);
     HIPCALL(hipMemcpyAsync(g->xg_dev, g->xg_host, bp + bd + bo, hipMemcpyHostToDevice, g->stream));
     const char* db = static_cast<const char*>(g->xg_dev);
-    opt_in_lds(reinterpret_cast<const void*>(&k_dir_xg<W, CPL>),
-               (int)(160 * 1024 - xr_static_lds(t.hs[0]->dstep_variant)));
-    hipLaunchKernelGGL((k_dir_xg<W, CPL>), dim3(goff[P]), dim3(kPcThreads), lds, g->stream,
-                       reinterpret_cast<const PcArgs*>(db), reinterpret_cast<const DirStep*>(db + bp),
-                       reinterpret_cast<const int*>(db + bp + bd), P);
+    const int cap = (int)(160 * 1024 - xr_static_lds(t.hs[0]->dstep_variant));
+    if (sup_launch<CPL>(das[0])) {
+      opt_in_lds(reinterpret_cast<const void*>(&k_dir_xg<W, CPL, CPL <= 2>), cap);
+      hipLaunchKernelGGL((k_dir_xg<W, CPL, CPL <= 2>), dim3(goff[P]), dim3(kPcThreads), lds,
+                         g->stream, reinterpret_cast<const PcArgs*>(db),
+                         reinterpret_cast<const DirStep*>(db + bp),
+                         reinterpret_cast<const int*>(db + bp + bd), P);
+    } else {
+      opt_in_lds(reinterpret_cast<const void*>(&k_dir_xg<W, CPL>), cap);
+      hipLaunchKernelGGL((k_dir_xg<W, CPL>), dim3(goff[P]), dim3(kPcThreads), lds, g->stream,
+                         reinterpret_cast<const PcArgs*>(db),
+                         reinterpret_cast<const DirStep*>(db + bp),
+                         reinterpret_cast<const int*>(db + bp + bd), P);
+    }
     HIPCALL(hipStreamSynchronize(g->stream));  // (the pinned staging is rewritten next launch)
   } else {
     nx_network* h = t.hs[0];
-    opt_in_lds(reinterpret_cast<const void*>(&k_dir_xr<W, CPL>),
-               (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
+    const int cap = (int)(160 * 1024 - xr_static_lds(h->dstep_variant));
     const bool prof = h->prof && h->dev[0];  // (events bound to the dispatch: bench.py)
-    hipExtLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
-                          h->stream, prof ? h->dev[0] : nullptr, prof ? h->dev[1] : nullptr, 0,
-                          h->pa, das[0]);
+    if (sup_launch<CPL>(das[0])) {
+      opt_in_lds(reinterpret_cast<const void*>(&k_dir_xr<W, CPL, CPL <= 2>), cap);
+      hipExtLaunchKernelGGL((k_dir_xr<W, CPL, CPL <= 2>), dim3(h->pc_jobs), dim3(kPcThreads),
+                            h->dstep_lds, h->stream, prof ? h->dev[0] : nullptr,
+                            prof ? h->dev[1] : nullptr, 0, h->pa, das[0]);
+    } else {
+      opt_in_lds(reinterpret_cast<const void*>(&k_dir_xr<W, CPL>), cap);
+      hipExtLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads),
+                            h->dstep_lds, h->stream, prof ? h->dev[0] : nullptr,
+                            prof ? h->dev[1] : nullptr, 0, h->pa, das[0]);
+    }
   }
   HIPCALL(hipGetLastError());
   for (int r = 0; r < P; ++r) {
@@ -10091,6 +10127,12 @@ size_t xr_static_lds(int v) {
                    : i == 3 ? reinterpret_cast<const void*>(&k_dir_xr<8, 3>)
                             : reinterpret_cast<const void*>(&k_dir_xr<16, 4>);
     s[i] = hipFuncGetAttributes(&a, fn) == hipSuccess ? a.sharedSizeBytes : 64 * 1024;
+    if (i == 0) {  // (and the superposition's instantiation, the larger of the two)
+      hipFuncAttributes b{};
+      const size_t sb = hipFuncGetAttributes(&b, reinterpret_cast<const void*>(&k_dir_xr<8, 2, true>))
+                                == hipSuccess ? b.sharedSizeBytes : 64 * 1024;
+      s[i] = std::max(s[i], sb);
+    }
   }
   return s[i];
 }
@@ -12771,9 +12813,10 @@ int xr_rehearse_wc(nx_network* h, int P, double rtol, int reps, float* ms_out) {
   hipEvent_t e0, e1;
   HIPCALL(hipEventCreate(&e0));
   HIPCALL(hipEventCreate(&e1));
-  const void* fn = reinterpret_cast<const void*>(&k_dir_xr<W, CPL>);
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
+  for (const void* fn : {reinterpret_cast<const void*>(&k_dir_xr<W, CPL>),
+                         reinterpret_cast<const void*>(&k_dir_xr<W, CPL, CPL <= 2>)})
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(160 * 1024 - xr_static_lds(h->dstep_variant)));
   (void)hipGetLastError();
   float total = 0.f;
   for (int k = 0; k <= reps && rc == NX_OK; ++k) {  // (launch 0: warm-up, not timed)
@@ -12787,8 +12830,12 @@ int xr_rehearse_wc(nx_network* h, int P, double rtol, int reps, float* ms_out) {
     da.xld2 = kXld2;
     da.xK = h->n_cut;
     da.xtag = tag;
-    hipExtLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
-                          h->stream, e0, e1, 0, h->pa, da);
+    if (sup_launch<CPL>(da))
+      hipExtLaunchKernelGGL((k_dir_xr<W, CPL, CPL <= 2>), dim3(h->pc_jobs), dim3(kPcThreads),
+                            h->dstep_lds, h->stream, e0, e1, 0, h->pa, da);
+    else
+      hipExtLaunchKernelGGL((k_dir_xr<W, CPL>), dim3(h->pc_jobs), dim3(kPcThreads), h->dstep_lds,
+                            h->stream, e0, e1, 0, h->pa, da);
     if (hipGetLastError() != hipSuccess) rc = fail(NX_ERR_HIP, "rehearsal launch failed");
     h->dstep_epoch += 1;
     h->seq += 1;
