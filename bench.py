@@ -556,7 +556,8 @@ def run(args, world: int) -> int:
             kb = dstep_bytes(n, nnz, E, N, B, (nnz - E * (7 * N + 1)) // 2)
             ach = kb / (t * 1e-3) / 1e9
             kname = "k_dir_step" if path == "fused" else "k_dir_xr"
-            rocname = f"{kname}<8, 2>"
+            # (round 6: phase 2 by superposition is its own instantiation, <8, 2, true>)
+            rocname = f"{kname}<8, 2{', true' if h.direct_sup() else ''}>"
             traffic, tsrc, rocprof_ns = (pmc_traffic(rocname) if default_workload
                                          else (None, None, None))
             k = {"avg_launch_ms": t, "algorithmic_bytes_per_launch": kb, "achieved_GBs": ach,

@@ -459,6 +459,10 @@ int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left);
  * 0 for the separate launches (assembly, up sweep, down sweep, publish). Replaces nothing
  * in the reference (PETSc's KSPSolve is one call: solver.py:127). */
 int nx_get_direct_path(nx_network_t* h, int32_t* path);
+/* Whether the last fused or exchange step (path 1 or 3) ran phase 2 by superposition
+ * (*sup = 1: the instantiation k_dir_step / k_dir_xr <W, CPL, true>, NXHIP_DIR_SUP; 0: the
+ * plain phase 2). Replaces nothing in the reference (its profiling names). */
+int nx_get_direct_sup(nx_network_t* h, int32_t* sup);
 /* (path 2: the (k, 0) condensed route of nx_fe_set_direct; path 4: the continuous-pressure
  * node-condensed route of nx_fe_set_cp; path 3: several ranks, the
  * exchange step k_dir_xr / k_dir_xg, one launch per rank.)

@@ -69,6 +69,7 @@ _SIGS = {
     "nx_get_profile_direct": (C.c_int, [_h, _pd, _pi64]),
     "nx_get_direct_info": (C.c_int, [_h, _pi32, _pi32]),
     "nx_get_direct_path": (C.c_int, [_h, _pi32]),
+    "nx_get_direct_sup": (C.c_int, [_h, _pi32]),
     "nx_debug_set_wait_polls": (C.c_int, [_h, C.c_uint32]),
     "nx_debug_xr_rehearse": (C.c_int, [_h, _f64, _i32, _pd]),
     "nx_reset_profile": (C.c_int, [_h]),
@@ -172,6 +173,29 @@ def lib():
     return _lib
 
 
+_FAST = None  # the _nxfast extension bound to lib()'s entry points, or False (ctypes)
+
+
+def _fast():
+    """The ``_nxfast`` extension (csrc/nxfast.c) bound to this library's ``nx_assemble`` /
+    ``nx_solve``; None when it is not built (then ctypes makes the calls) or
+    ``NXHIP_CTYPES=1``."""
+    global _FAST
+    if _FAST is None:
+        _FAST = False
+        if os.environ.get("NXHIP_CTYPES", "0") == "0":
+            try:
+                from . import _nxfast  # type: ignore[attr-defined]
+
+                L = lib()
+                _nxfast.bind(C.cast(L.nx_assemble, C.c_void_p).value,
+                             C.cast(L.nx_solve, C.c_void_p).value)
+                _FAST = _nxfast
+            except ImportError:
+                pass
+    return _FAST or None
+
+
 def check(rc: int) -> None:
     if rc != NX_OK:
         msg = lib().nx_last_error().decode(errors="replace")
@@ -266,6 +290,7 @@ class Handle:
 
     # ------------------------------------------------------------------ lifecycle
     def close(self) -> None:
+        self.__dict__.pop("_addr_v", None)
         if getattr(self, "_h", None):
             lib().nx_destroy(self._h)
             self._h = None
@@ -300,11 +325,21 @@ class Handle:
         check(lib().nx_set_source(self.ptr, _ptr(ef, C.c_double)))
 
     def assemble(self, lhs: bool = True, rhs: bool = True) -> None:
-        rc = lib().nx_assemble(self.ptr, 1 if lhs else 0, 1 if rhs else 0)
+        fast = _fast()
+        if fast is not None:  # (the per-step calls without ctypes: csrc/nxfast.c)
+            rc = fast.assemble(self._addr, 1 if lhs else 0, 1 if rhs else 0)
+        else:
+            rc = lib().nx_assemble(self.ptr, 1 if lhs else 0, 1 if rhs else 0)
         if rc != NX_OK:
             check(rc)
 
     def solve(self, rtol: float, maxit: int, check_every: int = 4):
+        fast = _fast()
+        if fast is not None:
+            rc, it, rr, conv = fast.solve(self._addr, float(rtol), int(maxit), int(check_every))
+            if rc != NX_OK:
+                check(rc)
+            return it, rr, conv
         # out-parameters allocated once per handle: this call sits in every step's host path
         out = self.__dict__.get("_solve_out")
         if out is None:
@@ -315,6 +350,18 @@ class Handle:
             check(rc)
         it, rr, conv = out[0]
         return int(it.value), float(rr.value), bool(conv.value)
+
+    @property
+    def _addr(self) -> int:
+        # (the handle's address for _nxfast, cached until close(); a closed handle fails
+        # loudly, as the ctypes path does)
+        a = self.__dict__.get("_addr_v")
+        if a is None:
+            h = self._h
+            if not h:
+                raise NxError("handle is closed")
+            a = self._addr_v = int(C.cast(h, C.c_void_p).value or 0)
+        return a
 
     def solution(self) -> np.ndarray:
         x = np.empty(self.n_rows, dtype=np.float64)
@@ -403,6 +450,13 @@ class Handle:
         n, per = C.c_int32(0), C.c_int32(0)
         check(lib().nx_fe_templates(self.ptr, C.byref(n), C.byref(per)))
         return int(n.value), int(per.value)
+
+    def direct_sup(self) -> bool:
+        """Whether the last one-launch step ran phase 2 by superposition
+        (nx_get_direct_sup)."""
+        v = C.c_int32(0)
+        check(lib().nx_get_direct_sup(self.ptr, C.byref(v)))
+        return bool(v.value)
 
     def direct_path(self) -> str:
         """What the last direct solve ran (nx_get_direct_path): ``"fused"`` (k_dir_step, one

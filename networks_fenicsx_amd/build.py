@@ -33,11 +33,38 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in (SRC, HEADER))
 
 
+FAST_SRC = HERE / "csrc" / "nxfast.c"
+
+
+def build_fast(force: bool = False) -> Path | None:
+    """The CPython extension ``_nxfast`` (the per-step ``nx_assemble`` / ``nx_solve`` calls
+    without ctypes; host plumbing, see csrc/nxfast.c), in-tree next to ``libnxhip.so``.
+    Returns None when no C compiler or Python headers are available (ctypes is used)."""
+    import sysconfig
+
+    out = HERE / ("_nxfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    if not force and out.exists() and out.stat().st_mtime >= FAST_SRC.stat().st_mtime:
+        return out
+    cc = shutil.which("gcc") or shutil.which("cc")
+    inc = sysconfig.get_paths().get("include")
+    if not cc or not inc or not (Path(inc) / "Python.h").exists():
+        return None
+    tmp = out.with_suffix(".tmp")
+    res = subprocess.run([cc, "-O2", "-shared", "-fPIC", "-Wall", f"-I{inc}", "-o", str(tmp),
+                          str(FAST_SRC)], capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"building _nxfast failed:\n{res.stderr}")
+    os.replace(tmp, out)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False, phase_timing: bool = False) -> Path:
     """Compile ``csrc/nxhip.hip`` into ``libnxhip.so`` (skipped when up to date).
     ``phase_timing`` builds the instrumented debug variant ``libnxhip_phase.so`` instead
     (``-DNX_PHASE_TIMING``; scripts/phase_timing.py loads it via ``NXHIP_LIB``)."""
     out = HERE / "libnxhip_phase.so" if phase_timing else LIB
+    if not phase_timing:
+        build_fast(force)
     if not phase_timing and not force and not needs_build():
         return LIB
     tmp = out.with_suffix(".so.tmp")

@@ -5574,11 +5574,6 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
       if constexpr (XR) coarse_idx_load(pa, ci);
       top_pre_val<true>(pa, nullptr, pre);
       if constexpr (XR) coarse_idx_val(pa, ci);
-      if (sup) {  // its slots' z_p / H while the inputs come (they queue behind the stores)
-        dir_sup_slots<W, CPL>(pa, sup_lds, S);
-        if (sup_wslots(S)) dir_sup_core_wave0<W, CPL>(pa, L, lane_on, park);
-        sup_s = true;
-      }
       NX_DSTAMP(6);
       if constexpr (XR) {
         // the rank's top part up to its coarse partials [D | J | G] (pc_coarse_partials: in
@@ -5618,6 +5613,12 @@ __device__ __forceinline__ void dir_step_body(const PcArgs& pa, const DirStep& d
         } else {
           chain_rec_load(da, fresh_chain<W>(c0), lane_on, rec);
           dir_chain_asm_rec<W, CPL>(pa, rec, lane_on, L);
+        }
+        if (sup) {  // its slots' z_p / H and wave 0's chains' part now (not before the top
+                    // part: on its own path either way, and there it delayed the top values)
+          dir_sup_slots<W, CPL>(pa, sup_lds, S);
+          if (sup_wslots(S)) dir_sup_core_wave0<W, CPL>(pa, L, lane_on, park);
+          sup_s = true;
         }
       }
     } else {
@@ -6981,6 +6982,7 @@ struct nx_network {
   size_t dstep_lds = 0;  // dynamic LDS bytes per workgroup
   bool dstep_park = false;  // dstep_lds holds the superposition's park (DirStep::sup)
   bool dstep_rec = false;   // and the chain records' copy (sup & 4)
+  bool last_sup = false;    // the last one-launch step ran the superposition instantiation
   unsigned* d_tsync = nullptr;  // k_dir_team_up's arrival counter (several ranks; pc_bufs)
   bool need_r = false;     // the last pass kept no residual: a refinement step forms it first
   int last_dir_path = 0;   // the last direct solve: 0 four launches, 1 k_dir_step
@@ -9502,6 +9504,7 @@ void launch_dstep_wc(nx_network* h, double rtol, bool prof) {
   const DirStep da = dir_args(h, rtol);
   static thread_local std::vector<const void*> opted;  // (the dynamic LDS above 64 KiB, once)
   const bool sup = sup_launch<CPL>(da);
+  h->last_sup = sup;
   const void* fn = sup ? reinterpret_cast<const void*>(&k_dir_step<W, CPL, CPL <= 2>)
                        : reinterpret_cast<const void*>(&k_dir_step<W, CPL>);
   if (std::find(opted.begin(), opted.end(), fn) == opted.end()) {
@@ -10072,6 +10075,7 @@ int launch_xr_wc(const Team& t, double rtol) {
     HIPCALL(hipMemcpyAsync(g->xg_dev, g->xg_host, bp + bd + bo, hipMemcpyHostToDevice, g->stream));
     const char* db = static_cast<const char*>(g->xg_dev);
     const int cap = (int)(160 * 1024 - xr_static_lds(t.hs[0]->dstep_variant));
+    for (int r = 0; r < P; ++r) t.hs[r]->last_sup = sup_launch<CPL>(das[0]);
     if (sup_launch<CPL>(das[0])) {
       opt_in_lds(reinterpret_cast<const void*>(&k_dir_xg<W, CPL, CPL <= 2>), cap);
       hipLaunchKernelGGL((k_dir_xg<W, CPL, CPL <= 2>), dim3(goff[P]), dim3(kPcThreads), lds,
@@ -10090,6 +10094,7 @@ int launch_xr_wc(const Team& t, double rtol) {
     nx_network* h = t.hs[0];
     const int cap = (int)(160 * 1024 - xr_static_lds(h->dstep_variant));
     const bool prof = h->prof && h->dev[0];  // (events bound to the dispatch: bench.py)
+    h->last_sup = sup_launch<CPL>(das[0]);
     if (sup_launch<CPL>(das[0])) {
       opt_in_lds(reinterpret_cast<const void*>(&k_dir_xr<W, CPL, CPL <= 2>), cap);
       hipExtLaunchKernelGGL((k_dir_xr<W, CPL, CPL <= 2>), dim3(h->pc_jobs), dim3(kPcThreads),
@@ -11292,6 +11297,12 @@ NX_API int nx_get_direct_info(nx_network_t* h, int32_t* fused, int32_t* n_left) 
 NX_API int nx_get_direct_path(nx_network_t* h, int32_t* path) {
   if (!h || !path) return fail(NX_ERR_ARG, "null argument");
   *path = h->last_dir_path;
+  return NX_OK;
+}
+
+NX_API int nx_get_direct_sup(nx_network_t* h, int32_t* sup) {
+  if (!h || !sup) return fail(NX_ERR_ARG, "null argument");
+  *sup = h->last_sup ? 1 : 0;
   return NX_OK;
 }
 
