@@ -115,7 +115,7 @@ _SIGS = {
     "nx_group_destroy": (C.c_int, [_h]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
-MAX_CYCLES = 128  # kMaxCyc of csrc/nxhip.hip: cycle-closing chains the direct solve corrects
+MAX_CYCLES = 2048  # kMaxCyc of csrc/nxhip.hip: cycle-closing chains the direct solve corrects
 
 
 class NxError(RuntimeError):

@@ -6534,7 +6534,9 @@ __global__ void k_dir_publish_red(const double* __restrict__ rb, double rtol, in
 //   A^{-1} b = x_g - Z Cinv U^T x_g,  x_g = A_g^{-1} b,  Z = A_g^{-1} U,
 //   Cinv = (C^{-1} + U^T Z)^{-1}                                   (Woodbury),
 // with Z (m columns) and Cinv built once per assembled matrix (cyc_build).
-constexpr int kMaxCyc = 128;  // cycle-closing chains (m = 2 kMaxCyc columns)
+// cycle-closing chains (m = 2 kMaxCyc columns; round 6: the capacitance matrix is inverted on
+// the device, cyc_invert, and the correction's kernels hold U^T x in dynamic LDS -- was 128)
+constexpr int kMaxCyc = 2048;
 
 // The m x m matrix U^T Z and the couplings a (row q of the CSR, column lam).
 __global__ __launch_bounds__(256) void k_cyc_cap(Csr A, const double* __restrict__ Z, int64_t ldz,
@@ -6555,23 +6557,25 @@ __global__ __launch_bounds__(256) void k_cyc_cap(Csr A, const double* __restrict
 
 // w = Cinv (U^T x - prev) (prev: U^T x before a refinement pass added its correction, or
 // null); save: U^T x is stored there instead (before a refinement pass). One workgroup.
+// Cinv is stored transposed (cinvT[j m + i] = Cinv[i][j]: a row per thread, coalesced); one
+// row of w per thread over ceil(m / 256) blocks (cyc_w_launch), U^T x in dynamic LDS (m doubles).
 __global__ __launch_bounds__(256) void k_cyc_w(const double* __restrict__ x, const int* __restrict__ rows,
-                                               int m, const double* __restrict__ cinv,
+                                               int m, const double* __restrict__ cinvT,
                                                const double* __restrict__ prev, double* __restrict__ w,
                                                double* __restrict__ save) {
-  __shared__ double g[2 * kMaxCyc];
+  extern __shared__ double g[];
   for (int i = threadIdx.x; i < m; i += 256) {
     const double v = x[rows[i]];
-    if (save) save[i] = v;
+    if (save && blockIdx.x == 0) save[i] = v;
     g[i] = prev ? v - prev[i] : v;
   }
   if (save) return;
   __syncthreads();
-  for (int i = threadIdx.x; i < m; i += 256) {
-    double s = 0.0;
-    for (int j = 0; j < m; ++j) s += cinv[(int64_t)i * m + j] * g[j];
-    w[i] = s;
-  }
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= m) return;
+  double s = 0.0;
+  for (int j = 0; j < m; ++j) s += cinvT[(int64_t)j * m + i] * g[j];
+  w[i] = s;
 }
 
 // x -= Z w, one row per thread (the m columns in order).
@@ -6627,16 +6631,108 @@ __global__ __launch_bounds__(256) void k_cyc_cap_team(Csr A, const double* __res
 
 // w = Cinv (u - prev) from the summed u (prev: U^T x before a refinement pass, or null).
 __global__ __launch_bounds__(256) void k_cyc_w_team(const double* __restrict__ u, int m,
-                                                    const double* __restrict__ cinv,
+                                                    const double* __restrict__ cinvT,
                                                     const double* __restrict__ prev,
                                                     double* __restrict__ w) {
-  __shared__ double g[2 * kMaxCyc];
+  extern __shared__ double g[];
   for (int i = threadIdx.x; i < m; i += 256) g[i] = prev ? u[i] - prev[i] : u[i];
   __syncthreads();
-  for (int i = threadIdx.x; i < m; i += 256) {
-    double s = 0.0;
-    for (int j = 0; j < m; ++j) s += cinv[(int64_t)i * m + j] * g[j];
-    w[i] = s;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= m) return;
+  double s = 0.0;
+  for (int j = 0; j < m; ++j) s += cinvT[(int64_t)j * m + i] * g[j];
+  w[i] = s;
+}
+
+// ---- the capacitance matrix's inverse on the device (cyc_invert): Gauss-Jordan with partial
+// pivoting on [A | I] (row-major, m x 2m), one column per pair of launches -- the pivot row
+// found, swapped in and normalised by one workgroup, then every other row eliminated by a
+// workgroup each -- the same operations in the same order on every rank (the same bits).
+// A = U^T Z + C^{-1}: C^{-1} of the coupling blocks [[0, a], [a, 0]] is [[0, 1/a], [1/a, 0]].
+__global__ __launch_bounds__(256) void k_gj_init(const double* __restrict__ cap, int m,
+                                                 double* __restrict__ aug, int* __restrict__ bad) {
+  const int64_t n = (int64_t)m * 2 * m;
+  for (int64_t t = blockIdx.x * (int64_t)256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int r = (int)(t / (2 * m)), c = (int)(t % (2 * m));
+    double v;
+    if (c < m) {
+      v = cap[(int64_t)r * m + c];
+      if ((r >> 1) == (c >> 1) && r != c) {  // the coupling pair's off-diagonal
+        const double a = cap[(int64_t)m * m + (r >> 1)];
+        if (a == 0.0) *bad = 1;  // (no coupling at a grounded end: cyc_invert fails)
+        v += 1.0 / a;
+      }
+    } else {
+      v = c - m == r ? 1.0 : 0.0;
+    }
+    aug[t] = v;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_gj_pivot(double* __restrict__ aug, int m, int col,
+                                                   int* __restrict__ bad) {
+  __shared__ double sv[1024];
+  __shared__ int si[1024];
+  const int w = 2 * m;
+  double best = -1.0;
+  int bi = col;
+  for (int r = col + threadIdx.x; r < m; r += 1024) {
+    const double v = fabs(aug[(int64_t)r * w + col]);
+    if (v > best) {  // (strictly: the first row of the largest magnitude in this thread)
+      best = v;
+      bi = r;
+    }
+  }
+  sv[threadIdx.x] = best;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const double a = sv[threadIdx.x], b = sv[threadIdx.x + o];
+      const int ia = si[threadIdx.x], ib = si[threadIdx.x + o];
+      if (b > a || (b == a && ib < ia)) {  // ties: the smaller row, as a serial scan
+        sv[threadIdx.x] = b;
+        si[threadIdx.x] = ib;
+      }
+    }
+    __syncthreads();
+  }
+  const int p = si[0];
+  if (!(sv[0] > 0.0)) {
+    if (threadIdx.x == 0) *bad = 2;
+    return;
+  }
+  if (p != col)
+    for (int c = threadIdx.x; c < w; c += 1024) {
+      const double t = aug[(int64_t)col * w + c];
+      aug[(int64_t)col * w + c] = aug[(int64_t)p * w + c];
+      aug[(int64_t)p * w + c] = t;
+    }
+  __syncthreads();
+  const double d = 1.0 / aug[(int64_t)col * w + col];
+  __syncthreads();  // (every thread holds the pivot before row col changes)
+  for (int c = threadIdx.x; c < w; c += 1024) aug[(int64_t)col * w + c] *= d;
+}
+
+__global__ __launch_bounds__(256) void k_gj_elim(double* __restrict__ aug, int m, int col) {
+  const int r = blockIdx.x;
+  if (r == col) return;
+  const int w = 2 * m;
+  const double f = aug[(int64_t)r * w + col];
+  if (f == 0.0) return;
+  __syncthreads();  // (f read by every thread before column col of this row changes)
+  const double* __restrict__ pr = aug + (int64_t)col * w;
+  double* __restrict__ rr = aug + (int64_t)r * w;
+  for (int c = threadIdx.x; c < w; c += 256) rr[c] -= f * pr[c];
+}
+
+// cinvT[j m + i] = inverse[i][j] (the right half of the reduced [I | A^{-1}])
+__global__ __launch_bounds__(256) void k_gj_out(const double* __restrict__ aug, int m,
+                                                double* __restrict__ cinvT) {
+  const int64_t n = (int64_t)m * m;
+  for (int64_t t = blockIdx.x * (int64_t)256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int j = (int)(t / m), i = (int)(t % m);
+    cinvT[t] = aug[(int64_t)i * 2 * m + m + j];
   }
 }
 
@@ -6966,6 +7062,7 @@ struct nx_network {
   int xr_nleft = 0;
   void* xmb = nullptr;
   XPeer* d_xpeers = nullptr;
+  std::vector<XPeer> xpeers_host;  // the same table on the host
   std::vector<void*> xr_opened;  // peers' mailboxes opened by IPC (closed on destroy)
   bool xr_linked = false;        // the peer table is set (group create / nx_xch_import)
   bool xr_off = false;           // the ranks agreed to leave it (xr_agree): the graph path
@@ -6996,6 +7093,7 @@ struct nx_network {
   double* cyc_z = nullptr;
   double* cyc_cinv = nullptr;
   double* cyc_cap = nullptr;   // m x m, then m / 2 couplings
+  double* cyc_gj = nullptr;    // cyc_invert's [A | I] (2 m^2) and its status word
   double* cyc_prev = nullptr;  // m
   double* cyc_w = nullptr;     // m
   bool cyc_raw = false;        // cyc_build's solves: the tree solve alone
@@ -9447,7 +9545,7 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   const bool cyc = h->n_cyc > 0 && !h->cyc_raw;  // graphs with cycles: Woodbury after the sweeps
   const int m = 2 * h->n_cyc;
   if (cyc && refine)  // U^T x before the sweeps add the tree solve's correction
-    hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
+    hipLaunchKernelGGL(k_cyc_w, dim3(grid_of(m, 256)), dim3(256), sizeof(double) * m, h->stream, h->x, h->d_cyc_rows, m,
                        h->cyc_cinv, nullptr, h->cyc_w, h->cyc_prev);
   {  // the LDS sweeps in mode kModeDirect (direct_local: pc_lds)
     h->pa.accum = refine ? 1 : 0;  // refinement: the sweeps add the correction to x
@@ -9472,7 +9570,7 @@ void launch_direct_wc(nx_network* h, double rtol, int refine, bool prof) {
   }
   if (h->cond_mass) return;  // an auxiliary solve: the (k, 0) handle checks its own residual
   if (cyc) {  // x -= Z Cinv U^T (x - x_before): the couplings the tree solve dropped
-    hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, h->x, h->d_cyc_rows, m,
+    hipLaunchKernelGGL(k_cyc_w, dim3(grid_of(m, 256)), dim3(256), sizeof(double) * m, h->stream, h->x, h->d_cyc_rows, m,
                        h->cyc_cinv, refine ? h->cyc_prev : nullptr, h->cyc_w, nullptr);
     hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
                        h->x, h->cyc_z, h->n_col, h->cyc_w, m, h->n_own);
@@ -9590,50 +9688,29 @@ int launch_direct(nx_network* h, double rtol, int refine, bool prof = false) {
   return NX_OK;
 }
 
-// Cinv = (C^{-1} + U^T Z)^{-1} on the host from cyc_cap (m x m U^T Z, then the m / 2
-// couplings a: C^{-1} of [[0, a], [a, 0]] is [[0, 1/a], [1/a, 0]]), Gauss-Jordan with
-// partial pivoting; the same on every rank of a team (the same summed inputs).
+// Cinv = (C^{-1} + U^T Z)^{-1} from cyc_cap (m x m U^T Z, then the m / 2 couplings a) on the
+// device: Gauss-Jordan with partial pivoting (k_gj_*), 2 m launches on the handle's stream,
+// stored transposed for the correction's kernels; the same on every rank of a team (the same
+// summed inputs, the same operations). One host sync: a zero coupling or pivot fails loudly.
 int cyc_invert(nx_network* h) {
   const int m = 2 * h->n_cyc;
-  std::vector<double> cap((size_t)m * m + m / 2);
-  HIPCALL(hipMemcpyAsync(cap.data(), h->cyc_cap, sizeof(double) * cap.size(),
-                         hipMemcpyDeviceToHost, h->stream));
-  HIPCALL(hipStreamSynchronize(h->stream));
-  // C^{-1} + U^T Z; C^{-1} of [[0, a], [a, 0]] is [[0, 1/a], [1/a, 0]]
-  std::vector<double> a(cap.begin(), cap.begin() + (int64_t)m * m), inv((size_t)m * m, 0.0);
-  for (int k = 0; k < m / 2; ++k) {
-    const double c = cap[(size_t)m * m + k];
-    if (c == 0.0) return fail(NX_ERR_STATE, "cycle chain: no coupling at its grounded end");
-    a[(size_t)(2 * k) * m + 2 * k + 1] += 1.0 / c;
-    a[(size_t)(2 * k + 1) * m + 2 * k] += 1.0 / c;
-  }
-  for (int i = 0; i < m; ++i) inv[(size_t)i * m + i] = 1.0;
+  if (!h->cyc_gj) HIPCALL(hipMalloc((void**)&h->cyc_gj, sizeof(double) * 2 * (size_t)m * m + 8));
+  int* bad = reinterpret_cast<int*>(h->cyc_gj + 2 * (size_t)m * m);
+  HIPCALL(hipMemsetAsync(bad, 0, sizeof(int), h->stream));
+  const int gb = std::min(4096, grid_of(2 * (int64_t)m * m, 256));
+  hipLaunchKernelGGL(k_gj_init, dim3(gb), dim3(256), 0, h->stream, h->cyc_cap, m, h->cyc_gj, bad);
   for (int col = 0; col < m; ++col) {
-    int piv = col;
-    for (int r = col + 1; r < m; ++r)
-      if (std::fabs(a[(size_t)r * m + col]) > std::fabs(a[(size_t)piv * m + col])) piv = r;
-    if (a[(size_t)piv * m + col] == 0.0) return fail(NX_ERR_STATE, "cycle correction is singular");
-    if (piv != col)
-      for (int k = 0; k < m; ++k) {
-        std::swap(a[(size_t)piv * m + k], a[(size_t)col * m + k]);
-        std::swap(inv[(size_t)piv * m + k], inv[(size_t)col * m + k]);
-      }
-    const double d = 1.0 / a[(size_t)col * m + col];
-    for (int k = 0; k < m; ++k) {
-      a[(size_t)col * m + k] *= d;
-      inv[(size_t)col * m + k] *= d;
-    }
-    for (int r = 0; r < m; ++r) {
-      if (r == col) continue;
-      const double f = a[(size_t)r * m + col];
-      if (f == 0.0) continue;
-      for (int k = 0; k < m; ++k) {
-        a[(size_t)r * m + k] -= f * a[(size_t)col * m + k];
-        inv[(size_t)r * m + k] -= f * inv[(size_t)col * m + k];
-      }
-    }
+    hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(1024), 0, h->stream, h->cyc_gj, m, col, bad);
+    hipLaunchKernelGGL(k_gj_elim, dim3(m), dim3(256), 0, h->stream, h->cyc_gj, m, col);
   }
-  HIPCALL(hipMemcpy(h->cyc_cinv, inv.data(), sizeof(double) * inv.size(), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_gj_out, dim3(std::min(4096, grid_of((int64_t)m * m, 256))), dim3(256), 0,
+                     h->stream, h->cyc_gj, m, h->cyc_cinv);
+  HIPCALL(hipGetLastError());
+  int b = 0;
+  HIPCALL(hipMemcpyAsync(&b, bad, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCALL(hipStreamSynchronize(h->stream));
+  if (b == 1) return fail(NX_ERR_STATE, "cycle chain: no coupling at its grounded end");
+  if (b == 2) return fail(NX_ERR_STATE, "cycle correction is singular");
   return NX_OK;
 }
 
@@ -9825,7 +9902,7 @@ int cyc_fix_team(const Team& t, double rtol, bool refine) {
   CHECK(cyc_gather_team(t, false));
   for (int r = 0; r < t.P; ++r) {
     nx_network* h = t.hs[r];
-    hipLaunchKernelGGL(k_cyc_w_team, dim3(1), dim3(256), 0, h->stream, h->cyc_u, m, h->cyc_cinv,
+    hipLaunchKernelGGL(k_cyc_w_team, dim3(grid_of(m, 256)), dim3(256), sizeof(double) * m, h->stream, h->cyc_u, m, h->cyc_cinv,
                        refine ? h->cyc_prev : nullptr, h->cyc_w);
     hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(h->n_own, kBlock)), dim3(kBlock), 0, h->stream,
                        h->x, h->cyc_z, h->n_col, h->cyc_w, m, h->n_own);
@@ -9947,6 +10024,7 @@ void xr_free(nx_network* h) {
 }
 int xr_link(nx_network* h, const std::vector<XPeer>& peers) {
   HIPCALL(hipMemcpy(h->d_xpeers, peers.data(), sizeof(XPeer) * peers.size(), hipMemcpyHostToDevice));
+  h->xpeers_host = peers;  // (xr_settle posts an abort word from the host through them)
   h->xr_linked = true;
   h->sched_checked = false;  // (the ranks agree on the exchange in check_schedules)
   return NX_OK;
@@ -10158,6 +10236,17 @@ int xr_settle(nx_network* h, bool* published) {
   unsigned sy[8];
   HIPCALL(hipMemcpy(sy, h->d_dsync, sizeof(sy), hipMemcpyDeviceToHost));
   h->xr_why = sy[5] ? sy[5] : (kXrFail1 | kXrFailLocal);
+  if (!sy[5] && (int)h->xpeers_host.size() == h->nranks) {
+    // no workgroup recorded a reason, so none wrote this launch's abort word either (the
+    // advisor's r05 finding): post it from here, or a peer past exchange 1 would wait out
+    // xr_host_finish's bound for this rank's exchange-2 share
+    const unsigned long long w = ((unsigned long long)h->xr_why << 32) | h->xtag;
+    for (int q = 0; q < h->nranks; ++q)
+      if (q != h->rank)
+        HIPCALL(hipMemcpy(reinterpret_cast<unsigned long long*>(h->xpeers_host[q].fl +
+                                                                2 * h->nranks) + h->rank,
+                          &w, sizeof(w), hipMemcpyHostToDevice));
+  }
   HIPCALL(hipMemset(h->d_dsync, 0, 8 * sizeof(unsigned)));
   HIPCALL(hipMemcpy(&h->seq, h->d_seq, sizeof(int), hipMemcpyDeviceToHost));
   h->dstep_epoch = 0;
@@ -10751,7 +10840,7 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
       CHECK(rc);
     }
     if (mcyc) {  // x_aux -= Z Cinv U^T x_aux: the couplings the tree solve dropped
-      hipLaunchKernelGGL(k_cyc_w, dim3(1), dim3(256), 0, h->stream, a->x, a->d_cyc_rows, mcyc,
+      hipLaunchKernelGGL(k_cyc_w, dim3(grid_of(mcyc, 256)), dim3(256), sizeof(double) * mcyc, h->stream, a->x, a->d_cyc_rows, mcyc,
                          a->cyc_cinv, nullptr, a->cyc_w, nullptr);
       hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(a->n_own, kBlock)), dim3(kBlock), 0, h->stream,
                          a->x, a->cyc_z, a->n_col, a->cyc_w, mcyc, a->n_own);
@@ -12082,8 +12171,9 @@ namespace {
 void free_cycles(nx_network* h) {
   for (void* p : {(void*)h->d_cyc_rows, (void*)h->cyc_z, (void*)h->cyc_cinv, (void*)h->cyc_cap,
                   (void*)h->cyc_prev, (void*)h->cyc_w, (void*)h->d_cyc_qloc, (void*)h->d_cyc_lcol,
-                  (void*)h->cyc_u})
+                  (void*)h->cyc_u, (void*)h->cyc_gj})
     if (p) (void)hipFree(p);
+  h->cyc_gj = nullptr;
   h->d_cyc_rows = h->d_cyc_qloc = h->d_cyc_lcol = nullptr;
   h->cyc_z = h->cyc_cinv = h->cyc_cap = h->cyc_prev = h->cyc_w = h->cyc_u = nullptr;
   h->cyc_team = false;
@@ -12268,6 +12358,16 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
       return fail(NX_ERR_ARG, "continuous pressure: edge tables out of range");
   if (lev_off[0] != 0 || lev_off[n_lev] != n || inc_off[0] != 0 || child_off[0] != 0)
     return fail(NX_ERR_ARG, "continuous pressure: offsets");
+  // (the host's record builder and the kernels index through these: monotone, and within
+  // what the tables can hold -- an edge has two ends, a node at most one parent)
+  for (int64_t i = 0; i < n_lev; ++i)
+    if (lev_off[i + 1] < lev_off[i]) return fail(NX_ERR_ARG, "continuous pressure: level offsets");
+  for (int64_t i = 0; i < n; ++i)
+    if (inc_off[i + 1] < inc_off[i] || child_off[i + 1] < child_off[i] || parent[3 * i + 2] < -1 ||
+        parent[3 * i + 2] > 1)
+      return fail(NX_ERR_ARG, "continuous pressure: offsets / parent end");
+  if (inc_off[n] > 2 * Es || child_off[n] > n)
+    return fail(NX_ERR_ARG, "continuous pressure: more incidences or children than the graph has");
   for (int64_t i = 0; i < n; ++i)
     if (order[i] < 0 || order[i] >= n) return fail(NX_ERR_ARG, "continuous pressure: order");
   for (int64_t j = 0; j < inc_off[n]; ++j)

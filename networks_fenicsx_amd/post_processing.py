@@ -15,6 +15,8 @@ Mirrors ``src/networks_fenicsx/post_processing.py``:
 
 from __future__ import annotations
 
+import base64
+
 from pathlib import Path
 
 import numpy as np
@@ -74,6 +76,14 @@ def write_vtu(path: Path | str, pts: np.ndarray, cell_type: int, point_data: dic
 
     def arr(name, a, ncomp=1, kind="Float64"):
         a = np.asarray(a).ravel()
+        if kind == "Float64" and not np.all(np.isfinite(a)):
+            # (VTK's ASCII reader cannot parse 'nan' -- e.g. a node value another rank
+            # owns: inline binary, base64 of a UInt32 byte count then the little-endian
+            # doubles, which carries NaN as such)
+            raw = np.ascontiguousarray(a, dtype="<f8").tobytes()
+            body = base64.b64encode(np.uint32(len(raw)).astype("<u4").tobytes() + raw).decode()
+            return (f'<DataArray type="Float64" Name="{name}" NumberOfComponents="{ncomp}" '
+                    f'format="binary">{body}</DataArray>')
         body = " ".join(repr(float(v)) if kind == "Float64" else str(int(v)) for v in a)
         return (f'<DataArray type="{kind}" Name="{name}" NumberOfComponents="{ncomp}" '
                 f'format="ascii">{body}</DataArray>')
@@ -158,18 +168,23 @@ def _export_vtu(fn: Function, path: Path) -> None:
 
 def export_functions(functions: list[Function], outpath: Path | str) -> None:
     """Write ``flux_{i}``, ``pressure`` and ``lm`` as ``.vtu`` (in place of the reference's
-    ``.bp``) and their raw arrays as ``.npz``."""
+    ``.bp``) and their raw arrays as ``.npz``. On several ranks every rank writes its own
+    piece, ``<name>_r{rank}`` (the reference writes one collective file; ranks must not
+    overwrite each other's)."""
     out = Path(outpath)
     out.mkdir(parents=True, exist_ok=True)
+    comm = getattr(functions[-1].function_space.mesh, "comm", None)
+    size = int(getattr(comm, "size", 1) or 1)
+    sfx = f"_r{int(comm.rank)}" if size > 1 else ""
     for i, q in enumerate(functions[:-2]):
-        _export_vtu(q, out / f"flux_{i}.vtu")
-    _export_vtu(functions[-2], out / "pressure.vtu")
-    _export_vtu(functions[-1], out / "lm.vtu")
+        _export_vtu(q, out / f"flux_{i}{sfx}.vtu")
+    _export_vtu(functions[-2], out / f"pressure{sfx}.vtu")
+    _export_vtu(functions[-1], out / f"lm{sfx}.vtu")
     for i, q in enumerate(functions[:-2]):
-        np.savez(out / f"flux_{i}.npz", values=q.x.array, edges=q.function_space.edges)
-    np.savez(out / "pressure.npz", values=functions[-2].x.array,
+        np.savez(out / f"flux_{i}{sfx}.npz", values=q.x.array, edges=q.function_space.edges)
+    np.savez(out / f"pressure{sfx}.npz", values=functions[-2].x.array,
              edges=functions[-2].function_space.edges)
-    np.savez(out / "lm.npz", values=functions[-1].x.array)
+    np.savez(out / f"lm{sfx}.npz", values=functions[-1].x.array)
 
 
 def export_submeshes(network_mesh: NetworkMesh, outpath: str | Path) -> None:

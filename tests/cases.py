@@ -105,4 +105,5 @@ def graph_arrays(G):
 # graphs with cycles (the direct solve's Woodbury correction), name -> (factory, N)
 CYCLIC = {"edge_info_N10": (edge_info_graph, 10),
           "lattice4x5_N6": (lambda: lattice_graph(4, 5), 6),
-          "lattice6x6_N3": (lambda: lattice_graph(6, 6), 3)}
+          "lattice6x6_N3": (lambda: lattice_graph(6, 6), 3),
+          "lattice19x20_N2": (lambda: lattice_graph(19, 20), 2)}  # (342 cycle chains)

@@ -9,6 +9,7 @@ multipliers as vertices; the XDMF topology and geometry against the mesh."""
 
 from __future__ import annotations
 
+import base64
 import xml.etree.ElementTree as ET
 
 import numpy as np
@@ -28,7 +29,14 @@ def _mesh():
 def _read(path):
     root = ET.parse(path).getroot()
     piece = root.find("UnstructuredGrid/Piece")
-    arrays = {a.get("Name"): np.array(a.text.split(), dtype=float) for a in root.iter("DataArray")}
+    arrays = {}
+    for a in root.iter("DataArray"):
+        if a.get("format") == "binary":  # base64 of a UInt32 byte count, then the doubles
+            raw = base64.b64decode(a.text)
+            n = int(np.frombuffer(raw[:4], dtype="<u4")[0])
+            arrays[a.get("Name")] = np.frombuffer(raw[4:4 + n], dtype="<f8")
+        else:
+            arrays[a.get("Name")] = np.array(a.text.split(), dtype=float)
     return piece, arrays
 
 
@@ -108,3 +116,32 @@ def test_export_submeshes_xdmf(tmp_path):
         np.testing.assert_array_equal(topo, cells)
         gx = mesh.mesh.geometry.x
         np.testing.assert_allclose(geo[:, : gx.shape[1]], gx)
+
+
+def test_export_nan_binary_and_rank_suffix(tmp_path):
+    """A node value another rank owns is NaN in this rank's continuous pressure (the advisor's
+    r05 finding): such an array is written as inline binary (VTK's ASCII reader cannot
+    parse 'nan'), every finite value unchanged; on several ranks every rank writes its own
+    files, name_r{rank}, instead of overwriting one name."""
+    mesh = _mesh()
+    N, E, m = mesh.N, mesh.num_edges, 2
+
+    class TwoRanks:
+        rank, size = 1, 2
+
+    mesh._comm = TwoRanks()  # (the property reads it)
+    nodes = np.flatnonzero(np.asarray(mesh.degrees) > 0)
+    vals = np.concatenate([mesh.node_coordinates[nodes, 0], np.zeros(E * (m * N - 1))])
+    vals[0] = np.nan  # (a node value this rank does not hold)
+    V = FunctionSpace(mesh, "pressure", "P", m, False, vals.size, np.arange(E))
+    V.nodes = nodes
+    Vq = FunctionSpace(mesh, "flux", "P", 1, False, 0, np.zeros(0, dtype=np.int64), 0)
+    Vl = FunctionSpace(mesh, "multiplier", "DG", 0, True, 0)
+    Vl.nodes = np.zeros(0, dtype=np.int64)
+    export_functions([Function(Vq, array=np.zeros(0)), Function(V, name="pressure", array=vals),
+                      Function(Vl, name="lm", array=np.zeros(0))], tmp_path)
+    assert not (tmp_path / "pressure.vtu").exists()
+    piece, a = _read(tmp_path / "pressure_r1.vtu")
+    p = a["pressure"]
+    assert p.size == E * N * (m + 1) and np.isnan(p).any() and np.isfinite(p).sum() > 0
+    assert (tmp_path / "lm_r1.vtu").exists() and (tmp_path / "flux_0_r1.npz").exists()

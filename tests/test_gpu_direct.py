@@ -197,7 +197,8 @@ def test_fused_residual_is_the_true_residual(case, monkeypatch):
         assert np.linalg.norm(h.solution() - x_ref[perm]) / np.linalg.norm(x_ref) <= SOL_TOL
 
 
-@pytest.mark.parametrize("case", ["edge_info_N10", "lattice4x5_N6", "lattice6x6_N3"])
+@pytest.mark.parametrize("case", ["edge_info_N10", "lattice4x5_N6", "lattice6x6_N3",
+                                  "lattice19x20_N2"])
 def test_direct_solve_with_cycles(case, monkeypatch):
     """Graphs with cycles: the tree solve of A without the cycle chains' grounded couplings
     plus the rank-2k Woodbury correction (k_cyc_*), checked with the CSR's true residual;

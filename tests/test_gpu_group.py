@@ -665,7 +665,8 @@ def test_exchange_one_rank_gives_up_exchange1(separate):
 
 
 @pytest.mark.parametrize("case,P", [("edge_info_N10", 3), ("lattice4x5_N6", 2),
-                                    ("lattice4x5_N6", 3), ("lattice6x6_N3", 4)])
+                                    ("lattice4x5_N6", 3), ("lattice6x6_N3", 4),
+                                    ("lattice19x20_N2", 3)])
 def test_group_direct_solve_cycles(case, P):
     """Graphs with cycles across ranks: cycle chains inside a rank and coarse chains closing a
     cycle between ranks are grounded by the decomposition; every rank holds its share of Z =

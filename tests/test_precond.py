@@ -301,10 +301,14 @@ def test_forced_coarse_terminals_one_rank(case, n_term):
 
 CYCLIC = {"edge_info_N10": (CASES["edge_info_N10"][0], 10),
           "lattice4x5_N6": (lambda: lattice_graph(4, 5), 6),
-          "lattice6x6_N3": (lambda: lattice_graph(6, 6), 3)}
+          "lattice6x6_N3": (lambda: lattice_graph(6, 6), 3),
+          # 342 cycle chains: past round 5's 128-chain cap (the capacitance matrix is inverted
+          # on the device since round 6)
+          "lattice19x20_N2": (lambda: lattice_graph(19, 20), 2)}
 
 
-@pytest.mark.parametrize("case", sorted(CYCLIC))
+# (the 342-chain lattice is the GPU tests' -- its dense CPU model takes minutes)
+@pytest.mark.parametrize("case", sorted(c for c in CYCLIC if c != "lattice19x20_N2"))
 def test_cycle_rows_and_woodbury(case):
     """Graphs with cycles (nx_set_cycles): the decomposition lists, per cycle-closing chain,
     the (flux end, multiplier) pair its grounded end drops -- a +-1 coupling of A. Without
