@@ -415,10 +415,19 @@ class HydraulicNetworkAssembler:
                                                            mesh.degrees, mesh.N, 0, 1)
         pc = build_tree_preconditioner(lp, src, dst, mesh.degrees, target_jobs=256)
         aux = None
-        # a graph with cycles on one rank: the auxiliary handle's Woodbury correction of its
-        # cycle chains (nx_set_cycles, set with its decomposition), as P1/DG0's direct solve
+        # a graph with cycles: the auxiliary handle's Woodbury correction of its cycle chains
+        # (one rank: nx_set_cycles, set with its decomposition; several: every rank's share of
+        # all ranks' chains, nx_set_cycles_team, the pairs gathered on the host), as P1/DG0's
+        # direct solve
         ncyc = int(np.asarray(pc.cyc_rows).reshape(-1, 2).shape[0])
-        ok = bool(pc.tree_exact) or (not ranks and 0 < ncyc <= _lib.MAX_CYCLES)
+        gpairs = []
+        if ranks:  # (collective: every rank, in the same order)
+            gpairs = [p for ps in mesh.comm.allgather(
+                cycle_pairs_global(lp, pc.cyc_rows, mesh.num_edges, mesh.bifurcation_index))
+                for p in ps]
+            ok = (bool(pc.tree_exact) and not gpairs) or 0 < len(gpairs) <= _lib.MAX_CYCLES
+        else:
+            ok = bool(pc.tree_exact) or 0 < ncyc <= _lib.MAX_CYCLES
         if ranks:  # (every rank makes the same collective calls below: decide together)
             ok = int(self._network_mesh.comm.allreduce(int(ok), MIN)) == 1
         if ok:
@@ -429,6 +438,10 @@ class HydraulicNetworkAssembler:
                 aux.set_cut(lp.n_cut, lp.lm_cut, lp.gk_off, lp.gk_row, lp.gk_coef)
             aux.set_preconditioner(pc)
             ok = aux.pc_lds()
+            if ok and gpairs:
+                own, qloc, lcol = team_cycle_tables(lp, pc.cyc_rows, gpairs, mesh.num_edges,
+                                                    mesh.bifurcation_index)
+                aux.set_cycles_team(own, qloc, lcol)
         if ok:
             alpha, beta, C, K, Mii = condensed_flux_mass(k)
             ratio = round(alpha / beta)

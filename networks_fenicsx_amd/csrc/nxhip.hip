@@ -10770,6 +10770,67 @@ __global__ __launch_bounds__(256) void k_cyc_cap_p1(const double* __restrict__ Z
   }
 }
 
+// Several ranks: this rank's share of U^T Z (the rows of U it owns) and the couplings of the
+// cycle chains it holds, by the flux end's position in the P1 layout (k_cyc_cap_team's, with
+// no CSR values: the auxiliary handle holds none)
+__global__ __launch_bounds__(256) void k_cyc_cap_team_p1(const double* __restrict__ Z, int64_t ldz,
+                                                         const int* __restrict__ own, int m,
+                                                         const int* __restrict__ qloc, int N,
+                                                         double* __restrict__ cap,
+                                                         double* __restrict__ acoef) {
+  for (int i = threadIdx.x; i < m * m; i += 256) {
+    const int r = i / m, c = i % m;
+    cap[i] = own[r] >= 0 ? Z[(int64_t)c * ldz + own[r]] : 0.0;
+  }
+  for (int k = threadIdx.x; 2 * k < m; k += 256) {
+    double a = 0.0;
+    if (qloc[k] >= 0) {
+      const int loc = qloc[k] % (2 * N + 1);
+      a = loc == 0 ? -1.0 : (loc == 2 * N ? 1.0 : 0.0);
+    }
+    acoef[k] = a;  // (summed over the ranks: one rank holds each chain)
+  }
+}
+
+// Several ranks: the auxiliary handle's team Woodbury correction (nx_set_cycles_team on it):
+// Z by the ranks' tree solves of unit right-hand sides (sweeps only, the coarse all-reduce
+// between their halves), U^T Z and the couplings summed over the ranks, Cinv on every rank
+int fe_cyc_build_team(nx_network* h, nx_network* a) {
+  const int m = 2 * a->n_cyc;
+  const hipStream_t as = a->stream;
+  a->stream = h->stream;
+  a->need_r = false;
+  a->cyc_raw = true;
+  nx_network* ah[1] = {a};
+  const Team t{ah, 1, nullptr};
+  int rc = NX_OK;
+  for (int j = 0; j < m && rc == NX_OK; ++j) {
+    if (hipMemsetAsync(a->tmp, 0, sizeof(double) * a->n_col, a->stream) != hipSuccess ||
+        hipMemsetAsync(a->x, 0, sizeof(double) * a->n_col, a->stream) != hipSuccess) {
+      rc = fail(NX_ERR_HIP, "fe_cyc_build_team: memset");
+      break;
+    }
+    hipLaunchKernelGGL(k_cyc_unit, dim3(1), dim3(1), 0, a->stream, a->tmp, a->d_cyc_rows, j);
+    rc = launch_direct_team(t, 0.0, 1, false, false);
+    if (rc == NX_OK &&
+        hipMemcpyAsync(a->cyc_z + (int64_t)j * a->n_col, a->x, sizeof(double) * a->n_col,
+                       hipMemcpyDeviceToDevice, a->stream) != hipSuccess)
+      rc = fail(NX_ERR_HIP, "fe_cyc_build_team: copy");
+  }
+  a->cyc_raw = false;
+  if (rc == NX_OK) {
+    hipLaunchKernelGGL(k_cyc_cap_team_p1, dim3(1), dim3(256), 0, a->stream, a->cyc_z, a->n_col,
+                       a->d_cyc_rows, m, a->d_cyc_qloc, (int)a->N, a->cyc_cap,
+                       a->cyc_cap + (int64_t)m * m);
+    rc = team_allreduce(t, -4, m * m + m / 2);
+  }
+  if (rc == NX_OK) rc = cyc_invert(a);
+  a->stream = as;
+  CHECK(rc);
+  a->cyc_version = h->lhs_version;
+  return NX_OK;
+}
+
 // (k, 0) on a graph with cycles (one rank): the auxiliary handle's Woodbury correction for
 // the condensed system (nx_set_cycles on the auxiliary handle): Z = A_g^{-1} U by its tree
 // solves of unit right-hand sides (the condensed lumped mass just written by k_fe_condense),
@@ -10828,8 +10889,10 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
     const double* b = pass ? h->tmp : h->rhs;  // refinement: the residual the check kept
     hipLaunchKernelGGL(k_fe_condense, dim3(grid_of(n0, kBlock)), dim3(kBlock), 0, h->stream, c,
                        b, pass ? nullptr : a->dq, a->rhs);
-    const int mcyc = ranks ? 0 : 2 * a->n_cyc;  // a graph with cycles (one rank): Woodbury
-    if (mcyc && pass == 0 && a->cyc_version != h->lhs_version) CHECK(fe_cyc_build(h, a));
+    // a graph with cycles: Woodbury (one rank; several: the team's, a->cyc_team)
+    const int mcyc = (!ranks || a->cyc_team) ? 2 * a->n_cyc : 0;
+    if (mcyc && pass == 0 && a->cyc_version != h->lhs_version)
+      CHECK(ranks ? fe_cyc_build_team(h, a) : fe_cyc_build(h, a));
     {  // the auxiliary tree solve on this handle's stream (no cross-queue hand-offs)
       const hipStream_t as = a->stream;
       a->stream = h->stream;
@@ -10839,11 +10902,25 @@ int fe_solve_direct(nx_network* h, double rtol, int32_t* iters, double* relres,
       a->stream = as;
       CHECK(rc);
     }
-    if (mcyc) {  // x_aux -= Z Cinv U^T x_aux: the couplings the tree solve dropped
+    if (mcyc && !ranks) {  // x_aux -= Z Cinv U^T x_aux: the couplings the tree solve dropped
       hipLaunchKernelGGL(k_cyc_w, dim3(grid_of(mcyc, 256)), dim3(256), sizeof(double) * mcyc, h->stream, a->x, a->d_cyc_rows, mcyc,
                          a->cyc_cinv, nullptr, a->cyc_w, nullptr);
       hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(a->n_own, kBlock)), dim3(kBlock), 0, h->stream,
                          a->x, a->cyc_z, a->n_col, a->cyc_w, mcyc, a->n_own);
+    } else if (mcyc) {  // several ranks: U^T x_aux summed over them first
+      const hipStream_t as = a->stream;
+      a->stream = h->stream;
+      nx_network* ah[1] = {a};
+      const int rc = cyc_gather_team(Team{ah, 1, nullptr}, false);
+      if (rc == NX_OK) {
+        hipLaunchKernelGGL(k_cyc_w_team, dim3(grid_of(mcyc, 256)), dim3(256),
+                           sizeof(double) * mcyc, h->stream, a->cyc_u, mcyc, a->cyc_cinv, nullptr,
+                           a->cyc_w);
+        hipLaunchKernelGGL(k_cyc_fix, dim3(grid_of(a->n_own, kBlock)), dim3(kBlock), 0,
+                           h->stream, a->x, a->cyc_z, a->n_col, a->cyc_w, mcyc, a->n_own);
+      }
+      a->stream = as;
+      CHECK(rc);
     }
     hipLaunchKernelGGL(k_fe_expand, dim3(grid_of(n0 + np, kBlock)), dim3(kBlock), 0, h->stream,
                        c, a->x, b, h->x, pass);
@@ -12466,7 +12543,8 @@ NX_API int nx_fe_set_direct(nx_network_t* h, nx_network_t* aux, int32_t k, int64
       !cst)
     return fail(NX_ERR_ARG, "NULL array");
   if (aux->fe || !aux->pc || !aux->cond_mass || aux->N != h->N || aux->E != h->E ||
-      (aux->n_cyc > 0 && (proc_rank(aux) || aux->nranks > 1)) || aux->device != h->device ||
+      (aux->n_cyc > 0 && !aux->cyc_team && (proc_rank(aux) || aux->nranks > 1)) ||
+      aux->device != h->device ||
       aux->nranks != h->nranks ||
       aux->rank != h->rank || proc_rank(aux) != proc_rank(h) || aux->group || h->group)
     return fail(NX_ERR_STATE, "the auxiliary handle must be a P1/DG0 handle of the same "

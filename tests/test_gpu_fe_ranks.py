@@ -94,7 +94,9 @@ def _gather(data, j, n):
 
 
 @pytest.mark.parametrize("case,P,k", [("depth6_N40", 2, 2), ("depth6_N40", 3, 3),
-                                      ("arterial5_N40", 2, 2), ("double_Y_N5", 2, 3)])
+                                      ("arterial5_N40", 2, 2), ("double_Y_N5", 2, 3),
+                                      # cycles (round 6): the auxiliary handle's team Woodbury
+                                      ("edge_info_N10", 2, 2), ("edge_info_N10", 3, 3)])
 def test_fe_ranks_direct(tmp_path, case, P, k):
     ranks, data = _run(tmp_path, case, P, k)
     x_ref = _reference(case, k)
