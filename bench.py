@@ -343,6 +343,50 @@ def fe_leg(mesh, steps: int = 20, warmup: int = 5) -> dict:
     return out
 
 
+def fe_leg_ranks(mesh, world: int, barrier, allmax, steps: int = 10, warmup: int = 3) -> dict:
+    """``--fe-ranks``: the general-degree direct solves on the bench's ranks (RCCL at P > 1:
+    (2, 0)'s condensed solve -- its auxiliary handle's team tree solve --, (2, 1)'s
+    node-condensed one with its all-reduce of the border blocks), timed like the headline,
+    with every rank's path, convergence and reported residual; the ranks must report the same
+    residual bits (one all-reduce of its sums). Opt-in: a rank that failed inside one of its
+    collectives would leave the others waiting in RCCL (no timeout), and the headline's JSON
+    line must come out; the host-transport tests cover the same code on one GPU
+    (tests/test_gpu_fe_ranks.py)."""
+    from networks_fenicsx_amd import HydraulicNetworkAssembler
+
+    out = {}
+    for k, m in ((2, 0), (2, 1)):
+        key = f"k{k}_m{m}"
+        asm = HydraulicNetworkAssembler(mesh, flux_degree=k, pressure_degree=m)
+        try:
+            asm.compute_forms(p_bc_ex=lambda x: x[1])
+            asm.set_direct(True)
+            h = asm.handle
+            res = None
+            for _ in range(warmup):
+                asm.assemble()
+                res = h.solve(1e-12, 50000, 32)
+            h.sync()
+            barrier()
+            ts = time.perf_counter()
+            for _ in range(steps):
+                asm.assemble()
+                res = h.solve(1e-12, 50000, 32)
+            h.sync()
+            barrier()
+            ms = allmax(1e3 * (time.perf_counter() - ts) / steps)
+            rr = float(res[1])
+            out[key] = {"ranks": world, "rows_max_per_rank": allmax(h.n_rows), "ms_per_step": ms,
+                        "steps": steps, "direct_path": h.direct_path(),
+                        "solver": "direct" if h.solver()[1] == 1 else "minres",
+                        "passes": res[0], "relres": rr, "converged": bool(res[2]),
+                        "all_ranks_direct": allmax(0.0 if h.solver()[1] == 1 else 1.0) == 0.0,
+                        "relres_equal_on_ranks": allmax(rr) == -allmax(-rr)}
+        finally:
+            asm.close()
+    return out
+
+
 def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -369,6 +413,9 @@ def parse_args(argv=None):
     ap.add_argument("--api-steps", type=int, default=10,
                     help="steps through the public Solver.assemble/solve surface (0: skip)")
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
+    ap.add_argument("--fe-ranks", action="store_true",
+                    help="at P > 1 also the general-degree direct solves over the ranks "
+                         "(RCCL; opt-in, see fe_leg_ranks)")
     ap.add_argument("--no-fe", dest="fe", action="store_false",
                     help="skip the general-degree leg ((2, 0) and (2, 1) on the headline tree)")
     ap.add_argument("--no-c4", dest="c4", action="store_false",
@@ -750,6 +797,8 @@ def run(args, world: int) -> int:
     fe = None
     if args.fe and world == 1 and (levels, N) == (15, 15):
         fe = fe_leg(mesh)
+    elif args.fe_ranks and world > 1:
+        fe = fe_leg_ranks(mesh, world, barrier, allmax)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
