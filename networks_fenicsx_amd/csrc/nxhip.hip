@@ -2997,8 +2997,11 @@ __device__ void pc_pack_last(const PcArgs& pa, const double* partB, const double
 }
 
 // DIRK: the direct solve's instantiation (mode kModeDirect only; without the MINRES paths its
-// registers fit the fused residual without spills)
-template <bool MULTI, int W, int CPL, bool DIRK>
+// registers fit the fused residual without spills). TOPL = false: the direct solve whose top
+// part (one rank) or coarse forest (several) a launch of its own solved (pa.topdown /
+// pa.coarsedown off, e.g. C4's 1024 jobs on one GPU): no top-part LDS, 141 -> 20 KB, two
+// workgroups per CU instead of one
+template <bool MULTI, int W, int CPL, bool DIRK, bool TOPL = true>
 __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* __restrict__ y,
                                                             const double* __restrict__ r2,
                                                             double* __restrict__ z,
@@ -3008,7 +3011,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   // one rank, direct (pa.topdown): the top part's first indices before anything else (they
   // need no per-job offsets; the scalar loads of the prologue below would hold them back)
   TopPre tpre;
-  if (DIRK && !MULTI && pa.topdown) top_pre_idx(pa, tpre);
+  if (DIRK && TOPL && !MULTI && pa.topdown) top_pre_idx(pa, tpre);
   __shared__ double sZ[kCapS], sA[kCapS], sB[kCapS];
   __shared__ int sP[kCapS];
   constexpr int kCT = DIRK ? 1 : kCapT;  // MINRES-only arrays (dense top, start's prep)
@@ -3017,15 +3020,15 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   __shared__ double sGz[kCT], sGt[kCT], sGd[kCT];  // start only: G columns (prep)
   __shared__ int sGp[kCT], sGc[kCT];
   // one rank, direct (pa.topdown): the top part's solve in every workgroup (top_body)
-  constexpr int kTT = DIRK ? kCapT : 1, kTD = DIRK && !MULTI ? kCapTDC : 1;
+  constexpr int kTT = DIRK && TOPL ? kCapT : 1, kTD = DIRK && TOPL && !MULTI ? kCapTDC : 1;
   __shared__ double tD0[kTT], tJ0[kTT], tD[kTT], tJ[kTT], tGp[kTT], tY[kTT];
   __shared__ int tPar[kTT], tLam[kTT], tOff[kTT + 1], tChild[kTD];
   __shared__ double tG[kTD], tDD[kTD], tDJ[kTD];
-  __shared__ int tLv[DIRK ? kMaxTopLvl + 1 : 1];
+  __shared__ int tLv[DIRK && TOPL ? kMaxTopLvl + 1 : 1];
   // several ranks, direct (pa.coarsedown): the coarse forest and the top part solved here
   // (k_pc_coarse's work) in tD0 / tJ0 / tD (coarse) and tJ (top values)
   __shared__ int sLvl[kCapLvl + 1];
-  __shared__ double sCz[MULTI ? kCapCoarseLds : 1];      // fused coarse solve
+  __shared__ double sCz[MULTI && TOPL ? kCapCoarseLds : 1];  // fused coarse solve
   __shared__ double sQt[DIRK ? kCapC : 1], sQb[DIRK ? kCapC : 1];  // fused residual
   // linear form: P^{-1}y is formed here and combined, z = P^{-1}y - c2 z_old, y' = y - c2 r2
   const bool lin = MULTI && pa.lin && mode == 0;
@@ -3051,10 +3054,10 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
   // (pa.coarsedown): the coarse forest and the top part's back-substitution (k_pc_coarse's
   // work; values in tJ). Before the chain prefetch: nothing of it is live across them
   // (spills otherwise).
-  const bool tdir = DIRK && !MULTI && pa.topdown;
-  const bool cdir = DIRK && MULTI && pa.coarsedown;
+  const bool tdir = DIRK && TOPL && !MULTI && pa.topdown;
+  const bool cdir = DIRK && TOPL && MULTI && pa.coarsedown;
   const int tts0 = pa.top_ts0;
-  if constexpr (DIRK && !MULTI) {
+  if constexpr (DIRK && TOPL && !MULTI) {
     if (tdir) {
       top_pre_val(pa, y, tpre);
       top_body<false>(pa, y, r2, z, st, nullptr, 0, nullptr, nullptr, kModeDirect,
@@ -3062,7 +3065,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pc_down_lds(PcArgs pa, double* _
                       true, tpre);
     }
   }
-  if constexpr (DIRK && MULTI) {
+  if constexpr (DIRK && TOPL && MULTI) {
     if (cdir) {
       CoarsePre cpre;
       coarse_top_pre(pa, cpre);
@@ -7526,9 +7529,13 @@ void launch_pc_wc(nx_network* h, double* y, const double* r2, MrState* st, MrSta
     hipLaunchKernelGGL(k_pc_coarse, dim3(1), dim3(kTopThreads), 0, h->stream, h->pa, y, r2, z,
                        st, h->partB, mode);
   if (h->pc_jobs > 0) {
-    if (h->pc_lds && mode == kModeDirect)
+    if (h->pc_lds && mode == kModeDirect && (MULTI ? h->pa.coarsedown : h->pa.topdown))
       hipExtLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL, true>), dim3(h->pc_jobs), dim3(kPcThreads),
                             0, h->stream, e[4], e[5], 0, h->pa, y, r2, z, st, h->partB, mode);
+    else if (h->pc_lds && mode == kModeDirect)  // (the top part / coarse forest solved before)
+      hipExtLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL, true, false>), dim3(h->pc_jobs),
+                            dim3(kPcThreads), 0, h->stream, e[4], e[5], 0, h->pa, y, r2, z, st,
+                            h->partB, mode);
     else if (h->pc_lds)
       hipExtLaunchKernelGGL((k_pc_down_lds<MULTI, W, CPL, false>), dim3(h->pc_jobs), dim3(kPcThreads),
                             0, h->stream, e[4], e[5], 0, h->pa, y, r2, z, st, h->partB, mode);
@@ -8451,7 +8458,8 @@ struct CpArgs {
   const int* tI;      // nI: +1 flux, -1 pressure (interior node types)
   const int* eb;      // per edge: u, v (border node indices), au, av (lam couplings: 0, +-1)
   const int* nrow;    // per border node: its pressure row, its multiplier row (or -1)
-  double* fac;        // per edge, per vertex (N + 1): Pi 4 | C 4 | W 8 | rho 2
+  double* fac;        // per vertex (N + 1), per factor: Pi 4 | C 4 | W 8 | rho 2, per edge
+                      // (edge-minor: a wave's lanes, consecutive edges, touch 512 B per access)
   double* se;         // per edge: Se 16 | ge 4
   double* xn;         // per border node: its (p, lam) values
   const int* gid;     // several ranks: the global edge of each local edge (its se slot)
@@ -8461,7 +8469,10 @@ constexpr int kCpFac = 18;
 __device__ __forceinline__ double cp_pow(double s, int ex) {  // s^ex, ex in {-1, 0, 1}
   return ex > 0 ? s : ex < 0 ? 1.0 / s : 1.0;
 }
+// (the node forest's arithmetic with contraction off: every kernel that inlines it -- the
+// lists', the records', the pipelined records' -- rounds the same way, bit for bit)
 __device__ __forceinline__ void inv2(const double* P, double* Pi) {
+#pragma clang fp contract(off)
   const double det = P[0] * P[3] - P[1] * P[2];
   const double id = 1.0 / det;
   Pi[0] = P[3] * id;
@@ -8481,7 +8492,8 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
   const double* Ch = a.cst + 16;
   const int au = a.eb[4 * e + 2], av = a.eb[4 * e + 3];
   const double R = a.edge_R[e];
-  double* fe = a.fac + e * (int64_t)(N + 1) * kCpFac;
+  double* fe = a.fac + e;
+  const int64_t E = a.E;
   auto prow = [&](int j) { return base + nf + j - 1; };  // interior pressure position j
   double P[4] = {0.0, 0.0, 0.0, 1.0}, W[8] = {0.0}, rho[2] = {b[base], 0.0};
   W[1] = (double)au;  // q_0 <-> lam_u
@@ -8555,12 +8567,12 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
       for (int q = 0; q < 4; ++q) Sb[4 * r + q] -= W[r] * Y[q] + W[4 + r] * Y[4 + q];
       gb[r] -= W[r] * z[0] + W[4 + r] * z[1];
     }
-    double* f = fe + (int64_t)c * kCpFac;
-    for (int i = 0; i < 4; ++i) f[i] = Pi[i];
-    for (int i = 0; i < 4; ++i) f[4 + i] = C[i];
-    for (int i = 0; i < 8; ++i) f[8 + i] = W[i];
-    f[16] = rho[0];
-    f[17] = rho[1];
+    double* f = fe + (int64_t)c * kCpFac * E;
+    for (int i = 0; i < 4; ++i) f[i * E] = Pi[i];
+    for (int i = 0; i < 4; ++i) f[(4 + i) * E] = C[i];
+    for (int i = 0; i < 8; ++i) f[(8 + i) * E] = W[i];
+    f[16 * E] = rho[0];
+    f[17 * E] = rho[1];
     for (int i = 0; i < 4; ++i) P[i] = Pn[i];
     for (int i = 0; i < 8; ++i) W[i] = Wn[i];
     rho[0] = rn[0];
@@ -8578,12 +8590,12 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
       for (int q = 0; q < 4; ++q) Sb[4 * r + q] -= W[r] * Y[q] + W[4 + r] * Y[4 + q];
       gb[r] -= W[r] * z[0] + W[4 + r] * z[1];
     }
-    double* f = fe + (int64_t)N * kCpFac;
-    for (int i = 0; i < 4; ++i) f[i] = Pi[i];
-    for (int i = 0; i < 4; ++i) f[4 + i] = 0.0;
-    for (int i = 0; i < 8; ++i) f[8 + i] = W[i];
-    f[16] = rho[0];
-    f[17] = rho[1];
+    double* f = fe + (int64_t)N * kCpFac * E;
+    for (int i = 0; i < 4; ++i) f[i * E] = Pi[i];
+    for (int i = 0; i < 4; ++i) f[(4 + i) * E] = 0.0;
+    for (int i = 0; i < 8; ++i) f[(8 + i) * E] = W[i];
+    f[16 * E] = rho[0];
+    f[17 * E] = rho[1];
   }
   double* o = a.se + 20 * (a.gid ? (int64_t)a.gid[e] : e);
   for (int i = 0; i < 16; ++i) o[i] = Sb[i];
@@ -8641,6 +8653,7 @@ __device__ __forceinline__ void cp_up_edge(const CpArgs& a, int e, int end, doub
 __device__ __forceinline__ void cp_up_child_v(const CpArgs& a, int ce, int cend,
                                               const double* Pc, const double* hc, double* D,
                                               double* g) {
+#pragma clang fp contract(off)
   double B[4];  // child rows x this node's columns
   cp_block(a.se, ce, cend, 1 - cend, B);
   double X[4], z[2];  // Pc B, Pc h
@@ -8715,6 +8728,7 @@ __device__ __forceinline__ void cp_node_up(const CpArgs& a, const CpTree& t,
 }
 // ... and its back-substitution: the node's values from its parent's
 __device__ __forceinline__ void cp_node_down(const CpArgs& a, const CpTree& t, int i) {
+#pragma clang fp contract(off)
   int n, p, pe, pend;
   if (t.rec != nullptr) {  // node and parent from the record (one 16-B load each)
     const int* q = t.rec + (int64_t)kCpRecPad * i;
@@ -8760,6 +8774,164 @@ __global__ __launch_bounds__(1024) void k_cp_nodes(CpArgs a, CpTree t, const dou
 }
 constexpr int kCpWide = 2048;  // wider levels: grid launches (cp_nodes_launch)
 
+// The same levels with the node records (t.rec), software-pipelined across the level barriers
+// (round 6): what a level reads that no level before it writes -- its records, b, its edges'
+// border blocks and, going down, its own pivots -- is loaded one level ahead (the record two
+// levels ahead going up), so a level waits on one round trip (its children's pivots and rhs
+// going up, its parent's values going down) instead of three. Same arithmetic, same order as
+// cp_node_up / cp_node_down; a node whose record overflows (more edges or children than the
+// record holds) runs cp_node_up itself. Levels of at most 1024 nodes (one per thread).
+struct CpUpMid {
+  int i, n, nch;  // i < 0: no node
+  bool slow;
+  double D[4], g[2];
+  int ch[kCpRecCh], ce[kCpRecCh], cend[kCpRecCh];  // children, their parent edges and ends
+};
+constexpr int kCpRecUp = 24;  // the up pass's part of a record (through the children)
+__device__ __forceinline__ void cp_rec_load(const CpTree& t, int i, int (&r)[kCpRecUp]) {
+  if (i < 0) return;
+  const int4* q4 = reinterpret_cast<const int4*>(t.rec + (int64_t)kCpRecPad * i);
+#pragma unroll
+  for (int w = 0; w < kCpRecUp / 4; ++w) {
+    const int4 v = q4[w];
+    r[4 * w] = v.x;
+    r[4 * w + 1] = v.y;
+    r[4 * w + 2] = v.z;
+    r[4 * w + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void cp_up_mid(const CpArgs& a, const double* __restrict__ b, int i,
+                                          const int (&r)[kCpRecUp], CpUpMid& m) {
+  constexpr int kc = kCpRecC;
+  m.i = i;
+  m.nch = 0;
+  m.slow = false;
+  if (i < 0) return;
+  m.n = r[0];
+  if (r[3] < 0 || r[kc] < 0) {
+    m.slow = true;
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) m.D[q] = 0.0;
+  const int lr = r[2];
+  m.g[0] = b[r[1]];
+  m.g[1] = lr >= 0 ? b[lr] : 0.0;
+#pragma unroll
+  for (int j = 0; j < kCpRecInc; ++j)
+    if (j < r[3]) cp_up_edge(a, r[4 + 2 * j], r[5 + 2 * j], m.D, m.g);
+  if (lr < 0) m.D[3] = 1.0;
+  m.nch = r[kc];
+#pragma unroll
+  for (int j = 0; j < kCpRecCh; ++j) {
+    m.ch[j] = r[kc + 1 + 3 * j];
+    m.ce[j] = r[kc + 2 + 3 * j];
+    m.cend[j] = r[kc + 3 + 3 * j];
+  }
+}
+__device__ __forceinline__ void cp_up_fin(const CpArgs& a, const CpTree& t,
+                                          const double* __restrict__ b, CpUpMid& m) {
+  if (m.i < 0) return;
+  if (m.slow) {
+    cp_node_up(a, t, b, m.i);
+    return;
+  }
+  // (the children's blocks load with their pivots: one round trip for both)
+#pragma unroll
+  for (int j = 0; j < kCpRecCh; ++j)
+    if (j < m.nch)
+      cp_up_child_v(a, m.ce[j], m.cend[j], t.Pinv + 4 * (int64_t)m.ch[j],
+                    t.hv + 2 * (int64_t)m.ch[j], m.D, m.g);
+  inv2(m.D, t.Pinv + 4 * (int64_t)m.n);
+  t.hv[2 * m.n] = m.g[0];
+  t.hv[2 * m.n + 1] = m.g[1];
+}
+struct CpDnMid {
+  int n, p;  // n < 0: no node
+  double r[2], B[4], P[4];
+};
+__device__ __forceinline__ void cp_dn_rec(const CpTree& t, int i, int4 (&r)[3]) {
+  if (i < 0) return;
+  const int* q = t.rec + (int64_t)kCpRecPad * i;
+  r[0] = *reinterpret_cast<const int4*>(q);
+  r[1] = *reinterpret_cast<const int4*>(q + 20);  // [22] parent, [23] its edge
+  r[2] = *reinterpret_cast<const int4*>(q + 24);  // [24] this node's end of it
+}
+__device__ __forceinline__ void cp_dn_mid(const CpArgs& a, const CpTree& t, int i,
+                                          const int4 (&r)[3], CpDnMid& m) {
+  m.n = -1;
+  if (i < 0) return;
+  const int n = r[0].x, p = r[1].z, pe = r[1].w, pend = r[2].x;
+  m.n = n;
+  m.p = p;
+  m.r[0] = t.hv[2 * n];
+  m.r[1] = t.hv[2 * n + 1];
+  if (p >= 0) cp_block(a.se, pe, pend, 1 - pend, m.B);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) m.P[q] = t.Pinv[4 * (int64_t)n + q];
+}
+__device__ __forceinline__ void cp_dn_fin(const CpArgs& a, CpDnMid& m) {
+#pragma clang fp contract(off)
+  if (m.n < 0) return;
+  double r0 = m.r[0], r1 = m.r[1];
+  if (m.p >= 0) {
+    const double* xp = a.xn + 2 * (int64_t)m.p;
+    r0 -= m.B[0] * xp[0] + m.B[1] * xp[1];
+    r1 -= m.B[2] * xp[0] + m.B[3] * xp[1];
+  }
+  a.xn[2 * m.n] = m.P[0] * r0 + m.P[1] * r1;
+  a.xn[2 * m.n + 1] = m.P[2] * r0 + m.P[3] * r1;
+}
+constexpr int kCpPipeLv = 64;  // levels per k_cp_nodes_rec launch (their offsets in LDS)
+__global__ __launch_bounds__(1024) void k_cp_nodes_rec(CpArgs a, CpTree t,
+                                                       const double* __restrict__ b, int L0,
+                                                       int L1, int up) {
+  __shared__ int sLo[kCpPipeLv + 1];
+  const int nlv = L1 - L0;
+  for (int k = threadIdx.x; k <= nlv; k += 1024) sLo[k] = t.lev_off[L0 + k];
+  __syncthreads();
+  // the node of this thread at the pass's k-th level (-1: none)
+  auto node = [&](int k) {
+    if (k >= nlv) return -1;
+    const int L = up ? nlv - 1 - k : k;
+    const int i = sLo[L] + (int)threadIdx.x;
+    return i < sLo[L + 1] ? i : -1;
+  };
+  if (up) {
+    int r[kCpRecUp];
+    CpUpMid m, mn;
+    int i = node(0);
+    cp_rec_load(t, i, r);
+    cp_up_mid(a, b, i, r, m);
+    int inx = node(1);
+    cp_rec_load(t, inx, r);  // level 1's record
+    for (int k = 0; k < nlv; ++k) {
+      cp_up_mid(a, b, inx, r, mn);  // level k + 1: b and its border blocks
+      inx = node(k + 2);
+      cp_rec_load(t, inx, r);       // level k + 2: its record
+      cp_up_fin(a, t, b, m);        // level k: the children's pivots (the one wait)
+      __syncthreads();
+      m = mn;
+    }
+  } else {
+    int4 r[3];
+    CpDnMid m, mn;
+    int i = node(0);
+    cp_dn_rec(t, i, r);
+    cp_dn_mid(a, t, i, r, m);
+    int inx = node(1);
+    cp_dn_rec(t, inx, r);
+    for (int k = 0; k < nlv; ++k) {
+      cp_dn_mid(a, t, inx, r, mn);  // level k + 1: its pivots, rhs and parent blocks
+      inx = node(k + 2);
+      cp_dn_rec(t, inx, r);
+      cp_dn_fin(a, m);              // level k: the parent's values (the one wait)
+      __syncthreads();
+      m = mn;
+    }
+  }
+}
+
 // One level [i0, i1) of level-order nodes, a thread per node across the grid
 __global__ __launch_bounds__(256) void k_cp_level(CpArgs a, CpTree t, const double* __restrict__ b,
                                                   int i0, int i1, int up) {
@@ -8782,7 +8954,8 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
   const int64_t base = e * (int64_t)(nf + m * N - 1);
   const int u = a.eb[4 * e], v = a.eb[4 * e + 1];
   const double xb[4] = {a.xn[2 * u], a.xn[2 * u + 1], a.xn[2 * v], a.xn[2 * v + 1]};
-  const double* fe = a.fac + e * (int64_t)(N + 1) * kCpFac;
+  const double* fe = a.fac + e;
+  const int64_t E = a.E;
   const double* Eh = a.cst + 16 + 4 * nI;
   const double* Fh = Eh + 4 * nI;
   const double R = a.edge_R[e];
@@ -8791,15 +8964,18 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
   double yn[2] = {0.0, 0.0};  // the next vertex's (q, p)
   const int tV[4] = {1, -1, 1, -1};
   for (int i = N; i >= 0; --i) {
-    const double* f = fe + (int64_t)i * kCpFac;
-    double r[2] = {f[16], f[17]};
+    const double* f = fe + (int64_t)i * kCpFac * E;
+    double fv[kCpFac];
+#pragma unroll
+    for (int q = 0; q < kCpFac; ++q) fv[q] = f[q * E];
+    double r[2] = {fv[16], fv[17]};
     for (int q = 0; q < 4; ++q) {
-      r[0] -= f[8 + q] * xb[q];
-      r[1] -= f[12 + q] * xb[q];
+      r[0] -= fv[8 + q] * xb[q];
+      r[1] -= fv[12 + q] * xb[q];
     }
-    r[0] -= f[4] * yn[0] + f[5] * yn[1];
-    r[1] -= f[6] * yn[0] + f[7] * yn[1];
-    const double y0 = f[0] * r[0] + f[1] * r[1], y1 = f[2] * r[0] + f[3] * r[1];
+    r[0] -= fv[4] * yn[0] + fv[5] * yn[1];
+    r[1] -= fv[6] * yn[0] + fv[7] * yn[1];
+    const double y0 = fv[0] * r[0] + fv[1] * r[1], y1 = fv[2] * r[0] + fv[3] * r[1];
     put(base + (int64_t)k * i, y0);
     if (i > 0 && i < N) put(prow(m * i), y1);
     if (i < N) {  // cell i: its interior nodes from (q_i, p_i, q_{i+1}, p_{i+1})
@@ -10968,12 +11144,20 @@ void fe_true_residual(nx_network* h, double rtol, int nrb) {
                      nrb, rtol, h->d_seq, h->d_last);
 }
 
+// NXHIP_CP_PIPE=0: the node forest's one-workgroup levels without the pipelining (A/B)
+bool cp_pipe_on() {
+  const char* e = std::getenv("NXHIP_CP_PIPE");
+  return e == nullptr || std::atoi(e) != 0;
+}
+
 // The node forest's solve: levels of more than kCpWide nodes as grid launches (a thread per
 // node), the runs of narrower levels in one workgroup each; up deepest first, then down.
 void cp_nodes_launch(nx_network* h, const CpArgs& a, const CpTree& tr, const double* b) {
   const std::vector<int>& lo = h->cp_lev_host;
   const int nl = h->cp_nlev;
-  auto wide = [&](int L) { return lo[L + 1] - lo[L] > kCpWide; };
+  // (pipelined: levels of more than 1024 nodes go to the grid launches)
+  const int wmax = tr.rec != nullptr && cp_pipe_on() ? 1024 : kCpWide;
+  auto wide = [&](int L) { return lo[L + 1] - lo[L] > wmax; };
   for (int up = 1; up >= 0; --up) {
     // runs of levels in the pass's order: a wide level alone, consecutive narrow ones together
     int k = 0;
@@ -10989,7 +11173,13 @@ void cp_nodes_launch(nx_network* h, const CpArgs& a, const CpTree& tr, const dou
       int k1 = k;
       while (k1 < nl && !wide(up ? nl - 1 - k1 : k1)) ++k1;
       const int La = up ? nl - k1 : k, Lb = up ? nl - k : k1;  // levels [La, Lb)
-      hipLaunchKernelGGL(k_cp_nodes, dim3(1), dim3(1024), 0, h->stream, a, tr, b, La, Lb, up);
+      // (the pipelined kernel: records, at most 1024 nodes per level and kCpPipeLv levels)
+      bool pipe = tr.rec != nullptr && Lb - La <= kCpPipeLv && cp_pipe_on();
+      for (int L = La; L < Lb && pipe; ++L) pipe = lo[L + 1] - lo[L] <= 1024;
+      if (pipe)
+        hipLaunchKernelGGL(k_cp_nodes_rec, dim3(1), dim3(1024), 0, h->stream, a, tr, b, La, Lb, up);
+      else
+        hipLaunchKernelGGL(k_cp_nodes, dim3(1), dim3(1024), 0, h->stream, a, tr, b, La, Lb, up);
       k = k1;
     }
   }
