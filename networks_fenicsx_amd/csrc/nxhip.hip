@@ -7169,6 +7169,15 @@ struct nx_network {
   double *cp_Pinv = nullptr, *cp_hv = nullptr;
   int *cp_tI = nullptr, *cp_eb = nullptr, *cp_nrow = nullptr, *cp_lev_off = nullptr;
   std::vector<int> cp_lev_host;  // the level offsets on the host (cp_nodes_launch)
+  // runs of wide levels as subtree chunks (k_cp_nodes_rec, one workgroup per chunk): per run
+  // its levels [L0, L1), its chunk count and its ranges' offset in cp_rng (2 (L1 - L0) ints
+  // per chunk: each level's [start, end) in the records' level order)
+  struct CpRun {
+    int L0, L1, nch, off;
+  };
+  std::vector<CpRun> cp_runs;
+  int* cp_rng = nullptr;
+  std::vector<char> cp_lev_full;  // per level: every record holds its edges and children
   int *cp_order = nullptr, *cp_inc_off = nullptr, *cp_inc = nullptr, *cp_parent = nullptr;
   int *cp_child_off = nullptr, *cp_child = nullptr, *cp_nown = nullptr;
   // several ranks (nx_fe_cp_ranks): this rank's edges run the edge kernels (cp_Eown), every
@@ -7178,6 +7187,7 @@ struct nx_network {
   int64_t cp_Eown = 0, cp_Eg = 0;
   int *cp_gid = nullptr, *cp_nrowx = nullptr;
   int* cp_rec = nullptr;  // the node records (CpTree::rec)
+  double* cp_ctr = nullptr;  // the nodes' Schur terms for their parents (CpTree::ctr)
   std::vector<int> cp_gid_host, cp_nrowx_host;
 };
 
@@ -8486,28 +8496,30 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.E) return;
   const int N = a.N, k = a.k, m = a.m, nI = a.nI;
-  const int nf = k * N + 1;
-  const int64_t base = e * (int64_t)(nf + m * N - 1);
+  const int nf = k * N + 1, per = nf + m * N - 1;
+  const int64_t base = e * (int64_t)per;
+  const double* bl = b + base;         // this edge's rows of b
+  const double* hl = a.cellh + e * N;  // its cells' lengths
   const double* Kh = a.cst;
   const double* Ch = a.cst + 16;
   const int au = a.eb[4 * e + 2], av = a.eb[4 * e + 3];
   const double R = a.edge_R[e];
   double* fe = a.fac + e;
   const int64_t E = a.E;
-  auto prow = [&](int j) { return base + nf + j - 1; };  // interior pressure position j
-  double P[4] = {0.0, 0.0, 0.0, 1.0}, W[8] = {0.0}, rho[2] = {b[base], 0.0};
+  auto prow = [&](int j) { return nf + j - 1; };  // interior pressure position j (local row)
+  double P[4] = {0.0, 0.0, 0.0, 1.0}, W[8] = {0.0}, rho[2] = {bl[0], 0.0};
   W[1] = (double)au;  // q_0 <-> lam_u
   double Sb[16] = {0.0}, gb[4] = {0.0};
   const int tV[4] = {1, -1, 1, -1};
   for (int c = 0; c < N; ++c) {
-    const double s = R * a.cellh[e * N + c];
+    const double s = R * hl[c];
     double K[16];
     for (int r = 0; r < 4; ++r)
       for (int q = 0; q < 4; ++q) K[4 * r + q] = Kh[4 * r + q] * cp_pow(s, (tV[r] + tV[q]) / 2);
     double rV[4] = {0.0, 0.0, 0.0, 0.0};
     for (int i = 0; i < nI; ++i) {  // the cell's interior rhs condensed onto its vertices
       const int ti = a.tI[i];
-      const double bi = ti > 0 ? b[base + c * k + 1 + i] : b[prow(c * m + 1 + (i - (k - 1)))];
+      const double bi = ti > 0 ? bl[c * k + 1 + i] : bl[prow(c * m + 1 + (i - (k - 1)))];
       for (int r = 0; r < 4; ++r) rV[r] -= Ch[r * nI + i] * cp_pow(s, (tV[r] - ti) / 2) * bi;
     }
     double C[4];  // left vertex rows (q, p) x right vertex columns (q, p)
@@ -8529,8 +8541,8 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
     }
     if (c + 1 < N) {
       Pn[0] = K[10]; Pn[1] = K[11]; Pn[2] = K[14]; Pn[3] = K[15];
-      rn[0] = rV[2] + b[base + (int64_t)k * (c + 1)];
-      rn[1] = rV[3] + b[prow(m * (c + 1))];
+      rn[0] = rV[2] + bl[k * (c + 1)];
+      rn[1] = rV[3] + bl[prow(m * (c + 1))];
     } else {  // the right p is the border p_v
       Sb[10] += K[15];
       gb[2] += rV[3];
@@ -8546,7 +8558,7 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
       C[1] = 0.0;
       C[3] = 0.0;
       Pn[0] = K[10]; Pn[1] = 0.0; Pn[2] = 0.0; Pn[3] = 1.0;
-      rn[0] = rV[2] + b[base + nf - 1];
+      rn[0] = rV[2] + bl[nf - 1];
       rn[1] = 0.0;
     }
     double Pi[4];
@@ -8622,6 +8634,10 @@ struct CpTree {
   // node's elimination / back-substitution reads, in one place -- one dependent load instead
   // of the chain order -> offsets -> lists -> entries; nullptr: the lists
   const int* rec;
+  // with the records: each node's Schur term for its parent (6 per node: B^T Pc B | B^T Pc h,
+  // the expressions cp_up_child_v subtracts), written by the node's own elimination, so the
+  // parent reads 6 doubles per child instead of forming them from 10 (round 6)
+  double* ctr;
 };
 // node record (ints): [0] n, [1] pressure row, [2] multiplier row, [3] #edges (-1: more
 // than kCpRecInc, read the lists), [4..11] (edge, end) x kCpRecInc, [12] #children (-1: more
@@ -8666,6 +8682,28 @@ __device__ __forceinline__ void cp_up_child_v(const CpArgs& a, int ce, int cend,
     g[r] -= B[r] * z[0] + B[2 + r] * z[1];
   }
 }
+// the node's Schur term for its parent (records' path; the same expressions, the same bits as
+// cp_up_child_v forms them in the parent): B = the node's block of its parent edge (node rows
+// x parent columns), Pc / hc its pivot inverse and rhs
+__device__ __forceinline__ void cp_up_term(const double* B, const double* Pc, const double* hc,
+                                           double* o) {
+#pragma clang fp contract(off)
+  double X[4], z[2];
+  for (int r = 0; r < 2; ++r) {
+    for (int q = 0; q < 2; ++q) X[2 * r + q] = Pc[2 * r] * B[q] + Pc[2 * r + 1] * B[2 + q];
+    z[r] = Pc[2 * r] * hc[0] + Pc[2 * r + 1] * hc[1];
+  }
+  for (int r = 0; r < 2; ++r) {
+    for (int q = 0; q < 2; ++q) o[2 * r + q] = B[r] * X[q] + B[2 + r] * X[2 + q];
+    o[4 + r] = B[r] * z[0] + B[2 + r] * z[1];
+  }
+}
+// a child's term into the node's pivot and rhs
+__device__ __forceinline__ void cp_up_sub(const double* tc, double* D, double* g) {
+  for (int q = 0; q < 4; ++q) D[q] -= tc[q];
+  g[0] -= tc[4];
+  g[1] -= tc[5];
+}
 __device__ __forceinline__ void cp_up_child(const CpArgs& a, const CpTree& t, int c, int ce,
                                             int cend, double* D, double* g) {
   cp_up_child_v(a, ce, cend, t.Pinv + 4 * (int64_t)c, t.hv + 2 * (int64_t)c, D, g);
@@ -8698,17 +8736,27 @@ __device__ __forceinline__ void cp_node_up(const CpArgs& a, const CpTree& t,
         cp_up_edge(a, t.inc[2 * j], t.inc[2 * j + 1], D, g);
     }
     if (lr < 0) D[3] = 1.0;  // (no multiplier: a decoupled dummy)
-    constexpr int kc = kCpRecC;  // the children's part of the record
+    constexpr int kc = kCpRecC;  // the children's part of the record: their terms (ctr)
     if (r[kc] >= 0) {
 #pragma unroll
       for (int j = 0; j < kCpRecCh; ++j)
-        if (j < r[kc]) cp_up_child(a, t, r[kc + 1 + 3 * j], r[kc + 2 + 3 * j], r[kc + 3 + 3 * j], D, g);
+        if (j < r[kc]) cp_up_sub(t.ctr + 6 * (int64_t)r[kc + 1 + 3 * j], D, g);
     } else {
-      for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j) {
-        const int c = t.child[j];
-        cp_up_child(a, t, c, t.parent[3 * c + 1], t.parent[3 * c + 2], D, g);
-      }
+      for (int j = t.child_off[n]; j < t.child_off[n + 1]; ++j)
+        cp_up_sub(t.ctr + 6 * (int64_t)t.child[j], D, g);
     }
+    double Pi[4];
+    inv2(D, Pi);
+    for (int q = 0; q < 4; ++q) t.Pinv[4 * (int64_t)n + q] = Pi[q];
+    t.hv[2 * n] = g[0];
+    t.hv[2 * n + 1] = g[1];
+    if (r[kCpRecP] >= 0) {  // this node's term for its parent
+      double B[4], o[6];
+      cp_block(a.se, r[kCpRecP + 1], r[kCpRecP + 2], 1 - r[kCpRecP + 2], B);
+      cp_up_term(B, Pi, g, o);
+      for (int q = 0; q < 6; ++q) t.ctr[6 * (int64_t)n + q] = o[q];
+    }
+    return;
   } else {
     n = t.order[i];
     const int pr = a.nrow[2 * n], lr = a.nrow[2 * n + 1];
@@ -8779,20 +8827,19 @@ constexpr int kCpWide = 2048;  // wider levels: grid launches (cp_nodes_launch)
 // border blocks and, going down, its own pivots -- is loaded one level ahead (the record two
 // levels ahead going up), so a level waits on one round trip (its children's pivots and rhs
 // going up, its parent's values going down) instead of three. Same arithmetic, same order as
-// cp_node_up / cp_node_down; a node whose record overflows (more edges or children than the
-// record holds) runs cp_node_up itself. Levels of at most 1024 nodes (one per thread).
+// cp_node_up / cp_node_down. Levels of at most 1024 nodes (one per thread) whose records all
+// hold their node's edges and children (cp_lev_full; else the level-by-level kernels).
 struct CpUpMid {
   int i, n, nch;  // i < 0: no node
-  bool slow;
   double D[4], g[2];
-  int ch[kCpRecCh], ce[kCpRecCh], cend[kCpRecCh];  // children, their parent edges and ends
+  int ch[kCpRecCh];
+  int pe, pend;  // the parent edge and this node's end of it (pe < 0: a root)
 };
-constexpr int kCpRecUp = 24;  // the up pass's part of a record (through the children)
-__device__ __forceinline__ void cp_rec_load(const CpTree& t, int i, int (&r)[kCpRecUp]) {
+__device__ __forceinline__ void cp_rec_load(const CpTree& t, int i, int (&r)[kCpRecPad]) {
   if (i < 0) return;
   const int4* q4 = reinterpret_cast<const int4*>(t.rec + (int64_t)kCpRecPad * i);
 #pragma unroll
-  for (int w = 0; w < kCpRecUp / 4; ++w) {
+  for (int w = 0; w < kCpRecPad / 4; ++w) {
     const int4 v = q4[w];
     r[4 * w] = v.x;
     r[4 * w + 1] = v.y;
@@ -8800,18 +8847,15 @@ __device__ __forceinline__ void cp_rec_load(const CpTree& t, int i, int (&r)[kCp
     r[4 * w + 3] = v.w;
   }
 }
+// a level's part that no level before it writes: b, its edges' border blocks (one level ahead)
 __device__ __forceinline__ void cp_up_mid(const CpArgs& a, const double* __restrict__ b, int i,
-                                          const int (&r)[kCpRecUp], CpUpMid& m) {
+                                          const int (&r)[kCpRecPad], CpUpMid& m) {
   constexpr int kc = kCpRecC;
   m.i = i;
   m.nch = 0;
-  m.slow = false;
+  m.pe = -1;
   if (i < 0) return;
   m.n = r[0];
-  if (r[3] < 0 || r[kc] < 0) {
-    m.slow = true;
-    return;
-  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) m.D[q] = 0.0;
   const int lr = r[2];
@@ -8823,28 +8867,46 @@ __device__ __forceinline__ void cp_up_mid(const CpArgs& a, const double* __restr
   if (lr < 0) m.D[3] = 1.0;
   m.nch = r[kc];
 #pragma unroll
-  for (int j = 0; j < kCpRecCh; ++j) {
-    m.ch[j] = r[kc + 1 + 3 * j];
-    m.ce[j] = r[kc + 2 + 3 * j];
-    m.cend[j] = r[kc + 3 + 3 * j];
+  for (int j = 0; j < kCpRecCh; ++j) m.ch[j] = r[kc + 1 + 3 * j];
+  if (r[kCpRecP] >= 0) {
+    m.pe = r[kCpRecP + 1];
+    m.pend = r[kCpRecP + 2];
   }
 }
-__device__ __forceinline__ void cp_up_fin(const CpArgs& a, const CpTree& t,
-                                          const double* __restrict__ b, CpUpMid& m) {
+// ... and the part after the level below: its children's terms (loaded first thing in the
+// level, with its own parent block: one round trip), the pivot, its term for its parent
+struct CpUpIn {
+  double tc[kCpRecCh][6], B[4];
+};
+__device__ __forceinline__ void cp_up_in(const CpArgs& a, const CpTree& t, const CpUpMid& m,
+                                         CpUpIn& in) {
   if (m.i < 0) return;
-  if (m.slow) {
-    cp_node_up(a, t, b, m.i);
-    return;
-  }
-  // (the children's blocks load with their pivots: one round trip for both)
 #pragma unroll
   for (int j = 0; j < kCpRecCh; ++j)
     if (j < m.nch)
-      cp_up_child_v(a, m.ce[j], m.cend[j], t.Pinv + 4 * (int64_t)m.ch[j],
-                    t.hv + 2 * (int64_t)m.ch[j], m.D, m.g);
-  inv2(m.D, t.Pinv + 4 * (int64_t)m.n);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) in.tc[j][q] = t.ctr[6 * (int64_t)m.ch[j] + q];
+  if (m.pe >= 0) cp_block(a.se, m.pe, m.pend, 1 - m.pend, in.B);
+}
+__device__ __forceinline__ void cp_up_fin(const CpArgs& a, const CpTree& t,
+                                          const double* __restrict__ b, CpUpMid& m,
+                                          const CpUpIn& in) {
+  if (m.i < 0) return;
+#pragma unroll
+  for (int j = 0; j < kCpRecCh; ++j)
+    if (j < m.nch) cp_up_sub(in.tc[j], m.D, m.g);
+  double Pi[4];
+  inv2(m.D, Pi);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t.Pinv[4 * (int64_t)m.n + q] = Pi[q];
   t.hv[2 * m.n] = m.g[0];
   t.hv[2 * m.n + 1] = m.g[1];
+  if (m.pe >= 0) {
+    double o[6];
+    cp_up_term(in.B, Pi, m.g, o);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) t.ctr[6 * (int64_t)m.n + q] = o[q];
+  }
 }
 struct CpDnMid {
   int n, p;  // n < 0: no node
@@ -8882,23 +8944,35 @@ __device__ __forceinline__ void cp_dn_fin(const CpArgs& a, CpDnMid& m) {
   a.xn[2 * m.n] = m.P[0] * r0 + m.P[1] * r1;
   a.xn[2 * m.n + 1] = m.P[2] * r0 + m.P[3] * r1;
 }
-constexpr int kCpPipeLv = 64;  // levels per k_cp_nodes_rec launch (their offsets in LDS)
+constexpr int kCpPipeLv = 64;  // levels per k_cp_nodes_rec launch (their ranges in LDS)
+constexpr int kCpChunk = 128;  // nodes per level of a subtree chunk (its workgroup's threads)
+// rng: a run of wide levels in subtree chunks, one per workgroup (each level's [start, end)
+// of this chunk; nx_fe_set_cp), or nullptr: levels [L0, L1) whole, in one workgroup
 __global__ __launch_bounds__(1024) void k_cp_nodes_rec(CpArgs a, CpTree t,
-                                                       const double* __restrict__ b, int L0,
+                                                       const double* __restrict__ b,
+                                                       const int* __restrict__ rng, int L0,
                                                        int L1, int up) {
-  __shared__ int sLo[kCpPipeLv + 1];
+  __shared__ int sLo[kCpPipeLv], sHi[kCpPipeLv];
   const int nlv = L1 - L0;
-  for (int k = threadIdx.x; k <= nlv; k += 1024) sLo[k] = t.lev_off[L0 + k];
+  for (int k = threadIdx.x; k < nlv; k += blockDim.x) {
+    if (rng != nullptr) {
+      sLo[k] = rng[2 * ((int64_t)blockIdx.x * nlv + k)];
+      sHi[k] = rng[2 * ((int64_t)blockIdx.x * nlv + k) + 1];
+    } else {
+      sLo[k] = t.lev_off[L0 + k];
+      sHi[k] = t.lev_off[L0 + k + 1];
+    }
+  }
   __syncthreads();
   // the node of this thread at the pass's k-th level (-1: none)
   auto node = [&](int k) {
     if (k >= nlv) return -1;
     const int L = up ? nlv - 1 - k : k;
     const int i = sLo[L] + (int)threadIdx.x;
-    return i < sLo[L + 1] ? i : -1;
+    return i < sHi[L] ? i : -1;
   };
   if (up) {
-    int r[kCpRecUp];
+    int r[kCpRecPad];
     CpUpMid m, mn;
     int i = node(0);
     cp_rec_load(t, i, r);
@@ -8906,10 +8980,12 @@ __global__ __launch_bounds__(1024) void k_cp_nodes_rec(CpArgs a, CpTree t,
     int inx = node(1);
     cp_rec_load(t, inx, r);  // level 1's record
     for (int k = 0; k < nlv; ++k) {
+      CpUpIn in;
+      cp_up_in(a, t, m, in);        // level k: its children's terms (the one wait)
       cp_up_mid(a, b, inx, r, mn);  // level k + 1: b and its border blocks
       inx = node(k + 2);
       cp_rec_load(t, inx, r);       // level k + 2: its record
-      cp_up_fin(a, t, b, m);        // level k: the children's pivots (the one wait)
+      cp_up_fin(a, t, b, m, in);
       __syncthreads();
       m = mn;
     }
@@ -8950,8 +9026,10 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.E) return;
   const int N = a.N, k = a.k, m = a.m, nI = a.nI;
-  const int nf = k * N + 1;
-  const int64_t base = e * (int64_t)(nf + m * N - 1);
+  const int nf = k * N + 1, per = nf + m * N - 1;
+  const int64_t base = e * (int64_t)per;
+  const double* bl = b + base;         // this edge's rows of b
+  const double* hl = a.cellh + e * N;  // its cells' lengths
   const int u = a.eb[4 * e], v = a.eb[4 * e + 1];
   const double xb[4] = {a.xn[2 * u], a.xn[2 * u + 1], a.xn[2 * v], a.xn[2 * v + 1]};
   const double* fe = a.fac + e;
@@ -8960,14 +9038,22 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
   const double* Fh = Eh + 4 * nI;
   const double R = a.edge_R[e];
   auto put = [&](int64_t r, double val) { x[r] = accum ? x[r] + val : val; };
-  auto prow = [&](int j) { return base + nf + j - 1; };
+  auto putl = [&](int r, double val) { put(base + r, val); };  // the edge's local row r
+  auto prow = [&](int j) { return nf + j - 1; };  // (local row)
   double yn[2] = {0.0, 0.0};  // the next vertex's (q, p)
   const int tV[4] = {1, -1, 1, -1};
-  for (int i = N; i >= 0; --i) {
-    const double* f = fe + (int64_t)i * kCpFac * E;
-    double fv[kCpFac];
+  // (the vertex factors one vertex ahead: the next vertex's loads fly while this one computes)
+  double fv[kCpFac], fn[kCpFac];
 #pragma unroll
-    for (int q = 0; q < kCpFac; ++q) fv[q] = f[q * E];
+  for (int q = 0; q < kCpFac; ++q) fn[q] = fe[((int64_t)N * kCpFac + q) * E];
+  for (int i = N; i >= 0; --i) {
+#pragma unroll
+    for (int q = 0; q < kCpFac; ++q) fv[q] = fn[q];
+    if (i > 0) {
+      const double* f = fe + (int64_t)(i - 1) * kCpFac * E;
+#pragma unroll
+      for (int q = 0; q < kCpFac; ++q) fn[q] = f[q * E];
+    }
     double r[2] = {fv[16], fv[17]};
     for (int q = 0; q < 4; ++q) {
       r[0] -= fv[8 + q] * xb[q];
@@ -8976,21 +9062,21 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
     r[0] -= fv[4] * yn[0] + fv[5] * yn[1];
     r[1] -= fv[6] * yn[0] + fv[7] * yn[1];
     const double y0 = fv[0] * r[0] + fv[1] * r[1], y1 = fv[2] * r[0] + fv[3] * r[1];
-    put(base + (int64_t)k * i, y0);
-    if (i > 0 && i < N) put(prow(m * i), y1);
+    putl(k * i, y0);
+    if (i > 0 && i < N) putl(prow(m * i), y1);
     if (i < N) {  // cell i: its interior nodes from (q_i, p_i, q_{i+1}, p_{i+1})
-      const double s = R * a.cellh[e * N + i];
+      const double s = R * hl[i];
       const double xv[4] = {y0, i == 0 ? xb[0] : y1, yn[0], i + 1 == N ? xb[2] : yn[1]};
       for (int j = 0; j < nI; ++j) {
         const int tj = a.tI[j];
         double val = 0.0;
         for (int l = 0; l < nI; ++l) {
           const int tl = a.tI[l];
-          const double bl = tl > 0 ? b[base + i * k + 1 + l] : b[prow(i * m + 1 + (l - (k - 1)))];
-          val += Fh[j * nI + l] * cp_pow(s, -(tj + tl) / 2) * bl;
+          const double bv = tl > 0 ? bl[i * k + 1 + l] : bl[prow(i * m + 1 + (l - (k - 1)))];
+          val += Fh[j * nI + l] * cp_pow(s, -(tj + tl) / 2) * bv;
         }
         for (int q = 0; q < 4; ++q) val -= Eh[j * 4 + q] * cp_pow(s, (-tj + tV[q]) / 2) * xv[q];
-        put(tj > 0 ? base + i * k + 1 + j : prow(i * m + 1 + (j - (k - 1))), val);
+        putl(tj > 0 ? i * k + 1 + j : prow(i * m + 1 + (j - (k - 1))), val);
       }
     }
     yn[0] = y0;
@@ -9356,10 +9442,10 @@ NX_API int nx_destroy(nx_network_t* h) {
                   h->d_cyc_rows, h->cyc_z, h->cyc_cinv, h->cyc_cap, h->cyc_prev, h->cyc_w,
                   h->fe_slot, h->fe_vfe, h->fe_vaux, h->fe_ife, h->fe_pfe, h->fe_paux, h->fe_lfe,
                   h->fe_laux, h->fe_cst, h->fe_cellh, h->d_cyc_qloc, h->d_cyc_lcol, h->cyc_u,
-                  h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_tI,
+                  h->cp_cst, h->cp_fac, h->cp_se, h->cp_xn, h->cp_Pinv, h->cp_hv, h->cp_ctr, h->cp_tI,
                   h->cp_eb, h->cp_nrow, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
                   h->cp_parent, h->cp_child_off, h->cp_child, h->cp_nown, h->cp_gid,
-                  h->cp_nrowx, h->cp_rec, h->fe_tpl_buf,
+                  h->cp_nrowx, h->cp_rec, h->cp_rng, h->fe_tpl_buf,
                   h->fe_tpl_rbuf, h->fe_tpl_rs, h->fe_tpl_shape, h->fe_tpl_lam};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -11163,6 +11249,16 @@ void cp_nodes_launch(nx_network* h, const CpArgs& a, const CpTree& tr, const dou
     int k = 0;
     while (k < nl) {
       const int L = up ? nl - 1 - k : k;
+      const nx_network::CpRun* run = nullptr;  // a run of wide levels in subtree chunks
+      if (wmax == 1024)
+        for (const auto& r : h->cp_runs)
+          if (up ? L == r.L1 - 1 : L == r.L0) run = &r;
+      if (run != nullptr) {
+        hipLaunchKernelGGL(k_cp_nodes_rec, dim3(run->nch), dim3(kCpChunk), 0, h->stream, a, tr,
+                           b, h->cp_rng + run->off, run->L0, run->L1, up);
+        k += run->L1 - run->L0;
+        continue;
+      }
       if (wide(L)) {
         const int n = lo[L + 1] - lo[L];
         hipLaunchKernelGGL(k_cp_level, dim3(grid_of(n, 256)), dim3(256), 0, h->stream, a, tr, b,
@@ -11170,14 +11266,23 @@ void cp_nodes_launch(nx_network* h, const CpArgs& a, const CpTree& tr, const dou
         ++k;
         continue;
       }
+      // (a narrow run ends at a wide level or where a chunked run starts)
+      auto run_at = [&](int Lq) {
+        if (wmax != 1024) return false;
+        for (const auto& r : h->cp_runs)
+          if (up ? Lq == r.L1 - 1 : Lq == r.L0) return true;
+        return false;
+      };
       int k1 = k;
-      while (k1 < nl && !wide(up ? nl - 1 - k1 : k1)) ++k1;
+      while (k1 < nl && !wide(up ? nl - 1 - k1 : k1) && (k1 == k || !run_at(up ? nl - 1 - k1 : k1)))
+        ++k1;
       const int La = up ? nl - k1 : k, Lb = up ? nl - k : k1;  // levels [La, Lb)
       // (the pipelined kernel: records, at most 1024 nodes per level and kCpPipeLv levels)
       bool pipe = tr.rec != nullptr && Lb - La <= kCpPipeLv && cp_pipe_on();
-      for (int L = La; L < Lb && pipe; ++L) pipe = lo[L + 1] - lo[L] <= 1024;
+      for (int L = La; L < Lb && pipe; ++L) pipe = lo[L + 1] - lo[L] <= 1024 && h->cp_lev_full[L];
       if (pipe)
-        hipLaunchKernelGGL(k_cp_nodes_rec, dim3(1), dim3(1024), 0, h->stream, a, tr, b, La, Lb, up);
+        hipLaunchKernelGGL(k_cp_nodes_rec, dim3(1), dim3(1024), 0, h->stream, a, tr, b,
+                           (const int*)nullptr, La, Lb, up);
       else
         hipLaunchKernelGGL(k_cp_nodes, dim3(1), dim3(1024), 0, h->stream, a, tr, b, La, Lb, up);
       k = k1;
@@ -11201,9 +11306,12 @@ int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int3
   nx_network* hs[1] = {h};
   const Team t{hs, 1, nullptr};
   const CpTree tr{h->cp_nn, h->cp_nlev, h->cp_lev_off, h->cp_order, h->cp_inc_off, h->cp_inc,
-                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_Pinv, h->cp_hv, h->cp_rec};
+                  h->cp_parent, h->cp_child_off, h->cp_child, h->cp_Pinv, h->cp_hv, h->cp_rec,
+                  h->cp_rec ? h->cp_ctr : nullptr};
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
-  // (one thread per edge: 64-thread workgroups spread the edges over every CU)
+  // (one thread per edge: 64-thread workgroups spread the edges over every CU. Staging the
+  // edges' rows of b in LDS was measured slower, r06zd: the sweeps are bound by their serial
+  // per-cell arithmetic, not by the loads)
   const int eb = std::max(1, grid_of(Ee, 64));
   MrState s{};
   int pass = 0;
@@ -12584,16 +12692,18 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
     return fail(NX_ERR_STATE, "several ranks: nx_fe_cp_ranks before nx_fe_set_cp");
   CHECK(set_device(h));
   HIPCALL(hipStreamSynchronize(h->stream));
-  for (double** p : {&h->cp_cst, &h->cp_fac, &h->cp_se, &h->cp_xn, &h->cp_Pinv, &h->cp_hv}) {
+  for (double** p : {&h->cp_cst, &h->cp_fac, &h->cp_se, &h->cp_xn, &h->cp_Pinv, &h->cp_hv,
+                     &h->cp_ctr}) {
     if (*p) HIPCALL(hipFree(*p));
     *p = nullptr;
   }
   for (int** p : {&h->cp_tI, &h->cp_eb, &h->cp_nrow, &h->cp_lev_off, &h->cp_order, &h->cp_inc_off,
                   &h->cp_inc, &h->cp_parent, &h->cp_child_off, &h->cp_child, &h->cp_nown,
-                  &h->cp_gid, &h->cp_nrowx, &h->cp_rec}) {
+                  &h->cp_gid, &h->cp_nrowx, &h->cp_rec, &h->cp_rng}) {
     if (*p) HIPCALL(hipFree(*p));
     *p = nullptr;
   }
+  h->cp_runs.clear();
   h->fe_cp = false;
   if (k == 0) {
     h->cp_Eown = h->cp_Eg = 0;
@@ -12656,10 +12766,93 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   if (child_off[n] > 0) CHECK(upload(&h->cp_child, child, child_off[n], h->stream));
   CHECK(upload(&h->cp_nown, nown, n, h->stream));
   {  // the node records in level order (CpTree::rec; the same sums in the same order)
+    // the levels from the first wider than kCpChunk nodes to the deepest (one run): their
+    // nodes re-ordered inside each level by their ancestor at the run's first level (stable),
+    // so a range of those ancestors owns one range per level -- a chunk, one workgroup's
+    // subtrees of at most kCpChunk nodes per level (cp_nodes_launch; one CU moves a level's
+    // few hundred bytes per node at a few tens of GB/s, so the chunks stay small). Within a
+    // level the nodes are independent: the order changes no sum.
+    std::vector<int> ord(order, order + n), lvl_of(n, 0), anc(n, -1);
+    for (int L = 0; L < n_lev; ++L)
+      for (int i = lev_off[L]; i < lev_off[L + 1]; ++i) lvl_of[order[i]] = L;
+    std::vector<int> rng;
+    int Lc = 0;
+    while (Lc < n_lev && lev_off[Lc + 1] - lev_off[Lc] <= kCpChunk) ++Lc;
+    for (int L = Lc; L < n_lev;) {
+      const int L1 = n_lev;
+      bool ok = L1 - L <= kCpPipeLv;
+      for (int i = lev_off[L]; i < lev_off[L + 1]; ++i) anc[ord[i]] = i - lev_off[L];
+      for (int Q = L + 1; Q < L1 && ok; ++Q) {
+        for (int i = lev_off[Q]; i < lev_off[Q + 1]; ++i) {
+          const int nd = ord[i], pn = parent[3 * nd];
+          if (pn < 0 || lvl_of[pn] != Q - 1) {
+            ok = false;  // (a BFS forest: the parent is one level up)
+            break;
+          }
+          anc[nd] = anc[pn];
+        }
+        if (ok)
+          std::stable_sort(ord.begin() + lev_off[Q], ord.begin() + lev_off[Q + 1],
+                           [&](int x, int y) { return anc[x] < anc[y]; });
+      }
+      if (ok) {  // chunks of ancestors, at most 1024 nodes per level
+        const int na = lev_off[L + 1] - lev_off[L], nq = L1 - L;
+        std::vector<std::vector<int>> cnt(nq, std::vector<int>(na, 0));
+        for (int Q = L; Q < L1; ++Q)
+          for (int i = lev_off[Q]; i < lev_off[Q + 1]; ++i) cnt[Q - L][anc[ord[i]]] += 1;
+        std::vector<int> start(nq), cur(nq, 0);
+        for (int Q = 0; Q < nq; ++Q) start[Q] = lev_off[L + Q];
+        nx_network::CpRun run{L, L1, 0, (int)rng.size()};
+        int a0 = 0;
+        while (a0 < na && ok) {
+          int a1 = a0;
+          std::vector<int> sum(nq, 0);
+          while (a1 < na) {
+            bool fits = true;
+            for (int Q = 0; Q < nq; ++Q) fits = fits && sum[Q] + cnt[Q][a1] <= kCpChunk;
+            if (!fits) break;
+            for (int Q = 0; Q < nq; ++Q) sum[Q] += cnt[Q][a1];
+            ++a1;
+          }
+          if (a1 == a0) {
+            ok = false;  // (one ancestor with more than kCpChunk descendants on a level)
+            break;
+          }
+          for (int Q = 0; Q < nq; ++Q) {
+            rng.push_back(start[Q] + cur[Q]);
+            cur[Q] += sum[Q];
+            rng.push_back(start[Q] + cur[Q]);
+          }
+          run.nch += 1;
+          a0 = a1;
+        }
+        if (ok)
+          h->cp_runs.push_back(run);
+        else
+          rng.resize(run.off);
+      }
+      if (!ok)  // (this run stays level by level: its original order)
+        for (int Q = L; Q < L1; ++Q)
+          for (int i = lev_off[Q]; i < lev_off[Q + 1]; ++i) ord[i] = order[i];
+      L = L1;
+    }
     std::vector<int> rec((size_t)n * kCpRecPad, 0);
+    h->cp_lev_full.assign(n_lev, 1);
+    for (int L = 0; L < n_lev; ++L)
+      for (int i = lev_off[L]; i < lev_off[L + 1]; ++i) {
+        const int nd = order[i];
+        if (inc_off[nd + 1] - inc_off[nd] > kCpRecInc || child_off[nd + 1] - child_off[nd] > kCpRecCh)
+          h->cp_lev_full[L] = 0;
+      }
+    for (size_t q = 0; q < h->cp_runs.size();)  // (a run with an overflowing record: by levels)
+      if (std::any_of(h->cp_lev_full.begin() + h->cp_runs[q].L0,
+                      h->cp_lev_full.begin() + h->cp_runs[q].L1, [](char f) { return !f; }))
+        h->cp_runs.erase(h->cp_runs.begin() + q);
+      else
+        ++q;
     for (int64_t i = 0; i < n; ++i) {
       int* r = rec.data() + i * kCpRecPad;
-      const int nd = order[i];
+      const int nd = ord[i];
       r[0] = nd;
       r[1] = nrow[2 * nd];
       r[2] = nrow[2 * nd + 1];
@@ -12683,7 +12876,11 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
     }
     static_assert(kCpRecP == 22 && kCpRecP + 3 <= kCpRecPad, "the record's parent at [22..24]");
 
-    if (!std::getenv("NXHIP_CP_NOREC")) CHECK(upload(&h->cp_rec, rec.data(), n * kCpRecPad, h->stream));
+    if (!std::getenv("NXHIP_CP_NOREC")) {
+      CHECK(upload(&h->cp_rec, rec.data(), n * kCpRecPad, h->stream));
+      if (!rng.empty()) CHECK(upload(&h->cp_rng, rng.data(), (int64_t)rng.size(), h->stream));
+    }
+    if (h->cp_rec == nullptr || h->cp_rng == nullptr) h->cp_runs.clear();
   }
   CHECK(dalloc(&h->cp_fac, std::max<int64_t>(1, E) * (h->N + 1) * (int64_t)kCpFac));
   // (several ranks: every rank's blocks by global edge, then the node rhs, summed)
@@ -12698,6 +12895,7 @@ NX_API int nx_fe_set_cp(nx_network_t* h, int32_t k, int32_t m, int32_t nI, const
   CHECK(dalloc(&h->cp_xn, 2 * n));
   CHECK(dalloc(&h->cp_Pinv, 4 * n));
   CHECK(dalloc(&h->cp_hv, 2 * n));
+  if (h->cp_rec) CHECK(dalloc(&h->cp_ctr, 6 * n));
   HIPCALL(hipStreamSynchronize(h->stream));
   h->cp_k = k;
   h->cp_m = m;

@@ -286,6 +286,45 @@ def test_fe_cp_node_records_bits(case, km, monkeypatch):
     np.testing.assert_array_equal(xs[0], xs[1])
 
 
+@pytest.mark.parametrize("km", [(2, 1), (3, 2)])
+def test_fe_cp_pipelined_node_forest(km, monkeypatch):
+    """The node forest pipelined across its level barriers (``k_cp_nodes_rec``), its levels
+    below the first of more than 128 nodes as subtree chunks (one workgroup each, records
+    re-ordered inside the levels): the same bits as the level-by-level kernels
+    (``NXHIP_CP_PIPE=0``), on a depth-12 tree (levels of up to 4096 nodes), and the analytic
+    answer."""
+    from networks_fenicsx_amd import network_generation as ng
+
+    mesh = NetworkMesh(ng.make_tree(13, 13, 13), N=3, color_strategy="smallest_last")
+    asm = HydraulicNetworkAssembler(mesh, flux_degree=km[0], pressure_degree=km[1])
+    try:
+        asm.compute_forms(p_bc_ex=lambda x: x[1])
+        asm.set_direct(True)
+        xs = []
+        for pipe in ("0", "1", "1"):
+            monkeypatch.setenv("NXHIP_CP_PIPE", pipe)
+            asm.assemble()
+            it, rr, conv = asm.handle.solve(1e-12, 100, 4)
+            assert conv and asm.handle.direct_path() == "node-condensed", (pipe, it, rr)
+            xs.append(asm.handle.solution())
+        for x in xs[1:]:
+            np.testing.assert_array_equal(xs[0], x)
+        F = OF.build_problem_fe(mesh.node_coordinates, *mesh.edges, 3, *km, mesh.edge_colors)
+        xa = OF.resistor_network_solution_fe(F, lambda x: x[1])
+        x = np.concatenate([fn.x.array for fn in _functions(asm)])
+        assert np.linalg.norm(x - xa) / np.linalg.norm(xa) <= SOL_TOL
+    finally:
+        asm.close()
+
+
+def _functions(asm):
+    from networks_fenicsx_amd.fem import Function
+
+    fns = [Function(V) for V in asm.flux_spaces] + [Function(asm.pressure_space),
+                                                     Function(asm.lm_space)]
+    return asm.scatter_solution(asm.handle.solution(), fns)
+
+
 @pytest.mark.parametrize("case", ["Y_N4", "double_Y_N5", "depth6_N40", "arterial5_N40",
                                   "linear_alt_N3"])
 @pytest.mark.parametrize("km", [(2, 1), (3, 2), (3, 1), (4, 3)])
