@@ -543,6 +543,22 @@ def run(args, world: int) -> int:
     ms_per_step = 1e3 * elapsed / args.steps
     iters = state["it"]
     solver_used = "direct" if h.solver()[1] == 1 else "minres"
+    # every rank's path and exchange status after the timed steps (one all-reduce of a row
+    # per rank): the driver's scaling run shows which ranks ran the exchange step
+    rank_status = None
+    if world > 1:
+        codes = {"fused": 1, "condensed": 2, "exchange": 3, "node-condensed": 4, "launches": 5}
+        xs = h.xr_status()
+        row = [0.0] * (5 * world)
+        row[5 * rank:5 * rank + 5] = [codes.get(h.direct_path(), 0) if solver_used == "direct"
+                                      else 0, float(xs["off"]), xs["why"], xs["agreed"],
+                                      xs["tag"]]
+        got = allsum(row)
+        names = {v: k for k, v in codes.items()}
+        rank_status = [{"rank": r, "path": names.get(int(got[5 * r]), "minres"),
+                        "xr_off": bool(got[5 * r + 1]), "xr_why": int(got[5 * r + 2]),
+                        "xr_agreed": int(got[5 * r + 3]), "xr_tag": int(got[5 * r + 4])}
+                       for r in range(world)]
     if direct and solver_used != "direct" and not args.allow_fallback:
         # the ranks decide together (schedule signature), so every rank stops here
         print(f"bench.py: rank {rank}: the direct solve was requested but the ranks ran "
@@ -833,6 +849,7 @@ def run(args, world: int) -> int:
                 "preconditioner": "tree Schur complement" if pc_on else "none",
             },
             "setup_s": setup,
+            "rank_status": rank_status,
             "api_ms_per_step": api_ms,
             "api_host_ms_per_step": api_host_ms,
             "strong_scaling": strong,
