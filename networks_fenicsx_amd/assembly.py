@@ -603,9 +603,10 @@ class HydraulicNetworkAssembler:
     def set_direct(self, enable: bool) -> None:
         """Ask ``nx_solve`` for the direct tree solve (``nx_set_solver``); the device runs it
         only where it is exact -- exact preconditioner; a forest (the decomposition's
-        ``tree_exact``) or, on one rank, up to 128 cycle-closing chains corrected by a
-        Woodbury step (``nx_set_cycles``); with several ranks the LDS sweeps with the coarse
-        step on every rank (the ranks decide together) -- and MINRES otherwise."""
+        ``tree_exact``) or up to ``MAX_CYCLES`` cycle-closing chains corrected by a Woodbury
+        step (``nx_set_cycles``, one rank; ``nx_set_cycles_team``, several); with several
+        ranks the LDS sweeps with the coarse step on every rank (the ranks decide together)
+        -- and MINRES otherwise."""
         exact = (self._pc is not None and self._pc.tree_exact) or self.fe_direct_available
         want = (bool(enable), bool(exact))
         if getattr(self, "_direct_state", None) != want:
