@@ -304,6 +304,58 @@ def c4_leg(args, world: int, rank: int, comm, timed_steps, state, allsum):
         asm.close()
 
 
+# the committed rocprofv3 passes (kernel trace + FETCH_SIZE / WRITE_SIZE) of the (2, 1)
+# direct step on this leg's workload (scripts/fe_timing.py 15 15 "2,1" direct)
+FE21_PROFILE = "r06zj"
+
+
+def summary_kernel(tag: str, prefix: str):
+    """(calls, avg ns, HBM bytes per launch) of a kernel in profiles/<tag>_summary.json."""
+    path = REPO / "profiles" / f"{tag}_summary.json"
+    if not path.exists():
+        return None
+    for name, d in json.loads(path.read_text()).get("kernels", {}).items():
+        if name == prefix or name.startswith(prefix + "<"):
+            return d.get("calls"), d.get("avg_ns"), d.get("hbm_bytes_per_launch")
+    return None
+
+
+def fe21_kernels(h, N: int, E: int, nn: int) -> dict:
+    """Continuous pressure (2, 1): every kernel of the direct step with its algorithmic bytes
+    per step (what it must read and write once: CSR values and rhs, b, x, cell lengths, the
+    per-vertex factors, the node records, blocks and pivots), the rocprof average and the
+    PMC traffic from the committed passes on this workload (FE21_PROFILE), and the HBM
+    fraction. Launches per step: one each, the node forest four (two per direction)."""
+    per = 2 * N + 1 + N - 1
+    n, nnz = h.n_rows, h.nnz
+    alg = {
+        "k_fe_tasm": 8 * nnz + 8 * n + 8 * E * N + 32 * E,
+        "k_cp_edge": 8 * E * per + 8 * E * N + 24 * E + 8 * 18 * E * (N + 1) + 8 * 20 * E,
+        "k_cp_nodes_rec": nn * 256 + 144 * E + nn * 160,
+        "k_cp_back": 8 * 18 * E * (N + 1) + 8 * E * per + 8 * E * N + 48 * E + 8 * E * per
+                     + 16 * nn,
+        "k_fe_tres": 3 * 8 * n + 8 * E * N + 32 * E,
+    }
+    launches = {"k_cp_nodes_rec": 4}
+    out = {}
+    for k, b in alg.items():
+        got = summary_kernel(FE21_PROFILE, k)
+        if not got:
+            out[k] = {"algorithmic_bytes_per_step": b}
+            continue
+        calls, avg_ns, traffic = got
+        nl = launches.get(k, 1)
+        t = (avg_ns or 0.0) * nl * 1e-9
+        ach = b / t / 1e9 if t > 0 else None
+        out[k] = {"algorithmic_bytes_per_step": b, "launches_per_step": nl,
+                  "rocprof_us_per_step": t * 1e6, "achieved_GBs": ach,
+                  "frac": ach / HBM_PEAK_GBS if ach else None,
+                  "traffic_bytes_per_step": traffic * nl if traffic else None,
+                  "traffic_ratio": traffic * nl / b if traffic else None,
+                  "source": f"profiles/{FE21_PROFILE}_summary.json"}
+    return out
+
+
 def fe_leg(mesh, steps: int = 20, warmup: int = 5) -> dict:
     """General element degrees on the headline tree (one GPU, reported beside the headline):
     (2, 0) through the condensed direct solve and (2, 1) through the node-condensed one,
@@ -336,6 +388,9 @@ def fe_leg(mesh, steps: int = 20, warmup: int = 5) -> dict:
                             "solver": "direct" if h.solver()[1] == 1 else "minres",
                             "direct_path": h.direct_path(), "passes": res[0],
                             "relres": res[1], "converged": res[2], "setup_s": setup}
+                if (k, m) == (2, 1):
+                    out[key]["kernels"] = fe21_kernels(h, mesh.N, mesh.num_edges,
+                                                       len(mesh.node_coordinates))
             finally:
                 asm.close()
         except Exception as e:  # (reported, never fatal to the headline)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """General element degrees on the GPU: assembly + plain-MINRES timing (and the direct solve,
 condensed for (k, 0)) at a mid-size tree (development / DESIGN numbers).
-Usage: python scripts/fe_timing.py [levels N ["k,m;k,m..."]]"""
+Usage: python scripts/fe_timing.py [levels N ["k,m;k,m..."] [direct]]  ("direct": the direct
+solves only, for profiling passes)"""
 
 from __future__ import annotations
 
@@ -27,10 +28,15 @@ def main() -> int:
     pairs = [(1, 0), (2, 0), (2, 1), (3, 2)]
     if len(sys.argv) > 3:  # e.g. "1,0;2,0;3,0"
         pairs = [tuple(int(v) for v in p.split(",")) for p in sys.argv[3].split(";")]
+    direct_only = len(sys.argv) > 4 and sys.argv[4] == "direct"
     for km in pairs:
         asm = HydraulicNetworkAssembler(mesh, flux_degree=km[0], pressure_degree=km[1])
         asm.compute_forms(p_bc_ex=pbc)
         h = asm.handle
+        if direct_only:
+            _direct(asm, h, km)
+            asm.close()
+            continue
         asm.set_preconditioner(False)
         h.assemble(True, True)
         h.solve(1e-12, 200000, 32)  # warm
@@ -48,22 +54,25 @@ def main() -> int:
             line += f" err_vs_analytic={np.linalg.norm(x - xa) / np.linalg.norm(xa):.2e}"
         print(line, flush=True)
         if asm.fe_direct_available or km == (1, 0):  # the direct solve (condensed for k >= 2)
-            if km == (1, 0):
-                asm.set_preconditioner(True)
-            asm.set_direct(True)
-            ts = []
-            for _ in range(6):
-                t0 = time.perf_counter()
-                h.assemble(True, True)
-                it, rr, conv = h.solve(1e-12, 200000, 4)
-                h.sync()
-                ts.append(1e3 * (time.perf_counter() - t0))
-            x = h.solution()
-            print(f"k={km[0]} m={km[1]} direct passes={it} relres={rr:.2e} conv={conv} "
-                  f"used={h.solver()[1]} min {min(ts[1:]):.3f} ms median "
-                  f"{float(np.median(ts[1:])):.3f} ms", flush=True)
+            _direct(asm, h, km)
         asm.close()
     return 0
+
+
+def _direct(asm, h, km):
+    if km == (1, 0):
+        asm.set_preconditioner(True)
+    asm.set_direct(True)
+    ts = []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        h.assemble(True, True)
+        it, rr, conv = h.solve(1e-12, 200000, 4)
+        h.sync()
+        ts.append(1e3 * (time.perf_counter() - t0))
+    print(f"k={km[0]} m={km[1]} direct passes={it} relres={rr:.2e} conv={conv} "
+          f"used={h.solver()[1]} min {min(ts[1:]):.3f} ms median "
+          f"{float(np.median(ts[1:])):.3f} ms", flush=True)
 
 
 def _functions(asm):
