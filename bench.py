@@ -306,7 +306,7 @@ def c4_leg(args, world: int, rank: int, comm, timed_steps, state, allsum):
 
 # the committed rocprofv3 passes (kernel trace + FETCH_SIZE / WRITE_SIZE) of the (2, 1)
 # direct step on this leg's workload (scripts/fe_timing.py 15 15 "2,1" direct)
-FE21_PROFILE = "r06zj"
+FE21_PROFILE = "r06zl"
 
 
 def summary_kernel(tag: str, prefix: str):
@@ -330,9 +330,9 @@ def fe21_kernels(h, N: int, E: int, nn: int) -> dict:
     n, nnz = h.n_rows, h.nnz
     alg = {
         "k_fe_tasm": 8 * nnz + 8 * n + 8 * E * N + 32 * E,
-        "k_cp_edge": 8 * E * per + 8 * E * N + 24 * E + 8 * 18 * E * (N + 1) + 8 * 20 * E,
+        "k_cp_edge": 8 * E * per + 8 * E * N + 24 * E + 8 * 14 * E * (N + 1) + 8 * 20 * E,
         "k_cp_nodes_rec": nn * 256 + 144 * E + nn * 160,
-        "k_cp_back": 8 * 18 * E * (N + 1) + 8 * E * per + 8 * E * N + 48 * E + 8 * E * per
+        "k_cp_back": 8 * 14 * E * (N + 1) + 8 * E * per + 8 * E * N + 48 * E + 8 * E * per
                      + 16 * nn,
         "k_fe_tres": 3 * 8 * n + 8 * E * N + 32 * E,
     }

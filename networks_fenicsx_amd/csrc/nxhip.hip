@@ -8468,13 +8468,16 @@ struct CpArgs {
   const int* tI;      // nI: +1 flux, -1 pressure (interior node types)
   const int* eb;      // per edge: u, v (border node indices), au, av (lam couplings: 0, +-1)
   const int* nrow;    // per border node: its pressure row, its multiplier row (or -1)
-  double* fac;        // per vertex (N + 1), per factor: Pi 4 | C 4 | W 8 | rho 2, per edge
+  double* fac;        // per vertex (N + 1), per factor (kCpFac), per edge
                       // (edge-minor: a wave's lanes, consecutive edges, touch 512 B per access)
   double* se;         // per edge: Se 16 | ge 4
   double* xn;         // per border node: its (p, lam) values
   const int* gid;     // several ranks: the global edge of each local edge (its se slot)
 };
-constexpr int kCpFac = 18;
+// per vertex (round 6): Pi C 4 | Pi W 8 | Pi rho 2 -- the back-substitution's products
+// formed once in the forward sweep (y = Pi rho - (Pi W) x_border - (Pi C) y_next), 14
+// doubles instead of Pi | C | W | rho's 18
+constexpr int kCpFac = 14;
 
 __device__ __forceinline__ double cp_pow(double s, int ex) {  // s^ex, ex in {-1, 0, 1}
   return ex > 0 ? s : ex < 0 ? 1.0 / s : 1.0;
@@ -8580,11 +8583,10 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
       gb[r] -= W[r] * z[0] + W[4 + r] * z[1];
     }
     double* f = fe + (int64_t)c * kCpFac * E;
-    for (int i = 0; i < 4; ++i) f[i * E] = Pi[i];
-    for (int i = 0; i < 4; ++i) f[(4 + i) * E] = C[i];
-    for (int i = 0; i < 8; ++i) f[(8 + i) * E] = W[i];
-    f[16 * E] = rho[0];
-    f[17 * E] = rho[1];
+    for (int i = 0; i < 4; ++i) f[i * E] = X[i];
+    for (int i = 0; i < 8; ++i) f[(4 + i) * E] = Y[i];
+    f[12 * E] = z[0];
+    f[13 * E] = z[1];
     for (int i = 0; i < 4; ++i) P[i] = Pn[i];
     for (int i = 0; i < 8; ++i) W[i] = Wn[i];
     rho[0] = rn[0];
@@ -8603,11 +8605,10 @@ __global__ __launch_bounds__(256) void k_cp_edge(CpArgs a, const double* __restr
       gb[r] -= W[r] * z[0] + W[4 + r] * z[1];
     }
     double* f = fe + (int64_t)N * kCpFac * E;
-    for (int i = 0; i < 4; ++i) f[i * E] = Pi[i];
-    for (int i = 0; i < 4; ++i) f[(4 + i) * E] = 0.0;
-    for (int i = 0; i < 8; ++i) f[(8 + i) * E] = W[i];
-    f[16 * E] = rho[0];
-    f[17 * E] = rho[1];
+    for (int i = 0; i < 4; ++i) f[i * E] = 0.0;
+    for (int i = 0; i < 8; ++i) f[(4 + i) * E] = Y[i];
+    f[12 * E] = z[0];
+    f[13 * E] = z[1];
   }
   double* o = a.se + 20 * (a.gid ? (int64_t)a.gid[e] : e);
   for (int i = 0; i < 16; ++i) o[i] = Sb[i];
@@ -9054,14 +9055,13 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
 #pragma unroll
       for (int q = 0; q < kCpFac; ++q) fn[q] = f[q * E];
     }
-    double r[2] = {fv[16], fv[17]};
+    double y0 = fv[12], y1 = fv[13];
     for (int q = 0; q < 4; ++q) {
-      r[0] -= fv[8 + q] * xb[q];
-      r[1] -= fv[12 + q] * xb[q];
+      y0 -= fv[4 + q] * xb[q];
+      y1 -= fv[8 + q] * xb[q];
     }
-    r[0] -= fv[4] * yn[0] + fv[5] * yn[1];
-    r[1] -= fv[6] * yn[0] + fv[7] * yn[1];
-    const double y0 = fv[0] * r[0] + fv[1] * r[1], y1 = fv[2] * r[0] + fv[3] * r[1];
+    y0 -= fv[0] * yn[0] + fv[1] * yn[1];
+    y1 -= fv[2] * yn[0] + fv[3] * yn[1];
     putl(k * i, y0);
     if (i > 0 && i < N) putl(prow(m * i), y1);
     if (i < N) {  // cell i: its interior nodes from (q_i, p_i, q_{i+1}, p_{i+1})
