@@ -306,7 +306,7 @@ def c4_leg(args, world: int, rank: int, comm, timed_steps, state, allsum):
 
 # the committed rocprofv3 passes (kernel trace + FETCH_SIZE / WRITE_SIZE) of the (2, 1)
 # direct step on this leg's workload (scripts/fe_timing.py 15 15 "2,1" direct)
-FE21_PROFILE = "r06zl"
+FE21_PROFILE = "r06zm"
 
 
 def summary_kernel(tag: str, prefix: str):

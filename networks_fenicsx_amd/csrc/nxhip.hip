@@ -9021,14 +9021,18 @@ __global__ __launch_bounds__(256) void k_cp_level(CpArgs a, CpTree t, const doub
 // Back-substitution of one edge (one thread): its vertices from the border values, then every
 // cell's interior nodes; x written (accum: added -- a refinement pass), the node rows too by
 // the edges whose source they are (or, for a node no edge leaves, its first edge in).
+// xs: dynamic LDS for the workgroup's edges' rows of x (blockDim.x * per doubles), written
+// out unit-stride at the end (round 6: lane-strided row stores left partial lines, 1.67x
+// the algorithmic traffic); nullptr-sized launch (0 bytes): the rows stored directly.
 __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restrict__ b,
                                                  double* __restrict__ x, const int* __restrict__ nown,
-                                                 int accum) {
+                                                 int accum, int stage) {
+  extern __shared__ double cp_xs[];
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.E) return;
   const int N = a.N, k = a.k, m = a.m, nI = a.nI;
   const int nf = k * N + 1, per = nf + m * N - 1;
   const int64_t base = e * (int64_t)per;
+  if (e < a.E) {
   const double* bl = b + base;         // this edge's rows of b
   const double* hl = a.cellh + e * N;  // its cells' lengths
   const int u = a.eb[4 * e], v = a.eb[4 * e + 1];
@@ -9039,7 +9043,12 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
   const double* Fh = Eh + 4 * nI;
   const double R = a.edge_R[e];
   auto put = [&](int64_t r, double val) { x[r] = accum ? x[r] + val : val; };
-  auto putl = [&](int r, double val) { put(base + r, val); };  // the edge's local row r
+  auto putl = [&](int r, double val) {  // the edge's local row r
+    if (stage)
+      cp_xs[(int64_t)threadIdx.x * per + r] = val;
+    else
+      put(base + r, val);
+  };
   auto prow = [&](int j) { return nf + j - 1; };  // (local row)
   double yn[2] = {0.0, 0.0};  // the next vertex's (q, p)
   const int tV[4] = {1, -1, 1, -1};
@@ -9088,6 +9097,15 @@ __global__ __launch_bounds__(256) void k_cp_back(CpArgs a, const double* __restr
     if (nown[n] != e) continue;
     put(a.nrow[2 * n], a.xn[2 * n]);
     if (a.nrow[2 * n + 1] >= 0) put(a.nrow[2 * n + 1], a.xn[2 * n + 1]);
+  }
+  }  // e < a.E
+  if (stage) {  // the workgroup's edge rows out, unit stride (every row of an edge written)
+    __syncthreads();
+    const int T = blockDim.x;
+    const int64_t e0 = (int64_t)blockIdx.x * T;
+    const int ne = (int)min<int64_t>(T, a.E - e0);
+    double* gx = x + e0 * per;
+    for (int j = threadIdx.x; j < ne * per; j += T) gx[j] = accum ? gx[j] + cp_xs[j] : cp_xs[j];
   }
 }
 
@@ -11310,9 +11328,15 @@ int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int3
                   h->cp_rec ? h->cp_ctr : nullptr};
   const int nrb = grid_of(h->n_own, kRowsPerBlock * res_chunks(h->n_own));
   // (one thread per edge: 64-thread workgroups spread the edges over every CU. Staging the
-  // edges' rows of b in LDS was measured slower, r06zd: the sweeps are bound by their serial
-  // per-cell arithmetic, not by the loads)
+  // edges' rows of b in LDS was measured slower, r06zd; the back-substitution's x rows go
+  // out through LDS when they fit 64 KB, NXHIP_CP_XS=0 off)
   const int eb = std::max(1, grid_of(Ee, 64));
+  const int per_e = h->cp_k * (int)h->N + 1 + h->cp_m * (int)h->N - 1;
+  const char* xs_env = std::getenv("NXHIP_CP_XS");
+  const size_t xs_lds = (xs_env == nullptr || std::atoi(xs_env) != 0) &&
+                                (size_t)64 * per_e * sizeof(double) <= 64 * 1024
+                            ? (size_t)64 * per_e * sizeof(double)
+                            : 0;
   MrState s{};
   int pass = 0;
   h->last_dir_path = 4;  // the node-condensed route (nx_get_direct_path)
@@ -11326,8 +11350,8 @@ int fe_cp_solve(nx_network* h, double rtol, int32_t* iters, double* relres, int3
       CHECK(team_allreduce(t, -5, (int)nsum));
     }
     cp_nodes_launch(h, ranks ? an : a, tr, ranks ? nb : b);
-    hipLaunchKernelGGL(k_cp_back, dim3(eb), dim3(64), 0, h->stream, a, b, h->x, h->cp_nown,
-                       pass ? 1 : 0);
+    hipLaunchKernelGGL(k_cp_back, dim3(eb), dim3(64), xs_lds, h->stream, a, b, h->x, h->cp_nown,
+                       pass ? 1 : 0, xs_lds > 0 ? 1 : 0);
     if (ranks)
       CHECK(fe_true_residual_team(h, rtol, nrb));
     else

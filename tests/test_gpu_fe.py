@@ -301,8 +301,9 @@ def test_fe_cp_pipelined_node_forest(km, monkeypatch):
         asm.compute_forms(p_bc_ex=lambda x: x[1])
         asm.set_direct(True)
         xs = []
-        for pipe in ("0", "1", "1"):
+        for pipe, via_lds in (("0", "0"), ("1", "1"), ("1", "1"), ("1", "0")):
             monkeypatch.setenv("NXHIP_CP_PIPE", pipe)
+            monkeypatch.setenv("NXHIP_CP_XS", via_lds)  # the back-substitution's rows via LDS
             asm.assemble()
             it, rr, conv = asm.handle.solve(1e-12, 100, 4)
             assert conv and asm.handle.direct_path() == "node-condensed", (pipe, it, rr)
