@@ -465,7 +465,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong", action="store_true",
                     help="P > 1: skip rank 0's one-GPU time of the same workload")
-    ap.add_argument("--api-steps", type=int, default=10,
+    ap.add_argument("--api-steps", type=int, default=200,
                     help="steps through the public Solver.assemble/solve surface (0: skip)")
     ap.add_argument("--no-pc", action="store_true", help="plain (unpreconditioned) MINRES")
     ap.add_argument("--fe-ranks", action="store_true",

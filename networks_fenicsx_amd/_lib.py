@@ -508,6 +508,7 @@ class Handle:
 
     def set_preconditioner(self, pc) -> None:
         """Upload a :class:`precond.TreePreconditioner` (``None`` disables it)."""
+        self._pcx = None  # (nx_set_preconditioner resets the flux mass choice)
         if pc is None:
             z = np.zeros(1, np.int32)
             check(lib().nx_set_preconditioner(self.ptr, 0, 0, *([_ptr(z, C.c_int32)] * 4), 0,
@@ -602,11 +603,17 @@ class Handle:
     def set_pc_exact(self, enable: bool) -> None:
         """Consistent (exact Schur complement, default) or lumped flux mass in P."""
         check(lib().nx_set_pc_exact(self.ptr, int(bool(enable))))
+        self._pcx = bool(enable)
 
     def pc_exact(self) -> bool:
-        e = C.c_int32(0)
-        check(lib().nx_get_pc_exact(self.ptr, C.byref(e)))
-        return bool(e.value)
+        """The flux mass P uses (nx_get_pc_exact; remembered after the first query or the
+        last set_pc_exact through this handle -- the per-solve check costs no C call)."""
+        v = getattr(self, "_pcx", None)
+        if v is None:
+            e = C.c_int32(0)
+            check(lib().nx_get_pc_exact(self.ptr, C.byref(e)))
+            v = self._pcx = bool(e.value)
+        return v
 
     def set_cell_mass(self, ratio: float, mo_div: float) -> None:
         """``nx_set_cell_mass``: this (auxiliary) handle's sweeps invert the condensed flux
