@@ -318,6 +318,38 @@ def test_fe_cp_pipelined_node_forest(km, monkeypatch):
         asm.close()
 
 
+@pytest.mark.parametrize("km", [(2, 1), (3, 2)])
+def test_fe_cp_deep_node_forest(km, monkeypatch):
+    """A 150-node line (150 node levels): the level run is longer than the pipelined
+    kernel's 64, so it runs level by level in one workgroup on the node records (their
+    parent terms); the same bits as the lists' path (NXHIP_CP_NOREC=1, read when the tables
+    are attached) and the oracle's LU to 1e-10."""
+    from cases import linear_graph
+
+    xs = []
+    for norec in ("0", "1"):
+        if norec == "1":
+            monkeypatch.setenv("NXHIP_CP_NOREC", "1")
+        mesh = NetworkMesh(linear_graph(150, ordered=lambda k: k % 3 != 0), N=2)
+        asm = HydraulicNetworkAssembler(mesh, flux_degree=km[0], pressure_degree=km[1])
+        try:
+            asm.compute_forms(p_bc_ex=lambda x: x[0])
+            asm.set_direct(True)
+            asm.assemble()
+            it, rr, conv = asm.handle.solve(1e-12, 100, 4)
+            assert conv and asm.handle.direct_path() == "node-condensed", (it, rr)
+            xs.append(np.concatenate([fn.x.array for fn in _functions(asm)]))
+            if norec == "0":
+                F = OF.build_problem_fe(mesh.node_coordinates, *mesh.edges, 2, *km,
+                                        mesh.edge_colors)
+                A, b = OF.assemble_reference_fe(F, lambda x: x[0])
+                x_ref = O.solve_reference(A, b)
+                assert np.linalg.norm(xs[0] - x_ref) / np.linalg.norm(x_ref) <= SOL_TOL
+        finally:
+            asm.close()
+    np.testing.assert_array_equal(xs[0], xs[1])
+
+
 def _functions(asm):
     from networks_fenicsx_amd.fem import Function
 
