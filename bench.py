@@ -356,6 +356,38 @@ def fe21_kernels(h, N: int, E: int, nn: int) -> dict:
     return out
 
 
+# the committed bench profile whose MINRES legs ran this workload (the preconditioner's
+# MINRES-mode sweeps, k_mr_a): profiles/r06u_*
+MINRES_PROFILE = "r06u"
+
+
+def minres_sweep_kernels(n: int, E: int, N: int, B: int) -> dict:
+    """The preconditioner's sweeps in MINRES mode (P^{-1} r' per iteration, mode 0) with
+    their algorithmic bytes per launch -- up: y and r2 at the edge DoFs read, y' = y - c r2
+    written back, the lumped mass read, the chains' T / It / Ib written, the slots' y, r2 and
+    statics; down: y at the edge DoFs and the lumped mass read, z written, the chain and slot
+    statics -- beside the rocprof average and the PMC traffic of MINRES_PROFILE's passes."""
+    n_e = E * (2 * N + 1)
+    dq = 8 * E * (N + 1)
+    alg = {"k_pc_up_lds<false, 8, 2>": 24 * n_e + dq + 32 * E + 80 * B,
+           "k_pc_down_lds<false, 8, 2, false>": 8 * n_e + dq + 8 * n + 16 * E + 32 * B}
+    out = {}
+    for k, b in alg.items():
+        got = summary_kernel(MINRES_PROFILE, k)
+        if not got:
+            out[k] = {"algorithmic_bytes_per_launch": b}
+            continue
+        calls, avg_ns, traffic = got
+        t = (avg_ns or 0.0) * 1e-9
+        ach = b / t / 1e9 if t > 0 else None
+        out[k] = {"algorithmic_bytes_per_launch": b, "rocprof_avg_launch_ms": t * 1e3,
+                  "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
+                  "traffic": traffic, "traffic_ratio": traffic / b if traffic else None,
+                  "source": f"profiles/{MINRES_PROFILE}_summary.json (its calls average the "
+                            "iterations' launches with the start's)"}
+    return out
+
+
 def fe_leg(mesh, steps: int = 20, warmup: int = 5) -> dict:
     """General element degrees on the headline tree (one GPU, reported beside the headline):
     (2, 0) through the condensed direct solve and (2, 1) through the node-condensed one,
@@ -650,7 +682,9 @@ def run(args, world: int) -> int:
                 "traffic_source": tsrc,
                 "rocprof_avg_launch_ms": rocprof_ns / 1e6 if rocprof_ns else None,
                 "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": spmv_ms,
-                "assembly_kernel_ms": prof["asm_ms"] / max(prof["asm_count"], 1)}
+                "assembly_kernel_ms": prof["asm_ms"] / max(prof["asm_count"], 1),
+                "sweeps": (minres_sweep_kernels(h.n_rows, E, N, B) if default_workload and pc_on
+                           else None)}
 
     def direct_roofline():
         """The direct solve's kernels (events bound to each dispatch, PROF_STEPS profiled
